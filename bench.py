@@ -1,0 +1,313 @@
+#!/usr/bin/env python3
+"""bench.py — decided+applied instances/s for the MI355X batched-consensus engine.
+
+Workload (BASELINE.json configs[4], SURVEY §8(d) config 5, per GPU): 65,536 independent Paxos
+groups x 256 instances x 4 AcceptReplies (N = 5) + 4 PUT/GET commands per instance, per-group
+keys uniform on [0,256). One step = for every group: the accept tally (handleAcceptReply, MIN
+by default), executeCommands over the committed prefix against the group's KV table, then ONE
+RCCL all-reduce (max) of the commit/executed watermark vector of all groups of the job.
+Weak scaling: each rank owns its own 65,536 groups (block-partitioned by global group id).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode min|classic]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line. Inputs are generated on the host (synthetic, counter-based
+splitmix64) and copied to HBM before timing; the timed region contains only device work.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from minpaxos_amd import records as R  # noqa: E402
+from minpaxos_amd import synth  # noqa: E402
+from minpaxos_amd import _lib  # noqa: E402
+from minpaxos_amd.engine import Engine  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--mode", default="min", choices=["min", "classic"])
+    ap.add_argument("--groups", type=int, default=65536, help="groups per GPU")
+    ap.add_argument("--ipg", type=int, default=256)
+    ap.add_argument("--cmds", type=int, default=4)
+    ap.add_argument("--keys", type=int, default=256)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-groups", type=int, default=0,
+                    help="groups timed on the CPU baseline (0 = auto, ~10-30 s of CPU work)")
+    ap.add_argument("--parity-groups", type=int, default=512)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    import torch
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    mode = R.MODE_MIN if a.mode == "min" else R.MODE_CLASSIC
+    N, G, ipg, B, K = 5, a.groups, a.ipg, a.cmds, 512
+    G_total = G * world
+    eng = Engine(local, n_replicas=N, mode=mode, kv_per_group=K)
+
+    # ---- this rank's block of groups, generated from their global ids --------------------------
+    t_gen = time.time()
+    b = synth.group_batch(G, ipg, N, B, a.keys, p_ok=0.7, p_put=0.5, seed=45,
+                          first_group=rank * G)
+    t_gen = time.time() - t_gen
+
+    def dt(x, dtype=None):
+        arr = np.ascontiguousarray(x)
+        if arr.dtype.names:
+            arr = arr.view(np.uint8)
+        return torch.from_numpy(arr).to(dev)
+
+    n_rec = len(b["recs"])
+    m = len(b["op"])
+    d = dict(
+        recs=dt(b["recs"]), off=dt(b["grp_rec_off"]), st_in=dt(b["st_in"]),
+        st_out=torch.empty(G * ipg * 16, dtype=torch.uint8, device=dev),
+        ci=dt(b["committed_in"]), ei=dt(b["executed_in"]), pi=dt(b["peer_in"]),
+        po=torch.empty(G * N, dtype=torch.int32, device=dev),
+        op=dt(b["op"]), key=dt(b["key"]), val=dt(b["val"]), coff=dt(b["cmd_off"]),
+        ret=torch.zeros(m, dtype=torch.int64, device=dev),
+        conf=torch.zeros(m, dtype=torch.uint8, device=dev),
+        kc0=torch.zeros(G, dtype=torch.int32, device=dev),
+        kk0=torch.zeros(G * K, dtype=torch.int64, device=dev),
+        kv0=torch.zeros(G * K, dtype=torch.int64, device=dev),
+        kc1=torch.zeros(G, dtype=torch.int32, device=dev),
+        kk1=torch.zeros(G * K, dtype=torch.int64, device=dev),
+        kv1=torch.zeros(G * K, dtype=torch.int64, device=dev),
+        wm=torch.full((2 * G_total,), -1, dtype=torch.int32, device=dev),
+    )
+    co = d["wm"][rank * G:(rank + 1) * G]
+    eo = d["wm"][G_total + rank * G:G_total + (rank + 1) * G]
+
+    def batch(kc_in, kk_in, kv_in, kc_out, kk_out, kv_out):
+        p = lambda t: t.data_ptr()  # noqa: E731
+        return _lib.MpxGroupBatch(
+            G, ipg, p(d["recs"]), p(d["off"]), p(d["st_in"]), p(d["st_out"]), p(d["ci"]), p(co),
+            p(d["ei"]), p(eo), p(d["pi"]), p(d["po"]), p(d["op"]), p(d["key"]), p(d["val"]),
+            p(d["coff"]), None, p(d["ret"]), p(d["conf"]), p(kc_in), p(kk_in), p(kv_in),
+            p(kc_out), p(kk_out), p(kv_out), None)
+
+    stream = torch.cuda.current_stream(dev)
+    sptr = C.c_void_p(stream.cuda_stream)
+    if world > 1:
+        uid = [Engine.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(world, rank, uid[0])
+    else:
+        eng.comm_init(1, 0, Engine.comm_unique_id())
+
+    # steady state: the group tables already hold their keys (one untimed step fills them),
+    # and every timed step reads that table and writes a fresh one (same work every step)
+    eng.group_step_dev(batch(d["kc1"], d["kk1"], d["kv1"], d["kc0"], d["kk0"], d["kv0"]), sptr)
+    eng.synchronize()
+    step_batch = batch(d["kc0"], d["kk0"], d["kv0"], d["kc1"], d["kk1"], d["kv1"])
+
+    def step(ev=None):
+        d["wm"].fill_(-1)
+        if ev is not None:
+            ev[0].record(stream)
+        eng.group_step_dev(step_batch, sptr)
+        if ev is not None:
+            ev[1].record(stream)
+        eng.watermarks_allreduce_dev(d["wm"].data_ptr(), G_total, sptr)
+
+    for _ in range(a.warmup):
+        step()
+    eng.synchronize()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(evs[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    eng.synchronize()  # raises if any kernel flagged an error
+    elapsed = t1 - t0
+    kern_ms = [s.elapsed_time(e) for s, e in evs]
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # ---- outputs of the (identical) timed steps -------------------------------------------------
+    wm = d["wm"].cpu().numpy()
+    committed = wm[:G_total]
+    executed = wm[G_total:]
+    own_c = committed[rank * G:(rank + 1) * G]
+    own_e = executed[rank * G:(rank + 1) * G]
+    coff = b["cmd_off"].astype(np.int64)
+    gidx = np.arange(G, dtype=np.int64) * ipg
+    lo = gidx + 0  # executed_in = -1 -> first instance 0
+    hi = gidx + own_e.astype(np.int64) + 1
+    n_exec_cmds = int((coff[hi] - coff[lo]).sum())
+    n_exec_inst = int((own_e.astype(np.int64) + 1).sum())
+    kc = d["kc1"].cpu().numpy()
+    # allreduce check: every rank sees every group's watermark (none left at -1)
+    wm_ok = bool((committed >= 0).all())
+
+    # algorithmic bytes of one group-step launch (per rank): replies + instance state in/out,
+    # executed commands (op,key,val in; ret,conf out), group table in/out, per-group scalars
+    alg = (n_rec * 16 + G * ipg * 16 * 2 + n_exec_cmds * (17 + 9)
+           + int(kc.sum()) * 16 * 2 + G * (4 * 4 + 2 * N * 4 + 4 * 2 + 8 * 2))
+    kern_avg_ms = float(np.mean(kern_ms))
+    achieved_gbs = alg / (kern_avg_ms * 1e-3) / 1e9
+
+    traffic = None
+    try:
+        tj = json.load(open(a.traffic_json))
+        if tj.get("mode") == a.mode and tj.get("groups") == G:
+            traffic = tj.get("bytes_per_launch")
+    except Exception:
+        pass
+
+    res = {}
+    if rank == 0:
+        # parity: the first groups of the timed output against the oracle (test infra)
+        res["parity"] = parity_sample(b, d, a, mode, N, K, rank)
+        if world == 1 and not a.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(b, a, mode, N, K)
+
+    units = G_total * ipg * a.steps
+    value = units / elapsed
+    if rank == 0:
+        line = {
+            "metric": "decided+applied instances/sec (tally + KV apply + RCCL watermark all-reduce)",
+            "value": value,
+            "unit": "instances/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32/int64",
+            "data": "synthetic (counter-based splitmix64, SURVEY §8(d) config 5)",
+            "config": {
+                "workload": f"config5: {G} groups/GPU x {ipg} instances x {N - 1} AcceptReplies "
+                            f"+ {B} cmds/instance, keys U[0,{a.keys}) per group, mode {a.mode}",
+                "groups_total": G_total, "instances_per_step": G_total * ipg,
+                "commands_per_step": G_total * ipg * B, "parallelism": f"groups block-sharded x{world}",
+                "collective": "RCCL all-reduce(max) of 2 x groups_total int32 watermarks per step",
+            },
+            "roofline": {
+                "bound": "hbm", "kernel": "k_group_step", "achieved": achieved_gbs,
+                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved_gbs / PEAK_HBM_GBS,
+                "traffic": traffic, "alg_bytes_per_launch": alg,
+                "kernel_ms_avg": kern_avg_ms, "kernel_ms_min": float(np.min(kern_ms)),
+            },
+            "decided_instances_per_step": int(((own_c >= 0).sum())),
+            "executed_instances_per_step": n_exec_inst,
+            "executed_commands_per_step": n_exec_cmds,
+            "watermark_allreduce_ok": wm_ok,
+            "gen_s": round(t_gen, 2),
+        }
+        line.update(res)
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _oracle_sub(b, g0, g1, ipg):
+    r0, r1 = int(b["grp_rec_off"][g0]), int(b["grp_rec_off"][g1])
+    c0, c1 = int(b["cmd_off"][g0 * ipg]), int(b["cmd_off"][g1 * ipg])
+    sub = dict(n_groups=g1 - g0, ipg=ipg, recs=b["recs"][r0:r1],
+               grp_rec_off=(b["grp_rec_off"][g0:g1 + 1] - np.uint64(r0)),
+               st_in=b["st_in"][g0 * ipg:g1 * ipg], committed_in=b["committed_in"][g0:g1],
+               executed_in=b["executed_in"][g0:g1], peer_in=b["peer_in"][g0 * 5:g1 * 5],
+               op=b["op"][c0:c1], key=b["key"][c0:c1], val=b["val"][c0:c1],
+               cmd_off=(b["cmd_off"][g0 * ipg:g1 * ipg + 1] - np.uint32(c0)))
+    return sub, (c0, c1)
+
+
+def parity_sample(b, d, a, mode, N, K, rank):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import Oracle  # CPU oracle: the checker, never the measured path
+    S = min(a.parity_groups, a.groups)
+    ipg = a.ipg
+    sub, (c0, c1) = _oracle_sub(b, 0, S, ipg)
+    o = Oracle(N, mode, kv_per_group=K)
+    # the timed steps started from the table the warm-up step produced
+    w0 = o.group_step(sub)
+    want = o.group_step(sub, w0["kv_cnt"], w0["kv_key"], w0["kv_val"])
+    ret = d["ret"][c0:c1].cpu().numpy()
+    conf = d["conf"][c0:c1].cpu().numpy()
+    G_total = a.groups * int(os.environ.get("WORLD_SIZE", "1"))
+    wm = d["wm"].cpu().numpy()
+    ok = (np.array_equal(ret, want["ret"]) and np.array_equal(conf, want["conf_prev"])
+          and np.array_equal(wm[:S], want["committed_out"])
+          and np.array_equal(wm[G_total:G_total + S], want["executed_out"])
+          and np.array_equal(d["kc1"][:S].cpu().numpy().astype(np.uint32), want["kv_cnt"]))
+    return {"groups_checked": S, "bit_exact": bool(ok)}
+
+
+def cpu_baseline(b, a, mode, N, K):
+    """the reference-faithful CPU loop (oracle/baseline.cpp), one core, bounded sample"""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as OL
+    lib = OL.load()
+    ipg = a.ipg
+
+    def run(g_n, threads):
+        sub, _ = _oracle_sub(b, 0, g_n, ipg)
+        o = OL.Oracle(N, mode, kv_per_group=K)
+        warm = o.group_step(sub)  # steady-state tables, as on the GPU
+        m = len(sub["op"])
+        arrs = [g_n, ipg, sub["recs"], sub["grp_rec_off"], sub["st_in"], sub["st_in"].copy(),
+                sub["committed_in"], np.zeros(g_n, np.int32), sub["executed_in"],
+                np.zeros(g_n, np.int32), sub["peer_in"], np.zeros(g_n * N, np.int32), sub["op"],
+                sub["key"], sub["val"], sub["cmd_off"], None, np.zeros(m, np.int64), None,
+                warm["kv_cnt"], warm["kv_key"], warm["kv_val"], warm["kv_cnt"].copy(),
+                warm["kv_key"].copy(), warm["kv_val"].copy(), None]
+        arrs = [np.ascontiguousarray(x) if isinstance(x, np.ndarray) else x for x in arrs]
+        gb = OL.group_batch_struct(arrs)
+        ns = lib.orc_bench_group_step(N, mode, C.byref(gb), K, threads)
+        return ns * 1e-9
+
+    if a.cpu_sample_groups:
+        g_n = min(a.cpu_sample_groups, a.groups)
+    else:
+        t = run(min(2048, a.groups), 1)
+        per = t / min(2048, a.groups)
+        g_n = int(min(a.groups, max(2048, 15.0 / max(per, 1e-9))))
+    secs = run(g_n, 1)
+    return {"value": g_n * ipg / secs, "unit": "instances/s", "cores": 1, "kind": "port",
+            "sample": f"first {g_n} groups of the same workload ({g_n * ipg} instances, "
+                      f"{g_n * ipg * (N - 1)} replies, {g_n * ipg * a.cmds} commands), "
+                      f"pointer-per-instance log + hash-map State, one thread, {secs:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,309 @@
+/*
+ * mpx.h — C ABI of the MI355X batched-consensus engine (minpaxos_amd).
+ *
+ * The engine replaces, for batches of records, the per-message hot path of the
+ * MinPaxos replica (arobertlin/MinPaxos, Go):
+ *
+ *   mpx_accept_tally      <- bareminpaxos.(*Replica).handleAcceptReply
+ *                              src/bareminpaxos/bareminpaxos.go:1014-1064   (MPX_MODE_MIN)
+ *                            paxos.(*Replica).handleAcceptReply
+ *                              src/paxos/paxos.go:631-673 (+ updateCommittedUpTo :259-264)
+ *                                                                          (MPX_MODE_CLASSIC)
+ *   mpx_prepare_select    <- paxos.(*Replica).handlePrepareReply  src/paxos/paxos.go:577-629
+ *   mpx_prepare_select_min<- bareminpaxos.(*Replica).handlePrepareReply
+ *                              src/bareminpaxos/bareminpaxos.go:912-966 (+ PrepareBookkeeping :75-82)
+ *   mpx_apply             <- (*state.Command).Execute  src/state/state.go:77-103, driven in log
+ *                            order by executeCommands  src/bareminpaxos/bareminpaxos.go:1066-1098
+ *                            (conf_prev output: state.Conflict  src/state/state.go:53-60)
+ *   mpx_conflict_batch    <- state.ConflictBatch  src/state/state.go:62-71
+ *   mpx_group_step        <- handleAcceptReply + executeCommands for many independent replicas
+ *                            (Paxos groups) at once: one tally and one apply per group
+ *   mpx_watermarks_allreduce <- (no reference equivalent; the one cross-shard step: an RCCL
+ *                            all-reduce of per-group committedUpTo / executed watermarks)
+ *
+ * Contract (every entry point):
+ *   - plain C, no exceptions cross the boundary, never aborts; return 0 (MPX_OK) or a negative
+ *     MPX_E_* code; mpx_last_error() explains the last failure of a handle.
+ *   - records are processed with SEQUENTIAL semantics in array order: the results equal those of
+ *     calling the reference handler once per record, in array order. Records must be grouped by
+ *     instance (all replies for one instance contiguous); within a group, slot order = arrival
+ *     order. MIN watermarks are "last assignment wins" in array order.
+ *   - host-pointer entry points are synchronous: results are in the caller's buffers on return.
+ *     *_dev entry points take device pointers and a hipStream_t (passed as void*, NULL = the
+ *     engine's stream) and are asynchronous; they never allocate or synchronise, so they can be
+ *     captured into a hipGraph.
+ *   - a handle is not re-entrant; use one handle per replica event loop / per GPU.
+ *   - where the reference would panic (nil instance, peer id outside peerCommits), the engine
+ *     returns MPX_E_NIL_INSTANCE / MPX_E_BAD_ID and the outputs are unspecified.
+ */
+#ifndef MPX_H_
+#define MPX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPX_ABI_VERSION 1
+
+/* ---- error codes ---------------------------------------------------------------------- */
+#define MPX_OK 0
+#define MPX_E_INVAL (-1)        /* bad argument / size / layout                            */
+#define MPX_E_NOMEM (-2)        /* host or device allocation failed                        */
+#define MPX_E_HIP (-3)          /* HIP runtime error                                       */
+#define MPX_E_RCCL (-4)         /* RCCL error                                              */
+#define MPX_E_NIL_INSTANCE (-5) /* record names an instance outside the window or nil:
+                                   the reference dereferences a nil *Instance (panic)     */
+#define MPX_E_BAD_ID (-6)       /* reply Id outside [0,N): reference indexes peerCommits   */
+#define MPX_E_KV_FULL (-7)      /* KV table capacity exceeded                              */
+#define MPX_E_NODEV (-8)        /* no GPU / HIP device unavailable                         */
+#define MPX_E_UNSUPPORTED (-9)  /* feature not built in / input beyond supported limits    */
+
+/* ---- enums (values mirror the reference) ---------------------------------------------- */
+/* minpaxosproto.InstanceStatus  src/minpaxosproto/minpaxosproto.go:8-15
+ * paxos.InstanceStatus          src/paxos/paxos.go:50-55                                   */
+#define MPX_PREPARING 0
+#define MPX_PREPARED 1
+#define MPX_ACCEPTED 2
+#define MPX_COMMITTED 3
+#define MPX_STATUS_NIL (-1) /* instanceSpace[i] == nil                                      */
+
+/* state.Operation  src/state/state.go:10-19 */
+#define MPX_OP_NONE 0
+#define MPX_OP_PUT 1
+#define MPX_OP_GET 2
+#define MPX_OP_DELETE 3
+#define MPX_OP_RLOCK 4
+#define MPX_OP_WLOCK 5
+
+#define MPX_MODE_MIN 0     /* bareminpaxos semantics (the live protocol)                   */
+#define MPX_MODE_CLASSIC 1 /* paxos semantics (classic per-instance Multi-Paxos)           */
+
+#define MPX_MAX_REPLICAS 16 /* ballots are (round<<4)|replicaId: bareminpaxos.go:383-385   */
+
+/* ---- packed records (no pointers: cgo-legal as unsafe.Pointer(&slice[0])) -------------- */
+
+/* minpaxosproto.AcceptReply{Instance,OK,Ballot,Id}  src/minpaxosproto/minpaxosproto.go:75-80
+ * (CLASSIC: paxosproto.AcceptReply{Instance,OK,Ballot} src/paxosproto/paxosproto.go:37-41;
+ * id unused). ok follows the reference test `OK == TRUE` (TRUE = 1).                        */
+typedef struct mpx_accept_reply {
+    int32_t instance;
+    int32_t ballot;
+    int32_t id;
+    uint8_t ok;
+    uint8_t pad[3];
+} mpx_accept_reply; /* 16 B */
+
+/* Instance.Status + LeaderBookkeeping{MaxRecvBallot,AcceptOKs,Nacks}
+ * src/minpaxosproto/minpaxosproto.go:17-29 ; src/paxos/paxos.go:57-70                      */
+typedef struct mpx_inst_state {
+    int32_t status;
+    int32_t accept_oks;
+    int32_t nacks;
+    int32_t max_recv_ballot;
+} mpx_inst_state; /* 16 B */
+
+/* paxosproto.PrepareReply{Instance,OK,Ballot,Command}  src/paxosproto/paxosproto.go:23-28.
+ * Command is an opaque handle the host resolves (an empty command is just another handle). */
+typedef struct mpx_prepare_reply {
+    int32_t instance;
+    int32_t ballot;
+    uint32_t ok;
+    uint32_t value_id;
+} mpx_prepare_reply; /* 16 B */
+
+/* per-instance CLASSIC prepare state: paxos Instance{cmds,ballot,status,lb}
+ * src/paxos/paxos.go:57-70 ; value_id = handle of inst.cmds                                */
+#define MPX_PF_HAS_PROPOSALS 1u /* lb.clientProposals != nil                                */
+#define MPX_PF_REQUEUED 2u      /* proposals were pushed back on ProposeChan in this call    */
+#define MPX_PF_PREPARED_NOW 4u  /* instance became PREPARED in this call (host bcastAccept)  */
+typedef struct mpx_prep_state {
+    int32_t ballot; /* inst.ballot                                                          */
+    int32_t status;
+    int32_t prepare_oks;
+    int32_t nacks;
+    int32_t max_recv_ballot;
+    uint32_t value_id;
+    uint32_t flags;
+    uint32_t pad;
+} mpx_prep_state; /* 32 B */
+
+/* minpaxosproto.PrepareReply{Id,Instance,OK,Ballot,LastCommitted,Command,CatchUpLog}
+ * src/minpaxosproto/minpaxosproto.go:56-64 (Command -> value_id; CatchUpLog stays host-side) */
+typedef struct mpx_prepare_reply_min {
+    int32_t id;
+    int32_t instance;
+    int32_t ballot;
+    int32_t last_committed;
+    uint32_t ok;
+    uint32_t value_id;
+} mpx_prepare_reply_min; /* 24 B */
+
+/* bareminpaxos PrepareBookkeeping src/bareminpaxos/bareminpaxos.go:75-82, plus the replica
+ * scalars it reads/writes (defaultBallot, committedUpTo). peerCommits lives in a separate
+ * [groups][N] int32 array.                                                                */
+typedef struct mpx_group_prep_state {
+    int32_t default_ballot;   /* r.defaultBallot (read only)                                */
+    int32_t prepare_oks;
+    int32_t nacks;
+    int32_t max_recv_ballot;
+    int32_t highest_instance; /* highestInstanceNumber                                      */
+    uint32_t value_id;        /* handle of prepareBookkeeping.cmds                          */
+    int32_t committed_upto;   /* r.committedUpTo                                            */
+    uint32_t triggered;       /* number of times the accept trigger (:945) fired            */
+} mpx_group_prep_state; /* 32 B */
+
+/* per-record effect of mpx_prepare_select_min: what the host must do for that reply        */
+#define MPX_EF_COUNTED 1u  /* ballot == defaultBallot: counted (:921-923)                   */
+#define MPX_EF_SELECTED 2u /* became the max (instance, ballot): cmds = reply.Command (:925) */
+#define MPX_EF_CATCHUP 4u  /* copy CatchUpLog[0 .. last_committed-catchup_from] into
+                              instanceSpace[catchup_from ..] (:934-940)                     */
+#define MPX_EF_TRIGGER 8u  /* install Instance{defaultBallot,ACCEPTED,cmds} at highest and
+                              bcastAccept (:945-958)                                        */
+typedef struct mpx_prepare_effect {
+    uint32_t flags;
+    int32_t catchup_from;
+} mpx_prepare_effect; /* 8 B */
+
+/* ---- engine ----------------------------------------------------------------------------- */
+typedef struct mpx_config {
+    int32_t n_replicas;     /* N, 1..16                                                     */
+    int32_t mode;           /* MPX_MODE_MIN / MPX_MODE_CLASSIC                              */
+    uint64_t kv_capacity;   /* key capacity of the engine's KV table (mpx_apply); 0 = 1<<20 */
+    uint32_t kv_per_group;  /* max live keys per group table (mpx_group_step); 0 = 512      */
+    uint32_t flags;         /* reserved, 0                                                  */
+} mpx_config;
+
+typedef struct mpx_engine mpx_engine;
+
+int mpx_abi_version(void);
+int mpx_device_count(int* count);
+int mpx_open(int device, const mpx_config* cfg, mpx_engine** out);
+int mpx_close(mpx_engine* eng);
+const char* mpx_last_error(mpx_engine* eng);
+/* the engine's HIP stream (hipStream_t), for callers that queue their own work on it      */
+void* mpx_stream(mpx_engine* eng);
+int mpx_synchronize(mpx_engine* eng);
+
+/* ---- A1/A2: accept tally (host pointers, synchronous) ----------------------------------
+ * st[i] is the state of instance inst_base+i, updated in place. committed_upto and
+ * peer_commits[N] are in/out (r.committedUpTo, r.prepareBookkeeping.peerCommits).
+ * decided_out (optional, n_inst bytes) = 1 for instances decided in this call, else 0.   */
+int mpx_accept_tally(mpx_engine* eng, const mpx_accept_reply* recs, size_t n,
+                     mpx_inst_state* st, size_t n_inst, int32_t inst_base,
+                     int32_t* committed_upto, int32_t* peer_commits, uint8_t* decided_out);
+
+/* device-pointer variant. st_in/st_out may alias; st_out[i] is written for every instance
+ * that has at least one record (other entries untouched). d_scalars: int32 in/out
+ * [0] = committedUpTo, [1..N] = peerCommits. d_decided (optional): as decided_out.        */
+int mpx_accept_tally_dev(mpx_engine* eng, const mpx_accept_reply* d_recs, size_t n,
+                         const mpx_inst_state* d_st_in, mpx_inst_state* d_st_out,
+                         size_t n_inst, int32_t inst_base, int32_t* d_scalars,
+                         uint8_t* d_decided, void* stream);
+
+/* ---- A4: CLASSIC prepare selection (max-ballot value selection) ------------------------
+ * default_ballot in/out (r.defaultBallot raised to inst.ballot of newly prepared instances)
+ * prepared_out (optional): 1 where the instance became PREPARED in this call.              */
+int mpx_prepare_select(mpx_engine* eng, const mpx_prepare_reply* recs, size_t n,
+                       mpx_prep_state* st, size_t n_inst, int32_t inst_base,
+                       int32_t* default_ballot, uint8_t* prepared_out);
+int mpx_prepare_select_dev(mpx_engine* eng, const mpx_prepare_reply* d_recs, size_t n,
+                           const mpx_prep_state* d_st_in, mpx_prep_state* d_st_out,
+                           size_t n_inst, int32_t inst_base, int32_t* d_default_ballot,
+                           uint8_t* d_prepared, void* stream);
+
+/* ---- A3: MIN prepare selection, one PrepareBookkeeping per group ------------------------
+ * replies of group g are recs[grp_rec_off[g] .. grp_rec_off[g+1]) in arrival order.
+ * peer_commits: [n_groups][N] in/out. eff (optional): one effect per record.              */
+int mpx_prepare_select_min(mpx_engine* eng, const mpx_prepare_reply_min* recs, size_t n,
+                           const uint64_t* grp_rec_off, mpx_group_prep_state* gst,
+                           size_t n_groups, int32_t* peer_commits, mpx_prepare_effect* eff);
+int mpx_prepare_select_min_dev(mpx_engine* eng, const mpx_prepare_reply_min* d_recs,
+                               size_t n, const uint64_t* d_grp_rec_off,
+                               mpx_group_prep_state* d_gst, size_t n_groups,
+                               int32_t* d_peer_commits, mpx_prepare_effect* d_eff,
+                               void* stream);
+
+/* ---- A5/A6: batched KV apply on the engine's State ---------------------------------------
+ * Executes the m commands in array (log) order against the engine's persistent table:
+ * ret[i] = Execute's return value; conf_prev[i] (optional) = state.Conflict(previous command
+ * on the same key in this call, command i), 0 if there is none.                            */
+int mpx_apply(mpx_engine* eng, const uint8_t* op, const int64_t* key, const int64_t* val,
+              size_t m, int64_t* ret, uint8_t* conf_prev);
+int mpx_apply_dev(mpx_engine* eng, const uint8_t* d_op, const int64_t* d_key,
+                  const int64_t* d_val, size_t m, int64_t* d_ret, uint8_t* d_conf_prev,
+                  void* stream);
+/* table access: number of present keys; export (any order) / import / clear               */
+int mpx_kv_size(mpx_engine* eng, size_t* n);
+int mpx_kv_export(mpx_engine* eng, int64_t* keys, int64_t* vals, size_t cap, size_t* n);
+int mpx_kv_import(mpx_engine* eng, const int64_t* keys, const int64_t* vals, size_t n);
+int mpx_kv_clear(mpx_engine* eng);
+
+/* state.ConflictBatch over consecutive instances: out[i] = ConflictBatch(inst i, inst i+1),
+ * instance i = commands [inst_off[i], inst_off[i+1]). out has n_inst-1 entries.            */
+int mpx_conflict_batch(mpx_engine* eng, const uint8_t* op, const int64_t* key,
+                       const uint64_t* inst_off, size_t n_inst, uint8_t* out);
+
+/* ---- A7: CLASSIC commit watermark (updateCommittedUpTo over a status window) ------------ */
+int mpx_committed_prefix(mpx_engine* eng, const mpx_inst_state* st, size_t n_inst,
+                         int32_t inst_base, int32_t* committed_upto);
+
+/* ---- fused per-group step (sharded engine, config 5) -------------------------------------
+ * G independent groups (replicas), each with ipg instance slots (instances 0..ipg-1 in its
+ * own instance space). Group g's accept replies: recs[grp_rec_off[g]..grp_rec_off[g+1]),
+ * grouped by instance, instance numbers group-local. Instance (g,i) owns commands
+ * [cmd_off[g*ipg+i], cmd_off[g*ipg+i+1]); has_cmds (optional) = 0 marks Cmds == nil.
+ * Per group: tally (cfg mode), then executeCommands from executed[g]+1 while
+ * i <= committed[g] and Cmds != nil, against the group's KV table.
+ * KV tables: kv_cnt[g] live entries in kv_key/kv_val[g*kv_per_group ..].                    */
+typedef struct mpx_group_batch {
+    uint32_t n_groups;
+    uint32_t ipg;
+    const mpx_accept_reply* recs;
+    const uint64_t* grp_rec_off;   /* n_groups+1                                            */
+    const mpx_inst_state* st_in;   /* n_groups*ipg                                          */
+    mpx_inst_state* st_out;        /* may alias st_in                                       */
+    const int32_t* committed_in;   /* n_groups                                              */
+    int32_t* committed_out;
+    const int32_t* executed_in;    /* n_groups (last executed instance, -1 = none)          */
+    int32_t* executed_out;
+    const int32_t* peer_in;        /* n_groups*N                                            */
+    int32_t* peer_out;
+    const uint8_t* op;             /* commands, global arrays                               */
+    const int64_t* key;
+    const int64_t* val;
+    const uint32_t* cmd_off;       /* n_groups*ipg+1                                        */
+    const uint8_t* has_cmds;       /* optional, n_groups*ipg                                */
+    int64_t* ret;                  /* written for executed commands                         */
+    uint8_t* conf_prev;            /* optional                                              */
+    const uint32_t* kv_cnt_in;     /* n_groups                                              */
+    const int64_t* kv_key_in;      /* n_groups*kv_per_group                                 */
+    const int64_t* kv_val_in;
+    uint32_t* kv_cnt_out;          /* may alias the inputs                                  */
+    int64_t* kv_key_out;
+    int64_t* kv_val_out;
+    uint8_t* decided;              /* optional, n_groups*ipg                                */
+} mpx_group_batch;
+
+/* host pointers (synchronous) / device pointers (asynchronous on stream)                  */
+int mpx_group_step(mpx_engine* eng, const mpx_group_batch* b);
+int mpx_group_step_dev(mpx_engine* eng, const mpx_group_batch* b, void* stream);
+
+/* ---- multi-GPU: the one collective (RCCL over xGMI) -------------------------------------
+ * Each rank owns a block of groups; non-owned entries must hold -1. After the call every
+ * rank holds max over ranks (= the owner's value) for every group. 128-byte unique id is
+ * produced by rank 0 and broadcast by the caller (e.g. through torch.distributed).         */
+int mpx_comm_unique_id(void* out128);
+int mpx_comm_init(mpx_engine* eng, int nranks, int rank, const void* unique_id128);
+int mpx_watermarks_allreduce(mpx_engine* eng, int32_t* committed, int32_t* executed,
+                             size_t n_groups);
+/* device pointers: committed/executed are one contiguous int32 buffer of 2*n_groups       */
+int mpx_watermarks_allreduce_dev(mpx_engine* eng, int32_t* d_watermarks, size_t n_groups,
+                                 void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPX_H_ */

@@ -1,0 +1,83 @@
+"""ctypes binding of libmpx.so (the C ABI declared in include/mpx.h).
+
+The library is built in-tree (`make -C minpaxos_amd`, or __graft_entry__.build()). There is no
+fallback: if the shared object is missing or fails to load, every entry point raises.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmpx.so")
+
+_p = C.c_void_p
+_i32 = C.c_int32
+_sz = C.c_size_t
+
+
+class MpxConfig(C.Structure):
+    _fields_ = [("n_replicas", C.c_int32), ("mode", C.c_int32), ("kv_capacity", C.c_uint64),
+                ("kv_per_group", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class MpxGroupBatch(C.Structure):
+    _fields_ = [("n_groups", C.c_uint32), ("ipg", C.c_uint32)] + [
+        (name, _p) for name in (
+            "recs", "grp_rec_off", "st_in", "st_out", "committed_in", "committed_out",
+            "executed_in", "executed_out", "peer_in", "peer_out", "op", "key", "val", "cmd_off",
+            "has_cmds", "ret", "conf_prev", "kv_cnt_in", "kv_key_in", "kv_val_in", "kv_cnt_out",
+            "kv_key_out", "kv_val_out", "decided")]
+
+
+# name -> (restype, argtypes); every symbol of include/mpx.h
+SIGNATURES = {
+    "mpx_abi_version": (C.c_int, []),
+    "mpx_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "mpx_open": (C.c_int, [C.c_int, C.POINTER(MpxConfig), C.POINTER(_p)]),
+    "mpx_close": (C.c_int, [_p]),
+    "mpx_last_error": (C.c_char_p, [_p]),
+    "mpx_stream": (_p, [_p]),
+    "mpx_synchronize": (C.c_int, [_p]),
+    "mpx_accept_tally": (C.c_int, [_p, _p, _sz, _p, _sz, _i32, _p, _p, _p]),
+    "mpx_accept_tally_dev": (C.c_int, [_p, _p, _sz, _p, _p, _sz, _i32, _p, _p, _p]),
+    "mpx_prepare_select": (C.c_int, [_p, _p, _sz, _p, _sz, _i32, _p, _p]),
+    "mpx_prepare_select_dev": (C.c_int, [_p, _p, _sz, _p, _p, _sz, _i32, _p, _p, _p]),
+    "mpx_prepare_select_min": (C.c_int, [_p, _p, _sz, _p, _p, _sz, _p, _p]),
+    "mpx_prepare_select_min_dev": (C.c_int, [_p, _p, _sz, _p, _p, _sz, _p, _p, _p]),
+    "mpx_apply": (C.c_int, [_p, _p, _p, _p, _sz, _p, _p]),
+    "mpx_apply_dev": (C.c_int, [_p, _p, _p, _p, _sz, _p, _p, _p]),
+    "mpx_kv_size": (C.c_int, [_p, C.POINTER(_sz)]),
+    "mpx_kv_export": (C.c_int, [_p, _p, _p, _sz, C.POINTER(_sz)]),
+    "mpx_kv_import": (C.c_int, [_p, _p, _p, _sz]),
+    "mpx_kv_clear": (C.c_int, [_p]),
+    "mpx_conflict_batch": (C.c_int, [_p, _p, _p, _p, _sz, _p]),
+    "mpx_committed_prefix": (C.c_int, [_p, _p, _sz, _i32, _p]),
+    "mpx_group_step": (C.c_int, [_p, C.POINTER(MpxGroupBatch)]),
+    "mpx_group_step_dev": (C.c_int, [_p, C.POINTER(MpxGroupBatch), _p]),
+    "mpx_comm_unique_id": (C.c_int, [_p]),
+    "mpx_comm_init": (C.c_int, [_p, C.c_int, C.c_int, _p]),
+    "mpx_watermarks_allreduce": (C.c_int, [_p, _p, _p, _sz]),
+    "mpx_watermarks_allreduce_dev": (C.c_int, [_p, _p, _sz, _p]),
+}
+
+_lib = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def load():
+    """Load libmpx.so (once). Raises NativeLibraryMissing if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryMissing(
+            f"{LIB_PATH} is not built; run `make -C minpaxos_amd` (hipcc, gfx950)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib

@@ -1,0 +1,70 @@
+// common.hpp — shared device helpers for the gfx950 kernels (wave64, CDNA4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mpx.h"
+#include "kernels.hpp"
+
+namespace mpx {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// mask of lanes 0..l inclusive
+__device__ __forceinline__ uint64_t lanes_upto(int l) {
+    return l >= 63 ? ~0ull : ((2ull << l) - 1ull);
+}
+// mask of lanes 0..l-1
+__device__ __forceinline__ uint64_t lanes_below(int l) { return l <= 0 ? 0ull : ((1ull << l) - 1ull); }
+
+__device__ __forceinline__ int hi_bit(uint64_t m) { return 63 - __clzll((long long)m); }
+__device__ __forceinline__ int lo_bit(uint64_t m) { return __ffsll((long long)m) - 1; }
+__device__ __forceinline__ int popc(uint64_t m) { return __popcll(m); }
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+template <typename T>
+__device__ __forceinline__ T readlane(T v, int l);
+template <>
+__device__ __forceinline__ int32_t readlane<int32_t>(int32_t v, int l) {
+    return __builtin_amdgcn_readlane(v, l);
+}
+template <>
+__device__ __forceinline__ uint32_t readlane<uint32_t>(uint32_t v, int l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
+__device__ __forceinline__ void raise_err(uint32_t* err, uint32_t bit) {
+    if (err) atomicOr(err, bit);
+}
+
+// Segmented inclusive max-scan over the wave. `head` marks the first lane of a segment.
+// Lanes before the first head of the wave form an open segment (no head).
+__device__ __forceinline__ int32_t seg_max_scan(int32_t v, bool head) {
+    const int l = lane_id();
+    int f = head ? 1 : 0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        int32_t t = __shfl_up(v, d);
+        int tf = __shfl_up(f, d);
+        if (l >= d && !f) {
+            v = v > t ? v : t;
+            f |= tf;
+        }
+    }
+    return v;
+}
+
+// Wave-wide max of a u64 key held by the lanes in `active` (others contribute 0).
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        uint64_t t = __shfl_xor(v, d);
+        v = v > t ? v : t;
+    }
+    return v;
+}
+
+}  // namespace mpx

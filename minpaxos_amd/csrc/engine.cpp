@@ -1,0 +1,651 @@
+// engine.cpp — the C ABI (include/mpx.h) over the gfx950 kernels.
+//
+// Host-pointer entry points stage through engine-owned device buffers on the engine's HIP
+// stream and return when results are back in caller memory. *_dev entry points enqueue on the
+// caller's stream with device pointers, never allocate and never synchronise.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "kernels.hpp"
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+}  // namespace
+
+struct mpx_engine {
+    int device = 0;
+    mpx_config cfg{};
+    hipStream_t stream = nullptr;
+    std::string err;
+    uint32_t* d_err = nullptr;
+    unsigned long long* d_red = nullptr;
+    // host-API staging
+    DevBuf b[12];
+    // global KV table (mpx_apply)
+    mpx::KvTable kv{};
+    bool kv_ready = false;
+    DevBuf apply_work;
+    // RCCL
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+};
+
+namespace {
+
+int fail(mpx_engine* e, int code, const std::string& what) {
+    if (e) e->err = what;
+    return code;
+}
+
+int hip_fail(mpx_engine* e, const char* what, hipError_t r) {
+    return fail(e, MPX_E_HIP, std::string(what) + ": " + hipGetErrorString(r));
+}
+
+#define HIPCHK(e, x)                                        \
+    do {                                                    \
+        hipError_t _r = (x);                                \
+        if (_r != hipSuccess) return hip_fail((e), #x, _r); \
+    } while (0)
+
+int grow(mpx_engine* e, DevBuf& b, size_t bytes) {
+    if (bytes <= b.cap) return MPX_OK;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    size_t c = std::max(bytes, (size_t)256);
+    if (hipMalloc(&b.p, c) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(e, MPX_E_NOMEM, "device allocation of " + std::to_string(c) + " bytes failed");
+    }
+    b.cap = c;
+    return MPX_OK;
+}
+
+#define GROW(e, buf, bytes)                       \
+    do {                                          \
+        int _c = grow((e), (buf), (bytes));       \
+        if (_c) return _c;                        \
+    } while (0)
+
+hipStream_t pick(mpx_engine* e, void* s) { return s ? (hipStream_t)s : e->stream; }
+
+int check_errword(mpx_engine* e, uint32_t w) {
+    if (!w) return MPX_OK;
+    if (w & mpx::kErrNil)
+        return fail(e, MPX_E_NIL_INSTANCE, "record names a nil or out-of-window instance");
+    if (w & mpx::kErrBadId) return fail(e, MPX_E_BAD_ID, "reply id outside [0, N)");
+    if (w & mpx::kErrOrder)
+        return fail(e, MPX_E_INVAL, "records are not grouped in ascending instance order");
+    if (w & mpx::kErrKvFull) return fail(e, MPX_E_KV_FULL, "KV table capacity exceeded");
+    return fail(e, MPX_E_INVAL, "malformed input (offsets / sizes)");
+}
+
+// synchronise the engine stream, read and clear the device error word
+int finish(mpx_engine* e) {
+    uint32_t w = 0;
+    HIPCHK(e, hipMemcpyAsync(&w, e->d_err, sizeof(w), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (w) HIPCHK(e, hipMemsetAsync(e->d_err, 0, sizeof(uint32_t), e->stream));
+    return check_errword(e, w);
+}
+
+int begin(mpx_engine* e) {
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipMemsetAsync(e->d_err, 0, sizeof(uint32_t), e->stream));
+    return MPX_OK;
+}
+
+int h2d(mpx_engine* e, void* d, const void* h, size_t bytes) {
+    if (!bytes) return MPX_OK;
+    HIPCHK(e, hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, e->stream));
+    return MPX_OK;
+}
+int d2h(mpx_engine* e, void* h, const void* d, size_t bytes) {
+    if (!bytes) return MPX_OK;
+    HIPCHK(e, hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, e->stream));
+    return MPX_OK;
+}
+#define CK(x)                  \
+    do {                       \
+        int _c = (x);          \
+        if (_c) return _c;     \
+    } while (0)
+
+int ensure_kv(mpx_engine* e) {
+    if (e->kv_ready) return MPX_OK;
+    uint64_t want = e->cfg.kv_capacity ? e->cfg.kv_capacity : (1ull << 20);
+    uint64_t cap = 1024;
+    while (cap < 2 * want) cap <<= 1;
+    mpx::KvTable t{};
+    t.cap = cap;
+    // cap hash slots + one side slot for the key INT64_MIN (the empty-slot sentinel)
+    if (hipMalloc(&t.keys, (cap + 1) * 8) != hipSuccess ||
+        hipMalloc(&t.vals, (cap + 1) * 8) != hipSuccess ||
+        hipMalloc(&t.state, (cap + 1) * 4) != hipSuccess ||
+        hipMalloc(&t.n_present, sizeof(unsigned long long)) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(e, MPX_E_NOMEM, "KV table allocation failed");
+    }
+    e->kv = t;
+    HIPCHK(e, mpx::launch_kv_clear(e->kv, e->stream));
+    e->kv_ready = true;
+    return MPX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mpx_abi_version(void) { return MPX_ABI_VERSION; }
+
+int mpx_device_count(int* count) {
+    if (!count) return MPX_E_INVAL;
+    int c = 0;
+    hipError_t r = hipGetDeviceCount(&c);
+    if (r != hipSuccess) {
+        (void)hipGetLastError();
+        *count = 0;
+        return MPX_OK;
+    }
+    *count = c;
+    return MPX_OK;
+}
+
+int mpx_open(int device, const mpx_config* cfg, mpx_engine** out) {
+    if (!cfg || !out) return MPX_E_INVAL;
+    *out = nullptr;
+    if (cfg->n_replicas < 1 || cfg->n_replicas > MPX_MAX_REPLICAS) return MPX_E_INVAL;
+    if (cfg->mode != MPX_MODE_MIN && cfg->mode != MPX_MODE_CLASSIC) return MPX_E_INVAL;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess || device < 0 || device >= c) {
+        (void)hipGetLastError();
+        return MPX_E_NODEV;
+    }
+    mpx_engine* e = new (std::nothrow) mpx_engine();
+    if (!e) return MPX_E_NOMEM;
+    e->device = device;
+    e->cfg = *cfg;
+    if (!e->cfg.kv_per_group) e->cfg.kv_per_group = 512;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&e->d_err, sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&e->d_red, mpx::kRedWords * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(e->d_err, 0, sizeof(uint32_t)) != hipSuccess) {
+        (void)hipGetLastError();
+        mpx_close(e);
+        return MPX_E_HIP;
+    }
+    *out = e;
+    return MPX_OK;
+}
+
+int mpx_close(mpx_engine* e) {
+    if (!e) return MPX_E_INVAL;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->comm) ncclCommDestroy(e->comm);
+    for (auto& x : e->b)
+        if (x.p) (void)hipFree(x.p);
+    if (e->apply_work.p) (void)hipFree(e->apply_work.p);
+    if (e->kv_ready) {
+        (void)hipFree(e->kv.keys);
+        (void)hipFree(e->kv.vals);
+        (void)hipFree(e->kv.state);
+        (void)hipFree(e->kv.n_present);
+    }
+    if (e->d_err) (void)hipFree(e->d_err);
+    if (e->d_red) (void)hipFree(e->d_red);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return MPX_OK;
+}
+
+const char* mpx_last_error(mpx_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+void* mpx_stream(mpx_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+int mpx_synchronize(mpx_engine* e) {
+    if (!e) return MPX_E_INVAL;
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipDeviceSynchronize());
+    return finish(e);
+}
+
+// ---- A1 / A2 --------------------------------------------------------------------------------
+int mpx_accept_tally(mpx_engine* e, const mpx_accept_reply* recs, size_t n, mpx_inst_state* st,
+                     size_t n_inst, int32_t inst_base, int32_t* committed_upto,
+                     int32_t* peer_commits, uint8_t* decided_out) {
+    if (!e) return MPX_E_INVAL;
+    if ((n && !recs) || (n_inst && !st) || !committed_upto || !peer_commits)
+        return fail(e, MPX_E_INVAL, "null argument");
+    if (n >= 0xFFFFFFFFull) return fail(e, MPX_E_UNSUPPORTED, "more than 2^32-2 records");
+    const int N = e->cfg.n_replicas;
+    CK(begin(e));
+    GROW(e, e->b[0], n * sizeof(mpx_accept_reply));
+    GROW(e, e->b[1], n_inst * sizeof(mpx_inst_state));
+    GROW(e, e->b[2], n_inst);
+    GROW(e, e->b[3], (1 + N) * sizeof(int32_t));
+    int32_t sc[1 + MPX_MAX_REPLICAS];
+    sc[0] = *committed_upto;
+    memcpy(sc + 1, peer_commits, N * sizeof(int32_t));
+    CK(h2d(e, e->b[0].p, recs, n * sizeof(mpx_accept_reply)));
+    CK(h2d(e, e->b[1].p, st, n_inst * sizeof(mpx_inst_state)));
+    CK(h2d(e, e->b[3].p, sc, (1 + N) * sizeof(int32_t)));
+    const bool want_dec = decided_out || e->cfg.mode == MPX_MODE_CLASSIC;
+    uint8_t* d_dec = want_dec ? (uint8_t*)e->b[2].p : nullptr;
+    HIPCHK(e, mpx::launch_accept_tally(e->cfg.mode, (const mpx_accept_reply*)e->b[0].p, n,
+                                       (const mpx_inst_state*)e->b[1].p,
+                                       (mpx_inst_state*)e->b[1].p, n_inst, inst_base, N,
+                                       (int32_t*)e->b[3].p, d_dec, e->d_red, e->d_err, e->stream));
+    CK(d2h(e, st, e->b[1].p, n_inst * sizeof(mpx_inst_state)));
+    CK(d2h(e, sc, e->b[3].p, (1 + N) * sizeof(int32_t)));
+    if (decided_out) CK(d2h(e, decided_out, d_dec, n_inst));
+    CK(finish(e));
+    *committed_upto = sc[0];
+    memcpy(peer_commits, sc + 1, N * sizeof(int32_t));
+    return MPX_OK;
+}
+
+int mpx_accept_tally_dev(mpx_engine* e, const mpx_accept_reply* d_recs, size_t n,
+                         const mpx_inst_state* d_st_in, mpx_inst_state* d_st_out, size_t n_inst,
+                         int32_t inst_base, int32_t* d_scalars, uint8_t* d_decided,
+                         void* stream) {
+    if (!e) return MPX_E_INVAL;
+    if ((n && !d_recs) || (n_inst && (!d_st_in || !d_st_out)) || !d_scalars)
+        return fail(e, MPX_E_INVAL, "null argument");
+    if (e->cfg.mode == MPX_MODE_CLASSIC && !d_decided)
+        return fail(e, MPX_E_INVAL, "CLASSIC mode needs d_decided (the commit watermark reads it)");
+    if (n >= 0xFFFFFFFFull) return fail(e, MPX_E_UNSUPPORTED, "more than 2^32-2 records");
+    HIPCHK(e, mpx::launch_accept_tally(e->cfg.mode, d_recs, n, d_st_in, d_st_out, n_inst,
+                                       inst_base, e->cfg.n_replicas, d_scalars, d_decided,
+                                       e->d_red, e->d_err, pick(e, stream)));
+    return MPX_OK;
+}
+
+int mpx_committed_prefix(mpx_engine* e, const mpx_inst_state* st, size_t n_inst,
+                         int32_t inst_base, int32_t* committed_upto) {
+    if (!e) return MPX_E_INVAL;
+    if ((n_inst && !st) || !committed_upto) return fail(e, MPX_E_INVAL, "null argument");
+    CK(begin(e));
+    GROW(e, e->b[1], n_inst * sizeof(mpx_inst_state));
+    GROW(e, e->b[3], sizeof(int32_t));
+    CK(h2d(e, e->b[1].p, st, n_inst * sizeof(mpx_inst_state)));
+    CK(h2d(e, e->b[3].p, committed_upto, sizeof(int32_t)));
+    HIPCHK(e, mpx::launch_committed_prefix((const mpx_inst_state*)e->b[1].p, n_inst, inst_base,
+                                           (int32_t*)e->b[3].p, e->d_red, e->stream));
+    CK(d2h(e, committed_upto, e->b[3].p, sizeof(int32_t)));
+    return finish(e);
+}
+
+// ---- A4 ---------------------------------------------------------------------------------------
+int mpx_prepare_select(mpx_engine* e, const mpx_prepare_reply* recs, size_t n, mpx_prep_state* st,
+                       size_t n_inst, int32_t inst_base, int32_t* default_ballot,
+                       uint8_t* prepared_out) {
+    if (!e) return MPX_E_INVAL;
+    if ((n && !recs) || (n_inst && !st) || !default_ballot)
+        return fail(e, MPX_E_INVAL, "null argument");
+    CK(begin(e));
+    GROW(e, e->b[0], n * sizeof(mpx_prepare_reply));
+    GROW(e, e->b[1], n_inst * sizeof(mpx_prep_state));
+    GROW(e, e->b[2], n_inst);
+    GROW(e, e->b[3], sizeof(int32_t));
+    CK(h2d(e, e->b[0].p, recs, n * sizeof(mpx_prepare_reply)));
+    CK(h2d(e, e->b[1].p, st, n_inst * sizeof(mpx_prep_state)));
+    CK(h2d(e, e->b[3].p, default_ballot, sizeof(int32_t)));
+    uint8_t* d_prep = prepared_out ? (uint8_t*)e->b[2].p : nullptr;
+    HIPCHK(e, mpx::launch_prepare_classic((const mpx_prepare_reply*)e->b[0].p, n,
+                                          (const mpx_prep_state*)e->b[1].p,
+                                          (mpx_prep_state*)e->b[1].p, n_inst, inst_base,
+                                          e->cfg.n_replicas, (int32_t*)e->b[3].p, d_prep,
+                                          e->d_err, e->stream));
+    CK(d2h(e, st, e->b[1].p, n_inst * sizeof(mpx_prep_state)));
+    CK(d2h(e, default_ballot, e->b[3].p, sizeof(int32_t)));
+    if (prepared_out) CK(d2h(e, prepared_out, d_prep, n_inst));
+    return finish(e);
+}
+
+int mpx_prepare_select_dev(mpx_engine* e, const mpx_prepare_reply* d_recs, size_t n,
+                           const mpx_prep_state* d_st_in, mpx_prep_state* d_st_out, size_t n_inst,
+                           int32_t inst_base, int32_t* d_default_ballot, uint8_t* d_prepared,
+                           void* stream) {
+    if (!e) return MPX_E_INVAL;
+    if ((n && !d_recs) || (n_inst && (!d_st_in || !d_st_out)) || !d_default_ballot)
+        return fail(e, MPX_E_INVAL, "null argument");
+    HIPCHK(e, mpx::launch_prepare_classic(d_recs, n, d_st_in, d_st_out, n_inst, inst_base,
+                                          e->cfg.n_replicas, d_default_ballot, d_prepared,
+                                          e->d_err, pick(e, stream)));
+    return MPX_OK;
+}
+
+// ---- A3 ---------------------------------------------------------------------------------------
+int mpx_prepare_select_min(mpx_engine* e, const mpx_prepare_reply_min* recs, size_t n,
+                           const uint64_t* grp_rec_off, mpx_group_prep_state* gst,
+                           size_t n_groups, int32_t* peer_commits, mpx_prepare_effect* eff) {
+    if (!e) return MPX_E_INVAL;
+    if ((n && !recs) || !grp_rec_off || (n_groups && (!gst || !peer_commits)))
+        return fail(e, MPX_E_INVAL, "null argument");
+    if (grp_rec_off[0] != 0 || grp_rec_off[n_groups] != n)
+        return fail(e, MPX_E_INVAL, "grp_rec_off must start at 0 and end at n");
+    for (size_t g = 0; g < n_groups; ++g)
+        if (grp_rec_off[g + 1] < grp_rec_off[g])
+            return fail(e, MPX_E_INVAL, "grp_rec_off must be non-decreasing");
+    const int N = e->cfg.n_replicas;
+    CK(begin(e));
+    GROW(e, e->b[0], n * sizeof(mpx_prepare_reply_min));
+    GROW(e, e->b[4], (n_groups + 1) * sizeof(uint64_t));
+    GROW(e, e->b[1], n_groups * sizeof(mpx_group_prep_state));
+    GROW(e, e->b[5], n_groups * N * sizeof(int32_t));
+    GROW(e, e->b[6], n * sizeof(mpx_prepare_effect));
+    CK(h2d(e, e->b[0].p, recs, n * sizeof(mpx_prepare_reply_min)));
+    CK(h2d(e, e->b[4].p, grp_rec_off, (n_groups + 1) * sizeof(uint64_t)));
+    CK(h2d(e, e->b[1].p, gst, n_groups * sizeof(mpx_group_prep_state)));
+    CK(h2d(e, e->b[5].p, peer_commits, n_groups * N * sizeof(int32_t)));
+    mpx_prepare_effect* d_eff = eff ? (mpx_prepare_effect*)e->b[6].p : nullptr;
+    HIPCHK(e, mpx::launch_prepare_min((const mpx_prepare_reply_min*)e->b[0].p, n,
+                                      (const uint64_t*)e->b[4].p, (mpx_group_prep_state*)e->b[1].p,
+                                      n_groups, N, (int32_t*)e->b[5].p, d_eff, e->d_err,
+                                      e->stream));
+    CK(d2h(e, gst, e->b[1].p, n_groups * sizeof(mpx_group_prep_state)));
+    CK(d2h(e, peer_commits, e->b[5].p, n_groups * N * sizeof(int32_t)));
+    if (eff) CK(d2h(e, eff, d_eff, n * sizeof(mpx_prepare_effect)));
+    return finish(e);
+}
+
+int mpx_prepare_select_min_dev(mpx_engine* e, const mpx_prepare_reply_min* d_recs, size_t n,
+                               const uint64_t* d_grp_rec_off, mpx_group_prep_state* d_gst,
+                               size_t n_groups, int32_t* d_peer_commits,
+                               mpx_prepare_effect* d_eff, void* stream) {
+    if (!e) return MPX_E_INVAL;
+    if ((n && !d_recs) || !d_grp_rec_off || (n_groups && (!d_gst || !d_peer_commits)))
+        return fail(e, MPX_E_INVAL, "null argument");
+    HIPCHK(e, mpx::launch_prepare_min(d_recs, n, d_grp_rec_off, d_gst, n_groups,
+                                      e->cfg.n_replicas, d_peer_commits, d_eff, e->d_err,
+                                      pick(e, stream)));
+    return MPX_OK;
+}
+
+// ---- A5 / A6 ----------------------------------------------------------------------------------
+int mpx_apply(mpx_engine* e, const uint8_t* op, const int64_t* key, const int64_t* val, size_t m,
+              int64_t* ret, uint8_t* conf_prev) {
+    if (!e) return MPX_E_INVAL;
+    if (m && (!op || !key || !val || !ret)) return fail(e, MPX_E_INVAL, "null argument");
+    if (m >= (1ull << 31)) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 commands per call");
+    CK(begin(e));
+    CK(ensure_kv(e));
+    GROW(e, e->b[7], m);
+    GROW(e, e->b[8], m * 8);
+    GROW(e, e->b[9], m * 8);
+    GROW(e, e->b[10], m * 8);
+    GROW(e, e->b[11], m);
+    GROW(e, e->apply_work, mpx::apply_work_bytes(m));
+    CK(h2d(e, e->b[7].p, op, m));
+    CK(h2d(e, e->b[8].p, key, m * 8));
+    CK(h2d(e, e->b[9].p, val, m * 8));
+    mpx::ApplyWork w{e->apply_work.p, e->apply_work.cap};
+    uint8_t* d_conf = conf_prev ? (uint8_t*)e->b[11].p : nullptr;
+    HIPCHK(e, mpx::launch_apply(e->kv, (const uint8_t*)e->b[7].p, (const int64_t*)e->b[8].p,
+                                (const int64_t*)e->b[9].p, m, (int64_t*)e->b[10].p, d_conf, w,
+                                e->d_err, e->stream));
+    CK(d2h(e, ret, e->b[10].p, m * 8));
+    if (conf_prev) CK(d2h(e, conf_prev, d_conf, m));
+    return finish(e);
+}
+
+int mpx_apply_dev(mpx_engine* e, const uint8_t* d_op, const int64_t* d_key, const int64_t* d_val,
+                  size_t m, int64_t* d_ret, uint8_t* d_conf_prev, void* stream) {
+    if (!e) return MPX_E_INVAL;
+    if (m && (!d_op || !d_key || !d_val || !d_ret)) return fail(e, MPX_E_INVAL, "null argument");
+    if (m >= (1ull << 31)) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 commands per call");
+    if (!e->kv_ready || e->apply_work.cap < mpx::apply_work_bytes(m))
+        return fail(e, MPX_E_INVAL,
+                    "mpx_apply_dev: call mpx_kv_clear and one host mpx_apply of >= m commands "
+                    "first (the dev entry point never allocates)");
+    mpx::ApplyWork w{e->apply_work.p, e->apply_work.cap};
+    HIPCHK(e, mpx::launch_apply(e->kv, d_op, d_key, d_val, m, d_ret, d_conf_prev, w, e->d_err,
+                                pick(e, stream)));
+    return MPX_OK;
+}
+
+int mpx_kv_size(mpx_engine* e, size_t* n) {
+    if (!e || !n) return MPX_E_INVAL;
+    CK(begin(e));
+    CK(ensure_kv(e));
+    unsigned long long c = 0;
+    CK(d2h(e, &c, e->kv.n_present, sizeof(c)));
+    CK(finish(e));
+    *n = (size_t)c;
+    return MPX_OK;
+}
+
+int mpx_kv_export(mpx_engine* e, int64_t* keys, int64_t* vals, size_t cap, size_t* n) {
+    if (!e || !n || (cap && (!keys || !vals))) return MPX_E_INVAL;
+    CK(begin(e));
+    CK(ensure_kv(e));
+    unsigned long long c = 0;
+    CK(d2h(e, &c, e->kv.n_present, sizeof(c)));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    const size_t want = (size_t)c;
+    GROW(e, e->b[8], std::max<size_t>(want, 1) * 8);
+    GROW(e, e->b[9], std::max<size_t>(want, 1) * 8);
+    HIPCHK(e, mpx::launch_kv_export(e->kv, (int64_t*)e->b[8].p, (int64_t*)e->b[9].p, want,
+                                    (unsigned long long*)e->d_red, e->stream));
+    const size_t k = std::min(cap, want);
+    CK(d2h(e, keys, e->b[8].p, k * 8));
+    CK(d2h(e, vals, e->b[9].p, k * 8));
+    CK(finish(e));
+    *n = want;
+    return MPX_OK;
+}
+
+int mpx_kv_import(mpx_engine* e, const int64_t* keys, const int64_t* vals, size_t n) {
+    if (!e || (n && (!keys || !vals))) return MPX_E_INVAL;
+    CK(begin(e));
+    CK(ensure_kv(e));
+    GROW(e, e->b[8], n * 8);
+    GROW(e, e->b[9], n * 8);
+    CK(h2d(e, e->b[8].p, keys, n * 8));
+    CK(h2d(e, e->b[9].p, vals, n * 8));
+    HIPCHK(e, mpx::launch_kv_import(e->kv, (const int64_t*)e->b[8].p, (const int64_t*)e->b[9].p, n,
+                                    e->d_err, e->stream));
+    return finish(e);
+}
+
+int mpx_kv_clear(mpx_engine* e) {
+    if (!e) return MPX_E_INVAL;
+    CK(begin(e));
+    CK(ensure_kv(e));
+    HIPCHK(e, mpx::launch_kv_clear(e->kv, e->stream));
+    return finish(e);
+}
+
+int mpx_conflict_batch(mpx_engine* e, const uint8_t* op, const int64_t* key,
+                       const uint64_t* inst_off, size_t n_inst, uint8_t* out) {
+    if (!e) return MPX_E_INVAL;
+    if (n_inst < 2) return MPX_OK;
+    if (!op || !key || !inst_off || !out) return fail(e, MPX_E_INVAL, "null argument");
+    const uint64_t m = inst_off[n_inst];
+    if (inst_off[0] != 0) return fail(e, MPX_E_INVAL, "inst_off[0] must be 0");
+    for (size_t i = 0; i < n_inst; ++i)
+        if (inst_off[i + 1] < inst_off[i]) return fail(e, MPX_E_INVAL, "inst_off not sorted");
+    CK(begin(e));
+    GROW(e, e->b[7], m);
+    GROW(e, e->b[8], m * 8);
+    GROW(e, e->b[4], (n_inst + 1) * 8);
+    GROW(e, e->b[11], n_inst);
+    CK(h2d(e, e->b[7].p, op, m));
+    CK(h2d(e, e->b[8].p, key, m * 8));
+    CK(h2d(e, e->b[4].p, inst_off, (n_inst + 1) * 8));
+    HIPCHK(e, mpx::launch_conflict_batch((const uint8_t*)e->b[7].p, (const int64_t*)e->b[8].p,
+                                         (const uint64_t*)e->b[4].p, n_inst,
+                                         (uint8_t*)e->b[11].p, e->stream));
+    CK(d2h(e, out, e->b[11].p, n_inst - 1));
+    return finish(e);
+}
+
+// ---- fused group step -------------------------------------------------------------------------
+int mpx_group_step_dev(mpx_engine* e, const mpx_group_batch* b, void* stream) {
+    if (!e || !b) return MPX_E_INVAL;
+    if (b->n_groups && (!b->recs || !b->grp_rec_off || !b->st_in || !b->st_out ||
+                        !b->committed_in || !b->committed_out || !b->executed_in ||
+                        !b->executed_out || !b->peer_in || !b->peer_out || !b->op || !b->key ||
+                        !b->val || !b->cmd_off || !b->ret || !b->kv_cnt_in || !b->kv_key_in ||
+                        !b->kv_val_in || !b->kv_cnt_out || !b->kv_key_out || !b->kv_val_out))
+        return fail(e, MPX_E_INVAL, "null field in mpx_group_batch");
+    if (b->ipg == 0 && b->n_groups) return fail(e, MPX_E_INVAL, "ipg must be > 0");
+    HIPCHK(e, mpx::launch_group_step(e->cfg.mode, e->cfg.n_replicas, e->cfg.kv_per_group, b,
+                                     e->d_err, pick(e, stream)));
+    return MPX_OK;
+}
+
+int mpx_group_step(mpx_engine* e, const mpx_group_batch* hb) {
+    if (!e || !hb) return MPX_E_INVAL;
+    const uint64_t G = hb->n_groups, ipg = hb->ipg, ni = G * ipg;
+    const int N = e->cfg.n_replicas;
+    const uint64_t K = e->cfg.kv_per_group;
+    if (!G) return MPX_OK;
+    if (!hb->grp_rec_off || !hb->cmd_off) return fail(e, MPX_E_INVAL, "null offsets");
+    const uint64_t nr = hb->grp_rec_off[G];
+    const uint64_t m = hb->cmd_off[ni];
+    if (hb->grp_rec_off[0] != 0) return fail(e, MPX_E_INVAL, "grp_rec_off[0] must be 0");
+    for (uint64_t g = 0; g < G; ++g)
+        if (hb->grp_rec_off[g + 1] < hb->grp_rec_off[g])
+            return fail(e, MPX_E_INVAL, "grp_rec_off not sorted");
+    for (uint64_t i = 0; i < ni; ++i)
+        if (hb->cmd_off[i + 1] < hb->cmd_off[i]) return fail(e, MPX_E_INVAL, "cmd_off not sorted");
+    CK(begin(e));
+    // one device arena for the whole batch
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off += (bytes + 255) & ~(size_t)255;
+        return o;
+    };
+    const size_t o_recs = take(nr * 16), o_roff = take((G + 1) * 8), o_st = take(ni * 16),
+                 o_ci = take(G * 4), o_co = take(G * 4), o_ei = take(G * 4), o_eo = take(G * 4),
+                 o_pi = take(G * N * 4), o_po = take(G * N * 4), o_op = take(m), o_key = take(m * 8),
+                 o_val = take(m * 8), o_coff = take((ni + 1) * 4), o_has = take(ni),
+                 o_ret = take(m * 8), o_conf = take(m), o_kc = take(G * 4), o_kk = take(G * K * 8),
+                 o_kvv = take(G * K * 8), o_dec = take(ni);
+    GROW(e, e->b[0], off);
+    char* d = (char*)e->b[0].p;
+    mpx_group_batch db{};
+    db.n_groups = (uint32_t)G;
+    db.ipg = (uint32_t)ipg;
+    db.recs = (const mpx_accept_reply*)(d + o_recs);
+    db.grp_rec_off = (const uint64_t*)(d + o_roff);
+    db.st_in = (const mpx_inst_state*)(d + o_st);
+    db.st_out = (mpx_inst_state*)(d + o_st);
+    db.committed_in = (const int32_t*)(d + o_ci);
+    db.committed_out = (int32_t*)(d + o_co);
+    db.executed_in = (const int32_t*)(d + o_ei);
+    db.executed_out = (int32_t*)(d + o_eo);
+    db.peer_in = (const int32_t*)(d + o_pi);
+    db.peer_out = (int32_t*)(d + o_po);
+    db.op = (const uint8_t*)(d + o_op);
+    db.key = (const int64_t*)(d + o_key);
+    db.val = (const int64_t*)(d + o_val);
+    db.cmd_off = (const uint32_t*)(d + o_coff);
+    db.has_cmds = hb->has_cmds ? (const uint8_t*)(d + o_has) : nullptr;
+    db.ret = (int64_t*)(d + o_ret);
+    db.conf_prev = hb->conf_prev ? (uint8_t*)(d + o_conf) : nullptr;
+    db.kv_cnt_in = (const uint32_t*)(d + o_kc);
+    db.kv_key_in = (const int64_t*)(d + o_kk);
+    db.kv_val_in = (const int64_t*)(d + o_kvv);
+    db.kv_cnt_out = (uint32_t*)(d + o_kc);
+    db.kv_key_out = (int64_t*)(d + o_kk);
+    db.kv_val_out = (int64_t*)(d + o_kvv);
+    db.decided = hb->decided ? (uint8_t*)(d + o_dec) : nullptr;
+    CK(h2d(e, d + o_recs, hb->recs, nr * 16));
+    CK(h2d(e, d + o_roff, hb->grp_rec_off, (G + 1) * 8));
+    CK(h2d(e, d + o_st, hb->st_in, ni * 16));
+    CK(h2d(e, d + o_ci, hb->committed_in, G * 4));
+    CK(h2d(e, d + o_ei, hb->executed_in, G * 4));
+    CK(h2d(e, d + o_pi, hb->peer_in, G * N * 4));
+    CK(h2d(e, d + o_op, hb->op, m));
+    CK(h2d(e, d + o_key, hb->key, m * 8));
+    CK(h2d(e, d + o_val, hb->val, m * 8));
+    CK(h2d(e, d + o_coff, hb->cmd_off, (ni + 1) * 4));
+    if (hb->has_cmds) CK(h2d(e, d + o_has, hb->has_cmds, ni));
+    CK(h2d(e, d + o_ret, hb->ret, m * 8));  // unexecuted commands keep the caller's values
+    if (hb->conf_prev) CK(h2d(e, d + o_conf, hb->conf_prev, m));
+    CK(h2d(e, d + o_kc, hb->kv_cnt_in, G * 4));
+    CK(h2d(e, d + o_kk, hb->kv_key_in, G * K * 8));
+    CK(h2d(e, d + o_kvv, hb->kv_val_in, G * K * 8));
+    HIPCHK(e, mpx::launch_group_step(e->cfg.mode, N, (uint32_t)K, &db, e->d_err, e->stream));
+    CK(d2h(e, hb->st_out, d + o_st, ni * 16));
+    CK(d2h(e, hb->committed_out, d + o_co, G * 4));
+    CK(d2h(e, hb->executed_out, d + o_eo, G * 4));
+    CK(d2h(e, hb->peer_out, d + o_po, G * N * 4));
+    CK(d2h(e, hb->ret, d + o_ret, m * 8));
+    if (hb->conf_prev) CK(d2h(e, hb->conf_prev, d + o_conf, m));
+    CK(d2h(e, hb->kv_cnt_out, d + o_kc, G * 4));
+    CK(d2h(e, hb->kv_key_out, d + o_kk, G * K * 8));
+    CK(d2h(e, hb->kv_val_out, d + o_kvv, G * K * 8));
+    if (hb->decided) CK(d2h(e, hb->decided, d + o_dec, ni));
+    return finish(e);
+}
+
+// ---- RCCL -------------------------------------------------------------------------------------
+int mpx_comm_unique_id(void* out128) {
+    if (!out128) return MPX_E_INVAL;
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return MPX_E_RCCL;
+    memcpy(out128, &id, sizeof(id));
+    return MPX_OK;
+}
+
+int mpx_comm_init(mpx_engine* e, int nranks, int rank, const void* unique_id128) {
+    if (!e || !unique_id128 || nranks < 1 || rank < 0 || rank >= nranks) return MPX_E_INVAL;
+    HIPCHK(e, hipSetDevice(e->device));
+    if (e->comm) {
+        ncclCommDestroy(e->comm);
+        e->comm = nullptr;
+    }
+    ncclUniqueId id;
+    memcpy(&id, unique_id128, sizeof(id));
+    ncclResult_t r = ncclCommInitRank(&e->comm, nranks, id, rank);
+    if (r != ncclSuccess) {
+        e->comm = nullptr;
+        return fail(e, MPX_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    e->nranks = nranks;
+    e->rank = rank;
+    return MPX_OK;
+}
+
+int mpx_watermarks_allreduce_dev(mpx_engine* e, int32_t* d_wm, size_t n_groups, void* stream) {
+    if (!e || (n_groups && !d_wm)) return MPX_E_INVAL;
+    if (!e->comm) return fail(e, MPX_E_INVAL, "mpx_comm_init has not been called");
+    ncclResult_t r = ncclAllReduce(d_wm, d_wm, 2 * n_groups, ncclInt32, ncclMax, e->comm,
+                                   pick(e, stream));
+    if (r != ncclSuccess) return fail(e, MPX_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    return MPX_OK;
+}
+
+int mpx_watermarks_allreduce(mpx_engine* e, int32_t* committed, int32_t* executed,
+                             size_t n_groups) {
+    if (!e || (n_groups && (!committed || !executed))) return MPX_E_INVAL;
+    CK(begin(e));
+    GROW(e, e->b[5], 2 * n_groups * 4);
+    int32_t* d = (int32_t*)e->b[5].p;
+    CK(h2d(e, d, committed, n_groups * 4));
+    CK(h2d(e, d + n_groups, executed, n_groups * 4));
+    CK(mpx_watermarks_allreduce_dev(e, d, n_groups, e->stream));
+    CK(d2h(e, committed, d, n_groups * 4));
+    CK(d2h(e, executed, d + n_groups, n_groups * 4));
+    return finish(e);
+}
+
+}  // extern "C"

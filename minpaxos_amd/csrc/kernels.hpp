@@ -1,0 +1,72 @@
+// kernels.hpp — launchers exported by the .hip translation units to the C-ABI layer.
+// Every launcher only enqueues on `stream` (no allocation, no synchronisation), so callers can
+// capture sequences of them into a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mpx.h"
+
+namespace mpx {
+
+// error bits raised by kernels into the engine's device error word
+constexpr uint32_t kErrNil = 1u;     // record names a nil / out-of-window instance
+constexpr uint32_t kErrBadId = 2u;   // reply id outside [0, N)
+constexpr uint32_t kErrOrder = 4u;   // records not in ascending instance order
+constexpr uint32_t kErrKvFull = 8u;  // KV capacity exceeded
+constexpr uint32_t kErrInval = 16u;  // other malformed input (offsets, sizes)
+
+// reduction scratch: kRedWords u64 per engine
+constexpr int kRedWords = 64;
+
+hipError_t launch_accept_tally(int mode, const mpx_accept_reply* recs, uint64_t n,
+                               const mpx_inst_state* st_in, mpx_inst_state* st_out,
+                               uint64_t n_inst, int32_t base, int32_t nrep, int32_t* scalars,
+                               uint8_t* decided, unsigned long long* red, uint32_t* err,
+                               hipStream_t stream);
+
+hipError_t launch_committed_prefix(const mpx_inst_state* st, uint64_t n_inst, int32_t base,
+                                   int32_t* scalars, unsigned long long* red, hipStream_t stream);
+
+hipError_t launch_prepare_classic(const mpx_prepare_reply* recs, uint64_t n,
+                                  const mpx_prep_state* st_in, mpx_prep_state* st_out,
+                                  uint64_t n_inst, int32_t base, int32_t nrep,
+                                  int32_t* default_ballot, uint8_t* prepared, uint32_t* err,
+                                  hipStream_t stream);
+
+hipError_t launch_prepare_min(const mpx_prepare_reply_min* recs, uint64_t n,
+                              const uint64_t* grp_rec_off, mpx_group_prep_state* gst,
+                              uint64_t n_groups, int32_t nrep, int32_t* peer_commits,
+                              mpx_prepare_effect* eff, uint32_t* err, hipStream_t stream);
+
+hipError_t launch_conflict_batch(const uint8_t* op, const int64_t* key, const uint64_t* inst_off,
+                                 uint64_t n_inst, uint8_t* out, hipStream_t stream);
+
+// fused per-group step: tally + executeCommands against per-group compact KV tables
+hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
+                             const mpx_group_batch* b, uint32_t* err, hipStream_t stream);
+
+// ---- global KV table apply (mpx_apply) ----------------------------------------------------
+struct KvTable {
+    int64_t* keys;       // [cap]
+    int64_t* vals;       // [cap]
+    uint32_t* state;     // [cap] 0 empty, 1 claimed, 2 key published, |4 present (has value)
+    uint64_t cap;        // power of two
+    unsigned long long* n_present;  // device counter
+};
+
+struct ApplyWork {      // scratch sized for m commands (see apply_work_bytes)
+    void* base;
+    uint64_t bytes;
+};
+uint64_t apply_work_bytes(uint64_t m);
+hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
+                        uint64_t m, int64_t* ret, uint8_t* conf, ApplyWork& w, uint32_t* err,
+                        hipStream_t stream);
+hipError_t launch_kv_clear(KvTable& t, hipStream_t stream);
+hipError_t launch_kv_import(KvTable& t, const int64_t* keys, const int64_t* vals, uint64_t n,
+                            uint32_t* err, hipStream_t stream);
+hipError_t launch_kv_export(KvTable& t, int64_t* keys, int64_t* vals, uint64_t cap,
+                            unsigned long long* counter, hipStream_t stream);
+
+}  // namespace mpx

@@ -1,0 +1,265 @@
+"""Python handle over the C ABI (numpy in, numpy out; device pointers for the *_dev paths).
+
+Names and argument meaning follow the reference handlers they replace:
+  accept_tally        <- bareminpaxos / paxos  handleAcceptReply
+  prepare_select      <- paxos.handlePrepareReply          (CLASSIC, per instance)
+  prepare_select_min  <- bareminpaxos.handlePrepareReply   (MIN, per group)
+  apply               <- executeCommands -> state.Command.Execute (+ state.Conflict)
+  conflict_batch      <- state.ConflictBatch
+  committed_prefix    <- updateCommittedUpTo
+  group_step          <- handleAcceptReply + executeCommands for many replicas at once
+Errors come back as MpxError carrying the reference-level reason (e.g. E_NIL_INSTANCE where the
+Go handler would dereference a nil *Instance).
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from . import records as R
+
+
+class MpxError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{R.ERROR_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+def device_count():
+    lib = _lib.load()
+    c = C.c_int(0)
+    lib.mpx_device_count(C.byref(c))
+    return c.value
+
+
+class Engine:
+    def __init__(self, device=0, n_replicas=5, mode=R.MODE_MIN, kv_capacity=0, kv_per_group=0):
+        self.lib = _lib.load()
+        if isinstance(mode, str):
+            mode = {"min": R.MODE_MIN, "classic": R.MODE_CLASSIC}[mode.lower()]
+        self.n_replicas = n_replicas
+        self.mode = mode
+        self.kv_per_group = kv_per_group or 512
+        cfg = _lib.MpxConfig(n_replicas, mode, kv_capacity, kv_per_group, 0)
+        h = C.c_void_p()
+        rc = self.lib.mpx_open(device, C.byref(cfg), C.byref(h))
+        if rc != 0:
+            raise MpxError(rc, f"mpx_open(device={device})")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.mpx_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self.lib.mpx_last_error(self.h)
+            raise MpxError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    @property
+    def stream(self):
+        return self.lib.mpx_stream(self.h)
+
+    def synchronize(self):
+        self._check(self.lib.mpx_synchronize(self.h), "mpx_synchronize")
+
+    # ---- A1 / A2 ----------------------------------------------------------------------------
+    def accept_tally(self, recs, st, inst_base=0, committed_upto=-1, peer_commits=None,
+                     want_decided=True):
+        recs = _c(recs, R.ACCEPT_REPLY)
+        st = np.array(st, dtype=R.INST_STATE, copy=True)
+        pc = np.zeros(self.n_replicas, np.int32) if peer_commits is None else \
+            np.array(peer_commits, dtype=np.int32, copy=True)
+        cu = C.c_int32(committed_upto)
+        dec = np.zeros(len(st), np.uint8) if want_decided else None
+        rc = self.lib.mpx_accept_tally(self.h, _ptr(recs), len(recs), _ptr(st), len(st), inst_base,
+                                       C.byref(cu), _ptr(pc), _ptr(dec))
+        self._check(rc, "mpx_accept_tally")
+        return st, cu.value, pc, dec
+
+    def accept_tally_dev(self, d_recs, n, d_st_in, d_st_out, n_inst, inst_base, d_scalars,
+                         d_decided=None, stream=None):
+        rc = self.lib.mpx_accept_tally_dev(self.h, d_recs, n, d_st_in, d_st_out, n_inst,
+                                           inst_base, d_scalars, d_decided, stream)
+        self._check(rc, "mpx_accept_tally_dev")
+
+    def committed_prefix(self, st, inst_base, committed_upto):
+        st = _c(st, R.INST_STATE)
+        cu = C.c_int32(committed_upto)
+        self._check(self.lib.mpx_committed_prefix(self.h, _ptr(st), len(st), inst_base,
+                                                  C.byref(cu)), "mpx_committed_prefix")
+        return cu.value
+
+    # ---- A4 ---------------------------------------------------------------------------------
+    def prepare_select(self, recs, st, inst_base=0, default_ballot=-1, want_prepared=True):
+        recs = _c(recs, R.PREPARE_REPLY)
+        st = np.array(st, dtype=R.PREP_STATE, copy=True)
+        db = C.c_int32(default_ballot)
+        prep = np.zeros(len(st), np.uint8) if want_prepared else None
+        rc = self.lib.mpx_prepare_select(self.h, _ptr(recs), len(recs), _ptr(st), len(st),
+                                         inst_base, C.byref(db), _ptr(prep))
+        self._check(rc, "mpx_prepare_select")
+        return st, db.value, prep
+
+    def prepare_select_dev(self, d_recs, n, d_st_in, d_st_out, n_inst, inst_base,
+                           d_default_ballot, d_prepared=None, stream=None):
+        rc = self.lib.mpx_prepare_select_dev(self.h, d_recs, n, d_st_in, d_st_out, n_inst,
+                                             inst_base, d_default_ballot, d_prepared, stream)
+        self._check(rc, "mpx_prepare_select_dev")
+
+    # ---- A3 ---------------------------------------------------------------------------------
+    def prepare_select_min(self, recs, grp_rec_off, gst, peer_commits=None, want_effects=True):
+        recs = _c(recs, R.PREPARE_REPLY_MIN)
+        off = _c(grp_rec_off, np.uint64)
+        gst = np.array(gst, dtype=R.GROUP_PREP_STATE, copy=True)
+        g = len(gst)
+        pc = np.zeros(g * self.n_replicas, np.int32) if peer_commits is None else \
+            np.array(peer_commits, dtype=np.int32, copy=True).reshape(-1)
+        eff = np.zeros(len(recs), R.PREPARE_EFFECT) if want_effects else None
+        rc = self.lib.mpx_prepare_select_min(self.h, _ptr(recs), len(recs), _ptr(off), _ptr(gst),
+                                             g, _ptr(pc), _ptr(eff))
+        self._check(rc, "mpx_prepare_select_min")
+        return gst, pc, eff
+
+    def prepare_select_min_dev(self, d_recs, n, d_off, d_gst, n_groups, d_peer, d_eff=None,
+                               stream=None):
+        rc = self.lib.mpx_prepare_select_min_dev(self.h, d_recs, n, d_off, d_gst, n_groups,
+                                                 d_peer, d_eff, stream)
+        self._check(rc, "mpx_prepare_select_min_dev")
+
+    # ---- A5 / A6 ----------------------------------------------------------------------------
+    def apply(self, op, key, val, want_conf=True):
+        op = _c(op, np.uint8)
+        key = _c(key, np.int64)
+        val = _c(val, np.int64)
+        m = len(op)
+        ret = np.zeros(m, np.int64)
+        conf = np.zeros(m, np.uint8) if want_conf else None
+        rc = self.lib.mpx_apply(self.h, _ptr(op), _ptr(key), _ptr(val), m, _ptr(ret), _ptr(conf))
+        self._check(rc, "mpx_apply")
+        return ret, conf
+
+    def apply_dev(self, d_op, d_key, d_val, m, d_ret, d_conf=None, stream=None):
+        self._check(self.lib.mpx_apply_dev(self.h, d_op, d_key, d_val, m, d_ret, d_conf, stream),
+                    "mpx_apply_dev")
+
+    def kv_size(self):
+        n = C.c_size_t(0)
+        self._check(self.lib.mpx_kv_size(self.h, C.byref(n)), "mpx_kv_size")
+        return n.value
+
+    def kv_export(self):
+        """Present (key, value) pairs sorted by key."""
+        n = self.kv_size()
+        keys = np.zeros(max(n, 1), np.int64)
+        vals = np.zeros(max(n, 1), np.int64)
+        got = C.c_size_t(0)
+        self._check(self.lib.mpx_kv_export(self.h, _ptr(keys), _ptr(vals), n, C.byref(got)),
+                    "mpx_kv_export")
+        k = min(n, got.value)
+        order = np.argsort(keys[:k], kind="stable")
+        return keys[:k][order], vals[:k][order]
+
+    def kv_import(self, keys, vals):
+        keys = _c(keys, np.int64)
+        vals = _c(vals, np.int64)
+        self._check(self.lib.mpx_kv_import(self.h, _ptr(keys), _ptr(vals), len(keys)),
+                    "mpx_kv_import")
+
+    def kv_clear(self):
+        self._check(self.lib.mpx_kv_clear(self.h), "mpx_kv_clear")
+
+    def conflict_batch(self, op, key, inst_off):
+        op = _c(op, np.uint8)
+        key = _c(key, np.int64)
+        off = _c(inst_off, np.uint64)
+        n_inst = len(off) - 1
+        out = np.zeros(max(n_inst - 1, 1), np.uint8)
+        self._check(self.lib.mpx_conflict_batch(self.h, _ptr(op), _ptr(key), _ptr(off), n_inst,
+                                                _ptr(out)), "mpx_conflict_batch")
+        return out[:max(n_inst - 1, 0)]
+
+    # ---- fused group step -------------------------------------------------------------------
+    def group_step(self, b, kv_cnt=None, kv_key=None, kv_val=None, ret=None, want_conf=True,
+                   want_decided=True):
+        """b: dict from synth.group_batch (or the same fields). Returns a dict of outputs."""
+        G, ipg, N = int(b["n_groups"]), int(b["ipg"]), self.n_replicas
+        K = self.kv_per_group
+        recs = _c(b["recs"], R.ACCEPT_REPLY)
+        off = _c(b["grp_rec_off"], np.uint64)
+        st = np.array(b["st_in"], dtype=R.INST_STATE, copy=True)
+        ci = _c(b["committed_in"], np.int32)
+        ei = _c(b["executed_in"], np.int32)
+        pi = _c(b["peer_in"], np.int32)
+        op, key, val = _c(b["op"], np.uint8), _c(b["key"], np.int64), _c(b["val"], np.int64)
+        coff = _c(b["cmd_off"], np.uint32)
+        has = _c(b["has_cmds"], np.uint8) if b.get("has_cmds") is not None else None
+        m = len(op)
+        ret = np.zeros(m, np.int64) if ret is None else np.array(ret, np.int64, copy=True)
+        conf = np.zeros(m, np.uint8) if want_conf else None
+        kc = np.zeros(G, np.uint32) if kv_cnt is None else np.array(kv_cnt, np.uint32, copy=True)
+        kk = np.zeros(G * K, np.int64) if kv_key is None else np.array(kv_key, np.int64, copy=True)
+        kv = np.zeros(G * K, np.int64) if kv_val is None else np.array(kv_val, np.int64, copy=True)
+        co = np.zeros(G, np.int32)
+        eo = np.zeros(G, np.int32)
+        po = np.zeros(G * N, np.int32)
+        dec = np.zeros(G * ipg, np.uint8) if want_decided else None
+        gb = _lib.MpxGroupBatch(G, ipg, *[C.cast(_ptr(x), C.c_void_p) if x is not None else None
+                                          for x in (recs, off, st, st, ci, co, ei, eo, pi, po, op,
+                                                    key, val, coff, has, ret, conf, kc, kk, kv,
+                                                    kc, kk, kv, dec)])
+        self._check(self.lib.mpx_group_step(self.h, C.byref(gb)), "mpx_group_step")
+        return dict(st_out=st, committed_out=co, executed_out=eo, peer_out=po, ret=ret,
+                    conf_prev=conf, kv_cnt=kc, kv_key=kk, kv_val=kv, decided=dec)
+
+    def group_step_dev(self, gb, stream=None):
+        self._check(self.lib.mpx_group_step_dev(self.h, C.byref(gb), stream), "mpx_group_step_dev")
+
+    # ---- multi-GPU ----------------------------------------------------------------------------
+    @staticmethod
+    def comm_unique_id():
+        lib = _lib.load()
+        buf = (C.c_ubyte * 128)()
+        rc = lib.mpx_comm_unique_id(C.cast(buf, C.c_void_p))
+        if rc != 0:
+            raise MpxError(rc, "mpx_comm_unique_id")
+        return bytes(buf)
+
+    def comm_init(self, nranks, rank, uid):
+        buf = (C.c_ubyte * 128).from_buffer_copy(uid)
+        self._check(self.lib.mpx_comm_init(self.h, nranks, rank, C.cast(buf, C.c_void_p)),
+                    "mpx_comm_init")
+
+    def watermarks_allreduce(self, committed, executed):
+        c = np.array(committed, np.int32, copy=True)
+        e = np.array(executed, np.int32, copy=True)
+        self._check(self.lib.mpx_watermarks_allreduce(self.h, _ptr(c), _ptr(e), len(c)),
+                    "mpx_watermarks_allreduce")
+        return c, e
+
+    def watermarks_allreduce_dev(self, d_wm, n_groups, stream=None):
+        self._check(self.lib.mpx_watermarks_allreduce_dev(self.h, d_wm, n_groups, stream),
+                    "mpx_watermarks_allreduce_dev")

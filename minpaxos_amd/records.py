@@ -1,0 +1,59 @@
+"""numpy mirrors of the packed records in include/mpx.h.
+
+Each dtype is byte-identical to its C struct, so arrays can be handed to the C ABI
+(ctypes) or viewed as int32 words for device tensors.
+"""
+import numpy as np
+
+# minpaxosproto.InstanceStatus  src/minpaxosproto/minpaxosproto.go:8-15
+PREPARING, PREPARED, ACCEPTED, COMMITTED = 0, 1, 2, 3
+STATUS_NIL = -1  # instanceSpace[i] == nil
+
+# state.Operation  src/state/state.go:10-19
+OP_NONE, OP_PUT, OP_GET, OP_DELETE, OP_RLOCK, OP_WLOCK = 0, 1, 2, 3, 4, 5
+
+MODE_MIN, MODE_CLASSIC = 0, 1
+MAX_REPLICAS = 16
+
+# mpx_prep_state.flags
+PF_HAS_PROPOSALS, PF_REQUEUED, PF_PREPARED_NOW = 1, 2, 4
+# mpx_prepare_effect.flags
+EF_COUNTED, EF_SELECTED, EF_CATCHUP, EF_TRIGGER = 1, 2, 4, 8
+
+# error codes
+OK = 0
+E_INVAL, E_NOMEM, E_HIP, E_RCCL, E_NIL_INSTANCE, E_BAD_ID, E_KV_FULL, E_NODEV, E_UNSUPPORTED = (
+    -1, -2, -3, -4, -5, -6, -7, -8, -9)
+ERROR_NAMES = {
+    0: "OK", -1: "E_INVAL", -2: "E_NOMEM", -3: "E_HIP", -4: "E_RCCL", -5: "E_NIL_INSTANCE",
+    -6: "E_BAD_ID", -7: "E_KV_FULL", -8: "E_NODEV", -9: "E_UNSUPPORTED",
+}
+
+# mpx_accept_reply  <- minpaxosproto.AcceptReply{Instance,OK,Ballot,Id}
+ACCEPT_REPLY = np.dtype([("instance", "<i4"), ("ballot", "<i4"), ("id", "<i4"), ("ok", "u1"),
+                         ("pad", "u1", (3,))])
+# mpx_inst_state  <- Instance.Status + LeaderBookkeeping
+INST_STATE = np.dtype([("status", "<i4"), ("accept_oks", "<i4"), ("nacks", "<i4"),
+                       ("max_recv_ballot", "<i4")])
+# mpx_prepare_reply  <- paxosproto.PrepareReply{Instance,OK,Ballot,Command}
+PREPARE_REPLY = np.dtype([("instance", "<i4"), ("ballot", "<i4"), ("ok", "<u4"),
+                          ("value_id", "<u4")])
+# mpx_prep_state  <- paxos Instance{cmds,ballot,status,lb}
+PREP_STATE = np.dtype([("ballot", "<i4"), ("status", "<i4"), ("prepare_oks", "<i4"),
+                       ("nacks", "<i4"), ("max_recv_ballot", "<i4"), ("value_id", "<u4"),
+                       ("flags", "<u4"), ("pad", "<u4")])
+# mpx_prepare_reply_min  <- minpaxosproto.PrepareReply
+PREPARE_REPLY_MIN = np.dtype([("id", "<i4"), ("instance", "<i4"), ("ballot", "<i4"),
+                              ("last_committed", "<i4"), ("ok", "<u4"), ("value_id", "<u4")])
+# mpx_group_prep_state  <- bareminpaxos PrepareBookkeeping + replica scalars
+GROUP_PREP_STATE = np.dtype([("default_ballot", "<i4"), ("prepare_oks", "<i4"), ("nacks", "<i4"),
+                             ("max_recv_ballot", "<i4"), ("highest_instance", "<i4"),
+                             ("value_id", "<u4"), ("committed_upto", "<i4"),
+                             ("triggered", "<u4")])
+# mpx_prepare_effect
+PREPARE_EFFECT = np.dtype([("flags", "<u4"), ("catchup_from", "<i4")])
+
+assert ACCEPT_REPLY.itemsize == 16 and INST_STATE.itemsize == 16
+assert PREPARE_REPLY.itemsize == 16 and PREP_STATE.itemsize == 32
+assert PREPARE_REPLY_MIN.itemsize == 24 and GROUP_PREP_STATE.itemsize == 32
+assert PREPARE_EFFECT.itemsize == 8

@@ -1,0 +1,57 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+TESTS = os.path.dirname(os.path.abspath(__file__))
+if TESTS not in sys.path:
+    sys.path.insert(0, TESTS)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP engine)")
+    config.addinivalue_line("markers", "slow: larger parity sizes")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _built():
+    """Build the oracle (g++) and, where hipcc exists, the engine (incremental make)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    if os.path.exists("/opt/rocm/bin/hipcc"):
+        subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "minpaxos_amd")], check=True)
+    yield
+
+
+@pytest.fixture(scope="session")
+def have_gpu():
+    from minpaxos_amd import engine
+    return engine.device_count() > 0
+
+
+@pytest.fixture
+def mk_oracle():
+    from oracle_lib import Oracle
+
+    def mk(n, mode, **kw):
+        return Oracle(n_replicas=n, mode=mode, **kw)
+    return mk
+
+
+@pytest.fixture
+def mk_engine():
+    from minpaxos_amd.engine import Engine, device_count
+    if device_count() < 1:
+        pytest.fail("GPU test collected but no HIP device is visible")
+    made = []
+
+    def mk(n, mode, **kw):
+        e = Engine(0, n_replicas=n, mode=mode, **kw)
+        made.append(e)
+        return e
+    yield mk
+    for e in made:
+        e.close()

@@ -1,0 +1,266 @@
+"""HIP engine vs the CPU oracle, bit-exact, through the C ABI (host-pointer entry points).
+
+Sizes are chosen so the oracle finishes in seconds; the full BASELINE sizes are covered by
+test_gpu_full.py.
+"""
+import numpy as np
+import pytest
+
+import gen_cases
+import kat_cases
+from oracle_lib import Oracle, OracleError
+from minpaxos_amd import records as R
+from minpaxos_amd import synth
+from minpaxos_amd.engine import MpxError
+
+pytestmark = pytest.mark.gpu
+
+
+def eq_struct(a, b):
+    assert a.dtype == b.dtype
+    for f in a.dtype.names:
+        if f == "pad":
+            continue
+        bad = np.nonzero(a[f] != b[f])[0]
+        assert len(bad) == 0, f"field {f} differs at {bad[:10]}: {a[f][bad[:5]]} vs {b[f][bad[:5]]}"
+
+
+@pytest.mark.parametrize("case", kat_cases.ALL, ids=lambda f: f.__name__)
+def test_engine_kat(case, mk_engine):
+    case(mk_engine)
+
+
+# ---- A1 / A2 ----------------------------------------------------------------------------------
+@pytest.mark.parametrize("mode", [R.MODE_MIN, R.MODE_CLASSIC])
+@pytest.mark.parametrize("n_rep", [1, 2, 3, 5, 7, 16])
+def test_accept_tally_ragged(mk_engine, mode, n_rep):
+    rng = np.random.default_rng(1000 + 17 * n_rep + mode)
+    for trial in range(3):
+        rec, st = gen_cases.ragged_accept(rng, 3000, n_rep, max_r=9, long_every=997,
+                                          long_len=200 + 70 * trial, base=trial * 50)
+        e, o = mk_engine(n_rep, mode), Oracle(n_rep, mode)
+        cu0 = int(rng.integers(-1, 60))
+        pc0 = rng.integers(-1, 10, n_rep).astype(np.int32)
+        got = e.accept_tally(rec, st, trial * 50, cu0, pc0)
+        want = o.accept_tally(rec, st, trial * 50, cu0, pc0)
+        eq_struct(got[0], want[0])
+        assert got[1] == want[1], (got[1], want[1])
+        assert np.array_equal(got[2], want[2])
+        assert np.array_equal(got[3], want[3])
+
+
+@pytest.mark.parametrize("mode", [R.MODE_MIN, R.MODE_CLASSIC])
+def test_accept_tally_config2_shape(mk_engine, mode):
+    rec, st = synth.accept_replies(1 << 16, 5, 0.7, seed=42)
+    e, o = mk_engine(5, mode), Oracle(5, mode)
+    got = e.accept_tally(rec, st, 0, -1, np.zeros(5, np.int32))
+    want = o.accept_tally(rec, st, 0, -1, np.zeros(5, np.int32))
+    eq_struct(got[0], want[0])
+    assert got[1:3][0] == want[1] and np.array_equal(got[2], want[2])
+    assert np.array_equal(got[3], want[3])
+
+
+def test_accept_tally_edges(mk_engine):
+    e = mk_engine(5, R.MODE_MIN)
+    # empty batch
+    st = kat_cases.inst_states(4)
+    got = e.accept_tally(np.zeros(0, R.ACCEPT_REPLY), st, 0, 3, np.arange(5, dtype=np.int32))
+    assert got[1] == 3 and list(got[2]) == [0, 1, 2, 3, 4] and not got[3].any()
+    # one instance with 5000 replies (MAX_BATCH-sized fan-in) spanning many waves
+    rec = kat_cases.acc(2, [(1 + (k % 4), int(k % 3 != 0), 16) for k in range(5000)])
+    o = Oracle(5, R.MODE_MIN)
+    g = e.accept_tally(rec, kat_cases.inst_states(3), 0, -1)
+    w = o.accept_tally(rec, kat_cases.inst_states(3), 0, -1)
+    eq_struct(g[0], w[0])
+    assert g[1] == w[1] and np.array_equal(g[2], w[2])
+
+
+def test_accept_tally_errors(mk_engine):
+    e = mk_engine(5, R.MODE_MIN)
+    # out-of-window instance -> E_NIL_INSTANCE (the reference indexes past instanceSpace)
+    with pytest.raises(MpxError) as ei:
+        e.accept_tally(kat_cases.acc(9, [(1, 0, 16)]), kat_cases.inst_states(4), 0, -1)
+    assert ei.value.code == R.E_NIL_INSTANCE
+    # MIN: a NACK for a nil instance is harmless, an OK dereferences it
+    st = kat_cases.inst_states(2)
+    st[1]["status"] = R.STATUS_NIL
+    e.accept_tally(kat_cases.acc(1, [(1, 0, 16)]), st, 0, -1)
+    with pytest.raises(MpxError) as ei:
+        e.accept_tally(kat_cases.acc(1, [(1, 1, 16)]), st, 0, -1)
+    assert ei.value.code == R.E_NIL_INSTANCE
+    # CLASSIC reads status for every reply
+    c = mk_engine(5, R.MODE_CLASSIC)
+    with pytest.raises(MpxError) as ei:
+        c.accept_tally(kat_cases.acc(1, [(1, 0, 16)]), st, 0, -1)
+    assert ei.value.code == R.E_NIL_INSTANCE
+    # peer id outside peerCommits, reached only past the quorum test
+    e.accept_tally(kat_cases.acc(0, [(9, 1, 16)]), kat_cases.inst_states(1), 0, -1)
+    with pytest.raises(MpxError) as ei:
+        e.accept_tally(kat_cases.acc(0, [(1, 1, 16), (9, 1, 16)]), kat_cases.inst_states(1), 0, -1)
+    assert ei.value.code == R.E_BAD_ID
+    # records out of ascending instance order
+    rec = np.concatenate([kat_cases.acc(1, [(1, 1, 16)]), kat_cases.acc(0, [(1, 1, 16)])])
+    with pytest.raises(MpxError) as ei:
+        e.accept_tally(rec, kat_cases.inst_states(2), 0, -1)
+    assert ei.value.code == R.E_INVAL
+
+
+def test_committed_prefix(mk_engine):
+    rng = np.random.default_rng(7)
+    e, o = mk_engine(5, R.MODE_CLASSIC), Oracle(5, R.MODE_CLASSIC)
+    for trial in range(20):
+        n = int(rng.integers(1, 5000))
+        st = kat_cases.inst_states(n, R.COMMITTED)
+        if trial % 3:
+            bad = rng.integers(0, n, int(rng.integers(1, 4)))
+            st["status"][bad] = rng.choice([R.PREPARED, R.STATUS_NIL], len(bad))
+        base = int(rng.integers(-3, 3))
+        cu = int(rng.integers(base - 2, base + n // 2))
+        assert e.committed_prefix(st, base, cu) == o.committed_prefix(st, base, cu)
+
+
+# ---- A4 ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n_rep", [1, 3, 5, 9])
+def test_prepare_classic_ragged(mk_engine, n_rep):
+    rng = np.random.default_rng(2000 + n_rep)
+    for trial in range(3):
+        rec, st = gen_cases.ragged_prepare(rng, 3000, n_rep, max_r=9, long_every=611,
+                                           long_len=150 + 80 * trial, base=-trial)
+        e, o = mk_engine(n_rep, R.MODE_CLASSIC), Oracle(n_rep, R.MODE_CLASSIC)
+        db = int(rng.integers(-1, 400))
+        got = e.prepare_select(rec, st, -trial, db)
+        want = o.prepare_select(rec, st, -trial, db)
+        eq_struct(got[0], want[0])
+        assert got[1] == want[1] and np.array_equal(got[2], want[2])
+
+
+def test_prepare_classic_config3_shape(mk_engine):
+    rec, st = synth.prepare_replies(1 << 16, 5, 0.8, seed=43)
+    e, o = mk_engine(5, R.MODE_CLASSIC), Oracle(5, R.MODE_CLASSIC)
+    got = e.prepare_select(rec, st, 0, -1)
+    want = o.prepare_select(rec, st, 0, -1)
+    eq_struct(got[0], want[0])
+    assert got[1] == want[1] and np.array_equal(got[2], want[2])
+
+
+# ---- A3 ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("r", [1, 4, 9])
+def test_prepare_min(mk_engine, r):
+    rec, off, gst = synth.prepare_replies_min(5000, 5, seed=46 + r, replies_per_group=r)
+    e, o = mk_engine(5, R.MODE_MIN), Oracle(5, R.MODE_MIN)
+    pc = np.random.default_rng(r).integers(-1, 50, 5000 * 5).astype(np.int32)
+    got = e.prepare_select_min(rec, off, gst, pc)
+    want = o.prepare_select_min(rec, off, gst, pc)
+    eq_struct(got[0], want[0])
+    assert np.array_equal(got[1], want[1])
+    eq_struct(got[2], want[2])
+
+
+# ---- A5 / A6 ----------------------------------------------------------------------------------
+@pytest.mark.parametrize("dist", ["uniform", "zipf"])
+def test_apply_config4_shape(mk_engine, dist):
+    op, key, val = synth.commands(1 << 18, 1 << 12, 0.5, dist, seed=44)
+    e, o = mk_engine(5, R.MODE_MIN), Oracle(5, R.MODE_MIN)
+    for part in range(3):  # the table persists across calls
+        sl = slice(part * (1 << 16), (part + 1) * (1 << 16) + part * 999)
+        gr, gc = e.apply(op[sl], key[sl], val[sl])
+        wr, wc = o.apply(op[sl], key[sl], val[sl])
+        assert np.array_equal(gr, wr) and np.array_equal(gc, wc)
+        gk, gv = e.kv_export()
+        wk, wv = o.kv_export()
+        assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
+
+
+def test_apply_mixed_ops_and_special_keys(mk_engine):
+    rng = np.random.default_rng(5)
+    e, o = mk_engine(5, R.MODE_MIN), Oracle(5, R.MODE_MIN)
+    for trial in range(4):
+        op, key, val = gen_cases.commands_mixed(rng, 50000, 300 + 3000 * trial)
+        gr, gc = e.apply(op, key, val)
+        wr, wc = o.apply(op, key, val)
+        assert np.array_equal(gr, wr) and np.array_equal(gc, wc)
+    gk, gv = e.kv_export()
+    wk, wv = o.kv_export()
+    assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
+    # empty call, import/clear
+    e.apply(np.zeros(0, np.uint8), np.zeros(0, np.int64), np.zeros(0, np.int64))
+    e.kv_clear()
+    assert e.kv_size() == 0
+    e.kv_import(np.array([3, -7], np.int64), np.array([30, 70], np.int64))
+    r, _ = e.apply(np.array([R.OP_GET, R.OP_GET, R.OP_GET], np.uint8),
+                   np.array([3, -7, 4], np.int64), np.zeros(3, np.int64))
+    assert list(r) == [30, 70, 0]
+
+
+def test_conflict_batch(mk_engine):
+    rng = np.random.default_rng(9)
+    e, o = mk_engine(5, R.MODE_MIN), Oracle(5, R.MODE_MIN)
+    sizes = rng.integers(0, 12, 4000)
+    sizes[::500] = 700
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    op, key, _ = gen_cases.commands_mixed(rng, int(off[-1]), 2000, neg_keys=False)
+    assert np.array_equal(e.conflict_batch(op, key, off), o.conflict_batch(op, key, off))
+
+
+# ---- fused group step (config 5 shape) ----------------------------------------------------------
+def _cmp_group(got, want, G, K):
+    for f in ("committed_out", "executed_out", "peer_out", "ret", "conf_prev", "kv_cnt",
+              "decided"):
+        a, b = got[f], want[f]
+        bad = np.nonzero(a != b)[0]
+        assert len(bad) == 0, f"{f} differs at {bad[:8]}: {a[bad[:5]]} vs {b[bad[:5]]}"
+    eq_struct(got["st_out"], want["st_out"])
+    cnt = want["kv_cnt"]
+    for g in range(G):
+        n = int(cnt[g])
+        assert np.array_equal(got["kv_key"][g * K:g * K + n], want["kv_key"][g * K:g * K + n]), g
+        assert np.array_equal(got["kv_val"][g * K:g * K + n], want["kv_val"][g * K:g * K + n]), g
+
+
+@pytest.mark.parametrize("mode", [R.MODE_MIN, R.MODE_CLASSIC])
+def test_group_step_config5_shape(mk_engine, mode):
+    G, ipg, K = 96, 256, 512
+    b = synth.group_batch(G, ipg, 5, 4, 256, seed=45)
+    e, o = mk_engine(5, mode, kv_per_group=K), Oracle(5, mode, kv_per_group=K)
+    got = e.group_step(b)
+    want = o.group_step(b)
+    _cmp_group(got, want, G, K)
+    # second step from the produced tables and watermarks, new replies/commands
+    b2 = synth.group_batch(G, ipg, 5, 4, 256, seed=46)
+    b2["committed_in"] = want["committed_out"]
+    b2["executed_in"] = np.minimum(want["executed_out"], 100).astype(np.int32)
+    b2["peer_in"] = want["peer_out"]
+    got2 = e.group_step(b2, want["kv_cnt"], want["kv_key"], want["kv_val"])
+    want2 = o.group_step(b2, want["kv_cnt"], want["kv_key"], want["kv_val"])
+    _cmp_group(got2, want2, G, K)
+
+
+def test_group_step_ragged(mk_engine):
+    """variable replies per instance, nil Cmds, big groups (multi-chunk apply), skewed keys"""
+    rng = np.random.default_rng(31)
+    G, ipg, K = 40, 512, 600
+    recs, offs, sts, ops, keys, vals, coff = [], [0], [], [], [], [], [0]
+    for g in range(G):
+        rec, st = gen_cases.ragged_accept(rng, ipg, 5, max_r=6, random_state=False, p_ok=0.75)
+        rec["id"] = rng.integers(0, 5, len(rec))
+        recs.append(rec)
+        offs.append(offs[-1] + len(rec))
+        sts.append(st)
+        nc = rng.integers(0, 9, ipg)
+        m = int(nc.sum())
+        op, key, val = gen_cases.commands_mixed(rng, m, 20 if g % 3 == 0 else 700, neg_keys=True)
+        ops.append(op); keys.append(key); vals.append(val)
+        coff.extend((coff[-1] + np.cumsum(nc)).tolist())
+    b = dict(n_groups=G, ipg=ipg, recs=np.concatenate(recs),
+             grp_rec_off=np.array(offs, np.uint64), st_in=np.concatenate(sts),
+             committed_in=rng.integers(-1, 5, G).astype(np.int32),
+             executed_in=rng.integers(-1, 3, G).astype(np.int32),
+             peer_in=np.zeros(G * 5, np.int32), op=np.concatenate(ops), key=np.concatenate(keys),
+             val=np.concatenate(vals), cmd_off=np.array(coff, np.uint32),
+             has_cmds=(rng.random(G * ipg) > 0.002).astype(np.uint8))
+    for mode in (R.MODE_MIN, R.MODE_CLASSIC):
+        e, o = mk_engine(5, mode, kv_per_group=K), Oracle(5, mode, kv_per_group=K)
+        ret0 = np.full(len(b["op"]), 12345, np.int64)
+        got = e.group_step(b, ret=ret0)
+        want = o.group_step(b, ret=ret0)
+        _cmp_group(got, want, G, K)
