@@ -174,6 +174,7 @@ typedef struct mpx_config {
     uint64_t kv_capacity;   /* key capacity of the engine's KV table (mpx_apply); 0 = 1<<20 */
     uint32_t kv_per_group;  /* max live keys per group table (mpx_group_step); 0 = 512      */
     uint32_t flags;         /* reserved, 0                                                  */
+    uint64_t max_groups;    /* groups per mpx_group_step_dev call (work list); 0 = 1<<20    */
 } mpx_config;
 
 typedef struct mpx_engine mpx_engine;

@@ -7,7 +7,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmpx.so")
+# MPX_LIB selects a diagnostic build of the same engine (e.g. libmpx_stamp.so)
+LIB_PATH = os.environ.get("MPX_LIB") or os.path.join(_HERE, "libmpx.so")
 
 _p = C.c_void_p
 _i32 = C.c_int32
@@ -16,7 +17,7 @@ _sz = C.c_size_t
 
 class MpxConfig(C.Structure):
     _fields_ = [("n_replicas", C.c_int32), ("mode", C.c_int32), ("kv_capacity", C.c_uint64),
-                ("kv_per_group", C.c_uint32), ("flags", C.c_uint32)]
+                ("kv_per_group", C.c_uint32), ("flags", C.c_uint32), ("max_groups", C.c_uint64)]
 
 
 class MpxGroupBatch(C.Structure):

@@ -36,6 +36,9 @@ struct mpx_engine {
     mpx::KvTable kv{};
     bool kv_ready = false;
     DevBuf apply_work;
+    // group-step work list (groups the fast kernel hands to the general kernel) + its count
+    DevBuf worklist;
+    uint32_t* d_wcount = nullptr;
     // RCCL
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -177,10 +180,18 @@ int mpx_open(int device, const mpx_config* cfg, mpx_engine** out) {
     e->device = device;
     e->cfg = *cfg;
     if (!e->cfg.kv_per_group) e->cfg.kv_per_group = 512;
+    if (!e->cfg.max_groups) e->cfg.max_groups = 1ull << 20;
+    if (e->cfg.kv_per_group > 1024) {
+        delete e;
+        return MPX_E_UNSUPPORTED;
+    }
+    e->worklist.cap = e->cfg.max_groups * sizeof(uint32_t);
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&e->d_err, sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&e->d_red, mpx::kRedWords * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&e->d_wcount, sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&e->worklist.p, e->worklist.cap) != hipSuccess ||
         hipMemset(e->d_err, 0, sizeof(uint32_t)) != hipSuccess) {
         (void)hipGetLastError();
         mpx_close(e);
@@ -198,6 +209,8 @@ int mpx_close(mpx_engine* e) {
     for (auto& x : e->b)
         if (x.p) (void)hipFree(x.p);
     if (e->apply_work.p) (void)hipFree(e->apply_work.p);
+    if (e->worklist.p) (void)hipFree(e->worklist.p);
+    if (e->d_wcount) (void)hipFree(e->d_wcount);
     if (e->kv_ready) {
         (void)hipFree(e->kv.keys);
         (void)hipFree(e->kv.vals);
@@ -503,8 +516,12 @@ int mpx_group_step_dev(mpx_engine* e, const mpx_group_batch* b, void* stream) {
                         !b->kv_val_in || !b->kv_cnt_out || !b->kv_key_out || !b->kv_val_out))
         return fail(e, MPX_E_INVAL, "null field in mpx_group_batch");
     if (b->ipg == 0 && b->n_groups) return fail(e, MPX_E_INVAL, "ipg must be > 0");
+    if (b->ipg > 8192) return fail(e, MPX_E_UNSUPPORTED, "more than 8192 instances per group");
+    if ((uint64_t)b->n_groups * sizeof(uint32_t) > e->worklist.cap)
+        return fail(e, MPX_E_INVAL, "n_groups exceeds mpx_config.max_groups");
     HIPCHK(e, mpx::launch_group_step(e->cfg.mode, e->cfg.n_replicas, e->cfg.kv_per_group, b,
-                                     e->d_err, pick(e, stream)));
+                                     (uint32_t*)e->worklist.p, e->d_wcount, e->d_err,
+                                     pick(e, stream)));
     return MPX_OK;
 }
 
@@ -582,7 +599,10 @@ int mpx_group_step(mpx_engine* e, const mpx_group_batch* hb) {
     CK(h2d(e, d + o_kc, hb->kv_cnt_in, G * 4));
     CK(h2d(e, d + o_kk, hb->kv_key_in, G * K * 8));
     CK(h2d(e, d + o_kvv, hb->kv_val_in, G * K * 8));
-    HIPCHK(e, mpx::launch_group_step(e->cfg.mode, N, (uint32_t)K, &db, e->d_err, e->stream));
+    if (ipg > 8192) return fail(e, MPX_E_UNSUPPORTED, "more than 8192 instances per group");
+    GROW(e, e->worklist, G * sizeof(uint32_t));
+    HIPCHK(e, mpx::launch_group_step(e->cfg.mode, N, (uint32_t)K, &db, (uint32_t*)e->worklist.p,
+                                     e->d_wcount, e->d_err, e->stream));
     CK(d2h(e, hb->st_out, d + o_st, ni * 16));
     CK(d2h(e, hb->committed_out, d + o_co, G * 4));
     CK(d2h(e, hb->executed_out, d + o_eo, G * 4));

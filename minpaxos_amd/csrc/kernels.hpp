@@ -42,9 +42,11 @@ hipError_t launch_prepare_min(const mpx_prepare_reply_min* recs, uint64_t n,
 hipError_t launch_conflict_batch(const uint8_t* op, const int64_t* key, const uint64_t* inst_off,
                                  uint64_t n_inst, uint8_t* out, hipStream_t stream);
 
-// fused per-group step: tally + executeCommands against per-group compact KV tables
+// fused per-group step: tally + executeCommands against per-group compact KV tables.
+// worklist: n_groups u32 + wcount (device) for groups the fast kernel hands on.
 hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
-                             const mpx_group_batch* b, uint32_t* err, hipStream_t stream);
+                             const mpx_group_batch* b, uint32_t* worklist, uint32_t* wcount,
+                             uint32_t* err, hipStream_t stream);
 
 // ---- global KV table apply (mpx_apply) ----------------------------------------------------
 struct KvTable {

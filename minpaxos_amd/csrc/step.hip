@@ -10,44 +10,51 @@
 //      (state.go:77-103) against the group's table, plus Conflict with the previous command
 //      on the same key (state.go:53-60).
 // The group's table lives in LDS as a dictionary (key, value, present) with an LDS hash
-// index. Commands are processed in LDS-sized chunks in log order; within a chunk they are
-// bucketed by key (counting sort in LDS) and each command finds its predecessor and the last
-// PUT before it in its key's bucket. HBM traffic is one pass over replies, instance state,
-// commands, outputs and the table.
+// index. Commands are bucketed by key (counting sort in LDS) and each command finds its
+// predecessor and the last PUT before it in its key's bucket.
+//
+// Two kernels:
+//   k_group_fast     groups that fit one LDS image (<= 1024 replies, <= 256 instances,
+//                    <= 1024 commands, <= 512 dictionary keys). Every global load of the group
+//                    is issued up front (replies and instance state into LDS, commands and table
+//                    entries into registers), so a workgroup pays one memory round trip; the
+//                    reply image is reused as the dictionary after the tally. Nothing is
+//                    written until the group succeeds; a group that does not fit is appended to
+//                    a work list instead.
+//   k_group_general  the work list: chunked apply of any size, larger instance spaces.
 #include "common.hpp"
 #include "kernels.hpp"
 #include "tally.hpp"
 
 namespace mpx {
 
+// Diagnostic build only (-DMPX_STAMPS=1, tools/stamp_step.py): thread 0 of every workgroup adds
+// the s_memtime delta of each barrier-delimited phase to a global accumulator.
+#ifndef MPX_STAMPS
+#define MPX_STAMPS 0
+#endif
+#if MPX_STAMPS
+__device__ unsigned long long mpx_stamp_acc[16];
+#define STAMP_DECL                                                     \
+    unsigned long long _st_prev = 0;                                   \
+    if (threadIdx.x == 0) _st_prev = __builtin_amdgcn_s_memtime();
+#define STAMP(k)                                                       \
+    do {                                                               \
+        if (threadIdx.x == 0) {                                        \
+            unsigned long long _n = __builtin_amdgcn_s_memtime();      \
+            atomicAdd(&mpx_stamp_acc[k], _n - _st_prev);               \
+            _st_prev = _n;                                             \
+        }                                                              \
+    } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(k)
+#endif
+
 constexpr int kStepBlock = 256;
-constexpr int kDCap = 1024;          // dictionary entries (table + distinct keys of the batch)
-constexpr int kHCap = 2 * kDCap;     // LDS hash slots
-constexpr int kChunk = 1024;         // commands per LDS chunk
-constexpr int kPer = kChunk / kStepBlock;
-constexpr int kMaxIpgBits = 8192;    // decided bitmap (CLASSIC prefix) covers ipg <= 8192
 constexpr uint32_t kLock = 0xFFFFFFFFu;
 constexpr uint32_t kDead = 0xFFFFFFFEu;
 constexpr uint32_t kNoFirst = 0xFFFFFFFFu;
-
-struct StepLds {
-    int64_t dkey[kDCap];
-    int64_t dval[kDCap];
-    uint32_t dfirst[kDCap];   // first PUT (command index) of keys new to the table
-    uint32_t cnt[kDCap];      // per-chunk commands per key
-    uint32_t off[kDCap];      // exclusive scan of cnt
-    uint32_t hslot[kHCap];    // 0 empty, kid+1, kLock, kDead
-    int64_t cval[kChunk];     // chunk values
-    uint16_t list[kChunk];    // (local index << 1) | isPut, bucketed by key
-    uint8_t dpresent[kDCap];  // key present in the table (has a value)
-    uint8_t dseen[kDCap];     // bit0: seen in this call, bit1: last op on it was a PUT
-    uint32_t dec_bits[kMaxIpgBits / 32];
-    uint32_t wsum[kStepBlock / kWave];
-    unsigned long long red[1 + MPX_MAX_REPLICAS];
-    uint32_t dn;
-    uint32_t n_orig;
-    uint32_t scal[4];
-};
 
 __device__ __forceinline__ uint32_t lhash(int64_t k) {
     uint64_t x = (uint64_t)k;
@@ -57,50 +64,73 @@ __device__ __forceinline__ uint32_t lhash(int64_t k) {
     return (uint32_t)x;
 }
 
-// find-or-insert into the LDS dictionary; returns kid or -1 (full)
-__device__ int dict_insert(StepLds& S, int64_t key, bool is_new_value_unknown, uint32_t* err) {
-    uint32_t h = lhash(key) & (kHCap - 1);
-    for (int probe = 0; probe < kHCap;) {
-        uint32_t cur = __hip_atomic_load(&S.hslot[h], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+// LDS dictionary views shared by both kernels
+struct Dict {
+    int64_t* dkey;
+    int64_t* dval;
+    uint32_t* dfirst;
+    uint32_t* cnt;
+    uint32_t* hslot;
+    uint8_t* dpresent;
+    uint8_t* dseen;
+    uint32_t* dn;
+    uint32_t dcap, hcap;
+};
+
+// find-or-insert; returns kid, or -1 when the dictionary is full
+__device__ int dict_insert(const Dict& D, int64_t key) {
+    uint32_t h = lhash(key) & (D.hcap - 1);
+    for (uint32_t probe = 0; probe < D.hcap;) {
+        uint32_t cur = __hip_atomic_load(&D.hslot[h], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (cur == 0) {
-            const uint32_t old = atomicCAS(&S.hslot[h], 0u, kLock);
+            const uint32_t old = atomicCAS(&D.hslot[h], 0u, kLock);
             if (old == 0) {
-                const uint32_t kid = atomicAdd(&S.dn, 1u);
-                if (kid >= (uint32_t)kDCap) {
-                    raise_err(err, kErrKvFull);
-                    __hip_atomic_store(&S.hslot[h], kDead, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const uint32_t kid = atomicAdd(D.dn, 1u);
+                if (kid >= D.dcap) {
+                    __hip_atomic_store(&D.hslot[h], kDead, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     return -1;
                 }
-                S.dkey[kid] = key;
-                S.dval[kid] = 0;
-                S.dpresent[kid] = 0;
-                S.dseen[kid] = 0;
-                S.dfirst[kid] = kNoFirst;
-                S.cnt[kid] = 0;
-                __hip_atomic_store(&S.hslot[h], kid + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                D.dkey[kid] = key;
+                D.dval[kid] = 0;
+                D.dpresent[kid] = 0;
+                D.dseen[kid] = 0;
+                D.dfirst[kid] = kNoFirst;
+                D.cnt[kid] = 0;
+                __hip_atomic_store(&D.hslot[h], kid + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 return (int)kid;
             }
             cur = old;
         }
         if (cur == kLock) continue;  // being published by another lane: re-read this slot
-        if (cur != kDead && S.dkey[cur - 1] == key) return (int)(cur - 1);
-        h = (h + 1) & (kHCap - 1);
+        if (cur != kDead && D.dkey[cur - 1] == key) return (int)(cur - 1);
+        h = (h + 1) & (D.hcap - 1);
         ++probe;
     }
-    raise_err(err, kErrKvFull);
     return -1;
 }
 
-// exclusive scan of S.cnt[0..n) into S.off (n <= kDCap), whole block
-__device__ __forceinline__ void block_scan_cnt(StepLds& S, uint32_t n) {
+// insert a key known to be absent (table load): no lock needed, keys are unique
+__device__ __forceinline__ void dict_put_unique(const Dict& D, uint32_t e, int64_t k, int64_t v) {
+    D.dkey[e] = k;
+    D.dval[e] = v;
+    D.dpresent[e] = 1;
+    D.dseen[e] = 0;
+    D.dfirst[e] = kNoFirst;
+    uint32_t h = lhash(k) & (D.hcap - 1);
+    while (atomicCAS(&D.hslot[h], 0u, e + 1) != 0u) h = (h + 1) & (D.hcap - 1);
+}
+
+// exclusive scan of cnt[0..n) into off (n <= PER*256), whole block
+template <int PER, typename OffT>
+__device__ __forceinline__ void block_scan(const uint32_t* cnt, OffT* off, uint32_t n,
+                                           uint32_t* wsum) {
     const int t = threadIdx.x, l = lane_id(), w = t / kWave;
-    constexpr int per = kDCap / kStepBlock;  // 4 contiguous entries per thread
-    uint32_t v[per];
+    uint32_t v[PER];
     uint32_t sum = 0;
 #pragma unroll
-    for (int k = 0; k < per; ++k) {
-        const uint32_t i = t * per + k;
-        v[k] = i < n ? S.cnt[i] : 0;
+    for (int k = 0; k < PER; ++k) {
+        const uint32_t i = t * PER + k;
+        v[k] = i < n ? cnt[i] : 0;
         sum += v[k];
     }
     uint32_t incl = sum;
@@ -109,44 +139,515 @@ __device__ __forceinline__ void block_scan_cnt(StepLds& S, uint32_t n) {
         const uint32_t x = __shfl_up(incl, d);
         if (l >= d) incl += x;
     }
-    if (l == kWave - 1) S.wsum[w] = incl;
+    if (l == kWave - 1) wsum[w] = incl;
     __syncthreads();
     uint32_t wbase = 0;
-    for (int k = 0; k < w; ++k) wbase += S.wsum[k];
+    for (int k = 0; k < w; ++k) wbase += wsum[k];
     uint32_t run = wbase + incl - sum;
 #pragma unroll
-    for (int k = 0; k < per; ++k) {
-        const uint32_t i = t * per + k;
-        if (i < (uint32_t)kDCap) S.off[i] = run;
+    for (int k = 0; k < PER; ++k) {
+        const uint32_t i = t * PER + k;
+        if (i < n) off[i] = (OffT)run;
         run += v[k];
     }
     __syncthreads();
 }
 
+// resolve one command against its key's bucket; returns flags bit0 last-of-key, bit1 last PUT,
+// bit2 first PUT (all within the bucket = this chunk)
+template <typename OffT>
+__device__ __forceinline__ uint8_t resolve_cmd(const Dict& D, const OffT* off,
+                                               const uint16_t* list, const int64_t* cval, int kd,
+                                               uint32_t li, uint8_t o, int64_t& r, bool& conf) {
+    const bool isput = o == MPX_OP_PUT;
+    int prev = -1, prevput = 0, lastput = -1;
+    bool later = false, laterput = false;
+    const uint32_t a = off[kd], z = a + D.cnt[kd];
+    for (uint32_t j = a; j < z; ++j) {
+        const uint32_t ent = list[j];
+        const int lj = (int)(ent >> 1);
+        const uint32_t pj = ent & 1u;
+        if (lj < (int)li) {
+            if (lj > prev) { prev = lj; prevput = (int)pj; }
+            if (pj && lj > lastput) lastput = lj;
+        } else if (lj > (int)li) {
+            later = true;
+            laterput |= pj != 0;
+        }
+    }
+    const uint8_t seen = D.dseen[kd];
+    if (prev >= 0) conf = prevput || isput;
+    else conf = (seen & 1u) && ((seen & 2u) || isput);
+    r = 0;
+    if (isput) r = cval[li];
+    else if (o == MPX_OP_GET) {
+        if (lastput >= 0) r = cval[lastput];
+        else if (D.dpresent[kd]) r = D.dval[kd];
+    }
+    uint8_t fl = 0;
+    if (!later) fl |= 1;
+    if (isput && !laterput) fl |= 2;
+    if (isput && lastput < 0) fl |= 4;
+    return fl;
+}
+
+__device__ __forceinline__ void apply_update(const Dict& D, int kd, uint8_t fl, uint8_t o,
+                                             int64_t v, uint32_t first_pos, uint32_t n_orig) {
+    if (fl & 1) D.dseen[kd] = (uint8_t)(1u | (o == MPX_OP_PUT ? 2u : 0u));
+    if (fl & 2) {
+        D.dval[kd] = v;
+        D.dpresent[kd] = 1;
+    }
+    if ((fl & 4) && (uint32_t)kd >= n_orig && D.dfirst[kd] == kNoFirst) D.dfirst[kd] = first_pos;
+}
+
+// write the dictionary back as the group's compact table: original entries in place, new
+// present keys appended in order of their first PUT. Returns nothing; sets *total (LDS).
+__device__ __forceinline__ void table_writeback(const Dict& D, uint32_t norig, uint32_t dn,
+                                                int64_t* kk, int64_t* kv, uint32_t kvpg,
+                                                uint32_t* total, uint32_t* err) {
+    const int t = threadIdx.x;
+    for (uint32_t e = t; e < norig; e += kStepBlock) {
+        kk[e] = D.dkey[e];
+        kv[e] = D.dval[e];
+    }
+    if (t == 0) *total = norig;
+    __syncthreads();
+    for (uint32_t e = norig + t; e < dn; e += kStepBlock) {
+        if (!D.dpresent[e]) continue;
+        const uint32_t f = D.dfirst[e];
+        uint32_t rank = 0;
+        for (uint32_t x = norig; x < dn; ++x)
+            if (D.dpresent[x] && D.dfirst[x] < f) ++rank;
+        atomicAdd(total, 1u);
+        const uint32_t dst = norig + rank;
+        if (dst < kvpg) {
+            kk[dst] = D.dkey[e];
+            kv[dst] = D.dval[e];
+        }
+    }
+    __syncthreads();
+    if (t == 0 && *total > kvpg) raise_err(err, kErrKvFull);
+}
+
+// ======================================== fast path ===========================================
+// Per workgroup = per group, three transpositions of the sequential reference loops:
+//   tally    one lane per INSTANCE walks that instance's replies in arrival order (the handler's
+//            own loop); replies of different instances are independent, and the only
+//            cross-instance outputs (committedUpTo, peerCommits: last assignment in array order)
+//            are max-reductions over (position+1)<<32 | value keys
+//   bucket   executed commands are counting-sorted by key into LDS buckets
+//   resolve  one lane per KEY sorts its bucket into log order (<= kFBucket entries) and walks it:
+//            Execute's return values, Conflict with the predecessor, and the key's final value
+// Nothing reaches global memory before the group is known to fit; otherwise the group is handed
+// to k_group_general through the work list.
+constexpr int kFRecs = 1024, kFIpg = 256, kFCmds = 1024, kFD = 256, kFH = 512, kFBucket = 32;
+constexpr int kFPer = kFCmds / kStepBlock;   // commands per thread
+constexpr int kFRecPer = kFRecs / kStepBlock;
+constexpr uint16_t kNoRange = 0xFFFF;
+
+struct FastLds {
+    union {
+        struct {                 // phase A: the group's replies + per-instance reply ranges
+            int4 recs[kFRecs];
+            uint16_t rstart[kFIpg];
+            uint16_t rend[kFIpg];
+        } a;
+        struct {                 // phase B: dictionary, buckets, command values / results
+            int64_t cval[kFCmds];    // value of each command, replaced in place by its ret
+            int64_t dkey[kFD];
+            int64_t dval[kFD];
+            uint32_t hslot[kFH];
+            uint32_t cnt[kFD];
+            uint32_t dfirst[kFD];
+            uint16_t off[kFD];
+            uint16_t list[kFCmds];   // (li << 3) | op
+            uint8_t cconf[kFCmds];
+            uint8_t dpresent[kFD];
+            uint8_t dseen[kFD];
+        } b;
+    } u;
+    int4 sst[kFIpg];          // instance states, tallied in place
+    uint32_t coff[kFIpg + 1];
+    uint8_t has[kFIpg];
+    uint32_t dec_bits[kFIpg / 32];
+    uint32_t touch_bits[kFIpg / 32];
+    unsigned long long red[1 + MPX_MAX_REPLICAS];
+    uint32_t wsum[kStepBlock / kWave];
+    uint32_t dn, scal[4];
+};
+
 template <int MODE>
-__global__ __launch_bounds__(kStepBlock) void k_group_step(mpx_group_batch b, int32_t nrep,
-                                                           uint32_t kvpg, uint32_t* err) {
-    __shared__ StepLds S;
+__device__ __forceinline__ void fast_tally_instance(FastLds& S, uint32_t inst, int32_t half,
+                                                    int32_t nrep, uint32_t* err) {
+    const uint32_t a = S.u.a.rstart[inst];
+    if (a == kNoRange) return;
+    const uint32_t z = S.u.a.rend[inst];
+    int4 st = S.sst[inst];
+    bool dec = false;
+    if (MODE == MPX_MODE_MIN) {
+        // bareminpaxos.go:1023-1053
+        unsigned long long cross = 0;
+        for (uint32_t p = a; p < z; ++p) {
+            const int4 r = S.u.a.recs[p];
+            if ((r.w & 0xff) != 1) continue;                 // OK != TRUE: ignored
+            if (st.x == MPX_STATUS_NIL) {
+                raise_err(err, kErrNil);
+                break;
+            }
+            st.y += 1;                                       // AcceptOKs++
+            if (st.y + 1 > half) {
+                if (st.y == half) {
+                    st.x = MPX_COMMITTED;
+                    dec = true;
+                    cross = ((unsigned long long)(p + 1) << 32) | (uint32_t)inst;
+                }
+                if (r.z < 0 || r.z >= nrep) raise_err(err, kErrBadId);
+                else atomicMax(&S.red[1 + r.z], ((unsigned long long)(p + 1) << 32) |
+                                                    (uint32_t)(inst - 1));
+            }
+        }
+        if (cross) atomicMax(&S.red[0], cross);
+    } else {
+        // paxos.go:634-673
+        if (st.x == MPX_STATUS_NIL) {
+            raise_err(err, kErrNil);
+            return;
+        }
+        for (uint32_t p = a; p < z; ++p) {
+            if (st.x != MPX_PREPARED && st.x != MPX_ACCEPTED) break;
+            const int4 r = S.u.a.recs[p];
+            if ((r.w & 0xff) == 1) {
+                st.y += 1;
+                if (st.y + 1 > half) {
+                    st.x = MPX_COMMITTED;
+                    dec = true;
+                }
+            } else {
+                st.z += 1;
+                if (r.y > st.w) st.w = r.y;
+            }
+        }
+        if (dec) atomicMax(&S.red[0], 1ull);
+    }
+    S.sst[inst] = st;
+    atomicOr(&S.touch_bits[inst >> 5], 1u << (inst & 31));
+    if (dec) atomicOr(&S.dec_bits[inst >> 5], 1u << (inst & 31));
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, int32_t nrep,
+                                                           uint32_t kvpg, uint32_t* worklist,
+                                                           uint32_t* wcount, uint32_t* err) {
+    __shared__ FastLds S;
+    STAMP_DECL
     const uint32_t g = blockIdx.x;
+    const int t = threadIdx.x;
+    const int32_t half = nrep >> 1;
+    const uint32_t ipg = b.ipg;
+    const uint64_t gi0 = (uint64_t)g * ipg;
+    const uint64_t r0 = b.grp_rec_off[g], r1 = b.grp_rec_off[g + 1];
+    const uint32_t c_lo = b.cmd_off[gi0], c_hi = b.cmd_off[gi0 + ipg];
+    const uint32_t kcnt = b.kv_cnt_in[g];
+    const uint64_t nrec = r1 - r0;
+    const uint32_t ncmd = c_hi - c_lo;
+    if (r1 < r0 || c_hi < c_lo || nrec > (uint64_t)kFRecs || ncmd > (uint32_t)kFCmds ||
+        kcnt > (uint32_t)kFD || kcnt > kvpg) {
+        if (t == 0) worklist[atomicAdd(wcount, 1u)] = g;
+        return;
+    }
+    // ---- one round of loads: every load is issued before any is consumed (indices are clamped
+    // instead of guarded, so no exec-mask branch splits the batch and forces vmcnt(0) waits)
+    int4 rr[kFRecPer];
+    if (nrec) {
+        const uint32_t last = (uint32_t)nrec - 1;
+#pragma unroll
+        for (int k = 0; k < kFRecPer; ++k) {
+            const uint32_t p = t + k * kStepBlock;
+            rr[k] = load_rec(b.recs, r0 + (p < last ? p : last));
+        }
+    }
+    const uint32_t ti = (uint32_t)t < ipg ? (uint32_t)t : ipg - 1;
+    const int4 sv = reinterpret_cast<const int4*>(b.st_in)[gi0 + ti];
+    const uint32_t co = b.cmd_off[gi0 + ti];
+    uint8_t hs = 1;
+    if (b.has_cmds) hs = b.has_cmds[gi0 + ti];
+    uint8_t o[kFPer];
+    int64_t ck[kFPer], cv[kFPer];
+    if (ncmd) {
+        const uint32_t last = ncmd - 1;
+#pragma unroll
+        for (int k = 0; k < kFPer; ++k) {
+            const uint32_t li = t + k * kStepBlock;
+            const uint64_t ci = c_lo + (li < last ? li : last);
+            o[k] = b.op[ci];
+            ck[k] = b.key[ci];
+            cv[k] = b.val[ci];
+        }
+    }
+    int64_t tk = 0, tv = 0;
+    if (kcnt) {
+        const uint64_t ei = (uint64_t)g * kvpg + ((uint32_t)t < kcnt ? (uint32_t)t : kcnt - 1);
+        tk = b.kv_key_in[ei];
+        tv = b.kv_val_in[ei];
+    }
+    if (t < kFIpg) S.u.a.rstart[t] = kNoRange;
+    if (t <= MPX_MAX_REPLICAS) S.red[t] = 0;
+    if (t < kFIpg / 32) {
+        S.dec_bits[t] = 0;
+        S.touch_bits[t] = 0;
+    }
+    if (nrec) {
+#pragma unroll
+        for (int k = 0; k < kFRecPer; ++k) {
+            const uint32_t p = t + k * kStepBlock;
+            if (p < nrec) S.u.a.recs[p] = rr[k];
+        }
+    }
+    if ((uint32_t)t < ipg) {
+        S.sst[t] = sv;
+        S.coff[t] = co - c_lo;
+        S.has[t] = hs;
+    }
+    if (t == 0) S.coff[ipg] = ncmd;
+    __syncthreads();
+    STAMP(0);
+
+    // ---- 1. tally: reply ranges from head flags, then one lane per instance -------------------
+#pragma unroll
+    for (int k = 0; k < kFRecPer; ++k) {
+        const uint32_t p = t * kFRecPer + k;
+        if (p < nrec) {
+            const int32_t inst = S.u.a.recs[p].x;
+            const int32_t prev = p ? S.u.a.recs[p - 1].x : 0;
+            const bool inwin = inst >= 0 && (uint32_t)inst < ipg;
+            if (!inwin) raise_err(err, kErrNil);  // names an instance outside instanceSpace
+            if (p == 0 || inst != prev) {
+                if (p && inst < prev) raise_err(err, kErrOrder);
+                if (inwin) S.u.a.rstart[inst] = (uint16_t)p;
+                if (p && prev >= 0 && (uint32_t)prev < ipg) S.u.a.rend[prev] = (uint16_t)p;
+            }
+            if (p + 1 == nrec && inwin) S.u.a.rend[inst] = (uint16_t)nrec;
+        }
+    }
+    __syncthreads();
+    if ((uint32_t)t < ipg) fast_tally_instance<MODE>(S, (uint32_t)t, half, nrep, err);
+    __syncthreads();
+    STAMP(1);
+
+    // ---- watermarks -------------------------------------------------------------------------------
+    const int32_t cu_in = b.committed_in[g];
+    int32_t cu = cu_in;
+    if (MODE == MPX_MODE_MIN) {
+        if (S.red[0]) cu = (int32_t)(uint32_t)(S.red[0] & 0xffffffffull);
+    } else if (S.red[0]) {
+        // updateCommittedUpTo over the final statuses (tallied in place)
+        if (t == 0) S.scal[1] = ipg;
+        __syncthreads();
+        const int64_t j0 = (int64_t)cu_in + 1;
+        if (j0 >= 0 && (uint64_t)j0 < ipg)
+            for (uint32_t j = (uint32_t)j0 + t; j < ipg; j += kStepBlock)
+                if (S.sst[j].x != MPX_COMMITTED) {
+                    atomicMin(&S.scal[1], j);
+                    break;
+                }
+        __syncthreads();
+        if (j0 >= 0 && (uint64_t)j0 < ipg) cu = (int32_t)S.scal[1] - 1;
+    }
+    // executeCommands range: instances lo .. stop-1
+    const int32_t ex_in = b.executed_in[g];
+    int64_t lo = (int64_t)ex_in + 1, hi = (int64_t)cu;
+    if (hi >= (int64_t)ipg) hi = (int64_t)ipg - 1;
+    if (lo < 0) lo = 0;
+    if (t == 0) {
+        S.scal[2] = (uint32_t)(hi + 1 > lo ? hi + 1 : lo);
+        S.dn = kcnt;
+        S.scal[3] = 0;
+    }
+    // the reply image is dead from here: build the dictionary over it
+    for (int i = t; i < kFH; i += kStepBlock) S.u.b.hslot[i] = 0;
+    if (t < kFD) S.u.b.cnt[t] = 0;
+    __syncthreads();
+    if (hi >= lo)
+        for (int64_t i = lo + t; i <= hi; i += kStepBlock)
+            if (S.sst[i].x == MPX_STATUS_NIL || !S.has[i]) {
+                atomicMin(&S.scal[2], (uint32_t)i);
+                break;
+            }
+    const Dict D{S.u.b.dkey, S.u.b.dval, S.u.b.dfirst, S.u.b.cnt, S.u.b.hslot, S.u.b.dpresent,
+                 S.u.b.dseen, &S.dn, (uint32_t)kFD, (uint32_t)kFH};
+    if ((uint32_t)t < kcnt) dict_put_unique(D, (uint32_t)t, tk, tv);
+    __syncthreads();
+    STAMP(2);
+    const int64_t stop = hi >= lo ? (int64_t)S.scal[2] : lo;
+    const uint32_t x0 = stop > lo ? S.coff[lo] : 0, x1 = stop > lo ? S.coff[stop] : 0;
+
+    // ---- 2. bucket the executed commands by key ---------------------------------------------------
+    int kid[kFPer];
+    uint32_t pos[kFPer];
+#pragma unroll
+    for (int k = 0; k < kFPer; ++k) {
+        const uint32_t li = t + k * kStepBlock;
+        kid[k] = -1;
+        if (li >= x0 && li < x1) {
+            S.u.b.cval[li] = cv[k];
+            kid[k] = dict_insert(D, ck[k]);
+            if (kid[k] >= 0) pos[k] = atomicAdd(&S.u.b.cnt[kid[k]], 1u);
+            else S.scal[3] = 1;  // dictionary overflow: hand the group to the general kernel
+        }
+    }
+    __syncthreads();
+    STAMP(3);
+    if (S.scal[3]) {
+        if (t == 0) worklist[atomicAdd(wcount, 1u)] = g;
+        return;
+    }
+    const uint32_t dn = S.dn;
+    block_scan<1>(S.u.b.cnt, S.u.b.off, dn, S.wsum);
+#pragma unroll
+    for (int k = 0; k < kFPer; ++k) {
+        const uint32_t li = t + k * kStepBlock;
+        // 3-bit op code; any op outside the enum is a no-op for Execute, as NONE (code 6)
+        if (kid[k] >= 0)
+            S.u.b.list[S.u.b.off[kid[k]] + pos[k]] =
+                (uint16_t)((li << 3) | (o[k] <= MPX_OP_WLOCK ? o[k] : 6u));
+    }
+    __syncthreads();
+    STAMP(4);
+
+    // ---- 3. resolve: one lane per key walks its bucket in log order --------------------------------
+    if ((uint32_t)t < dn) {
+        const uint32_t kd = (uint32_t)t;
+        const uint32_t n = S.u.b.cnt[kd];
+        if (n > (uint32_t)kFBucket) {
+            S.scal[3] = 1;  // long bucket: the general kernel's per-command scan handles it
+        } else if (n) {
+            uint16_t* L = S.u.b.list + S.u.b.off[kd];
+            // insertion sort by log position (entries sort by li, the high bits)
+            for (uint32_t i = 1; i < n; ++i) {
+                const uint16_t x = L[i];
+                uint32_t j = i;
+                while (j > 0 && L[j - 1] > x) {
+                    L[j] = L[j - 1];
+                    --j;
+                }
+                L[j] = x;
+            }
+            const uint8_t seen = S.u.b.dseen[kd];
+            bool have = S.u.b.dpresent[kd];
+            int64_t cur = S.u.b.dval[kd];
+            bool exists = seen & 1u, prevput = (seen & 2u) != 0;
+            uint32_t first_put = kNoFirst;
+            uint8_t lastop = 0;
+            for (uint32_t j = 0; j < n; ++j) {
+                const uint32_t e = L[j];
+                const uint32_t li = e >> 3;
+                const uint8_t op = (uint8_t)(e & 7u);
+                const bool put = op == MPX_OP_PUT;
+                S.u.b.cconf[li] = exists && (prevput || put);  // state.Conflict(prev, this)
+                int64_t r = 0;
+                if (put) {
+                    r = S.u.b.cval[li];
+                    cur = r;
+                    have = true;
+                    if (first_put == kNoFirst) first_put = li - x0;
+                } else if (op == MPX_OP_GET) {
+                    r = have ? cur : 0;
+                }
+                S.u.b.cval[li] = r;  // Execute's return value, in place of the command's value
+                exists = true;
+                prevput = put;
+                lastop = op;
+            }
+            S.u.b.dseen[kd] = (uint8_t)(1u | (lastop == MPX_OP_PUT ? 2u : 0u));
+            if (have) {
+                S.u.b.dval[kd] = cur;
+                S.u.b.dpresent[kd] = 1;
+            }
+            if (kd >= kcnt && first_put != kNoFirst && S.u.b.dfirst[kd] == kNoFirst)
+                S.u.b.dfirst[kd] = first_put;
+        }
+    }
+    __syncthreads();
+    STAMP(5);
+    if (S.scal[3]) {
+        if (t == 0) worklist[atomicAdd(wcount, 1u)] = g;
+        return;
+    }
+    // ret / conf_prev for the executed commands, coalesced
+#pragma unroll
+    for (int k = 0; k < kFPer; ++k) {
+        const uint32_t li = t + k * kStepBlock;
+        if (li >= x0 && li < x1) {
+            b.ret[c_lo + li] = S.u.b.cval[li];
+            if (b.conf_prev) b.conf_prev[c_lo + li] = S.u.b.cconf[li];
+        }
+    }
+    STAMP(6);
+
+    // ---- 4. outputs ------------------------------------------------------------------------------
+    table_writeback(D, kcnt, dn, b.kv_key_out + (uint64_t)g * kvpg, b.kv_val_out + (uint64_t)g * kvpg,
+                    kvpg, &S.scal[0], err);
+    if ((uint32_t)t < ipg) {
+        if ((S.touch_bits[t >> 5] >> (t & 31)) & 1u)
+            reinterpret_cast<int4*>(b.st_out)[gi0 + t] = S.sst[t];
+        if (b.decided) b.decided[gi0 + t] = (S.dec_bits[t >> 5] >> (t & 31)) & 1u;
+    }
+    if (t < nrep) {
+        const unsigned long long k = MODE == MPX_MODE_MIN ? S.red[1 + t] : 0ull;
+        b.peer_out[(uint64_t)g * nrep + t] =
+            k ? (int32_t)(uint32_t)(k & 0xffffffffull) : b.peer_in[(uint64_t)g * nrep + t];
+    }
+    if (t == 0) {
+        b.committed_out[g] = cu;
+        b.executed_out[g] = stop > lo ? (int32_t)(stop - 1) : ex_in;
+        const uint32_t total = S.scal[0];
+        b.kv_cnt_out[g] = total < kvpg ? total : kvpg;
+    }
+    STAMP(7);
+}
+
+// ======================================= general path =========================================
+constexpr int kDCap = 1024;
+constexpr int kHCap = 2 * kDCap;
+constexpr int kChunk = 1024;
+constexpr int kPer = kChunk / kStepBlock;
+constexpr int kMaxIpgBits = 8192;
+
+struct GenLds {
+    int64_t dkey[kDCap];
+    int64_t dval[kDCap];
+    uint32_t dfirst[kDCap];
+    uint32_t cnt[kDCap];
+    uint32_t off[kDCap];
+    uint32_t hslot[kHCap];
+    int64_t cval[kChunk];
+    uint16_t list[kChunk];
+    uint8_t dpresent[kDCap];
+    uint8_t dseen[kDCap];
+    uint32_t dec_bits[kMaxIpgBits / 32];
+    uint32_t wsum[kStepBlock / kWave];
+    unsigned long long red[1 + MPX_MAX_REPLICAS];
+    uint32_t dn, n_orig, scal[4];
+};
+
+template <int MODE>
+__device__ void group_general(GenLds& S, const mpx_group_batch& b, uint32_t g, int32_t nrep,
+                             uint32_t kvpg, uint32_t* err) {
     const int t = threadIdx.x, l = lane_id(), w = t / kWave;
     const int32_t half = nrep >> 1;
     const uint64_t ipg = b.ipg;
     const uint64_t gi0 = (uint64_t)g * ipg;
     const mpx_inst_state* st_in = b.st_in + gi0;
     mpx_inst_state* st_out = b.st_out + gi0;
-    const bool use_bits = MODE == MPX_MODE_CLASSIC;
 
     if (t <= MPX_MAX_REPLICAS) S.red[t] = 0;
-    if (use_bits)
-        for (int i = t; i < kMaxIpgBits / 32; i += kStepBlock) S.dec_bits[i] = 0;
+    for (int i = t; i < kMaxIpgBits / 32; i += kStepBlock) S.dec_bits[i] = 0;
     for (int i = t; i < kHCap; i += kStepBlock) S.hslot[i] = 0;
-    if (t == 0) {
-        S.dn = 0;
-        S.scal[0] = 0;
-    }
+    if (t == 0) S.dn = 0;
     __syncthreads();
 
-    // ---- 1. tally: 4 waves, each on an instance-aligned quarter of the group's replies ----
+    // ---- 1. tally straight from global memory ------------------------------------------------------
     const uint64_t r0 = b.grp_rec_off[g], r1 = b.grp_rec_off[g + 1];
     if (r1 > r0) {
         const uint64_t len = r1 - r0;
@@ -156,9 +657,8 @@ __global__ __launch_bounds__(kStepBlock) void k_group_step(mpx_group_batch b, in
         const uint64_t e = (n1 >= r1) ? r1 : find_head(b.recs, n1, r0, r1);
         if (s < e) {
             TallyOut out{0, 0, false};
-            tally_range<MODE>(b.recs, s, e, st_in, st_out, ipg, 0, half, nrep,
-                              b.decided ? b.decided + gi0 : nullptr, err, 0, out,
-                              use_bits ? S.dec_bits : nullptr);
+            tally_range<MODE>(b.recs, s, e, st_in, st_out, ipg, 0, half, nrep, nullptr, err, 0,
+                              out, S.dec_bits);
             if (MODE == MPX_MODE_MIN) {
                 if (l == 0 && out.cu_key) atomicMax(&S.red[0], (unsigned long long)out.cu_key);
                 if (l < nrep && out.pc_key) atomicMax(&S.red[1 + l], (unsigned long long)out.pc_key);
@@ -166,13 +666,15 @@ __global__ __launch_bounds__(kStepBlock) void k_group_step(mpx_group_batch b, in
                 if (l == 0 && out.any_dec) atomicMax(&S.red[0], 1ull);
             }
         }
+    } else if (r1 < r0) {
+        raise_err(err, kErrInval);
     }
-    // decided flags of instances without replies
-    if (b.decided && r1 == r0)
-        for (uint64_t i = t; i < ipg; i += kStepBlock) b.decided[gi0 + i] = 0;
     __syncthreads();
+    if (b.decided)
+        for (uint64_t i = t; i < ipg; i += kStepBlock)
+            b.decided[gi0 + i] = (S.dec_bits[i >> 5] >> (i & 31)) & 1u;
 
-    // ---- watermarks ----------------------------------------------------------------------
+    // ---- watermarks --------------------------------------------------------------------------------
     const int32_t cu_in = b.committed_in[g];
     int32_t cu = cu_in;
     if (MODE == MPX_MODE_MIN) {
@@ -185,15 +687,13 @@ __global__ __launch_bounds__(kStepBlock) void k_group_step(mpx_group_batch b, in
     } else {
         if (t < nrep) b.peer_out[(uint64_t)g * nrep + t] = b.peer_in[(uint64_t)g * nrep + t];
         if (S.red[0]) {
-            // updateCommittedUpTo: first instance >= cu_in+1 neither COMMITTED nor decided now
             if (t == 0) S.scal[1] = (uint32_t)ipg;
             __syncthreads();
             const int64_t j0 = (int64_t)cu_in + 1;
             if (j0 >= 0 && (uint64_t)j0 < ipg) {
                 for (uint64_t j = (uint64_t)j0 + t; j < ipg; j += kStepBlock) {
-                    const bool dec = j < (uint64_t)kMaxIpgBits && ((S.dec_bits[j >> 5] >> (j & 31)) & 1u);
-                    const bool c = dec || st_in[j].status == MPX_COMMITTED;
-                    if (!c) {
+                    const bool dec = (S.dec_bits[j >> 5] >> (j & 31)) & 1u;
+                    if (!(dec || st_in[j].status == MPX_COMMITTED)) {
                         atomicMin(&S.scal[1], (uint32_t)j);
                         break;
                     }
@@ -205,18 +705,17 @@ __global__ __launch_bounds__(kStepBlock) void k_group_step(mpx_group_batch b, in
     }
     if (t == 0) b.committed_out[g] = cu;
 
-    // ---- 2. executeCommands: instances exec+1 .. cu while Cmds != nil -------------------------
+    // ---- 2. executeCommands: instances exec+1 .. cu while Cmds != nil ------------------------------
     const int32_t ex_in = b.executed_in[g];
     int64_t lo = (int64_t)ex_in + 1;
-    int64_t hi = (int64_t)cu;  // inclusive
+    int64_t hi = (int64_t)cu;
     if (hi >= (int64_t)ipg) hi = (int64_t)ipg - 1;
-    if (lo < 0) lo = 0;  // (executed_in < -1 is treated as -1)
+    if (lo < 0) lo = 0;
     if (t == 0) S.scal[2] = (uint32_t)(hi + 1 > lo ? hi + 1 : lo);
     __syncthreads();
     if (hi >= lo) {
         for (int64_t i = lo + t; i <= hi; i += kStepBlock) {
-            const bool nil = st_in[i].status == MPX_STATUS_NIL ||
-                             (b.has_cmds && !b.has_cmds[gi0 + i]);
+            const bool nil = st_in[i].status == MPX_STATUS_NIL || (b.has_cmds && !b.has_cmds[gi0 + i]);
             if (nil) {
                 atomicMin(&S.scal[2], (uint32_t)i);
                 break;
@@ -224,26 +723,18 @@ __global__ __launch_bounds__(kStepBlock) void k_group_step(mpx_group_batch b, in
         }
     }
     __syncthreads();
-    const int64_t stop = hi >= lo ? (int64_t)S.scal[2] : lo;  // first instance not executed
+    const int64_t stop = hi >= lo ? (int64_t)S.scal[2] : lo;
     if (t == 0) b.executed_out[g] = stop > lo ? (int32_t)(stop - 1) : ex_in;
 
-    // load the group's table into the dictionary
+    const Dict D{S.dkey, S.dval, S.dfirst, S.cnt, S.hslot, S.dpresent, S.dseen, &S.dn,
+                 (uint32_t)kDCap, (uint32_t)kHCap};
     const uint32_t ncnt = b.kv_cnt_in[g];
-    if (ncnt > kvpg) {
+    if (ncnt > kvpg || ncnt > (uint32_t)kDCap) {
         raise_err(err, kErrInval);
         return;
     }
-    for (uint32_t e = t; e < ncnt; e += kStepBlock) {
-        const int64_t k = b.kv_key_in[(uint64_t)g * kvpg + e];
-        const int64_t v = b.kv_val_in[(uint64_t)g * kvpg + e];
-        S.dkey[e] = k;
-        S.dval[e] = v;
-        S.dpresent[e] = 1;
-        S.dseen[e] = 0;
-        S.dfirst[e] = kNoFirst;
-        uint32_t h = lhash(k) & (kHCap - 1);
-        while (atomicCAS(&S.hslot[h], 0u, e + 1) != 0u) h = (h + 1) & (kHCap - 1);
-    }
+    for (uint32_t e = t; e < ncnt; e += kStepBlock)
+        dict_put_unique(D, e, b.kv_key_in[(uint64_t)g * kvpg + e], b.kv_val_in[(uint64_t)g * kvpg + e]);
     if (t == 0) {
         S.dn = ncnt;
         S.n_orig = ncnt;
@@ -266,15 +757,15 @@ __global__ __launch_bounds__(kStepBlock) void k_group_step(mpx_group_batch b, in
                 o[k] = 0;
                 if (li < n) {
                     o[k] = b.op[c0 + li];
-                    const int64_t key = b.key[c0 + li];
                     S.cval[li] = b.val[c0 + li];
-                    kid[k] = dict_insert(S, key, true, err);
+                    kid[k] = dict_insert(D, b.key[c0 + li]);
                     if (kid[k] >= 0) pos[k] = atomicAdd(&S.cnt[kid[k]], 1u);
+                    else raise_err(err, kErrKvFull);
                 }
             }
             __syncthreads();
             const uint32_t dn = S.dn < (uint32_t)kDCap ? S.dn : (uint32_t)kDCap;
-            block_scan_cnt(S, dn);
+            block_scan<kDCap / kStepBlock>(S.cnt, S.off, dn, S.wsum);
 #pragma unroll
             for (int k = 0; k < kPer; ++k) {
                 const uint32_t li = t + k * kStepBlock;
@@ -282,105 +773,94 @@ __global__ __launch_bounds__(kStepBlock) void k_group_step(mpx_group_batch b, in
                     S.list[S.off[kid[k]] + pos[k]] = (uint16_t)((li << 1) | (o[k] == MPX_OP_PUT ? 1u : 0u));
             }
             __syncthreads();
-            // resolve every command against its key's bucket
-            uint8_t fl[kPer];  // bit0 last of key in chunk, bit1 last PUT, bit2 first PUT
+            uint8_t fl[kPer];
 #pragma unroll
             for (int k = 0; k < kPer; ++k) {
                 const uint32_t li = t + k * kStepBlock;
                 fl[k] = 0;
                 if (li >= n || kid[k] < 0) continue;
-                const int kd = kid[k];
-                const bool isput = o[k] == MPX_OP_PUT;
-                int prev = -1, prevput = 0, lastput = -1;
-                bool later = false, laterput = false;
-                const uint32_t a = S.off[kd], z = a + S.cnt[kd];
-                for (uint32_t j = a; j < z; ++j) {
-                    const uint32_t ent = S.list[j];
-                    const int lj = (int)(ent >> 1);
-                    const uint32_t pj = ent & 1u;
-                    if (lj < (int)li) {
-                        if (lj > prev) { prev = lj; prevput = (int)pj; }
-                        if (pj && lj > lastput) lastput = lj;
-                    } else if (lj > (int)li) {
-                        later = true;
-                        laterput |= pj != 0;
-                    }
-                }
-                const uint8_t seen = S.dseen[kd];
+                int64_t r;
                 bool conf;
-                if (prev >= 0) conf = prevput || isput;
-                else conf = (seen & 1u) && ((seen & 2u) || isput);
-                int64_t r = 0;
-                if (isput) r = S.cval[li];
-                else if (o[k] == MPX_OP_GET) {
-                    if (lastput >= 0) r = S.cval[lastput];
-                    else if (S.dpresent[kd]) r = S.dval[kd];
-                }
+                fl[k] = resolve_cmd(D, S.off, S.list, S.cval, kid[k], li, o[k], r, conf);
                 b.ret[c0 + li] = r;
                 if (b.conf_prev) b.conf_prev[c0 + li] = conf ? 1 : 0;
-                if (!later) fl[k] |= 1;
-                if (isput && !laterput) fl[k] |= 2;
-                if (isput && lastput < 0) fl[k] |= 4;
             }
             __syncthreads();
 #pragma unroll
             for (int k = 0; k < kPer; ++k) {
                 const uint32_t li = t + k * kStepBlock;
-                if (li >= n || kid[k] < 0) continue;
-                const int kd = kid[k];
-                if (fl[k] & 1) S.dseen[kd] = (uint8_t)(1u | (o[k] == MPX_OP_PUT ? 2u : 0u));
-                if (fl[k] & 2) {
-                    S.dval[kd] = S.cval[li];
-                    S.dpresent[kd] = 1;
-                }
-                if ((fl[k] & 4) && (uint32_t)kd >= S.n_orig && S.dfirst[kd] == kNoFirst)
-                    S.dfirst[kd] = (uint32_t)(c0 + li - c_begin);
+                if (li < n && kid[k] >= 0)
+                    apply_update(D, kid[k], fl[k], o[k], S.cval[li], (uint32_t)(c0 + li - c_begin),
+                                 S.n_orig);
             }
             __syncthreads();
         }
     }
-
-    // ---- write the table back: original entries in place, new keys in first-PUT order ----
     const uint32_t dn = S.dn < (uint32_t)kDCap ? S.dn : (uint32_t)kDCap;
-    const uint32_t norig = S.n_orig;
-    for (uint32_t e = t; e < norig; e += kStepBlock) {
-        b.kv_key_out[(uint64_t)g * kvpg + e] = S.dkey[e];
-        b.kv_val_out[(uint64_t)g * kvpg + e] = S.dval[e];
-    }
-    if (t == 0) S.scal[3] = 0;
-    __syncthreads();
-    for (uint32_t e = norig + t; e < dn; e += kStepBlock) {
-        if (!S.dpresent[e]) continue;
-        const uint32_t f = S.dfirst[e];
-        uint32_t rank = 0;
-        for (uint32_t x = norig; x < dn; ++x)
-            if (S.dpresent[x] && S.dfirst[x] < f) ++rank;
-        atomicAdd(&S.scal[3], 1u);
-        const uint32_t dst = norig + rank;
-        if (dst < kvpg) {
-            b.kv_key_out[(uint64_t)g * kvpg + dst] = S.dkey[e];
-            b.kv_val_out[(uint64_t)g * kvpg + dst] = S.dval[e];
-        }
-    }
-    __syncthreads();
-    if (t == 0) {
-        const uint32_t total = norig + S.scal[3];
-        if (total > kvpg) raise_err(err, kErrKvFull);
-        b.kv_cnt_out[g] = total < kvpg ? total : kvpg;
+    table_writeback(D, S.n_orig, dn, b.kv_key_out + (uint64_t)g * kvpg,
+                    b.kv_val_out + (uint64_t)g * kvpg, kvpg, &S.scal[0], err);
+    if (t == 0) b.kv_cnt_out[g] = S.scal[0] < kvpg ? S.scal[0] : kvpg;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kStepBlock) void k_group_general(mpx_group_batch b, int32_t nrep,
+                                                              uint32_t kvpg,
+                                                              const uint32_t* worklist,
+                                                              const uint32_t* wcount, uint32_t* err) {
+    __shared__ GenLds S;
+    const uint32_t n = *wcount;
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        group_general<MODE>(S, b, worklist[i], nrep, kvpg, err);
+        __syncthreads();
     }
 }
 
+__global__ void k_fill_worklist(uint32_t* worklist, uint32_t* wcount, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) worklist[i] = i;
+    if (i == 0) *wcount = n;
+}
+
 hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
-                             const mpx_group_batch* b, uint32_t* err, hipStream_t stream) {
+                             const mpx_group_batch* b, uint32_t* worklist, uint32_t* wcount,
+                             uint32_t* err, hipStream_t stream) {
     if (!b->n_groups) return hipSuccess;
     if (kv_per_group > (uint32_t)kDCap) return hipErrorInvalidValue;
-    if (mode == MPX_MODE_CLASSIC && b->ipg > (uint32_t)kMaxIpgBits) return hipErrorInvalidValue;
-    if (mode == MPX_MODE_MIN)
-        k_group_step<MPX_MODE_MIN><<<b->n_groups, kStepBlock, 0, stream>>>(*b, nrep, kv_per_group, err);
-    else
-        k_group_step<MPX_MODE_CLASSIC><<<b->n_groups, kStepBlock, 0, stream>>>(*b, nrep, kv_per_group,
-                                                                             err);
+    if (b->ipg > (uint32_t)kMaxIpgBits) return hipErrorInvalidValue;
+    hipError_t r = hipMemsetAsync(wcount, 0, sizeof(uint32_t), stream);
+    if (r != hipSuccess) return r;
+    const bool fast_ok = b->ipg <= (uint32_t)kFIpg;
+    const unsigned gen_grid = b->n_groups < 1024 ? b->n_groups : 1024;
+    if (mode == MPX_MODE_MIN) {
+        if (fast_ok)
+            k_group_fast<MPX_MODE_MIN><<<b->n_groups, kStepBlock, 0, stream>>>(*b, nrep, kv_per_group,
+                                                                             worklist, wcount, err);
+        else
+            k_fill_worklist<<<(b->n_groups + 255) / 256, 256, 0, stream>>>(worklist, wcount, b->n_groups);
+        k_group_general<MPX_MODE_MIN><<<gen_grid, kStepBlock, 0, stream>>>(*b, nrep, kv_per_group,
+                                                                          worklist, wcount, err);
+    } else {
+        if (fast_ok)
+            k_group_fast<MPX_MODE_CLASSIC><<<b->n_groups, kStepBlock, 0, stream>>>(
+                *b, nrep, kv_per_group, worklist, wcount, err);
+        else
+            k_fill_worklist<<<(b->n_groups + 255) / 256, 256, 0, stream>>>(worklist, wcount, b->n_groups);
+        k_group_general<MPX_MODE_CLASSIC><<<gen_grid, kStepBlock, 0, stream>>>(
+            *b, nrep, kv_per_group, worklist, wcount, err);
+    }
     return hipGetLastError();
 }
 
 }  // namespace mpx
+
+#if MPX_STAMPS
+extern "C" int mpx_debug_stamps(unsigned long long* out16, int reset) {
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(mpx::mpx_stamp_acc), 16 * sizeof(unsigned long long)) != hipSuccess)
+        return -3;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(mpx::mpx_stamp_acc), z, sizeof(z)) != hipSuccess) return -3;
+    }
+    return 0;
+}
+#endif

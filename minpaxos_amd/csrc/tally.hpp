@@ -83,7 +83,8 @@ __device__ __forceinline__ void tally_range(const mpx_accept_reply* __restrict__
                                             uint64_t n_inst, int32_t base, int32_t half,
                                             int32_t nrep, uint8_t* __restrict__ decided,
                                             uint32_t* err, uint64_t pos_off, TallyOut& out,
-                                            uint32_t* lds_dec_bits = nullptr) {
+                                            uint32_t* lds_dec_bits = nullptr,
+                                            uint32_t* lds_touch_bits = nullptr) {
     const int l = lane_id();
     const uint64_t mine = lanes_upto(l);
     // open (carried) segment, wave-uniform
@@ -115,6 +116,7 @@ __device__ __forceinline__ void tally_range(const mpx_accept_reply* __restrict__
                 reinterpret_cast<int4*>(st_out)[c_inst - base] = f;
                 if (decided) decided[c_inst - base] = cr;
                 if (lds_dec_bits && cr) mark_bit(lds_dec_bits, c_inst - base);
+                if (lds_touch_bits) mark_bit(lds_touch_bits, c_inst - base);
             }
             c_open = false;
         }
@@ -192,6 +194,7 @@ __device__ __forceinline__ void tally_range(const mpx_accept_reply* __restrict__
             reinterpret_cast<int4*>(st_out)[inst - base] = f;
             if (decided) decided[inst - base] = cr;
             if (lds_dec_bits && cr) mark_bit(lds_dec_bits, inst - base);
+            if (lds_touch_bits) mark_bit(lds_touch_bits, inst - base);
         }
         // the segment holding the last valid lane stays open
         const int L = hi_bit(Vm);
@@ -212,6 +215,7 @@ __device__ __forceinline__ void tally_range(const mpx_accept_reply* __restrict__
         reinterpret_cast<int4*>(st_out)[c_inst - base] = f;
         if (decided) decided[c_inst - base] = cr;
         if (lds_dec_bits && cr) mark_bit(lds_dec_bits, c_inst - base);
+        if (lds_touch_bits) mark_bit(lds_touch_bits, c_inst - base);
     }
 }
 

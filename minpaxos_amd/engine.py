@@ -43,14 +43,15 @@ def device_count():
 
 
 class Engine:
-    def __init__(self, device=0, n_replicas=5, mode=R.MODE_MIN, kv_capacity=0, kv_per_group=0):
+    def __init__(self, device=0, n_replicas=5, mode=R.MODE_MIN, kv_capacity=0, kv_per_group=0,
+                 max_groups=0):
         self.lib = _lib.load()
         if isinstance(mode, str):
             mode = {"min": R.MODE_MIN, "classic": R.MODE_CLASSIC}[mode.lower()]
         self.n_replicas = n_replicas
         self.mode = mode
         self.kv_per_group = kv_per_group or 512
-        cfg = _lib.MpxConfig(n_replicas, mode, kv_capacity, kv_per_group, 0)
+        cfg = _lib.MpxConfig(n_replicas, mode, kv_capacity, kv_per_group, 0, max_groups)
         h = C.c_void_p()
         rc = self.lib.mpx_open(device, C.byref(cfg), C.byref(h))
         if rc != 0:

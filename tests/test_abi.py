@@ -42,7 +42,7 @@ def test_no_device_calls_fail_cleanly():
     assert lib.mpx_close(None) == R.E_INVAL
     assert lib.mpx_accept_tally(None, None, 0, None, 0, 0, None, None, None) == R.E_INVAL
     if c.value == 0:  # this container: opening fails loudly with E_NODEV, never a CPU fallback
-        cfg = _lib.MpxConfig(5, 0, 0, 0, 0)
+        cfg = _lib.MpxConfig(5, 0, 0, 0, 0, 0)
         h = C.c_void_p()
         assert lib.mpx_open(0, C.byref(cfg), C.byref(h)) == R.E_NODEV
 
