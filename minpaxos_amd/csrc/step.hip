@@ -231,109 +231,52 @@ __device__ __forceinline__ void table_writeback(const Dict& D, uint32_t norig, u
 }
 
 // ======================================== fast path ===========================================
-// Per workgroup = per group, three transpositions of the sequential reference loops:
+// Per workgroup = per group, transpositions of the sequential reference loops:
 //   tally    one lane per INSTANCE walks that instance's replies in arrival order (the handler's
-//            own loop); replies of different instances are independent, and the only
-//            cross-instance outputs (committedUpTo, peerCommits: last assignment in array order)
-//            are max-reductions over (position+1)<<32 | value keys
-//   bucket   executed commands are counting-sorted by key into LDS buckets
-//   resolve  one lane per KEY sorts its bucket into log order (<= kFBucket entries) and walks it:
-//            Execute's return values, Conflict with the predecessor, and the key's final value
-// Nothing reaches global memory before the group is known to fit; otherwise the group is handed
-// to k_group_general through the work list.
+//            own loop, state in registers); the only cross-instance outputs (committedUpTo,
+//            peerCommits: last assignment in array order) are max-reductions over
+//            (position+1)<<32 | value keys
+//   bucket   every executed command pushes itself on its key's LDS linked list
+//   resolve  one lane per KEY copies its list into a reserved run, sorts it into log order
+//            (<= kFBucket entries) and walks it: Execute's return values, Conflict with the
+//            predecessor, and the key's final value
+// Five barriers per group. Nothing reaches global memory before the group is known to fit;
+// otherwise the group is handed to k_group_general through the work list.
 constexpr int kFRecs = 1024, kFIpg = 256, kFCmds = 1024, kFD = 256, kFH = 512, kFBucket = 32;
 constexpr int kFPer = kFCmds / kStepBlock;   // commands per thread
 constexpr int kFRecPer = kFRecs / kStepBlock;
-constexpr uint16_t kNoRange = 0xFFFF;
+constexpr uint16_t kNone16 = 0xFFFF;
+constexpr uint8_t kIdBad = 31;
 
 struct FastLds {
     union {
-        struct {                 // phase A: the group's replies + per-instance reply ranges
-            int4 recs[kFRecs];
+        struct {                 // until the tally: the group's replies (SoA) + reply ranges
+            int32_t inst[kFRecs];
+            int32_t bal[kFRecs];
+            uint8_t idok[kFRecs];    // (id code << 1) | ok, id code kIdBad = outside [0, N)
             uint16_t rstart[kFIpg];
             uint16_t rend[kFIpg];
         } a;
-        struct {                 // phase B: dictionary, buckets, command values / results
+        struct {                 // after the tally: command values / results and bucket lists
             int64_t cval[kFCmds];    // value of each command, replaced in place by its ret
-            int64_t dkey[kFD];
-            int64_t dval[kFD];
-            uint32_t hslot[kFH];
-            uint32_t cnt[kFD];
-            uint32_t dfirst[kFD];
-            uint16_t off[kFD];
-            uint16_t list[kFCmds];   // (li << 3) | op
-            uint8_t cconf[kFCmds];
-            uint8_t dpresent[kFD];
-            uint8_t dseen[kFD];
+            uint16_t next[kFCmds];   // linked list of the commands of one key
+            uint16_t list[kFCmds];   // command indices, one contiguous run per key
+            uint8_t cconf[kFCmds];   // op code until the walk, then Conflict(prev, this)
         } b;
     } u;
-    int4 sst[kFIpg];          // instance states, tallied in place
+    // dictionary: lives across the whole kernel (filled with the table right after the loads)
+    int64_t dkey[kFD];
+    int64_t dval[kFD];
+    uint32_t hslot[kFH];
+    uint32_t cnt[kFD];
+    uint32_t dfirst[kFD];
+    uint32_t head[kFD];
+    uint8_t dpresent[kFD];
+    uint8_t dseen[kFD];
     uint32_t coff[kFIpg + 1];
-    uint8_t has[kFIpg];
-    uint32_t dec_bits[kFIpg / 32];
-    uint32_t touch_bits[kFIpg / 32];
     unsigned long long red[1 + MPX_MAX_REPLICAS];
-    uint32_t wsum[kStepBlock / kWave];
-    uint32_t dn, scal[4];
+    uint32_t dn, bump, firstnil, firstbad, flags;
 };
-
-template <int MODE>
-__device__ __forceinline__ void fast_tally_instance(FastLds& S, uint32_t inst, int32_t half,
-                                                    int32_t nrep, uint32_t* err) {
-    const uint32_t a = S.u.a.rstart[inst];
-    if (a == kNoRange) return;
-    const uint32_t z = S.u.a.rend[inst];
-    int4 st = S.sst[inst];
-    bool dec = false;
-    if (MODE == MPX_MODE_MIN) {
-        // bareminpaxos.go:1023-1053
-        unsigned long long cross = 0;
-        for (uint32_t p = a; p < z; ++p) {
-            const int4 r = S.u.a.recs[p];
-            if ((r.w & 0xff) != 1) continue;                 // OK != TRUE: ignored
-            if (st.x == MPX_STATUS_NIL) {
-                raise_err(err, kErrNil);
-                break;
-            }
-            st.y += 1;                                       // AcceptOKs++
-            if (st.y + 1 > half) {
-                if (st.y == half) {
-                    st.x = MPX_COMMITTED;
-                    dec = true;
-                    cross = ((unsigned long long)(p + 1) << 32) | (uint32_t)inst;
-                }
-                if (r.z < 0 || r.z >= nrep) raise_err(err, kErrBadId);
-                else atomicMax(&S.red[1 + r.z], ((unsigned long long)(p + 1) << 32) |
-                                                    (uint32_t)(inst - 1));
-            }
-        }
-        if (cross) atomicMax(&S.red[0], cross);
-    } else {
-        // paxos.go:634-673
-        if (st.x == MPX_STATUS_NIL) {
-            raise_err(err, kErrNil);
-            return;
-        }
-        for (uint32_t p = a; p < z; ++p) {
-            if (st.x != MPX_PREPARED && st.x != MPX_ACCEPTED) break;
-            const int4 r = S.u.a.recs[p];
-            if ((r.w & 0xff) == 1) {
-                st.y += 1;
-                if (st.y + 1 > half) {
-                    st.x = MPX_COMMITTED;
-                    dec = true;
-                }
-            } else {
-                st.z += 1;
-                if (r.y > st.w) st.w = r.y;
-            }
-        }
-        if (dec) atomicMax(&S.red[0], 1ull);
-    }
-    S.sst[inst] = st;
-    atomicOr(&S.touch_bits[inst >> 5], 1u << (inst & 31));
-    if (dec) atomicOr(&S.dec_bits[inst >> 5], 1u << (inst & 31));
-}
 
 template <int MODE>
 __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, int32_t nrep,
@@ -349,6 +292,8 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     const uint64_t r0 = b.grp_rec_off[g], r1 = b.grp_rec_off[g + 1];
     const uint32_t c_lo = b.cmd_off[gi0], c_hi = b.cmd_off[gi0 + ipg];
     const uint32_t kcnt = b.kv_cnt_in[g];
+    const int32_t cu_in = b.committed_in[g];
+    const int32_t ex_in = b.executed_in[g];
     const uint64_t nrec = r1 - r0;
     const uint32_t ncmd = c_hi - c_lo;
     if (r1 < r0 || c_hi < c_lo || nrec > (uint64_t)kFRecs || ncmd > (uint32_t)kFCmds ||
@@ -356,8 +301,10 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
         if (t == 0) worklist[atomicAdd(wcount, 1u)] = g;
         return;
     }
-    // ---- one round of loads: every load is issued before any is consumed (indices are clamped
-    // instead of guarded, so no exec-mask branch splits the batch and forces vmcnt(0) waits)
+    const int64_t lo = (int64_t)ex_in + 1 < 0 ? 0 : (int64_t)ex_in + 1;  // first instance to run
+
+    // ---- phase 0: one round of loads. Every load is issued before any is consumed (indices are
+    // clamped instead of guarded, so no exec-mask branch splits the batch into vmcnt(0) waits)
     int4 rr[kFRecPer];
     if (nrec) {
         const uint32_t last = (uint32_t)nrec - 1;
@@ -367,8 +314,9 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
             rr[k] = load_rec(b.recs, r0 + (p < last ? p : last));
         }
     }
-    const uint32_t ti = (uint32_t)t < ipg ? (uint32_t)t : ipg - 1;
-    const int4 sv = reinterpret_cast<const int4*>(b.st_in)[gi0 + ti];
+    const bool own = (uint32_t)t < ipg;  // this lane owns instance t
+    const uint32_t ti = own ? (uint32_t)t : ipg - 1;
+    int4 st = reinterpret_cast<const int4*>(b.st_in)[gi0 + ti];
     const uint32_t co = b.cmd_off[gi0 + ti];
     uint8_t hs = 1;
     if (b.has_cmds) hs = b.has_cmds[gi0 + ti];
@@ -391,158 +339,192 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
         tk = b.kv_key_in[ei];
         tv = b.kv_val_in[ei];
     }
-    if (t < kFIpg) S.u.a.rstart[t] = kNoRange;
-    if (t <= MPX_MAX_REPLICAS) S.red[t] = 0;
-    if (t < kFIpg / 32) {
-        S.dec_bits[t] = 0;
-        S.touch_bits[t] = 0;
+    // LDS initialisation (regions that do not overlap the reply image)
+    for (int i = t; i < kFH; i += kStepBlock) S.hslot[i] = 0;
+    if (t < kFD) {
+        S.cnt[t] = 0;
+        S.head[t] = 0xFFFFFFFFu;
     }
+    if (t < kFIpg) S.u.a.rstart[t] = kNone16;
+    if (t <= MPX_MAX_REPLICAS) S.red[t] = 0;
+    if (t == 0) {
+        S.dn = kcnt;
+        S.bump = 0;
+        S.firstnil = ipg;
+        S.firstbad = ipg;
+        S.flags = 0;
+    }
+    if (own) S.coff[t] = co - c_lo;
+    if (t == 0) S.coff[ipg] = ncmd;
     if (nrec) {
 #pragma unroll
         for (int k = 0; k < kFRecPer; ++k) {
             const uint32_t p = t + k * kStepBlock;
-            if (p < nrec) S.u.a.recs[p] = rr[k];
+            if (p < nrec) {
+                S.u.a.inst[p] = rr[k].x;
+                S.u.a.bal[p] = rr[k].y;
+                const uint32_t idc = (rr[k].z >= 0 && rr[k].z < nrep) ? (uint32_t)rr[k].z : kIdBad;
+                S.u.a.idok[p] = (uint8_t)((idc << 1) | ((rr[k].w & 0xff) == 1 ? 1u : 0u));
+            }
         }
     }
-    if ((uint32_t)t < ipg) {
-        S.sst[t] = sv;
-        S.coff[t] = co - c_lo;
-        S.has[t] = hs;
-    }
-    if (t == 0) S.coff[ipg] = ncmd;
-    __syncthreads();
+    __syncthreads();  // B1
     STAMP(0);
 
-    // ---- 1. tally: reply ranges from head flags, then one lane per instance -------------------
+    // ---- phase 1: reply ranges from head flags; the group's table into the dictionary ----------
+    const Dict D{S.dkey, S.dval, S.dfirst, S.cnt, S.hslot, S.dpresent, S.dseen, &S.dn,
+                 (uint32_t)kFD, (uint32_t)kFH};
+    if (nrec) {
 #pragma unroll
-    for (int k = 0; k < kFRecPer; ++k) {
-        const uint32_t p = t * kFRecPer + k;
-        if (p < nrec) {
-            const int32_t inst = S.u.a.recs[p].x;
-            const int32_t prev = p ? S.u.a.recs[p - 1].x : 0;
-            const bool inwin = inst >= 0 && (uint32_t)inst < ipg;
-            if (!inwin) raise_err(err, kErrNil);  // names an instance outside instanceSpace
-            if (p == 0 || inst != prev) {
-                if (p && inst < prev) raise_err(err, kErrOrder);
-                if (inwin) S.u.a.rstart[inst] = (uint16_t)p;
-                if (p && prev >= 0 && (uint32_t)prev < ipg) S.u.a.rend[prev] = (uint16_t)p;
+        for (int k = 0; k < kFRecPer; ++k) {
+            const uint32_t p = t + k * kStepBlock;
+            if (p < nrec) {
+                const int32_t inst = S.u.a.inst[p];
+                const int32_t prev = p ? S.u.a.inst[p - 1] : 0;
+                const bool inwin = inst >= 0 && (uint32_t)inst < ipg;
+                if (!inwin) raise_err(err, kErrNil);  // outside instanceSpace
+                if (p == 0 || inst != prev) {
+                    if (p && inst < prev) raise_err(err, kErrOrder);
+                    if (inwin) S.u.a.rstart[inst] = (uint16_t)p;
+                    if (p && prev >= 0 && (uint32_t)prev < ipg) S.u.a.rend[prev] = (uint16_t)p;
+                }
+                if (p + 1 == nrec && inwin) S.u.a.rend[inst] = (uint16_t)nrec;
             }
-            if (p + 1 == nrec && inwin) S.u.a.rend[inst] = (uint16_t)nrec;
         }
     }
-    __syncthreads();
-    if ((uint32_t)t < ipg) fast_tally_instance<MODE>(S, (uint32_t)t, half, nrep, err);
-    __syncthreads();
+    if ((uint32_t)t < kcnt) dict_put_unique(D, (uint32_t)t, tk, tv);
+    __syncthreads();  // B2
     STAMP(1);
 
-    // ---- watermarks -------------------------------------------------------------------------------
-    const int32_t cu_in = b.committed_in[g];
+    // ---- phase 2: tally, one lane per instance ---------------------------------------------------
+    bool dec = false, touched = false;
+    if (own) {
+        const uint32_t a = S.u.a.rstart[t];
+        if (a != kNone16) {
+            touched = true;
+            const uint32_t z = S.u.a.rend[t];
+            if (MODE == MPX_MODE_MIN) {
+                // bareminpaxos.go:1023-1053: no status check, NACKs and ballots ignored
+                unsigned long long cross = 0;
+                for (uint32_t p = a; p < z; ++p) {
+                    const uint32_t io = S.u.a.idok[p];
+                    if (!(io & 1u)) continue;                 // OK != TRUE
+                    if (st.x == MPX_STATUS_NIL) {             // inst.Lb on a nil instance
+                        raise_err(err, kErrNil);
+                        break;
+                    }
+                    st.y += 1;                                // AcceptOKs++
+                    if (st.y + 1 > half) {
+                        if (st.y == half) {                   // first crossing: COMMITTED
+                            st.x = MPX_COMMITTED;
+                            dec = true;
+                            cross = ((unsigned long long)(p + 1) << 32) | (uint32_t)t;
+                        }
+                        const uint32_t id = io >> 1;          // peerCommits[Id] = Instance-1
+                        if (id == kIdBad) raise_err(err, kErrBadId);
+                        else atomicMax(&S.red[1 + id],
+                                       ((unsigned long long)(p + 1) << 32) | (uint32_t)(t - 1));
+                    }
+                }
+                if (cross) atomicMax(&S.red[0], cross);
+            } else {
+                // paxos.go:634-673
+                if (st.x == MPX_STATUS_NIL) raise_err(err, kErrNil);
+                for (uint32_t p = a; p < z; ++p) {
+                    if (st.x != MPX_PREPARED && st.x != MPX_ACCEPTED) break;
+                    if (S.u.a.idok[p] & 1u) {
+                        st.y += 1;
+                        if (st.y + 1 > half) {
+                            st.x = MPX_COMMITTED;
+                            dec = true;
+                        }
+                    } else {
+                        st.z += 1;
+                        const int32_t bb = S.u.a.bal[p];
+                        if (bb > st.w) st.w = bb;
+                    }
+                }
+                if (dec) atomicMax(&S.red[0], 1ull);
+            }
+        }
+        // executeCommands stops at the first nil instance (nil Cmds); CLASSIC's watermark at the
+        // first instance that is not COMMITTED
+        if ((int64_t)t >= lo && (st.x == MPX_STATUS_NIL || !hs)) atomicMin(&S.firstnil, (uint32_t)t);
+        if (MODE == MPX_MODE_CLASSIC && (int64_t)t >= (int64_t)cu_in + 1 && st.x != MPX_COMMITTED)
+            atomicMin(&S.firstbad, (uint32_t)t);
+    }
+    __syncthreads();  // B3
+    STAMP(2);
+
+    // ---- watermarks and the executed range (uniform) -----------------------------------------------
     int32_t cu = cu_in;
     if (MODE == MPX_MODE_MIN) {
         if (S.red[0]) cu = (int32_t)(uint32_t)(S.red[0] & 0xffffffffull);
-    } else if (S.red[0]) {
-        // updateCommittedUpTo over the final statuses (tallied in place)
-        if (t == 0) S.scal[1] = ipg;
-        __syncthreads();
-        const int64_t j0 = (int64_t)cu_in + 1;
-        if (j0 >= 0 && (uint64_t)j0 < ipg)
-            for (uint32_t j = (uint32_t)j0 + t; j < ipg; j += kStepBlock)
-                if (S.sst[j].x != MPX_COMMITTED) {
-                    atomicMin(&S.scal[1], j);
-                    break;
-                }
-        __syncthreads();
-        if (j0 >= 0 && (uint64_t)j0 < ipg) cu = (int32_t)S.scal[1] - 1;
+    } else if (S.red[0] && (int64_t)cu_in + 1 >= 0 && (int64_t)cu_in + 1 < (int64_t)ipg) {
+        cu = (int32_t)S.firstbad - 1;  // updateCommittedUpTo over the final statuses
     }
-    // executeCommands range: instances lo .. stop-1
-    const int32_t ex_in = b.executed_in[g];
-    int64_t lo = (int64_t)ex_in + 1, hi = (int64_t)cu;
+    int64_t hi = (int64_t)cu;
     if (hi >= (int64_t)ipg) hi = (int64_t)ipg - 1;
-    if (lo < 0) lo = 0;
-    if (t == 0) {
-        S.scal[2] = (uint32_t)(hi + 1 > lo ? hi + 1 : lo);
-        S.dn = kcnt;
-        S.scal[3] = 0;
-    }
-    // the reply image is dead from here: build the dictionary over it
-    for (int i = t; i < kFH; i += kStepBlock) S.u.b.hslot[i] = 0;
-    if (t < kFD) S.u.b.cnt[t] = 0;
-    __syncthreads();
-    if (hi >= lo)
-        for (int64_t i = lo + t; i <= hi; i += kStepBlock)
-            if (S.sst[i].x == MPX_STATUS_NIL || !S.has[i]) {
-                atomicMin(&S.scal[2], (uint32_t)i);
-                break;
-            }
-    const Dict D{S.u.b.dkey, S.u.b.dval, S.u.b.dfirst, S.u.b.cnt, S.u.b.hslot, S.u.b.dpresent,
-                 S.u.b.dseen, &S.dn, (uint32_t)kFD, (uint32_t)kFH};
-    if ((uint32_t)t < kcnt) dict_put_unique(D, (uint32_t)t, tk, tv);
-    __syncthreads();
-    STAMP(2);
-    const int64_t stop = hi >= lo ? (int64_t)S.scal[2] : lo;
+    int64_t stop = hi >= lo ? hi + 1 : lo;
+    if ((int64_t)S.firstnil < stop && (int64_t)S.firstnil >= lo) stop = S.firstnil;
     const uint32_t x0 = stop > lo ? S.coff[lo] : 0, x1 = stop > lo ? S.coff[stop] : 0;
 
-    // ---- 2. bucket the executed commands by key ---------------------------------------------------
+    // ---- phase 3: each executed command joins its key's list (the reply image is dead) ---------
     int kid[kFPer];
-    uint32_t pos[kFPer];
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) {
         const uint32_t li = t + k * kStepBlock;
         kid[k] = -1;
         if (li >= x0 && li < x1) {
             S.u.b.cval[li] = cv[k];
+            // park the op (3-bit code; ops outside the enum are no-ops, as NONE) for the walker
+            S.u.b.cconf[li] = (uint8_t)(o[k] <= MPX_OP_WLOCK ? o[k] : 6u);
             kid[k] = dict_insert(D, ck[k]);
-            if (kid[k] >= 0) pos[k] = atomicAdd(&S.u.b.cnt[kid[k]], 1u);
-            else S.scal[3] = 1;  // dictionary overflow: hand the group to the general kernel
+            if (kid[k] >= 0) {
+                atomicAdd(&S.cnt[kid[k]], 1u);
+                S.u.b.next[li] = (uint16_t)atomicExch(&S.head[kid[k]], li);
+            } else {
+                atomicOr(&S.flags, 1u);  // dictionary overflow: the general kernel takes it
+            }
         }
     }
-    __syncthreads();
+    __syncthreads();  // B4
     STAMP(3);
-    if (S.scal[3]) {
+    if (S.flags) {
         if (t == 0) worklist[atomicAdd(wcount, 1u)] = g;
         return;
     }
     const uint32_t dn = S.dn;
-    block_scan<1>(S.u.b.cnt, S.u.b.off, dn, S.wsum);
-#pragma unroll
-    for (int k = 0; k < kFPer; ++k) {
-        const uint32_t li = t + k * kStepBlock;
-        // 3-bit op code; any op outside the enum is a no-op for Execute, as NONE (code 6)
-        if (kid[k] >= 0)
-            S.u.b.list[S.u.b.off[kid[k]] + pos[k]] =
-                (uint16_t)((li << 3) | (o[k] <= MPX_OP_WLOCK ? o[k] : 6u));
-    }
-    __syncthreads();
-    STAMP(4);
 
-    // ---- 3. resolve: one lane per key walks its bucket in log order --------------------------------
+    // ---- phase 4: one lane per key: gather, sort into log order, walk ----------------------------
     if ((uint32_t)t < dn) {
         const uint32_t kd = (uint32_t)t;
-        const uint32_t n = S.u.b.cnt[kd];
+        const uint32_t n = S.cnt[kd];
         if (n > (uint32_t)kFBucket) {
-            S.scal[3] = 1;  // long bucket: the general kernel's per-command scan handles it
+            atomicOr(&S.flags, 2u);  // long bucket: the general kernel's scan handles it
         } else if (n) {
-            uint16_t* L = S.u.b.list + S.u.b.off[kd];
-            // insertion sort by log position (entries sort by li, the high bits)
-            for (uint32_t i = 1; i < n; ++i) {
-                const uint16_t x = L[i];
+            const uint32_t base = atomicAdd(&S.bump, n);
+            uint16_t* L = S.u.b.list + base;
+            uint32_t c = S.head[kd];
+            for (uint32_t i = 0; i < n; ++i) {  // gather + insertion sort by log position
+                const uint32_t li = c;
+                c = S.u.b.next[li];
                 uint32_t j = i;
-                while (j > 0 && L[j - 1] > x) {
+                while (j > 0 && L[j - 1] > li) {
                     L[j] = L[j - 1];
                     --j;
                 }
-                L[j] = x;
+                L[j] = (uint16_t)li;
             }
-            const uint8_t seen = S.u.b.dseen[kd];
-            bool have = S.u.b.dpresent[kd];
-            int64_t cur = S.u.b.dval[kd];
+            const uint8_t seen = S.dseen[kd];
+            bool have = S.dpresent[kd];
+            int64_t cur = S.dval[kd];
             bool exists = seen & 1u, prevput = (seen & 2u) != 0;
             uint32_t first_put = kNoFirst;
-            uint8_t lastop = 0;
+            bool lastput = false;
             for (uint32_t j = 0; j < n; ++j) {
-                const uint32_t e = L[j];
-                const uint32_t li = e >> 3;
-                const uint8_t op = (uint8_t)(e & 7u);
+                const uint32_t li = L[j];
+                const uint8_t op = S.u.b.cconf[li];  // the op code parked by phase 3
                 const bool put = op == MPX_OP_PUT;
                 S.u.b.cconf[li] = exists && (prevput || put);  // state.Conflict(prev, this)
                 int64_t r = 0;
@@ -557,24 +539,27 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
                 S.u.b.cval[li] = r;  // Execute's return value, in place of the command's value
                 exists = true;
                 prevput = put;
-                lastop = op;
+                lastput = put;
             }
-            S.u.b.dseen[kd] = (uint8_t)(1u | (lastop == MPX_OP_PUT ? 2u : 0u));
+            S.dseen[kd] = (uint8_t)(1u | (lastput ? 2u : 0u));
             if (have) {
-                S.u.b.dval[kd] = cur;
-                S.u.b.dpresent[kd] = 1;
+                S.dval[kd] = cur;
+                S.dpresent[kd] = 1;
             }
-            if (kd >= kcnt && first_put != kNoFirst && S.u.b.dfirst[kd] == kNoFirst)
-                S.u.b.dfirst[kd] = first_put;
+            if (kd >= kcnt && first_put != kNoFirst) {
+                S.dfirst[kd] = first_put;
+                atomicOr(&S.flags, 4u);  // a key new to the table
+            }
         }
     }
-    __syncthreads();
-    STAMP(5);
-    if (S.scal[3]) {
+    __syncthreads();  // B5
+    STAMP(4);
+    if (S.flags & 3) {
         if (t == 0) worklist[atomicAdd(wcount, 1u)] = g;
         return;
     }
-    // ret / conf_prev for the executed commands, coalesced
+
+    // ---- phase 5: outputs ----------------------------------------------------------------------
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) {
         const uint32_t li = t + k * kStepBlock;
@@ -583,15 +568,32 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
             if (b.conf_prev) b.conf_prev[c_lo + li] = S.u.b.cconf[li];
         }
     }
-    STAMP(6);
-
-    // ---- 4. outputs ------------------------------------------------------------------------------
-    table_writeback(D, kcnt, dn, b.kv_key_out + (uint64_t)g * kvpg, b.kv_val_out + (uint64_t)g * kvpg,
-                    kvpg, &S.scal[0], err);
-    if ((uint32_t)t < ipg) {
-        if ((S.touch_bits[t >> 5] >> (t & 31)) & 1u)
-            reinterpret_cast<int4*>(b.st_out)[gi0 + t] = S.sst[t];
-        if (b.decided) b.decided[gi0 + t] = (S.dec_bits[t >> 5] >> (t & 31)) & 1u;
+    int64_t* kko = b.kv_key_out + (uint64_t)g * kvpg;
+    int64_t* kvo = b.kv_val_out + (uint64_t)g * kvpg;
+    if ((uint32_t)t < kcnt) {  // original entries stay in place
+        kko[t] = tk;
+        kvo[t] = S.dval[t];
+    }
+    uint32_t total = kcnt;
+    if (S.flags & 4) {  // keys first PUT in this step: appended in order of their first PUT
+        uint32_t n_new = 0, rank = 0;
+        const bool mine = (uint32_t)t >= kcnt && (uint32_t)t < dn && S.dpresent[t];
+        const uint32_t f = mine ? S.dfirst[t] : 0;
+        for (uint32_t x = kcnt; x < dn; ++x)
+            if (S.dpresent[x]) {
+                ++n_new;
+                if (mine && S.dfirst[x] < f) ++rank;
+            }
+        total = kcnt + n_new;
+        if (mine && kcnt + rank < kvpg) {
+            kko[kcnt + rank] = S.dkey[t];
+            kvo[kcnt + rank] = S.dval[t];
+        }
+        if (t == 0 && total > kvpg) raise_err(err, kErrKvFull);
+    }
+    if (own) {
+        if (touched) reinterpret_cast<int4*>(b.st_out)[gi0 + t] = st;
+        if (b.decided) b.decided[gi0 + t] = dec ? 1 : 0;
     }
     if (t < nrep) {
         const unsigned long long k = MODE == MPX_MODE_MIN ? S.red[1 + t] : 0ull;
@@ -601,10 +603,9 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     if (t == 0) {
         b.committed_out[g] = cu;
         b.executed_out[g] = stop > lo ? (int32_t)(stop - 1) : ex_in;
-        const uint32_t total = S.scal[0];
         b.kv_cnt_out[g] = total < kvpg ? total : kvpg;
     }
-    STAMP(7);
+    STAMP(5);
 }
 
 // ======================================= general path =========================================

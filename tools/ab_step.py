@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of several builds of the engine on the same data, in ONE process
+(cdna_hip_programming.md §5.4 rule 24): each build is loaded as its own shared object, and the
+fused group step of every build is timed round-robin with HIP events on its engine stream.
+
+  python tools/ab_step.py minpaxos_amd/libmpx.so /tmp/libmpx_old.so [--rounds 5 --iters 10]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+from minpaxos_amd import _lib, synth  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--groups", type=int, default=65536)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--mode", type=int, default=0)
+    a = ap.parse_args()
+    import torch
+    dev = torch.device("cuda", 0)
+    G, ipg, N, K = a.groups, 256, 5, 512
+    b = synth.group_batch(G, ipg, N, 4, 256, seed=45)
+
+    def dt(x):
+        arr = np.ascontiguousarray(x)
+        if arr.dtype.names:
+            arr = arr.view(np.uint8)
+        return torch.from_numpy(arr).to(dev)
+
+    m = len(b["op"])
+    d = dict(recs=dt(b["recs"]), off=dt(b["grp_rec_off"]), st_in=dt(b["st_in"]),
+             st_out=torch.empty(G * ipg * 16, dtype=torch.uint8, device=dev),
+             ci=dt(b["committed_in"]), ei=dt(b["executed_in"]), pi=dt(b["peer_in"]),
+             po=torch.empty(G * N, dtype=torch.int32, device=dev),
+             co=torch.empty(G, dtype=torch.int32, device=dev),
+             eo=torch.empty(G, dtype=torch.int32, device=dev),
+             op=dt(b["op"]), key=dt(b["key"]), val=dt(b["val"]), coff=dt(b["cmd_off"]),
+             ret=torch.zeros(m, dtype=torch.int64, device=dev),
+             conf=torch.zeros(m, dtype=torch.uint8, device=dev))
+    for s in ("0", "1"):
+        d["kc" + s] = torch.zeros(G, dtype=torch.int32, device=dev)
+        d["kk" + s] = torch.zeros(G * K, dtype=torch.int64, device=dev)
+        d["kv" + s] = torch.zeros(G * K, dtype=torch.int64, device=dev)
+    p = lambda t: t.data_ptr()  # noqa: E731
+
+    def batch(i, o):
+        return _lib.MpxGroupBatch(G, ipg, p(d["recs"]), p(d["off"]), p(d["st_in"]), p(d["st_out"]),
+                                  p(d["ci"]), p(d["co"]), p(d["ei"]), p(d["eo"]), p(d["pi"]),
+                                  p(d["po"]), p(d["op"]), p(d["key"]), p(d["val"]), p(d["coff"]),
+                                  None, p(d["ret"]), p(d["conf"]), p(d["kc" + i]), p(d["kk" + i]),
+                                  p(d["kv" + i]), p(d["kc" + o]), p(d["kk" + o]), p(d["kv" + o]),
+                                  None)
+
+    engines = []
+    for path in a.libs:
+        lib = C.CDLL(os.path.abspath(path))
+        for name, (res, args) in _lib.SIGNATURES.items():
+            f = getattr(lib, name)
+            f.restype, f.argtypes = res, args
+        cfg = _lib.MpxConfig(N, a.mode, 0, K, 0, 0)
+        h = C.c_void_p()
+        assert lib.mpx_open(0, C.byref(cfg), C.byref(h)) == 0
+        stream = lib.mpx_stream(h)
+        engines.append((path, lib, h, stream))
+    warm = batch("1", "0")
+    step = batch("0", "1")
+    for path, lib, h, s in engines:
+        assert lib.mpx_group_step_dev(h, C.byref(warm), s) == 0
+        assert lib.mpx_synchronize(h) == 0
+    times = {path: [] for path, *_ in engines}
+    outs = {}
+    for r in range(a.rounds):
+        for path, lib, h, s in engines:
+            ts = torch.cuda.ExternalStream(s, device=dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(ts)
+            for _ in range(a.iters):
+                lib.mpx_group_step_dev(h, C.byref(step), s)
+            e1.record(ts)
+            assert lib.mpx_synchronize(h) == 0
+            times[path].append(e0.elapsed_time(e1) / a.iters)
+            if r == 0:
+                outs[path] = (d["ret"].sum().item(), d["co"].sum().item(), d["kv1"].sum().item())
+    ref = None
+    for path, ts in times.items():
+        same = "" if ref is None else ("  outputs " + ("==" if outs[path] == ref else "DIFFER"))
+        ref = ref or outs[path]
+        print(f"{os.path.basename(path):28s} median {np.median(ts):.4f} ms  min {np.min(ts):.4f} ms{same}")
+
+
+if __name__ == "__main__":
+    main()

@@ -19,8 +19,7 @@ from minpaxos_amd import _lib, synth  # noqa: E402
 from minpaxos_amd import records as R  # noqa: E402
 from minpaxos_amd.engine import Engine  # noqa: E402
 
-PHASES = ["loads", "tally", "watermarks+table", "bucket/insert", "scan+list", "resolve+ret",
-          "dict update", "outputs"]
+PHASES = ["loads", "heads+table", "tally", "bucket/insert", "walk", "outputs"]
 
 
 def main():
@@ -38,7 +37,7 @@ def main():
     lib.mpx_debug_stamps(C.cast(buf, C.c_void_p), 1)
     e.group_step(b, w["kv_cnt"], w["kv_key"], w["kv_val"])
     lib.mpx_debug_stamps(C.cast(buf, C.c_void_p), 1)
-    tot = sum(buf[:8])
+    tot = sum(buf[:len(PHASES)])
     for i, name in enumerate(PHASES):
         print(f"{name:18s} {buf[i] / a.groups:10.0f} cycles/WG  {100.0 * buf[i] / max(tot, 1):5.1f}%")
     print(f"{'total':18s} {tot / a.groups:10.0f} cycles/WG")
