@@ -50,6 +50,12 @@ __device__ unsigned long long mpx_stamp_acc[16];
 #define STAMP_DECL
 #define STAMP(k)
 #endif
+// Diagnostic A/B builds only (make variant DEFS=-DMPX_ABLATE=bits): skip a phase of k_group_fast
+// to price it (results are wrong). 1 tally, 2 key lookup, 4 resolve scan, 8 reply ranges,
+// 16 table/state outputs.
+#ifndef MPX_ABLATE
+#define MPX_ABLATE 0
+#endif
 
 constexpr int kStepBlock = 256;
 constexpr uint32_t kLock = 0xFFFFFFFFu;
@@ -231,18 +237,20 @@ __device__ __forceinline__ void table_writeback(const Dict& D, uint32_t norig, u
 }
 
 // ======================================== fast path ===========================================
-// Per workgroup = per group, transpositions of the sequential reference loops:
-//   tally    one lane per INSTANCE walks that instance's replies in arrival order (the handler's
-//            own loop, state in registers); the only cross-instance outputs (committedUpTo,
+// Per workgroup = per group, transpositions of the sequential reference loops, written with
+// uniform control flow (loop trip counts are wave maxima, bodies are predicated) because the
+// scalar unit, shared by the CU's four SIMDs, is what divergent code saturates:
+//   tally    one lane per INSTANCE applies the handler to that instance's replies in arrival
+//            order (state in registers); the only cross-instance outputs (committedUpTo,
 //            peerCommits: last assignment in array order) are max-reductions over
 //            (position+1)<<32 | value keys
-//   bucket   every executed command pushes itself on its key's LDS linked list
-//   resolve  one lane per KEY copies its list into a reserved run, sorts it into log order
-//            (<= kFBucket entries) and walks it: Execute's return values, Conflict with the
-//            predecessor, and the key's final value
-// Five barriers per group. Nothing reaches global memory before the group is known to fit;
-// otherwise the group is handed to k_group_general through the work list.
-constexpr int kFRecs = 1024, kFIpg = 256, kFCmds = 1024, kFD = 256, kFH = 512, kFBucket = 32;
+//   bucket   executed commands are counting-sorted by key into LDS buckets
+//   resolve  one lane per COMMAND scans its key's bucket: predecessor (Conflict), last PUT before
+//            it (Execute's return value), last PUT of the key (its final value)
+// The group is applied in one chunk, so no per-key state carries between chunks: a key is
+// present at the start iff it is one of the table's entries. Nothing reaches global memory
+// before the group is known to fit; otherwise it goes to k_group_general via the work list.
+constexpr int kFRecs = 1024, kFIpg = 256, kFCmds = 1024, kFD = 256, kFH = 512;
 constexpr int kFPer = kFCmds / kStepBlock;   // commands per thread
 constexpr int kFRecPer = kFRecs / kStepBlock;
 constexpr uint16_t kNone16 = 0xFFFF;
@@ -257,26 +265,87 @@ struct FastLds {
             uint16_t rstart[kFIpg];
             uint16_t rend[kFIpg];
         } a;
-        struct {                 // after the tally: command values / results and bucket lists
-            int64_t cval[kFCmds];    // value of each command, replaced in place by its ret
-            uint16_t next[kFCmds];   // linked list of the commands of one key
-            uint16_t list[kFCmds];   // command indices, one contiguous run per key
-            uint8_t cconf[kFCmds];   // op code until the walk, then Conflict(prev, this)
+        struct {                 // after the tally: command values and key buckets
+            int64_t cval[kFCmds];
+            uint16_t list[kFCmds];   // (li << 1) | isPut, contiguous per key
         } b;
     } u;
-    // dictionary: lives across the whole kernel (filled with the table right after the loads)
+    // dictionary (filled with the group's table right after the loads)
     int64_t dkey[kFD];
-    int64_t dval[kFD];
-    uint32_t hslot[kFH];
+    int64_t dval[kFD];       // value at the start of the step
+    int64_t dnew[kFD];       // value after the step (valid where dput is set)
+    uint32_t hslot[kFH];     // 0 empty | (fingerprint << 16) | (kid + 1) | kLock | kDead
     uint32_t cnt[kFD];
-    uint32_t dfirst[kFD];
-    uint32_t head[kFD];
-    uint8_t dpresent[kFD];
-    uint8_t dseen[kFD];
+    uint32_t off[kFD];
+    uint32_t dfirst[kFD];    // first PUT (relative command index) of keys new to the table
+    uint8_t dput[kFD];
     uint32_t coff[kFIpg + 1];
     unsigned long long red[1 + MPX_MAX_REPLICAS];
-    uint32_t dn, bump, firstnil, firstbad, flags;
+    uint32_t dn, firstnil, firstbad, flags;
 };
+
+__device__ __forceinline__ uint32_t fslot(uint32_t h, uint32_t kid) {
+    return (h & 0xFFFF0000u) | (kid + 1);
+}
+
+// wave-uniform maximum of a per-lane value
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t x = __shfl_xor(v, d);
+        v = v > x ? v : x;
+    }
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+// lookup with a few unrolled probes; -1 absent, -2 unresolved (needs the slow path)
+__device__ __forceinline__ int fast_lookup(const FastLds& S, int64_t key, uint32_t h) {
+    int kid = -2;
+    uint32_t i = h & (kFH - 1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t e = S.hslot[(i + q) & (kFH - 1)];
+        const bool cand = e != 0 && e < kDead && (e & 0xFFFF0000u) == (h & 0xFFFF0000u);
+        const uint32_t k = cand ? (e & 0xFFFFu) - 1 : 0;
+        const bool match = cand && S.dkey[k] == key;
+        const bool stop = kid == -2 && (match || e == 0);
+        kid = stop ? (match ? (int)k : -1) : kid;
+        if (__builtin_amdgcn_readfirstlane(__ballot(kid == -2) == 0)) break;  // all resolved
+    }
+    return kid;
+}
+
+// find-or-insert (slow path: new keys, long probe chains); -1 when the dictionary is full
+__device__ int fast_insert(FastLds& S, int64_t key, uint32_t h) {
+    uint32_t i = h & (kFH - 1);
+    for (uint32_t probe = 0; probe < (uint32_t)kFH;) {
+        uint32_t cur = __hip_atomic_load(&S.hslot[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == 0) {
+            const uint32_t old = atomicCAS(&S.hslot[i], 0u, kLock);
+            if (old == 0) {
+                const uint32_t kid = atomicAdd(&S.dn, 1u);
+                if (kid >= (uint32_t)kFD) {
+                    __hip_atomic_store(&S.hslot[i], kDead, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    return -1;
+                }
+                S.dkey[kid] = key;
+                S.dval[kid] = 0;
+                S.dput[kid] = 0;
+                S.dfirst[kid] = kNoFirst;
+                __hip_atomic_store(&S.hslot[i], fslot(h, kid), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return (int)kid;
+            }
+            cur = old;
+        }
+        if (cur == kLock) continue;  // being published by another lane: re-read this slot
+        if (cur != kDead && (cur & 0xFFFF0000u) == (h & 0xFFFF0000u) &&
+            S.dkey[(cur & 0xFFFFu) - 1] == key)
+            return (int)((cur & 0xFFFFu) - 1);
+        i = (i + 1) & (kFH - 1);
+        ++probe;
+    }
+    return -1;
+}
 
 template <int MODE>
 __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, int32_t nrep,
@@ -285,7 +354,7 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     __shared__ FastLds S;
     STAMP_DECL
     const uint32_t g = blockIdx.x;
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, l = lane_id();
     const int32_t half = nrep >> 1;
     const uint32_t ipg = b.ipg;
     const uint64_t gi0 = (uint64_t)g * ipg;
@@ -302,27 +371,29 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
         return;
     }
     const int64_t lo = (int64_t)ex_in + 1 < 0 ? 0 : (int64_t)ex_in + 1;  // first instance to run
+    uint32_t ebits = 0;                                                  // error bits of this lane
 
-    // ---- phase 0: one round of loads. Every load is issued before any is consumed (indices are
-    // clamped instead of guarded, so no exec-mask branch splits the batch into vmcnt(0) waits)
+    // ---- phase 0: one round of loads (indices clamped, not guarded: no branch splits the batch)
     int4 rr[kFRecPer];
-    if (nrec) {
+    if (nrec) {  // uniform: groups without replies read nothing (the array may end here)
         const uint32_t last = (uint32_t)nrec - 1;
 #pragma unroll
         for (int k = 0; k < kFRecPer; ++k) {
             const uint32_t p = t + k * kStepBlock;
             rr[k] = load_rec(b.recs, r0 + (p < last ? p : last));
         }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kFRecPer; ++k) rr[k] = make_int4(-1, 0, 0, 0);
     }
     const bool own = (uint32_t)t < ipg;  // this lane owns instance t
     const uint32_t ti = own ? (uint32_t)t : ipg - 1;
     int4 st = reinterpret_cast<const int4*>(b.st_in)[gi0 + ti];
     const uint32_t co = b.cmd_off[gi0 + ti];
-    uint8_t hs = 1;
-    if (b.has_cmds) hs = b.has_cmds[gi0 + ti];
+    const uint8_t hs = b.has_cmds ? b.has_cmds[gi0 + ti] : (uint8_t)1;
     uint8_t o[kFPer];
     int64_t ck[kFPer], cv[kFPer];
-    if (ncmd) {
+    if (ncmd) {  // uniform
         const uint32_t last = ncmd - 1;
 #pragma unroll
         for (int k = 0; k < kFPer; ++k) {
@@ -332,126 +403,159 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
             ck[k] = b.key[ci];
             cv[k] = b.val[ci];
         }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kFPer; ++k) {
+            o[k] = 0;
+            ck[k] = 0;
+            cv[k] = 0;
+        }
     }
-    int64_t tk = 0, tv = 0;
-    if (kcnt) {
-        const uint64_t ei = (uint64_t)g * kvpg + ((uint32_t)t < kcnt ? (uint32_t)t : kcnt - 1);
-        tk = b.kv_key_in[ei];
-        tv = b.kv_val_in[ei];
-    }
-    // LDS initialisation (regions that do not overlap the reply image)
-    for (int i = t; i < kFH; i += kStepBlock) S.hslot[i] = 0;
-    if (t < kFD) {
-        S.cnt[t] = 0;
-        S.head[t] = 0xFFFFFFFFu;
-    }
-    if (t < kFIpg) S.u.a.rstart[t] = kNone16;
+    const uint64_t ei = (uint64_t)g * kvpg + ((uint32_t)t < kcnt ? (uint32_t)t : (kcnt ? kcnt - 1 : 0));
+    const int64_t tk = b.kv_key_in[ei];
+    const int64_t tv = b.kv_val_in[ei];
+    // LDS initialisation (regions outside the reply image)
+    S.hslot[t] = 0;
+    S.hslot[t + kStepBlock] = 0;
+    S.cnt[t] = 0;
+    S.u.a.rstart[t] = kNone16;
+    S.coff[t] = own ? co - c_lo : ncmd;
     if (t <= MPX_MAX_REPLICAS) S.red[t] = 0;
     if (t == 0) {
+        S.coff[kFIpg] = ncmd;
         S.dn = kcnt;
-        S.bump = 0;
         S.firstnil = ipg;
         S.firstbad = ipg;
         S.flags = 0;
     }
-    if (own) S.coff[t] = co - c_lo;
-    if (t == 0) S.coff[ipg] = ncmd;
-    if (nrec) {
 #pragma unroll
-        for (int k = 0; k < kFRecPer; ++k) {
-            const uint32_t p = t + k * kStepBlock;
-            if (p < nrec) {
-                S.u.a.inst[p] = rr[k].x;
-                S.u.a.bal[p] = rr[k].y;
-                const uint32_t idc = (rr[k].z >= 0 && rr[k].z < nrep) ? (uint32_t)rr[k].z : kIdBad;
-                S.u.a.idok[p] = (uint8_t)((idc << 1) | ((rr[k].w & 0xff) == 1 ? 1u : 0u));
-            }
-        }
+    for (int k = 0; k < kFRecPer; ++k) {
+        const uint32_t p = t + k * kStepBlock;
+        const uint32_t idc = (rr[k].z >= 0 && rr[k].z < nrep) ? (uint32_t)rr[k].z : kIdBad;
+        S.u.a.inst[p] = rr[k].x;
+        S.u.a.bal[p] = rr[k].y;
+        S.u.a.idok[p] = (uint8_t)((idc << 1) | ((rr[k].w & 0xff) == 1 ? 1u : 0u));
     }
     __syncthreads();  // B1
     STAMP(0);
 
     // ---- phase 1: reply ranges from head flags; the group's table into the dictionary ----------
-    const Dict D{S.dkey, S.dval, S.dfirst, S.cnt, S.hslot, S.dpresent, S.dseen, &S.dn,
-                 (uint32_t)kFD, (uint32_t)kFH};
-    if (nrec) {
 #pragma unroll
-        for (int k = 0; k < kFRecPer; ++k) {
-            const uint32_t p = t + k * kStepBlock;
-            if (p < nrec) {
-                const int32_t inst = S.u.a.inst[p];
-                const int32_t prev = p ? S.u.a.inst[p - 1] : 0;
-                const bool inwin = inst >= 0 && (uint32_t)inst < ipg;
-                if (!inwin) raise_err(err, kErrNil);  // outside instanceSpace
-                if (p == 0 || inst != prev) {
-                    if (p && inst < prev) raise_err(err, kErrOrder);
-                    if (inwin) S.u.a.rstart[inst] = (uint16_t)p;
-                    if (p && prev >= 0 && (uint32_t)prev < ipg) S.u.a.rend[prev] = (uint16_t)p;
-                }
-                if (p + 1 == nrec && inwin) S.u.a.rend[inst] = (uint16_t)nrec;
-            }
-        }
+    for (int k = 0; k < kFRecPer; ++k) {
+        const uint32_t p = t + k * kStepBlock;
+        const bool valid = p < nrec;
+        const int32_t inst = S.u.a.inst[p];
+        const int32_t prev = S.u.a.inst[p ? p - 1 : 0];
+        const bool inwin = inst >= 0 && (uint32_t)inst < ipg;
+        const bool pinwin = prev >= 0 && (uint32_t)prev < ipg;
+        const bool head = valid && (p == 0 || inst != prev);
+        ebits |= (valid && !inwin) ? kErrNil : 0u;               // outside instanceSpace
+        ebits |= (head && p && inst < prev) ? kErrOrder : 0u;
+        if (head && inwin) S.u.a.rstart[inst] = (uint16_t)p;
+        if (head && p && pinwin) S.u.a.rend[prev] = (uint16_t)p;
+        if (valid && p + 1 == nrec && inwin) S.u.a.rend[inst] = (uint16_t)nrec;
     }
-    if ((uint32_t)t < kcnt) dict_put_unique(D, (uint32_t)t, tk, tv);
+    const uint32_t th = lhash(tk);
+    if ((uint32_t)t < kcnt) {
+        S.dkey[t] = tk;
+        S.dval[t] = tv;
+        S.dput[t] = 0;
+        uint32_t i = th & (kFH - 1);
+        while (atomicCAS(&S.hslot[i], 0u, fslot(th, (uint32_t)t)) != 0u) i = (i + 1) & (kFH - 1);
+    }
     __syncthreads();  // B2
     STAMP(1);
 
-    // ---- phase 2: tally, one lane per instance ---------------------------------------------------
-    bool dec = false, touched = false;
-    if (own) {
-        const uint32_t a = S.u.a.rstart[t];
-        if (a != kNone16) {
-            touched = true;
-            const uint32_t z = S.u.a.rend[t];
-            if (MODE == MPX_MODE_MIN) {
-                // bareminpaxos.go:1023-1053: no status check, NACKs and ballots ignored
-                unsigned long long cross = 0;
-                for (uint32_t p = a; p < z; ++p) {
-                    const uint32_t io = S.u.a.idok[p];
-                    if (!(io & 1u)) continue;                 // OK != TRUE
-                    if (st.x == MPX_STATUS_NIL) {             // inst.Lb on a nil instance
-                        raise_err(err, kErrNil);
-                        break;
-                    }
-                    st.y += 1;                                // AcceptOKs++
-                    if (st.y + 1 > half) {
-                        if (st.y == half) {                   // first crossing: COMMITTED
-                            st.x = MPX_COMMITTED;
-                            dec = true;
-                            cross = ((unsigned long long)(p + 1) << 32) | (uint32_t)t;
-                        }
-                        const uint32_t id = io >> 1;          // peerCommits[Id] = Instance-1
-                        if (id == kIdBad) raise_err(err, kErrBadId);
-                        else atomicMax(&S.red[1 + id],
-                                       ((unsigned long long)(p + 1) << 32) | (uint32_t)(t - 1));
-                    }
-                }
-                if (cross) atomicMax(&S.red[0], cross);
-            } else {
-                // paxos.go:634-673
-                if (st.x == MPX_STATUS_NIL) raise_err(err, kErrNil);
-                for (uint32_t p = a; p < z; ++p) {
-                    if (st.x != MPX_PREPARED && st.x != MPX_ACCEPTED) break;
-                    if (S.u.a.idok[p] & 1u) {
-                        st.y += 1;
-                        if (st.y + 1 > half) {
-                            st.x = MPX_COMMITTED;
-                            dec = true;
-                        }
-                    } else {
-                        st.z += 1;
-                        const int32_t bb = S.u.a.bal[p];
-                        if (bb > st.w) st.w = bb;
-                    }
-                }
-                if (dec) atomicMax(&S.red[0], 1ull);
-            }
+    // ---- phase 2: tally, one lane per instance (uniform trip count, predicated body) ----------
+    bool dec = false;
+#if MPX_ABLATE & 8
+    const uint32_t ra = (uint32_t)t * 4;
+    const bool touched = true;
+    const uint32_t rn = 4;
+#else
+    const uint32_t ra = own ? S.u.a.rstart[t] : kNone16;
+    const bool touched = ra != kNone16;
+    const uint32_t rn = touched ? (uint32_t)S.u.a.rend[t] - ra : 0;
+#endif
+#if MPX_ABLATE & 1
+    const uint32_t rmax = 0;
+#else
+    const uint32_t rmax = wave_max_u32(rn);
+#endif
+    if (MODE == MPX_MODE_MIN) {
+        // bareminpaxos.go:1023-1053: no status check; NACKs and ballots ignored
+        unsigned long long cross = 0;
+        // predicates are 0/1 integers (see the resolve scan): no lane-mask arithmetic per reply
+        int32_t deci = 0;
+        for (uint32_t j = 0; j < rmax; ++j) {
+            const uint32_t p = j < rn ? ra + j : 0;
+            const uint32_t io0 = S.u.a.idok[p];            // unconditional load, then select
+            const uint32_t io = j < rn ? io0 : 0u;
+            const int32_t okj = (int32_t)(io & 1u);                      // OK == TRUE
+            const uint32_t nilbit = st.x == MPX_STATUS_NIL ? kErrNil : 0u;
+            ebits |= okj ? nilbit : 0u;                                  // inst.Lb of a nil instance
+            const int32_t oks = st.y + okj;                              // AcceptOKs++
+            const int32_t c1 = oks >= half ? okj : 0;                    // AcceptOKs+1 > N>>1
+            const int32_t dj = oks == half ? c1 : 0;                     // the crossing: COMMITTED
+            st.y = oks;
+            st.x = dj ? MPX_COMMITTED : st.x;
+            deci |= dj;
+            cross = dj ? (((unsigned long long)(p + 1) << 32) | (uint32_t)t) : cross;
+            const uint32_t id = io >> 1;                                 // peerCommits[Id] = inst-1
+            const uint32_t badbit = id == kIdBad ? kErrBadId : 0u;
+            ebits |= c1 ? badbit : 0u;
+            if ((c1 ? (int32_t)(id != kIdBad) : 0) != 0)
+                atomicMax(&S.red[1 + id], ((unsigned long long)(p + 1) << 32) | (uint32_t)(t - 1));
         }
-        // executeCommands stops at the first nil instance (nil Cmds); CLASSIC's watermark at the
-        // first instance that is not COMMITTED
-        if ((int64_t)t >= lo && (st.x == MPX_STATUS_NIL || !hs)) atomicMin(&S.firstnil, (uint32_t)t);
-        if (MODE == MPX_MODE_CLASSIC && (int64_t)t >= (int64_t)cu_in + 1 && st.x != MPX_COMMITTED)
-            atomicMin(&S.firstbad, (uint32_t)t);
+        dec = deci != 0;
+        // last crossing in array order: wave max, one LDS atomic per wave
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const unsigned long long x = __shfl_xor(cross, d);
+            cross = cross > x ? cross : x;
+        }
+        if (l == 0 && cross) atomicMax(&S.red[0], cross);
+    } else {
+        // paxos.go:634-673
+        ebits |= (touched && st.x == MPX_STATUS_NIL) ? kErrNil : 0u;
+        int32_t deci = 0;
+        for (uint32_t j = 0; j < rmax; ++j) {
+            const uint32_t p = j < rn ? ra + j : 0;
+            const int32_t act = j < rn ? 1 : 0;
+            const int32_t io = (int32_t)S.u.a.idok[p];
+            const int32_t bj = S.u.a.bal[p];
+            // status PREPARED (1) or ACCEPTED (2): the reply is processed
+            const int32_t live = (uint32_t)(st.x - MPX_PREPARED) < 2u ? act : 0;
+            const int32_t okj = live & io & 1;
+            const int32_t nk = live & ((io & 1) ^ 1);
+            const int32_t oks = st.y + okj;
+            const int32_t c = oks >= half ? okj : 0;                     // acceptOKs+1 > N>>1
+            st.y = oks;
+            st.x = c ? MPX_COMMITTED : st.x;
+            deci |= c;
+            st.z += nk;
+            const int32_t nb = nk ? bj : INT32_MIN;
+            st.w = st.w > nb ? st.w : nb;
+        }
+        dec = deci != 0;
+        if (__ballot(dec) && l == 0) atomicMax(&S.red[0], 1ull);
+    }
+    // executeCommands stops at the first nil instance (nil Cmds); CLASSIC's watermark at the first
+    // instance that is not COMMITTED: wave minima, one LDS atomic per wave
+    {
+        uint32_t fn = (own && (int64_t)t >= lo && (st.x == MPX_STATUS_NIL || !hs)) ? (uint32_t)t : ipg;
+        uint32_t fb = (MODE == MPX_MODE_CLASSIC && own && (int64_t)t >= (int64_t)cu_in + 1 &&
+                       st.x != MPX_COMMITTED) ? (uint32_t)t : ipg;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t x = __shfl_xor(fn, d), y = __shfl_xor(fb, d);
+            fn = fn < x ? fn : x;
+            fb = fb < y ? fb : y;
+        }
+        if (l == 0) {
+            if (fn < ipg) atomicMin(&S.firstnil, fn);
+            if (MODE == MPX_MODE_CLASSIC && fb < ipg) atomicMin(&S.firstbad, fb);
+        }
     }
     __syncthreads();  // B3
     STAMP(2);
@@ -469,130 +573,145 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     if ((int64_t)S.firstnil < stop && (int64_t)S.firstnil >= lo) stop = S.firstnil;
     const uint32_t x0 = stop > lo ? S.coff[lo] : 0, x1 = stop > lo ? S.coff[stop] : 0;
 
-    // ---- phase 3: each executed command joins its key's list (the reply image is dead) ---------
+    // ---- phase 3: key of every executed command (the reply image is dead: values go there) ----
     int kid[kFPer];
+    uint32_t pos[kFPer];
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) {
         const uint32_t li = t + k * kStepBlock;
-        kid[k] = -1;
-        if (li >= x0 && li < x1) {
-            S.u.b.cval[li] = cv[k];
-            // park the op (3-bit code; ops outside the enum are no-ops, as NONE) for the walker
-            S.u.b.cconf[li] = (uint8_t)(o[k] <= MPX_OP_WLOCK ? o[k] : 6u);
-            kid[k] = dict_insert(D, ck[k]);
-            if (kid[k] >= 0) {
-                atomicAdd(&S.cnt[kid[k]], 1u);
-                S.u.b.next[li] = (uint16_t)atomicExch(&S.head[kid[k]], li);
-            } else {
-                atomicOr(&S.flags, 1u);  // dictionary overflow: the general kernel takes it
-            }
-        }
+        S.u.b.cval[li] = cv[k];
+        const bool act = li >= x0 && li < x1;
+        const uint32_t h = lhash(ck[k]);
+#if MPX_ABLATE & 2
+        int kd = (int)(uint32_t)(((uint64_t)h * (kcnt ? kcnt : 1)) >> 32);
+#else
+        int kd = fast_lookup(S, ck[k], h);                  // every lane: uniform probes
+        if (act && kd < 0) kd = fast_insert(S, ck[k], h);  // key new to the table (rare)
+#endif
+        ebits |= (act && kd < 0) ? 0x80000000u : 0u;       // dictionary full
+        kid[k] = act ? kd : -1;
+        pos[k] = (kid[k] >= 0) ? atomicAdd(&S.cnt[kid[k]], 1u) : 0u;
     }
+    if (ebits & 0x80000000u) atomicOr(&S.flags, 1u);
     __syncthreads();  // B4
     STAMP(3);
-    if (S.flags) {
+    if (S.flags & 1u) {  // dictionary overflow: the general kernel takes the group
         if (t == 0) worklist[atomicAdd(wcount, 1u)] = g;
         return;
     }
     const uint32_t dn = S.dn;
-
-    // ---- phase 4: one lane per key: gather, sort into log order, walk ----------------------------
-    if ((uint32_t)t < dn) {
-        const uint32_t kd = (uint32_t)t;
-        const uint32_t n = S.cnt[kd];
-        if (n > (uint32_t)kFBucket) {
-            atomicOr(&S.flags, 2u);  // long bucket: the general kernel's scan handles it
-        } else if (n) {
-            const uint32_t base = atomicAdd(&S.bump, n);
-            uint16_t* L = S.u.b.list + base;
-            uint32_t c = S.head[kd];
-            for (uint32_t i = 0; i < n; ++i) {  // gather + insertion sort by log position
-                const uint32_t li = c;
-                c = S.u.b.next[li];
-                uint32_t j = i;
-                while (j > 0 && L[j - 1] > li) {
-                    L[j] = L[j - 1];
-                    --j;
-                }
-                L[j] = (uint16_t)li;
-            }
-            const uint8_t seen = S.dseen[kd];
-            bool have = S.dpresent[kd];
-            int64_t cur = S.dval[kd];
-            bool exists = seen & 1u, prevput = (seen & 2u) != 0;
-            uint32_t first_put = kNoFirst;
-            bool lastput = false;
-            for (uint32_t j = 0; j < n; ++j) {
-                const uint32_t li = L[j];
-                const uint8_t op = S.u.b.cconf[li];  // the op code parked by phase 3
-                const bool put = op == MPX_OP_PUT;
-                S.u.b.cconf[li] = exists && (prevput || put);  // state.Conflict(prev, this)
-                int64_t r = 0;
-                if (put) {
-                    r = S.u.b.cval[li];
-                    cur = r;
-                    have = true;
-                    if (first_put == kNoFirst) first_put = li - x0;
-                } else if (op == MPX_OP_GET) {
-                    r = have ? cur : 0;
-                }
-                S.u.b.cval[li] = r;  // Execute's return value, in place of the command's value
-                exists = true;
-                prevput = put;
-                lastput = put;
-            }
-            S.dseen[kd] = (uint8_t)(1u | (lastput ? 2u : 0u));
-            if (have) {
-                S.dval[kd] = cur;
-                S.dpresent[kd] = 1;
-            }
-            if (kd >= kcnt && first_put != kNoFirst) {
-                S.dfirst[kd] = first_put;
-                atomicOr(&S.flags, 4u);  // a key new to the table
-            }
+    if (t < kWave) {  // exclusive scan of the bucket sizes, one wave, 4 keys per lane
+        uint32_t v[4], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[k] = S.cnt[l * 4 + k];
+            sum += v[k];
+        }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const uint32_t x = __shfl_up(incl, d);
+            if (l >= d) incl += x;
+        }
+        uint32_t run = incl - sum;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            S.off[l * 4 + k] = run;
+            run += v[k];
         }
     }
     __syncthreads();  // B5
-    STAMP(4);
-    if (S.flags & 3) {
-        if (t == 0) worklist[atomicAdd(wcount, 1u)] = g;
-        return;
-    }
-
-    // ---- phase 5: outputs ----------------------------------------------------------------------
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) {
         const uint32_t li = t + k * kStepBlock;
-        if (li >= x0 && li < x1) {
-            b.ret[c_lo + li] = S.u.b.cval[li];
-            if (b.conf_prev) b.conf_prev[c_lo + li] = S.u.b.cconf[li];
+        if (kid[k] >= 0)
+            S.u.b.list[S.off[kid[k]] + pos[k]] = (uint16_t)((li << 1) | (o[k] == MPX_OP_PUT ? 1u : 0u));
+    }
+    __syncthreads();  // B6
+    STAMP(4);
+
+    // ---- phase 4: resolve, one lane per command (uniform scans of the key's bucket) -------------
+#pragma unroll
+    for (int k = 0; k < kFPer; ++k) {
+        const uint32_t li = t + k * kStepBlock;
+        const bool act = kid[k] >= 0;
+        const uint32_t kd = act ? (uint32_t)kid[k] : 0;
+        const uint32_t a = S.off[kd];
+        const uint32_t n = act ? S.cnt[kd] : 0;
+#if MPX_ABLATE & 4
+        const uint32_t nmax = 0;
+#else
+        const uint32_t nmax = wave_max_u32(n);
+#endif
+        // Entries are e = (lj << 1) | isPut, so "lj < li" is "e < 2li" and the entry with the
+        // largest lj wins a plain max: the predecessor and the last earlier PUT are integer
+        // max-reductions (kept out of boolean lane masks, which the compiler would combine on
+        // the scalar unit). Past the bucket's end the scan reads a sentinel that never matches.
+        const int32_t li2 = (int32_t)(li << 1);
+        int32_t pe = -1, lpe = -1, later_put = 0;
+        for (uint32_t j = 0; j < nmax; ++j) {
+            const uint32_t ix = a + j < (uint32_t)kFCmds - 1 ? a + j : (uint32_t)kFCmds - 1;
+            const int32_t e0 = (int32_t)S.u.b.list[ix];  // unconditional load, then select
+            const int32_t e = j < n ? e0 : 0x7FFFFFFE;
+            const int32_t before = e < li2 ? e : -1;        // earlier command of this key
+            pe = pe > before ? pe : before;
+            const int32_t bput = before | ((before & 1) - 1);  // earlier PUT, else -1
+            lpe = lpe > bput ? lpe : bput;
+            later_put |= e > li2 + 1 ? (e & 1) : 0;         // a later PUT of this key
+        }
+        const int prev = pe >> 1;                // -1 if none (pe = -1 >> 1 = -1)
+        const bool prevput = pe >= 0 && (pe & 1);
+        const int lastput = lpe >> 1;            // -1 if none
+        const bool laterput = later_put != 0;
+        const uint8_t op = o[k];
+        const bool isput = op == MPX_OP_PUT;
+        const int64_t from_put = S.u.b.cval[lastput >= 0 ? lastput : 0];
+        const int64_t at_start = kd < kcnt ? S.dval[kd] : 0;  // present iff a table entry
+        const int64_t r = isput ? cv[k] : (op == MPX_OP_GET ? (lastput >= 0 ? from_put : at_start) : 0);
+        const bool conf = prev >= 0 && (prevput || isput);    // state.Conflict(prev, this)
+        if (act) {
+            b.ret[c_lo + li] = r;
+            if (b.conf_prev) b.conf_prev[c_lo + li] = conf ? 1 : 0;
+            if (isput && !laterput) {  // the key's last PUT: its value after the step
+                S.dnew[kd] = cv[k];
+                S.dput[kd] = 1;
+            }
+            if (isput && lastput < 0 && kd >= kcnt) S.dfirst[kd] = li - x0;
         }
     }
+    __syncthreads();  // B7
+    STAMP(5);
+
+    // ---- phase 5: outputs ----------------------------------------------------------------------
     int64_t* kko = b.kv_key_out + (uint64_t)g * kvpg;
     int64_t* kvo = b.kv_val_out + (uint64_t)g * kvpg;
-    if ((uint32_t)t < kcnt) {  // original entries stay in place
+    if (!(MPX_ABLATE & 16) && (uint32_t)t < kcnt) {  // original entries stay in place
         kko[t] = tk;
-        kvo[t] = S.dval[t];
+        kvo[t] = S.dput[t] ? S.dnew[t] : S.dval[t];
     }
     uint32_t total = kcnt;
-    if (S.flags & 4) {  // keys first PUT in this step: appended in order of their first PUT
+#if MPX_ABLATE & 16
+    if (0) {
+#else
+    if (dn > kcnt) {
+#endif  // keys first PUT in this step: appended in order of their first PUT
         uint32_t n_new = 0, rank = 0;
-        const bool mine = (uint32_t)t >= kcnt && (uint32_t)t < dn && S.dpresent[t];
-        const uint32_t f = mine ? S.dfirst[t] : 0;
-        for (uint32_t x = kcnt; x < dn; ++x)
-            if (S.dpresent[x]) {
-                ++n_new;
-                if (mine && S.dfirst[x] < f) ++rank;
-            }
+        const bool mine = (uint32_t)t >= kcnt && (uint32_t)t < dn && S.dput[t];
+        const uint32_t f = S.dfirst[mine ? t : 0];
+        for (uint32_t x = kcnt; x < dn; ++x) {
+            const bool px = S.dput[x];
+            n_new += px ? 1 : 0;
+            rank += (mine && px && S.dfirst[x] < f) ? 1 : 0;
+        }
         total = kcnt + n_new;
         if (mine && kcnt + rank < kvpg) {
             kko[kcnt + rank] = S.dkey[t];
-            kvo[kcnt + rank] = S.dval[t];
+            kvo[kcnt + rank] = S.dnew[t];
         }
-        if (t == 0 && total > kvpg) raise_err(err, kErrKvFull);
+        ebits |= (t == 0 && total > kvpg) ? kErrKvFull : 0u;
     }
     if (own) {
-        if (touched) reinterpret_cast<int4*>(b.st_out)[gi0 + t] = st;
+        if (!(MPX_ABLATE & 16) && touched) reinterpret_cast<int4*>(b.st_out)[gi0 + t] = st;
         if (b.decided) b.decided[gi0 + t] = dec ? 1 : 0;
     }
     if (t < nrep) {
@@ -605,7 +724,9 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
         b.executed_out[g] = stop > lo ? (int32_t)(stop - 1) : ex_in;
         b.kv_cnt_out[g] = total < kvpg ? total : kvpg;
     }
-    STAMP(5);
+    ebits &= 0x7FFFFFFFu;
+    if (ebits) raise_err(err, ebits);
+    STAMP(6);
 }
 
 // ======================================= general path =========================================

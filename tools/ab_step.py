@@ -47,19 +47,20 @@ def main():
              op=dt(b["op"]), key=dt(b["key"]), val=dt(b["val"]), coff=dt(b["cmd_off"]),
              ret=torch.zeros(m, dtype=torch.int64, device=dev),
              conf=torch.zeros(m, dtype=torch.uint8, device=dev))
-    for s in ("0", "1"):
-        d["kc" + s] = torch.zeros(G, dtype=torch.int32, device=dev)
-        d["kk" + s] = torch.zeros(G * K, dtype=torch.int64, device=dev)
-        d["kv" + s] = torch.zeros(G * K, dtype=torch.int64, device=dev)
     p = lambda t: t.data_ptr()  # noqa: E731
 
-    def batch(i, o):
+    def tables():  # each engine gets its own table buffers (its warm-up fills them)
+        return {k + s: torch.zeros(G * (K if k != "kc" else 1),
+                                   dtype=torch.int32 if k == "kc" else torch.int64, device=dev)
+                for k in ("kc", "kk", "kv") for s in ("0", "1")}
+
+    def batch(tb, i, o):
         return _lib.MpxGroupBatch(G, ipg, p(d["recs"]), p(d["off"]), p(d["st_in"]), p(d["st_out"]),
                                   p(d["ci"]), p(d["co"]), p(d["ei"]), p(d["eo"]), p(d["pi"]),
                                   p(d["po"]), p(d["op"]), p(d["key"]), p(d["val"]), p(d["coff"]),
-                                  None, p(d["ret"]), p(d["conf"]), p(d["kc" + i]), p(d["kk" + i]),
-                                  p(d["kv" + i]), p(d["kc" + o]), p(d["kk" + o]), p(d["kv" + o]),
-                                  None)
+                                  None, p(d["ret"]), p(d["conf"]), p(tb["kc" + i]), p(tb["kk" + i]),
+                                  p(tb["kv" + i]), p(tb["kc" + o]), p(tb["kk" + o]),
+                                  p(tb["kv" + o]), None)
 
     engines = []
     for path in a.libs:
@@ -71,16 +72,14 @@ def main():
         h = C.c_void_p()
         assert lib.mpx_open(0, C.byref(cfg), C.byref(h)) == 0
         stream = lib.mpx_stream(h)
-        engines.append((path, lib, h, stream))
-    warm = batch("1", "0")
-    step = batch("0", "1")
-    for path, lib, h, s in engines:
-        assert lib.mpx_group_step_dev(h, C.byref(warm), s) == 0
+        tb = tables()
+        engines.append((path, lib, h, stream, tb, batch(tb, "0", "1")))
+        assert lib.mpx_group_step_dev(h, C.byref(batch(tb, "1", "0")), stream) == 0  # warm-up
         assert lib.mpx_synchronize(h) == 0
-    times = {path: [] for path, *_ in engines}
+    times = {e[0]: [] for e in engines}
     outs = {}
     for r in range(a.rounds):
-        for path, lib, h, s in engines:
+        for path, lib, h, s, tb, step in engines:
             ts = torch.cuda.ExternalStream(s, device=dev)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(ts)
@@ -90,7 +89,7 @@ def main():
             assert lib.mpx_synchronize(h) == 0
             times[path].append(e0.elapsed_time(e1) / a.iters)
             if r == 0:
-                outs[path] = (d["ret"].sum().item(), d["co"].sum().item(), d["kv1"].sum().item())
+                outs[path] = (d["ret"].sum().item(), d["co"].sum().item(), tb["kv1"].sum().item())
     ref = None
     for path, ts in times.items():
         same = "" if ref is None else ("  outputs " + ("==" if outs[path] == ref else "DIFFER"))

@@ -19,7 +19,8 @@ from minpaxos_amd import _lib, synth  # noqa: E402
 from minpaxos_amd import records as R  # noqa: E402
 from minpaxos_amd.engine import Engine  # noqa: E402
 
-PHASES = ["loads", "heads+table", "tally", "bucket/insert", "walk", "outputs"]
+PHASES = ["loads (B1)", "heads+table (B2)", "tally (B3)", "lookup/insert (B4)", "scan+list (B5,B6)",
+          "resolve (B7)", "outputs"]
 
 
 def main():
