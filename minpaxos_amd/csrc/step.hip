@@ -52,7 +52,7 @@ __device__ unsigned long long mpx_stamp_acc[16];
 #endif
 // Diagnostic A/B builds only (make variant DEFS=-DMPX_ABLATE=bits): skip a phase of k_group_fast
 // to price it (results are wrong). 1 tally, 2 key lookup, 4 resolve scan, 8 reply ranges,
-// 16 table/state outputs.
+// 16 table/state outputs, 32 every instance commits (with 1: the apply without the tally).
 #ifndef MPX_ABLATE
 #define MPX_ABLATE 0
 #endif
@@ -244,17 +244,24 @@ __device__ __forceinline__ void table_writeback(const Dict& D, uint32_t norig, u
 //            order (state in registers); the only cross-instance outputs (committedUpTo,
 //            peerCommits: last assignment in array order) are max-reductions over
 //            (position+1)<<32 | value keys
-//   bucket   executed commands are counting-sorted by key into LDS buckets
+//   table    the group's table and the executed commands' keys share one open-addressing LDS
+//            table keyed by the 64-bit key itself: one 64-bit compare-and-swap per probe finds
+//            the key or claims a free slot for it (no locks, no second lookup), and the slot
+//            index is the key's bucket id
+//   bucket   executed commands are counting-sorted by slot into LDS buckets
 //   resolve  one lane per COMMAND scans its key's bucket: predecessor (Conflict), last PUT before
 //            it (Execute's return value), last PUT of the key (its final value)
 // The group is applied in one chunk, so no per-key state carries between chunks: a key is
 // present at the start iff it is one of the table's entries. Nothing reaches global memory
-// before the group is known to fit; otherwise it goes to k_group_general via the work list.
-constexpr int kFRecs = 1024, kFIpg = 256, kFCmds = 1024, kFD = 256, kFH = 512;
+// before the group is known to fit; otherwise it goes to k_group_general via the work list
+// (also for the one key the free-slot marker cannot hold, INT64_MIN).
+constexpr int kFRecs = 1024, kFIpg = 256, kFCmds = 1024, kFTab = 256, kFH = 512;
 constexpr int kFPer = kFCmds / kStepBlock;   // commands per thread
 constexpr int kFRecPer = kFRecs / kStepBlock;
 constexpr uint16_t kNone16 = 0xFFFF;
 constexpr uint8_t kIdBad = 31;
+constexpr unsigned long long kFreeKey = 0x8000000000000000ull;  // INT64_MIN marks a free slot
+constexpr uint32_t kOverflow = 0x80000000u;                      // ebits: group leaves the fast path
 
 struct FastLds {
     union {
@@ -267,26 +274,21 @@ struct FastLds {
         } a;
         struct {                 // after the tally: command values and key buckets
             int64_t cval[kFCmds];
-            uint16_t list[kFCmds];   // (li << 1) | isPut, contiguous per key
+            uint16_t list[kFCmds];   // (li << 1) | isPut, contiguous per slot
         } b;
     } u;
-    // dictionary (filled with the group's table right after the loads)
-    int64_t dkey[kFD];
-    int64_t dval[kFD];       // value at the start of the step
-    int64_t dnew[kFD];       // value after the step (valid where dput is set)
-    uint32_t hslot[kFH];     // 0 empty | (fingerprint << 16) | (kid + 1) | kLock | kDead
-    uint32_t cnt[kFD];
-    uint32_t off[kFD];
-    uint32_t dfirst[kFD];    // first PUT (relative command index) of keys new to the table
-    uint8_t dput[kFD];
+    unsigned long long hkey[kFH];  // slot -> key; kFreeKey = free
+    int64_t sval[kFH];       // value at the start of the step (slots of table entries)
+    uint32_t cnt[kFH];       // executed commands per slot
+    uint16_t off[kFH];       // bucket start in u.b.list
+    uint16_t tabidx[kFH];    // table entry holding the slot's key; kNone16 = new to the table
+    uint16_t dlast[kFH];     // 1 + command index of the key's last PUT; 0 = no PUT
+    uint16_t dfirst[kFH];    // command index of the first PUT of a key new to the table
+    uint32_t newbits[kFCmds / 32];  // first PUTs of new keys, as a bitmap over command index
     uint32_t coff[kFIpg + 1];
     unsigned long long red[1 + MPX_MAX_REPLICAS];
-    uint32_t dn, firstnil, firstbad, flags;
+    uint32_t firstnil, firstbad, flags;
 };
-
-__device__ __forceinline__ uint32_t fslot(uint32_t h, uint32_t kid) {
-    return (h & 0xFFFF0000u) | (kid + 1);
-}
 
 // wave-uniform maximum of a per-lane value
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
@@ -298,51 +300,19 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
-// lookup with a few unrolled probes; -1 absent, -2 unresolved (needs the slow path)
-__device__ __forceinline__ int fast_lookup(const FastLds& S, int64_t key, uint32_t h) {
-    int kid = -2;
+// slot of key in the group's table, claiming a free slot if the key is absent (*fresh = 1);
+// -1 when the table is full. Linear probing; the CAS returns the slot's key, so a probe that
+// meets the key (inserted earlier or concurrently by another lane) ends there too.
+__device__ __forceinline__ int fast_slot(FastLds& S, unsigned long long key, uint32_t h,
+                                         int& fresh) {
     uint32_t i = h & (kFH - 1);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t e = S.hslot[(i + q) & (kFH - 1)];
-        const bool cand = e != 0 && e < kDead && (e & 0xFFFF0000u) == (h & 0xFFFF0000u);
-        const uint32_t k = cand ? (e & 0xFFFFu) - 1 : 0;
-        const bool match = cand && S.dkey[k] == key;
-        const bool stop = kid == -2 && (match || e == 0);
-        kid = stop ? (match ? (int)k : -1) : kid;
-        if (__builtin_amdgcn_readfirstlane(__ballot(kid == -2) == 0)) break;  // all resolved
-    }
-    return kid;
-}
-
-// find-or-insert (slow path: new keys, long probe chains); -1 when the dictionary is full
-__device__ int fast_insert(FastLds& S, int64_t key, uint32_t h) {
-    uint32_t i = h & (kFH - 1);
-    for (uint32_t probe = 0; probe < (uint32_t)kFH;) {
-        uint32_t cur = __hip_atomic_load(&S.hslot[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (cur == 0) {
-            const uint32_t old = atomicCAS(&S.hslot[i], 0u, kLock);
-            if (old == 0) {
-                const uint32_t kid = atomicAdd(&S.dn, 1u);
-                if (kid >= (uint32_t)kFD) {
-                    __hip_atomic_store(&S.hslot[i], kDead, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    return -1;
-                }
-                S.dkey[kid] = key;
-                S.dval[kid] = 0;
-                S.dput[kid] = 0;
-                S.dfirst[kid] = kNoFirst;
-                __hip_atomic_store(&S.hslot[i], fslot(h, kid), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                return (int)kid;
-            }
-            cur = old;
+    for (int probe = 0; probe < kFH; ++probe) {
+        const unsigned long long old = atomicCAS(&S.hkey[i], kFreeKey, key);
+        if (old == kFreeKey || old == key) {
+            fresh = old == kFreeKey;
+            return (int)i;
         }
-        if (cur == kLock) continue;  // being published by another lane: re-read this slot
-        if (cur != kDead && (cur & 0xFFFF0000u) == (h & 0xFFFF0000u) &&
-            S.dkey[(cur & 0xFFFFu) - 1] == key)
-            return (int)((cur & 0xFFFFu) - 1);
         i = (i + 1) & (kFH - 1);
-        ++probe;
     }
     return -1;
 }
@@ -366,7 +336,7 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     const uint64_t nrec = r1 - r0;
     const uint32_t ncmd = c_hi - c_lo;
     if (r1 < r0 || c_hi < c_lo || nrec > (uint64_t)kFRecs || ncmd > (uint32_t)kFCmds ||
-        kcnt > (uint32_t)kFD || kcnt > kvpg) {
+        kcnt > (uint32_t)kFTab || kcnt > kvpg) {
         if (t == 0) worklist[atomicAdd(wcount, 1u)] = g;
         return;
     }
@@ -415,15 +385,17 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     const int64_t tk = b.kv_key_in[ei];
     const int64_t tv = b.kv_val_in[ei];
     // LDS initialisation (regions outside the reply image)
-    S.hslot[t] = 0;
-    S.hslot[t + kStepBlock] = 0;
-    S.cnt[t] = 0;
+    S.hkey[t] = kFreeKey;
+    S.hkey[t + kStepBlock] = kFreeKey;
+    reinterpret_cast<uint2*>(S.cnt)[t] = make_uint2(0u, 0u);
+    reinterpret_cast<uint32_t*>(S.tabidx)[t] = 0xFFFFFFFFu;  // kNone16 pairs
+    reinterpret_cast<uint32_t*>(S.dlast)[t] = 0u;
+    if (t < kFCmds / 32) S.newbits[t] = 0u;
     S.u.a.rstart[t] = kNone16;
     S.coff[t] = own ? co - c_lo : ncmd;
     if (t <= MPX_MAX_REPLICAS) S.red[t] = 0;
     if (t == 0) {
         S.coff[kFIpg] = ncmd;
-        S.dn = kcnt;
         S.firstnil = ipg;
         S.firstbad = ipg;
         S.flags = 0;
@@ -455,13 +427,17 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
         if (head && p && pinwin) S.u.a.rend[prev] = (uint16_t)p;
         if (valid && p + 1 == nrec && inwin) S.u.a.rend[inst] = (uint16_t)nrec;
     }
-    const uint32_t th = lhash(tk);
+    int tslot = 0;  // slot of this lane's table entry
     if ((uint32_t)t < kcnt) {
-        S.dkey[t] = tk;
-        S.dval[t] = tv;
-        S.dput[t] = 0;
-        uint32_t i = th & (kFH - 1);
-        while (atomicCAS(&S.hslot[i], 0u, fslot(th, (uint32_t)t)) != 0u) i = (i + 1) & (kFH - 1);
+        int fresh = 0;
+        const int sl = (unsigned long long)tk == kFreeKey
+                           ? -1 : fast_slot(S, (unsigned long long)tk, lhash(tk), fresh);
+        ebits |= sl < 0 ? kOverflow : 0u;
+        tslot = sl < 0 ? 0 : sl;
+        if (fresh) {  // (a duplicate entry of a malformed table shares the first one's slot)
+            S.tabidx[sl] = (uint16_t)t;
+            S.sval[sl] = tv;
+        }
     }
     __syncthreads();  // B2
     STAMP(1);
@@ -562,7 +538,9 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
 
     // ---- watermarks and the executed range (uniform) -----------------------------------------------
     int32_t cu = cu_in;
-    if (MODE == MPX_MODE_MIN) {
+    if (MPX_ABLATE & 32) {
+        cu = (int32_t)ipg - 1;
+    } else if (MODE == MPX_MODE_MIN) {
         if (S.red[0]) cu = (int32_t)(uint32_t)(S.red[0] & 0xffffffffull);
     } else if (S.red[0] && (int64_t)cu_in + 1 >= 0 && (int64_t)cu_in + 1 < (int64_t)ipg) {
         cu = (int32_t)S.firstbad - 1;  // updateCommittedUpTo over the final statuses
@@ -581,44 +559,47 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
         const uint32_t li = t + k * kStepBlock;
         S.u.b.cval[li] = cv[k];
         const bool act = li >= x0 && li < x1;
-        const uint32_t h = lhash(ck[k]);
+        const unsigned long long key = (unsigned long long)ck[k];
+        int kd = -1;
 #if MPX_ABLATE & 2
-        int kd = (int)(uint32_t)(((uint64_t)h * (kcnt ? kcnt : 1)) >> 32);
+        if (act) kd = (int)(lhash(ck[k]) & (kFH - 1));
 #else
-        int kd = fast_lookup(S, ck[k], h);                  // every lane: uniform probes
-        if (act && kd < 0) kd = fast_insert(S, ck[k], h);  // key new to the table (rare)
+        if (act && key != kFreeKey) {
+            int fresh = 0;
+            kd = fast_slot(S, key, lhash(ck[k]), fresh);
+        }
 #endif
-        ebits |= (act && kd < 0) ? 0x80000000u : 0u;       // dictionary full
+        ebits |= (act && kd < 0) ? kOverflow : 0u;  // table full, or the key INT64_MIN
         kid[k] = act ? kd : -1;
         pos[k] = (kid[k] >= 0) ? atomicAdd(&S.cnt[kid[k]], 1u) : 0u;
     }
-    if (ebits & 0x80000000u) atomicOr(&S.flags, 1u);
+    if (ebits & kOverflow) atomicOr(&S.flags, 1u);
     __syncthreads();  // B4
     STAMP(3);
     if (S.flags & 1u) {  // dictionary overflow: the general kernel takes the group
         if (t == 0) worklist[atomicAdd(wcount, 1u)] = g;
         return;
     }
-    const uint32_t dn = S.dn;
-    if (t < kWave) {  // exclusive scan of the bucket sizes, one wave, 4 keys per lane
-        uint32_t v[4], sum = 0;
+    if (t < kWave) {  // exclusive scan of the bucket sizes, one wave, 8 slots per lane
+        const uint4 c0 = reinterpret_cast<const uint4*>(S.cnt)[2 * l];
+        const uint4 c1 = reinterpret_cast<const uint4*>(S.cnt)[2 * l + 1];
+        const uint32_t v[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        uint32_t sum = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            v[k] = S.cnt[l * 4 + k];
-            sum += v[k];
-        }
+        for (int k = 0; k < 8; ++k) sum += v[k];
         uint32_t incl = sum;
 #pragma unroll
         for (int d = 1; d < kWave; d <<= 1) {
             const uint32_t x = __shfl_up(incl, d);
             if (l >= d) incl += x;
         }
-        uint32_t run = incl - sum;
+        uint32_t run = incl - sum, o16[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            S.off[l * 4 + k] = run;
-            run += v[k];
+        for (int k = 0; k < 4; ++k) {  // bucket starts fit 16 bits (<= 1024)
+            o16[k] = run | ((run + v[2 * k]) << 16);
+            run += v[2 * k] + v[2 * k + 1];
         }
+        reinterpret_cast<uint4*>(S.off)[l] = make_uint4(o16[0], o16[1], o16[2], o16[3]);
     }
     __syncthreads();  // B5
 #pragma unroll
@@ -666,17 +647,18 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
         const uint8_t op = o[k];
         const bool isput = op == MPX_OP_PUT;
         const int64_t from_put = S.u.b.cval[lastput >= 0 ? lastput : 0];
-        const int64_t at_start = kd < kcnt ? S.dval[kd] : 0;  // present iff a table entry
+        const bool intab = S.tabidx[kd] != kNone16;            // present at the start
+        const int64_t at_start = intab ? S.sval[kd] : 0;
         const int64_t r = isput ? cv[k] : (op == MPX_OP_GET ? (lastput >= 0 ? from_put : at_start) : 0);
         const bool conf = prev >= 0 && (prevput || isput);    // state.Conflict(prev, this)
         if (act) {
             b.ret[c_lo + li] = r;
             if (b.conf_prev) b.conf_prev[c_lo + li] = conf ? 1 : 0;
-            if (isput && !laterput) {  // the key's last PUT: its value after the step
-                S.dnew[kd] = cv[k];
-                S.dput[kd] = 1;
+            if (isput && !laterput) S.dlast[kd] = (uint16_t)(li + 1);  // value after the step
+            if (isput && lastput < 0 && !intab) {  // first PUT of a new key: its append rank
+                S.dfirst[kd] = (uint16_t)li;
+                atomicOr(&S.newbits[li >> 5], 1u << (li & 31));
             }
-            if (isput && lastput < 0 && kd >= kcnt) S.dfirst[kd] = li - x0;
         }
     }
     __syncthreads();  // B7
@@ -686,30 +668,37 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     int64_t* kko = b.kv_key_out + (uint64_t)g * kvpg;
     int64_t* kvo = b.kv_val_out + (uint64_t)g * kvpg;
     if (!(MPX_ABLATE & 16) && (uint32_t)t < kcnt) {  // original entries stay in place
+        const uint32_t dl = S.dlast[tslot];
         kko[t] = tk;
-        kvo[t] = S.dput[t] ? S.dnew[t] : S.dval[t];
+        kvo[t] = dl ? S.u.b.cval[dl - 1] : tv;
     }
-    uint32_t total = kcnt;
-#if MPX_ABLATE & 16
-    if (0) {
-#else
-    if (dn > kcnt) {
-#endif  // keys first PUT in this step: appended in order of their first PUT
-        uint32_t n_new = 0, rank = 0;
-        const bool mine = (uint32_t)t >= kcnt && (uint32_t)t < dn && S.dput[t];
-        const uint32_t f = S.dfirst[mine ? t : 0];
-        for (uint32_t x = kcnt; x < dn; ++x) {
-            const bool px = S.dput[x];
-            n_new += px ? 1 : 0;
-            rank += (mine && px && S.dfirst[x] < f) ? 1 : 0;
-        }
-        total = kcnt + n_new;
-        if (mine && kcnt + rank < kvpg) {
-            kko[kcnt + rank] = S.dkey[t];
-            kvo[kcnt + rank] = S.dnew[t];
-        }
-        ebits |= (t == 0 && total > kvpg) ? kErrKvFull : 0u;
+    // keys new to the table that hold a value: appended in order of their first PUT, whose
+    // rank is a popcount over the first-PUT bitmap (each wave scans the 32 words itself)
+    const uint32_t wbits = l < kFCmds / 32 ? S.newbits[l] : 0u;
+    const uint32_t pc = __popc(wbits);
+    uint32_t incl = pc;
+#pragma unroll
+    for (int d = 1; d < kFCmds / 32; d <<= 1) {
+        const uint32_t x = __shfl_up(incl, d);
+        if (l >= d) incl += x;
     }
+    const uint32_t excl = incl - pc;
+    const uint32_t n_new = (uint32_t)__shfl((int)incl, kFCmds / 32 - 1);
+    const uint32_t total = kcnt + n_new;
+#pragma unroll
+    for (int k = 0; k < kFH / kStepBlock; ++k) {
+        const uint32_t sl = t + k * kStepBlock;
+        const uint32_t dl = S.dlast[sl];
+        const bool nk = dl != 0 && S.tabidx[sl] == kNone16;
+        const uint32_t f = nk ? S.dfirst[sl] : 0u;
+        const uint32_t base = (uint32_t)__shfl((int)excl, (int)(f >> 5));
+        const uint32_t rank = base + __popc(S.newbits[f >> 5] & ((1u << (f & 31)) - 1u));
+        if (!(MPX_ABLATE & 16) && nk && kcnt + rank < kvpg) {
+            kko[kcnt + rank] = (int64_t)S.hkey[sl];
+            kvo[kcnt + rank] = S.u.b.cval[dl - 1];
+        }
+    }
+    ebits |= (t == 0 && total > kvpg) ? kErrKvFull : 0u;
     if (own) {
         if (!(MPX_ABLATE & 16) && touched) reinterpret_cast<int4*>(b.st_out)[gi0 + t] = st;
         if (b.decided) b.decided[gi0 + t] = dec ? 1 : 0;
@@ -799,7 +788,9 @@ __device__ void group_general(GenLds& S, const mpx_group_batch& b, uint32_t g, i
     // ---- watermarks --------------------------------------------------------------------------------
     const int32_t cu_in = b.committed_in[g];
     int32_t cu = cu_in;
-    if (MODE == MPX_MODE_MIN) {
+    if (MPX_ABLATE & 32) {
+        cu = (int32_t)ipg - 1;
+    } else if (MODE == MPX_MODE_MIN) {
         if (S.red[0]) cu = (int32_t)(uint32_t)(S.red[0] & 0xffffffffull);
         if (t < nrep) {
             const unsigned long long k = S.red[1 + t];
