@@ -278,14 +278,12 @@ struct FastLds {
         } b;
     } u;
     unsigned long long hkey[kFH];  // slot -> key; kFreeKey = free
-    int64_t sval[kFH];       // value at the start of the step (slots of table entries)
-    uint32_t cnt[kFH];       // executed commands per slot
-    uint16_t off[kFH];       // bucket start in u.b.list
+    int64_t dval[kFTab];     // table entry values at the start of the step
+    uint32_t cnt[kFH + 1];   // executed commands per slot, then (in place) bucket starts
     uint16_t tabidx[kFH];    // table entry holding the slot's key; kNone16 = new to the table
     uint16_t dlast[kFH];     // 1 + command index of the key's last PUT; 0 = no PUT
-    uint16_t dfirst[kFH];    // command index of the first PUT of a key new to the table
     uint32_t newbits[kFCmds / 32];  // first PUTs of new keys, as a bitmap over command index
-    uint32_t coff[kFIpg + 1];
+    uint16_t coff[kFIpg + 2];       // instance -> first command (group-relative)
     unsigned long long red[1 + MPX_MAX_REPLICAS];
     uint32_t firstnil, firstbad, flags;
 };
@@ -318,7 +316,10 @@ __device__ __forceinline__ int fast_slot(FastLds& S, unsigned long long key, uin
 }
 
 template <int MODE>
-__global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, int32_t nrep,
+#ifndef MPX_FAST_WAVES_PER_EU
+#define MPX_FAST_WAVES_PER_EU 1
+#endif
+__global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fast(mpx_group_batch b, int32_t nrep,
                                                            uint32_t kvpg, uint32_t* worklist,
                                                            uint32_t* wcount, uint32_t* err) {
     __shared__ FastLds S;
@@ -361,26 +362,6 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     int4 st = reinterpret_cast<const int4*>(b.st_in)[gi0 + ti];
     const uint32_t co = b.cmd_off[gi0 + ti];
     const uint8_t hs = b.has_cmds ? b.has_cmds[gi0 + ti] : (uint8_t)1;
-    uint8_t o[kFPer];
-    int64_t ck[kFPer], cv[kFPer];
-    if (ncmd) {  // uniform
-        const uint32_t last = ncmd - 1;
-#pragma unroll
-        for (int k = 0; k < kFPer; ++k) {
-            const uint32_t li = t + k * kStepBlock;
-            const uint64_t ci = c_lo + (li < last ? li : last);
-            o[k] = b.op[ci];
-            ck[k] = b.key[ci];
-            cv[k] = b.val[ci];
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < kFPer; ++k) {
-            o[k] = 0;
-            ck[k] = 0;
-            cv[k] = 0;
-        }
-    }
     const uint64_t ei = (uint64_t)g * kvpg + ((uint32_t)t < kcnt ? (uint32_t)t : (kcnt ? kcnt - 1 : 0));
     const int64_t tk = b.kv_key_in[ei];
     const int64_t tv = b.kv_val_in[ei];
@@ -392,10 +373,10 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     reinterpret_cast<uint32_t*>(S.dlast)[t] = 0u;
     if (t < kFCmds / 32) S.newbits[t] = 0u;
     S.u.a.rstart[t] = kNone16;
-    S.coff[t] = own ? co - c_lo : ncmd;
+    S.coff[t] = (uint16_t)(own ? co - c_lo : ncmd);
     if (t <= MPX_MAX_REPLICAS) S.red[t] = 0;
     if (t == 0) {
-        S.coff[kFIpg] = ncmd;
+        S.coff[kFIpg] = (uint16_t)ncmd;
         S.firstnil = ipg;
         S.firstbad = ipg;
         S.flags = 0;
@@ -407,6 +388,19 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
         S.u.a.inst[p] = rr[k].x;
         S.u.a.bal[p] = rr[k].y;
         S.u.a.idok[p] = (uint8_t)((idc << 1) | ((rr[k].w & 0xff) == 1 ? 1u : 0u));
+    }
+    // command keys and opcodes: issued now, they arrive during the tally (the replies' registers
+    // are free again, so the two batches of loads are never in flight together). Values follow
+    // after the tally. Uniform guard: a group without commands reads nothing.
+    const uint32_t clast = ncmd ? ncmd - 1 : 0;
+    uint8_t o[kFPer];
+    int64_t ck[kFPer];
+#pragma unroll
+    for (int k = 0; k < kFPer; ++k) {
+        const uint32_t li = t + k * kStepBlock;
+        const uint64_t ci = c_lo + (li < clast ? li : clast);
+        o[k] = ncmd ? b.op[ci] : (uint8_t)0;
+        ck[k] = ncmd ? b.key[ci] : 0;
     }
     __syncthreads();  // B1
     STAMP(0);
@@ -434,10 +428,8 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
                            ? -1 : fast_slot(S, (unsigned long long)tk, lhash(tk), fresh);
         ebits |= sl < 0 ? kOverflow : 0u;
         tslot = sl < 0 ? 0 : sl;
-        if (fresh) {  // (a duplicate entry of a malformed table shares the first one's slot)
-            S.tabidx[sl] = (uint16_t)t;
-            S.sval[sl] = tv;
-        }
+        if (fresh) S.tabidx[sl] = (uint16_t)t;  // (a duplicate entry of a malformed table
+        S.dval[t] = tv;                          //  shares the first one's slot)
     }
     __syncthreads();  // B2
     STAMP(1);
@@ -551,13 +543,21 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     if ((int64_t)S.firstnil < stop && (int64_t)S.firstnil >= lo) stop = S.firstnil;
     const uint32_t x0 = stop > lo ? S.coff[lo] : 0, x1 = stop > lo ? S.coff[stop] : 0;
 
-    // ---- phase 3: key of every executed command (the reply image is dead: values go there) ----
+    // ---- phase 3: slot of every executed command (the reply image is dead: values go there) ---
+    int64_t cv[kFPer];  // command values, stored to LDS once the lookup has covered their latency
+#pragma unroll
+    for (int k = 0; k < kFPer; ++k) {
+        const uint32_t li = t + k * kStepBlock;
+        cv[k] = ncmd ? b.val[c_lo + (li < clast ? li : clast)] : 0;
+    }
+    uint32_t ops = 0;  // the four opcodes, one byte each
+#pragma unroll
+    for (int k = 0; k < kFPer; ++k) ops |= (uint32_t)o[k] << (8 * k);
     int kid[kFPer];
     uint32_t pos[kFPer];
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) {
         const uint32_t li = t + k * kStepBlock;
-        S.u.b.cval[li] = cv[k];
         const bool act = li >= x0 && li < x1;
         const unsigned long long key = (unsigned long long)ck[k];
         int kd = -1;
@@ -576,9 +576,15 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     if (ebits & kOverflow) atomicOr(&S.flags, 1u);
     __syncthreads();  // B4
     STAMP(3);
-    if (S.flags & 1u) {  // dictionary overflow: the general kernel takes the group
+    if (S.flags & 1u) {  // table overflow: the general kernel takes the group
         if (t == 0) worklist[atomicAdd(wcount, 1u)] = g;
         return;
+    }
+    // the group stays here: the instance outputs can go now (st_out may alias st_in, so not
+    // before this point), which frees their registers for the resolve
+    if (own) {
+        if (!(MPX_ABLATE & 16) && touched) reinterpret_cast<int4*>(b.st_out)[gi0 + t] = st;
+        if (b.decided) b.decided[gi0 + t] = dec ? 1 : 0;
     }
     if (t < kWave) {  // exclusive scan of the bucket sizes, one wave, 8 slots per lane
         const uint4 c0 = reinterpret_cast<const uint4*>(S.cnt)[2 * l];
@@ -593,32 +599,37 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
             const uint32_t x = __shfl_up(incl, d);
             if (l >= d) incl += x;
         }
-        uint32_t run = incl - sum, o16[4];
+        uint32_t run = incl - sum, of[8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {  // bucket starts fit 16 bits (<= 1024)
-            o16[k] = run | ((run + v[2 * k]) << 16);
-            run += v[2 * k] + v[2 * k + 1];
+        for (int k = 0; k < 8; ++k) {
+            of[k] = run;
+            run += v[k];
         }
-        reinterpret_cast<uint4*>(S.off)[l] = make_uint4(o16[0], o16[1], o16[2], o16[3]);
+        reinterpret_cast<uint4*>(S.cnt)[2 * l] = make_uint4(of[0], of[1], of[2], of[3]);
+        reinterpret_cast<uint4*>(S.cnt)[2 * l + 1] = make_uint4(of[4], of[5], of[6], of[7]);
+        if (l == kWave - 1) S.cnt[kFH] = run;  // bucket kFH-1 ends here
     }
     __syncthreads();  // B5
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) {
         const uint32_t li = t + k * kStepBlock;
+        S.u.b.cval[li] = cv[k];
         if (kid[k] >= 0)
-            S.u.b.list[S.off[kid[k]] + pos[k]] = (uint16_t)((li << 1) | (o[k] == MPX_OP_PUT ? 1u : 0u));
+            S.u.b.list[S.cnt[kid[k]] + pos[k]] =
+                (uint16_t)((li << 1) | (((ops >> (8 * k)) & 0xffu) == MPX_OP_PUT ? 1u : 0u));
     }
     __syncthreads();  // B6
     STAMP(4);
 
     // ---- phase 4: resolve, one lane per command (uniform scans of the key's bucket) -------------
+    uint32_t fnew = 0;  // bit k: command k is the first PUT of a key new to the table
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) {
         const uint32_t li = t + k * kStepBlock;
         const bool act = kid[k] >= 0;
         const uint32_t kd = act ? (uint32_t)kid[k] : 0;
-        const uint32_t a = S.off[kd];
-        const uint32_t n = act ? S.cnt[kd] : 0;
+        const uint32_t a = S.cnt[kd];
+        const uint32_t n = act ? S.cnt[kd + 1] - a : 0;
 #if MPX_ABLATE & 4
         const uint32_t nmax = 0;
 #else
@@ -644,19 +655,21 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
         const bool prevput = pe >= 0 && (pe & 1);
         const int lastput = lpe >> 1;            // -1 if none
         const bool laterput = later_put != 0;
-        const uint8_t op = o[k];
+        const uint32_t op = (ops >> (8 * k)) & 0xffu;
         const bool isput = op == MPX_OP_PUT;
-        const int64_t from_put = S.u.b.cval[lastput >= 0 ? lastput : 0];
-        const bool intab = S.tabidx[kd] != kNone16;            // present at the start
-        const int64_t at_start = intab ? S.sval[kd] : 0;
-        const int64_t r = isput ? cv[k] : (op == MPX_OP_GET ? (lastput >= 0 ? from_put : at_start) : 0);
+        const int src = isput ? (int)li : lastput;                // PUT: own value, GET: last PUT
+        const int64_t sv = S.u.b.cval[src >= 0 ? src : 0];
+        const uint32_t ti = S.tabidx[kd];
+        const bool intab = ti != kNone16;                        // present at the start
+        const int64_t at_start = S.dval[intab ? ti : 0];
+        const int64_t r = isput ? sv : (op == MPX_OP_GET ? (lastput >= 0 ? sv : (intab ? at_start : 0)) : 0);
         const bool conf = prev >= 0 && (prevput || isput);    // state.Conflict(prev, this)
         if (act) {
             b.ret[c_lo + li] = r;
             if (b.conf_prev) b.conf_prev[c_lo + li] = conf ? 1 : 0;
             if (isput && !laterput) S.dlast[kd] = (uint16_t)(li + 1);  // value after the step
             if (isput && lastput < 0 && !intab) {  // first PUT of a new key: its append rank
-                S.dfirst[kd] = (uint16_t)li;
+                fnew |= 1u << k;
                 atomicOr(&S.newbits[li >> 5], 1u << (li & 31));
             }
         }
@@ -669,8 +682,8 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     int64_t* kvo = b.kv_val_out + (uint64_t)g * kvpg;
     if (!(MPX_ABLATE & 16) && (uint32_t)t < kcnt) {  // original entries stay in place
         const uint32_t dl = S.dlast[tslot];
-        kko[t] = tk;
-        kvo[t] = dl ? S.u.b.cval[dl - 1] : tv;
+        kko[t] = (int64_t)S.hkey[tslot];
+        kvo[t] = dl ? S.u.b.cval[dl - 1] : S.dval[t];
     }
     // keys new to the table that hold a value: appended in order of their first PUT, whose
     // rank is a popcount over the first-PUT bitmap (each wave scans the 32 words itself)
@@ -686,23 +699,17 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     const uint32_t n_new = (uint32_t)__shfl((int)incl, kFCmds / 32 - 1);
     const uint32_t total = kcnt + n_new;
 #pragma unroll
-    for (int k = 0; k < kFH / kStepBlock; ++k) {
-        const uint32_t sl = t + k * kStepBlock;
-        const uint32_t dl = S.dlast[sl];
-        const bool nk = dl != 0 && S.tabidx[sl] == kNone16;
-        const uint32_t f = nk ? S.dfirst[sl] : 0u;
-        const uint32_t base = (uint32_t)__shfl((int)excl, (int)(f >> 5));
-        const uint32_t rank = base + __popc(S.newbits[f >> 5] & ((1u << (f & 31)) - 1u));
-        if (!(MPX_ABLATE & 16) && nk && kcnt + rank < kvpg) {
-            kko[kcnt + rank] = (int64_t)S.hkey[sl];
-            kvo[kcnt + rank] = S.u.b.cval[dl - 1];
+    for (int k = 0; k < kFPer; ++k) {  // the lane of the key's first PUT appends it
+        const uint32_t li = t + k * kStepBlock;
+        const uint32_t base = (uint32_t)__shfl((int)excl, (int)(li >> 5));
+        const uint32_t rank = base + __popc(S.newbits[li >> 5] & ((1u << (li & 31)) - 1u));
+        if (!(MPX_ABLATE & 16) && ((fnew >> k) & 1u) && kcnt + rank < kvpg) {
+            const uint32_t kd = (uint32_t)kid[k];
+            kko[kcnt + rank] = (int64_t)S.hkey[kd];
+            kvo[kcnt + rank] = S.u.b.cval[S.dlast[kd] - 1];
         }
     }
     ebits |= (t == 0 && total > kvpg) ? kErrKvFull : 0u;
-    if (own) {
-        if (!(MPX_ABLATE & 16) && touched) reinterpret_cast<int4*>(b.st_out)[gi0 + t] = st;
-        if (b.decided) b.decided[gi0 + t] = dec ? 1 : 0;
-    }
     if (t < nrep) {
         const unsigned long long k = MODE == MPX_MODE_MIN ? S.red[1 + t] : 0ull;
         b.peer_out[(uint64_t)g * nrep + t] =
