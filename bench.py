@@ -223,7 +223,7 @@ def main():
                 "collective": "RCCL all-reduce(max) of 2 x groups_total int32 watermarks per step",
             },
             "roofline": {
-                "bound": "hbm", "kernel": "k_group_step", "achieved": achieved_gbs,
+                "bound": "hbm", "kernel": "k_group_fast", "achieved": achieved_gbs,
                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved_gbs / PEAK_HBM_GBS,
                 "traffic": traffic, "alg_bytes_per_launch": alg,
                 "kernel_ms_avg": kern_avg_ms, "kernel_ms_min": float(np.min(kern_ms)),
