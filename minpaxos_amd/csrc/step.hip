@@ -284,7 +284,7 @@ struct FastLds {
     uint16_t dlast[kFH];     // 1 + command index of the key's last PUT; 0 = no PUT
     uint32_t newbits[kFCmds / 32];  // first PUTs of new keys, as a bitmap over command index
     uint16_t coff[kFIpg + 2];       // instance -> first command (group-relative)
-    unsigned long long red[1 + MPX_MAX_REPLICAS];
+    uint32_t red[1 + MPX_MAX_REPLICAS];  // 1 + instance: last crossing, last peerCommits[id] source
     uint32_t firstnil, firstbad, flags;
 };
 
@@ -451,9 +451,13 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
     const uint32_t rmax = wave_max_u32(rn);
 #endif
     if (MODE == MPX_MODE_MIN) {
-        // bareminpaxos.go:1023-1053: no status check; NACKs and ballots ignored
-        unsigned long long cross = 0;
-        // predicates are 0/1 integers (see the resolve scan): no lane-mask arithmetic per reply
+        // bareminpaxos.go:1023-1053: no status check; NACKs and ballots ignored. Replies arrive in
+        // ascending instance order (anything else is MPX_E_INVAL), so the LAST assignment in array
+        // order of committedUpTo and of peerCommits[id] comes from the HIGHEST instance that makes
+        // one: each lane keeps which ids it assigned (a bitmask), a wave ballot per id finds the
+        // highest such lane, one LDS atomic per wave and id. Predicates are 0/1 integers (see the
+        // resolve scan): no lane-mask arithmetic per reply.
+        uint32_t idmask = 0;
         int32_t deci = 0;
         for (uint32_t j = 0; j < rmax; ++j) {
             const uint32_t p = j < rn ? ra + j : 0;
@@ -468,21 +472,19 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
             st.y = oks;
             st.x = dj ? MPX_COMMITTED : st.x;
             deci |= dj;
-            cross = dj ? (((unsigned long long)(p + 1) << 32) | (uint32_t)t) : cross;
             const uint32_t id = io >> 1;                                 // peerCommits[Id] = inst-1
             const uint32_t badbit = id == kIdBad ? kErrBadId : 0u;
             ebits |= c1 ? badbit : 0u;
-            if ((c1 ? (int32_t)(id != kIdBad) : 0) != 0)
-                atomicMax(&S.red[1 + id], ((unsigned long long)(p + 1) << 32) | (uint32_t)(t - 1));
+            idmask |= c1 ? (1u << id) : 0u;  // (kIdBad = 31 lies above every valid id)
         }
         dec = deci != 0;
-        // last crossing in array order: wave max, one LDS atomic per wave
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            const unsigned long long x = __shfl_xor(cross, d);
-            cross = cross > x ? cross : x;
+        const uint32_t wbase = (uint32_t)(t - l) + 1;  // 1 + instance of lane 0
+        const unsigned long long dm = __ballot(deci != 0);
+        if (l == 0 && dm) atomicMax(&S.red[0], wbase + 63u - (uint32_t)__clzll(dm));
+        for (int i = 0; i < nrep; ++i) {
+            const unsigned long long m = __ballot((idmask >> i) & 1u);
+            if (l == 0 && m) atomicMax(&S.red[1 + i], wbase + 63u - (uint32_t)__clzll(m));
         }
-        if (l == 0 && cross) atomicMax(&S.red[0], cross);
     } else {
         // paxos.go:634-673
         ebits |= (touched && st.x == MPX_STATUS_NIL) ? kErrNil : 0u;
@@ -506,7 +508,7 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
             st.w = st.w > nb ? st.w : nb;
         }
         dec = deci != 0;
-        if (__ballot(dec) && l == 0) atomicMax(&S.red[0], 1ull);
+        if (__ballot(dec) && l == 0) atomicMax(&S.red[0], 1u);
     }
     // executeCommands stops at the first nil instance (nil Cmds); CLASSIC's watermark at the first
     // instance that is not COMMITTED: wave minima, one LDS atomic per wave
@@ -533,7 +535,7 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
     if (MPX_ABLATE & 32) {
         cu = (int32_t)ipg - 1;
     } else if (MODE == MPX_MODE_MIN) {
-        if (S.red[0]) cu = (int32_t)(uint32_t)(S.red[0] & 0xffffffffull);
+        if (S.red[0]) cu = (int32_t)S.red[0] - 1;
     } else if (S.red[0] && (int64_t)cu_in + 1 >= 0 && (int64_t)cu_in + 1 < (int64_t)ipg) {
         cu = (int32_t)S.firstbad - 1;  // updateCommittedUpTo over the final statuses
     }
@@ -711,9 +713,9 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
     }
     ebits |= (t == 0 && total > kvpg) ? kErrKvFull : 0u;
     if (t < nrep) {
-        const unsigned long long k = MODE == MPX_MODE_MIN ? S.red[1 + t] : 0ull;
+        const uint32_t k = MODE == MPX_MODE_MIN ? S.red[1 + t] : 0u;
         b.peer_out[(uint64_t)g * nrep + t] =
-            k ? (int32_t)(uint32_t)(k & 0xffffffffull) : b.peer_in[(uint64_t)g * nrep + t];
+            k ? (int32_t)k - 2 : b.peer_in[(uint64_t)g * nrep + t];  // instance - 1
     }
     if (t == 0) {
         b.committed_out[g] = cu;

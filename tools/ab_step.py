@@ -75,7 +75,9 @@ def main():
         tb = tables()
         engines.append((path, lib, h, stream, tb, batch(tb, "0", "1")))
         assert lib.mpx_group_step_dev(h, C.byref(batch(tb, "1", "0")), stream) == 0  # warm-up
-        assert lib.mpx_synchronize(h) == 0
+        rc = lib.mpx_synchronize(h)  # ablation builds may flag errors (their results are wrong)
+        if rc:
+            print(f"{os.path.basename(path)}: warm-up returned {rc}")
     times = {e[0]: [] for e in engines}
     outs = {}
     for r in range(a.rounds):
@@ -86,7 +88,7 @@ def main():
             for _ in range(a.iters):
                 lib.mpx_group_step_dev(h, C.byref(step), s)
             e1.record(ts)
-            assert lib.mpx_synchronize(h) == 0
+            lib.mpx_synchronize(h)
             times[path].append(e0.elapsed_time(e1) / a.iters)
             if r == 0:
                 outs[path] = (d["ret"].sum().item(), d["co"].sum().item(), tb["kv1"].sum().item())
