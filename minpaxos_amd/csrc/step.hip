@@ -9,19 +9,16 @@
 //      executed+1 .. committedUpTo while Cmds != nil, each command through Execute
 //      (state.go:77-103) against the group's table, plus Conflict with the previous command
 //      on the same key (state.go:53-60).
-// The group's table lives in LDS as a dictionary (key, value, present) with an LDS hash
-// index. Commands are bucketed by key (counting sort in LDS) and each command finds its
-// predecessor and the last PUT before it in its key's bucket.
-//
 // Two kernels:
 //   k_group_fast     groups that fit one LDS image (<= 1024 replies, <= 256 instances,
-//                    <= 1024 commands, <= 512 dictionary keys). Every global load of the group
-//                    is issued up front (replies and instance state into LDS, commands and table
-//                    entries into registers), so a workgroup pays one memory round trip; the
-//                    reply image is reused as the dictionary after the tally. Nothing is
-//                    written until the group succeeds; a group that does not fit is appended to
-//                    a work list instead.
-//   k_group_general  the work list: chunked apply of any size, larger instance spaces.
+//                    <= 1024 commands, <= 256 table entries, <= 512 distinct keys). The replies
+//                    and instance state are loaded up front (the reply image goes to LDS), the
+//                    commands while the tally runs; the group's table becomes an LDS hash table
+//                    keyed by the 64-bit key and the commands are resolved by a chunk scan in
+//                    log order (see "fast path" below). Nothing is written until the group is
+//                    known to fit; a group that does not is appended to a work list instead.
+//   k_group_general  the work list: chunked apply of any size, larger instance spaces; its
+//                    dictionary and per-key command buckets live in LDS.
 #include "common.hpp"
 #include "kernels.hpp"
 #include "tally.hpp"
@@ -246,11 +243,12 @@ __device__ __forceinline__ void table_writeback(const Dict& D, uint32_t norig, u
 //            (position+1)<<32 | value keys
 //   table    the group's table and the executed commands' keys share one open-addressing LDS
 //            table keyed by the 64-bit key itself: one 64-bit compare-and-swap per probe finds
-//            the key or claims a free slot for it (no locks, no second lookup), and the slot
-//            index is the key's bucket id
-//   bucket   executed commands are counting-sorted by slot into LDS buckets
-//   resolve  one lane per COMMAND scans its key's bucket: predecessor (Conflict), last PUT before
-//            it (Execute's return value), last PUT of the key (its final value)
+//            the key or claims a free slot for it (no locks, no second lookup)
+//   scan     commands in log order, wave w owning commands [256w, 256w+256) as four chunks of
+//            64: a command's predecessor and last earlier PUT on its key come from the lower
+//            lanes of its chunk (ballot match on the slot), the wave's earlier chunks (a per-wave
+//            slot table) and the earlier waves (their tables); the key's last PUT overall is its
+//            value after the step
 // The group is applied in one chunk, so no per-key state carries between chunks: a key is
 // present at the start iff it is one of the table's entries. Nothing reaches global memory
 // before the group is known to fit; otherwise it goes to k_group_general via the work list
@@ -258,6 +256,7 @@ __device__ __forceinline__ void table_writeback(const Dict& D, uint32_t norig, u
 constexpr int kFRecs = 1024, kFIpg = 256, kFCmds = 1024, kFTab = 256, kFH = 512;
 constexpr int kFPer = kFCmds / kStepBlock;   // commands per thread
 constexpr int kFRecPer = kFRecs / kStepBlock;
+constexpr int kFWaves = kStepBlock / kWave;
 constexpr uint16_t kNone16 = 0xFFFF;
 constexpr uint8_t kIdBad = 31;
 constexpr unsigned long long kFreeKey = 0x8000000000000000ull;  // INT64_MIN marks a free slot
@@ -272,16 +271,15 @@ struct FastLds {
             uint16_t rstart[kFIpg];
             uint16_t rend[kFIpg];
         } a;
-        struct {                 // after the tally: command values and key buckets
+        struct {                 // after the tally: command values and the chunk-scan tables
             int64_t cval[kFCmds];
-            uint16_t list[kFCmds];   // (li << 1) | isPut, contiguous per slot
+            // per wave and slot: (1 + last command) | (1 + last PUT) << 16 seen so far; 0 = none
+            uint32_t tab[kFWaves * kFH];
         } b;
     } u;
     unsigned long long hkey[kFH];  // slot -> key; kFreeKey = free
     int64_t dval[kFTab];     // table entry values at the start of the step
-    uint32_t cnt[kFH + 1];   // executed commands per slot, then (in place) bucket starts
     uint16_t tabidx[kFH];    // table entry holding the slot's key; kNone16 = new to the table
-    uint16_t dlast[kFH];     // 1 + command index of the key's last PUT; 0 = no PUT
     uint32_t newbits[kFCmds / 32];  // first PUTs of new keys, as a bitmap over command index
     uint16_t coff[kFIpg + 2];       // instance -> first command (group-relative)
     uint32_t red[1 + MPX_MAX_REPLICAS];  // 1 + instance: last crossing, last peerCommits[id] source
@@ -368,9 +366,7 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
     // LDS initialisation (regions outside the reply image)
     S.hkey[t] = kFreeKey;
     S.hkey[t + kStepBlock] = kFreeKey;
-    reinterpret_cast<uint2*>(S.cnt)[t] = make_uint2(0u, 0u);
     reinterpret_cast<uint32_t*>(S.tabidx)[t] = 0xFFFFFFFFu;  // kNone16 pairs
-    reinterpret_cast<uint32_t*>(S.dlast)[t] = 0u;
     if (t < kFCmds / 32) S.newbits[t] = 0u;
     S.u.a.rstart[t] = kNone16;
     S.coff[t] = (uint16_t)(own ? co - c_lo : ncmd);
@@ -393,11 +389,14 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
     // are free again, so the two batches of loads are never in flight together). Values follow
     // after the tally. Uniform guard: a group without commands reads nothing.
     const uint32_t clast = ncmd ? ncmd - 1 : 0;
+    // wave w owns commands [256w, 256w + 256) in four chunks of 64: lane l of chunk k holds
+    // command cbase + 64k (the chunk scan below relies on this log order)
+    const uint32_t cbase = (uint32_t)(t - l) * kFPer + (uint32_t)l;
     uint8_t o[kFPer];
     int64_t ck[kFPer];
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) {
-        const uint32_t li = t + k * kStepBlock;
+        const uint32_t li = cbase + k * kWave;
         const uint64_t ci = c_lo + (li < clast ? li : clast);
         o[k] = ncmd ? b.op[ci] : (uint8_t)0;
         ck[k] = ncmd ? b.key[ci] : 0;
@@ -545,21 +544,31 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
     if ((int64_t)S.firstnil < stop && (int64_t)S.firstnil >= lo) stop = S.firstnil;
     const uint32_t x0 = stop > lo ? S.coff[lo] : 0, x1 = stop > lo ? S.coff[stop] : 0;
 
-    // ---- phase 3: slot of every executed command (the reply image is dead: values go there) ---
+    // ---- phase 3: slot of every executed command, then the chunk scan of its wave -------------
+    // In log order a command's predecessors on its key are: the lower lanes of its chunk on the
+    // same slot (a 9-bit ballot match), the wave's earlier chunks (the wave's table, updated by
+    // the last lane of each slot in each chunk) and the earlier waves (their tables, after B4).
+    // Per command this yields the predecessor (state.Conflict) and the last PUT before it
+    // (Execute's GET result); the key's last PUT overall gives its value after the step.
     int64_t cv[kFPer];  // command values, stored to LDS once the lookup has covered their latency
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) {
-        const uint32_t li = t + k * kStepBlock;
+        const uint32_t li = cbase + k * kWave;
         cv[k] = ncmd ? b.val[c_lo + (li < clast ? li : clast)] : 0;
     }
     uint32_t ops = 0;  // the four opcodes, one byte each
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) ops |= (uint32_t)o[k] << (8 * k);
+    const int wv = __builtin_amdgcn_readfirstlane(t / kWave);
+    uint32_t* T = S.u.b.tab + wv * kFH;  // this wave's table (the reply image is dead)
+    reinterpret_cast<uint4*>(T)[l] = make_uint4(0u, 0u, 0u, 0u);
+    reinterpret_cast<uint4*>(T)[l + kWave] = make_uint4(0u, 0u, 0u, 0u);
+    const unsigned long long below = (1ull << l) - 1ull;
     int kid[kFPer];
-    uint32_t pos[kFPer];
+    uint32_t seen[kFPer];  // (1 + predecessor) | (1 + last PUT before) << 16 within the wave
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) {
-        const uint32_t li = t + k * kStepBlock;
+        const uint32_t li = cbase + k * kWave;
         const bool act = li >= x0 && li < x1;
         const unsigned long long key = (unsigned long long)ck[k];
         int kd = -1;
@@ -572,9 +581,41 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
         }
 #endif
         ebits |= (act && kd < 0) ? kOverflow : 0u;  // table full, or the key INT64_MIN
-        kid[k] = act ? kd : -1;
-        pos[k] = (kid[k] >= 0) ? atomicAdd(&S.cnt[kid[k]], 1u) : 0u;
+        const bool live = act && kd >= 0;
+        kid[k] = live ? kd : -1;
+        const uint32_t sl = live ? (uint32_t)kd : 0u;
+        const bool isput = ((ops >> (8 * k)) & 0xffu) == MPX_OP_PUT;
+        const unsigned long long livem = __ballot(live);
+        if (!livem) {  // uniform: no executed command in this chunk
+            seen[k] = 0;
+            continue;
+        }
+        // lanes whose slot differs from this lane's in some bit: per bit, the ballot of the bit
+        // XOR this lane's bit splatted to all 64 positions
+        unsigned long long diff = 0;
+#pragma unroll
+        for (int bb = 0; bb < 9; ++bb) {  // kFH = 512 slots
+            const int32_t sb = (int32_t)(sl << (31 - bb)) >> 31;  // 0 or -1
+            const unsigned long long m = __ballot(sb != 0);
+            diff |= m ^ (unsigned long long)(int64_t)sb;
+        }
+        const unsigned long long peers = livem & ~diff;
+        const unsigned long long putm = __ballot(live && isput);
+        const unsigned long long lp_m = peers & below;
+        const unsigned long long lput_m = lp_m & putm;
+        const uint32_t e = live ? T[sl] : 0u;
+        const uint32_t base1 = li - (uint32_t)l + 1u;  // 1 + command index of the chunk's lane 0
+        const uint32_t pv = lp_m ? base1 + 63u - (uint32_t)__clzll(lp_m) : (e & 0xFFFFu);
+        const uint32_t lp = lput_m ? base1 + 63u - (uint32_t)__clzll(lput_m) : (e >> 16);
+        seen[k] = pv | (lp << 16);
+        if (live && (peers >> l) == 1ull) {  // the chunk's last command on this slot
+            const unsigned long long allput = peers & putm;
+            const uint32_t gl = allput ? base1 + 63u - (uint32_t)__clzll(allput) : (e >> 16);
+            T[sl] = (li + 1u) | (gl << 16);
+        }
     }
+#pragma unroll
+    for (int k = 0; k < kFPer; ++k) S.u.b.cval[cbase + k * kWave] = cv[k];
     if (ebits & kOverflow) atomicOr(&S.flags, 1u);
     __syncthreads();  // B4
     STAMP(3);
@@ -583,93 +624,41 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
         return;
     }
     // the group stays here: the instance outputs can go now (st_out may alias st_in, so not
-    // before this point), which frees their registers for the resolve
+    // before this point)
     if (own) {
         if (!(MPX_ABLATE & 16) && touched) reinterpret_cast<int4*>(b.st_out)[gi0 + t] = st;
         if (b.decided) b.decided[gi0 + t] = dec ? 1 : 0;
     }
-    if (t < kWave) {  // exclusive scan of the bucket sizes, one wave, 8 slots per lane
-        const uint4 c0 = reinterpret_cast<const uint4*>(S.cnt)[2 * l];
-        const uint4 c1 = reinterpret_cast<const uint4*>(S.cnt)[2 * l + 1];
-        const uint32_t v[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-        uint32_t sum = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) sum += v[k];
-        uint32_t incl = sum;
-#pragma unroll
-        for (int d = 1; d < kWave; d <<= 1) {
-            const uint32_t x = __shfl_up(incl, d);
-            if (l >= d) incl += x;
-        }
-        uint32_t run = incl - sum, of[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            of[k] = run;
-            run += v[k];
-        }
-        reinterpret_cast<uint4*>(S.cnt)[2 * l] = make_uint4(of[0], of[1], of[2], of[3]);
-        reinterpret_cast<uint4*>(S.cnt)[2 * l + 1] = make_uint4(of[4], of[5], of[6], of[7]);
-        if (l == kWave - 1) S.cnt[kFH] = run;  // bucket kFH-1 ends here
-    }
-    __syncthreads();  // B5
-#pragma unroll
-    for (int k = 0; k < kFPer; ++k) {
-        const uint32_t li = t + k * kStepBlock;
-        S.u.b.cval[li] = cv[k];
-        if (kid[k] >= 0)
-            S.u.b.list[S.cnt[kid[k]] + pos[k]] =
-                (uint16_t)((li << 1) | (((ops >> (8 * k)) & 0xffu) == MPX_OP_PUT ? 1u : 0u));
-    }
-    __syncthreads();  // B6
     STAMP(4);
 
-    // ---- phase 4: resolve, one lane per command (uniform scans of the key's bucket) -------------
+    // ---- phase 4: resolve: earlier waves, Execute's result, Conflict --------------------------
     uint32_t fnew = 0;  // bit k: command k is the first PUT of a key new to the table
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) {
-        const uint32_t li = t + k * kStepBlock;
+        const uint32_t li = cbase + k * kWave;
         const bool act = kid[k] >= 0;
-        const uint32_t kd = act ? (uint32_t)kid[k] : 0;
-        const uint32_t a = S.cnt[kd];
-        const uint32_t n = act ? S.cnt[kd + 1] - a : 0;
-#if MPX_ABLATE & 4
-        const uint32_t nmax = 0;
-#else
-        const uint32_t nmax = wave_max_u32(n);
-#endif
-        // Entries are e = (lj << 1) | isPut, so "lj < li" is "e < 2li" and the entry with the
-        // largest lj wins a plain max: the predecessor and the last earlier PUT are integer
-        // max-reductions (kept out of boolean lane masks, which the compiler would combine on
-        // the scalar unit). Past the bucket's end the scan reads a sentinel that never matches.
-        const int32_t li2 = (int32_t)(li << 1);
-        int32_t pe = -1, lpe = -1, later_put = 0;
-        for (uint32_t j = 0; j < nmax; ++j) {
-            const uint32_t ix = a + j < (uint32_t)kFCmds - 1 ? a + j : (uint32_t)kFCmds - 1;
-            const int32_t e0 = (int32_t)S.u.b.list[ix];  // unconditional load, then select
-            const int32_t e = j < n ? e0 : 0x7FFFFFFE;
-            const int32_t before = e < li2 ? e : -1;        // earlier command of this key
-            pe = pe > before ? pe : before;
-            const int32_t bput = before | ((before & 1) - 1);  // earlier PUT, else -1
-            lpe = lpe > bput ? lpe : bput;
-            later_put |= e > li2 + 1 ? (e & 1) : 0;         // a later PUT of this key
+        if (!__ballot(act)) continue;  // uniform: nothing executed in this chunk
+        const uint32_t sl = act ? (uint32_t)kid[k] : 0u;
+        uint32_t pv = seen[k] & 0xFFFFu, lp = seen[k] >> 16;
+        for (int w2 = wv - 1; w2 >= 0; --w2) {  // earlier waves, latest first
+            const uint32_t e = S.u.b.tab[w2 * kFH + sl];
+            pv = pv ? pv : (e & 0xFFFFu);
+            lp = lp ? lp : (e >> 16);
         }
-        const int prev = pe >> 1;                // -1 if none (pe = -1 >> 1 = -1)
-        const bool prevput = pe >= 0 && (pe & 1);
-        const int lastput = lpe >> 1;            // -1 if none
-        const bool laterput = later_put != 0;
+        const int prev = (int)pv - 1, lastput = (int)lp - 1;  // -1: none
         const uint32_t op = (ops >> (8 * k)) & 0xffu;
         const bool isput = op == MPX_OP_PUT;
-        const int src = isput ? (int)li : lastput;                // PUT: own value, GET: last PUT
+        const bool prevput = prev >= 0 && prev == lastput;     // the predecessor is a PUT
+        const int src = isput ? (int)li : lastput;              // PUT: own value, GET: last PUT
         const int64_t sv = S.u.b.cval[src >= 0 ? src : 0];
-        const uint32_t ti = S.tabidx[kd];
-        const bool intab = ti != kNone16;                        // present at the start
+        const uint32_t ti = S.tabidx[sl];
+        const bool intab = ti != kNone16;                       // present at the start
         const int64_t at_start = S.dval[intab ? ti : 0];
         const int64_t r = isput ? sv : (op == MPX_OP_GET ? (lastput >= 0 ? sv : (intab ? at_start : 0)) : 0);
         const bool conf = prev >= 0 && (prevput || isput);    // state.Conflict(prev, this)
         if (act) {
             b.ret[c_lo + li] = r;
             if (b.conf_prev) b.conf_prev[c_lo + li] = conf ? 1 : 0;
-            if (isput && !laterput) S.dlast[kd] = (uint16_t)(li + 1);  // value after the step
             if (isput && lastput < 0 && !intab) {  // first PUT of a new key: its append rank
                 fnew |= 1u << k;
                 atomicOr(&S.newbits[li >> 5], 1u << (li & 31));
@@ -680,10 +669,20 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
     STAMP(5);
 
     // ---- phase 5: outputs ----------------------------------------------------------------------
+    // 1 + command index of the last PUT of the key in slot sl (0: none) over all four waves
+    auto last_put = [&](uint32_t sl) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < kFWaves; ++w2) {
+            const uint32_t x = S.u.b.tab[w2 * kFH + sl] >> 16;
+            m = m > x ? m : x;
+        }
+        return m;
+    };
     int64_t* kko = b.kv_key_out + (uint64_t)g * kvpg;
     int64_t* kvo = b.kv_val_out + (uint64_t)g * kvpg;
     if (!(MPX_ABLATE & 16) && (uint32_t)t < kcnt) {  // original entries stay in place
-        const uint32_t dl = S.dlast[tslot];
+        const uint32_t dl = last_put((uint32_t)tslot);
         kko[t] = (int64_t)S.hkey[tslot];
         kvo[t] = dl ? S.u.b.cval[dl - 1] : S.dval[t];
     }
@@ -702,13 +701,13 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
     const uint32_t total = kcnt + n_new;
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) {  // the lane of the key's first PUT appends it
-        const uint32_t li = t + k * kStepBlock;
+        const uint32_t li = cbase + k * kWave;
         const uint32_t base = (uint32_t)__shfl((int)excl, (int)(li >> 5));
         const uint32_t rank = base + __popc(S.newbits[li >> 5] & ((1u << (li & 31)) - 1u));
         if (!(MPX_ABLATE & 16) && ((fnew >> k) & 1u) && kcnt + rank < kvpg) {
             const uint32_t kd = (uint32_t)kid[k];
             kko[kcnt + rank] = (int64_t)S.hkey[kd];
-            kvo[kcnt + rank] = S.u.b.cval[S.dlast[kd] - 1];
+            kvo[kcnt + rank] = S.u.b.cval[last_put(kd) - 1];
         }
     }
     ebits |= (t == 0 && total > kvpg) ? kErrKvFull : 0u;

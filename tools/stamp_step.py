@@ -19,7 +19,7 @@ from minpaxos_amd import _lib, synth  # noqa: E402
 from minpaxos_amd import records as R  # noqa: E402
 from minpaxos_amd.engine import Engine  # noqa: E402
 
-PHASES = ["loads (B1)", "heads+table (B2)", "tally (B3)", "lookup/insert (B4)", "scan+list (B5,B6)",
+PHASES = ["loads (B1)", "heads+table (B2)", "tally (B3)", "lookup+chunk scan (B4)", "instance outputs",
           "resolve (B7)", "outputs"]
 
 
