@@ -261,6 +261,13 @@ constexpr uint16_t kNone16 = 0xFFFF;
 constexpr uint8_t kIdBad = 31;
 constexpr unsigned long long kFreeKey = 0x8000000000000000ull;  // INT64_MIN marks a free slot
 constexpr uint32_t kOverflow = 0x80000000u;                      // ebits: group leaves the fast path
+// chunk-scan state of a slot: a per-wave table entry (16 bits) and a command's view of its
+// predecessors (32 bits) share the two flag bits; the low bits hold 1 + the last PUT (0 = none),
+// relative to the wave's first command in a table entry, absolute in a command's view
+constexpr uint32_t kTabAny = 0x8000u;  // some earlier command used the slot
+constexpr uint32_t kTabPut = 0x4000u;  // ... and the latest of them is a PUT
+constexpr uint32_t kTabLp = 0x07FFu;
+constexpr int kWaveCmds = kFCmds / kFWaves;  // commands per wave (256)
 
 struct FastLds {
     union {
@@ -273,8 +280,14 @@ struct FastLds {
         } a;
         struct {                 // after the tally: command values and the chunk-scan tables
             int64_t cval[kFCmds];
-            // per wave and slot: (1 + last command) | (1 + last PUT) << 16 seen so far; 0 = none
-            uint32_t tab[kFWaves * kFH];
+            // per wave and slot, over the wave's commands seen so far (see kTabAny): whether any
+            // command used the slot, whether the last one was a PUT, 1 + the last PUT relative
+            // to the wave's first command (0 = none)
+            uint16_t tab[kFWaves * kFH];
+            // per wave, the chunk match: slot -> a lane of the chunk on that slot (the class),
+            // class -> mask of the chunk's lanes on the slot
+            uint8_t win[kFWaves * kFH];
+            unsigned long long pmask[kFWaves * kWave];
         } b;
     } u;
     unsigned long long hkey[kFH];  // slot -> key; kFreeKey = free
@@ -284,6 +297,9 @@ struct FastLds {
     uint16_t coff[kFIpg + 2];       // instance -> first command (group-relative)
     uint32_t red[1 + MPX_MAX_REPLICAS];  // 1 + instance: last crossing, last peerCommits[id] source
     uint32_t firstnil, firstbad, flags;
+#ifdef MPX_LDS_PAD
+    uint8_t lds_pad[MPX_LDS_PAD];  // A/B builds only: lowers occupancy to price it
+#endif
 };
 
 // wave-uniform maximum of a per-lane value
@@ -295,6 +311,14 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     }
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
+
+// home slot of a key in the fast path's table: Fibonacci hashing of the folded key (the top
+// log2(kFH) bits of a 32-bit multiplicative hash)
+__device__ __forceinline__ uint32_t fhash(int64_t k) {
+    const uint32_t x = (uint32_t)(uint64_t)k ^ (uint32_t)((uint64_t)k >> 32);
+    return (x * 0x9E3779B1u) >> (32 - 9);
+}
+static_assert(kFH == 512, "fhash returns 9 bits");
 
 // slot of key in the group's table, claiming a free slot if the key is absent (*fresh = 1);
 // -1 when the table is full. Linear probing; the CAS returns the slot's key, so a probe that
@@ -315,9 +339,9 @@ __device__ __forceinline__ int fast_slot(FastLds& S, unsigned long long key, uin
 
 template <int MODE>
 #ifndef MPX_FAST_WAVES_PER_EU
-#define MPX_FAST_WAVES_PER_EU 1
+#define MPX_FAST_WAVES_PER_EU 8
 #endif
-__global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fast(mpx_group_batch b, int32_t nrep,
+__global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(MPX_FAST_WAVES_PER_EU, MPX_FAST_WAVES_PER_EU))) void k_group_fast(mpx_group_batch b, int32_t nrep,
                                                            uint32_t kvpg, uint32_t* worklist,
                                                            uint32_t* wcount, uint32_t* err) {
     __shared__ FastLds S;
@@ -424,7 +448,7 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
     if ((uint32_t)t < kcnt) {
         int fresh = 0;
         const int sl = (unsigned long long)tk == kFreeKey
-                           ? -1 : fast_slot(S, (unsigned long long)tk, lhash(tk), fresh);
+                           ? -1 : fast_slot(S, (unsigned long long)tk, fhash(tk), fresh);
         ebits |= sl < 0 ? kOverflow : 0u;
         tslot = sl < 0 ? 0 : sl;
         if (fresh) S.tabidx[sl] = (uint16_t)t;  // (a duplicate entry of a malformed table
@@ -560,12 +584,20 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) ops |= (uint32_t)o[k] << (8 * k);
     const int wv = __builtin_amdgcn_readfirstlane(t / kWave);
-    uint32_t* T = S.u.b.tab + wv * kFH;  // this wave's table (the reply image is dead)
+    uint16_t* T = S.u.b.tab + wv * kFH;  // this wave's table (the reply image is dead)
+    static_assert(kFH * 2 == kWave * 16, "one 16-byte store per lane clears a wave's table");
     reinterpret_cast<uint4*>(T)[l] = make_uint4(0u, 0u, 0u, 0u);
-    reinterpret_cast<uint4*>(T)[l + kWave] = make_uint4(0u, 0u, 0u, 0u);
-    const unsigned long long below = (1ull << l) - 1ull;
+    // volatile LDS pointers: every access below is a real ds_* instruction, in program order
+    typedef __attribute__((address_space(3))) volatile uint8_t lds_u8;
+    typedef __attribute__((address_space(3))) volatile unsigned long long lds_u64;
+    lds_u8* W = (lds_u8*)(S.u.b.win + wv * kFH);
+    lds_u64* PM = (lds_u64*)(S.u.b.pmask + wv * kWave);
+    PM[l] = 0ull;
+    const unsigned long long lanebit = 1ull << l;
+    const unsigned long long below = lanebit - 1ull;
+    const uint32_t wfirst = (uint32_t)wv * kWaveCmds;  // the wave's first command
     int kid[kFPer];
-    uint32_t seen[kFPer];  // (1 + predecessor) | (1 + last PUT before) << 16 within the wave
+    uint32_t seen[kFPer];  // kTabAny | kTabPut | (1 + last PUT before), within the wave
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) {
         const uint32_t li = cbase + k * kWave;
@@ -573,11 +605,11 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
         const unsigned long long key = (unsigned long long)ck[k];
         int kd = -1;
 #if MPX_ABLATE & 2
-        if (act) kd = (int)(lhash(ck[k]) & (kFH - 1));
+        if (act) kd = (int)fhash(ck[k]);
 #else
         if (act && key != kFreeKey) {
             int fresh = 0;
-            kd = fast_slot(S, key, lhash(ck[k]), fresh);
+            kd = fast_slot(S, key, fhash(ck[k]), fresh);
         }
 #endif
         ebits |= (act && kd < 0) ? kOverflow : 0u;  // table full, or the key INT64_MIN
@@ -590,28 +622,36 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
             seen[k] = 0;
             continue;
         }
-        // lanes whose slot differs from this lane's in some bit: per bit, the ballot of the bit
-        // XOR this lane's bit splatted to all 64 positions
-        unsigned long long diff = 0;
-#pragma unroll
-        for (int bb = 0; bb < 9; ++bb) {  // kFH = 512 slots
-            const int32_t sb = (int32_t)(sl << (31 - bb)) >> 31;  // 0 or -1
-            const unsigned long long m = __ballot(sb != 0);
-            diff |= m ^ (unsigned long long)(int64_t)sb;
+        // the chunk's lanes on this lane's slot, through the wave's LDS scratch (LDS executes a
+        // wave's instructions in order, so each step sees the previous one complete): every lane
+        // writes its id into its slot's byte and one of the ids remains (which one does not
+        // matter: it only names the slot's class within the chunk); every lane ORs its bit into
+        // its class's mask, reads the mask back, and clears it for the next chunk
+        unsigned long long peers = 0;
+        if (live) {
+            W[sl] = (uint8_t)l;
+            const uint32_t cls = W[sl];
+            __hip_atomic_fetch_or((__attribute__((address_space(3))) unsigned long long*)&PM[cls],
+                                  lanebit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            peers = PM[cls];
+            PM[cls] = 0ull;
         }
-        const unsigned long long peers = livem & ~diff;
         const unsigned long long putm = __ballot(live && isput);
         const unsigned long long lp_m = peers & below;
         const unsigned long long lput_m = lp_m & putm;
-        const uint32_t e = live ? T[sl] : 0u;
-        const uint32_t base1 = li - (uint32_t)l + 1u;  // 1 + command index of the chunk's lane 0
-        const uint32_t pv = lp_m ? base1 + 63u - (uint32_t)__clzll(lp_m) : (e & 0xFFFFu);
-        const uint32_t lp = lput_m ? base1 + 63u - (uint32_t)__clzll(lput_m) : (e >> 16);
-        seen[k] = pv | (lp << 16);
+        const uint32_t e = live ? (uint32_t)T[sl] : 0u;
+        const uint32_t rl1 = li - (uint32_t)l + 1u - wfirst;  // 1 + wave-relative lane-0 index
+        const uint32_t elp = e & kTabLp;                        // wave-relative, 0 = none
+        // the predecessor: the highest lower lane on the slot, else the wave's earlier chunks
+        const uint32_t hp = 63u - (uint32_t)__clzll(lp_m | 1ull);
+        const uint32_t pflags = lp_m ? (kTabAny | (((putm >> hp) & 1ull) ? kTabPut : 0u))
+                                     : (e & (kTabAny | kTabPut));
+        const uint32_t lpr = lput_m ? rl1 + 63u - (uint32_t)__clzll(lput_m) : elp;
+        seen[k] = pflags | (lpr ? lpr + wfirst : 0u);
         if (live && (peers >> l) == 1ull) {  // the chunk's last command on this slot
             const unsigned long long allput = peers & putm;
-            const uint32_t gl = allput ? base1 + 63u - (uint32_t)__clzll(allput) : (e >> 16);
-            T[sl] = (li + 1u) | (gl << 16);
+            const uint32_t gl = allput ? rl1 + 63u - (uint32_t)__clzll(allput) : elp;
+            T[sl] = (uint16_t)(kTabAny | (isput ? kTabPut : 0u) | gl);
         }
     }
 #pragma unroll
@@ -639,23 +679,25 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
         const bool act = kid[k] >= 0;
         if (!__ballot(act)) continue;  // uniform: nothing executed in this chunk
         const uint32_t sl = act ? (uint32_t)kid[k] : 0u;
-        uint32_t pv = seen[k] & 0xFFFFu, lp = seen[k] >> 16;
+        uint32_t pf = seen[k] & (kTabAny | kTabPut), lp = seen[k] & kTabLp;
         for (int w2 = wv - 1; w2 >= 0; --w2) {  // earlier waves, latest first
             const uint32_t e = S.u.b.tab[w2 * kFH + sl];
-            pv = pv ? pv : (e & 0xFFFFu);
-            lp = lp ? lp : (e >> 16);
+            const uint32_t elp = e & kTabLp;
+            pf = pf ? pf : (e & (kTabAny | kTabPut));
+            lp = lp ? lp : (elp ? elp + (uint32_t)w2 * kWaveCmds : 0u);
         }
-        const int prev = (int)pv - 1, lastput = (int)lp - 1;  // -1: none
+        const bool hasprev = pf != 0;                           // (kTabAny is set with kTabPut)
+        const int lastput = (int)lp - 1;                        // -1: none
         const uint32_t op = (ops >> (8 * k)) & 0xffu;
         const bool isput = op == MPX_OP_PUT;
-        const bool prevput = prev >= 0 && prev == lastput;     // the predecessor is a PUT
+        const bool prevput = (pf & kTabPut) != 0;              // the predecessor is a PUT
         const int src = isput ? (int)li : lastput;              // PUT: own value, GET: last PUT
         const int64_t sv = S.u.b.cval[src >= 0 ? src : 0];
         const uint32_t ti = S.tabidx[sl];
         const bool intab = ti != kNone16;                       // present at the start
         const int64_t at_start = S.dval[intab ? ti : 0];
         const int64_t r = isput ? sv : (op == MPX_OP_GET ? (lastput >= 0 ? sv : (intab ? at_start : 0)) : 0);
-        const bool conf = prev >= 0 && (prevput || isput);    // state.Conflict(prev, this)
+        const bool conf = hasprev && (prevput || isput);      // state.Conflict(prev, this)
         if (act) {
             b.ret[c_lo + li] = r;
             if (b.conf_prev) b.conf_prev[c_lo + li] = conf ? 1 : 0;
@@ -674,8 +716,8 @@ __global__ __launch_bounds__(kStepBlock, MPX_FAST_WAVES_PER_EU) void k_group_fas
         uint32_t m = 0;
 #pragma unroll
         for (int w2 = 0; w2 < kFWaves; ++w2) {
-            const uint32_t x = S.u.b.tab[w2 * kFH + sl] >> 16;
-            m = m > x ? m : x;
+            const uint32_t x = S.u.b.tab[w2 * kFH + sl] & kTabLp;
+            m = x ? x + (uint32_t)w2 * kWaveCmds : m;
         }
         return m;
     };
