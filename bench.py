@@ -11,6 +11,14 @@ Weak scaling: each rank owns its own 65,536 groups (block-partitioned by global 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--mode min|classic]
   torchrun --nproc-per-node N bench.py --gpus N ...
 
+The other single-GPU configurations of BASELINE.json are kernel benches of their own
+(--workload; the default `step` is the headline line above):
+  tally    config 2: accept tally, 16M instances x 4 replies (k_accept_tally), --mode min|classic
+  prepare  config 3: CLASSIC prepare selection, 16M instances x 4 replies (k_prepare_classic)
+  apply    config 4: batched KV apply, 64M PUT/GET over 1M keys (the mpx_apply pipeline),
+           --dist uniform|zipf
+Each prints one JSON line in the same format, with its own roofline, parity and CPU baseline.
+
 Rank 0 prints ONE JSON line. Inputs are generated on the host (synthetic, counter-based
 splitmix64) and copied to HBM before timing; the timed region contains only device work.
 """
@@ -49,11 +57,18 @@ def parse():
                     help="groups timed on the CPU baseline (0 = auto, ~10-30 s of CPU work)")
     ap.add_argument("--parity-groups", type=int, default=512)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--workload", default="step", choices=["step", "tally", "prepare", "apply"])
+    ap.add_argument("--instances", type=int, default=1 << 24, help="tally / prepare: instances")
+    ap.add_argument("--commands", type=int, default=1 << 26, help="apply: commands")
+    ap.add_argument("--apply-keys", type=int, default=1 << 20, help="apply: key space")
+    ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
     return ap.parse_args()
 
 
 def main():
     a = parse()
+    if a.workload != "step":
+        return kernel_bench(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -313,6 +328,203 @@ def cpu_baseline(b, a, mode, N, K):
                       f"{g_n * ipg * (N - 1)} replies, {g_n * ipg * a.cmds} commands) x {reps} "
                       f"reps, pointer-per-instance log + hash-map State, one thread, "
                       f"{secs:.1f} s timed"}
+
+
+# ============================ single-kernel configurations (2, 3, 4) ============================
+def _timed(stream, eng, steps, warmup, launch, before=None):
+    """warmup + steps launches on the engine stream; HIP events around each launch (the stream
+    the kernels run on); wall clock around the timed loop. Returns (wall_s, [ms per launch])."""
+    import torch
+    for _ in range(warmup):
+        if before:
+            before()
+        launch()
+    eng.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        if before:
+            before()
+        e0.record(stream)
+        launch()
+        e1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    eng.synchronize()
+    return wall, [e0.elapsed_time(e1) for e0, e1 in evs]
+
+
+def kernel_bench(a):
+    """BASELINE.json configs 2-4 on one GPU (replicas only: under torchrun every rank runs its
+    own copy of the workload and `value` sums the ranks)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as OL  # CPU oracle: the checker and the CPU baseline, never the measured path
+    N = 5
+    mode = R.MODE_MIN if a.mode == "min" else R.MODE_CLASSIC
+    eng = Engine(local, n_replicas=N, mode=mode, kv_capacity=2 * a.apply_keys)
+    stream = torch.cuda.ExternalStream(eng.stream, device=dev)
+    torch.cuda.set_stream(stream)
+
+    def dt(x):
+        arr = np.ascontiguousarray(x)
+        if arr.dtype.names:
+            arr = arr.view(np.uint8)
+        return torch.from_numpy(arr).to(dev)
+
+    t_gen = time.time()
+    if a.workload == "tally":
+        I = a.instances
+        recs, st = synth.accept_replies(I, N, 0.7, seed=42)
+        n = len(recs)
+        d_recs, d_st = dt(recs), dt(st)
+        d_out = torch.empty_like(d_st)
+        d_scal = torch.empty(1 + N, dtype=torch.int32, device=dev)
+        scal0 = torch.tensor([-1] + [0] * N, dtype=torch.int32, device=dev)
+        d_dec = torch.empty(I, dtype=torch.uint8, device=dev)
+        t_gen = time.time() - t_gen
+        wall, ms = _timed(stream, eng, a.steps, a.warmup,
+                          lambda: eng.accept_tally_dev(d_recs.data_ptr(), n, d_st.data_ptr(),
+                                                       d_out.data_ptr(), I, 0, d_scal.data_ptr(),
+                                                       d_dec.data_ptr(), eng.stream),
+                          before=lambda: d_scal.copy_(scal0))
+        alg = n * 16 + I * 16 * 2 + I  # replies + state in/out + decided flags
+        units, unit = I, "instances/s"
+        kernel = f"k_accept_tally<{a.mode}>"
+        o = OL.Oracle(N, mode)
+        w_st, w_cu, w_pc, w_dec = o.accept_tally(recs, st, 0, -1)
+        got_st = d_out.cpu().numpy().view(R.INST_STATE)
+        sc = d_scal.cpu().numpy()
+        bit_exact = bool(np.array_equal(got_st.view(np.int32), w_st.view(np.int32))
+                         and sc[0] == w_cu and np.array_equal(sc[1:], w_pc)
+                         and np.array_equal(d_dec.cpu().numpy(), w_dec))
+        parity = {"instances_checked": I, "bit_exact": bit_exact}
+        lib = OL.load()
+        secs, reps = 0.0, 0
+        while secs < 10.0 and reps < 20:
+            s2 = st.copy()
+            cu = C.c_int32(-1)
+            pc = np.zeros(N, np.int32)
+            secs += lib.orc_bench_accept(N, mode, recs.ctypes.data, n, s2.ctypes.data, I, 0,
+                                         C.byref(cu), pc.ctypes.data) * 1e-9
+            reps += 1
+        cpu = {"value": I * reps / secs, "unit": unit, "cores": 1, "kind": "port",
+               "sample": f"the full workload ({I} instances, {n} replies) x {reps}, "
+                         f"pointer-per-instance log, one thread, {secs:.1f} s timed"}
+        workload = f"config2: {I} instances x {N - 1} AcceptReplies, N={N}, p_ok=0.7, mode {a.mode}"
+    elif a.workload == "prepare":
+        I = a.instances
+        recs, st = synth.prepare_replies(I, N, 0.8, seed=43)
+        n = len(recs)
+        d_recs, d_st = dt(recs), dt(st)
+        d_out = torch.empty_like(d_st)
+        d_db = torch.empty(1, dtype=torch.int32, device=dev)
+        db0 = torch.tensor([-1], dtype=torch.int32, device=dev)
+        d_prep = torch.empty(I, dtype=torch.uint8, device=dev)
+        t_gen = time.time() - t_gen
+        wall, ms = _timed(stream, eng, a.steps, a.warmup,
+                          lambda: eng.prepare_select_dev(d_recs.data_ptr(), n, d_st.data_ptr(),
+                                                         d_out.data_ptr(), I, 0, d_db.data_ptr(),
+                                                         d_prep.data_ptr(), eng.stream),
+                          before=lambda: d_db.copy_(db0))
+        alg = n * 16 + I * 32 * 2 + I
+        units, unit = I, "instances/s"
+        kernel = "k_prepare_classic"
+        o = OL.Oracle(N, R.MODE_CLASSIC)
+        t0 = time.perf_counter()
+        w_st, w_db, w_prep = o.prepare_select(recs, st, 0, -1)
+        t_orc = time.perf_counter() - t0
+        got = d_out.cpu().numpy().view(R.PREP_STATE)
+        bit_exact = bool(np.array_equal(got.view(np.int32), w_st.view(np.int32))
+                         and int(d_db.item()) == w_db
+                         and np.array_equal(d_prep.cpu().numpy(), w_prep))
+        parity = {"instances_checked": I, "bit_exact": bit_exact}
+        reps, secs = 1, t_orc
+        while secs < 10.0 and reps < 20:
+            t0 = time.perf_counter()
+            o.prepare_select(recs, st, 0, -1)
+            secs += time.perf_counter() - t0
+            reps += 1
+        cpu = {"value": I * reps / secs, "unit": unit, "cores": 1, "kind": "port",
+               "sample": f"the full workload ({I} instances, {n} replies) x {reps} through the "
+                         f"oracle's sequential handler loop (incl. its numpy copy-in/out), "
+                         f"one thread, {secs:.1f} s timed"}
+        workload = f"config3: {I} instances x {N - 1} PrepareReplies, N={N}, p_ok=0.8, random ballots"
+    else:
+        M, K = a.commands, a.apply_keys
+        op, key, val = synth.commands(M, K, 0.5, a.dist, seed=44)
+        d_op, d_key, d_val = dt(op), dt(key), dt(val)
+        d_ret = torch.empty(M, dtype=torch.int64, device=dev)
+        d_conf = torch.empty(M, dtype=torch.uint8, device=dev)
+        t_gen = time.time() - t_gen
+        launch = lambda: eng.apply_dev(d_op.data_ptr(), d_key.data_ptr(), d_val.data_ptr(), M,  # noqa: E731
+                                       d_ret.data_ptr(), d_conf.data_ptr(), eng.stream)
+        eng.apply_reserve(M)
+        launch()  # the table holds every key from here on: every timed call does the same work
+        eng.synchronize()
+        wall, ms = _timed(stream, eng, a.steps, a.warmup, launch)
+        n_keys = eng.kv_size()
+        alg = M * (17 + 9) + n_keys * 16 * 2  # commands in, ret+conf out, table read + written
+        units, unit = M, "commands/s"
+        kernel = "mpx_apply pipeline (insert, lookup, radix sort, mark, scan, finish, commit)"
+        o = OL.Oracle(N, mode)
+        o.apply(op, key, val)
+        w_ret, w_conf = o.apply(op, key, val)
+        wk, wv = o.kv_export()
+        order = np.argsort(wk, kind="stable")
+        gk, gv = eng.kv_export()
+        bit_exact = bool(np.array_equal(d_ret.cpu().numpy(), w_ret)
+                         and np.array_equal(d_conf.cpu().numpy(), w_conf)
+                         and np.array_equal(gk, wk[order]) and np.array_equal(gv, wv[order]))
+        parity = {"commands_checked": M, "bit_exact": bit_exact}
+        lib = OL.load()
+        ret = np.zeros(M, np.int64)
+        k0, v0 = np.ascontiguousarray(wk), np.ascontiguousarray(wv)
+        secs, reps = 0.0, 0
+        while secs < 10.0 and reps < 20:
+            secs += lib.orc_bench_apply(k0.ctypes.data, v0.ctypes.data, len(k0), op.ctypes.data,
+                                        key.ctypes.data, val.ctypes.data, M, ret.ctypes.data) * 1e-9
+            reps += 1
+        cpu = {"value": M * reps / secs, "unit": unit, "cores": 1, "kind": "port",
+               "sample": f"the full workload ({M} commands over {K} keys, {a.dist}) x {reps}, "
+                         f"Execute per command on an unordered_map, one thread, {secs:.1f} s timed"}
+        workload = f"config4: {M} PUT/GET (p_put=0.5) over {K} keys, {a.dist}"
+    if world > 1:
+        tt = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall = float(tt.item())
+    kern_avg = float(np.mean(ms))
+    achieved = alg / (kern_avg * 1e-3) / 1e9
+    if rank == 0:
+        line = {
+            "metric": f"{a.workload} throughput ({unit})", "value": units * a.steps * world / wall,
+            "unit": unit, "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": wall / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int32/int64", "data": "synthetic (splitmix64)",
+            "config": {"workload": workload, "parallelism": f"replicas x{world}"},
+            "roofline": {"bound": "hbm", "kernel": kernel, "achieved": achieved,
+                         "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+                         "traffic": None, "alg_bytes_per_launch": alg, "kernel_ms_avg": kern_avg,
+                         "kernel_ms_min": float(np.min(ms))},
+            "gen_s": round(t_gen, 2), "parity": parity,
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            line["cpu_baseline"] = cpu
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -233,6 +233,9 @@ int mpx_prepare_select_min_dev(mpx_engine* eng, const mpx_prepare_reply_min* d_r
  * on the same key in this call, command i), 0 if there is none.                            */
 int mpx_apply(mpx_engine* eng, const uint8_t* op, const int64_t* key, const int64_t* val,
               size_t m, int64_t* ret, uint8_t* conf_prev);
+/* allocate the KV table and the apply workspace for calls of up to max_cmds commands, so
+ * that mpx_apply_dev (which never allocates) can run; idempotent, grows only               */
+int mpx_apply_reserve(mpx_engine* eng, size_t max_cmds);
 int mpx_apply_dev(mpx_engine* eng, const uint8_t* d_op, const int64_t* d_key,
                   const int64_t* d_val, size_t m, int64_t* d_ret, uint8_t* d_conf_prev,
                   void* stream);

@@ -45,6 +45,7 @@ SIGNATURES = {
     "mpx_prepare_select_min": (C.c_int, [_p, _p, _sz, _p, _p, _sz, _p, _p]),
     "mpx_prepare_select_min_dev": (C.c_int, [_p, _p, _sz, _p, _p, _sz, _p, _p, _p]),
     "mpx_apply": (C.c_int, [_p, _p, _p, _p, _sz, _p, _p]),
+    "mpx_apply_reserve": (C.c_int, [_p, _sz]),
     "mpx_apply_dev": (C.c_int, [_p, _p, _p, _p, _sz, _p, _p, _p]),
     "mpx_kv_size": (C.c_int, [_p, C.POINTER(_sz)]),
     "mpx_kv_export": (C.c_int, [_p, _p, _p, _sz, C.POINTER(_sz)]),

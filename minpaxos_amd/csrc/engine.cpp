@@ -30,6 +30,7 @@ struct mpx_engine {
     std::string err;
     uint32_t* d_err = nullptr;
     unsigned long long* d_red = nullptr;
+    uint32_t* d_part = nullptr;  // tile kernels' per-workgroup partials
     // host-API staging
     DevBuf b[12];
     // global KV table (mpx_apply)
@@ -190,6 +191,8 @@ int mpx_open(int device, const mpx_config* cfg, mpx_engine** out) {
         hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&e->d_err, sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&e->d_red, mpx::kRedWords * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&e->d_part, (size_t)mpx::kTileGrid * mpx::kPartStride * sizeof(uint32_t)) !=
+            hipSuccess ||
         hipMalloc(&e->d_wcount, sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&e->worklist.p, e->worklist.cap) != hipSuccess ||
         hipMemset(e->d_err, 0, sizeof(uint32_t)) != hipSuccess) {
@@ -219,6 +222,7 @@ int mpx_close(mpx_engine* e) {
     }
     if (e->d_err) (void)hipFree(e->d_err);
     if (e->d_red) (void)hipFree(e->d_red);
+    if (e->d_part) (void)hipFree(e->d_part);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return MPX_OK;
@@ -260,7 +264,8 @@ int mpx_accept_tally(mpx_engine* e, const mpx_accept_reply* recs, size_t n, mpx_
     HIPCHK(e, mpx::launch_accept_tally(e->cfg.mode, (const mpx_accept_reply*)e->b[0].p, n,
                                        (const mpx_inst_state*)e->b[1].p,
                                        (mpx_inst_state*)e->b[1].p, n_inst, inst_base, N,
-                                       (int32_t*)e->b[3].p, d_dec, e->d_red, e->d_err, e->stream));
+                                       (int32_t*)e->b[3].p, d_dec, e->d_red, e->d_part,
+                                       e->d_err, e->stream));
     CK(d2h(e, st, e->b[1].p, n_inst * sizeof(mpx_inst_state)));
     CK(d2h(e, sc, e->b[3].p, (1 + N) * sizeof(int32_t)));
     if (decided_out) CK(d2h(e, decided_out, d_dec, n_inst));
@@ -282,7 +287,7 @@ int mpx_accept_tally_dev(mpx_engine* e, const mpx_accept_reply* d_recs, size_t n
     if (n >= 0xFFFFFFFFull) return fail(e, MPX_E_UNSUPPORTED, "more than 2^32-2 records");
     HIPCHK(e, mpx::launch_accept_tally(e->cfg.mode, d_recs, n, d_st_in, d_st_out, n_inst,
                                        inst_base, e->cfg.n_replicas, d_scalars, d_decided,
-                                       e->d_red, e->d_err, pick(e, stream)));
+                                       e->d_red, e->d_part, e->d_err, pick(e, stream)));
     return MPX_OK;
 }
 
@@ -321,7 +326,7 @@ int mpx_prepare_select(mpx_engine* e, const mpx_prepare_reply* recs, size_t n, m
                                           (const mpx_prep_state*)e->b[1].p,
                                           (mpx_prep_state*)e->b[1].p, n_inst, inst_base,
                                           e->cfg.n_replicas, (int32_t*)e->b[3].p, d_prep,
-                                          e->d_err, e->stream));
+                                          e->d_part, e->d_err, e->stream));
     CK(d2h(e, st, e->b[1].p, n_inst * sizeof(mpx_prep_state)));
     CK(d2h(e, default_ballot, e->b[3].p, sizeof(int32_t)));
     if (prepared_out) CK(d2h(e, prepared_out, d_prep, n_inst));
@@ -337,7 +342,7 @@ int mpx_prepare_select_dev(mpx_engine* e, const mpx_prepare_reply* d_recs, size_
         return fail(e, MPX_E_INVAL, "null argument");
     HIPCHK(e, mpx::launch_prepare_classic(d_recs, n, d_st_in, d_st_out, n_inst, inst_base,
                                           e->cfg.n_replicas, d_default_ballot, d_prepared,
-                                          e->d_err, pick(e, stream)));
+                                          e->d_part, e->d_err, pick(e, stream)));
     return MPX_OK;
 }
 
@@ -415,6 +420,15 @@ int mpx_apply(mpx_engine* e, const uint8_t* op, const int64_t* key, const int64_
     return finish(e);
 }
 
+int mpx_apply_reserve(mpx_engine* e, size_t max_cmds) {
+    if (!e) return MPX_E_INVAL;
+    if (max_cmds >= (1ull << 31)) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 commands");
+    CK(begin(e));
+    CK(ensure_kv(e));
+    GROW(e, e->apply_work, mpx::apply_work_bytes(max_cmds));
+    return finish(e);
+}
+
 int mpx_apply_dev(mpx_engine* e, const uint8_t* d_op, const int64_t* d_key, const int64_t* d_val,
                   size_t m, int64_t* d_ret, uint8_t* d_conf_prev, void* stream) {
     if (!e) return MPX_E_INVAL;
@@ -422,8 +436,8 @@ int mpx_apply_dev(mpx_engine* e, const uint8_t* d_op, const int64_t* d_key, cons
     if (m >= (1ull << 31)) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 commands per call");
     if (!e->kv_ready || e->apply_work.cap < mpx::apply_work_bytes(m))
         return fail(e, MPX_E_INVAL,
-                    "mpx_apply_dev: call mpx_kv_clear and one host mpx_apply of >= m commands "
-                    "first (the dev entry point never allocates)");
+                    "mpx_apply_dev: call mpx_apply_reserve(m) first (the dev entry point never "
+                    "allocates)");
     mpx::ApplyWork w{e->apply_work.p, e->apply_work.cap};
     HIPCHK(e, mpx::launch_apply(e->kv, d_op, d_key, d_val, m, d_ret, d_conf_prev, w, e->d_err,
                                 pick(e, stream)));

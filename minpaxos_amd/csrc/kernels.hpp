@@ -18,12 +18,16 @@ constexpr uint32_t kErrInval = 16u;  // other malformed input (offsets, sizes)
 
 // reduction scratch: kRedWords u64 per engine
 constexpr int kRedWords = 64;
+// per-workgroup partials of the tile kernels (tile.hpp): at most kTileGrid workgroups, each
+// writing kPartStride u32
+constexpr int kTileGrid = 2048;
+constexpr int kPartStride = 32;
 
 hipError_t launch_accept_tally(int mode, const mpx_accept_reply* recs, uint64_t n,
                                const mpx_inst_state* st_in, mpx_inst_state* st_out,
                                uint64_t n_inst, int32_t base, int32_t nrep, int32_t* scalars,
-                               uint8_t* decided, unsigned long long* red, uint32_t* err,
-                               hipStream_t stream);
+                               uint8_t* decided, unsigned long long* red, uint32_t* part,
+                               uint32_t* err, hipStream_t stream);
 
 hipError_t launch_committed_prefix(const mpx_inst_state* st, uint64_t n_inst, int32_t base,
                                    int32_t* scalars, unsigned long long* red, hipStream_t stream);
@@ -31,8 +35,8 @@ hipError_t launch_committed_prefix(const mpx_inst_state* st, uint64_t n_inst, in
 hipError_t launch_prepare_classic(const mpx_prepare_reply* recs, uint64_t n,
                                   const mpx_prep_state* st_in, mpx_prep_state* st_out,
                                   uint64_t n_inst, int32_t base, int32_t nrep,
-                                  int32_t* default_ballot, uint8_t* prepared, uint32_t* err,
-                                  hipStream_t stream);
+                                  int32_t* default_ballot, uint8_t* prepared, uint32_t* part,
+                                  uint32_t* err, hipStream_t stream);
 
 hipError_t launch_prepare_min(const mpx_prepare_reply_min* recs, uint64_t n,
                               const uint64_t* grp_rec_off, mpx_group_prep_state* gst,

@@ -338,10 +338,7 @@ __device__ __forceinline__ int fast_slot(FastLds& S, unsigned long long key, uin
 }
 
 template <int MODE>
-#ifndef MPX_FAST_WAVES_PER_EU
-#define MPX_FAST_WAVES_PER_EU 8
-#endif
-__global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(MPX_FAST_WAVES_PER_EU, MPX_FAST_WAVES_PER_EU))) void k_group_fast(mpx_group_batch b, int32_t nrep,
+__global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, int32_t nrep,
                                                            uint32_t kvpg, uint32_t* worklist,
                                                            uint32_t* wcount, uint32_t* err) {
     __shared__ FastLds S;

@@ -1,38 +1,135 @@
 // tally.hip — accept tally kernels for one instance log (configs 2 and the single-group API).
 #include "kernels.hpp"
 #include "tally.hpp"
+#include "tile.hpp"
 
 namespace mpx {
 
-// One wave per tile of kTallyTile records; tiles are shifted to instance boundaries so an
-// instance is always tallied by exactly one wave.
-constexpr uint64_t kTallyTile = 512;
-constexpr int kTallyBlock = 256;
-
-// red layout (u64): [0] MIN last-crossing key | CLASSIC any-decided flag
-//                   [1..N] MIN peer-commit keys ; [17] CLASSIC first non-committed index
+// Accept tally of one instance log: tile_walk (tile.hpp) hands every lane one instance and its
+// replies in arrival order; the lane applies handleAcceptReply to each (state in registers).
+//   MIN      bareminpaxos.go:1023-1053: OK replies only, no status check
+//   CLASSIC  paxos.go:634-673: replies to instances not PREPARED/ACCEPTED are ignored
+// The "last assignment wins" scalars of MIN (committedUpTo :1048, peerCommits[id] :1050) come
+// from the highest instance that assigns them (instances ascend in array order; all of an
+// instance's assignments of one scalar write the same value): per round a wave ballot finds the
+// highest lane, one LDS max per wave, one partial per workgroup, a final one-block reduction.
+// Window-relative keys idx+1 (0 = none) keep them unsigned.
 constexpr int kRedFirstBad = 1 + MPX_MAX_REPLICAS;
 
 template <int MODE>
-__global__ __launch_bounds__(kTallyBlock) void k_accept_tally(
+__global__ __launch_bounds__(kTileBlock) void k_accept_tile(
     const mpx_accept_reply* __restrict__ recs, uint64_t n, const mpx_inst_state* __restrict__ st_in,
     mpx_inst_state* __restrict__ st_out, uint64_t n_inst, int32_t base, int32_t half, int32_t nrep,
-    unsigned long long* __restrict__ red, uint8_t* __restrict__ decided, uint32_t* err) {
-    const uint64_t wave = ((uint64_t)blockIdx.x * kTallyBlock + threadIdx.x) / kWave;
-    const uint64_t s0 = wave * kTallyTile;
-    if (s0 >= n) return;
-    const uint64_t e0 = s0 + kTallyTile;
-    const uint64_t s = find_head(recs, s0, 0, n);
-    const uint64_t e = e0 >= n ? n : find_head(recs, e0, 0, n);
-    if (s >= e) return;
-    TallyOut out{0, 0, false};
-    tally_range<MODE>(recs, s, e, st_in, st_out, n_inst, base, half, nrep, decided, err, 0, out);
-    const int l = lane_id();
-    if (MODE == MPX_MODE_MIN) {
-        if (l == 0 && out.cu_key) atomicMax(&red[0], (unsigned long long)out.cu_key);
-        if (l < nrep && out.pc_key) atomicMax(&red[1 + l], (unsigned long long)out.pc_key);
-    } else {
-        if (l == 0 && out.any_dec) atomicMax(&red[0], 1ull);
+    uint32_t* __restrict__ part, uint8_t* __restrict__ decided, uint32_t* err) {
+    __shared__ TileLds S;
+    __shared__ uint32_t red[1 + MPX_MAX_REPLICAS];
+    const int t = threadIdx.x, l = lane_id();
+    if (t <= MPX_MAX_REPLICAS) red[t] = 0;
+    uint32_t ebits = 0;
+    const int4* r4 = reinterpret_cast<const int4*>(recs);
+    tile_walk(S, r4, n, err, [&](uint32_t a, uint32_t cnt, uint64_t after, uint64_t oend, bool own) {
+        const int32_t inst = own ? S.rec[a].x : 0;
+        const int64_t idx = (int64_t)inst - base;
+        const bool inwin = own && idx >= 0 && (uint64_t)idx < n_inst;
+        int4 st = inwin ? reinterpret_cast<const int4*>(st_in)[idx]
+                        : make_int4(MPX_STATUS_NIL, 0, 0, 0);
+        const bool nil = st.x == MPX_STATUS_NIL;
+        ebits |= (own && !inwin) ? kErrNil : 0u;  // outside instanceSpace
+        if (MODE == MPX_MODE_CLASSIC) ebits |= (own && nil) ? kErrNil : 0u;  // paxos.go:634
+        uint32_t idmask = 0;
+        int32_t deci = 0;
+        auto step = [&](int4 r, int32_t act) {  // act: 0/1, the record takes part
+            const int32_t okj = (r.w & 0xff) == 1 ? act : 0;  // OK == TRUE
+            if (MODE == MPX_MODE_MIN) {
+                ebits |= (okj && nil) ? kErrNil : 0u;  // inst.Lb of a nil instance (:1024)
+                const int32_t oks = st.y + okj;       // AcceptOKs++
+                const int32_t c1 = oks >= half ? okj : 0;   // AcceptOKs+1 > N>>1
+                const int32_t dj = oks == half ? c1 : 0;    // AcceptOKs == N>>1: COMMITTED
+                st.y = oks;
+                st.x = dj ? MPX_COMMITTED : st.x;
+                deci |= dj;
+                const bool badid = r.z < 0 || r.z >= nrep;
+                ebits |= (c1 && badid) ? kErrBadId : 0u;
+                idmask |= (c1 && !badid) ? (1u << r.z) : 0u;
+            } else {
+                const int32_t live = (uint32_t)(st.x - MPX_PREPARED) < 2u ? act : 0;
+                const int32_t okl = live & okj, nk = live & (okj ^ act);
+                const int32_t oks = st.y + okl;
+                const int32_t c = oks >= half ? okl : 0;  // acceptOKs+1 > N>>1
+                st.y = oks;
+                st.x = c ? MPX_COMMITTED : st.x;
+                deci |= c;
+                st.z += nk;
+                const int32_t nb = nk ? r.y : INT32_MIN;
+                st.w = st.w > nb ? st.w : nb;
+            }
+        };
+        // the tile part: uniform trip count (wave maximum), predicated body
+        uint32_t rmax = cnt;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t x = (uint32_t)__shfl_xor((int)rmax, d);
+            rmax = rmax > x ? rmax : x;
+        }
+        rmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)rmax);
+        for (uint32_t j = 0; j < rmax; ++j) {
+            const int4 r = S.rec[j < cnt ? a + j : 0];
+            step(r, (j < cnt && inwin) ? 1 : 0);
+        }
+        // the overhang of the tile's last instance (one lane per tile)
+        for (uint64_t q = after; inwin && q < oend; ++q) step(r4[q], 1);
+        if (inwin) {
+            reinterpret_cast<int4*>(st_out)[idx] = st;
+            if (decided) decided[idx] = deci ? 1 : 0;
+        }
+        const uint32_t key = (uint32_t)(idx + 1);
+        if (MODE == MPX_MODE_MIN) {
+            const unsigned long long dm = __ballot(inwin && deci);
+            if (dm) {
+                const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)key, 63 - __clzll(dm));
+                if (l == 0) atomicMax(&red[0], k);
+            }
+            for (int i = 0; i < nrep; ++i) {
+                const unsigned long long m = __ballot(inwin && ((idmask >> i) & 1u));
+                if (m) {
+                    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)key, 63 - __clzll(m));
+                    if (l == 0) atomicMax(&red[1 + i], k);
+                }
+            }
+        } else {
+            if (__ballot(inwin && deci) && l == 0) atomicMax(&red[0], 1u);
+        }
+    });
+    __syncthreads();
+    if (t <= nrep) part[(uint64_t)blockIdx.x * kPartStride + t] = red[t];
+    if (ebits) raise_err(err, ebits);
+}
+
+// reduce the workgroups' partials; MIN: write committedUpTo / peerCommits; CLASSIC: set red[0]
+// (some instance committed) and red[kRedFirstBad] for k_classic_first_bad
+template <int MODE>
+__global__ void k_accept_reduce(const uint32_t* __restrict__ part, uint32_t n_part, int32_t nrep,
+                                int32_t base, uint64_t n_inst, int32_t* scalars,
+                                unsigned long long* red) {
+    const int l = lane_id();  // each wave takes every (blockDim/64)-th scalar
+    for (int w = threadIdx.x / kWave; w <= nrep; w += blockDim.x / kWave) {
+        uint32_t m = 0;
+        for (uint32_t i = l; i < n_part; i += kWave) {
+            const uint32_t x = part[(uint64_t)i * kPartStride + w];
+            m = m > x ? m : x;
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t x = (uint32_t)__shfl_xor((int)m, d);
+            m = m > x ? m : x;
+        }
+        if (l != 0) continue;
+        if (MODE == MPX_MODE_MIN) {
+            if (m) scalars[w] = (int32_t)((int64_t)base + m - 1 - (w ? 1 : 0));  // peerCommits: inst-1
+        } else if (w == 0) {
+            red[0] = m;
+            red[kRedFirstBad] = n_inst;
+        }
     }
 }
 
@@ -82,24 +179,23 @@ __global__ void k_tally_finalize(const unsigned long long* __restrict__ red, int
 hipError_t launch_accept_tally(int mode, const mpx_accept_reply* recs, uint64_t n,
                                const mpx_inst_state* st_in, mpx_inst_state* st_out,
                                uint64_t n_inst, int32_t base, int32_t nrep, int32_t* scalars,
-                               uint8_t* decided, unsigned long long* red, uint32_t* err,
-                               hipStream_t stream) {
+                               uint8_t* decided, unsigned long long* red, uint32_t* part,
+                               uint32_t* err, hipStream_t stream) {
     const int32_t half = nrep >> 1;
-    k_tally_init<<<1, 64, 0, stream>>>(red, n_inst);
     if (decided && n_inst) (void)hipMemsetAsync(decided, 0, n_inst, stream);
-    if (n) {
-        const uint64_t waves = (n + kTallyTile - 1) / kTallyTile;
-        const uint64_t blocks = (waves * kWave + kTallyBlock - 1) / kTallyBlock;
-        if (mode == MPX_MODE_MIN)
-            k_accept_tally<MPX_MODE_MIN><<<dim3((unsigned)blocks), kTallyBlock, 0, stream>>>(
-                recs, n, st_in, st_out, n_inst, base, half, nrep, red, decided, err);
-        else
-            k_accept_tally<MPX_MODE_CLASSIC><<<dim3((unsigned)blocks), kTallyBlock, 0, stream>>>(
-                recs, n, st_in, st_out, n_inst, base, half, nrep, red, decided, err);
-    }
+    const uint64_t tiles = (n + kTileRecs - 1) / kTileRecs;
+    const uint32_t grid = (uint32_t)(tiles < (uint64_t)kTileGrid ? (tiles ? tiles : 1) : kTileGrid);
+    const unsigned rblock = (unsigned)(kWave * (1 + nrep) < 256 ? kWave * (1 + nrep) : 256);
     if (mode == MPX_MODE_MIN) {
-        k_tally_finalize<MPX_MODE_MIN><<<1, 64, 0, stream>>>(red, scalars, nrep, n_inst, base);
+        k_accept_tile<MPX_MODE_MIN><<<grid, kTileBlock, 0, stream>>>(
+            recs, n, st_in, st_out, n_inst, base, half, nrep, part, decided, err);
+        k_accept_reduce<MPX_MODE_MIN><<<1, rblock, 0, stream>>>(part, grid, nrep, base, n_inst,
+                                                                scalars, red);
     } else {
+        k_accept_tile<MPX_MODE_CLASSIC><<<grid, kTileBlock, 0, stream>>>(
+            recs, n, st_in, st_out, n_inst, base, half, nrep, part, decided, err);
+        k_accept_reduce<MPX_MODE_CLASSIC><<<1, kWave, 0, stream>>>(part, grid, 0, base, n_inst,
+                                                                   scalars, red);
         if (n_inst) {
             uint64_t blocks = (n_inst + 255) / 256;
             if (blocks > 2048) blocks = 2048;

@@ -1,0 +1,142 @@
+// tile.hpp — lane-per-instance processing of one instance log's reply records (configs 2 and 3).
+//
+// The records of a call (16 B each, instance number first) are grouped by instance in ascending
+// order with arbitrary (ragged) fan-in. A 256-thread workgroup walks tiles of kTileRecs records
+// (grid-stride, the next tile's records prefetched into registers while the current one is
+// processed):
+//   1. the tile goes to LDS with coalesced 16-byte loads;
+//   2. head flags (first record of an instance) are compacted into the tile's list of OWNED
+//      instances: those whose first record lies in the tile. Records at the start of a tile that
+//      continue an instance of the previous tile belong to that tile's last instance, which
+//      reads them (the "overhang") straight from global memory;
+//   3. one lane per owned instance applies the reference handler to the instance's records in
+//      arrival order, with the instance state in registers (the caller's `body`).
+// A call's record array therefore needs no instance-boundary search and every record is read
+// once from HBM (overhangs aside, which are at most the rest of one instance per tile).
+#pragma once
+#include "common.hpp"
+
+namespace mpx {
+
+constexpr int kTileRecs = 1024;
+constexpr int kTileBlock = 256;
+constexpr int kTilePer = kTileRecs / kTileBlock;
+constexpr int kTileWaves = kTileBlock / kWave;
+
+struct TileLds {
+    int4 rec[kTileRecs];                 // the tile's records
+    uint16_t hpos[kTileRecs + 1];        // positions of the owned instances' first records
+    uint32_t wcnt[kTilePer * kTileWaves];  // heads per (register k, wave), then their offsets
+    uint32_t nh;                         // owned instances in the tile
+    uint64_t oend;                       // end of the last owned instance's overhang
+};
+
+__device__ __forceinline__ int4 tile_load(const int4* __restrict__ recs, uint64_t n, uint64_t p) {
+    return p < n ? recs[p] : make_int4(0, 0, 0, 0);
+}
+
+// Runs body(pos_first, count, overhang_end, t_round) for every owned instance of every tile this
+// workgroup takes. Records of the instance are S.rec[pos_first .. pos_first+count) followed, for
+// the tile's last instance, by global records [tile_end, overhang_end). Every lane of the
+// workgroup calls `body` the same number of times per tile (rounds of 256 instances; lanes
+// without an instance in a round get count = 0), so `body` may use wave-level ballots.
+// `err` receives kErrOrder when instances are not ascending.
+template <typename Body>
+__device__ __forceinline__ void tile_walk(TileLds& S, const int4* __restrict__ recs, uint64_t n,
+                                          uint32_t* err, Body&& body) {
+    const int t = threadIdx.x, l = lane_id(), w = t / kWave;
+    const uint64_t n_tiles = (n + kTileRecs - 1) / kTileRecs;
+    const unsigned long long below = (1ull << l) - 1ull;
+    uint64_t T = blockIdx.x;
+    int4 cur[kTilePer];
+#pragma unroll
+    for (int k = 0; k < kTilePer; ++k)
+        cur[k] = tile_load(recs, n, T * kTileRecs + t + k * kTileBlock);
+    uint32_t ebits = 0;
+    for (; T < n_tiles; T += gridDim.x) {
+        const uint64_t p0 = T * kTileRecs;
+        const uint32_t cnt = (uint32_t)((n - p0) < (uint64_t)kTileRecs ? (n - p0) : kTileRecs);
+        // neighbours of the tile: the record before it and the one after it
+        const int32_t prev_inst = p0 ? recs[p0 - 1].x : 0;
+        const uint64_t after = p0 + cnt;
+        const int32_t after_inst = after < n ? recs[after].x : 0;
+#pragma unroll
+        for (int k = 0; k < kTilePer; ++k) S.rec[t + k * kTileBlock] = cur[k];
+        // the next tile of this workgroup: issued now, consumed after this tile's barriers
+        const uint64_t Tn = T + gridDim.x;
+#pragma unroll
+        for (int k = 0; k < kTilePer; ++k)
+            cur[k] = Tn < n_tiles ? tile_load(recs, n, Tn * kTileRecs + t + k * kTileBlock)
+                                  : make_int4(0, 0, 0, 0);
+        __syncthreads();
+        bool head[kTilePer];
+#pragma unroll
+        for (int k = 0; k < kTilePer; ++k) {
+            const uint32_t p = t + k * kTileBlock;
+            const bool valid = p < cnt;
+            const int32_t inst = S.rec[p].x;
+            const int32_t prev = p ? S.rec[p - 1].x : prev_inst;
+            const bool first = p0 + p == 0;
+            head[k] = valid && (first || inst != prev);
+            ebits |= (head[k] && !first && inst < prev) ? kErrOrder : 0u;
+            const unsigned long long hm = __ballot(head[k]);
+            if (l == 0) S.wcnt[k * kTileWaves + w] = (uint32_t)__popcll(hm);
+        }
+        __syncthreads();
+        uint32_t base[kTilePer];
+        {
+            // exclusive offsets of (k, w) in record order (p = 256k + 64w + l)
+            uint32_t run = 0, tot = 0;
+#pragma unroll
+            for (int k = 0; k < kTilePer; ++k)
+#pragma unroll
+                for (int w2 = 0; w2 < kTileWaves; ++w2) {
+                    const uint32_t c = S.wcnt[k * kTileWaves + w2];
+                    if (w2 == w) base[k] = run;
+                    run += c;
+                    tot += c;
+                }
+            if (t == 0) S.nh = tot;
+        }
+        // the tile's last record continues into the next tile: wave 0 finds where its
+        // instance ends, 64 records per step
+        if (w == 0) {
+            uint64_t oend = after;
+            if (after < n && cnt && after_inst == S.rec[cnt - 1].x) {
+                const int32_t inst = after_inst;
+                for (uint64_t q = after + 1;; q += kWave) {
+                    const uint64_t p = q + l;
+                    const bool stop = p >= n || recs[p].x != inst;
+                    const unsigned long long m = __ballot(stop);
+                    if (m) {
+                        oend = q + (uint64_t)__ffsll((long long)m) - 1;
+                        break;
+                    }
+                }
+            }
+            if (l == 0) S.oend = oend;
+        }
+#pragma unroll
+        for (int k = 0; k < kTilePer; ++k) {
+            const unsigned long long hm = __ballot(head[k]);
+            if (head[k]) S.hpos[base[k] + (uint32_t)__popcll(hm & below)] = (uint16_t)(t + k * kTileBlock);
+        }
+        __syncthreads();
+        const uint32_t nh = S.nh;
+        const uint64_t oend_t = S.oend;
+        const uint32_t rounds = (nh + kTileBlock - 1) / kTileBlock;
+        for (uint32_t r = 0; r < rounds; ++r) {
+            const uint32_t j = (uint32_t)t + r * kTileBlock;
+            const bool own = j < nh;
+            const uint32_t a = own ? S.hpos[j] : 0u;
+            const uint32_t z = own ? (j + 1 < nh ? (uint32_t)S.hpos[j + 1] : cnt) : 0u;
+            // end of the overhang (global position), == after if none
+            const uint64_t oend = (own && j + 1 == nh) ? oend_t : after;
+            body(a, z - a, after, oend, own);
+        }
+        __syncthreads();  // the LDS tile is rewritten next
+    }
+    if (ebits) raise_err(err, ebits);
+}
+
+}  // namespace mpx

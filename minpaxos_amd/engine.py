@@ -163,6 +163,9 @@ class Engine:
         self._check(rc, "mpx_apply")
         return ret, conf
 
+    def apply_reserve(self, max_cmds):
+        self._check(self.lib.mpx_apply_reserve(self.h, max_cmds), "mpx_apply_reserve")
+
     def apply_dev(self, d_op, d_key, d_val, m, d_ret, d_conf=None, stream=None):
         self._check(self.lib.mpx_apply_dev(self.h, d_op, d_key, d_val, m, d_ret, d_conf, stream),
                     "mpx_apply_dev")
