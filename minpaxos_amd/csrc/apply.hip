@@ -10,13 +10,29 @@
 //   conf[i] = Conflict(previous command on k in this call, command i)
 //   table   : k <- val of the last PUT on k in this call
 // Only keys that are PUT in this call or already present can change any output, so:
-//   1. k_kv_insert_puts   insert every PUT key (one 64-bit CAS per probe; the key value
-//                         INT64_MIN is kept in a side slot so the table needs no state word)
-//   2. k_kv_lookup        slot of every command (absent, never-PUT keys: ret 0, conf 0 now)
-//   3. radix sort of (slot << 32 | i) on the slot bits — stable, so log order within a slot
+//   0. k_epoch_bump       a new call epoch (device counter, so captured graphs stay correct)
+//   1. k_kv_insert_puts   insert every PUT key of the whole call (one 64-bit CAS per probe; the
+//                         key INT64_MIN is kept in a side slot so the table needs no key state)
+// then the log is cut into chunks of C commands, processed in order; per chunk:
+//   2. k_kv_lookup        sort key (slot << 32 | j << 2 | op class) of every command j of the
+//                         chunk (absent, never-PUT keys: ret 0, conf 0 now, sorted last)
+//   3. radix sort on the slot bits - stable, so log order within a slot; the op class rides in
+//                         the key's low bits
 //   4. k_apply_mark       per sorted position q: slot[q], lp[q] = q if PUT else -1
 //   5. segmented inclusive max-scan of lp by slot  -> last PUT at or before q in its slot
-//   6. k_apply_finish     ret / conf per command; the last PUT of each slot updates the table
+//   6. k_apply_finish     a 32-bit result code per command (conf bit + where its ret comes
+//                         from); a slot's first command in the chunk takes its predecessor
+//                         from the table's per-slot state word (epoch-tagged)
+//   7. radix sort of (command index, code) pairs on the index bits above the low 12: the codes
+//                         back in log order up to blocks of 4096 commands
+//   8. k_apply_emit       per block of 4096: places the codes by the low index bits in LDS, then
+//                         log order ret / conf; a GET's value is gathered from val[] or the table
+//   9. k_apply_commit     the last command of each slot in the chunk updates value + state
+// Random access is the cost driver (a uniform key stream is a random permutation of the log):
+// a command-indexed scatter of results costs HBM a read-modify-write per partial line, so the
+// results travel back by a second radix sort instead; what stays random is one table probe per
+// command (2), one per PUT (1) and one value gather per GET (8), all reads. Chunks only bound
+// the scratch memory.
 // Steps 3 and 5 use rocPRIM device primitives (stable LSD radix sort, look-back scan_by_key).
 #include <cstring>
 
@@ -28,6 +44,13 @@
 namespace mpx {
 
 constexpr int64_t kSentinel = INT64_MIN;
+// per-slot state word: bit 0 present (has a value); bit 1 the last command on the slot in call
+// epoch (word >> 2) was a PUT. Epochs start at 1, so a cleared word (0) is "untouched".
+constexpr uint32_t kPresent = 1u;
+constexpr uint32_t kLastPut = 2u;
+constexpr uint32_t kEpochMax = 1u << 30;
+// op class carried in the low 2 bits of a sort key
+constexpr uint32_t kClsOther = 0, kClsPut = 1, kClsGet = 2;
 
 __device__ __forceinline__ uint64_t hash64(uint64_t x) {
     x ^= x >> 30;
@@ -78,6 +101,24 @@ __global__ void k_kv_fill(KvTable t) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *t.n_present = 0;
 }
 
+// epoch[0] = current call epoch, epoch[1] = wrap flag (the next kernel clears every slot's tag)
+__global__ void k_epoch_bump(uint32_t* epoch) {
+    uint32_t e = epoch[0] + 1;
+    epoch[1] = 0;
+    if (e >= kEpochMax) {
+        e = 1;
+        epoch[1] = 1;
+    }
+    epoch[0] = e;
+}
+
+__global__ void k_epoch_wrap(KvTable t) {
+    if (!t.epoch[1]) return;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= t.cap; s += stride)
+        t.state[s] &= kPresent;
+}
+
 hipError_t launch_kv_clear(KvTable& t, hipStream_t stream) {
     k_kv_fill<<<1024, 256, 0, stream>>>(t);
     return hipGetLastError();
@@ -96,7 +137,7 @@ __global__ void k_kv_import_set(KvTable t, const int64_t* __restrict__ keys,
     const int64_t s = kv_lookup(t, keys[i]);
     if (s < 0) return;
     t.vals[s] = vals[i];
-    if (atomicExch(&t.state[s], 1u) == 0u) atomicAdd(t.n_present, 1ull);
+    if ((atomicOr(&t.state[s], kPresent) & kPresent) == 0u) atomicAdd(t.n_present, 1ull);
 }
 
 hipError_t launch_kv_import(KvTable& t, const int64_t* keys, const int64_t* vals, uint64_t n,
@@ -112,7 +153,7 @@ __global__ void k_kv_export(KvTable t, int64_t* __restrict__ keys, int64_t* __re
                             uint64_t cap_out, unsigned long long* counter) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= t.cap; s += stride) {
-        if (t.state[s]) {
+        if (t.state[s] & kPresent) {
             const unsigned long long pos = atomicAdd(counter, 1ull);
             if (pos < cap_out) {
                 keys[pos] = s == t.cap ? kSentinel : t.keys[s];
@@ -140,101 +181,180 @@ __global__ __launch_bounds__(256) void k_kv_insert_puts(KvTable t, const uint8_t
         if (op[i] == MPX_OP_PUT) kv_insert(t, key[i], err);
 }
 
-// slot of every command -> sort keys (slot << 32 | i); NONE slot = cap+1 sorts last
-__global__ __launch_bounds__(256) void k_kv_lookup(KvTable t, const int64_t* __restrict__ key,
-                                                   uint64_t m, uint64_t* __restrict__ skey,
-                                                   int64_t* __restrict__ ret,
-                                                   uint8_t* __restrict__ conf) {
+__device__ __forceinline__ uint32_t op_class(uint8_t o) {
+    return o == MPX_OP_PUT ? kClsPut : (o == MPX_OP_GET ? kClsGet : kClsOther);
+}
+
+// sort key of chunk command j: slot << 32 | j << 2 | class; an absent key that is never PUT in
+// this call gets slot cap+1 (sorts last; its outputs are zero: GET -> NIL, and no conflict since
+// nothing before or after it on that key in this call is a PUT)
+__global__ __launch_bounds__(256) void k_kv_lookup(KvTable t, const uint8_t* __restrict__ op,
+                                                   const int64_t* __restrict__ key, uint64_t n,
+                                                   uint64_t* __restrict__ skey) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
-        const int64_t s = kv_lookup(t, key[i]);
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+        const int64_t s = kv_lookup(t, key[j]);
         const uint64_t sl = s < 0 ? t.cap + 1 : (uint64_t)s;
-        skey[i] = (sl << 32) | i;
-        if (s < 0) {  // never PUT in this call and absent: GET -> NIL, no conflicts
-            ret[i] = 0;
-            if (conf) conf[i] = 0;
-        }
+        skey[j] = (sl << 32) | (j << 2) | op_class(op[j]);
     }
 }
 
-__global__ __launch_bounds__(256) void k_apply_mark(const uint64_t* __restrict__ skey, uint64_t m,
-                                                    const uint8_t* __restrict__ op,
+__device__ __forceinline__ uint32_t sk_index(uint64_t k) { return (uint32_t)k >> 2; }
+__device__ __forceinline__ uint32_t sk_class(uint64_t k) { return (uint32_t)k & 3u; }
+
+__global__ __launch_bounds__(256) void k_apply_mark(const uint64_t* __restrict__ skey, uint64_t n,
                                                     uint32_t* __restrict__ sslot,
                                                     int32_t* __restrict__ lp) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += stride) {
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
         const uint64_t k = skey[q];
-        const uint32_t i = (uint32_t)k;
         sslot[q] = (uint32_t)(k >> 32);
-        lp[q] = op[i] == MPX_OP_PUT ? (int32_t)q : -1;
+        lp[q] = sk_class(k) == kClsPut ? (int32_t)q : -1;
     }
 }
 
-__global__ __launch_bounds__(256) void k_apply_finish(
-    KvTable t, const uint64_t* __restrict__ skey, const uint32_t* __restrict__ sslot,
-    const int32_t* __restrict__ lps, uint64_t m, const uint8_t* __restrict__ op,
-    const int64_t* __restrict__ val, int64_t* __restrict__ ret, uint8_t* __restrict__ conf) {
+// per sorted position q: the command's chunk index and a 32-bit result code
+//   bit 31 conf | bits 29-30 kind | bits 0-28 payload
+//   kind 0: ret 0 (other ops, GET of an absent key); 1: ret = own val (PUT);
+//   2: ret = val of chunk command `payload` (the last PUT before it in this chunk);
+//   3: ret = table value of slot `payload` at chunk start (no PUT before it in this chunk)
+// The codes are sorted back to log order (k_apply_emit reads them sequentially), so no
+// command-indexed store is ever scattered: a random partial-line store costs HBM a
+// read-modify-write, a radix pass over 8 bytes does not.
+constexpr uint32_t kCodeConf = 1u << 31;
+constexpr uint32_t kKindShift = 29;
+constexpr uint32_t kPayloadMask = (1u << kKindShift) - 1u;
+constexpr uint32_t kKindZero = 0, kKindOwn = 1, kKindLog = 2, kKindTable = 3;
+
+__global__ __launch_bounds__(256) void k_apply_finish(KvTable t, const uint64_t* __restrict__ skey,
+                                                      const uint32_t* __restrict__ sslot,
+                                                      const int32_t* __restrict__ lps, uint64_t n,
+                                                      uint32_t* __restrict__ jkey,
+                                                      uint32_t* __restrict__ code) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint32_t none = (uint32_t)(t.cap + 1);
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += stride) {
+    const uint32_t ep = t.epoch[0];
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
+        const uint64_t k = skey[q];
         const uint32_t sl = sslot[q];
-        if (sl == none) continue;
-        const uint32_t i = (uint32_t)skey[q];
-        const uint8_t o = op[i];
-        const bool has_prev = q > 0 && sslot[q - 1] == sl;
-        if (conf) {
-            bool c = false;
-            if (has_prev) {
-                const uint8_t po = op[(uint32_t)skey[q - 1]];
-                c = (po == MPX_OP_PUT) || (o == MPX_OP_PUT);
+        jkey[q] = sk_index(k);
+        if (sl == none) {
+            code[q] = 0;
+            continue;
+        }
+        const uint32_t c = sk_class(k);
+        const bool in_chunk = q > 0 && sslot[q - 1] == sl;
+        uint32_t st = 0;
+        bool prev, prev_put;
+        if (in_chunk) {
+            prev = true;
+            prev_put = sk_class(skey[q - 1]) == kClsPut;
+        } else {
+            st = t.state[sl];
+            prev = (st >> 2) == ep;
+            prev_put = prev && (st & kLastPut);
+        }
+        uint32_t x = kKindZero << kKindShift;
+        if (c == kClsPut) {
+            x = kKindOwn << kKindShift;
+        } else if (c == kClsGet) {
+            const int32_t pp = in_chunk ? lps[q - 1] : -1;  // last PUT strictly before q
+            if (pp >= 0) {
+                x = (kKindLog << kKindShift) | sk_index(skey[pp]);
+            } else {
+                if (in_chunk) st = t.state[sl];
+                if (st & kPresent) x = (kKindTable << kKindShift) | sl;
             }
-            conf[i] = c;
         }
-        int64_t r = 0;
-        if (o == MPX_OP_PUT) {
-            r = val[i];
-        } else if (o == MPX_OP_GET) {
-            const int32_t pp = has_prev ? lps[q - 1] : -1;  // last PUT strictly before q
-            if (pp >= 0) r = val[(uint32_t)skey[pp]];
-            else if (t.state[sl]) r = t.vals[sl];
-        }
-        ret[i] = r;
+        code[q] = x | (prev && (prev_put || c == kClsPut) ? kCodeConf : 0u);
     }
 }
 
-// the last PUT of every slot writes the table (after every read of the start value is done)
+// log order: the caller's ret / conf from the sorted-back codes (before the chunk commits, so
+// kind 3 still reads the chunk-start table value). The back-sort only orders by j >> kEmitBits:
+// block g receives exactly the kEmitGroup codes of commands [g * kEmitGroup, (g+1) * kEmitGroup)
+// in some order and places them by j's low bits in LDS (saves two of the four radix passes).
+constexpr int kEmitBits = 12;
+constexpr int kEmitGroup = 1 << kEmitBits;
+__global__ __launch_bounds__(256) void k_apply_emit(KvTable t, const uint32_t* __restrict__ jkey,
+                                                    const uint32_t* __restrict__ code, uint64_t n,
+                                                    const int64_t* __restrict__ val,
+                                                    int64_t* __restrict__ ret,
+                                                    uint8_t* __restrict__ conf) {
+    __shared__ uint32_t lc[kEmitGroup];
+    const uint64_t g0 = (uint64_t)blockIdx.x * kEmitGroup;
+    const uint32_t cnt = (uint32_t)(n - g0 < (uint64_t)kEmitGroup ? n - g0 : kEmitGroup);
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x)
+        lc[jkey[g0 + i] & (kEmitGroup - 1)] = code[g0 + i];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+        const uint64_t j = g0 + i;
+        const uint32_t x = lc[i];
+        const uint32_t kind = (x >> kKindShift) & 3u, p = x & kPayloadMask;
+        int64_t r = 0;
+        if (kind == kKindOwn) r = val[j];
+        else if (kind == kKindLog) r = val[p];
+        else if (kind == kKindTable) r = t.vals[p];
+        ret[j] = r;
+        if (conf) conf[j] = (uint8_t)(x >> 31);
+    }
+}
+
+// the last command of every slot in the chunk writes the slot's value (if the chunk PUT it) and
+// its state word, after every read of the chunk-start state is done (previous kernels)
 __global__ __launch_bounds__(256) void k_apply_commit(KvTable t, const uint64_t* __restrict__ skey,
                                                       const uint32_t* __restrict__ sslot,
-                                                      const int32_t* __restrict__ lps, uint64_t m,
+                                                      const int32_t* __restrict__ lps, uint64_t n,
                                                       const int64_t* __restrict__ val) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint32_t none = (uint32_t)(t.cap + 1);
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += stride) {
+    const uint32_t ep = t.epoch[0];
+    unsigned long long added = 0;
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
         const uint32_t sl = sslot[q];
         if (sl == none) continue;
-        const bool seg_end = (q + 1 == m) || sslot[q + 1] != sl;
-        if (!seg_end) continue;
+        if (q + 1 < n && sslot[q + 1] == sl) continue;
         const int32_t pp = lps[q];
-        if (pp < 0) continue;
-        t.vals[sl] = val[(uint32_t)skey[pp]];
-        if (t.state[sl] == 0) {
-            t.state[sl] = 1;
-            atomicAdd(t.n_present, 1ull);
+        const uint32_t old = t.state[sl];
+        uint32_t present = old & kPresent;
+        if (pp >= 0) {
+            t.vals[sl] = val[sk_index(skey[pp])];
+            added += present ? 0 : 1;
+            present = kPresent;
         }
+        t.state[sl] = (ep << 2) | (sk_class(skey[q]) == kClsPut ? kLastPut : 0u) | present;
     }
+    // one counter atomic per wave
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) added += __shfl_xor(added, d);
+    if (lane_id() == 0 && added) atomicAdd(t.n_present, added);
 }
 
 namespace {
+hipError_t sort_slot_keys(void* tmp, size_t& tb, uint64_t* in, uint64_t* out, size_t n,
+                          unsigned b0, unsigned b1, hipStream_t st) {
+    return rocprim::radix_sort_keys(tmp, tb, in, out, n, b0, b1, st);
+}
+
+hipError_t sort_back_pairs(void* tmp, size_t& tb, uint32_t* ki, uint32_t* ko, uint32_t* vi,
+                           uint32_t* vo, size_t n, unsigned b0, unsigned b1, hipStream_t st) {
+    return rocprim::radix_sort_pairs(tmp, tb, ki, ko, vi, vo, n, b0, b1, st);
+}
+
 struct WorkLayout {
-    uint64_t skey_a, skey_b, sslot, lp, lps, tmp, tmp_bytes, total;
+    uint64_t skey_a, skey_b, sslot, lp, lps, jkey, code, jkey_b, code_b, tmp, tmp_bytes, total;
 };
 WorkLayout layout(uint64_t m) {
-    size_t sort_tmp = 0, scan_tmp = 0;
-    (void)rocprim::radix_sort_keys(nullptr, sort_tmp, (uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)m,
-                             32u, 64u);
+    size_t sort_tmp = 0, scan_tmp = 0, back_tmp = 0;
+    (void)sort_slot_keys(nullptr, sort_tmp, nullptr, nullptr, (size_t)m, 32u, 64u, 0);
     (void)rocprim::inclusive_scan_by_key(nullptr, scan_tmp, (uint32_t*)nullptr, (int32_t*)nullptr,
-                                   (int32_t*)nullptr, (size_t)m, rocprim::maximum<int32_t>(),
-                                   rocprim::equal_to<uint32_t>());
+                                         (int32_t*)nullptr, (size_t)m,
+                                         rocprim::maximum<int32_t>(),
+                                         rocprim::equal_to<uint32_t>());
+    (void)sort_back_pairs(nullptr, back_tmp, nullptr, nullptr, nullptr, nullptr, (size_t)m, 0u,
+                          32u, 0);
+    size_t t = sort_tmp > scan_tmp ? sort_tmp : scan_tmp;
+    t = t > back_tmp ? t : back_tmp;
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
     WorkLayout w;
     uint64_t o = 0;
@@ -243,20 +363,45 @@ WorkLayout layout(uint64_t m) {
     w.sslot = o; o += al(m * 4);
     w.lp = o; o += al(m * 4);
     w.lps = o; o += al(m * 4);
-    w.tmp_bytes = al(sort_tmp > scan_tmp ? sort_tmp : scan_tmp);
+    w.jkey = o; o += al(m * 4);
+    w.code = o; o += al(m * 4);
+    w.jkey_b = o; o += al(m * 4);
+    w.code_b = o; o += al(m * 4);
+    w.tmp_bytes = al(t);
     w.tmp = o; o += w.tmp_bytes;
     w.total = o;
     return w;
 }
+
+unsigned grid_for(uint64_t n) {
+    uint64_t b = (n + 255) / 256;
+    return (unsigned)(b > 8192 ? 8192 : (b ? b : 1));
+}
+
+unsigned bits_for(uint64_t x) {  // bits to represent every value < x
+    unsigned b = 1;
+    while ((1ull << b) < x) ++b;
+    return b;
+}
 }  // namespace
 
-uint64_t apply_work_bytes(uint64_t m) { return layout(m < 1 ? 1 : m).total; }
+uint64_t apply_chunk_commands(uint64_t chunk, uint64_t m) {
+    const uint64_t c = chunk ? chunk : kApplyChunkDefault;
+    return m < c ? (m ? m : 1) : c;
+}
+
+uint64_t apply_work_bytes(uint64_t chunk, uint64_t m) {
+    return layout(apply_chunk_commands(chunk, m)).total;
+}
 
 hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
-                        uint64_t m, int64_t* ret, uint8_t* conf, ApplyWork& w, uint32_t* err,
-                        hipStream_t stream) {
+                        uint64_t m, int64_t* ret, uint8_t* conf, uint64_t chunk, ApplyWork& w,
+                        uint32_t* err, hipStream_t stream) {
     if (!m) return hipSuccess;
-    const WorkLayout L = layout(m);
+    const uint64_t C = apply_chunk_commands(chunk, m);
+    // result codes carry a chunk index or a slot in 29 bits
+    if (C > kPayloadMask || t.cap + 1 > kPayloadMask) return hipErrorInvalidValue;
+    const WorkLayout L = layout(C);
     if (w.bytes < L.total) return hipErrorInvalidValue;
     char* b = (char*)w.base;
     uint64_t* skey_a = (uint64_t*)(b + L.skey_a);
@@ -264,25 +409,46 @@ hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const
     uint32_t* sslot = (uint32_t*)(b + L.sslot);
     int32_t* lp = (int32_t*)(b + L.lp);
     int32_t* lps = (int32_t*)(b + L.lps);
+    uint32_t* jkey = (uint32_t*)(b + L.jkey);
+    uint32_t* code = (uint32_t*)(b + L.code);
+    uint32_t* jkey_b = (uint32_t*)(b + L.jkey_b);
+    uint32_t* code_b = (uint32_t*)(b + L.code_b);
     void* tmp = b + L.tmp;
-    size_t tmp_bytes = L.tmp_bytes;
-    unsigned blocks = (unsigned)((m + 255) / 256);
-    if (blocks > 8192) blocks = 8192;
-    k_kv_insert_puts<<<blocks, 256, 0, stream>>>(t, op, key, m, err);
-    k_kv_lookup<<<blocks, 256, 0, stream>>>(t, key, m, skey_a, ret, conf);
-    unsigned bits = 1;
-    while ((1ull << bits) <= t.cap + 1) ++bits;
-    hipError_t r = rocprim::radix_sort_keys(tmp, tmp_bytes, skey_a, skey_b, (size_t)m, 32u,
-                                            32u + bits, stream);
-    if (r != hipSuccess) return r;
-    k_apply_mark<<<blocks, 256, 0, stream>>>(skey_b, m, op, sslot, lp);
-    tmp_bytes = L.tmp_bytes;
-    r = rocprim::inclusive_scan_by_key(tmp, tmp_bytes, sslot, lp, lps, (size_t)m,
-                                       rocprim::maximum<int32_t>(), rocprim::equal_to<uint32_t>(),
-                                       stream);
-    if (r != hipSuccess) return r;
-    k_apply_finish<<<blocks, 256, 0, stream>>>(t, skey_b, sslot, lps, m, op, val, ret, conf);
-    k_apply_commit<<<blocks, 256, 0, stream>>>(t, skey_b, sslot, lps, m, val);
+    const unsigned slot_bits = bits_for(t.cap + 2);
+
+    k_epoch_bump<<<1, 1, 0, stream>>>(t.epoch);
+    k_epoch_wrap<<<1024, 256, 0, stream>>>(t);
+    k_kv_insert_puts<<<grid_for(m), 256, 0, stream>>>(t, op, key, m, err);
+    for (uint64_t c0 = 0; c0 < m; c0 += C) {
+        const uint64_t n = m - c0 < C ? m - c0 : C;
+        const unsigned g = grid_for(n);
+        k_kv_lookup<<<g, 256, 0, stream>>>(t, op + c0, key + c0, n, skey_a);
+        size_t tmp_bytes = L.tmp_bytes;
+        hipError_t r = sort_slot_keys(tmp, tmp_bytes, skey_a, skey_b, (size_t)n, 32u,
+                                      32u + slot_bits, stream);
+        if (r != hipSuccess) return r;
+        k_apply_mark<<<g, 256, 0, stream>>>(skey_b, n, sslot, lp);
+        tmp_bytes = L.tmp_bytes;
+        r = rocprim::inclusive_scan_by_key(tmp, tmp_bytes, sslot, lp, lps, (size_t)n,
+                                           rocprim::maximum<int32_t>(),
+                                           rocprim::equal_to<uint32_t>(), stream);
+        if (r != hipSuccess) return r;
+        k_apply_finish<<<g, 256, 0, stream>>>(t, skey_b, sslot, lps, n, jkey, code);
+        tmp_bytes = L.tmp_bytes;
+        const unsigned jb = bits_for(n);
+        const uint32_t *jk = jkey, *cd = code;  // one emit group: LDS placement alone suffices
+        if (jb > (unsigned)kEmitBits) {
+            r = sort_back_pairs(tmp, tmp_bytes, jkey, jkey_b, code, code_b, (size_t)n,
+                                (unsigned)kEmitBits, jb, stream);
+            if (r != hipSuccess) return r;
+            jk = jkey_b;
+            cd = code_b;
+        }
+        const unsigned eg = (unsigned)((n + kEmitGroup - 1) / kEmitGroup);
+        k_apply_emit<<<eg, 256, 0, stream>>>(t, jk, cd, n, val + c0, ret + c0,
+                                             conf ? conf + c0 : nullptr);
+        k_apply_commit<<<g, 256, 0, stream>>>(t, skey_b, sslot, lps, n, val + c0);
+    }
     return hipGetLastError();
 }
 

@@ -37,6 +37,7 @@ struct mpx_engine {
     mpx::KvTable kv{};
     bool kv_ready = false;
     DevBuf apply_work;
+    uint64_t apply_chunk = 0;  // commands per apply chunk (0 = kApplyChunkDefault)
     // group-step work list (groups the fast kernel hands to the general kernel) + its count
     DevBuf worklist;
     uint32_t* d_wcount = nullptr;
@@ -137,7 +138,9 @@ int ensure_kv(mpx_engine* e) {
     if (hipMalloc(&t.keys, (cap + 1) * 8) != hipSuccess ||
         hipMalloc(&t.vals, (cap + 1) * 8) != hipSuccess ||
         hipMalloc(&t.state, (cap + 1) * 4) != hipSuccess ||
-        hipMalloc(&t.n_present, sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&t.n_present, sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&t.epoch, 2 * sizeof(uint32_t)) != hipSuccess ||
+        hipMemsetAsync(t.epoch, 0, 2 * sizeof(uint32_t), e->stream) != hipSuccess) {
         (void)hipGetLastError();
         return fail(e, MPX_E_NOMEM, "KV table allocation failed");
     }
@@ -181,6 +184,7 @@ int mpx_open(int device, const mpx_config* cfg, mpx_engine** out) {
     e->device = device;
     e->cfg = *cfg;
     if (!e->cfg.kv_per_group) e->cfg.kv_per_group = 512;
+    if (const char* c = getenv("MPX_APPLY_CHUNK")) e->apply_chunk = strtoull(c, nullptr, 10);
     if (!e->cfg.max_groups) e->cfg.max_groups = 1ull << 20;
     if (e->cfg.kv_per_group > 1024) {
         delete e;
@@ -219,6 +223,7 @@ int mpx_close(mpx_engine* e) {
         (void)hipFree(e->kv.vals);
         (void)hipFree(e->kv.state);
         (void)hipFree(e->kv.n_present);
+        (void)hipFree(e->kv.epoch);
     }
     if (e->d_err) (void)hipFree(e->d_err);
     if (e->d_red) (void)hipFree(e->d_red);
@@ -406,15 +411,15 @@ int mpx_apply(mpx_engine* e, const uint8_t* op, const int64_t* key, const int64_
     GROW(e, e->b[9], m * 8);
     GROW(e, e->b[10], m * 8);
     GROW(e, e->b[11], m);
-    GROW(e, e->apply_work, mpx::apply_work_bytes(m));
+    GROW(e, e->apply_work, mpx::apply_work_bytes(e->apply_chunk, m));
     CK(h2d(e, e->b[7].p, op, m));
     CK(h2d(e, e->b[8].p, key, m * 8));
     CK(h2d(e, e->b[9].p, val, m * 8));
     mpx::ApplyWork w{e->apply_work.p, e->apply_work.cap};
     uint8_t* d_conf = conf_prev ? (uint8_t*)e->b[11].p : nullptr;
     HIPCHK(e, mpx::launch_apply(e->kv, (const uint8_t*)e->b[7].p, (const int64_t*)e->b[8].p,
-                                (const int64_t*)e->b[9].p, m, (int64_t*)e->b[10].p, d_conf, w,
-                                e->d_err, e->stream));
+                                (const int64_t*)e->b[9].p, m, (int64_t*)e->b[10].p, d_conf,
+                                e->apply_chunk, w, e->d_err, e->stream));
     CK(d2h(e, ret, e->b[10].p, m * 8));
     if (conf_prev) CK(d2h(e, conf_prev, d_conf, m));
     return finish(e);
@@ -425,7 +430,7 @@ int mpx_apply_reserve(mpx_engine* e, size_t max_cmds) {
     if (max_cmds >= (1ull << 31)) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 commands");
     CK(begin(e));
     CK(ensure_kv(e));
-    GROW(e, e->apply_work, mpx::apply_work_bytes(max_cmds));
+    GROW(e, e->apply_work, mpx::apply_work_bytes(e->apply_chunk, max_cmds));
     return finish(e);
 }
 
@@ -434,13 +439,13 @@ int mpx_apply_dev(mpx_engine* e, const uint8_t* d_op, const int64_t* d_key, cons
     if (!e) return MPX_E_INVAL;
     if (m && (!d_op || !d_key || !d_val || !d_ret)) return fail(e, MPX_E_INVAL, "null argument");
     if (m >= (1ull << 31)) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 commands per call");
-    if (!e->kv_ready || e->apply_work.cap < mpx::apply_work_bytes(m))
+    if (!e->kv_ready || e->apply_work.cap < mpx::apply_work_bytes(e->apply_chunk, m))
         return fail(e, MPX_E_INVAL,
                     "mpx_apply_dev: call mpx_apply_reserve(m) first (the dev entry point never "
                     "allocates)");
     mpx::ApplyWork w{e->apply_work.p, e->apply_work.cap};
-    HIPCHK(e, mpx::launch_apply(e->kv, d_op, d_key, d_val, m, d_ret, d_conf_prev, w, e->d_err,
-                                pick(e, stream)));
+    HIPCHK(e, mpx::launch_apply(e->kv, d_op, d_key, d_val, m, d_ret, d_conf_prev,
+                                e->apply_chunk, w, e->d_err, pick(e, stream)));
     return MPX_OK;
 }
 

@@ -56,19 +56,24 @@ hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
 struct KvTable {
     int64_t* keys;       // [cap]
     int64_t* vals;       // [cap]
-    uint32_t* state;     // [cap] 0 empty, 1 claimed, 2 key published, |4 present (has value)
+    uint32_t* state;     // [cap] bit 0 present, bit 1 last command of epoch (>> 2) was a PUT
     uint64_t cap;        // power of two
     unsigned long long* n_present;  // device counter
+    uint32_t* epoch;     // device: [0] call epoch of mpx_apply, [1] wrap flag
 };
 
 struct ApplyWork {      // scratch sized for m commands (see apply_work_bytes)
     void* base;
     uint64_t bytes;
 };
-uint64_t apply_work_bytes(uint64_t m);
+// commands per apply chunk (0 = default): bounds the pipeline's scratch (48 B per command);
+// env MPX_APPLY_CHUNK overrides it per engine (tests use tiny chunks to cross boundaries)
+constexpr uint64_t kApplyChunkDefault = 1ull << 26;
+uint64_t apply_chunk_commands(uint64_t chunk, uint64_t m);
+uint64_t apply_work_bytes(uint64_t chunk, uint64_t m);
 hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
-                        uint64_t m, int64_t* ret, uint8_t* conf, ApplyWork& w, uint32_t* err,
-                        hipStream_t stream);
+                        uint64_t m, int64_t* ret, uint8_t* conf, uint64_t chunk, ApplyWork& w,
+                        uint32_t* err, hipStream_t stream);
 hipError_t launch_kv_clear(KvTable& t, hipStream_t stream);
 hipError_t launch_kv_import(KvTable& t, const int64_t* keys, const int64_t* vals, uint64_t n,
                             uint32_t* err, hipStream_t stream);

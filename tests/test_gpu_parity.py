@@ -192,6 +192,28 @@ def test_apply_mixed_ops_and_special_keys(mk_engine):
     assert list(r) == [30, 70, 0]
 
 
+@pytest.mark.parametrize("chunk", [1, 7, 777, 4096])
+def test_apply_chunked(mk_engine, monkeypatch, chunk):
+    """the apply pipeline cuts a call into chunks (MPX_APPLY_CHUNK commands): slot state and
+    conflicts carry across chunk boundaries and calls; a GET in one chunk on a key that is
+    only PUT in a later chunk still conflicts with that PUT"""
+    monkeypatch.setenv("MPX_APPLY_CHUNK", str(chunk))
+    rng = np.random.default_rng(77 + chunk)
+    e, o = mk_engine(5, R.MODE_MIN), Oracle(5, R.MODE_MIN)
+    handmade = (np.array([R.OP_GET, R.OP_DELETE, R.OP_GET, R.OP_PUT, R.OP_GET, R.OP_PUT, R.OP_GET],
+                         np.uint8),
+                np.array([5, 6, 5, 5, 7, 6, 6], np.int64), np.arange(7, dtype=np.int64) + 100)
+    calls = [handmade] + [gen_cases.commands_mixed(rng, 5000 if chunk > 1 else 300, 40 + 400 * t)
+                          for t in range(3)] + [handmade]
+    for op, key, val in calls:
+        gr, gc = e.apply(op, key, val)
+        wr, wc = o.apply(op, key, val)
+        assert np.array_equal(gr, wr) and np.array_equal(gc, wc)
+        gk, gv = e.kv_export()
+        wk, wv = o.kv_export()
+        assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
+
+
 def test_conflict_batch(mk_engine):
     rng = np.random.default_rng(9)
     e, o = mk_engine(5, R.MODE_MIN), Oracle(5, R.MODE_MIN)

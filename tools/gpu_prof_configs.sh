@@ -1,0 +1,22 @@
+#!/bin/bash
+# GPU-box rocprofv3 kernel stats for the single-kernel configurations (BASELINE configs 2-4).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/profcfg_${TAG:-r01}
+mkdir -p $OUT
+run() {
+  name=$1; shift
+  timeout -k 10 ${BT:-400} rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$name -o $name -- python3 bench.py "$@" > $OUT/$name.log 2>&1
+  rc=$?; echo "$name rc=$rc"; grep '^{' $OUT/$name.log | tail -1 | cut -c1-400
+  case $rc in 0) ;; *) exit $rc;; esac
+}
+for w in ${WORKLOADS:-tally_min tally_classic prepare apply_uniform apply_zipf}; do
+  case $w in
+    tally_min) run $w --workload tally --mode min --steps 10 --warmup 2 ${XARGS:-};;
+    tally_classic) run $w --workload tally --mode classic --steps 10 --warmup 2 ${XARGS:-};;
+    prepare) run $w --workload prepare --steps 10 --warmup 2 ${XARGS:-};;
+    apply_uniform) run $w --workload apply --dist uniform --steps 5 --warmup 1 ${XARGS:-};;
+    apply_zipf) run $w --workload apply --dist zipf --steps 5 --warmup 1 ${XARGS:-};;
+  esac
+done
