@@ -17,6 +17,8 @@ The other single-GPU configurations of BASELINE.json are kernel benches of their
   prepare  config 3: CLASSIC prepare selection, 16M instances x 4 replies (k_prepare_classic)
   apply    config 4: batched KV apply, 64M PUT/GET over 1M keys (the mpx_apply pipeline),
            --dist uniform|zipf
+  decode   SURVEY §8(f) rank 1: peer-stream framing + AcceptReply decode of the config-2 replies
+           (16M instances x 4 = 64M frames of 14 B, a Beacon every ~4096 frames, 0.9 GB)
 Each prints one JSON line in the same format, with its own roofline, parity and CPU baseline.
 
 Rank 0 prints ONE JSON line. Inputs are generated on the host (synthetic, counter-based
@@ -57,7 +59,7 @@ def parse():
                     help="groups timed on the CPU baseline (0 = auto, ~10-30 s of CPU work)")
     ap.add_argument("--parity-groups", type=int, default=512)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--workload", default="step", choices=["step", "tally", "prepare", "apply"])
+    ap.add_argument("--workload", default="step", choices=["step", "tally", "prepare", "apply", "decode"])
     ap.add_argument("--instances", type=int, default=1 << 24, help="tally / prepare: instances")
     ap.add_argument("--commands", type=int, default=1 << 26, help="apply: commands")
     ap.add_argument("--apply-keys", type=int, default=1 << 20, help="apply: key space")
@@ -460,7 +462,7 @@ def kernel_bench(a):
                          f"oracle's sequential handler loop (incl. its numpy copy-in/out), "
                          f"one thread, {secs:.1f} s timed"}
         workload = f"config3: {I} instances x {N - 1} PrepareReplies, N={N}, p_ok=0.8, random ballots"
-    else:
+    elif a.workload == "apply":
         M, K = a.commands, a.apply_keys
         op, key, val = synth.commands(M, K, 0.5, a.dist, seed=44)
         d_op, d_key, d_val = dt(op), dt(key), dt(val)
@@ -499,6 +501,50 @@ def kernel_bench(a):
                "sample": f"the full workload ({M} commands over {K} keys, {a.dist}) x {reps}, "
                          f"Execute per command on an unordered_map, one thread, {secs:.1f} s timed"}
         workload = f"config4: {M} PUT/GET (p_put=0.5) over {K} keys, {a.dist}"
+    else:  # decode
+        I = a.instances
+        recs, _ = synth.accept_replies(I, N, 0.7, seed=42)
+        buf = synth.peer_stream(recs, seed=52, p_beacon=1.0 / 4096)
+        L = len(buf)
+        o = OL.Oracle(N, mode)
+        w_ar, w_oth, w_res = o.decode_peer_stream(buf)
+        n_ar, n_oth = int(w_res["n_accept_replies"]), int(w_res["n_other"])
+        d_buf = dt(buf)
+        d_ar = torch.empty(n_ar * 16, dtype=torch.uint8, device=dev)
+        d_oth = torch.empty(max(n_oth, 1) * 8, dtype=torch.uint8, device=dev)
+        d_res = torch.empty(32, dtype=torch.uint8, device=dev)
+        eng.decode_reserve(L)
+        t_gen = time.time() - t_gen
+        wall, ms = _timed(stream, eng, a.steps, a.warmup,
+                          lambda: eng.decode_peer_stream_dev(d_buf.data_ptr(), L, d_ar.data_ptr(),
+                                                             n_ar, d_oth.data_ptr(), n_oth,
+                                                             d_res.data_ptr(), eng.stream))
+        alg = L + n_ar * 16 + n_oth * 8  # stream read once, records written once
+        units, unit = n_ar, "AcceptReplies/s"
+        kernel = ("mpx_decode_peer_stream pipeline (tile maps, group maps, walk, tile entries, "
+                  "emit)")
+        got_res = d_res.cpu().numpy().view(R.DECODE_RESULT)[0]
+        bit_exact = bool(got_res.tobytes() == w_res.tobytes()
+                         and d_ar.cpu().numpy().tobytes() == w_ar.tobytes()
+                         and d_oth.cpu().numpy()[:n_oth * 8].tobytes() == w_oth.tobytes())
+        parity = {"frames_checked": n_ar + n_oth, "bytes": L, "bit_exact": bit_exact}
+        lib = OL.load()
+        car = np.zeros(n_ar, R.ACCEPT_REPLY)
+        coth = np.zeros(max(n_oth, 1), R.PEER_FRAME)
+        cres = np.zeros(1, R.DECODE_RESULT)
+        secs, reps = 0.0, 0
+        while secs < 10.0 and reps < 20:
+            t0 = time.perf_counter()
+            lib.orc_decode_peer_stream(buf.ctypes.data, L, car.ctypes.data, n_ar, coth.ctypes.data,
+                                       n_oth, cres.ctypes.data)
+            secs += time.perf_counter() - t0
+            reps += 1
+        cpu = {"value": n_ar * reps / secs, "unit": unit, "cores": 1, "kind": "port",
+               "sample": f"the full stream ({L} bytes, {n_ar} AcceptReplies, {n_oth} Beacons) "
+                         f"x {reps} through the oracle's replicaListener loop, one thread, "
+                         f"{secs:.1f} s timed"}
+        workload = (f"decode: {n_ar} AcceptReply frames (config-2 replies, {I} instances) + "
+                    f"{n_oth} Beacons, {L} bytes")
     if world > 1:
         tt = torch.tensor([wall], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)

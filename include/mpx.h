@@ -20,6 +20,11 @@
  *                            (Paxos groups) at once: one tally and one apply per group
  *   mpx_watermarks_allreduce <- (no reference equivalent; the one cross-shard step: an RCCL
  *                            all-reduce of per-group committedUpTo / executed watermarks)
+ *   mpx_decode_peer_stream <- genericsmr.(*Replica).replicaListener
+ *                              src/genericsmr/genericsmr.go:402-446 with the fixed-size
+ *                            Unmarshal()s it dispatches to (minpaxosprotomarsh.go:259-270,
+ *                            :568-580, :737-749; Beacon/BeaconReply): frames a peer byte stream
+ *                            and decodes its AcceptReplies into mpx_accept_reply records
  *
  * Contract (every entry point):
  *   - plain C, no exceptions cross the boundary, never aborts; return 0 (MPX_OK) or a negative
@@ -306,6 +311,58 @@ int mpx_watermarks_allreduce(mpx_engine* eng, int32_t* committed, int32_t* execu
 /* device pointers: committed/executed are one contiguous int32 buffer of 2*n_groups       */
 int mpx_watermarks_allreduce_dev(mpx_engine* eng, int32_t* d_watermarks, size_t n_groups,
                                  void* stream);
+
+/* ---- peer stream framing + AcceptReply decode ----------------------
+ * A peer connection carries frames [code u8][body]. Codes (genericsmrproto.go:7-18 and the
+ * registration order of bareminpaxos.NewReplica, bareminpaxos.go:108-113):                 */
+#define MPX_PEER_BEACON 6        /* 8-byte timestamp                                         */
+#define MPX_PEER_BEACON_REPLY 7  /* 8-byte timestamp                                         */
+#define MPX_PEER_PREPARE 8       /* 12-byte body                                             */
+#define MPX_PEER_ACCEPT 9        /* variable length (Command + CatchUpLog slices)            */
+#define MPX_PEER_COMMIT 10       /* variable length (Command slice)                          */
+#define MPX_PEER_COMMIT_SHORT 11 /* 16-byte body                                             */
+#define MPX_PEER_PREPARE_REPLY 12/* variable length                                          */
+#define MPX_PEER_ACCEPT_REPLY 13 /* 13-byte body {Instance i32, OK u8, Ballot i32, Id i32}   */
+/* every other code is a 1-byte frame (replicaListener logs "unknown message type" and reads
+ * the next byte as a new code, genericsmr.go:440-442)                                       */
+
+/* a fixed-size frame other than AcceptReply: where it starts (its code byte) and its code  */
+typedef struct mpx_peer_frame {
+    uint32_t offset;
+    uint8_t code;
+    uint8_t pad[3];
+} mpx_peer_frame; /* 8 B */
+
+#define MPX_DECODE_END 0      /* the buffer ends exactly at a frame boundary                 */
+#define MPX_DECODE_PARTIAL 1  /* stopped at a frame whose body runs past the buffer: keep the
+                                 tail [consumed, len) and call again when more bytes arrive   */
+#define MPX_DECODE_VARIABLE 2 /* stopped at a variable-length frame (Accept / Commit /
+                                 PrepareReply) at `consumed`: the host unmarshals it and
+                                 calls again after it                                        */
+#define MPX_DECODE_MAX_BYTES 0x7FFFFFFFu /* per call                                        */
+
+typedef struct mpx_decode_result {
+    uint64_t consumed;         /* bytes framed (start of the stop frame, or len)            */
+    uint64_t n_accept_replies; /* AcceptReply frames in [0, consumed)                       */
+    uint64_t n_other;          /* other fixed-size frames in [0, consumed)                  */
+    int32_t stop_reason;       /* MPX_DECODE_*                                              */
+    int32_t stop_code;         /* code byte at `consumed`, -1 at MPX_DECODE_END             */
+} mpx_decode_result; /* 32 B */
+
+/* Frames buf[0..len) in stream order. AcceptReplies go to ar[0..min(n, ar_cap)) in arrival
+ * order, other fixed-size frames to other[0..min(n, other_cap)); the counts in *res are
+ * always complete, so a caller whose capacity was short sees n > cap and can call again.
+ * AcceptReply is framed as the 13 bytes its Marshal writes (minpaxosprotomarsh.go:545-566);
+ * the reference's io.ReadAtLeast(wire, bs, 9) (:571) can return a short body on a partial
+ * TCP read and desynchronise the stream, which the engine does not reproduce.              */
+int mpx_decode_peer_stream(mpx_engine* eng, const uint8_t* buf, size_t len,
+                           mpx_accept_reply* ar, size_t ar_cap, mpx_peer_frame* other,
+                           size_t other_cap, mpx_decode_result* res);
+/* scratch for mpx_decode_peer_stream_dev on buffers of up to max_len bytes (grows only)    */
+int mpx_decode_reserve(mpx_engine* eng, size_t max_len);
+int mpx_decode_peer_stream_dev(mpx_engine* eng, const uint8_t* d_buf, size_t len,
+                               mpx_accept_reply* d_ar, size_t ar_cap, mpx_peer_frame* d_other,
+                               size_t other_cap, mpx_decode_result* d_res, void* stream);
 
 #ifdef __cplusplus
 }

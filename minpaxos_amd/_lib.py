@@ -59,6 +59,9 @@ SIGNATURES = {
     "mpx_comm_init": (C.c_int, [_p, C.c_int, C.c_int, _p]),
     "mpx_watermarks_allreduce": (C.c_int, [_p, _p, _p, _sz]),
     "mpx_watermarks_allreduce_dev": (C.c_int, [_p, _p, _sz, _p]),
+    "mpx_decode_peer_stream": (C.c_int, [_p, _p, _sz, _p, _sz, _p, _sz, _p]),
+    "mpx_decode_reserve": (C.c_int, [_p, _sz]),
+    "mpx_decode_peer_stream_dev": (C.c_int, [_p, _p, _sz, _p, _sz, _p, _sz, _p, _p]),
 }
 
 _lib = None

@@ -1,0 +1,440 @@
+// decode.hip — batched peer-stream framing + AcceptReply decode.
+//
+// Reference: genericsmr.(*Replica).replicaListener  src/genericsmr/genericsmr.go:402-446 reads
+// one peer connection as a sequence of frames [code u8][body]: GENERIC_SMR_BEACON (6) and
+// GENERIC_SMR_BEACON_REPLY (7) carry an 8-byte timestamp; codes 8..13 are the RPCs registered by
+// bareminpaxos.NewReplica (bareminpaxos.go:108-113; rpcCode starts at
+// GENERIC_SMR_BEACON_REPLY+1, genericsmr.go:92): Prepare (12-byte body,
+// minpaxosprotomarsh.go:259-270), Accept (variable, :470-507), Commit (variable, :648-672),
+// CommitShort (16, :737-749), PrepareReply (variable, :352-387), AcceptReply (13, :545-580).
+// Any other code is logged and skipped (genericsmr.go:440-442), so it is a 1-byte frame.
+// AcceptReply bodies decode into mpx_accept_reply (Instance, OK, Ballot, Id; little endian);
+// every other fixed-size frame is reported as (offset, code) for the host. Framing stops at the
+// first variable-length frame (the host parses it and calls again past it) or at a frame that
+// runs past the end of the buffer (a partial read: the host keeps the tail).
+//
+// Framing is sequential by nature (each frame's start depends on every earlier length). The
+// engine makes it data parallel with entry maps: a frame that starts in a 64-byte chunk ends at
+// most 16 bytes into the next one (the longest fixed frame is 17 bytes), so a chunk's behaviour
+// is a function from its entry offset (0..16) to (exit offset into the next chunk | stop
+// position, AcceptReplies and other frames passed on the way). Each lane computes its chunk's
+// 17-entry map with a register-window DP over the chunk's bytes (the possible lengths are 1, 9,
+// 13, 14 and 17, so the DP only looks back at fixed distances). Maps compose associatively: a
+// workgroup reduces its 128 chunk maps to an 8 KB tile map (tree in LDS), 256 tile maps reduce
+// to a group map, one block walks the group maps from entry 0, and the down-sweeps hand every
+// tile, then every chunk, its true entry and output offsets; the chunks then emit their records.
+// HBM traffic: the stream is read twice (maps, emit), the records written once; the maps are
+// 204 bytes per 8 KB tile.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace mpx {
+
+namespace {
+
+constexpr int kChunk = 64;                 // bytes per lane
+constexpr int kTileLanes = 128;            // lanes per tile workgroup
+constexpr int kTileBytes = kChunk * kTileLanes;
+constexpr int kEntries = 17;               // entry offsets 0..16
+constexpr int kGroupTiles = 256;           // tile maps per group
+constexpr uint32_t kDead = 0xFFFFFFFFu;    // tile / chunk past the stop of the frame chain
+
+// frame length by code, code byte included (0 = variable-length frame: stop); codes 6..13 from
+// a byte-lane table, everything else is a 1-byte unknown frame
+constexpr uint64_t kLenLut = 9ull | (9ull << 8) | (13ull << 16) | (0ull << 24) | (0ull << 32) |
+                             (17ull << 40) | (0ull << 48) | (14ull << 56);
+__device__ __forceinline__ uint32_t frame_len(uint32_t code) {
+    const uint32_t i = code - (uint32_t)MPX_PEER_BEACON;
+    const uint32_t in = 0u - (uint32_t)(i < 8u);
+    return (((uint32_t)(kLenLut >> ((i & 7u) * 8u)) & 0xFFu) & in) | (1u & ~in);
+}
+static_assert(MPX_PEER_BEACON == 6 && MPX_PEER_BEACON_REPLY == 7 && MPX_PEER_PREPARE == 8 &&
+                  MPX_PEER_ACCEPT == 9 && MPX_PEER_COMMIT == 10 && MPX_PEER_COMMIT_SHORT == 11 &&
+                  MPX_PEER_PREPARE_REPLY == 12 && MPX_PEER_ACCEPT_REPLY == 13,
+              "kLenLut is laid out for codes 6..13");
+
+// lane-map entry (u32): [0..6] pos (exit offset into the next chunk, or stop offset in the
+// chunk), [7] stop, [8..11] AcceptReplies, [12..18] other frames
+constexpr uint32_t kLStop = 1u << 7;
+__device__ __forceinline__ uint32_t l_pos(uint32_t x) { return x & 0x7Fu; }
+__device__ __forceinline__ uint32_t l_ar(uint32_t x) { return (x >> 8) & 0xFu; }
+__device__ __forceinline__ uint32_t l_oth(uint32_t x) { return (x >> 12) & 0x7Fu; }
+
+// tile-level entry (u64): [0..15] pos (exit offset, or stop offset from the tile start),
+// [16] stop, [17..32] AcceptReplies, [33..48] other frames
+constexpr uint64_t kTStop = 1ull << 16;
+__device__ __forceinline__ uint64_t t_make(uint32_t pos, bool stop, uint32_t ar, uint32_t oth) {
+    return (uint64_t)pos | (stop ? kTStop : 0ull) | ((uint64_t)ar << 17) | ((uint64_t)oth << 33);
+}
+__device__ __forceinline__ uint32_t t_pos(uint64_t x) { return (uint32_t)x & 0xFFFFu; }
+__device__ __forceinline__ bool t_stop(uint64_t x) { return (x & kTStop) != 0; }
+__device__ __forceinline__ uint32_t t_ar(uint64_t x) { return (uint32_t)(x >> 17) & 0xFFFFu; }
+__device__ __forceinline__ uint32_t t_oth(uint64_t x) { return (uint32_t)(x >> 33) & 0xFFFFu; }
+// a, then the map b of the chunks right after a's
+__device__ __forceinline__ uint64_t t_compose(uint64_t a, const uint64_t* b) {
+    if (t_stop(a)) return a;
+    const uint64_t y = b[t_pos(a)];
+    return (y & 0x1FFFFull) | ((uint64_t)(t_ar(a) + t_ar(y)) << 17) |
+           ((uint64_t)(t_oth(a) + t_oth(y)) << 33);
+}
+
+// The lane's 64-byte chunk -> its 17 map entries (w[k] = entry k) by a backward DP over the
+// chunk's positions: dp[p] = frame p reaches past the chunk ? exit : dp[p + len(p)] + frame p.
+// Before step p the window holds w[k] = dp[p+1+k]; the lengths are compile-time offsets into it.
+// kEdge: the chunk is within 81 bytes of the end of the buffer, so positions past the end and
+// frames running past it must be checked (every other chunk skips both tests).
+template <bool kEdge>
+__device__ __forceinline__ void lane_map_dp(const uint32_t (&wd)[16], uint32_t c0, uint32_t len,
+                                            uint32_t (&w)[kEntries]) {
+#pragma unroll
+    for (int k = 0; k < kEntries; ++k) w[k] = 0;
+#pragma unroll
+    for (int p = kChunk - 1; p >= 0; --p) {
+        // branch-free: every select below is a mask, so the unrolled loop stays straight-line
+        // code and the window shift is pure register renaming
+        const uint32_t code = (wd[p >> 2] >> ((p & 3) * 8)) & 0xFFu;
+        const uint32_t fl = frame_len(code);
+        uint32_t stop = (uint32_t)(fl == 0);
+        if (kEdge) stop |= (uint32_t)(c0 + (uint32_t)p >= len) | (uint32_t)(c0 + (uint32_t)p + fl > len);
+        const uint32_t inc = (1u << 12) - (uint32_t)(code == MPX_PEER_ACCEPT_REPLY) * ((1u << 12) - (1u << 8));
+        uint32_t nx = (w[13] & (0u - (uint32_t)(fl == 14))) | (w[8] & (0u - (uint32_t)(fl == 9))) |
+                      (w[12] & (0u - (uint32_t)(fl == 13))) | (w[16] & (0u - (uint32_t)(fl == 17))) |
+                      (w[0] & (0u - (uint32_t)(fl == 1)));
+        if (p + 17 > kChunk) {  // compile time: only the last 17 positions can leave the chunk
+            const uint32_t out = 0u - (uint32_t)((uint32_t)p + fl >= (uint32_t)kChunk);
+            nx = (nx & ~out) | (((uint32_t)p + fl - kChunk) & out);
+        }
+        const uint32_t sm = 0u - stop;
+        const uint32_t d = (((uint32_t)p | kLStop) & sm) | ((nx + inc) & ~sm);
+#pragma unroll
+        for (int k = kEntries - 1; k > 0; --k) w[k] = w[k - 1];
+        w[0] = d;
+    }
+}
+
+__device__ __forceinline__ void lane_map(const uint32_t (&wd)[16], uint64_t c0, uint64_t len,
+                                         uint32_t (&w)[kEntries]) {
+    if (c0 + kChunk + kEntries > len) lane_map_dp<true>(wd, (uint32_t)c0, (uint32_t)len, w);
+    else lane_map_dp<false>(wd, (uint32_t)c0, (uint32_t)len, w);
+}
+
+__device__ __forceinline__ void load_chunk(const uint8_t* __restrict__ buf, uint64_t len,
+                                           uint64_t c0, uint32_t (&wd)[16]) {
+    if (c0 + kChunk <= len) {
+        const uint4* s = reinterpret_cast<const uint4*>(buf + c0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint4 v = s[i];
+            wd[4 * i] = v.x;
+            wd[4 * i + 1] = v.y;
+            wd[4 * i + 2] = v.z;
+            wd[4 * i + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            uint32_t x = 0;
+            for (int b = 0; b < 4; ++b) {
+                const uint64_t a = c0 + 4 * i + b;
+                if (a < len) x |= (uint32_t)buf[a] << (8 * b);
+            }
+            wd[i] = x;
+        }
+    }
+}
+
+// The reduction tree of a tile: level 0 = the 128 lane maps, level k = 128 >> k maps, each the
+// composition of two maps of level k-1. Every level is kept for the emit pass's down-sweep.
+struct TileTree {
+    uint64_t m[2 * kTileLanes - 1][kEntries];
+};
+__device__ __forceinline__ int level_base(int k) { return 2 * kTileLanes - (2 * kTileLanes >> k); }
+constexpr int kLevels = 7;  // log2(kTileLanes)
+
+__device__ void tile_upsweep(TileTree& T, const uint32_t (&w)[kEntries]) {
+    const int l = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < kEntries; ++e) {
+        const uint32_t x = w[e];
+        const bool st = (x & kLStop) != 0;
+        const uint32_t pos = st ? (uint32_t)(l * kChunk) + l_pos(x) : l_pos(x);
+        T.m[l][e] = t_make(pos, st, l_ar(x), l_oth(x));
+    }
+    __syncthreads();
+    for (int k = 1; k <= kLevels; ++k) {
+        const int nodes = kTileLanes >> k;
+        const int src = level_base(k - 1), dst = level_base(k);
+        for (int t = l; t < nodes * kEntries; t += kTileLanes) {
+            const int j = t / kEntries, e = t % kEntries;
+            T.m[dst + j][e] = t_compose(T.m[src + 2 * j][e], T.m[src + 2 * j + 1]);
+        }
+        __syncthreads();
+    }
+}
+
+// map entry across tiles: pos (bit 31 = stop: absolute stop position in bits 0..30; else exit
+// offset into the next tile), AcceptReplies and other frames passed
+struct GEntry {
+    uint32_t pos, ar, oth;
+};
+constexpr uint32_t kGStop = 1u << 31;
+
+}  // namespace
+
+// ---- pass A: tile maps -------------------------------------------------------------------------
+__global__ __launch_bounds__(kTileLanes) void k_dec_tile_maps(const uint8_t* __restrict__ buf,
+                                                              uint64_t len,
+                                                              GEntry* __restrict__ tmap) {
+    __shared__ TileTree T;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kTileBytes;
+    const uint64_t c0 = t0 + (uint64_t)threadIdx.x * kChunk;
+    uint32_t wd[16], w[kEntries];
+    load_chunk(buf, len, c0, wd);
+    lane_map(wd, c0, len, w);
+    tile_upsweep(T, w);
+    if (threadIdx.x < kEntries) {
+        const uint64_t x = T.m[level_base(kLevels)][threadIdx.x];
+        GEntry g;
+        g.pos = t_stop(x) ? (kGStop | (uint32_t)(t0 + t_pos(x))) : t_pos(x);
+        g.ar = t_ar(x);
+        g.oth = t_oth(x);
+        tmap[(uint64_t)blockIdx.x * kEntries + threadIdx.x] = g;
+    }
+}
+
+// ---- pass B1: group maps (a group = 256 consecutive tiles; lane e walks entry e) -------------
+__global__ __launch_bounds__(256) void k_dec_group_maps(const GEntry* __restrict__ tmap,
+                                                        uint32_t n_tiles,
+                                                        GEntry* __restrict__ gmap) {
+    __shared__ GEntry S[kGroupTiles][kEntries];
+    const uint32_t g = blockIdx.x, first = g * kGroupTiles;
+    const uint32_t nt = min((uint32_t)kGroupTiles, n_tiles - first);
+    for (uint32_t i = threadIdx.x; i < nt * kEntries; i += blockDim.x)
+        (&S[0][0])[i] = tmap[(uint64_t)first * kEntries + i];
+    __syncthreads();
+    if (threadIdx.x < kEntries) {
+        GEntry a = S[0][threadIdx.x];
+        for (uint32_t t = 1; t < nt && !(a.pos & kGStop); ++t) {
+            const GEntry y = S[t][a.pos];
+            a = GEntry{y.pos, a.ar + y.ar, a.oth + y.oth};
+        }
+        gmap[(uint64_t)g * kEntries + threadIdx.x] = a;
+    }
+}
+
+// ---- pass B2: the true chain through the group maps from entry 0 (one block; the maps are
+// staged in LDS 256 groups at a time and thread 0 walks them) ----------------------------------
+// gres[g] = {entry of group g (kDead past the stop), AcceptReplies before it, others before it}
+__global__ __launch_bounds__(256) void k_dec_walk(const GEntry* __restrict__ gmap,
+                                                  uint32_t n_groups, uint64_t len,
+                                                  const uint8_t* __restrict__ buf,
+                                                  GEntry* __restrict__ gres,
+                                                  mpx_decode_result* __restrict__ res) {
+    __shared__ GEntry S[kGroupTiles][kEntries];
+    __shared__ uint32_t st[4];  // e, ar, oth, stop (kDead = not yet)
+    if (threadIdx.x == 0) {
+        st[0] = 0;
+        st[1] = 0;
+        st[2] = 0;
+        st[3] = kDead;
+    }
+    for (uint32_t b0 = 0; b0 < n_groups; b0 += kGroupTiles) {
+        const uint32_t nb = min((uint32_t)kGroupTiles, n_groups - b0);
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nb * kEntries; i += blockDim.x)
+            (&S[0][0])[i] = gmap[(uint64_t)b0 * kEntries + i];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t e = st[0], ar = st[1], oth = st[2], stop = st[3];
+            for (uint32_t g = 0; g < nb; ++g) {
+                if (stop != kDead) {
+                    gres[b0 + g] = GEntry{kDead, ar, oth};
+                    continue;
+                }
+                gres[b0 + g] = GEntry{e, ar, oth};
+                const GEntry x = S[g][e];
+                ar += x.ar;
+                oth += x.oth;
+                if (x.pos & kGStop) stop = x.pos & ~kGStop;
+                else e = x.pos;
+            }
+            st[0] = e;
+            st[1] = ar;
+            st[2] = oth;
+            st[3] = stop;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // the chain always stops inside the last tile at the latest (position len)
+        const uint64_t stop = st[3] == kDead ? len : st[3];
+        res->consumed = stop;
+        res->n_accept_replies = st[1];
+        res->n_other = st[2];
+        int32_t why = MPX_DECODE_END, code = -1;
+        if (stop < len) {
+            code = buf[stop];
+            why = frame_len((uint32_t)code) == 0 ? MPX_DECODE_VARIABLE : MPX_DECODE_PARTIAL;
+        }
+        res->stop_reason = why;
+        res->stop_code = code;
+    }
+}
+
+// ---- pass B3: tile entries inside each group (thread 0 walks the group's tile maps) ---------
+__global__ __launch_bounds__(256) void k_dec_tile_entries(const GEntry* __restrict__ tmap,
+                                                          uint32_t n_tiles,
+                                                          const GEntry* __restrict__ gres,
+                                                          GEntry* __restrict__ tres) {
+    __shared__ GEntry S[kGroupTiles][kEntries];
+    const uint32_t g = blockIdx.x, first = g * kGroupTiles;
+    const uint32_t nt = min((uint32_t)kGroupTiles, n_tiles - first);
+    const GEntry r = gres[g];
+    if (r.pos == kDead) {
+        for (uint32_t t = threadIdx.x; t < nt; t += blockDim.x) tres[first + t] = GEntry{kDead, 0, 0};
+        return;
+    }
+    for (uint32_t i = threadIdx.x; i < nt * kEntries; i += blockDim.x)
+        (&S[0][0])[i] = tmap[(uint64_t)first * kEntries + i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t e = r.pos, ar = r.ar, oth = r.oth;
+        bool dead = false;
+        for (uint32_t t = 0; t < nt; ++t) {
+            if (dead) {
+                tres[first + t] = GEntry{kDead, 0, 0};
+                continue;
+            }
+            tres[first + t] = GEntry{e, ar, oth};
+            const GEntry x = S[t][e];
+            ar += x.ar;
+            oth += x.oth;
+            if (x.pos & kGStop) dead = true;
+            else e = x.pos;
+        }
+    }
+}
+
+// ---- pass C: chunk entries (tree down-sweep) and record emission ----------------------------
+__global__ __launch_bounds__(kTileLanes) void k_dec_emit(
+    const uint8_t* __restrict__ buf, uint64_t len, const GEntry* __restrict__ tres,
+    mpx_accept_reply* __restrict__ ar_out, uint64_t ar_cap, mpx_peer_frame* __restrict__ oth_out,
+    uint64_t oth_cap) {
+    __shared__ TileTree T;
+    __shared__ uint32_t E[2 * kTileLanes - 1][3];  // per tree node: entry, AR offset, other offset
+    const GEntry r = tres[blockIdx.x];
+    if (r.pos == kDead) return;  // uniform per block
+    const uint64_t t0 = (uint64_t)blockIdx.x * kTileBytes;
+    const uint64_t c0 = t0 + (uint64_t)threadIdx.x * kChunk;
+    const int l = threadIdx.x;
+    uint32_t wd[16], w[kEntries];
+    load_chunk(buf, len, c0, wd);
+    lane_map(wd, c0, len, w);
+    tile_upsweep(T, w);
+    if (l == 0) {
+        const int root = level_base(kLevels);
+        E[root][0] = r.pos;
+        E[root][1] = r.ar;
+        E[root][2] = r.oth;
+    }
+    __syncthreads();
+    for (int k = kLevels; k >= 1; --k) {
+        const int nodes = kTileLanes >> k;
+        const int src = level_base(k), dst = level_base(k - 1);
+        if (l < nodes) {
+            const uint32_t e = E[src + l][0], ar = E[src + l][1], oth = E[src + l][2];
+            E[dst + 2 * l][0] = e;
+            E[dst + 2 * l][1] = ar;
+            E[dst + 2 * l][2] = oth;
+            uint32_t re = kDead, rar = ar, roth = oth;
+            if (e != kDead) {
+                const uint64_t x = T.m[dst + 2 * l][e];
+                if (!t_stop(x)) re = t_pos(x);
+                rar += t_ar(x);
+                roth += t_oth(x);
+            }
+            E[dst + 2 * l + 1][0] = re;
+            E[dst + 2 * l + 1][1] = rar;
+            E[dst + 2 * l + 1][2] = roth;
+        }
+        __syncthreads();
+    }
+    const uint32_t e = E[l][0];
+    if (e == kDead) return;
+    uint64_t ar_i = E[l][1], oth_i = E[l][2];
+    // walk the chunk from its entry, emitting the frames that start inside it
+    for (uint32_t p = e; p < (uint32_t)kChunk;) {
+        const uint64_t ap = c0 + p;
+        if (ap >= len) break;
+        const uint32_t code = buf[ap];
+        const uint32_t fl = frame_len(code);
+        if (fl == 0 || ap + fl > len) break;
+        if (code == MPX_PEER_ACCEPT_REPLY) {
+            if (ar_i < ar_cap) {
+                const uint8_t* b = buf + ap + 1;  // Instance, OK, Ballot, Id (little endian)
+                mpx_accept_reply rec;
+                rec.instance = (int32_t)((uint32_t)b[0] | ((uint32_t)b[1] << 8) |
+                                         ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24));
+                rec.ok = b[4];
+                rec.ballot = (int32_t)((uint32_t)b[5] | ((uint32_t)b[6] << 8) |
+                                       ((uint32_t)b[7] << 16) | ((uint32_t)b[8] << 24));
+                rec.id = (int32_t)((uint32_t)b[9] | ((uint32_t)b[10] << 8) |
+                                   ((uint32_t)b[11] << 16) | ((uint32_t)b[12] << 24));
+                rec.pad[0] = rec.pad[1] = rec.pad[2] = 0;
+                ar_out[ar_i] = rec;
+            }
+            ++ar_i;
+        } else {
+            if (oth_i < oth_cap) {
+                mpx_peer_frame f;
+                f.offset = (uint32_t)ap;
+                f.code = (uint8_t)code;
+                f.pad[0] = f.pad[1] = f.pad[2] = 0;
+                oth_out[oth_i] = f;
+            }
+            ++oth_i;
+        }
+        p += fl;
+    }
+}
+
+__global__ void k_dec_empty(mpx_decode_result* res) {
+    res->consumed = 0;
+    res->n_accept_replies = 0;
+    res->n_other = 0;
+    res->stop_reason = MPX_DECODE_END;
+    res->stop_code = -1;
+}
+
+uint64_t decode_work_bytes(uint64_t len) {
+    const uint64_t tiles = (len + kTileBytes - 1) / kTileBytes;
+    const uint64_t groups = (tiles + kGroupTiles - 1) / kGroupTiles;
+    return (tiles * (kEntries + 1) + groups * (kEntries + 1)) * sizeof(GEntry) + 256;
+}
+
+hipError_t launch_decode_peer_stream(const uint8_t* buf, uint64_t len, mpx_accept_reply* ar_out,
+                                     uint64_t ar_cap, mpx_peer_frame* oth_out, uint64_t oth_cap,
+                                     mpx_decode_result* res, void* work, uint64_t work_bytes,
+                                     hipStream_t stream) {
+    if (len > (uint64_t)MPX_DECODE_MAX_BYTES) return hipErrorInvalidValue;
+    if (work_bytes < decode_work_bytes(len)) return hipErrorInvalidValue;
+    if (len == 0) {
+        k_dec_empty<<<1, 1, 0, stream>>>(res);
+        return hipGetLastError();
+    }
+    const uint32_t tiles = (uint32_t)((len + kTileBytes - 1) / kTileBytes);
+    const uint32_t groups = (tiles + kGroupTiles - 1) / kGroupTiles;
+    GEntry* tmap = (GEntry*)work;
+    GEntry* tres = tmap + (uint64_t)tiles * kEntries;
+    GEntry* gmap = tres + tiles;
+    GEntry* gres = gmap + (uint64_t)groups * kEntries;
+    k_dec_tile_maps<<<tiles, kTileLanes, 0, stream>>>(buf, len, tmap);
+    k_dec_group_maps<<<groups, 256, 0, stream>>>(tmap, tiles, gmap);
+    k_dec_walk<<<1, 256, 0, stream>>>(gmap, groups, len, buf, gres, res);
+    k_dec_tile_entries<<<groups, 256, 0, stream>>>(tmap, tiles, gres, tres);
+    k_dec_emit<<<tiles, kTileLanes, 0, stream>>>(buf, len, tres, ar_out, ar_cap, oth_out,
+                                                 oth_cap);
+    return hipGetLastError();
+}
+
+}  // namespace mpx

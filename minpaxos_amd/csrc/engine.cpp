@@ -37,6 +37,9 @@ struct mpx_engine {
     mpx::KvTable kv{};
     bool kv_ready = false;
     DevBuf apply_work;
+    // peer stream decode: staging (bytes, AcceptReplies, other frames, result) + scratch
+    DevBuf dec[4];
+    DevBuf decode_work;
     uint64_t apply_chunk = 0;  // commands per apply chunk (0 = kApplyChunkDefault)
     // group-step work list (groups the fast kernel hands to the general kernel) + its count
     DevBuf worklist;
@@ -216,6 +219,9 @@ int mpx_close(mpx_engine* e) {
     for (auto& x : e->b)
         if (x.p) (void)hipFree(x.p);
     if (e->apply_work.p) (void)hipFree(e->apply_work.p);
+    for (auto& x : e->dec)
+        if (x.p) (void)hipFree(x.p);
+    if (e->decode_work.p) (void)hipFree(e->decode_work.p);
     if (e->worklist.p) (void)hipFree(e->worklist.p);
     if (e->d_wcount) (void)hipFree(e->d_wcount);
     if (e->kv_ready) {
@@ -684,6 +690,60 @@ int mpx_watermarks_allreduce(mpx_engine* e, int32_t* committed, int32_t* execute
     CK(mpx_watermarks_allreduce_dev(e, d, n_groups, e->stream));
     CK(d2h(e, committed, d, n_groups * 4));
     CK(d2h(e, executed, d + n_groups, n_groups * 4));
+    return finish(e);
+}
+
+// ---- §8(f) rank 1: peer stream framing + AcceptReply decode --------------------------------
+int mpx_decode_reserve(mpx_engine* e, size_t max_len) {
+    if (!e) return MPX_E_INVAL;
+    if (max_len > MPX_DECODE_MAX_BYTES)
+        return fail(e, MPX_E_UNSUPPORTED, "decode buffers are limited to 2^31-1 bytes per call");
+    CK(begin(e));
+    GROW(e, e->decode_work, mpx::decode_work_bytes(max_len));
+    return finish(e);
+}
+
+int mpx_decode_peer_stream_dev(mpx_engine* e, const uint8_t* d_buf, size_t len,
+                               mpx_accept_reply* d_ar, size_t ar_cap, mpx_peer_frame* d_other,
+                               size_t other_cap, mpx_decode_result* d_res, void* stream) {
+    if (!e || !d_res || (len && !d_buf) || (ar_cap && !d_ar) || (other_cap && !d_other))
+        return MPX_E_INVAL;
+    if (len > MPX_DECODE_MAX_BYTES)
+        return fail(e, MPX_E_UNSUPPORTED, "decode buffers are limited to 2^31-1 bytes per call");
+    if (e->decode_work.cap < mpx::decode_work_bytes(len))
+        return fail(e, MPX_E_INVAL,
+                    "mpx_decode_peer_stream_dev: call mpx_decode_reserve(len) first (the dev "
+                    "entry point never allocates)");
+    HIPCHK(e, mpx::launch_decode_peer_stream(d_buf, len, d_ar, ar_cap, d_other, other_cap, d_res,
+                                             e->decode_work.p, e->decode_work.cap,
+                                             pick(e, stream)));
+    return MPX_OK;
+}
+
+int mpx_decode_peer_stream(mpx_engine* e, const uint8_t* buf, size_t len, mpx_accept_reply* ar,
+                           size_t ar_cap, mpx_peer_frame* other, size_t other_cap,
+                           mpx_decode_result* res) {
+    if (!e || !res || (len && !buf) || (ar_cap && !ar) || (other_cap && !other))
+        return MPX_E_INVAL;
+    if (len > MPX_DECODE_MAX_BYTES)
+        return fail(e, MPX_E_UNSUPPORTED, "decode buffers are limited to 2^31-1 bytes per call");
+    CK(begin(e));
+    GROW(e, e->dec[0], len);
+    GROW(e, e->dec[1], ar_cap * sizeof(mpx_accept_reply));
+    GROW(e, e->dec[2], other_cap * sizeof(mpx_peer_frame));
+    GROW(e, e->dec[3], sizeof(mpx_decode_result));
+    GROW(e, e->decode_work, mpx::decode_work_bytes(len));
+    CK(h2d(e, e->dec[0].p, buf, len));
+    CK(mpx_decode_peer_stream_dev(e, (const uint8_t*)e->dec[0].p, len,
+                                  (mpx_accept_reply*)e->dec[1].p, ar_cap,
+                                  (mpx_peer_frame*)e->dec[2].p, other_cap,
+                                  (mpx_decode_result*)e->dec[3].p, e->stream));
+    CK(d2h(e, res, e->dec[3].p, sizeof(mpx_decode_result)));
+    CK(finish(e));
+    CK(d2h(e, ar, e->dec[1].p, std::min<uint64_t>(res->n_accept_replies, ar_cap) *
+                                   sizeof(mpx_accept_reply)));
+    CK(d2h(e, other, e->dec[2].p, std::min<uint64_t>(res->n_other, other_cap) *
+                                      sizeof(mpx_peer_frame)));
     return finish(e);
 }
 

@@ -80,4 +80,11 @@ hipError_t launch_kv_import(KvTable& t, const int64_t* keys, const int64_t* vals
 hipError_t launch_kv_export(KvTable& t, int64_t* keys, int64_t* vals, uint64_t cap,
                             unsigned long long* counter, hipStream_t stream);
 
+// ---- peer stream framing (mpx_decode_peer_stream) ---------------------------------------
+uint64_t decode_work_bytes(uint64_t len);
+hipError_t launch_decode_peer_stream(const uint8_t* buf, uint64_t len, mpx_accept_reply* ar_out,
+                                     uint64_t ar_cap, mpx_peer_frame* oth_out, uint64_t oth_cap,
+                                     mpx_decode_result* res, void* work, uint64_t work_bytes,
+                                     hipStream_t stream);
+
 }  // namespace mpx

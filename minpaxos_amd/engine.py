@@ -8,6 +8,7 @@ Names and argument meaning follow the reference handlers they replace:
   conflict_batch      <- state.ConflictBatch
   committed_prefix    <- updateCommittedUpTo
   group_step          <- handleAcceptReply + executeCommands for many replicas at once
+  decode_peer_stream  <- genericsmr.replicaListener framing + AcceptReply.Unmarshal
 Errors come back as MpxError carrying the reference-level reason (e.g. E_NIL_INSTANCE where the
 Go handler would dereference a nil *Instance).
 """
@@ -241,6 +242,35 @@ class Engine:
 
     def group_step_dev(self, gb, stream=None):
         self._check(self.lib.mpx_group_step_dev(self.h, C.byref(gb), stream), "mpx_group_step_dev")
+
+    # ---- peer stream framing ------------------------------------------
+    def decode_peer_stream(self, buf, ar_cap=None, other_cap=None):
+        """Frame one peer connection's bytes. Returns (accept_replies, other_frames, result):
+        AcceptReplies in arrival order (mpx_accept_reply), the other fixed-size frames as
+        (offset, code), and the mpx_decode_result (consumed, counts, stop reason / code)."""
+        buf = np.frombuffer(buf, np.uint8) if isinstance(buf, (bytes, bytearray)) else \
+            _c(buf, np.uint8)
+        n = len(buf)
+        ar_cap = n // 14 + 1 if ar_cap is None else ar_cap
+        other_cap = n + 1 if other_cap is None else other_cap
+        ar = np.zeros(max(ar_cap, 1), R.ACCEPT_REPLY)
+        oth = np.zeros(max(other_cap, 1), R.PEER_FRAME)
+        res = np.zeros(1, R.DECODE_RESULT)
+        self._check(self.lib.mpx_decode_peer_stream(self.h, _ptr(buf), n, _ptr(ar), ar_cap,
+                                                    _ptr(oth), other_cap, _ptr(res)),
+                    "mpx_decode_peer_stream")
+        r = res[0]
+        return (ar[:min(int(r["n_accept_replies"]), ar_cap)],
+                oth[:min(int(r["n_other"]), other_cap)], r)
+
+    def decode_reserve(self, max_len):
+        self._check(self.lib.mpx_decode_reserve(self.h, max_len), "mpx_decode_reserve")
+
+    def decode_peer_stream_dev(self, d_buf, n, d_ar, ar_cap, d_other, other_cap, d_res,
+                               stream=None):
+        self._check(self.lib.mpx_decode_peer_stream_dev(self.h, d_buf, n, d_ar, ar_cap, d_other,
+                                                        other_cap, d_res, stream),
+                    "mpx_decode_peer_stream_dev")
 
     # ---- multi-GPU ----------------------------------------------------------------------------
     @staticmethod

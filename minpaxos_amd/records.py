@@ -53,6 +53,21 @@ GROUP_PREP_STATE = np.dtype([("default_ballot", "<i4"), ("prepare_oks", "<i4"), 
 # mpx_prepare_effect
 PREPARE_EFFECT = np.dtype([("flags", "<u4"), ("catchup_from", "<i4")])
 
+# peer-stream frame codes (include/mpx.h MPX_PEER_*; genericsmrproto.go:7-18 and the RPC
+# registration order of bareminpaxos.NewReplica, bareminpaxos.go:108-113)
+PEER_BEACON, PEER_BEACON_REPLY, PEER_PREPARE, PEER_ACCEPT, PEER_COMMIT = 6, 7, 8, 9, 10
+PEER_COMMIT_SHORT, PEER_PREPARE_REPLY, PEER_ACCEPT_REPLY = 11, 12, 13
+# body bytes after the code byte (None = variable length; unknown codes have none)
+PEER_BODY = {PEER_BEACON: 8, PEER_BEACON_REPLY: 8, PEER_PREPARE: 12, PEER_COMMIT_SHORT: 16,
+             PEER_ACCEPT_REPLY: 13, PEER_ACCEPT: None, PEER_COMMIT: None, PEER_PREPARE_REPLY: None}
+DECODE_END, DECODE_PARTIAL, DECODE_VARIABLE = 0, 1, 2
+DECODE_MAX_BYTES = 0x7FFFFFFF
+# mpx_peer_frame / mpx_decode_result
+PEER_FRAME = np.dtype([("offset", "<u4"), ("code", "u1"), ("pad", "u1", (3,))])
+DECODE_RESULT = np.dtype([("consumed", "<u8"), ("n_accept_replies", "<u8"), ("n_other", "<u8"),
+                          ("stop_reason", "<i4"), ("stop_code", "<i4")])
+
+assert PEER_FRAME.itemsize == 8 and DECODE_RESULT.itemsize == 32
 assert ACCEPT_REPLY.itemsize == 16 and INST_STATE.itemsize == 16
 assert PREPARE_REPLY.itemsize == 16 and PREP_STATE.itemsize == 32
 assert PREPARE_REPLY_MIN.itemsize == 24 and GROUP_PREP_STATE.itemsize == 32

@@ -175,3 +175,56 @@ def group_batch(n_groups, ipg=256, n_replicas=5, cmds_per_inst=4, keys_per_group
         executed_in=np.full(n_groups, -1, np.int32),
         peer_in=np.zeros(n_groups * n_replicas, np.int32), op=op, key=key, val=val,
         cmd_off=cmd_off)
+
+
+def peer_stream(recs, seed=47, p_beacon=0.0, p_prepare=0.0, p_commit_short=0.0, p_unknown=0.0,
+                tail=None):
+    """A peer connection's bytes: every AcceptReply of `recs` (mpx_accept_reply, arrival order)
+    framed as [13][Instance i32][OK u8][Ballot i32][Id i32] (minpaxosprotomarsh.go:545-566),
+    with other fixed-size frames interleaved before AcceptReply k with the given per-frame
+    probabilities: Beacon [6][ts u64], Prepare [8][12 B], CommitShort [11][16 B], or one byte
+    of an unregistered code. `tail`: bytes appended at the end (e.g. a partial frame or the
+    start of a variable-length one). Returns a uint8 array."""
+    n = len(recs)
+    u = stream(seed, 20, 0, n)
+    lim = lambda p: np.uint64(int(p * (1 << 24)))  # noqa: E731
+    r = u & np.uint64(0xFFFFFF)
+    kind = np.zeros(n, np.int8)  # 0 none, 1 beacon, 2 prepare, 3 commit short, 4 unknown
+    a = lim(p_beacon)
+    b = a + lim(p_prepare)
+    c = b + lim(p_commit_short)
+    d = c + lim(p_unknown)
+    kind[r < a] = 1
+    kind[(r >= a) & (r < b)] = 2
+    kind[(r >= b) & (r < c)] = 3
+    kind[(r >= c) & (r < d)] = 4
+    pre = np.array([0, 9, 13, 17, 1], np.int64)[kind]
+    size = pre + 14
+    off = np.zeros(n + 1, np.int64)
+    np.cumsum(size, out=off[1:])
+    extra = b"" if tail is None else bytes(tail)
+    buf = np.zeros(int(off[-1]) + len(extra), np.uint8)
+    pay = stream(seed, 21, 0, n)  # payload bytes of the interleaved frames
+    for k, code, body in ((1, R.PEER_BEACON, 8), (2, R.PEER_PREPARE, 12),
+                          (3, R.PEER_COMMIT_SHORT, 16)):
+        at = off[:-1][kind == k]
+        buf[at] = code
+        pk = pay[kind == k]
+        for j in range(body):
+            buf[at + 1 + j] = ((pk >> np.uint64((8 * j) % 64)) & np.uint64(0xFF)).astype(np.uint8)
+    unk = off[:-1][kind == 4]
+    codes = (pay[kind == 4] % np.uint64(251)).astype(np.int64)
+    codes = np.where((codes >= 6) & (codes <= 13), codes + 20, codes)  # never a registered code
+    buf[unk] = codes.astype(np.uint8)
+    at = off[:-1] + pre
+    buf[at] = R.PEER_ACCEPT_REPLY
+    fields = ((1, recs["instance"].astype("<i4")), (6, recs["ballot"].astype("<i4")),
+              (10, recs["id"].astype("<i4")))
+    for o, v in fields:
+        vb = v.view(np.uint8).reshape(n, 4)
+        for j in range(4):
+            buf[at + o + j] = vb[:, j]
+    buf[at + 5] = recs["ok"]
+    if extra:
+        buf[int(off[-1]):] = np.frombuffer(extra, np.uint8)
+    return buf

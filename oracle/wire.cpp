@@ -1,0 +1,96 @@
+// oracle/wire.cpp — TEST INFRASTRUCTURE ONLY. CPU restatement of the peer-stream framing
+// (SURVEY §8(f) rank 1); the parity checker for minpaxos_amd/csrc/decode.hip.
+//
+// genericsmr.(*Replica).replicaListener  src/genericsmr/genericsmr.go:402-446, one frame per
+// loop iteration: ReadByte() the code (:410), then
+//   GENERIC_SMR_BEACON / _REPLY (6, 7): Beacon/BeaconReply.Unmarshal, 8 bytes (:414-428)
+//   rpcTable codes (:433-439), registered 8..13 by bareminpaxos.NewReplica (:108-113):
+//     Prepare.Unmarshal          ReadAtLeast 12   minpaxosprotomarsh.go:259-270
+//     Accept / Commit / PrepareReply: varint-prefixed slices (:470-507, :648-672, :352-387)
+//     CommitShort.Unmarshal      ReadAtLeast 16   :737-749
+//     AcceptReply.Unmarshal      13 bytes, LE     :568-580 (written by Marshal :545-566)
+//   anything else: log "unknown message type" and continue with the next byte (:440-442).
+// The engine's contract stops at variable-length frames and at a frame that runs past the end
+// of the buffer (include/mpx.h, mpx_decode_peer_stream); this restatement does the same.
+#include <cstdint>
+#include <cstring>
+
+#include "../include/mpx.h"
+
+namespace {
+
+int32_t le32(const uint8_t* b) {
+    return (int32_t)((uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) |
+                     ((uint32_t)b[3] << 24));
+}
+
+// body length after the code byte; -1 = variable-length message
+int body_len(uint8_t code) {
+    switch (code) {
+    case MPX_PEER_BEACON:
+    case MPX_PEER_BEACON_REPLY: return 8;
+    case MPX_PEER_PREPARE: return 12;
+    case MPX_PEER_COMMIT_SHORT: return 16;
+    case MPX_PEER_ACCEPT_REPLY: return 13;
+    case MPX_PEER_ACCEPT:
+    case MPX_PEER_COMMIT:
+    case MPX_PEER_PREPARE_REPLY: return -1;
+    default: return 0;  // unknown code: only the code byte is consumed
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int orc_decode_peer_stream(const uint8_t* buf, size_t len, mpx_accept_reply* ar, size_t ar_cap,
+                           mpx_peer_frame* other, size_t other_cap, mpx_decode_result* res) {
+    size_t p = 0;
+    uint64_t n_ar = 0, n_oth = 0;
+    int32_t why = MPX_DECODE_END, code_at = -1;
+    while (p < len) {
+        const uint8_t code = buf[p];
+        const int bl = body_len(code);
+        if (bl < 0) {
+            why = MPX_DECODE_VARIABLE;
+            code_at = code;
+            break;
+        }
+        if (p + 1 + (size_t)bl > len) {
+            why = MPX_DECODE_PARTIAL;
+            code_at = code;
+            break;
+        }
+        if (code == MPX_PEER_ACCEPT_REPLY) {
+            const uint8_t* b = buf + p + 1;
+            if (n_ar < ar_cap) {
+                mpx_accept_reply r;
+                memset(&r, 0, sizeof(r));
+                r.instance = le32(b);      // t.Instance  bs[0:4]
+                r.ok = b[4];               // t.OK        bs[4]
+                r.ballot = le32(b + 5);    // t.Ballot    bs[5:9]
+                r.id = le32(b + 9);        // t.Id        bs[9:13]
+                ar[n_ar] = r;
+            }
+            ++n_ar;
+        } else {
+            if (n_oth < other_cap) {
+                mpx_peer_frame f;
+                memset(&f, 0, sizeof(f));
+                f.offset = (uint32_t)p;
+                f.code = code;
+                other[n_oth] = f;
+            }
+            ++n_oth;
+        }
+        p += 1 + (size_t)bl;
+    }
+    res->consumed = p;
+    res->n_accept_replies = n_ar;
+    res->n_other = n_oth;
+    res->stop_reason = why;
+    res->stop_code = code_at;
+    return MPX_OK;
+}
+
+}  // extern "C"

@@ -61,6 +61,14 @@ def cases():
         out[f"group_step_config5_{mname}"] = ("group", dict(n=5, mode=mode, kv=512),
                                               {k: v for k, v in gb.items()
                                                if isinstance(v, np.ndarray)})
+    drec, _ = synth.accept_replies(750, 5, 0.7, seed=48)
+    out["decode_mixed"] = ("decode", dict(), dict(buf=synth.peer_stream(
+        drec, seed=49, p_beacon=0.02, p_prepare=0.01, p_commit_short=0.01, p_unknown=0.03,
+        tail=bytes([R.PEER_ACCEPT_REPLY, 7, 0, 0]))))
+    head = synth.peer_stream(drec[:1000], seed=50, p_beacon=0.01)
+    var = np.array([R.PEER_PREPARE_REPLY, 1, 0, 0, 0], np.uint8)
+    out["decode_variable_stop"] = ("decode", dict(), dict(buf=np.concatenate(
+        [head, var, synth.peer_stream(drec[1000:], seed=51)])))
     return out
 
 
@@ -91,6 +99,10 @@ def run_case(kind, p, x, backend_mk):
         gbat = dict(x, n_groups=len(x["committed_in"]), ipg=len(x["st_in"]) // len(x["committed_in"]))
         o = b.group_step(gbat)
         return {k: v for k, v in o.items() if v is not None}
+    if kind == "decode":
+        b = backend_mk(5, R.MODE_MIN)
+        ar, oth, res = b.decode_peer_stream(x["buf"])
+        return dict(ar=ar, other=oth, res=np.array([res], R.DECODE_RESULT))
     raise ValueError(kind)
 
 

@@ -50,6 +50,7 @@ def load():
         "orc_group_step": (C.c_int, [C.c_int, C.c_int, C.POINTER(L.MpxGroupBatch), C.c_uint32]),
         "orc_bench_accept": (C.c_int64, [C.c_int, C.c_int, _p, _sz, _p, _sz, _i32, _p, _p]),
         "orc_bench_apply": (C.c_int64, [_p, _p, _sz, _p, _p, _p, _sz, _p]),
+        "orc_decode_peer_stream": (C.c_int, [_p, _sz, _p, _sz, _p, _sz, _p]),
         "orc_bench_group_step": (C.c_int64, [C.c_int, C.c_int, C.POINTER(L.MpxGroupBatch),
                                              C.c_uint32, C.c_int]),
     }
@@ -164,6 +165,21 @@ class Oracle:
         _check(self.lib.orc_conflict_batch(_ptr(op), _ptr(key), _ptr(off), n_inst, _ptr(out)),
                "orc_conflict_batch")
         return out[:max(n_inst - 1, 0)]
+
+    def decode_peer_stream(self, buf, ar_cap=None, other_cap=None):
+        buf = np.frombuffer(buf, np.uint8) if isinstance(buf, (bytes, bytearray)) else \
+            np.ascontiguousarray(buf, np.uint8)
+        n = len(buf)
+        ar_cap = n // 14 + 1 if ar_cap is None else ar_cap
+        other_cap = n + 1 if other_cap is None else other_cap
+        ar = np.zeros(max(ar_cap, 1), R.ACCEPT_REPLY)
+        oth = np.zeros(max(other_cap, 1), R.PEER_FRAME)
+        res = np.zeros(1, R.DECODE_RESULT)
+        _check(self.lib.orc_decode_peer_stream(_ptr(buf), n, _ptr(ar), ar_cap, _ptr(oth),
+                                               other_cap, _ptr(res)), "orc_decode_peer_stream")
+        r = res[0]
+        return (ar[:min(int(r["n_accept_replies"]), ar_cap)],
+                oth[:min(int(r["n_other"]), other_cap)], r)
 
     def group_step(self, b, kv_cnt=None, kv_key=None, kv_val=None, ret=None, want_conf=True,
                    want_decided=True):
