@@ -14,17 +14,18 @@
 // runs past the end of the buffer (a partial read: the host keeps the tail).
 //
 // Framing is sequential by nature (each frame's start depends on every earlier length). The
-// engine makes it data parallel with entry maps: a frame that starts in a 64-byte chunk ends at
+// engine makes it data parallel with entry maps: a frame that starts in a 128-byte chunk ends at
 // most 16 bytes into the next one (the longest fixed frame is 17 bytes), so a chunk's behaviour
 // is a function from its entry offset (0..16) to (exit offset into the next chunk | stop
 // position, AcceptReplies and other frames passed on the way). Each lane computes its chunk's
 // 17-entry map with a register-window DP over the chunk's bytes (the possible lengths are 1, 9,
 // 13, 14 and 17, so the DP only looks back at fixed distances). Maps compose associatively: a
-// workgroup reduces its 128 chunk maps to an 8 KB tile map (tree in LDS), 256 tile maps reduce
+// workgroup reduces its 128 chunk maps to a 16 KB tile map (tree in LDS), 256 tile maps reduce
 // to a group map, one block walks the group maps from entry 0, and the down-sweeps hand every
 // tile, then every chunk, its true entry and output offsets; the chunks then emit their records.
 // HBM traffic: the stream is read twice (maps, emit), the records written once; the maps are
-// 204 bytes per 8 KB tile.
+// 204 bytes per 16 KB tile plus a 16-byte exit map per 128-byte chunk, which the emit pass reads
+// instead of recomputing the DP.
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -32,7 +33,7 @@ namespace mpx {
 
 namespace {
 
-constexpr int kChunk = 64;                 // bytes per lane
+constexpr int kChunk = 128;                // bytes per lane
 constexpr int kTileLanes = 128;            // lanes per tile workgroup
 constexpr int kTileBytes = kChunk * kTileLanes;
 constexpr int kEntries = 17;               // entry offsets 0..16
@@ -54,11 +55,12 @@ static_assert(MPX_PEER_BEACON == 6 && MPX_PEER_BEACON_REPLY == 7 && MPX_PEER_PRE
               "kLenLut is laid out for codes 6..13");
 
 // lane-map entry (u32): [0..6] pos (exit offset into the next chunk, or stop offset in the
-// chunk), [7] stop, [8..11] AcceptReplies, [12..18] other frames
+// chunk), [7] stop, [8..11] AcceptReplies (<= 128/14), [12..19] other frames (<= 128)
 constexpr uint32_t kLStop = 1u << 7;
 __device__ __forceinline__ uint32_t l_pos(uint32_t x) { return x & 0x7Fu; }
 __device__ __forceinline__ uint32_t l_ar(uint32_t x) { return (x >> 8) & 0xFu; }
-__device__ __forceinline__ uint32_t l_oth(uint32_t x) { return (x >> 12) & 0x7Fu; }
+__device__ __forceinline__ uint32_t l_oth(uint32_t x) { return (x >> 12) & 0xFFu; }
+static_assert(kChunk <= 128, "lane-map fields are sized for 128-byte chunks");
 
 // tile-level entry (u64): [0..15] pos (exit offset, or stop offset from the tile start),
 // [16] stop, [17..32] AcceptReplies, [33..48] other frames
@@ -78,13 +80,14 @@ __device__ __forceinline__ uint64_t t_compose(uint64_t a, const uint64_t* b) {
            ((uint64_t)(t_oth(a) + t_oth(y)) << 33);
 }
 
-// The lane's 64-byte chunk -> its 17 map entries (w[k] = entry k) by a backward DP over the
+// The lane's chunk -> its 17 map entries (w[k] = entry k) by a backward DP over the
 // chunk's positions: dp[p] = frame p reaches past the chunk ? exit : dp[p + len(p)] + frame p.
 // Before step p the window holds w[k] = dp[p+1+k]; the lengths are compile-time offsets into it.
-// kEdge: the chunk is within 81 bytes of the end of the buffer, so positions past the end and
+// kEdge: the chunk ends within 17 bytes of the end of the buffer, so positions past the end and
 // frames running past it must be checked (every other chunk skips both tests).
 template <bool kEdge>
-__device__ __forceinline__ void lane_map_dp(const uint32_t (&wd)[16], uint32_t c0, uint32_t len,
+__device__ __forceinline__ void lane_map_dp(const uint32_t (&wd)[kChunk / 4], uint32_t c0,
+                                            uint32_t len,
                                             uint32_t (&w)[kEntries]) {
 #pragma unroll
     for (int k = 0; k < kEntries; ++k) w[k] = 0;
@@ -112,18 +115,19 @@ __device__ __forceinline__ void lane_map_dp(const uint32_t (&wd)[16], uint32_t c
     }
 }
 
-__device__ __forceinline__ void lane_map(const uint32_t (&wd)[16], uint64_t c0, uint64_t len,
+__device__ __forceinline__ void lane_map(const uint32_t (&wd)[kChunk / 4], uint64_t c0,
+                                         uint64_t len,
                                          uint32_t (&w)[kEntries]) {
     if (c0 + kChunk + kEntries > len) lane_map_dp<true>(wd, (uint32_t)c0, (uint32_t)len, w);
     else lane_map_dp<false>(wd, (uint32_t)c0, (uint32_t)len, w);
 }
 
 __device__ __forceinline__ void load_chunk(const uint8_t* __restrict__ buf, uint64_t len,
-                                           uint64_t c0, uint32_t (&wd)[16]) {
+                                           uint64_t c0, uint32_t (&wd)[kChunk / 4]) {
     if (c0 + kChunk <= len) {
         const uint4* s = reinterpret_cast<const uint4*>(buf + c0);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < kChunk / 16; ++i) {
             const uint4 v = s[i];
             wd[4 * i] = v.x;
             wd[4 * i + 1] = v.y;
@@ -132,7 +136,7 @@ __device__ __forceinline__ void load_chunk(const uint8_t* __restrict__ buf, uint
         }
     } else {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < kChunk / 4; ++i) {
             uint32_t x = 0;
             for (int b = 0; b < 4; ++b) {
                 const uint64_t a = c0 + 4 * i + b;
@@ -161,12 +165,26 @@ __device__ void tile_upsweep(TileTree& T, const uint32_t (&w)[kEntries]) {
         T.m[l][e] = t_make(pos, st, l_ar(x), l_oth(x));
     }
     __syncthreads();
+    // per level, every thread first loads all of its left operands, then composes (the loads
+    // of a level are independent, so they overlap instead of forming a latency chain)
+    constexpr int kMaxTasks = (kTileLanes / 2 * kEntries + kTileLanes - 1) / kTileLanes;
+#pragma unroll
     for (int k = 1; k <= kLevels; ++k) {
-        const int nodes = kTileLanes >> k;
+        const int total = (kTileLanes >> k) * kEntries;
         const int src = level_base(k - 1), dst = level_base(k);
-        for (int t = l; t < nodes * kEntries; t += kTileLanes) {
-            const int j = t / kEntries, e = t % kEntries;
-            T.m[dst + j][e] = t_compose(T.m[src + 2 * j][e], T.m[src + 2 * j + 1]);
+        uint64_t av[kMaxTasks];
+#pragma unroll
+        for (int i = 0; i < kMaxTasks; ++i) {
+            const int t = l + i * kTileLanes;
+            if (t < total) av[i] = T.m[src + 2 * (t / kEntries)][t % kEntries];
+        }
+#pragma unroll
+        for (int i = 0; i < kMaxTasks; ++i) {
+            const int t = l + i * kTileLanes;
+            if (t < total) {
+                const int j = t / kEntries;
+                T.m[dst + j][t % kEntries] = t_compose(av[i], T.m[src + 2 * j + 1]);
+            }
         }
         __syncthreads();
     }
@@ -182,15 +200,38 @@ constexpr uint32_t kGStop = 1u << 31;
 }  // namespace
 
 // ---- pass A: tile maps -------------------------------------------------------------------------
+// exit map of a chunk for the emit pass: 6 bits per entry (exit offset, or kXStop), entries
+// 0..9 in the low 64 bits, 10..16 in the high 64 bits
+constexpr uint32_t kXStop = 63u;
+__device__ __forceinline__ ulonglong2 pack_exits(const uint32_t (&w)[kEntries]) {
+    uint64_t lo = 0, hi = 0;
+#pragma unroll
+    for (int e = 0; e < kEntries; ++e) {
+        const uint64_t x = (w[e] & kLStop) ? kXStop : l_pos(w[e]);
+        if (e < 10) lo |= x << (6 * e);
+        else hi |= x << (6 * (e - 10));
+    }
+    return make_ulonglong2(lo, hi);
+}
+
 __global__ __launch_bounds__(kTileLanes) void k_dec_tile_maps(const uint8_t* __restrict__ buf,
                                                               uint64_t len,
-                                                              GEntry* __restrict__ tmap) {
+                                                              GEntry* __restrict__ tmap,
+                                                              ulonglong2* __restrict__ xmap) {
     __shared__ TileTree T;
     const uint64_t t0 = (uint64_t)blockIdx.x * kTileBytes;
     const uint64_t c0 = t0 + (uint64_t)threadIdx.x * kChunk;
-    uint32_t wd[16], w[kEntries];
+    uint32_t wd[kChunk / 4], w[kEntries];
     load_chunk(buf, len, c0, wd);
     lane_map(wd, c0, len, w);
+    xmap[(uint64_t)blockIdx.x * kTileLanes + threadIdx.x] = pack_exits(w);
+#ifdef MPX_DEC_ABLATE_TREE
+    if (threadIdx.x < kEntries) {  // timing ablation only: skips the tile tree (wrong results)
+        tmap[(uint64_t)blockIdx.x * kEntries + threadIdx.x] = GEntry{w[threadIdx.x] & 15u, 0, 0};
+        return;
+    }
+    return;
+#endif
     tile_upsweep(T, w);
     if (threadIdx.x < kEntries) {
         const uint64_t x = T.m[level_base(kLevels)][threadIdx.x];
@@ -315,79 +356,115 @@ __global__ __launch_bounds__(256) void k_dec_tile_entries(const GEntry* __restri
     }
 }
 
-// ---- pass C: chunk entries (tree down-sweep) and record emission ----------------------------
+// ---- pass C: chunk entries (tree over the stored exit maps) and record emission -------------
+// The tile's bytes are staged in LDS; the true chain is walked per chunk twice (count, then
+// emit at the offsets of a block-wide exclusive scan of the counts).
+constexpr int kXPad = 20;  // bytes per exit map in LDS (17 used)
 __global__ __launch_bounds__(kTileLanes) void k_dec_emit(
     const uint8_t* __restrict__ buf, uint64_t len, const GEntry* __restrict__ tres,
-    mpx_accept_reply* __restrict__ ar_out, uint64_t ar_cap, mpx_peer_frame* __restrict__ oth_out,
-    uint64_t oth_cap) {
-    __shared__ TileTree T;
-    __shared__ uint32_t E[2 * kTileLanes - 1][3];  // per tree node: entry, AR offset, other offset
+    const ulonglong2* __restrict__ xmap, mpx_accept_reply* __restrict__ ar_out, uint64_t ar_cap,
+    mpx_peer_frame* __restrict__ oth_out, uint64_t oth_cap) {
+    __shared__ uint8_t X[2 * kTileLanes - 1][kXPad];
+    __shared__ uint8_t E[2 * kTileLanes - 1];  // entry per tree node (kXStop = dead)
+    __shared__ __attribute__((aligned(16))) uint8_t B[kTileBytes + 32];
+    __shared__ uint32_t wsum[kTileLanes / kWave];
     const GEntry r = tres[blockIdx.x];
     if (r.pos == kDead) return;  // uniform per block
     const uint64_t t0 = (uint64_t)blockIdx.x * kTileBytes;
-    const uint64_t c0 = t0 + (uint64_t)threadIdx.x * kChunk;
     const int l = threadIdx.x;
-    uint32_t wd[16], w[kEntries];
-    load_chunk(buf, len, c0, wd);
-    lane_map(wd, c0, len, w);
-    tile_upsweep(T, w);
-    if (l == 0) {
-        const int root = level_base(kLevels);
-        E[root][0] = r.pos;
-        E[root][1] = r.ar;
-        E[root][2] = r.oth;
+    // stage the tile (+32 bytes of the next) in LDS
+    for (int i = l; i < (kTileBytes + 32) / 16; i += kTileLanes) {
+        const uint64_t a = t0 + (uint64_t)i * 16;
+        uint4 v;
+        if (a + 16 <= len) {
+            v = *reinterpret_cast<const uint4*>(buf + a);
+        } else {
+            uint32_t q[4] = {0, 0, 0, 0};
+            for (int b = 0; b < 16; ++b)
+                if (a + b < len) q[b >> 2] |= (uint32_t)buf[a + b] << (8 * (b & 3));
+            v = make_uint4(q[0], q[1], q[2], q[3]);
+        }
+        *reinterpret_cast<uint4*>(&B[i * 16]) = v;
     }
+    {
+        const ulonglong2 m = xmap[(uint64_t)blockIdx.x * kTileLanes + l];
+#pragma unroll
+        for (int e = 0; e < kEntries; ++e)
+            X[l][e] = (uint8_t)((e < 10 ? m.x >> (6 * e) : m.y >> (6 * (e - 10))) & 63u);
+    }
+    __syncthreads();
+    for (int k = 1; k <= kLevels; ++k) {
+        const int nodes = kTileLanes >> k;
+        const int src = level_base(k - 1), dst = level_base(k);
+        for (int t = l; t < nodes * kEntries; t += kTileLanes) {
+            const int j = t / kEntries, e = t % kEntries;
+            const uint8_t a = X[src + 2 * j][e];
+            X[dst + j][e] = a == kXStop ? (uint8_t)kXStop : X[src + 2 * j + 1][a];
+        }
+        __syncthreads();
+    }
+    if (l == 0) E[level_base(kLevels)] = (uint8_t)r.pos;
     __syncthreads();
     for (int k = kLevels; k >= 1; --k) {
         const int nodes = kTileLanes >> k;
         const int src = level_base(k), dst = level_base(k - 1);
         if (l < nodes) {
-            const uint32_t e = E[src + l][0], ar = E[src + l][1], oth = E[src + l][2];
-            E[dst + 2 * l][0] = e;
-            E[dst + 2 * l][1] = ar;
-            E[dst + 2 * l][2] = oth;
-            uint32_t re = kDead, rar = ar, roth = oth;
-            if (e != kDead) {
-                const uint64_t x = T.m[dst + 2 * l][e];
-                if (!t_stop(x)) re = t_pos(x);
-                rar += t_ar(x);
-                roth += t_oth(x);
-            }
-            E[dst + 2 * l + 1][0] = re;
-            E[dst + 2 * l + 1][1] = rar;
-            E[dst + 2 * l + 1][2] = roth;
+            const uint8_t e = E[src + l];
+            E[dst + 2 * l] = e;
+            E[dst + 2 * l + 1] = e == kXStop ? (uint8_t)kXStop : X[dst + 2 * l][e];
         }
         __syncthreads();
     }
-    const uint32_t e = E[l][0];
-    if (e == kDead) return;
-    uint64_t ar_i = E[l][1], oth_i = E[l][2];
-    // walk the chunk from its entry, emitting the frames that start inside it
-    for (uint32_t p = e; p < (uint32_t)kChunk;) {
-        const uint64_t ap = c0 + p;
-        if (ap >= len) break;
-        const uint32_t code = buf[ap];
+    const uint32_t e = E[l];
+    // walk 1: frames starting in this chunk on the true chain
+    const uint32_t base = (uint32_t)l * kChunk;  // chunk start within the tile
+    const uint64_t tl = len - t0;               // bytes of the buffer from the tile start
+    uint32_t n_ar = 0, n_oth = 0;
+    if (e != kXStop) {
+        for (uint32_t p = base + e; p < base + kChunk;) {
+            const uint32_t code = B[p];
+            const uint32_t fl = frame_len(code);
+            if ((uint64_t)p >= tl || fl == 0 || (uint64_t)p + fl > tl) break;
+            if (code == MPX_PEER_ACCEPT_REPLY) ++n_ar;
+            else ++n_oth;
+            p += fl;
+        }
+    }
+    // block exclusive scan of (n_ar | n_oth << 16)
+    uint32_t v = n_ar | (n_oth << 16), inc = v;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t t = __shfl_up(inc, d);
+        if (lane_id() >= d) inc += t;
+    }
+    if (lane_id() == kWave - 1) wsum[l / kWave] = inc;
+    __syncthreads();
+    uint32_t pre = inc - v;
+    for (int w2 = 0; w2 < l / kWave; ++w2) pre += wsum[w2];
+    if (e == kXStop) return;
+    uint64_t ar_i = r.ar + (pre & 0xFFFFu), oth_i = r.oth + (pre >> 16);
+    // walk 2: emit
+    for (uint32_t p = base + e; p < base + kChunk;) {
+        const uint32_t code = B[p];
         const uint32_t fl = frame_len(code);
-        if (fl == 0 || ap + fl > len) break;
+        if ((uint64_t)p >= tl || fl == 0 || (uint64_t)p + fl > tl) break;
         if (code == MPX_PEER_ACCEPT_REPLY) {
-            if (ar_i < ar_cap) {
-                const uint8_t* b = buf + ap + 1;  // Instance, OK, Ballot, Id (little endian)
-                mpx_accept_reply rec;
-                rec.instance = (int32_t)((uint32_t)b[0] | ((uint32_t)b[1] << 8) |
-                                         ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24));
-                rec.ok = b[4];
-                rec.ballot = (int32_t)((uint32_t)b[5] | ((uint32_t)b[6] << 8) |
-                                       ((uint32_t)b[7] << 16) | ((uint32_t)b[8] << 24));
-                rec.id = (int32_t)((uint32_t)b[9] | ((uint32_t)b[10] << 8) |
-                                   ((uint32_t)b[11] << 16) | ((uint32_t)b[12] << 24));
-                rec.pad[0] = rec.pad[1] = rec.pad[2] = 0;
-                ar_out[ar_i] = rec;
-            }
+            const uint8_t* b = B + p + 1;  // Instance, OK, Ballot, Id (little endian)
+            mpx_accept_reply rec;
+            rec.instance = (int32_t)((uint32_t)b[0] | ((uint32_t)b[1] << 8) |
+                                     ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24));
+            rec.ok = b[4];
+            rec.ballot = (int32_t)((uint32_t)b[5] | ((uint32_t)b[6] << 8) |
+                                   ((uint32_t)b[7] << 16) | ((uint32_t)b[8] << 24));
+            rec.id = (int32_t)((uint32_t)b[9] | ((uint32_t)b[10] << 8) |
+                               ((uint32_t)b[11] << 16) | ((uint32_t)b[12] << 24));
+            rec.pad[0] = rec.pad[1] = rec.pad[2] = 0;
+            if (ar_i < ar_cap) ar_out[ar_i] = rec;
             ++ar_i;
         } else {
             if (oth_i < oth_cap) {
                 mpx_peer_frame f;
-                f.offset = (uint32_t)ap;
+                f.offset = (uint32_t)(t0 + p);
                 f.code = (uint8_t)code;
                 f.pad[0] = f.pad[1] = f.pad[2] = 0;
                 oth_out[oth_i] = f;
@@ -409,7 +486,8 @@ __global__ void k_dec_empty(mpx_decode_result* res) {
 uint64_t decode_work_bytes(uint64_t len) {
     const uint64_t tiles = (len + kTileBytes - 1) / kTileBytes;
     const uint64_t groups = (tiles + kGroupTiles - 1) / kGroupTiles;
-    return (tiles * (kEntries + 1) + groups * (kEntries + 1)) * sizeof(GEntry) + 256;
+    return (tiles * (kEntries + 1) + groups * (kEntries + 1)) * sizeof(GEntry) +
+           tiles * kTileLanes * sizeof(ulonglong2) + 256;
 }
 
 hipError_t launch_decode_peer_stream(const uint8_t* buf, uint64_t len, mpx_accept_reply* ar_out,
@@ -428,11 +506,12 @@ hipError_t launch_decode_peer_stream(const uint8_t* buf, uint64_t len, mpx_accep
     GEntry* tres = tmap + (uint64_t)tiles * kEntries;
     GEntry* gmap = tres + tiles;
     GEntry* gres = gmap + (uint64_t)groups * kEntries;
-    k_dec_tile_maps<<<tiles, kTileLanes, 0, stream>>>(buf, len, tmap);
+    ulonglong2* xmap = (ulonglong2*)(((uintptr_t)(gres + groups) + 15) & ~(uintptr_t)15);
+    k_dec_tile_maps<<<tiles, kTileLanes, 0, stream>>>(buf, len, tmap, xmap);
     k_dec_group_maps<<<groups, 256, 0, stream>>>(tmap, tiles, gmap);
     k_dec_walk<<<1, 256, 0, stream>>>(gmap, groups, len, buf, gres, res);
     k_dec_tile_entries<<<groups, 256, 0, stream>>>(tmap, tiles, gres, tres);
-    k_dec_emit<<<tiles, kTileLanes, 0, stream>>>(buf, len, tres, ar_out, ar_cap, oth_out,
+    k_dec_emit<<<tiles, kTileLanes, 0, stream>>>(buf, len, tres, xmap, ar_out, ar_cap, oth_out,
                                                  oth_cap);
     return hipGetLastError();
 }

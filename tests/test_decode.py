@@ -4,7 +4,7 @@ CPU: hand-built known-answer streams against the oracle (oracle/wire.cpp), each 
 the cited Go: replicaListener's frame loop (genericsmr.go:402-446) and the Unmarshal()s it
 dispatches to (minpaxosprotomarsh.go, gsmrprotomarsh.go).
 GPU: mpx_decode_peer_stream vs the oracle, bit for bit, on streams that cross the engine's
-chunk (64 B), tile (8 KB) and group (2 MB) boundaries, junk, partial tails, variable-length
+chunk (128 B), tile (16 KB) and group (4 MB) boundaries, junk, partial tails, variable-length
 stops and short output capacities.
 """
 import struct
@@ -92,14 +92,14 @@ def _eq(got, want):
 
 def _streams():
     rng = np.random.default_rng(31)
-    rec, _ = synth.accept_replies(1 << 16, 5, 0.7, seed=42)
+    rec, _ = synth.accept_replies(1 << 17, 5, 0.7, seed=42)
     out = {}
-    for n in (1, 3, 4, 5, 37, 585, 586, 587, 1000):  # 585 frames ~ one 8 KB tile
+    for n in (1, 3, 4, 5, 37, 585, 1170, 1171, 1172, 2000):  # 1170 frames ~ one 16 KB tile
         out[f"ar_only_{n}"] = synth.peer_stream(rec[:n])
     out["mixed_small"] = synth.peer_stream(rec[:3000], p_beacon=0.05, p_prepare=0.03,
                                            p_commit_short=0.03, p_unknown=0.1)
     out["mixed_groups"] = synth.peer_stream(rec, seed=5, p_beacon=0.01, p_prepare=0.01,
-                                            p_commit_short=0.01, p_unknown=0.01)  # > 2 MB
+                                            p_commit_short=0.01, p_unknown=0.01)  # > 4 MB
     out["unknown_heavy"] = synth.peer_stream(rec[:20000], seed=6, p_unknown=0.6)
     junk = rng.integers(0, 256, 300000).astype(np.uint8)
     junk[np.isin(junk, [R.PEER_ACCEPT, R.PEER_COMMIT, R.PEER_PREPARE_REPLY])] = 200
@@ -109,7 +109,7 @@ def _streams():
         out[f"partial_{cut}"] = synth.peer_stream(rec[:2000], tail=bytes([13] + [0] * cut))
     base = synth.peer_stream(rec[:40000], seed=7, p_beacon=0.01)
     starts = _frame_starts(base)
-    for at in (0, 13, 8192 * 3 + 5, len(base) // 2):
+    for at in (0, 13, 16384 * 3 + 5, len(base) // 2):
         # a variable-length frame spliced in at the first frame boundary at or after `at`
         pos = int(starts[min(int(np.searchsorted(starts, at)), len(starts) - 1)])
         out[f"variable_at_{at}"] = np.concatenate(
