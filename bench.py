@@ -19,6 +19,8 @@ The other single-GPU configurations of BASELINE.json are kernel benches of their
            --dist uniform|zipf
   decode   SURVEY §8(f) rank 1: peer-stream framing + AcceptReply decode of the config-2 replies
            (16M instances x 4 = 64M frames of 14 B, a Beacon every ~4096 frames, 0.9 GB)
+  fanout   SURVEY §8(f) rank 2: ProposeReplyTS fan-out of the config-4 commands (64M replies
+           over --clients connections, 25-byte records grouped per connection)
 Each prints one JSON line in the same format, with its own roofline, parity and CPU baseline.
 
 Rank 0 prints ONE JSON line. Inputs are generated on the host (synthetic, counter-based
@@ -59,7 +61,8 @@ def parse():
                     help="groups timed on the CPU baseline (0 = auto, ~10-30 s of CPU work)")
     ap.add_argument("--parity-groups", type=int, default=512)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--workload", default="step", choices=["step", "tally", "prepare", "apply", "decode"])
+    ap.add_argument("--workload", default="step", choices=["step", "tally", "prepare", "apply", "decode", "fanout"])
+    ap.add_argument("--clients", type=int, default=1024, help="fanout: client connections")
     ap.add_argument("--instances", type=int, default=1 << 24, help="tally / prepare: instances")
     ap.add_argument("--commands", type=int, default=1 << 26, help="apply: commands")
     ap.add_argument("--apply-keys", type=int, default=1 << 20, help="apply: key space")
@@ -501,6 +504,41 @@ def kernel_bench(a):
                "sample": f"the full workload ({M} commands over {K} keys, {a.dist}) x {reps}, "
                          f"Execute per command on an unordered_map, one thread, {secs:.1f} s timed"}
         workload = f"config4: {M} PUT/GET (p_put=0.5) over {K} keys, {a.dist}"
+    elif a.workload == "fanout":
+        M, Cn = a.commands, a.clients
+        recs = synth.replies(M, Cn, seed=55)
+        d_recs = dt(recs)
+        d_out = torch.empty(M * R.PROPOSE_REPLY_BYTES, dtype=torch.uint8, device=dev)
+        d_off = torch.empty(Cn + 1, dtype=torch.int64, device=dev)
+        eng.encode_replies_reserve(M)
+        t_gen = time.time() - t_gen
+        wall, ms = _timed(stream, eng, a.steps, a.warmup,
+                          lambda: eng.encode_replies_dev(d_recs.data_ptr(), M, Cn, 1, 0,
+                                                         d_out.data_ptr(), d_off.data_ptr(),
+                                                         eng.stream))
+        alg = M * (24 + R.PROPOSE_REPLY_BYTES) + (Cn + 1) * 8  # records in, wire bytes out
+        units, unit = M, "replies/s"
+        kernel = "mpx_encode_replies pipeline (client keys, radix sort, gather + encode)"
+        o = OL.Oracle(N, mode)
+        w_out, w_off = o.encode_replies(recs, Cn, 1, 0)
+        bit_exact = bool(d_out.cpu().numpy().tobytes() == w_out.tobytes()
+                         and np.array_equal(d_off.cpu().numpy().view(np.uint64), w_off))
+        parity = {"replies_checked": M, "bit_exact": bit_exact}
+        lib = OL.load()
+        cout = np.zeros(M * R.PROPOSE_REPLY_BYTES, np.uint8)
+        coff = np.zeros(Cn + 1, np.uint64)
+        secs, reps = 0.0, 0
+        while secs < 10.0 and reps < 20:
+            t0 = time.perf_counter()
+            lib.orc_encode_replies(recs.ctypes.data, M, Cn, 1, 0, cout.ctypes.data,
+                                   coff.ctypes.data)
+            secs += time.perf_counter() - t0
+            reps += 1
+        cpu = {"value": M * reps / secs, "unit": unit, "cores": 1, "kind": "port",
+               "sample": f"the full batch ({M} replies over {Cn} connections) x {reps}, one "
+                         f"Marshal per reply into per-connection buffers, one thread, "
+                         f"{secs:.1f} s timed"}
+        workload = f"fanout: {M} ProposeReplyTS over {Cn} client connections"
     else:  # decode
         I = a.instances
         recs, _ = synth.accept_replies(I, N, 0.7, seed=42)

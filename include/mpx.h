@@ -25,6 +25,10 @@
  *                            Unmarshal()s it dispatches to (minpaxosprotomarsh.go:259-270,
  *                            :568-580, :737-749; Beacon/BeaconReply): frames a peer byte stream
  *                            and decodes its AcceptReplies into mpx_accept_reply records
+ *   mpx_encode_replies    <- the ProposeReplyTS fan-out of handleAcceptReply
+ *                              src/bareminpaxos/bareminpaxos.go:1030-1042 and executeCommands
+ *                            :1076-1084 through ReplyProposeTS (genericsmr.go:529-535): the byte
+ *                            run each client connection receives for a batch of replies
  *
  * Contract (every entry point):
  *   - plain C, no exceptions cross the boundary, never aborts; return 0 (MPX_OK) or a negative
@@ -363,6 +367,32 @@ int mpx_decode_reserve(mpx_engine* eng, size_t max_len);
 int mpx_decode_peer_stream_dev(mpx_engine* eng, const uint8_t* d_buf, size_t len,
                                mpx_accept_reply* d_ar, size_t ar_cap, mpx_peer_frame* d_other,
                                size_t other_cap, mpx_decode_result* d_res, void* stream);
+
+/* ---- client reply fan-out -----------------------------------------
+ * One reply per executed (or decided) command, in execution order: the proposing client's
+ * connection index, and the ProposeReplyTS fields the leader fills from
+ * inst.Lb.ClientProposals[j] (CommandId, Timestamp) and Execute's return (Value; state.NIL = 0
+ * for replies sent at decide time). genericsmrproto.ProposeReplyTS  genericsmrproto.go:31-37 */
+typedef struct mpx_reply_rec {
+    int64_t value;
+    int64_t timestamp;
+    int32_t command_id;
+    uint32_t client; /* 0 .. n_clients-1                                                     */
+} mpx_reply_rec; /* 24 B */
+
+#define MPX_PROPOSE_REPLY_BYTES 25 /* gsmrprotomarsh.go:702-732: OK, CommandId, Value,
+                                      Timestamp, Leader (little endian)                      */
+
+/* out (25*n bytes) receives, client by client, each client's replies in execution order,
+ * encoded exactly as ProposeReplyTS.Marshal writes them with OK = ok and Leader = leader;
+ * client c's run is out[client_off[c] .. client_off[c+1]) (client_off: n_clients+1 entries).
+ * A record whose client >= n_clients makes the call fail with MPX_E_INVAL.                  */
+int mpx_encode_replies(mpx_engine* eng, const mpx_reply_rec* recs, size_t n, uint32_t n_clients,
+                       uint8_t ok, int32_t leader, uint8_t* out, uint64_t* client_off);
+int mpx_encode_replies_reserve(mpx_engine* eng, size_t max_n);
+int mpx_encode_replies_dev(mpx_engine* eng, const mpx_reply_rec* d_recs, size_t n,
+                           uint32_t n_clients, uint8_t ok, int32_t leader, uint8_t* d_out,
+                           uint64_t* d_client_off, void* stream);
 
 #ifdef __cplusplus
 }

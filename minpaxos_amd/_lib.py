@@ -62,6 +62,9 @@ SIGNATURES = {
     "mpx_decode_peer_stream": (C.c_int, [_p, _p, _sz, _p, _sz, _p, _sz, _p]),
     "mpx_decode_reserve": (C.c_int, [_p, _sz]),
     "mpx_decode_peer_stream_dev": (C.c_int, [_p, _p, _sz, _p, _sz, _p, _sz, _p, _p]),
+    "mpx_encode_replies": (C.c_int, [_p, _p, _sz, C.c_uint32, C.c_uint8, _i32, _p, _p]),
+    "mpx_encode_replies_reserve": (C.c_int, [_p, _sz]),
+    "mpx_encode_replies_dev": (C.c_int, [_p, _p, _sz, C.c_uint32, C.c_uint8, _i32, _p, _p, _p]),
 }
 
 _lib = None

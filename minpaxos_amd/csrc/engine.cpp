@@ -40,6 +40,9 @@ struct mpx_engine {
     // peer stream decode: staging (bytes, AcceptReplies, other frames, result) + scratch
     DevBuf dec[4];
     DevBuf decode_work;
+    // client reply fan-out: staging (records, bytes, offsets) + scratch
+    DevBuf fan[3];
+    DevBuf fan_work;
     uint64_t apply_chunk = 0;  // commands per apply chunk (0 = kApplyChunkDefault)
     // group-step work list (groups the fast kernel hands to the general kernel) + its count
     DevBuf worklist;
@@ -222,6 +225,9 @@ int mpx_close(mpx_engine* e) {
     for (auto& x : e->dec)
         if (x.p) (void)hipFree(x.p);
     if (e->decode_work.p) (void)hipFree(e->decode_work.p);
+    for (auto& x : e->fan)
+        if (x.p) (void)hipFree(x.p);
+    if (e->fan_work.p) (void)hipFree(e->fan_work.p);
     if (e->worklist.p) (void)hipFree(e->worklist.p);
     if (e->d_wcount) (void)hipFree(e->d_wcount);
     if (e->kv_ready) {
@@ -745,6 +751,49 @@ int mpx_decode_peer_stream(mpx_engine* e, const uint8_t* buf, size_t len, mpx_ac
     CK(d2h(e, other, e->dec[2].p, std::min<uint64_t>(res->n_other, other_cap) *
                                       sizeof(mpx_peer_frame)));
     return finish(e);
+}
+
+// ---- §8(f) rank 2: client reply fan-out -----------------------------------------------------
+int mpx_encode_replies_reserve(mpx_engine* e, size_t max_n) {
+    if (!e) return MPX_E_INVAL;
+    if (max_n >= (1ull << 32)) return fail(e, MPX_E_UNSUPPORTED, "at most 2^32-1 replies per call");
+    CK(begin(e));
+    GROW(e, e->fan_work, mpx::fanout_work_bytes(max_n));
+    return finish(e);
+}
+
+int mpx_encode_replies_dev(mpx_engine* e, const mpx_reply_rec* d_recs, size_t n,
+                           uint32_t n_clients, uint8_t ok, int32_t leader, uint8_t* d_out,
+                           uint64_t* d_client_off, void* stream) {
+    if (!e || !n_clients || !d_client_off || (n && (!d_recs || !d_out))) return MPX_E_INVAL;
+    if (n >= (1ull << 32)) return fail(e, MPX_E_UNSUPPORTED, "at most 2^32-1 replies per call");
+    if (e->fan_work.cap < mpx::fanout_work_bytes(n))
+        return fail(e, MPX_E_INVAL,
+                    "mpx_encode_replies_dev: call mpx_encode_replies_reserve(n) first (the dev "
+                    "entry point never allocates)");
+    HIPCHK(e, mpx::launch_encode_replies(d_recs, n, n_clients, ok, leader, d_out, d_client_off,
+                                         e->fan_work.p, e->fan_work.cap, e->d_err,
+                                         pick(e, stream)));
+    return MPX_OK;
+}
+
+int mpx_encode_replies(mpx_engine* e, const mpx_reply_rec* recs, size_t n, uint32_t n_clients,
+                       uint8_t ok, int32_t leader, uint8_t* out, uint64_t* client_off) {
+    if (!e || !n_clients || !client_off || (n && (!recs || !out))) return MPX_E_INVAL;
+    if (n >= (1ull << 32)) return fail(e, MPX_E_UNSUPPORTED, "at most 2^32-1 replies per call");
+    CK(begin(e));
+    GROW(e, e->fan[0], n * sizeof(mpx_reply_rec));
+    GROW(e, e->fan[1], n * MPX_PROPOSE_REPLY_BYTES);
+    GROW(e, e->fan[2], ((size_t)n_clients + 1) * sizeof(uint64_t));
+    GROW(e, e->fan_work, mpx::fanout_work_bytes(n));
+    CK(h2d(e, e->fan[0].p, recs, n * sizeof(mpx_reply_rec)));
+    CK(mpx_encode_replies_dev(e, (const mpx_reply_rec*)e->fan[0].p, n, n_clients, ok, leader,
+                              (uint8_t*)e->fan[1].p, (uint64_t*)e->fan[2].p, e->stream));
+    CK(d2h(e, out, e->fan[1].p, n * MPX_PROPOSE_REPLY_BYTES));
+    CK(d2h(e, client_off, e->fan[2].p, ((size_t)n_clients + 1) * sizeof(uint64_t)));
+    int rc = finish(e);
+    if (rc == MPX_E_INVAL) return fail(e, MPX_E_INVAL, "a reply names a client >= n_clients");
+    return rc;
 }
 
 }  // extern "C"

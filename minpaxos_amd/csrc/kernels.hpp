@@ -87,4 +87,11 @@ hipError_t launch_decode_peer_stream(const uint8_t* buf, uint64_t len, mpx_accep
                                      mpx_decode_result* res, void* work, uint64_t work_bytes,
                                      hipStream_t stream);
 
+// ---- client reply fan-out (mpx_encode_replies) -------------------------------------------
+uint64_t fanout_work_bytes(uint64_t n);
+hipError_t launch_encode_replies(const mpx_reply_rec* recs, uint64_t n, uint32_t n_clients,
+                                 uint8_t ok, int32_t leader, uint8_t* out, uint64_t* client_off,
+                                 void* work, uint64_t work_bytes, uint32_t* err,
+                                 hipStream_t stream);
+
 }  // namespace mpx

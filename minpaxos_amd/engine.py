@@ -9,6 +9,7 @@ Names and argument meaning follow the reference handlers they replace:
   committed_prefix    <- updateCommittedUpTo
   group_step          <- handleAcceptReply + executeCommands for many replicas at once
   decode_peer_stream  <- genericsmr.replicaListener framing + AcceptReply.Unmarshal
+  encode_replies      <- the ProposeReplyTS fan-out (ReplyProposeTS per executed command)
 Errors come back as MpxError carrying the reference-level reason (e.g. E_NIL_INSTANCE where the
 Go handler would dereference a nil *Instance).
 """
@@ -271,6 +272,27 @@ class Engine:
         self._check(self.lib.mpx_decode_peer_stream_dev(self.h, d_buf, n, d_ar, ar_cap, d_other,
                                                         other_cap, d_res, stream),
                     "mpx_decode_peer_stream_dev")
+
+    # ---- client reply fan-out -----------------------------------------
+    def encode_replies(self, recs, n_clients, ok=1, leader=0):
+        """recs: REPLY_REC in execution order. Returns (bytes uint8[25 n], client_off u64[C+1]):
+        client c's connection receives out[client_off[c]:client_off[c+1]]."""
+        recs = _c(recs, R.REPLY_REC)
+        n = len(recs)
+        out = np.zeros(max(n * R.PROPOSE_REPLY_BYTES, 1), np.uint8)
+        off = np.zeros(n_clients + 1, np.uint64)
+        self._check(self.lib.mpx_encode_replies(self.h, _ptr(recs), n, n_clients, ok, leader,
+                                                _ptr(out), _ptr(off)), "mpx_encode_replies")
+        return out[:n * R.PROPOSE_REPLY_BYTES], off
+
+    def encode_replies_reserve(self, max_n):
+        self._check(self.lib.mpx_encode_replies_reserve(self.h, max_n),
+                    "mpx_encode_replies_reserve")
+
+    def encode_replies_dev(self, d_recs, n, n_clients, ok, leader, d_out, d_off, stream=None):
+        self._check(self.lib.mpx_encode_replies_dev(self.h, d_recs, n, n_clients, ok, leader,
+                                                    d_out, d_off, stream),
+                    "mpx_encode_replies_dev")
 
     # ---- multi-GPU ----------------------------------------------------------------------------
     @staticmethod

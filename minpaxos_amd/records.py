@@ -67,6 +67,12 @@ PEER_FRAME = np.dtype([("offset", "<u4"), ("code", "u1"), ("pad", "u1", (3,))])
 DECODE_RESULT = np.dtype([("consumed", "<u8"), ("n_accept_replies", "<u8"), ("n_other", "<u8"),
                           ("stop_reason", "<i4"), ("stop_code", "<i4")])
 
+# mpx_reply_rec: one client reply (genericsmrproto.ProposeReplyTS fields + connection index)
+REPLY_REC = np.dtype([("value", "<i8"), ("timestamp", "<i8"), ("command_id", "<i4"),
+                      ("client", "<u4")])
+PROPOSE_REPLY_BYTES = 25
+
+assert REPLY_REC.itemsize == 24
 assert PEER_FRAME.itemsize == 8 and DECODE_RESULT.itemsize == 32
 assert ACCEPT_REPLY.itemsize == 16 and INST_STATE.itemsize == 16
 assert PREPARE_REPLY.itemsize == 16 and PREP_STATE.itemsize == 32

@@ -228,3 +228,21 @@ def peer_stream(recs, seed=47, p_beacon=0.0, p_prepare=0.0, p_commit_short=0.0, 
     if extra:
         buf[int(off[-1]):] = np.frombuffer(extra, np.uint8)
     return buf
+
+
+def replies(m, n_clients, seed=53, value=None):
+    """Client replies for m executed commands, in execution order: client connection uniform on
+    [0, n_clients), CommandId = the client's own running counter (client.go sends ids 0..q-1
+    per client), Timestamp a nanosecond clock, Value = `value` (e.g. apply's ret) or index."""
+    rec = np.zeros(m, R.REPLY_REC)
+    c = (stream(seed, 30, 0, m) % np.uint64(n_clients)).astype(np.uint32)
+    rec["client"] = c
+    order = np.argsort(c, kind="stable")
+    cnt = np.bincount(c, minlength=n_clients)
+    start = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+    ids = np.empty(m, np.int64)
+    ids[order] = np.arange(m) - np.repeat(start, cnt)
+    rec["command_id"] = ids.astype(np.int32)
+    rec["timestamp"] = (1_700_000_000_000_000_000 + np.arange(m, dtype=np.int64) * 37)
+    rec["value"] = np.arange(m, dtype=np.int64) if value is None else value
+    return rec

@@ -14,6 +14,7 @@
 // of the buffer (include/mpx.h, mpx_decode_peer_stream); this restatement does the same.
 #include <cstdint>
 #include <cstring>
+#include <vector>
 
 #include "../include/mpx.h"
 
@@ -90,6 +91,35 @@ int orc_decode_peer_stream(const uint8_t* buf, size_t len, mpx_accept_reply* ar,
     res->n_other = n_oth;
     res->stop_reason = why;
     res->stop_code = code_at;
+    return MPX_OK;
+}
+
+// Client reply fan-out: every reply, in execution order, is one
+// genericsmr.(*Replica).ReplyProposeTS(reply, client writer) (genericsmr.go:529-535), i.e.
+// ProposeReplyTS.Marshal (gsmrprotomarsh.go:702-732) appended to that client's stream:
+// OK u8, CommandId i32, Value i64 (state.Value.Marshal, statemarsh.go:48-53), Timestamp i64,
+// Leader i32, little endian. out holds the clients' streams back to back, client 0 first.
+int orc_encode_replies(const mpx_reply_rec* recs, size_t n, uint32_t n_clients, uint8_t ok,
+                       int32_t leader, uint8_t* out, uint64_t* client_off) {
+    if (!n_clients) return MPX_E_INVAL;
+    std::vector<std::vector<uint8_t>> wire(n_clients);
+    for (size_t i = 0; i < n; ++i) {
+        const mpx_reply_rec& r = recs[i];
+        if (r.client >= n_clients) return MPX_E_INVAL;
+        std::vector<uint8_t>& w = wire[r.client];
+        w.push_back(ok);
+        for (int k = 0; k < 4; ++k) w.push_back((uint8_t)((uint32_t)r.command_id >> (8 * k)));
+        for (int k = 0; k < 8; ++k) w.push_back((uint8_t)((uint64_t)r.value >> (8 * k)));
+        for (int k = 0; k < 8; ++k) w.push_back((uint8_t)((uint64_t)r.timestamp >> (8 * k)));
+        for (int k = 0; k < 4; ++k) w.push_back((uint8_t)((uint32_t)leader >> (8 * k)));
+    }
+    uint64_t o = 0;
+    for (uint32_t c = 0; c < n_clients; ++c) {
+        client_off[c] = o;
+        if (!wire[c].empty()) memcpy(out + o, wire[c].data(), wire[c].size());
+        o += wire[c].size();
+    }
+    client_off[n_clients] = o;
     return MPX_OK;
 }
 

@@ -69,6 +69,8 @@ def cases():
     var = np.array([R.PEER_PREPARE_REPLY, 1, 0, 0, 0], np.uint8)
     out["decode_variable_stop"] = ("decode", dict(), dict(buf=np.concatenate(
         [head, var, synth.peer_stream(drec[1000:], seed=51)])))
+    out["fanout_replies"] = ("fanout", dict(n_clients=37, ok=1, leader=3),
+                             dict(recs=synth.replies(5000, 37, seed=54)))
     return out
 
 
@@ -103,6 +105,10 @@ def run_case(kind, p, x, backend_mk):
         b = backend_mk(5, R.MODE_MIN)
         ar, oth, res = b.decode_peer_stream(x["buf"])
         return dict(ar=ar, other=oth, res=np.array([res], R.DECODE_RESULT))
+    if kind == "fanout":
+        b = backend_mk(5, R.MODE_MIN)
+        out, off = b.encode_replies(x["recs"], p["n_clients"], p["ok"], p["leader"])
+        return dict(out=out, client_off=off)
     raise ValueError(kind)
 
 

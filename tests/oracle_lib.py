@@ -51,6 +51,7 @@ def load():
         "orc_bench_accept": (C.c_int64, [C.c_int, C.c_int, _p, _sz, _p, _sz, _i32, _p, _p]),
         "orc_bench_apply": (C.c_int64, [_p, _p, _sz, _p, _p, _p, _sz, _p]),
         "orc_decode_peer_stream": (C.c_int, [_p, _sz, _p, _sz, _p, _sz, _p]),
+        "orc_encode_replies": (C.c_int, [_p, _sz, C.c_uint32, C.c_uint8, _i32, _p, _p]),
         "orc_bench_group_step": (C.c_int64, [C.c_int, C.c_int, C.POINTER(L.MpxGroupBatch),
                                              C.c_uint32, C.c_int]),
     }
@@ -180,6 +181,15 @@ class Oracle:
         r = res[0]
         return (ar[:min(int(r["n_accept_replies"]), ar_cap)],
                 oth[:min(int(r["n_other"]), other_cap)], r)
+
+    def encode_replies(self, recs, n_clients, ok=1, leader=0):
+        recs = np.ascontiguousarray(recs, R.REPLY_REC)
+        n = len(recs)
+        out = np.zeros(max(n * R.PROPOSE_REPLY_BYTES, 1), np.uint8)
+        off = np.zeros(n_clients + 1, np.uint64)
+        _check(self.lib.orc_encode_replies(_ptr(recs), n, n_clients, ok, leader, _ptr(out),
+                                           _ptr(off)), "orc_encode_replies")
+        return out[:n * R.PROPOSE_REPLY_BYTES], off
 
     def group_step(self, b, kv_cnt=None, kv_key=None, kv_val=None, ret=None, want_conf=True,
                    want_decided=True):

@@ -1,0 +1,70 @@
+"""Client reply fan-out.
+
+CPU: the oracle's byte runs against ProposeReplyTS.Marshal restated with struct.pack
+(gsmrprotomarsh.go:702-732: OK u8, CommandId i32, Value i64, Timestamp i64, Leader i32, LE),
+one run per client connection in execution order (ReplyProposeTS, genericsmr.go:529-535).
+GPU: mpx_encode_replies vs the oracle, bit for bit.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+from oracle_lib import Oracle, OracleError
+from minpaxos_amd import records as R
+from minpaxos_amd import synth
+
+
+def marshal(ok, cid, value, ts, leader):
+    return struct.pack("<BiqqiB", ok, cid, value, ts, leader, 0)[:25]
+
+
+def test_kat_two_clients_in_execution_order():
+    rec = np.zeros(4, R.REPLY_REC)
+    rec["client"] = [1, 0, 1, 1]
+    rec["command_id"] = [10, 20, 11, -1]
+    rec["value"] = [0, -5, 7, 1 << 40]
+    rec["timestamp"] = [100, 200, 300, -400]
+    out, off = Oracle().encode_replies(rec, 3, ok=1, leader=2)
+    assert list(off) == [0, 25, 100, 100]
+    assert out[0:25].tobytes() == marshal(1, 20, -5, 200, 2)
+    assert out[25:100].tobytes() == (marshal(1, 10, 0, 100, 2) + marshal(1, 11, 7, 300, 2) +
+                                     marshal(1, -1, 1 << 40, -400, 2))
+
+
+def test_kat_empty_and_bad_client():
+    out, off = Oracle().encode_replies(np.zeros(0, R.REPLY_REC), 4)
+    assert len(out) == 0 and list(off) == [0, 0, 0, 0, 0]
+    rec = np.zeros(1, R.REPLY_REC)
+    rec["client"] = 4
+    with pytest.raises(OracleError):
+        Oracle().encode_replies(rec, 4)
+
+
+@pytest.mark.gpu
+def test_fanout_parity(mk_engine):
+    e, o = mk_engine(5, R.MODE_MIN), Oracle()
+    for n, c in ((1, 1), (255, 2), (256, 7), (257, 7), (1000, 1024), (4099, 3),
+                 (300000, 1024), (200000, 65536), (70000, 1)):
+        rec = synth.replies(n, c, seed=n + c)
+        for ok, leader in ((1, 0), (0, 7)):
+            got = e.encode_replies(rec, c, ok, leader)
+            want = o.encode_replies(rec, c, ok, leader)
+            assert np.array_equal(got[1], want[1]), (n, c)
+            assert got[0].tobytes() == want[0].tobytes(), (n, c)
+
+
+@pytest.mark.gpu
+def test_fanout_empty_and_bad_client(mk_engine):
+    from minpaxos_amd.engine import MpxError
+    e = mk_engine(5, R.MODE_MIN)
+    out, off = e.encode_replies(np.zeros(0, R.REPLY_REC), 5)
+    assert len(out) == 0 and list(off) == [0] * 6
+    rec = synth.replies(100, 4)
+    rec["client"][50] = 9
+    with pytest.raises(MpxError):
+        e.encode_replies(rec, 4)
+    rec["client"][50] = 1  # the handle stays usable
+    got = e.encode_replies(rec, 4)
+    want = Oracle().encode_replies(rec, 4)
+    assert got[0].tobytes() == want[0].tobytes() and np.array_equal(got[1], want[1])
