@@ -21,6 +21,8 @@ The other single-GPU configurations of BASELINE.json are kernel benches of their
            (16M instances x 4 = 64M frames of 14 B, a Beacon every ~4096 frames, 0.9 GB)
   fanout   SURVEY §8(f) rank 2: ProposeReplyTS fan-out of the config-4 commands (64M replies
            over --clients connections, 25-byte records grouped per connection)
+  log      SURVEY §8(f) ranks 3/4: instance-log encoding of 16M committed instances x 4 commands
+           (--log-format catchup = Instance.Marshal for bcastAccept, durable = the stable store)
 Each prints one JSON line in the same format, with its own roofline, parity and CPU baseline.
 
 Rank 0 prints ONE JSON line. Inputs are generated on the host (synthetic, counter-based
@@ -61,7 +63,8 @@ def parse():
                     help="groups timed on the CPU baseline (0 = auto, ~10-30 s of CPU work)")
     ap.add_argument("--parity-groups", type=int, default=512)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--workload", default="step", choices=["step", "tally", "prepare", "apply", "decode", "fanout"])
+    ap.add_argument("--workload", default="step", choices=["step", "tally", "prepare", "apply", "decode", "fanout", "log"])
+    ap.add_argument("--log-format", default="catchup", choices=["catchup", "durable"])
     ap.add_argument("--clients", type=int, default=1024, help="fanout: client connections")
     ap.add_argument("--instances", type=int, default=1 << 24, help="tally / prepare: instances")
     ap.add_argument("--commands", type=int, default=1 << 26, help="apply: commands")
@@ -539,6 +542,47 @@ def kernel_bench(a):
                          f"Marshal per reply into per-connection buffers, one thread, "
                          f"{secs:.1f} s timed"}
         workload = f"fanout: {M} ProposeReplyTS over {Cn} client connections"
+    elif a.workload == "log":
+        I = a.instances
+        fmt = R.LOG_CATCHUP if a.log_format == "catchup" else R.LOG_DURABLE
+        recs, coff, op, key, val = synth.log_records(I, 4, seed=58)
+        M = len(op)
+        d_recs, d_off, d_op, d_key, d_val = dt(recs), dt(coff), dt(op), dt(key), dt(val)
+        bound = eng.lib.mpx_encode_log_bound(I, M)
+        d_out = torch.empty(bound, dtype=torch.uint8, device=dev)
+        d_ro = torch.empty(I + 1, dtype=torch.int64, device=dev)
+        eng.encode_log_reserve(I, M)
+        t_gen = time.time() - t_gen
+        wall, ms = _timed(stream, eng, a.steps, a.warmup,
+                          lambda: eng.encode_log_dev(fmt, d_recs.data_ptr(), I, d_off.data_ptr(),
+                                                     d_op.data_ptr(), d_key.data_ptr(),
+                                                     d_val.data_ptr(), M, d_out.data_ptr(),
+                                                     d_ro.data_ptr(), eng.stream))
+        o = OL.Oracle(N, mode)
+        w_out, w_ro = o.encode_log(fmt, recs, coff, op, key, val)
+        total = int(w_ro[-1])
+        # records + offsets + commands in, the encoding + record offsets out
+        alg = I * (16 + 8) + M * 17 + total + (I + 1) * 8
+        units, unit = I, "instances/s"
+        kernel = "mpx_encode_log pipeline (record sizes, scan, output-parallel emit)"
+        bit_exact = bool(np.array_equal(d_ro.cpu().numpy().view(np.uint64), w_ro)
+                         and d_out[:total].cpu().numpy().tobytes() == w_out.tobytes())
+        parity = {"instances_checked": I, "bytes": total, "bit_exact": bit_exact}
+        lib = OL.load()
+        cout = np.zeros(total, np.uint8)
+        cro = np.zeros(I + 1, np.uint64)
+        secs, reps = 0.0, 0
+        while secs < 10.0 and reps < 20:
+            t0 = time.perf_counter()
+            lib.orc_encode_log(fmt, recs.ctypes.data, I, coff.ctypes.data, op.ctypes.data,
+                               key.ctypes.data, val.ctypes.data, cout.ctypes.data, total,
+                               cro.ctypes.data)
+            secs += time.perf_counter() - t0
+            reps += 1
+        cpu = {"value": I * reps / secs, "unit": unit, "cores": 1, "kind": "port",
+               "sample": f"the full run ({I} instances, {M} commands, {total} bytes) x {reps}, "
+                         f"one Marshal per instance and command, one thread, {secs:.1f} s timed"}
+        workload = f"log ({a.log_format}): {I} committed instances x 4 commands, {total} bytes"
     else:  # decode
         I = a.instances
         recs, _ = synth.accept_replies(I, N, 0.7, seed=42)

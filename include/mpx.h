@@ -29,6 +29,9 @@
  *                              src/bareminpaxos/bareminpaxos.go:1030-1042 and executeCommands
  *                            :1076-1084 through ReplyProposeTS (genericsmr.go:529-535): the byte
  *                            run each client connection receives for a batch of replies
+ *   mpx_encode_log        <- minpaxosproto.(*Instance).Marshal (minpaxosprotomarsh.go:100-124) for
+ *                            the CatchUpLog of bcastAccept (bareminpaxos.go:488-513), and
+ *                            recordInstanceMetadata + recordCommands (bareminpaxos.go:164-188)
  *
  * Contract (every entry point):
  *   - plain C, no exceptions cross the boundary, never aborts; return 0 (MPX_OK) or a negative
@@ -393,6 +396,40 @@ int mpx_encode_replies_reserve(mpx_engine* eng, size_t max_n);
 int mpx_encode_replies_dev(mpx_engine* eng, const mpx_reply_rec* d_recs, size_t n,
                            uint32_t n_clients, uint8_t ok, int32_t leader, uint8_t* d_out,
                            uint64_t* d_client_off, void* stream);
+
+/* ---- instance-log encoding ----------------------------------
+ * A run of log records (instance metadata + commands [cmd_off[i], cmd_off[i+1]) of the SoA
+ * command arrays op/key/val, the layout mpx_apply takes) encoded back to back in one of the
+ * reference's two byte formats; rec_off[i] is where record i starts, rec_off[n] the total.
+ *   MPX_LOG_CATCHUP  Instance.Marshal: Ballot i32, Status i32, PutVarint(len(Cmds)), Cmds (17 B
+ *                    each: Op, K, V). bcastAccept sends peer q the records peerCommits[q]+1 ..
+ *                    lastCommitted: the suffix out[rec_off[from] .. rec_off[n]).
+ *   MPX_LOG_DURABLE  recordInstanceMetadata (Ballot u32, Status u32, instNo u32) +
+ *                    recordCommands (17 B per command; an empty or nil slice writes nothing). */
+#define MPX_LOG_CATCHUP 0
+#define MPX_LOG_DURABLE 1
+typedef struct mpx_log_rec {
+    int32_t ballot;
+    int32_t status;
+    int32_t inst_no; /* instNo (MPX_LOG_DURABLE; unused by MPX_LOG_CATCHUP)                  */
+    uint32_t pad;
+} mpx_log_rec; /* 16 B */
+
+/* bytes out must hold for n records with m commands in total                              */
+size_t mpx_encode_log_bound(size_t n, size_t m);
+/* cmd_off: n+1 non-decreasing offsets with cmd_off[n] <= m. The output is never larger than
+ * mpx_encode_log_bound(n, m); if rec_off[n] > out_cap the call fails with MPX_E_INVAL and only
+ * rec_off is written.                                                                      */
+int mpx_encode_log(mpx_engine* eng, int format, const mpx_log_rec* recs, size_t n,
+                   const uint64_t* cmd_off, const uint8_t* op, const int64_t* key,
+                   const int64_t* val, size_t m, uint8_t* out, size_t out_cap,
+                   uint64_t* rec_off);
+int mpx_encode_log_reserve(mpx_engine* eng, size_t max_n, size_t max_m);
+/* d_out must hold mpx_encode_log_bound(n, m) bytes; cmd_off is trusted (not validated)     */
+int mpx_encode_log_dev(mpx_engine* eng, int format, const mpx_log_rec* d_recs, size_t n,
+                       const uint64_t* d_cmd_off, const uint8_t* d_op, const int64_t* d_key,
+                       const int64_t* d_val, size_t m, uint8_t* d_out, uint64_t* d_rec_off,
+                       void* stream);
 
 #ifdef __cplusplus
 }

@@ -65,6 +65,10 @@ SIGNATURES = {
     "mpx_encode_replies": (C.c_int, [_p, _p, _sz, C.c_uint32, C.c_uint8, _i32, _p, _p]),
     "mpx_encode_replies_reserve": (C.c_int, [_p, _sz]),
     "mpx_encode_replies_dev": (C.c_int, [_p, _p, _sz, C.c_uint32, C.c_uint8, _i32, _p, _p, _p]),
+    "mpx_encode_log_bound": (_sz, [_sz, _sz]),
+    "mpx_encode_log": (C.c_int, [_p, C.c_int, _p, _sz, _p, _p, _p, _p, _sz, _p, _sz, _p]),
+    "mpx_encode_log_reserve": (C.c_int, [_p, _sz, _sz]),
+    "mpx_encode_log_dev": (C.c_int, [_p, C.c_int, _p, _sz, _p, _p, _p, _p, _sz, _p, _p, _p]),
 }
 
 _lib = None

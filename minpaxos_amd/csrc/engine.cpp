@@ -43,6 +43,9 @@ struct mpx_engine {
     // client reply fan-out: staging (records, bytes, offsets) + scratch
     DevBuf fan[3];
     DevBuf fan_work;
+    // instance-log encoding: staging (records, offsets, op, key, val, out, rec_off) + scratch
+    DevBuf lg[7];
+    DevBuf log_work;
     uint64_t apply_chunk = 0;  // commands per apply chunk (0 = kApplyChunkDefault)
     // group-step work list (groups the fast kernel hands to the general kernel) + its count
     DevBuf worklist;
@@ -228,6 +231,9 @@ int mpx_close(mpx_engine* e) {
     for (auto& x : e->fan)
         if (x.p) (void)hipFree(x.p);
     if (e->fan_work.p) (void)hipFree(e->fan_work.p);
+    for (auto& x : e->lg)
+        if (x.p) (void)hipFree(x.p);
+    if (e->log_work.p) (void)hipFree(e->log_work.p);
     if (e->worklist.p) (void)hipFree(e->worklist.p);
     if (e->d_wcount) (void)hipFree(e->d_wcount);
     if (e->kv_ready) {
@@ -794,6 +800,72 @@ int mpx_encode_replies(mpx_engine* e, const mpx_reply_rec* recs, size_t n, uint3
     int rc = finish(e);
     if (rc == MPX_E_INVAL) return fail(e, MPX_E_INVAL, "a reply names a client >= n_clients");
     return rc;
+}
+
+// ---- §8(f) ranks 3/4: instance-log encoding -------------------------------------------------
+size_t mpx_encode_log_bound(size_t n, size_t m) { return (size_t)mpx::logenc_max_bytes(n, m); }
+
+int mpx_encode_log_reserve(mpx_engine* e, size_t max_n, size_t max_m) {
+    if (!e) return MPX_E_INVAL;
+    CK(begin(e));
+    GROW(e, e->log_work, mpx::logenc_work_bytes(max_n, max_m));
+    return finish(e);
+}
+
+int mpx_encode_log_dev(mpx_engine* e, int format, const mpx_log_rec* d_recs, size_t n,
+                       const uint64_t* d_cmd_off, const uint8_t* d_op, const int64_t* d_key,
+                       const int64_t* d_val, size_t m, uint8_t* d_out, uint64_t* d_rec_off,
+                       void* stream) {
+    if (!e || !d_rec_off || (n && (!d_recs || !d_cmd_off || !d_out)) ||
+        (m && (!d_op || !d_key || !d_val)))
+        return MPX_E_INVAL;
+    if (format != MPX_LOG_CATCHUP && format != MPX_LOG_DURABLE)
+        return fail(e, MPX_E_INVAL, "unknown log format");
+    if (e->log_work.cap < mpx::logenc_work_bytes(n, m))
+        return fail(e, MPX_E_INVAL,
+                    "mpx_encode_log_dev: call mpx_encode_log_reserve(n, m) first (the dev entry "
+                    "point never allocates)");
+    HIPCHK(e, mpx::launch_encode_log(format, d_recs, n, d_cmd_off, d_op, d_key, d_val, m, d_out,
+                                     d_rec_off, e->log_work.p, e->log_work.cap, pick(e, stream)));
+    return MPX_OK;
+}
+
+int mpx_encode_log(mpx_engine* e, int format, const mpx_log_rec* recs, size_t n,
+                   const uint64_t* cmd_off, const uint8_t* op, const int64_t* key,
+                   const int64_t* val, size_t m, uint8_t* out, size_t out_cap,
+                   uint64_t* rec_off) {
+    if (!e || !rec_off || (n && (!recs || !cmd_off)) || (m && (!op || !key || !val)) ||
+        (out_cap && !out))
+        return MPX_E_INVAL;
+    if (format != MPX_LOG_CATCHUP && format != MPX_LOG_DURABLE)
+        return fail(e, MPX_E_INVAL, "unknown log format");
+    for (size_t i = 0; i < n; ++i)  // the device kernels trust the offsets
+        if (cmd_off[i] > cmd_off[i + 1] || cmd_off[i + 1] > m)
+            return fail(e, MPX_E_INVAL, "cmd_off must be non-decreasing and <= m");
+    const size_t bound = mpx::logenc_max_bytes(n, m);
+    CK(begin(e));
+    GROW(e, e->lg[0], n * sizeof(mpx_log_rec));
+    GROW(e, e->lg[1], (n + 1) * 8);
+    GROW(e, e->lg[2], m);
+    GROW(e, e->lg[3], m * 8);
+    GROW(e, e->lg[4], m * 8);
+    GROW(e, e->lg[5], bound);
+    GROW(e, e->lg[6], (n + 1) * 8);
+    GROW(e, e->log_work, mpx::logenc_work_bytes(n, m));
+    CK(h2d(e, e->lg[0].p, recs, n * sizeof(mpx_log_rec)));
+    if (n) CK(h2d(e, e->lg[1].p, cmd_off, (n + 1) * 8));
+    CK(h2d(e, e->lg[2].p, op, m));
+    CK(h2d(e, e->lg[3].p, key, m * 8));
+    CK(h2d(e, e->lg[4].p, val, m * 8));
+    CK(mpx_encode_log_dev(e, format, (const mpx_log_rec*)e->lg[0].p, n,
+                          (const uint64_t*)e->lg[1].p, (const uint8_t*)e->lg[2].p,
+                          (const int64_t*)e->lg[3].p, (const int64_t*)e->lg[4].p, m,
+                          (uint8_t*)e->lg[5].p, (uint64_t*)e->lg[6].p, e->stream));
+    CK(d2h(e, rec_off, e->lg[6].p, (n + 1) * 8));
+    CK(finish(e));
+    if (rec_off[n] > out_cap) return fail(e, MPX_E_INVAL, "out_cap is smaller than the encoding");
+    CK(d2h(e, out, e->lg[5].p, rec_off[n]));
+    return finish(e);
 }
 
 }  // extern "C"

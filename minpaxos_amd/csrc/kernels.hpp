@@ -94,4 +94,12 @@ hipError_t launch_encode_replies(const mpx_reply_rec* recs, uint64_t n, uint32_t
                                  void* work, uint64_t work_bytes, uint32_t* err,
                                  hipStream_t stream);
 
+// ---- instance-log encoding (mpx_encode_log) ----------------------------------------------
+uint64_t logenc_work_bytes(uint64_t n, uint64_t m);
+uint64_t logenc_max_bytes(uint64_t n, uint64_t m);
+hipError_t launch_encode_log(int format, const mpx_log_rec* recs, uint64_t n,
+                             const uint64_t* cmd_off, const uint8_t* op, const int64_t* key,
+                             const int64_t* val, uint64_t m, uint8_t* out, uint64_t* rec_off,
+                             void* work, uint64_t work_bytes, hipStream_t stream);
+
 }  // namespace mpx

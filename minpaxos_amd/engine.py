@@ -10,6 +10,8 @@ Names and argument meaning follow the reference handlers they replace:
   group_step          <- handleAcceptReply + executeCommands for many replicas at once
   decode_peer_stream  <- genericsmr.replicaListener framing + AcceptReply.Unmarshal
   encode_replies      <- the ProposeReplyTS fan-out (ReplyProposeTS per executed command)
+  encode_log          <- Instance.Marshal (bcastAccept's CatchUpLog) / recordInstanceMetadata +
+                         recordCommands (the durable log)
 Errors come back as MpxError carrying the reference-level reason (e.g. E_NIL_INSTANCE where the
 Go handler would dereference a nil *Instance).
 """
@@ -293,6 +295,32 @@ class Engine:
         self._check(self.lib.mpx_encode_replies_dev(self.h, d_recs, n, n_clients, ok, leader,
                                                     d_out, d_off, stream),
                     "mpx_encode_replies_dev")
+
+    # ---- instance-log encoding ------------------------------------
+    def encode_log(self, fmt, recs, cmd_off, op, key, val):
+        """Returns (bytes, rec_off u64[n+1]) of the run in format fmt (R.LOG_CATCHUP /
+        R.LOG_DURABLE); record i is bytes[rec_off[i]:rec_off[i+1]]."""
+        recs = _c(recs, R.LOG_REC)
+        off = _c(cmd_off, np.uint64)
+        op, key, val = _c(op, np.uint8), _c(key, np.int64), _c(val, np.int64)
+        n, m = len(recs), len(op)
+        cap = self.lib.mpx_encode_log_bound(n, m)
+        out = np.zeros(max(cap, 1), np.uint8)
+        ro = np.zeros(n + 1, np.uint64)
+        self._check(self.lib.mpx_encode_log(self.h, fmt, _ptr(recs), n, _ptr(off), _ptr(op),
+                                            _ptr(key), _ptr(val), m, _ptr(out), cap, _ptr(ro)),
+                    "mpx_encode_log")
+        return out[:int(ro[-1])], ro
+
+    def encode_log_reserve(self, max_n, max_m):
+        self._check(self.lib.mpx_encode_log_reserve(self.h, max_n, max_m),
+                    "mpx_encode_log_reserve")
+
+    def encode_log_dev(self, fmt, d_recs, n, d_cmd_off, d_op, d_key, d_val, m, d_out, d_rec_off,
+                       stream=None):
+        self._check(self.lib.mpx_encode_log_dev(self.h, fmt, d_recs, n, d_cmd_off, d_op, d_key,
+                                                d_val, m, d_out, d_rec_off, stream),
+                    "mpx_encode_log_dev")
 
     # ---- multi-GPU ----------------------------------------------------------------------------
     @staticmethod

@@ -72,6 +72,11 @@ REPLY_REC = np.dtype([("value", "<i8"), ("timestamp", "<i8"), ("command_id", "<i
                       ("client", "<u4")])
 PROPOSE_REPLY_BYTES = 25
 
+# mpx_log_rec / log formats (instance-log encoding)
+LOG_CATCHUP, LOG_DURABLE = 0, 1
+LOG_REC = np.dtype([("ballot", "<i4"), ("status", "<i4"), ("inst_no", "<i4"), ("pad", "<u4")])
+
+assert LOG_REC.itemsize == 16
 assert REPLY_REC.itemsize == 24
 assert PEER_FRAME.itemsize == 8 and DECODE_RESULT.itemsize == 32
 assert ACCEPT_REPLY.itemsize == 16 and INST_STATE.itemsize == 16

@@ -246,3 +246,24 @@ def replies(m, n_clients, seed=53, value=None):
     rec["timestamp"] = (1_700_000_000_000_000_000 + np.arange(m, dtype=np.int64) * 37)
     rec["value"] = np.arange(m, dtype=np.int64) if value is None else value
     return rec
+
+
+def log_records(n_inst, cmds_per_inst=4, seed=56, ragged=False, first_inst=0):
+    """A run of committed log records for the instance-log encoders: ballot makeUniqueBallot(1)
+    = 16 (a few re-proposed at 32), status COMMITTED, instNo = first_inst + i, and
+    cmds_per_inst commands each (ragged: 0..2*cmds_per_inst, some instances empty) from the
+    config-4 command stream. Returns (recs, cmd_off, op, key, val)."""
+    u = stream(seed, 40, 0, n_inst)
+    if ragged:
+        cnt = (u % np.uint64(2 * cmds_per_inst + 1)).astype(np.int64)
+    else:
+        cnt = np.full(n_inst, cmds_per_inst, np.int64)
+    off = np.zeros(n_inst + 1, np.uint64)
+    np.cumsum(cnt, out=off[1:])
+    m = int(off[-1])
+    op, key, val = commands(m, 1 << 20, 0.5, "uniform", seed=seed)
+    recs = np.zeros(n_inst, R.LOG_REC)
+    recs["ballot"] = np.where((u >> np.uint64(40)) % np.uint64(64) == 0, 32, 16)
+    recs["status"] = R.COMMITTED
+    recs["inst_no"] = np.arange(first_inst, first_inst + n_inst, dtype=np.int64).astype(np.int32)
+    return recs, off, op, key, val

@@ -123,4 +123,57 @@ int orc_encode_replies(const mpx_reply_rec* recs, size_t n, uint32_t n_clients, 
     return MPX_OK;
 }
 
+// Instance-log encodings of a run of log records:
+//   MPX_LOG_CATCHUP  (*Instance).Marshal  minpaxosprotomarsh.go:100-124: Ballot (4 bytes LE),
+//                    int32(Status) (4), binary.PutVarint(len(Cmds)) written as b[0:wlen] (:117-120),
+//                    then Cmds[i].Marshal (statemarsh.go:8-19): Op byte, K and V little endian.
+//   MPX_LOG_DURABLE  recordInstanceMetadata  bareminpaxos.go:164-174 (Ballot, Status, instNo as
+//                    LittleEndian.PutUint32) + recordCommands :177-188 (nil -> nothing).
+namespace {
+size_t put_varint(uint8_t* b, int64_t x) {  // encoding/binary.PutVarint
+    uint64_t ux = (uint64_t)x << 1;
+    if (x < 0) ux = ~ux;
+    size_t i = 0;
+    while (ux >= 0x80) {
+        b[i++] = (uint8_t)(ux | 0x80);
+        ux >>= 7;
+    }
+    b[i++] = (uint8_t)ux;
+    return i;
+}
+void put_le(std::vector<uint8_t>& w, uint64_t v, int bytes) {
+    for (int k = 0; k < bytes; ++k) w.push_back((uint8_t)(v >> (8 * k)));
+}
+}  // namespace
+
+int orc_encode_log(int format, const mpx_log_rec* recs, size_t n, const uint64_t* cmd_off,
+                   const uint8_t* op, const int64_t* key, const int64_t* val, uint8_t* out,
+                   size_t out_cap, uint64_t* rec_off) {
+    if (format != MPX_LOG_CATCHUP && format != MPX_LOG_DURABLE) return MPX_E_INVAL;
+    std::vector<uint8_t> w;
+    for (size_t i = 0; i < n; ++i) {
+        rec_off[i] = w.size();
+        const mpx_log_rec& r = recs[i];
+        const uint64_t c0 = cmd_off[i], c1 = cmd_off[i + 1];
+        put_le(w, (uint32_t)r.ballot, 4);
+        put_le(w, (uint32_t)r.status, 4);
+        if (format == MPX_LOG_CATCHUP) {
+            uint8_t b[10];
+            const size_t l = put_varint(b, (int64_t)(c1 - c0));
+            w.insert(w.end(), b, b + l);
+        } else {
+            put_le(w, (uint32_t)r.inst_no, 4);
+        }
+        for (uint64_t j = c0; j < c1; ++j) {
+            w.push_back(op[j]);
+            put_le(w, (uint64_t)key[j], 8);
+            put_le(w, (uint64_t)val[j], 8);
+        }
+    }
+    rec_off[n] = w.size();
+    if (w.size() > out_cap) return MPX_E_INVAL;
+    if (!w.empty()) memcpy(out, w.data(), w.size());
+    return MPX_OK;
+}
+
 }  // extern "C"

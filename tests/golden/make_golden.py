@@ -71,6 +71,10 @@ def cases():
         [head, var, synth.peer_stream(drec[1000:], seed=51)])))
     out["fanout_replies"] = ("fanout", dict(n_clients=37, ok=1, leader=3),
                              dict(recs=synth.replies(5000, 37, seed=54)))
+    lrec, loff, lop, lkey, lval = synth.log_records(3000, 4, seed=57, ragged=True)
+    for fmt, fname in ((R.LOG_CATCHUP, "catchup"), (R.LOG_DURABLE, "durable")):
+        out[f"log_{fname}"] = ("log", dict(fmt=fmt),
+                               dict(recs=lrec, cmd_off=loff, op=lop, key=lkey, val=lval))
     return out
 
 
@@ -109,6 +113,10 @@ def run_case(kind, p, x, backend_mk):
         b = backend_mk(5, R.MODE_MIN)
         out, off = b.encode_replies(x["recs"], p["n_clients"], p["ok"], p["leader"])
         return dict(out=out, client_off=off)
+    if kind == "log":
+        b = backend_mk(5, R.MODE_MIN)
+        out, ro = b.encode_log(p["fmt"], x["recs"], x["cmd_off"], x["op"], x["key"], x["val"])
+        return dict(out=out, rec_off=ro)
     raise ValueError(kind)
 
 

@@ -52,6 +52,7 @@ def load():
         "orc_bench_apply": (C.c_int64, [_p, _p, _sz, _p, _p, _p, _sz, _p]),
         "orc_decode_peer_stream": (C.c_int, [_p, _sz, _p, _sz, _p, _sz, _p]),
         "orc_encode_replies": (C.c_int, [_p, _sz, C.c_uint32, C.c_uint8, _i32, _p, _p]),
+        "orc_encode_log": (C.c_int, [C.c_int, _p, _sz, _p, _p, _p, _p, _p, _sz, _p]),
         "orc_bench_group_step": (C.c_int64, [C.c_int, C.c_int, C.POINTER(L.MpxGroupBatch),
                                              C.c_uint32, C.c_int]),
     }
@@ -190,6 +191,20 @@ class Oracle:
         _check(self.lib.orc_encode_replies(_ptr(recs), n, n_clients, ok, leader, _ptr(out),
                                            _ptr(off)), "orc_encode_replies")
         return out[:n * R.PROPOSE_REPLY_BYTES], off
+
+    def encode_log(self, fmt, recs, cmd_off, op, key, val):
+        recs = np.ascontiguousarray(recs, R.LOG_REC)
+        off = np.ascontiguousarray(cmd_off, np.uint64)
+        op = np.ascontiguousarray(op, np.uint8)
+        key = np.ascontiguousarray(key, np.int64)
+        val = np.ascontiguousarray(val, np.int64)
+        n, m = len(recs), len(op)
+        cap = n * 18 + 17 * m
+        out = np.zeros(max(cap, 1), np.uint8)
+        ro = np.zeros(n + 1, np.uint64)
+        _check(self.lib.orc_encode_log(fmt, _ptr(recs), n, _ptr(off), _ptr(op), _ptr(key),
+                                       _ptr(val), _ptr(out), cap, _ptr(ro)), "orc_encode_log")
+        return out[:int(ro[-1])], ro
 
     def group_step(self, b, kv_cnt=None, kv_key=None, kv_val=None, ret=None, want_conf=True,
                    want_decided=True):
