@@ -1,5 +1,6 @@
 #!/bin/bash
-# GPU-box rocprofv3 kernel stats for the single-kernel configurations (BASELINE configs 2-4).
+# GPU-box rocprofv3 kernel stats + bench lines (with CPU baselines) for the single-path
+# workloads: BASELINE configs 2-4 and the SURVEY 8(f) rows (decode, fanout, log).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -11,12 +12,16 @@ run() {
   rc=$?; echo "$name rc=$rc"; grep '^{' $OUT/$name.log | tail -1 | cut -c1-400
   case $rc in 0) ;; *) exit $rc;; esac
 }
-for w in ${WORKLOADS:-tally_min tally_classic prepare apply_uniform apply_zipf}; do
+for w in ${WORKLOADS:-tally_min tally_classic prepare apply_uniform apply_zipf decode fanout log_catchup log_durable}; do
   case $w in
     tally_min) run $w --workload tally --mode min --steps 10 --warmup 2 ${XARGS:-};;
     tally_classic) run $w --workload tally --mode classic --steps 10 --warmup 2 ${XARGS:-};;
     prepare) run $w --workload prepare --steps 10 --warmup 2 ${XARGS:-};;
     apply_uniform) run $w --workload apply --dist uniform --steps 5 --warmup 1 ${XARGS:-};;
     apply_zipf) run $w --workload apply --dist zipf --steps 5 --warmup 1 ${XARGS:-};;
+    decode) run $w --workload decode --steps 10 --warmup 2 ${XARGS:-};;
+    fanout) run $w --workload fanout --steps 10 --warmup 2 ${XARGS:-};;
+    log_catchup) run $w --workload log --log-format catchup --steps 10 --warmup 2 ${XARGS:-};;
+    log_durable) run $w --workload log --log-format durable --steps 10 --warmup 2 ${XARGS:-};;
   esac
 done
