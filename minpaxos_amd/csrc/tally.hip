@@ -142,20 +142,58 @@ __global__ void k_tally_init(unsigned long long* red, uint64_t n_inst) {
 // CLASSIC updateCommittedUpTo (paxos.go:259-264) over the final statuses: find the first
 // instance >= committedUpTo+1 that is not COMMITTED (final COMMITTED <=> st_in COMMITTED or
 // decided in this call).
+// The first non-committed instance is almost always a few instances past committedUpTo, so one
+// block scans the head window [j0, j0 + kHeadWindow) in order and stops at the first hit; the
+// grid-wide kernel below then covers the rest of the window only if the head found nothing.
+constexpr uint64_t kHeadWindow = 1ull << 16;
+__global__ __launch_bounds__(256) void k_classic_first_bad_head(
+    const mpx_inst_state* __restrict__ st, const uint8_t* __restrict__ decided, uint64_t n_inst,
+    int32_t base, const int32_t* __restrict__ scalars, unsigned long long* __restrict__ red) {
+    __shared__ int found;
+    if (red[0] == 0) return;
+    const int64_t j0 = (int64_t)scalars[0] + 1 - base;
+    if (j0 < 0 || (uint64_t)j0 >= n_inst) return;
+    const uint64_t end = (uint64_t)j0 + kHeadWindow < n_inst ? (uint64_t)j0 + kHeadWindow : n_inst;
+    if (threadIdx.x == 0) found = 0;
+    __syncthreads();
+    for (uint64_t b = (uint64_t)j0; b < end; b += blockDim.x) {
+        const uint64_t j = b + threadIdx.x;
+        const bool bad = j < end && !(st[j].status == MPX_COMMITTED || (decided && decided[j]));
+        const uint64_t m = ballot(bad);
+        if (m && lane_id() == 0) {
+            atomicMin(&red[kRedFirstBad], (unsigned long long)(j + lo_bit(m)));
+            found = 1;
+        }
+        __syncthreads();
+        if (found) break;  // uniform per block
+    }
+}
+
 __global__ __launch_bounds__(256) void k_classic_first_bad(
     const mpx_inst_state* __restrict__ st, const uint8_t* __restrict__ decided, uint64_t n_inst,
     int32_t base, const int32_t* __restrict__ scalars, unsigned long long* __restrict__ red) {
+    __shared__ unsigned long long fb_s;
     if (red[0] == 0) return;  // no crossing in this call: committedUpTo unchanged
-    const int64_t j0 = (int64_t)scalars[0] + 1 - base;
-    if (j0 < 0 || (uint64_t)j0 >= n_inst) return;
+    const int64_t jc = (int64_t)scalars[0] + 1 - base;
+    if (jc < 0 || (uint64_t)jc >= n_inst) return;
+    const int64_t j0 = jc + (int64_t)kHeadWindow;  // the head kernel covered [jc, j0)
+    if ((uint64_t)j0 >= n_inst) return;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t)j0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n_inst;
-         j += stride) {
-        const unsigned long long fb = __hip_atomic_load(&red[kRedFirstBad], __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
-        if (j >= fb) break;
-        const bool committed = st[j].status == MPX_COMMITTED || (decided && decided[j]);
-        if (!committed) atomicMin(&red[kRedFirstBad], (unsigned long long)j);
+    for (uint64_t b = (uint64_t)j0 + (uint64_t)blockIdx.x * blockDim.x; b < n_inst; b += stride) {
+        // one read of the running minimum per block and round (a per-thread atomic load of one
+        // address serialises every thread of the grid on a single L2 channel)
+        if (threadIdx.x == 0)
+            fb_s = __hip_atomic_load(&red[kRedFirstBad], __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const unsigned long long fb = fb_s;
+        __syncthreads();
+        if (b >= fb) break;  // uniform per block
+        const uint64_t j = b + threadIdx.x;
+        const bool bad = j < n_inst && !(st[j].status == MPX_COMMITTED || (decided && decided[j]));
+        const uint64_t m = ballot(bad);
+        if (m && lane_id() == 0)  // the wave's first non-committed instance, one atomic per wave
+            atomicMin(&red[kRedFirstBad], (unsigned long long)(j + lo_bit(m)));
     }
 }
 
@@ -199,6 +237,8 @@ hipError_t launch_accept_tally(int mode, const mpx_accept_reply* recs, uint64_t 
         if (n_inst) {
             uint64_t blocks = (n_inst + 255) / 256;
             if (blocks > 2048) blocks = 2048;
+            k_classic_first_bad_head<<<1, 256, 0, stream>>>(st_in, decided, n_inst, base,
+                                                            scalars, red);
             k_classic_first_bad<<<dim3((unsigned)blocks), 256, 0, stream>>>(st_in, decided, n_inst,
                                                                              base, scalars, red);
         }
@@ -218,6 +258,7 @@ hipError_t launch_committed_prefix(const mpx_inst_state* st, uint64_t n_inst, in
     if (n_inst) {
         uint64_t blocks = (n_inst + 255) / 256;
         if (blocks > 2048) blocks = 2048;
+        k_classic_first_bad_head<<<1, 256, 0, stream>>>(st, nullptr, n_inst, base, scalars, red);
         k_classic_first_bad<<<dim3((unsigned)blocks), 256, 0, stream>>>(st, nullptr, n_inst, base,
                                                                          scalars, red);
     }
