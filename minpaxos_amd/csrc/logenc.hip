@@ -11,10 +11,10 @@
 //                    instNo u32) followed by recordCommands (:177-188: Command.Marshal each; a
 //                    nil slice writes nothing), one record per stable-store append.
 // Pipeline: k_log_sizes (bytes per record) -> rocPRIM inclusive scan (record offsets) ->
-// k_log_emit, output-parallel: each 4 KB block finds its first record by binary search over the
-// offsets, stages the offsets of the records it overlaps in LDS, and every thread produces 16
-// consecutive output bytes and stores them as one vector (coalesced, no partial lines except at
-// the run's two ends).
+// k_log_block_first (the record holding each 4 KB output block's first byte) -> k_log_emit:
+// per block, the overlapping records' headers and commands are written into an LDS image of the
+// block (one thread per header, one per command, so the command loads are coalesced) and the
+// image goes out as 16-byte vector stores (no partial lines except at the run's two ends).
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -76,90 +76,95 @@ __global__ __launch_bounds__(256) void k_log_block_first(const uint64_t* __restr
     }
 }
 
-// rec_off: n+1 record offsets (rec_off[n] = total bytes)
+// rec_off: n+1 record offsets (rec_off[n] = total bytes). One block per 4 KB output window:
+// the records overlapping it are first .. first+nr-1 (blk_first of this block and the next);
+// their headers and the commands overlapping the window are written into an LDS image of the
+// window (a thread per header, a thread per command: op/key/val loads are coalesced across
+// threads), which then goes out as 16-byte vector stores.
 __global__ __launch_bounds__(kLogBlock) void k_log_emit(
     int format, const mpx_log_rec* __restrict__ recs, const uint64_t* __restrict__ cmd_off,
     const uint8_t* __restrict__ op, const int64_t* __restrict__ key,
     const int64_t* __restrict__ val, uint64_t n, const uint64_t* __restrict__ rec_off,
-    const uint64_t* __restrict__ blk_first, uint8_t* __restrict__ out) {
+    const uint64_t* __restrict__ blk_first, uint32_t n_blocks, uint8_t* __restrict__ out) {
     __shared__ uint64_t off[kLogMaxRecs + 1];
+    __shared__ uint64_t coff[kLogMaxRecs + 1];
+    __shared__ __attribute__((aligned(16))) uint8_t S[kLogBlockBytes];
     const uint64_t total = rec_off[n];
     const uint64_t b0 = (uint64_t)blockIdx.x * kLogBlockBytes;
     if (b0 >= total) return;  // uniform per block
     const uint64_t first = blk_first[blockIdx.x];
     const uint64_t b1 = b0 + kLogBlockBytes < total ? b0 + kLogBlockBytes : total;
-    // offsets of the records overlapping [b0, b1), plus the end of the last one
-    const uint64_t maxr = n - first < (uint64_t)kLogMaxRecs ? n - first : (uint64_t)kLogMaxRecs;
-    for (uint64_t k = threadIdx.x; k <= maxr; k += kLogBlock) off[k] = rec_off[first + k];
+    const uint64_t nr = (b1 < total && blockIdx.x + 1 < n_blocks)
+                            ? blk_first[blockIdx.x + 1] - first + 1
+                            : n - first;
+    for (uint64_t k = threadIdx.x; k <= nr; k += kLogBlock) {
+        off[k] = rec_off[first + k];
+        coff[k] = cmd_off[first + k];
+    }
     __syncthreads();
-    // at most kLogMaxRecs - 1 records start inside one block, so off[0..maxr] covers every
-    // record that overlaps it
-    const uint32_t nr = (uint32_t)maxr;
-    const uint64_t o0 = b0 + (uint64_t)threadIdx.x * 16;
-    if (o0 >= b1) return;
-    // the record holding o0
-    uint32_t lo = 0, hi = nr;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) / 2;
-        if (off[mid] <= o0) lo = mid;
-        else hi = mid;
-    }
-    // walk the 16 bytes with a cursor: the record's header fields and the current command are
-    // loaded once, not per byte
-    uint32_t r = lo;
-    uint64_t rs = 0, re = off[r], ri = 0, c0 = 0;
-    uint32_t hb = 0, w_ballot = 0, w_status = 0, w_third = 0;
-    uint64_t zz = 0;
-    uint64_t cur_x = ~0ull, k_key = 0, k_val = 0;
-    uint32_t k_op = 0;
-    bool first_rec = true;
-    uint32_t bytes[4] = {0, 0, 0, 0};
-    const uint32_t cnt = (uint32_t)(b1 - o0 < 16 ? b1 - o0 : 16);
-    for (uint32_t k = 0; k < cnt; ++k) {
-        const uint64_t o = o0 + k;
-        while (first_rec || o >= re) {  // (next) record
-            if (!first_rec) ++r;
-            first_rec = false;
-            rs = off[r];
-            re = off[r + 1];
-            ri = first + r;
-            c0 = cmd_off[ri];
-            const uint64_t nc = cmd_off[ri + 1] - c0;
-            hb = (uint32_t)(re - rs - 17 * nc);
-            const mpx_log_rec m = recs[ri];
-            w_ballot = (uint32_t)m.ballot;
-            w_status = (uint32_t)m.status;
-            w_third = (uint32_t)m.inst_no;
-            zz = zigzag((int64_t)nc);
-            cur_x = ~0ull;
+    // headers
+    for (uint64_t k = threadIdx.x; k < nr; k += kLogBlock) {
+        const uint64_t rs = off[k], nc = coff[k + 1] - coff[k];
+        const uint32_t hb = (uint32_t)(off[k + 1] - rs - 17 * nc);
+        if (rs + hb <= b0 || rs >= b1) continue;
+        const mpx_log_rec m = recs[first + k];
+        const uint64_t zz = zigzag((int64_t)nc);
+        for (uint32_t h = 0; h < hb; ++h) {
+            const uint64_t o = rs + h;
+            if (o < b0 || o >= b1) continue;
+            uint32_t v;
+            if (h < 4) v = ((uint32_t)m.ballot >> (8 * h)) & 0xFF;
+            else if (h < 8) v = ((uint32_t)m.status >> (8 * (h - 4))) & 0xFF;
+            else if (format == MPX_LOG_DURABLE) v = ((uint32_t)m.inst_no >> (8 * (h - 8))) & 0xFF;
+            else v = uvarint_byte(zz, h - 8);
+            S[o - b0] = (uint8_t)v;
         }
-        const uint32_t rel = (uint32_t)(o - rs);
-        uint32_t v;
-        if (rel < hb) {
-            if (rel < 4) v = (w_ballot >> (8 * rel)) & 0xFF;
-            else if (rel < 8) v = (w_status >> (8 * (rel - 4))) & 0xFF;
-            else if (format == MPX_LOG_DURABLE) v = (w_third >> (8 * (rel - 8))) & 0xFF;
-            else v = uvarint_byte(zz, rel - 8);
-        } else {
-            const uint64_t x = rel - hb;
-            if (cur_x == ~0ull || x >= cur_x + 17) {  // a new command: load it once
-                cur_x = x - x % 17;
-                const uint64_t j = c0 + x / 17;
-                k_op = op[j];
-                k_key = (uint64_t)key[j];
-                k_val = (uint64_t)val[j];
-            }
-            const uint32_t f = (uint32_t)(x - cur_x);
-            if (f == 0) v = k_op;
-            else if (f < 9) v = (uint32_t)(k_key >> (8 * (f - 1))) & 0xFF;
-            else v = (uint32_t)(k_val >> (8 * (f - 9))) & 0xFF;
-        }
-        bytes[k >> 2] |= v << (8 * (k & 3));
     }
-    if (cnt == 16 && (((uintptr_t)(out + o0)) & 15) == 0) {
-        *reinterpret_cast<uint4*>(out + o0) = make_uint4(bytes[0], bytes[1], bytes[2], bytes[3]);
+    // commands overlapping [b0, b1): [j_lo, j_hi) (all commands of the records strictly
+    // inside, the tail of the first record, the head of the last)
+    uint64_t j_lo, j_hi;
+    {
+        const uint64_t hb0 = off[1] - off[0] - 17 * (coff[1] - coff[0]);
+        const uint64_t cs0 = off[0] + hb0;  // first record's commands start here
+        j_lo = coff[0] + (b0 > cs0 ? (b0 - cs0) / 17 : 0);
+        const uint64_t L = nr - 1;
+        const uint64_t hbl = off[L + 1] - off[L] - 17 * (coff[L + 1] - coff[L]);
+        const uint64_t csl = off[L] + hbl;
+        const uint64_t c = b1 > csl ? (b1 - csl + 16) / 17 : 0;
+        j_hi = coff[L] + c < coff[L + 1] ? coff[L] + c : coff[L + 1];
+    }
+    for (uint64_t j = j_lo + threadIdx.x; j < j_hi; j += kLogBlock) {
+        uint32_t lo = 0, hi = (uint32_t)nr;  // the record holding command j
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) / 2;
+            if (coff[mid] <= j) lo = mid;
+            else hi = mid;
+        }
+        while (lo + 1 < nr && coff[lo + 1] <= j) ++lo;  // skip records without commands
+        const uint64_t nc = coff[lo + 1] - coff[lo];
+        const uint64_t cs = off[lo + 1] - 17 * nc;  // commands of record lo start here
+        const uint64_t pos = cs + 17 * (j - coff[lo]);
+        const uint32_t o8 = op[j];
+        const uint64_t k8 = (uint64_t)key[j], v8 = (uint64_t)val[j];
+#pragma unroll
+        for (int f = 0; f < 17; ++f) {
+            const uint64_t o = pos + f;
+            if (o < b0 || o >= b1) continue;
+            const uint32_t v = f == 0 ? o8 : f < 9 ? (uint32_t)(k8 >> (8 * (f - 1))) & 0xFF
+                                                   : (uint32_t)(v8 >> (8 * (f - 9))) & 0xFF;
+            S[o - b0] = (uint8_t)v;
+        }
+    }
+    __syncthreads();
+    const uint32_t bytes = (uint32_t)(b1 - b0);
+    uint8_t* dst = out + b0;
+    if (((uintptr_t)dst & 15) == 0) {
+        const uint32_t nv = bytes / 16;
+        for (uint32_t i = threadIdx.x; i < nv; i += kLogBlock)
+            reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(S)[i];
+        for (uint32_t i = nv * 16 + threadIdx.x; i < bytes; i += kLogBlock) dst[i] = S[i];
     } else {
-        for (uint32_t k = 0; k < cnt; ++k) out[o0 + k] = (uint8_t)(bytes[k >> 2] >> (8 * (k & 3)));
+        for (uint32_t i = threadIdx.x; i < bytes; i += kLogBlock) dst[i] = S[i];
     }
 }
 
@@ -203,7 +208,8 @@ hipError_t launch_encode_log(int format, const mpx_log_rec* recs, uint64_t n,
     k_log_block_first<<<gg, 256, 0, stream>>>(rec_off, n, (uint32_t)blocks, blk_first);
     // grid from the largest possible output (the exact size is only known on the device)
     k_log_emit<<<(unsigned)blocks, kLogBlock, 0, stream>>>(format, recs, cmd_off, op, key, val, n,
-                                                          rec_off, blk_first, out);
+                                                          rec_off, blk_first, (uint32_t)blocks,
+                                                          out);
     return hipGetLastError();
 }
 
