@@ -128,7 +128,7 @@ __device__ __forceinline__ void load_chunk(const uint8_t* __restrict__ buf, uint
         const uint4* s = reinterpret_cast<const uint4*>(buf + c0);
 #pragma unroll
         for (int i = 0; i < kChunk / 16; ++i) {
-            const uint4 v = s[i];
+            const uint4 v = s[i];  // default policy: the emit pass reads the stream again
             wd[4 * i] = v.x;
             wd[4 * i + 1] = v.y;
             wd[4 * i + 2] = v.z;

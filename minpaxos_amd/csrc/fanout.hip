@@ -83,7 +83,7 @@ __global__ __launch_bounds__(kFanBlock) void k_fan_encode(
     if (kAligned) {  // q0 * 25 is a multiple of 16: full 16-byte vectors, then the tail
         const uint32_t nv = bytes / 16;
         for (uint32_t i = threadIdx.x; i < nv; i += kFanBlock)
-            reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(S)[i];
+            st_stream(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(S)[i]);
         for (uint32_t i = nv * 16 + threadIdx.x; i < bytes; i += kFanBlock) dst[i] = S[i];
     } else {
         for (uint32_t i = threadIdx.x; i < bytes; i += kFanBlock) dst[i] = S[i];

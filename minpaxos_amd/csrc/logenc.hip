@@ -161,7 +161,7 @@ __global__ __launch_bounds__(kLogBlock) void k_log_emit(
     if (((uintptr_t)dst & 15) == 0) {
         const uint32_t nv = bytes / 16;
         for (uint32_t i = threadIdx.x; i < nv; i += kLogBlock)
-            reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(S)[i];
+            st_stream(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(S)[i]);
         for (uint32_t i = nv * 16 + threadIdx.x; i < bytes; i += kLogBlock) dst[i] = S[i];
     } else {
         for (uint32_t i = threadIdx.x; i < bytes; i += kLogBlock) dst[i] = S[i];

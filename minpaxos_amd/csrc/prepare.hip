@@ -42,8 +42,8 @@ __global__ __launch_bounds__(kTileBlock) void k_prepare_tile(
         const int32_t inst = own ? S.rec[a].x : 0;
         const int64_t idx = (int64_t)inst - base;
         const bool inwin = own && idx >= 0 && (uint64_t)idx < n_inst;
-        int4 A = inwin ? s4[2 * idx] : make_int4(0, MPX_STATUS_NIL, 0, 0);      // ballot status oks nacks
-        int4 B = inwin ? s4[2 * idx + 1] : make_int4(0, 0, 0, 0);              // mx value_id flags pad
+        int4 A = inwin ? ld_stream(s4 + 2 * idx) : make_int4(0, MPX_STATUS_NIL, 0, 0);      // ballot status oks nacks
+        int4 B = inwin ? ld_stream(s4 + 2 * idx + 1) : make_int4(0, 0, 0, 0);              // mx value_id flags pad
         const bool live_inst = inwin && A.y != MPX_STATUS_NIL;
         ebits |= (own && !live_inst) ? kErrNil : 0u;
         // per-call event flags describe this call (the head record clears them)
@@ -88,9 +88,9 @@ __global__ __launch_bounds__(kTileBlock) void k_prepare_tile(
         for (uint64_t q = after; live_inst && q < oend; ++q) step(r4[q]);
         if (inwin && live_inst) {
             B.z = (int32_t)fl;
-            o4[2 * idx] = A;
-            o4[2 * idx + 1] = B;
-            if (prepared) prepared[idx] = prep ? 1 : 0;
+            st_stream(o4 + 2 * idx, A);
+            st_stream(o4 + 2 * idx + 1, B);
+            if (prepared) st_stream(prepared + idx, (uint8_t)(prep ? 1 : 0));
         }
         // defaultBallot = max(defaultBallot, inst.ballot) over newly prepared instances
         uint32_t key = (live_inst && prep) ? ((uint32_t)A.x ^ 0x80000000u) : 0u;

@@ -370,7 +370,7 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
 #pragma unroll
         for (int k = 0; k < kFRecPer; ++k) {
             const uint32_t p = t + k * kStepBlock;
-            rr[k] = load_rec(b.recs, r0 + (p < last ? p : last));
+            rr[k] = ld_stream(reinterpret_cast<const int4*>(b.recs) + r0 + (p < last ? p : last));
         }
     } else {
 #pragma unroll
@@ -378,7 +378,7 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     }
     const bool own = (uint32_t)t < ipg;  // this lane owns instance t
     const uint32_t ti = own ? (uint32_t)t : ipg - 1;
-    int4 st = reinterpret_cast<const int4*>(b.st_in)[gi0 + ti];
+    int4 st = ld_stream(reinterpret_cast<const int4*>(b.st_in) + gi0 + ti);
     const uint32_t co = b.cmd_off[gi0 + ti];
     const uint8_t hs = b.has_cmds ? b.has_cmds[gi0 + ti] : (uint8_t)1;
     const uint64_t ei = (uint64_t)g * kvpg + ((uint32_t)t < kcnt ? (uint32_t)t : (kcnt ? kcnt - 1 : 0));
@@ -419,8 +419,8 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     for (int k = 0; k < kFPer; ++k) {
         const uint32_t li = cbase + k * kWave;
         const uint64_t ci = c_lo + (li < clast ? li : clast);
-        o[k] = ncmd ? b.op[ci] : (uint8_t)0;
-        ck[k] = ncmd ? b.key[ci] : 0;
+        o[k] = ncmd ? ld_stream(b.op + ci) : (uint8_t)0;
+        ck[k] = ncmd ? ld_stream(b.key + ci) : 0;
     }
     __syncthreads();  // B1
     STAMP(0);
@@ -575,7 +575,7 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
 #pragma unroll
     for (int k = 0; k < kFPer; ++k) {
         const uint32_t li = cbase + k * kWave;
-        cv[k] = ncmd ? b.val[c_lo + (li < clast ? li : clast)] : 0;
+        cv[k] = ncmd ? ld_stream(b.val + c_lo + (li < clast ? li : clast)) : 0;
     }
     uint32_t ops = 0;  // the four opcodes, one byte each
 #pragma unroll
@@ -663,7 +663,7 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     // the group stays here: the instance outputs can go now (st_out may alias st_in, so not
     // before this point)
     if (own) {
-        if (!(MPX_ABLATE & 16) && touched) reinterpret_cast<int4*>(b.st_out)[gi0 + t] = st;
+        if (!(MPX_ABLATE & 16) && touched) st_stream(reinterpret_cast<int4*>(b.st_out) + gi0 + t, st);
         if (b.decided) b.decided[gi0 + t] = dec ? 1 : 0;
     }
     STAMP(4);
@@ -696,8 +696,8 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
         const int64_t r = isput ? sv : (op == MPX_OP_GET ? (lastput >= 0 ? sv : (intab ? at_start : 0)) : 0);
         const bool conf = hasprev && (prevput || isput);      // state.Conflict(prev, this)
         if (act) {
-            b.ret[c_lo + li] = r;
-            if (b.conf_prev) b.conf_prev[c_lo + li] = conf ? 1 : 0;
+            st_stream(b.ret + c_lo + li, r);
+            if (b.conf_prev) st_stream(b.conf_prev + c_lo + li, (uint8_t)(conf ? 1 : 0));
             if (isput && lastput < 0 && !intab) {  // first PUT of a new key: its append rank
                 fnew |= 1u << k;
                 atomicOr(&S.newbits[li >> 5], 1u << (li & 31));

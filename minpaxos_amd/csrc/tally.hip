@@ -31,7 +31,7 @@ __global__ __launch_bounds__(kTileBlock) void k_accept_tile(
         const int32_t inst = own ? S.rec[a].x : 0;
         const int64_t idx = (int64_t)inst - base;
         const bool inwin = own && idx >= 0 && (uint64_t)idx < n_inst;
-        int4 st = inwin ? reinterpret_cast<const int4*>(st_in)[idx]
+        int4 st = inwin ? ld_stream(reinterpret_cast<const int4*>(st_in) + idx)
                         : make_int4(MPX_STATUS_NIL, 0, 0, 0);
         const bool nil = st.x == MPX_STATUS_NIL;
         ebits |= (own && !inwin) ? kErrNil : 0u;  // outside instanceSpace
@@ -79,8 +79,8 @@ __global__ __launch_bounds__(kTileBlock) void k_accept_tile(
         // the overhang of the tile's last instance (one lane per tile)
         for (uint64_t q = after; inwin && q < oend; ++q) step(r4[q], 1);
         if (inwin) {
-            reinterpret_cast<int4*>(st_out)[idx] = st;
-            if (decided) decided[idx] = deci ? 1 : 0;
+            st_stream(reinterpret_cast<int4*>(st_out) + idx, st);
+            if (decided) st_stream(decided + idx, (uint8_t)(deci ? 1 : 0));
         }
         const uint32_t key = (uint32_t)(idx + 1);
         if (MODE == MPX_MODE_MIN) {

@@ -32,7 +32,7 @@ struct TileLds {
 };
 
 __device__ __forceinline__ int4 tile_load(const int4* __restrict__ recs, uint64_t n, uint64_t p) {
-    return p < n ? recs[p] : make_int4(0, 0, 0, 0);
+    return p < n ? ld_stream(recs + p) : make_int4(0, 0, 0, 0);
 }
 
 // Runs body(pos_first, count, overhang_end, t_round) for every owned instance of every tile this
