@@ -12,14 +12,17 @@
 // Only keys that are PUT in this call or already present can change any output, so:
 //   0. k_epoch_bump       a new call epoch (device counter, so captured graphs stay correct)
 //   1. k_kv_insert_puts   insert every PUT key of the whole call (one 64-bit CAS per probe; the
-//                         key INT64_MIN is kept in a side slot so the table needs no key state)
+//                         key INT64_MIN is kept in a side slot so the table needs no key state);
+//                         in a one-chunk call a PUT also writes its sort key (2) from the slot
+//                         the insert returned, so step 2 probes the non-PUT commands only
 // then the log is cut into chunks of C commands, processed in order; per chunk:
 //   2. k_kv_lookup        sort key (slot << 32 | j << 2 | op class) of every command j of the
 //                         chunk (absent, never-PUT keys: ret 0, conf 0 now, sorted last)
 //   3. radix sort on the slot bits - stable, so log order within a slot; the op class rides in
 //                         the key's low bits
-//   4. k_apply_mark       per sorted position q: slot[q], lp[q] = q if PUT else -1
-//   5. segmented inclusive max-scan of lp by slot  -> last PUT at or before q in its slot
+//   4-5. segmented inclusive max-scan by slot of (q if PUT else -1) -> last PUT at or before q
+//                         in its slot; keys and values are transform iterators over the sorted
+//                         keys, so nothing but the scan's output is materialised
 //   6. k_apply_finish     a 32-bit result code per command (conf bit + where its ret comes
 //                         from); a slot's first command in the chunk takes its predecessor
 //                         from the table's per-slot state word (epoch-tagged)
@@ -33,7 +36,7 @@
 // results travel back by a second radix sort instead; what stays random is one table probe per
 // command (2), one per PUT (1) and one value gather per GET (8), all reads. Chunks only bound
 // the scratch memory.
-// Steps 3 and 5 use rocPRIM device primitives (stable LSD radix sort, look-back scan_by_key).
+// Steps 3, 5 and 7 use rocPRIM device primitives (stable LSD radix sort, look-back scan_by_key).
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -173,12 +176,22 @@ hipError_t launch_kv_export(KvTable& t, int64_t* keys, int64_t* vals, uint64_t c
 }
 
 // ---- the apply pipeline -------------------------------------------------------------------
+// kKeys (single-chunk calls): the insert's slot is the PUT's sort key slot, so the PUT also
+// writes its sort key here and the lookup pass probes only the other commands
+template <bool kKeys>
 __global__ __launch_bounds__(256) void k_kv_insert_puts(KvTable t, const uint8_t* __restrict__ op,
                                                         const int64_t* __restrict__ key,
-                                                        uint64_t m, uint32_t* err) {
+                                                        uint64_t m, uint32_t* err,
+                                                        uint64_t* __restrict__ skey) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride)
-        if (op[i] == MPX_OP_PUT) kv_insert(t, key[i], err);
+        if (op[i] == MPX_OP_PUT) {
+            const int64_t s = kv_insert(t, key[i], err);
+            if (kKeys) {
+                const uint64_t sl = s < 0 ? t.cap + 1 : (uint64_t)s;  // full table: call fails
+                skey[i] = (sl << 32) | (i << 2) | kClsPut;
+            }
+        }
 }
 
 __device__ __forceinline__ uint32_t op_class(uint8_t o) {
@@ -188,30 +201,38 @@ __device__ __forceinline__ uint32_t op_class(uint8_t o) {
 // sort key of chunk command j: slot << 32 | j << 2 | class; an absent key that is never PUT in
 // this call gets slot cap+1 (sorts last; its outputs are zero: GET -> NIL, and no conflict since
 // nothing before or after it on that key in this call is a PUT)
+template <bool kSkipPut>
 __global__ __launch_bounds__(256) void k_kv_lookup(KvTable t, const uint8_t* __restrict__ op,
                                                    const int64_t* __restrict__ key, uint64_t n,
                                                    uint64_t* __restrict__ skey) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+        const uint8_t o = op[j];
+        if (kSkipPut && o == MPX_OP_PUT) continue;
         const int64_t s = kv_lookup(t, key[j]);
         const uint64_t sl = s < 0 ? t.cap + 1 : (uint64_t)s;
-        skey[j] = (sl << 32) | (j << 2) | op_class(op[j]);
+        skey[j] = (sl << 32) | (j << 2) | op_class(o);
     }
 }
 
 __device__ __forceinline__ uint32_t sk_index(uint64_t k) { return (uint32_t)k >> 2; }
 __device__ __forceinline__ uint32_t sk_class(uint64_t k) { return (uint32_t)k & 3u; }
 
-__global__ __launch_bounds__(256) void k_apply_mark(const uint64_t* __restrict__ skey, uint64_t n,
-                                                    uint32_t* __restrict__ sslot,
-                                                    int32_t* __restrict__ lp) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
-        const uint64_t k = skey[q];
-        sslot[q] = (uint32_t)(k >> 32);
-        lp[q] = sk_class(k) == kClsPut ? (int32_t)q : -1;
+// the segmented max-scan reads its keys (slots) and values (own position if PUT, else -1)
+// straight from the sorted keys: no materialised slot / position arrays
+__device__ __forceinline__ uint32_t sk_slot(uint64_t k) { return (uint32_t)(k >> 32); }
+struct SlotOf {
+    __host__ __device__ uint32_t operator()(uint64_t k) const { return (uint32_t)(k >> 32); }
+};
+struct PutPos {
+    const uint64_t* skey;
+    __host__ __device__ int32_t operator()(uint32_t q) const {
+        return ((uint32_t)skey[q] & 3u) == kClsPut ? (int32_t)q : -1;
     }
-}
+};
+using SlotIter = rocprim::transform_iterator<const uint64_t*, SlotOf, uint32_t>;
+using PutPosIter =
+    rocprim::transform_iterator<rocprim::counting_iterator<uint32_t>, PutPos, int32_t>;
 
 // per sorted position q: the command's chunk index and a 32-bit result code
 //   bit 31 conf | bits 29-30 kind | bits 0-28 payload
@@ -227,7 +248,6 @@ constexpr uint32_t kPayloadMask = (1u << kKindShift) - 1u;
 constexpr uint32_t kKindZero = 0, kKindOwn = 1, kKindLog = 2, kKindTable = 3;
 
 __global__ __launch_bounds__(256) void k_apply_finish(KvTable t, const uint64_t* __restrict__ skey,
-                                                      const uint32_t* __restrict__ sslot,
                                                       const int32_t* __restrict__ lps, uint64_t n,
                                                       uint32_t* __restrict__ jkey,
                                                       uint32_t* __restrict__ code) {
@@ -236,19 +256,20 @@ __global__ __launch_bounds__(256) void k_apply_finish(KvTable t, const uint64_t*
     const uint32_t ep = t.epoch[0];
     for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
         const uint64_t k = skey[q];
-        const uint32_t sl = sslot[q];
+        const uint32_t sl = sk_slot(k);
         jkey[q] = sk_index(k);
         if (sl == none) {
             code[q] = 0;
             continue;
         }
         const uint32_t c = sk_class(k);
-        const bool in_chunk = q > 0 && sslot[q - 1] == sl;
+        const uint64_t kp = q > 0 ? skey[q - 1] : ~0ull;
+        const bool in_chunk = q > 0 && sk_slot(kp) == sl;
         uint32_t st = 0;
         bool prev, prev_put;
         if (in_chunk) {
             prev = true;
-            prev_put = sk_class(skey[q - 1]) == kClsPut;
+            prev_put = sk_class(kp) == kClsPut;
         } else {
             st = t.state[sl];
             prev = (st >> 2) == ep;
@@ -303,7 +324,6 @@ __global__ __launch_bounds__(256) void k_apply_emit(KvTable t, const uint32_t* _
 // the last command of every slot in the chunk writes the slot's value (if the chunk PUT it) and
 // its state word, after every read of the chunk-start state is done (previous kernels)
 __global__ __launch_bounds__(256) void k_apply_commit(KvTable t, const uint64_t* __restrict__ skey,
-                                                      const uint32_t* __restrict__ sslot,
                                                       const int32_t* __restrict__ lps, uint64_t n,
                                                       const int64_t* __restrict__ val) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -311,9 +331,10 @@ __global__ __launch_bounds__(256) void k_apply_commit(KvTable t, const uint64_t*
     const uint32_t ep = t.epoch[0];
     unsigned long long added = 0;
     for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
-        const uint32_t sl = sslot[q];
+        const uint64_t k = skey[q];
+        const uint32_t sl = sk_slot(k);
         if (sl == none) continue;
-        if (q + 1 < n && sslot[q + 1] == sl) continue;
+        if (q + 1 < n && sk_slot(skey[q + 1]) == sl) continue;
         const int32_t pp = lps[q];
         const uint32_t old = t.state[sl];
         uint32_t present = old & kPresent;
@@ -322,7 +343,7 @@ __global__ __launch_bounds__(256) void k_apply_commit(KvTable t, const uint64_t*
             added += present ? 0 : 1;
             present = kPresent;
         }
-        t.state[sl] = (ep << 2) | (sk_class(skey[q]) == kClsPut ? kLastPut : 0u) | present;
+        t.state[sl] = (ep << 2) | (sk_class(k) == kClsPut ? kLastPut : 0u) | present;
     }
     // one counter atomic per wave
 #pragma unroll
@@ -342,12 +363,14 @@ hipError_t sort_back_pairs(void* tmp, size_t& tb, uint32_t* ki, uint32_t* ko, ui
 }
 
 struct WorkLayout {
-    uint64_t skey_a, skey_b, sslot, lp, lps, jkey, code, jkey_b, code_b, tmp, tmp_bytes, total;
+    uint64_t skey_a, skey_b, lps, jkey, code, jkey_b, code_b, tmp, tmp_bytes, total;
 };
 WorkLayout layout(uint64_t m) {
     size_t sort_tmp = 0, scan_tmp = 0, back_tmp = 0;
     (void)sort_slot_keys(nullptr, sort_tmp, nullptr, nullptr, (size_t)m, 32u, 64u, 0);
-    (void)rocprim::inclusive_scan_by_key(nullptr, scan_tmp, (uint32_t*)nullptr, (int32_t*)nullptr,
+    (void)rocprim::inclusive_scan_by_key(nullptr, scan_tmp, SlotIter(nullptr, SlotOf()),
+                                         PutPosIter(rocprim::counting_iterator<uint32_t>(0),
+                                                    PutPos{nullptr}),
                                          (int32_t*)nullptr, (size_t)m,
                                          rocprim::maximum<int32_t>(),
                                          rocprim::equal_to<uint32_t>());
@@ -360,8 +383,6 @@ WorkLayout layout(uint64_t m) {
     uint64_t o = 0;
     w.skey_a = o; o += al(m * 8);
     w.skey_b = o; o += al(m * 8);
-    w.sslot = o; o += al(m * 4);
-    w.lp = o; o += al(m * 4);
     w.lps = o; o += al(m * 4);
     w.jkey = o; o += al(m * 4);
     w.code = o; o += al(m * 4);
@@ -406,8 +427,6 @@ hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const
     char* b = (char*)w.base;
     uint64_t* skey_a = (uint64_t*)(b + L.skey_a);
     uint64_t* skey_b = (uint64_t*)(b + L.skey_b);
-    uint32_t* sslot = (uint32_t*)(b + L.sslot);
-    int32_t* lp = (int32_t*)(b + L.lp);
     int32_t* lps = (int32_t*)(b + L.lps);
     uint32_t* jkey = (uint32_t*)(b + L.jkey);
     uint32_t* code = (uint32_t*)(b + L.code);
@@ -418,22 +437,31 @@ hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const
 
     k_epoch_bump<<<1, 1, 0, stream>>>(t.epoch);
     k_epoch_wrap<<<1024, 256, 0, stream>>>(t);
-    k_kv_insert_puts<<<grid_for(m), 256, 0, stream>>>(t, op, key, m, err);
+    const bool one = C >= m;  // one chunk: the inserts also write the PUTs' sort keys
+    if (one)
+        k_kv_insert_puts<true><<<grid_for(m), 256, 0, stream>>>(t, op, key, m, err, skey_a);
+    else
+        k_kv_insert_puts<false><<<grid_for(m), 256, 0, stream>>>(t, op, key, m, err, nullptr);
     for (uint64_t c0 = 0; c0 < m; c0 += C) {
         const uint64_t n = m - c0 < C ? m - c0 : C;
         const unsigned g = grid_for(n);
-        k_kv_lookup<<<g, 256, 0, stream>>>(t, op + c0, key + c0, n, skey_a);
+        if (one)
+            k_kv_lookup<true><<<g, 256, 0, stream>>>(t, op + c0, key + c0, n, skey_a);
+        else
+            k_kv_lookup<false><<<g, 256, 0, stream>>>(t, op + c0, key + c0, n, skey_a);
         size_t tmp_bytes = L.tmp_bytes;
         hipError_t r = sort_slot_keys(tmp, tmp_bytes, skey_a, skey_b, (size_t)n, 32u,
                                       32u + slot_bits, stream);
         if (r != hipSuccess) return r;
-        k_apply_mark<<<g, 256, 0, stream>>>(skey_b, n, sslot, lp);
         tmp_bytes = L.tmp_bytes;
-        r = rocprim::inclusive_scan_by_key(tmp, tmp_bytes, sslot, lp, lps, (size_t)n,
+        r = rocprim::inclusive_scan_by_key(tmp, tmp_bytes, SlotIter(skey_b, SlotOf()),
+                                           PutPosIter(rocprim::counting_iterator<uint32_t>(0),
+                                                      PutPos{skey_b}),
+                                           lps, (size_t)n,
                                            rocprim::maximum<int32_t>(),
                                            rocprim::equal_to<uint32_t>(), stream);
         if (r != hipSuccess) return r;
-        k_apply_finish<<<g, 256, 0, stream>>>(t, skey_b, sslot, lps, n, jkey, code);
+        k_apply_finish<<<g, 256, 0, stream>>>(t, skey_b, lps, n, jkey, code);
         tmp_bytes = L.tmp_bytes;
         const unsigned jb = bits_for(n);
         const uint32_t *jk = jkey, *cd = code;  // one emit group: LDS placement alone suffices
@@ -447,7 +475,7 @@ hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const
         const unsigned eg = (unsigned)((n + kEmitGroup - 1) / kEmitGroup);
         k_apply_emit<<<eg, 256, 0, stream>>>(t, jk, cd, n, val + c0, ret + c0,
                                              conf ? conf + c0 : nullptr);
-        k_apply_commit<<<g, 256, 0, stream>>>(t, skey_b, sslot, lps, n, val + c0);
+        k_apply_commit<<<g, 256, 0, stream>>>(t, skey_b, lps, n, val + c0);
     }
     return hipGetLastError();
 }
