@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--instances", type=int, default=1 << 24, help="tally / prepare: instances")
     ap.add_argument("--commands", type=int, default=1 << 26, help="apply: commands")
     ap.add_argument("--apply-keys", type=int, default=1 << 20, help="apply: key space")
+    ap.add_argument("--kv-capacity", type=int, default=0,
+                    help="apply: engine key capacity (0 = 2 x --apply-keys; the table gets >= 2x slots)")
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
     return ap.parse_args()
 
@@ -185,6 +187,10 @@ def main():
         elapsed = float(tt.item())
 
     # ---- outputs of the (identical) timed steps -------------------------------------------------
+    # instances decided by one step: status COMMITTED after it and not before it
+    st_o = d["st_out"].view(torch.int32).view(-1, 4)[:, 0]
+    st_i = d["st_in"].view(torch.int32).view(-1, 4)[:, 0]
+    n_decided = int(((st_o == R.COMMITTED) & (st_i != R.COMMITTED)).sum().item())
     wm = d["wm"].cpu().numpy()
     committed = wm[:G_total]
     executed = wm[G_total:]
@@ -251,7 +257,8 @@ def main():
                 "traffic": traffic, "alg_bytes_per_launch": alg,
                 "kernel_ms_avg": kern_avg_ms, "kernel_ms_min": float(np.min(kern_ms)),
             },
-            "decided_instances_per_step": int(((own_c >= 0).sum())),
+            "decided_instances_per_step": n_decided,
+            "groups_with_commit_watermark": int(((own_c >= 0).sum())),
             "executed_instances_per_step": n_exec_inst,
             "executed_commands_per_step": n_exec_cmds,
             "watermark_allreduce_ok": wm_ok,
@@ -380,7 +387,7 @@ def kernel_bench(a):
     import oracle_lib as OL  # CPU oracle: the checker and the CPU baseline, never the measured path
     N = 5
     mode = R.MODE_MIN if a.mode == "min" else R.MODE_CLASSIC
-    eng = Engine(local, n_replicas=N, mode=mode, kv_capacity=2 * a.apply_keys)
+    eng = Engine(local, n_replicas=N, mode=mode, kv_capacity=a.kv_capacity or 2 * a.apply_keys)
     stream = torch.cuda.ExternalStream(eng.stream, device=dev)
     torch.cuda.set_stream(stream)
 

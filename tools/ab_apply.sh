@@ -9,7 +9,7 @@ rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/apply_ab/pytest.log; [ $rc -eq 0
 for d in ${DISTS:-uniform zipf}; do
   for rep in 1 2; do
     for lib in ${LIBS:-libmpx_old.so libmpx.so}; do
-      r=$(MPX_LIB=$PWD/minpaxos_amd/$lib timeout -k 10 300 python bench.py --workload apply --dist $d --steps 5 --warmup 1 --no-cpu-baseline 2>gpurun_out/apply_ab/err.log | python3 -c "import json,sys; d=json.loads([l for l in sys.stdin if l.startswith('{')][-1]); print('%.3f' % d['ms_per_step'], d['parity'])")
+      r=$(MPX_LIB=$PWD/minpaxos_amd/$lib timeout -k 10 300 python bench.py --workload apply --dist $d --steps 5 --warmup 1 --no-cpu-baseline ${BARGS:-} 2>gpurun_out/apply_ab/err.log | python3 -c "import json,sys; d=json.loads([l for l in sys.stdin if l.startswith('{')][-1]); print('%.3f' % d['ms_per_step'], d['parity'])")
       rc=$?; [ $rc -eq 0 ] || { echo "bench $d $lib rc=$rc"; tail -5 gpurun_out/apply_ab/err.log; exit $rc; }
       echo "$d $lib $r"
     done
