@@ -12,12 +12,13 @@
 // Only keys that are PUT in this call or already present can change any output, so:
 //   0. k_epoch_bump       a new call epoch (device counter, so captured graphs stay correct)
 //   1. k_kv_insert_puts   insert every PUT key of the whole call (one 64-bit CAS per probe; the
-//                         key INT64_MIN is kept in a side slot so the table needs no key state);
-//                         in a one-chunk call a PUT also writes its sort key (2) from the slot
-//                         the insert returned, so step 2 probes the non-PUT commands only
+//                         key INT64_MIN is kept in a side slot so the table needs no key state)
 // then the log is cut into chunks of C commands, processed in order; per chunk:
 //   2. k_kv_lookup        sort key (slot << 32 | j << 2 | op class) of every command j of the
 //                         chunk (absent, never-PUT keys: ret 0, conf 0 now, sorted last)
+//   1+2 in a one-chunk call (the default): k_kv_index writes every sort key in one pass (PUTs
+//                         insert, the other commands probe concurrently), k_kv_reprobe redoes the
+//                         probes that missed once every insert is done
 //   3. radix sort on the slot bits - stable, so log order within a slot; the op class rides in
 //                         the key's low bits
 //   4-5. segmented inclusive max-scan by slot of (q if PUT else -1) -> last PUT at or before q
@@ -104,8 +105,10 @@ __global__ void k_kv_fill(KvTable t) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *t.n_present = 0;
 }
 
-// epoch[0] = current call epoch, epoch[1] = wrap flag (the next kernel clears every slot's tag)
-__global__ void k_epoch_bump(uint32_t* epoch) {
+// epoch[0] = current call epoch, epoch[1] = wrap flag (the next kernel clears every slot's tag);
+// also zeroes the call's miss counter (k_kv_index)
+__global__ void k_epoch_bump(uint32_t* epoch, uint32_t* n_miss) {
+    *n_miss = 0;
     uint32_t e = epoch[0] + 1;
     epoch[1] = 0;
     if (e >= kEpochMax) {
@@ -176,39 +179,97 @@ hipError_t launch_kv_export(KvTable& t, int64_t* keys, int64_t* vals, uint64_t c
 }
 
 // ---- the apply pipeline -------------------------------------------------------------------
-// kKeys (single-chunk calls): the insert's slot is the PUT's sort key slot, so the PUT also
-// writes its sort key here and the lookup pass probes only the other commands
-template <bool kKeys>
+// multi-chunk calls: insert every PUT key of the whole call before any chunk is looked up
 __global__ __launch_bounds__(256) void k_kv_insert_puts(KvTable t, const uint8_t* __restrict__ op,
                                                         const int64_t* __restrict__ key,
-                                                        uint64_t m, uint32_t* err,
-                                                        uint64_t* __restrict__ skey) {
+                                                        uint64_t m, uint32_t* err) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride)
-        if (op[i] == MPX_OP_PUT) {
-            const int64_t s = kv_insert(t, key[i], err);
-            if (kKeys) {
-                const uint64_t sl = s < 0 ? t.cap + 1 : (uint64_t)s;  // full table: call fails
-                skey[i] = (sl << 32) | (i << 2) | kClsPut;
-            }
-        }
+        if (op[i] == MPX_OP_PUT) kv_insert(t, key[i], err);
 }
 
 __device__ __forceinline__ uint32_t op_class(uint8_t o) {
     return o == MPX_OP_PUT ? kClsPut : (o == MPX_OP_GET ? kClsGet : kClsOther);
 }
 
+// probe while other lanes insert: relaxed loads. A slot's key changes at most once per call
+// (empty -> key), so a hit is final; a miss may be an insert this probe did not see yet and is
+// re-probed by k_kv_reprobe after the pass
+__device__ __forceinline__ int64_t kv_probe_racy(const KvTable& t, int64_t key) {
+    if (key == kSentinel) return (int64_t)t.cap;
+    const uint64_t mask = t.cap - 1;
+    uint64_t s = hash64((uint64_t)key) & mask;
+    for (uint64_t probe = 0; probe < t.cap; ++probe, s = (s + 1) & mask) {
+        const int64_t cur = (int64_t)__hip_atomic_load(
+            reinterpret_cast<unsigned long long*>(t.keys + s), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == key) return (int64_t)s;
+        if (cur == kSentinel) return -1;
+    }
+    return -1;
+}
+
+// one-chunk calls: the sort key of every command in one pass, so every lane probes (the split
+// insert / lookup passes left half the lanes of each wave idle). PUTs insert; the others probe
+// concurrently and append a miss to `miss` (one counter atomic per wave)
+__global__ __launch_bounds__(256) void k_kv_index(KvTable t, const uint8_t* __restrict__ op,
+                                                  const int64_t* __restrict__ key, uint64_t m,
+                                                  uint32_t* err, uint64_t* __restrict__ skey,
+                                                  uint32_t* __restrict__ miss,
+                                                  uint32_t* __restrict__ n_miss) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < m; i0 += stride) {
+        const uint64_t i = i0 + threadIdx.x;
+        bool missed = false;
+        if (i < m) {
+            const uint8_t o = op[i];
+            const int64_t k = key[i];
+            int64_t s;
+            if (o == MPX_OP_PUT) {
+                s = kv_insert(t, k, err);
+                if (s < 0) s = (int64_t)t.cap + 1;  // full table: the call fails
+            } else {
+                s = kv_probe_racy(t, k);
+                missed = s < 0;
+            }
+            if (!missed) skey[i] = ((uint64_t)s << 32) | (i << 2) | op_class(o);
+        }
+        const uint64_t bal = __ballot(missed);
+        if (bal) {
+            uint32_t base = 0;
+            if (lane_id() == 0) base = atomicAdd(n_miss, (uint32_t)__popcll(bal));
+            base = __shfl(base, 0);
+            if (missed) miss[base + __popcll(bal & ((1ull << lane_id()) - 1))] = (uint32_t)i;
+        }
+    }
+}
+
+// after every insert of the call: the missed probes again (an absent key that no PUT of the
+// call inserted gets slot cap+1: its outputs are zero)
+__global__ __launch_bounds__(256) void k_kv_reprobe(KvTable t, const uint8_t* __restrict__ op,
+                                                    const int64_t* __restrict__ key,
+                                                    const uint32_t* __restrict__ miss,
+                                                    const uint32_t* __restrict__ n_miss,
+                                                    uint64_t* __restrict__ skey) {
+    const uint32_t n = *n_miss;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += stride) {
+        const uint64_t j = miss[x];
+        const int64_t s = kv_lookup(t, key[j]);
+        const uint64_t sl = s < 0 ? t.cap + 1 : (uint64_t)s;
+        skey[j] = (sl << 32) | (j << 2) | op_class(op[j]);
+    }
+}
+
 // sort key of chunk command j: slot << 32 | j << 2 | class; an absent key that is never PUT in
 // this call gets slot cap+1 (sorts last; its outputs are zero: GET -> NIL, and no conflict since
 // nothing before or after it on that key in this call is a PUT)
-template <bool kSkipPut>
 __global__ __launch_bounds__(256) void k_kv_lookup(KvTable t, const uint8_t* __restrict__ op,
                                                    const int64_t* __restrict__ key, uint64_t n,
                                                    uint64_t* __restrict__ skey) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
         const uint8_t o = op[j];
-        if (kSkipPut && o == MPX_OP_PUT) continue;
         const int64_t s = kv_lookup(t, key[j]);
         const uint64_t sl = s < 0 ? t.cap + 1 : (uint64_t)s;
         skey[j] = (sl << 32) | (j << 2) | op_class(o);
@@ -308,16 +369,31 @@ __global__ __launch_bounds__(256) void k_apply_emit(KvTable t, const uint32_t* _
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x)
         lc[jkey[g0 + i] & (kEmitGroup - 1)] = code[g0 + i];
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-        const uint64_t j = g0 + i;
-        const uint32_t x = lc[i];
-        const uint32_t kind = (x >> kKindShift) & 3u, p = x & kPayloadMask;
-        int64_t r = 0;
-        if (kind == kKindOwn) r = val[j];
-        else if (kind == kKindLog) r = val[p];
-        else if (kind == kKindTable) r = t.vals[p];
-        ret[j] = r;
-        if (conf) conf[j] = (uint8_t)(x >> 31);
+    // kEmitUnroll commands per lane per round: their (random) value gathers are all issued
+    // before the first store, so each lane keeps several loads in flight
+    constexpr int kEmitUnroll = 4;
+    for (uint32_t i0 = threadIdx.x; i0 < cnt; i0 += kEmitUnroll * blockDim.x) {
+        uint32_t x[kEmitUnroll];
+        int64_t r[kEmitUnroll];
+#pragma unroll
+        for (int u = 0; u < kEmitUnroll; ++u) {
+            const uint32_t i = i0 + u * blockDim.x;
+            x[u] = i < cnt ? lc[i] : 0u;
+            const uint32_t kind = (x[u] >> kKindShift) & 3u, p = x[u] & kPayloadMask;
+            const int64_t* src = kind == kKindOwn ? val + g0 + i
+                                 : kind == kKindLog ? val + p
+                                 : kind == kKindTable ? t.vals + p
+                                 : nullptr;
+            r[u] = src ? *src : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kEmitUnroll; ++u) {
+            const uint32_t i = i0 + u * blockDim.x;
+            if (i < cnt) {
+                ret[g0 + i] = r[u];
+                if (conf) conf[g0 + i] = (uint8_t)(x[u] >> 31);
+            }
+        }
     }
 }
 
@@ -363,7 +439,7 @@ hipError_t sort_back_pairs(void* tmp, size_t& tb, uint32_t* ki, uint32_t* ko, ui
 }
 
 struct WorkLayout {
-    uint64_t skey_a, skey_b, lps, jkey, code, jkey_b, code_b, tmp, tmp_bytes, total;
+    uint64_t skey_a, skey_b, lps, jkey, code, jkey_b, code_b, n_miss, tmp, tmp_bytes, total;
 };
 WorkLayout layout(uint64_t m) {
     size_t sort_tmp = 0, scan_tmp = 0, back_tmp = 0;
@@ -388,6 +464,7 @@ WorkLayout layout(uint64_t m) {
     w.code = o; o += al(m * 4);
     w.jkey_b = o; o += al(m * 4);
     w.code_b = o; o += al(m * 4);
+    w.n_miss = o; o += al(4);
     w.tmp_bytes = al(t);
     w.tmp = o; o += w.tmp_bytes;
     w.total = o;
@@ -435,20 +512,25 @@ hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const
     void* tmp = b + L.tmp;
     const unsigned slot_bits = bits_for(t.cap + 2);
 
-    k_epoch_bump<<<1, 1, 0, stream>>>(t.epoch);
+    uint32_t* n_miss = (uint32_t*)(b + L.n_miss);
+    k_epoch_bump<<<1, 1, 0, stream>>>(t.epoch, n_miss);
     k_epoch_wrap<<<1024, 256, 0, stream>>>(t);
-    const bool one = C >= m;  // one chunk: the inserts also write the PUTs' sort keys
-    if (one)
-        k_kv_insert_puts<true><<<grid_for(m), 256, 0, stream>>>(t, op, key, m, err, skey_a);
-    else
-        k_kv_insert_puts<false><<<grid_for(m), 256, 0, stream>>>(t, op, key, m, err, nullptr);
+    // one chunk: one pass writes every sort key (PUTs insert, the rest probe; misses re-probed
+    // after the pass, through lps as the miss list - lps is not live until the scan)
+    const bool one = C >= m;
+    if (one) {
+        k_kv_index<<<grid_for(m), 256, 0, stream>>>(t, op, key, m, err, skey_a, (uint32_t*)lps,
+                                                    n_miss);
+        k_kv_reprobe<<<grid_for(m), 256, 0, stream>>>(t, op, key, (const uint32_t*)lps, n_miss,
+                                                      skey_a);
+    } else {
+        k_kv_insert_puts<<<grid_for(m), 256, 0, stream>>>(t, op, key, m, err);
+    }
     for (uint64_t c0 = 0; c0 < m; c0 += C) {
         const uint64_t n = m - c0 < C ? m - c0 : C;
         const unsigned g = grid_for(n);
-        if (one)
-            k_kv_lookup<true><<<g, 256, 0, stream>>>(t, op + c0, key + c0, n, skey_a);
-        else
-            k_kv_lookup<false><<<g, 256, 0, stream>>>(t, op + c0, key + c0, n, skey_a);
+        if (!one)
+            k_kv_lookup<<<g, 256, 0, stream>>>(t, op + c0, key + c0, n, skey_a);
         size_t tmp_bytes = L.tmp_bytes;
         hipError_t r = sort_slot_keys(tmp, tmp_bytes, skey_a, skey_b, (size_t)n, 32u,
                                       32u + slot_bits, stream);
