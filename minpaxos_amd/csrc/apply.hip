@@ -192,54 +192,101 @@ __device__ __forceinline__ uint32_t op_class(uint8_t o) {
     return o == MPX_OP_PUT ? kClsPut : (o == MPX_OP_GET ? kClsGet : kClsOther);
 }
 
-// probe while other lanes insert: relaxed loads. A slot's key changes at most once per call
-// (empty -> key), so a hit is final; a miss may be an insert this probe did not see yet and is
-// re-probed by k_kv_reprobe after the pass
-__device__ __forceinline__ int64_t kv_probe_racy(const KvTable& t, int64_t key) {
-    if (key == kSentinel) return (int64_t)t.cap;
+// probes while other lanes insert use relaxed loads. A slot's key changes at most once per call
+// (empty -> key), so a hit is final; a miss may be an insert the probe did not see yet and is
+// re-probed by k_kv_reprobe after the pass.
+// the two probe loops resumed at slot s whose key `cur` was already loaded (k_kv_index issues
+// the first probe of several commands together)
+__device__ __forceinline__ int64_t kv_insert_from(const KvTable& t, int64_t key, uint64_t s,
+                                                  unsigned long long cur, uint32_t* err) {
     const uint64_t mask = t.cap - 1;
-    uint64_t s = hash64((uint64_t)key) & mask;
-    for (uint64_t probe = 0; probe < t.cap; ++probe, s = (s + 1) & mask) {
-        const int64_t cur = (int64_t)__hip_atomic_load(
-            reinterpret_cast<unsigned long long*>(t.keys + s), __ATOMIC_RELAXED,
-            __HIP_MEMORY_SCOPE_AGENT);
-        if (cur == key) return (int64_t)s;
-        if (cur == kSentinel) return -1;
+    for (uint64_t probe = 0; probe < t.cap; ++probe) {
+        unsigned long long* slot = reinterpret_cast<unsigned long long*>(t.keys + s);
+        if (probe) cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == (unsigned long long)kSentinel) {
+            cur = atomicCAS(slot, (unsigned long long)kSentinel, (unsigned long long)key);
+            if (cur == (unsigned long long)kSentinel) return (int64_t)s;  // claimed
+        }
+        if ((int64_t)cur == key) return (int64_t)s;
+        s = (s + 1) & mask;
+    }
+    raise_err(err, kErrKvFull);
+    return -1;
+}
+
+__device__ __forceinline__ int64_t kv_probe_racy_from(const KvTable& t, int64_t key, uint64_t s,
+                                                      unsigned long long cur) {
+    const uint64_t mask = t.cap - 1;
+    for (uint64_t probe = 0; probe < t.cap; ++probe) {
+        if (probe)
+            cur = __hip_atomic_load(reinterpret_cast<unsigned long long*>(t.keys + s),
+                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((int64_t)cur == key) return (int64_t)s;
+        if ((int64_t)cur == kSentinel) return -1;
+        s = (s + 1) & mask;
     }
     return -1;
 }
 
 // one-chunk calls: the sort key of every command in one pass, so every lane probes (the split
 // insert / lookup passes left half the lanes of each wave idle). PUTs insert; the others probe
-// concurrently and append a miss to `miss` (one counter atomic per wave)
+// concurrently and append a miss to `miss` (one counter atomic per wave). Each lane takes
+// kIndexUnroll commands per round and issues their first probes together.
+#ifndef MPX_INDEX_UNROLL
+#define MPX_INDEX_UNROLL 2
+#endif
+constexpr int kIndexUnroll = MPX_INDEX_UNROLL;
 __global__ __launch_bounds__(256) void k_kv_index(KvTable t, const uint8_t* __restrict__ op,
                                                   const int64_t* __restrict__ key, uint64_t m,
                                                   uint32_t* err, uint64_t* __restrict__ skey,
                                                   uint32_t* __restrict__ miss,
                                                   uint32_t* __restrict__ n_miss) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < m; i0 += stride) {
-        const uint64_t i = i0 + threadIdx.x;
-        bool missed = false;
-        if (i < m) {
-            const uint8_t o = op[i];
-            const int64_t k = key[i];
-            int64_t s;
-            if (o == MPX_OP_PUT) {
-                s = kv_insert(t, k, err);
-                if (s < 0) s = (int64_t)t.cap + 1;  // full table: the call fails
-            } else {
-                s = kv_probe_racy(t, k);
-                missed = s < 0;
-            }
-            if (!missed) skey[i] = ((uint64_t)s << 32) | (i << 2) | op_class(o);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * kIndexUnroll;
+    const uint64_t mask = t.cap - 1;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x * kIndexUnroll; i0 < m; i0 += stride) {
+        uint8_t o[kIndexUnroll];
+        int64_t k[kIndexUnroll];
+        uint64_t h[kIndexUnroll];
+        unsigned long long cur[kIndexUnroll];
+#pragma unroll
+        for (int u = 0; u < kIndexUnroll; ++u) {
+            const uint64_t i = i0 + (uint64_t)u * blockDim.x + threadIdx.x;
+            o[u] = i < m ? op[i] : 0;
+            k[u] = i < m ? key[i] : 0;
         }
-        const uint64_t bal = __ballot(missed);
-        if (bal) {
-            uint32_t base = 0;
-            if (lane_id() == 0) base = atomicAdd(n_miss, (uint32_t)__popcll(bal));
-            base = __shfl(base, 0);
-            if (missed) miss[base + __popcll(bal & ((1ull << lane_id()) - 1))] = (uint32_t)i;
+#pragma unroll
+        for (int u = 0; u < kIndexUnroll; ++u) {
+            const uint64_t i = i0 + (uint64_t)u * blockDim.x + threadIdx.x;
+            h[u] = hash64((uint64_t)k[u]) & mask;
+            cur[u] = i < m && k[u] != kSentinel
+                         ? __hip_atomic_load(reinterpret_cast<unsigned long long*>(t.keys + h[u]),
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                         : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < kIndexUnroll; ++u) {
+            const uint64_t i = i0 + (uint64_t)u * blockDim.x + threadIdx.x;
+            bool missed = false;
+            if (i < m) {
+                int64_t s;
+                if (k[u] == kSentinel) {
+                    s = (int64_t)t.cap;  // side slot
+                } else if (o[u] == MPX_OP_PUT) {
+                    s = kv_insert_from(t, k[u], h[u], cur[u], err);
+                    if (s < 0) s = (int64_t)t.cap + 1;  // full table: the call fails
+                } else {
+                    s = kv_probe_racy_from(t, k[u], h[u], cur[u]);
+                    missed = s < 0;
+                }
+                if (!missed) skey[i] = ((uint64_t)s << 32) | (i << 2) | op_class(o[u]);
+            }
+            const uint64_t bal = __ballot(missed);
+            if (bal) {
+                uint32_t base = 0;
+                if (lane_id() == 0) base = atomicAdd(n_miss, (uint32_t)__popcll(bal));
+                base = __shfl(base, 0);
+                if (missed) miss[base + __popcll(bal & ((1ull << lane_id()) - 1))] = (uint32_t)i;
+            }
         }
     }
 }
@@ -308,47 +355,60 @@ constexpr uint32_t kKindShift = 29;
 constexpr uint32_t kPayloadMask = (1u << kKindShift) - 1u;
 constexpr uint32_t kKindZero = 0, kKindOwn = 1, kKindLog = 2, kKindTable = 3;
 
+// kUnroll positions per lane per round, loads of a round issued together (memory-level
+// parallelism: each round's loads are one dependent chain per lane otherwise)
+constexpr int kUnroll = 4;
+
 __global__ __launch_bounds__(256) void k_apply_finish(KvTable t, const uint64_t* __restrict__ skey,
                                                       const int32_t* __restrict__ lps, uint64_t n,
                                                       uint32_t* __restrict__ jkey,
                                                       uint32_t* __restrict__ code) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * kUnroll;
     const uint32_t none = (uint32_t)(t.cap + 1);
     const uint32_t ep = t.epoch[0];
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
-        const uint64_t k = skey[q];
-        const uint32_t sl = sk_slot(k);
-        jkey[q] = sk_index(k);
-        if (sl == none) {
-            code[q] = 0;
-            continue;
+    for (uint64_t q0 = (uint64_t)blockIdx.x * blockDim.x * kUnroll + threadIdx.x; q0 < n;
+         q0 += stride) {
+        uint64_t k[kUnroll], kp[kUnroll], kq[kUnroll];
+        int32_t pp[kUnroll];
+        uint32_t st[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {  // round 1: the sorted neighbours
+            const uint64_t q = q0 + (uint64_t)u * blockDim.x;
+            const bool in = q < n;
+            k[u] = in ? skey[q] : ~0ull;
+            kp[u] = in && q > 0 ? skey[q - 1] : ~0ull;
+            pp[u] = in && q > 0 ? lps[q - 1] : -1;
         }
-        const uint32_t c = sk_class(k);
-        const uint64_t kp = q > 0 ? skey[q - 1] : ~0ull;
-        const bool in_chunk = q > 0 && sk_slot(kp) == sl;
-        uint32_t st = 0;
-        bool prev, prev_put;
-        if (in_chunk) {
-            prev = true;
-            prev_put = sk_class(kp) == kClsPut;
-        } else {
-            st = t.state[sl];
-            prev = (st >> 2) == ep;
-            prev_put = prev && (st & kLastPut);
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {  // round 2: slot state word, last PUT's key
+            const uint32_t sl = sk_slot(k[u]);
+            const bool live = k[u] != ~0ull && sl != none;
+            const bool in_chunk = live && sk_slot(kp[u]) == sl;
+            if (!in_chunk) pp[u] = -1;  // last PUT strictly before q, within the slot's run
+            const bool get = sk_class(k[u]) == kClsGet;
+            st[u] = live && (!in_chunk || (get && pp[u] < 0)) ? t.state[sl] : 0u;
+            kq[u] = live && get && pp[u] >= 0 ? skey[pp[u]] : 0ull;
         }
-        uint32_t x = kKindZero << kKindShift;
-        if (c == kClsPut) {
-            x = kKindOwn << kKindShift;
-        } else if (c == kClsGet) {
-            const int32_t pp = in_chunk ? lps[q - 1] : -1;  // last PUT strictly before q
-            if (pp >= 0) {
-                x = (kKindLog << kKindShift) | sk_index(skey[pp]);
-            } else {
-                if (in_chunk) st = t.state[sl];
-                if (st & kPresent) x = (kKindTable << kKindShift) | sl;
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const uint64_t q = q0 + (uint64_t)u * blockDim.x;
+            if (q >= n) continue;
+            const uint32_t sl = sk_slot(k[u]);
+            jkey[q] = sk_index(k[u]);
+            if (sl == none) {
+                code[q] = 0;
+                continue;
             }
+            const uint32_t c = sk_class(k[u]);
+            const bool in_chunk = q > 0 && sk_slot(kp[u]) == sl;
+            const bool prev = in_chunk || (st[u] >> 2) == ep;
+            const bool prev_put = in_chunk ? sk_class(kp[u]) == kClsPut : prev && (st[u] & kLastPut);
+            uint32_t x = kKindZero << kKindShift;
+            if (c == kClsPut) x = kKindOwn << kKindShift;
+            else if (c == kClsGet && pp[u] >= 0) x = (kKindLog << kKindShift) | sk_index(kq[u]);
+            else if (c == kClsGet && (st[u] & kPresent)) x = (kKindTable << kKindShift) | sl;
+            code[q] = x | (prev && (prev_put || c == kClsPut) ? kCodeConf : 0u);
         }
-        code[q] = x | (prev && (prev_put || c == kClsPut) ? kCodeConf : 0u);
     }
 }
 
@@ -402,24 +462,41 @@ __global__ __launch_bounds__(256) void k_apply_emit(KvTable t, const uint32_t* _
 __global__ __launch_bounds__(256) void k_apply_commit(KvTable t, const uint64_t* __restrict__ skey,
                                                       const int32_t* __restrict__ lps, uint64_t n,
                                                       const int64_t* __restrict__ val) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * kUnroll;
     const uint32_t none = (uint32_t)(t.cap + 1);
     const uint32_t ep = t.epoch[0];
     unsigned long long added = 0;
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
-        const uint64_t k = skey[q];
-        const uint32_t sl = sk_slot(k);
-        if (sl == none) continue;
-        if (q + 1 < n && sk_slot(skey[q + 1]) == sl) continue;
-        const int32_t pp = lps[q];
-        const uint32_t old = t.state[sl];
-        uint32_t present = old & kPresent;
-        if (pp >= 0) {
-            t.vals[sl] = val[sk_index(skey[pp])];
-            added += present ? 0 : 1;
-            present = kPresent;
+    for (uint64_t q0 = (uint64_t)blockIdx.x * blockDim.x * kUnroll + threadIdx.x; q0 < n;
+         q0 += stride) {
+        uint64_t k[kUnroll], kq[kUnroll];
+        int32_t pp[kUnroll];
+        bool last[kUnroll];
+        uint32_t old[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {  // round 1: is q its slot's last command?
+            const uint64_t q = q0 + (uint64_t)u * blockDim.x;
+            k[u] = q < n ? skey[q] : 0ull;
+            const uint64_t kn = q + 1 < n ? skey[q + 1] : ~0ull;
+            last[u] = q < n && sk_slot(k[u]) != none && sk_slot(kn) != sk_slot(k[u]);
+            pp[u] = last[u] ? lps[q] : -1;
         }
-        t.state[sl] = (ep << 2) | (sk_class(k) == kClsPut ? kLastPut : 0u) | present;
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {  // round 2: old state, last PUT's key
+            old[u] = last[u] ? t.state[sk_slot(k[u])] : 0u;
+            kq[u] = pp[u] >= 0 ? skey[pp[u]] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            if (!last[u]) continue;
+            const uint32_t sl = sk_slot(k[u]);
+            uint32_t present = old[u] & kPresent;
+            if (pp[u] >= 0) {
+                t.vals[sl] = val[sk_index(kq[u])];
+                added += present ? 0 : 1;
+                present = kPresent;
+            }
+            t.state[sl] = (ep << 2) | (sk_class(k[u]) == kClsPut ? kLastPut : 0u) | present;
+        }
     }
     // one counter atomic per wave
 #pragma unroll
