@@ -2,7 +2,7 @@
 
 usage: python tools/collect_configs.py gpurun_out/profcfg_<tag> profiles/r01/configs
 Per workload it keeps the bench JSON line (<name>_bench.json) and the rocprofv3 kernel stats
-(<name>_kernel_stats.csv); the table rows come from the bench lines.
+(<name>_kernel_stats.csv); the table has a row per bench line kept in the destination.
 """
 import json
 import os
@@ -20,12 +20,16 @@ def main(src: str, dst: str) -> None:
         lines = [ln for ln in open(log) if ln.startswith("{")]
         if not lines:
             continue
-        d = json.loads(lines[-1])
         with open(os.path.join(dst, name + "_bench.json"), "w") as f:
             f.write(lines[-1] if lines[-1].endswith("\n") else lines[-1] + "\n")
         stats = os.path.join(src, name, name + "_kernel_stats.csv")
         if os.path.exists(stats):
             shutil.copy(stats, os.path.join(dst, name + "_kernel_stats.csv"))
+    for f in sorted(os.listdir(dst)):  # the table covers every row kept in dst
+        if not f.endswith("_bench.json"):
+            continue
+        name = f[:-len("_bench.json")]
+        d = json.loads(open(os.path.join(dst, f)).read())
         rf, cb = d.get("roofline") or {}, d.get("cpu_baseline") or {}
         par = d.get("parity", {})
         rows.append("| %s | %s | %.3g %s | %.3f | %.0f | %.3f | %.3g (%s core) | %s |" % (
