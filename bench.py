@@ -312,7 +312,11 @@ def cpu_baseline(b, a, mode, N, K):
     lib = OL.load()
     ipg = a.ipg
 
+    built = {}  # g_n -> (arrays kept alive, batch struct): inputs are never written
+
     def run(g_n, threads):
+        if g_n in built:
+            return lib.orc_bench_group_step(N, mode, C.byref(built[g_n][1]), K, threads) * 1e-9
         sub, _ = _oracle_sub(b, 0, g_n, ipg)
         o = OL.Oracle(N, mode, kv_per_group=K)
         warm = o.group_step(sub)  # steady-state tables, as on the GPU
@@ -325,6 +329,7 @@ def cpu_baseline(b, a, mode, N, K):
                 warm["kv_key"].copy(), warm["kv_val"].copy(), None]
         arrs = [np.ascontiguousarray(x) if isinstance(x, np.ndarray) else x for x in arrs]
         gb = OL.group_batch_struct(arrs)
+        built[g_n] = (arrs, gb)
         ns = lib.orc_bench_group_step(N, mode, C.byref(gb), K, threads)
         return ns * 1e-9
 
@@ -338,11 +343,24 @@ def cpu_baseline(b, a, mode, N, K):
     while secs < 10.0 and reps < 50:  # about 10 s of CPU work in total
         secs += run(g_n, 1)
         reps += 1
-    return {"value": g_n * ipg * reps / secs, "unit": "instances/s", "cores": 1, "kind": "port",
-            "sample": f"first {g_n} groups of the same workload ({g_n * ipg} instances, "
-                      f"{g_n * ipg * (N - 1)} replies, {g_n * ipg * a.cmds} commands) x {reps} "
-                      f"reps, pointer-per-instance log + hash-map State, one thread, "
-                      f"{secs:.1f} s timed"}
+    out = {"value": g_n * ipg * reps / secs, "unit": "instances/s", "cores": 1, "kind": "port",
+           "sample": f"first {g_n} groups of the same workload ({g_n * ipg} instances, "
+                     f"{g_n * ipg * (N - 1)} replies, {g_n * ipg * a.cmds} commands) x {reps} "
+                     f"reps, pointer-per-instance log + hash-map State, one thread, "
+                     f"{secs:.1f} s timed"}
+    # the same loop with the groups sharded over host threads (one per core, at
+    # most the box's CPU share of 16), reported beside the one-core reference-faithful figure
+    th = max(1, min(16, os.cpu_count() or 1))
+    if th > 1:
+        g_s = min(a.groups, g_n * th)
+        ssecs, sreps = 0.0, 0
+        while ssecs < 4.0 and sreps < 5:  # each rep also rebuilds the per-group maps (untimed)
+            ssecs += run(g_s, th)
+            sreps += 1
+        out["sharded"] = {"value": g_s * ipg * sreps / ssecs, "unit": "instances/s",
+                          "cores": th, "sample": f"first {g_s} groups x {sreps} reps, groups "
+                                                 f"block-sharded over {th} threads"}
+    return out
 
 
 # ============================ single-kernel configurations (2, 3, 4) ============================
