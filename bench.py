@@ -63,7 +63,7 @@ def parse():
                     help="groups timed on the CPU baseline (0 = auto, ~10-30 s of CPU work)")
     ap.add_argument("--parity-groups", type=int, default=512)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--workload", default="step", choices=["step", "tally", "prepare", "apply", "decode", "fanout", "log"])
+    ap.add_argument("--workload", default="step", choices=["step", "tally", "prepare", "apply", "decode", "fanout", "log", "replay"])
     ap.add_argument("--log-format", default="catchup", choices=["catchup", "durable"])
     ap.add_argument("--clients", type=int, default=1024, help="fanout: client connections")
     ap.add_argument("--instances", type=int, default=1 << 24, help="tally / prepare: instances")
@@ -608,6 +608,55 @@ def kernel_bench(a):
                "sample": f"the full run ({I} instances, {M} commands, {total} bytes) x {reps}, "
                          f"one Marshal per instance and command, one thread, {secs:.1f} s timed"}
         workload = f"log ({a.log_format}): {I} committed instances x 4 commands, {total} bytes"
+    elif a.workload == "replay":
+        I = a.instances
+        recs, coff, op, key, val = synth.log_records(I, 1, seed=59)
+        recs = recs.copy()
+        recs["inst_no"] = np.random.default_rng(60).permutation(I).astype(np.int32)
+        o = OL.Oracle(N, mode)
+        log, _ = o.encode_log(R.LOG_DURABLE, recs, coff, op, key, val)
+        L = len(log)
+        d_log = dt(log)
+        d_recs = torch.empty(I * 16, dtype=torch.uint8, device=dev)
+        d_op = torch.empty(I, dtype=torch.uint8, device=dev)
+        d_key = torch.empty(I, dtype=torch.int64, device=dev)
+        d_val = torch.empty(I, dtype=torch.int64, device=dev)
+        d_last = torch.full((I,), -1, dtype=torch.int32, device=dev)
+        d_sc = torch.tensor([0, -1], dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        t_gen = time.time() - t_gen
+        # every output is idempotent under repetition (slots and watermarks are maxima)
+        wall, ms = _timed(stream, eng, a.steps, a.warmup,
+                          lambda: eng.replay_durable_dev(d_log.data_ptr(), L, I, d_recs.data_ptr(),
+                                                         d_op.data_ptr(), d_key.data_ptr(),
+                                                         d_val.data_ptr(), d_last.data_ptr(),
+                                                         d_sc.data_ptr(), eng.stream))
+        w = o.replay_durable(log, I)
+        # log read once; records, op, key, val written once; one 4-byte slot per record
+        alg = L + I * (16 + 1 + 8 + 8) + I * 4
+        units, unit = I, "records/s"
+        kernel = "k_replay_durable"
+        bit_exact = bool(np.array_equal(d_recs.cpu().numpy().view(R.LOG_REC), w[0])
+                         and np.array_equal(d_op.cpu().numpy(), w[1])
+                         and np.array_equal(d_key.cpu().numpy(), w[2])
+                         and np.array_equal(d_val.cpu().numpy(), w[3])
+                         and np.array_equal(d_last.cpu().numpy(), w[4])
+                         and d_sc.cpu().tolist() == [w[5], w[6]])
+        parity = {"records_checked": I, "bytes": L, "bit_exact": bit_exact}
+        lib = OL.load()
+        c = [np.zeros(I, R.LOG_REC), np.zeros(I, np.uint8), np.zeros(I, np.int64),
+             np.zeros(I, np.int64), np.zeros(I, np.int32), np.zeros(2, np.int32)]
+        secs, reps = 0.0, 0
+        while secs < 10.0 and reps < 20:
+            c[5][:] = (0, -1)
+            t0 = time.perf_counter()
+            lib.orc_replay_durable(log.ctypes.data, L, I, *[x.ctypes.data for x in c])
+            secs += time.perf_counter() - t0
+            reps += 1
+        cpu = {"value": I * reps / secs, "unit": unit, "cores": 1, "kind": "port",
+               "sample": f"the full log ({I} records, {L} bytes) x {reps} through the oracle's "
+                         f"getDataFromStableStore loop, one thread, {secs:.1f} s timed"}
+        workload = f"replay (durable): {I} records x 1 command, {L} bytes, instNo a permutation"
     else:  # decode
         I = a.instances
         recs, _ = synth.accept_replies(I, N, 0.7, seed=42)

@@ -32,6 +32,8 @@
  *   mpx_encode_log        <- minpaxosproto.(*Instance).Marshal (minpaxosprotomarsh.go:100-124) for
  *                            the CatchUpLog of bcastAccept (bareminpaxos.go:488-513), and
  *                            recordInstanceMetadata + recordCommands (bareminpaxos.go:164-188)
+ *   mpx_replay_durable    <- getDataFromStableStore (bareminpaxos.go:122-161): the durable log
+ *                            read back into records, watermarks and the instance slots
  *
  * Contract (every entry point):
  *   - plain C, no exceptions cross the boundary, never aborts; return 0 (MPX_OK) or a negative
@@ -430,6 +432,29 @@ int mpx_encode_log_dev(mpx_engine* eng, int format, const mpx_log_rec* d_recs, s
                        const uint64_t* d_cmd_off, const uint8_t* d_op, const int64_t* d_key,
                        const int64_t* d_val, size_t m, uint8_t* d_out, uint64_t* d_rec_off,
                        void* stream);
+
+/* ---- durable-log replay (read side) ----------------------------------
+ * bareminpaxos.(*Replica).getDataFromStableStore  src/bareminpaxos/bareminpaxos.go:122-161:
+ * the stable store as back-to-back MPX_DURABLE_REC_BYTES records (metadata Ballot, Status,
+ * instNo as LE u32, then exactly ONE state.Command: Op u8, K i64, V i64). Per record, as the
+ * sequential loop leaves it:
+ *   recs[i] / op[i] / key[i] / val[i]  the decoded record (recs[i].pad = 0)
+ *   scalars[0] (in/out) defaultBallot  = max(defaultBallot, every ballot)          (:145-147)
+ *   scalars[1] (in/out) committedUpTo  = max(committedUpTo, instNo of COMMITTED)    (:149-151)
+ *   last_rec[instNo]  = index of the LAST record naming instNo (-1: none)            (:153-157)
+ * len must be a whole number of records (a trailing partial record, which the reference decodes
+ * as a zero-padded garbage instance, is rejected with MPX_E_INVAL) and len / 29 < 2^31.
+ * instNo outside [0, inst_cap) is where the reference's instanceSpace index panics:
+ * MPX_E_NIL_INSTANCE, outputs unspecified.                                                   */
+#define MPX_DURABLE_REC_BYTES 29
+int mpx_replay_durable(mpx_engine* eng, const uint8_t* log, size_t len, int32_t inst_cap,
+                       mpx_log_rec* recs, uint8_t* op, int64_t* key, int64_t* val,
+                       int32_t* last_rec, int32_t* scalars);
+/* device form: d_log 16-byte aligned; d_last_rec[inst_cap] initialised by the caller (-1, or a
+ * previous call's indices shifted below this call's); d_scalars[2] in/out                    */
+int mpx_replay_durable_dev(mpx_engine* eng, const uint8_t* d_log, size_t len, int32_t inst_cap,
+                           mpx_log_rec* d_recs, uint8_t* d_op, int64_t* d_key, int64_t* d_val,
+                           int32_t* d_last_rec, int32_t* d_scalars, void* stream);
 
 #ifdef __cplusplus
 }

@@ -69,6 +69,8 @@ SIGNATURES = {
     "mpx_encode_log": (C.c_int, [_p, C.c_int, _p, _sz, _p, _p, _p, _p, _sz, _p, _sz, _p]),
     "mpx_encode_log_reserve": (C.c_int, [_p, _sz, _sz]),
     "mpx_encode_log_dev": (C.c_int, [_p, C.c_int, _p, _sz, _p, _p, _p, _p, _sz, _p, _p, _p]),
+    "mpx_replay_durable": (C.c_int, [_p, _p, _sz, _i32, _p, _p, _p, _p, _p, _p]),
+    "mpx_replay_durable_dev": (C.c_int, [_p, _p, _sz, _i32, _p, _p, _p, _p, _p, _p, _p]),
 }
 
 _lib = None

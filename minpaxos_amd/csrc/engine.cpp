@@ -46,6 +46,8 @@ struct mpx_engine {
     // instance-log encoding: staging (records, offsets, op, key, val, out, rec_off) + scratch
     DevBuf lg[7];
     DevBuf log_work;
+    // durable-log replay staging: log bytes, records, op, key, val, last_rec, scalars
+    DevBuf rp[7];
     uint64_t apply_chunk = 0;  // commands per apply chunk (0 = kApplyChunkDefault)
     // group-step work list (groups the fast kernel hands to the general kernel) + its count
     DevBuf worklist;
@@ -234,6 +236,8 @@ int mpx_close(mpx_engine* e) {
     for (auto& x : e->lg)
         if (x.p) (void)hipFree(x.p);
     if (e->log_work.p) (void)hipFree(e->log_work.p);
+    for (auto& x : e->rp)
+        if (x.p) (void)hipFree(x.p);
     if (e->worklist.p) (void)hipFree(e->worklist.p);
     if (e->d_wcount) (void)hipFree(e->d_wcount);
     if (e->kv_ready) {
@@ -866,6 +870,60 @@ int mpx_encode_log(mpx_engine* e, int format, const mpx_log_rec* recs, size_t n,
     if (rec_off[n] > out_cap) return fail(e, MPX_E_INVAL, "out_cap is smaller than the encoding");
     CK(d2h(e, out, e->lg[5].p, rec_off[n]));
     return finish(e);
+}
+
+// ---- §8(f) rank 3, read side: durable-log replay --------------------------------------------
+int mpx_replay_durable_dev(mpx_engine* e, const uint8_t* d_log, size_t len, int32_t inst_cap,
+                           mpx_log_rec* d_recs, uint8_t* d_op, int64_t* d_key, int64_t* d_val,
+                           int32_t* d_last_rec, int32_t* d_scalars, void* stream) {
+    if (!e || !d_scalars || inst_cap < 0) return MPX_E_INVAL;
+    if (len % MPX_DURABLE_REC_BYTES)
+        return fail(e, MPX_E_INVAL, "durable log ends in a partial record");
+    const size_t n = len / MPX_DURABLE_REC_BYTES;
+    if (n > (size_t)INT32_MAX) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 records");
+    if (n && (!d_log || !d_recs || !d_op || !d_key || !d_val || !d_last_rec))
+        return MPX_E_INVAL;
+    if ((uintptr_t)d_log % 16)
+        return fail(e, MPX_E_INVAL, "d_log must be 16-byte aligned (the tiles load 16 B vectors)");
+    HIPCHK(e, mpx::launch_replay_durable(d_log, n, inst_cap, d_recs, d_op, d_key, d_val,
+                                         d_last_rec, d_scalars, e->d_err, pick(e, stream)));
+    return MPX_OK;
+}
+
+int mpx_replay_durable(mpx_engine* e, const uint8_t* log, size_t len, int32_t inst_cap,
+                       mpx_log_rec* recs, uint8_t* op, int64_t* key, int64_t* val,
+                       int32_t* last_rec, int32_t* scalars) {
+    if (!e || !scalars || inst_cap < 0 || (inst_cap && !last_rec)) return MPX_E_INVAL;
+    if (len % MPX_DURABLE_REC_BYTES)
+        return fail(e, MPX_E_INVAL, "durable log ends in a partial record");
+    const size_t n = len / MPX_DURABLE_REC_BYTES;
+    if (n > (size_t)INT32_MAX) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 records");
+    if (n && (!log || !recs || !op || !key || !val)) return MPX_E_INVAL;
+    CK(begin(e));
+    GROW(e, e->rp[0], len);
+    GROW(e, e->rp[1], n * sizeof(mpx_log_rec));
+    GROW(e, e->rp[2], n);
+    GROW(e, e->rp[3], n * 8);
+    GROW(e, e->rp[4], n * 8);
+    GROW(e, e->rp[5], (size_t)inst_cap * 4);
+    GROW(e, e->rp[6], 2 * sizeof(int32_t));
+    CK(h2d(e, e->rp[0].p, log, len));
+    if (inst_cap) HIPCHK(e, hipMemsetAsync(e->rp[5].p, 0xff, (size_t)inst_cap * 4, e->stream));
+    CK(h2d(e, e->rp[6].p, scalars, 2 * sizeof(int32_t)));
+    CK(mpx_replay_durable_dev(e, (const uint8_t*)e->rp[0].p, len, inst_cap,
+                              (mpx_log_rec*)e->rp[1].p, (uint8_t*)e->rp[2].p,
+                              (int64_t*)e->rp[3].p, (int64_t*)e->rp[4].p, (int32_t*)e->rp[5].p,
+                              (int32_t*)e->rp[6].p, e->stream));
+    CK(d2h(e, recs, e->rp[1].p, n * sizeof(mpx_log_rec)));
+    CK(d2h(e, op, e->rp[2].p, n));
+    CK(d2h(e, key, e->rp[3].p, n * 8));
+    CK(d2h(e, val, e->rp[4].p, n * 8));
+    CK(d2h(e, last_rec, e->rp[5].p, (size_t)inst_cap * 4));
+    CK(d2h(e, scalars, e->rp[6].p, 2 * sizeof(int32_t)));
+    int rc = finish(e);
+    if (rc == MPX_E_NIL_INSTANCE)
+        return fail(e, rc, "a durable record's instNo is outside [0, inst_cap)");
+    return rc;
 }
 
 }  // extern "C"

@@ -102,4 +102,11 @@ hipError_t launch_encode_log(int format, const mpx_log_rec* recs, uint64_t n,
                              const int64_t* val, uint64_t m, uint8_t* out, uint64_t* rec_off,
                              void* work, uint64_t work_bytes, hipStream_t stream);
 
+
+// ---- durable-log replay (mpx_replay_durable) ---------------------------------------------
+hipError_t launch_replay_durable(const uint8_t* log, uint64_t n, int32_t inst_cap,
+                                 mpx_log_rec* recs, uint8_t* op, int64_t* key, int64_t* val,
+                                 int32_t* last_rec, int32_t* scalars, uint32_t* err,
+                                 hipStream_t stream);
+
 }  // namespace mpx

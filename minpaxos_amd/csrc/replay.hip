@@ -1,0 +1,113 @@
+// replay.hip — durable-log replay (the read side of the durable log).
+//
+// bareminpaxos.(*Replica).getDataFromStableStore  src/bareminpaxos/bareminpaxos.go:122-161 reads
+// the stable store as back-to-back 29-byte records: 12 bytes of metadata (Ballot, Status, instNo as
+// little-endian u32, :130-140) and exactly one state.Command (:142-143, Command.Unmarshal
+// statemarsh.go:21-37: Op u8, K i64, V i64). Per record, in file order:
+//   defaultBallot = ballot            if ballot > defaultBallot                     (:145-147)
+//   committedUpTo = instNo            if instNo > committedUpTo && COMMITTED        (:149-151)
+//   instanceSpace[instNo] = {ballot, status, {0,0,0,nil}, [command]}               (:153-157)
+// The two watermarks are running maxima, so they are order-free; the last record naming an
+// instance wins its slot, so the slot keeps the HIGHEST record index (atomicMax).
+//
+// Layout: one workgroup per 256-record tile (7424 bytes = 464 x 16 B, so every tile starts
+// 16-byte aligned when the log does); the tile is staged into LDS with 16-byte loads and each lane
+// cuts its record out of LDS, then writes the SoA outputs coalesced (16-byte mpx_log_rec, op,
+// key, val). Wave max-reductions feed one atomicMax per wave for each watermark. HBM-bound:
+// 29 B in + 33 B out + one 4-byte slot update per record.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace mpx {
+
+namespace {
+constexpr int kReplayBlock = 256;
+constexpr int kRecBytes = MPX_DURABLE_REC_BYTES;               // 12 + 17
+constexpr int kTileBytes = kReplayBlock * kRecBytes;           // 7424
+constexpr int kTileVec = kTileBytes / 16;                      // 464
+static_assert(kTileBytes % 16 == 0, "tile must be a whole number of 16-byte vectors");
+
+__device__ __forceinline__ uint32_t ld_u32(const uint8_t* s) {
+    return (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
+}
+__device__ __forceinline__ uint64_t ld_u64(const uint8_t* s) {
+    return (uint64_t)ld_u32(s) | ((uint64_t)ld_u32(s + 4) << 32);
+}
+
+__device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const int32_t t = __shfl_xor(v, d);
+        v = v > t ? v : t;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(kReplayBlock) void k_replay_durable(
+    const uint8_t* __restrict__ log, uint64_t n, int32_t inst_cap, mpx_log_rec* __restrict__ recs,
+    uint8_t* __restrict__ op, int64_t* __restrict__ key, int64_t* __restrict__ val,
+    int32_t* __restrict__ last_rec, int32_t* __restrict__ scalars, uint32_t* __restrict__ err) {
+    __shared__ uint4 tile[kTileVec];
+    const uint64_t r0 = (uint64_t)blockIdx.x * kReplayBlock;
+    const uint64_t nrec = n - r0 < (uint64_t)kReplayBlock ? n - r0 : (uint64_t)kReplayBlock;
+    const uint64_t tile_bytes = nrec * kRecBytes;
+    const uint8_t* src = log + r0 * kRecBytes;
+    // stage: whole 16-byte vectors inside the tile's records, the ragged tail byte by byte
+    const uint64_t nvec = tile_bytes / 16;
+    for (int v = threadIdx.x; v < kTileVec; v += kReplayBlock) {
+        if ((uint64_t)v < nvec) {
+            tile[v] = ld_stream(reinterpret_cast<const uint4*>(src) + v);
+        } else if ((uint64_t)v * 16 < tile_bytes) {
+            uint8_t b[16] = {};
+            for (uint64_t k = (uint64_t)v * 16; k < tile_bytes; ++k) b[k - (uint64_t)v * 16] = src[k];
+            tile[v] = *reinterpret_cast<const uint4*>(b);
+        }
+    }
+    __syncthreads();
+
+    const int t = threadIdx.x;
+    int32_t ballot = INT32_MIN, committed = INT32_MIN;
+    if ((uint64_t)t < nrec) {
+        const uint8_t* s = reinterpret_cast<const uint8_t*>(tile) + t * kRecBytes;
+        const int32_t b = (int32_t)ld_u32(s);
+        const int32_t st = (int32_t)ld_u32(s + 4);
+        const int32_t inst = (int32_t)ld_u32(s + 8);
+        const uint64_t i = r0 + t;
+        mpx_log_rec r;
+        r.ballot = b;
+        r.status = st;
+        r.inst_no = inst;
+        r.pad = 0;
+        st_stream(reinterpret_cast<int4*>(recs + i), *reinterpret_cast<const int4*>(&r));
+        st_stream(op + i, s[12]);
+        st_stream(key + i, (int64_t)ld_u64(s + 13));
+        st_stream(val + i, (int64_t)ld_u64(s + 21));
+        ballot = b;
+        if (st == MPX_COMMITTED) committed = inst;
+        // instanceSpace[instNo] panics outside the array (Go index check)
+        if (inst < 0 || inst >= inst_cap)
+            raise_err(err, kErrNil);
+        else
+            atomicMax(last_rec + inst, (int32_t)i);
+    }
+    ballot = wave_max_i32(ballot);
+    committed = wave_max_i32(committed);
+    if (lane_id() == 0) {
+        if (ballot != INT32_MIN) atomicMax(scalars + 0, ballot);
+        if (committed != INT32_MIN) atomicMax(scalars + 1, committed);
+    }
+}
+}  // namespace
+
+hipError_t launch_replay_durable(const uint8_t* log, uint64_t n, int32_t inst_cap,
+                                 mpx_log_rec* recs, uint8_t* op, int64_t* key, int64_t* val,
+                                 int32_t* last_rec, int32_t* scalars, uint32_t* err,
+                                 hipStream_t stream) {
+    if (!n) return hipSuccess;
+    const uint64_t grid = (n + kReplayBlock - 1) / kReplayBlock;
+    hipLaunchKernelGGL(k_replay_durable, dim3((unsigned)grid), dim3(kReplayBlock), 0, stream, log,
+                       n, inst_cap, recs, op, key, val, last_rec, scalars, err);
+    return hipGetLastError();
+}
+
+}  // namespace mpx

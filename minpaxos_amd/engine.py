@@ -10,6 +10,7 @@ Names and argument meaning follow the reference handlers they replace:
   group_step          <- handleAcceptReply + executeCommands for many replicas at once
   decode_peer_stream  <- genericsmr.replicaListener framing + AcceptReply.Unmarshal
   encode_replies      <- the ProposeReplyTS fan-out (ReplyProposeTS per executed command)
+  replay_durable      <- getDataFromStableStore (bareminpaxos.go:122-161)
   encode_log          <- Instance.Marshal (bcastAccept's CatchUpLog) / recordInstanceMetadata +
                          recordCommands (the durable log)
 Errors come back as MpxError carrying the reference-level reason (e.g. E_NIL_INSTANCE where the
@@ -321,6 +322,31 @@ class Engine:
         self._check(self.lib.mpx_encode_log_dev(self.h, fmt, d_recs, n, d_cmd_off, d_op, d_key,
                                                 d_val, m, d_out, d_rec_off, stream),
                     "mpx_encode_log_dev")
+
+    # ---- durable-log replay (read side) ---------------------------------
+    def replay_durable(self, log, inst_cap, default_ballot=0, committed_up_to=-1):
+        """getDataFromStableStore (bareminpaxos.go:122-161) over a durable log of 29-byte
+        records. Returns (recs, op, key, val, last_rec, default_ballot, committed_up_to):
+        last_rec[i] is the index of the last record naming instance i (-1: none)."""
+        log = _c(log, np.uint8)
+        n = len(log) // R.DURABLE_REC_BYTES
+        recs = np.zeros(n, R.LOG_REC)
+        op = np.zeros(n, np.uint8)
+        key = np.zeros(n, np.int64)
+        val = np.zeros(n, np.int64)
+        last = np.zeros(inst_cap, np.int32)
+        sc = np.array([default_ballot, committed_up_to], np.int32)
+        self._check(self.lib.mpx_replay_durable(self.h, _ptr(log), len(log), inst_cap, _ptr(recs),
+                                                _ptr(op), _ptr(key), _ptr(val), _ptr(last),
+                                                _ptr(sc)),
+                    "mpx_replay_durable")
+        return recs, op, key, val, last, int(sc[0]), int(sc[1])
+
+    def replay_durable_dev(self, d_log, nbytes, inst_cap, d_recs, d_op, d_key, d_val, d_last,
+                           d_scalars, stream=None):
+        self._check(self.lib.mpx_replay_durable_dev(self.h, d_log, nbytes, inst_cap, d_recs, d_op,
+                                                    d_key, d_val, d_last, d_scalars, stream),
+                    "mpx_replay_durable_dev")
 
     # ---- multi-GPU ----------------------------------------------------------------------------
     @staticmethod

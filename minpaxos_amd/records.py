@@ -74,6 +74,8 @@ PROPOSE_REPLY_BYTES = 25
 
 # mpx_log_rec / log formats (instance-log encoding)
 LOG_CATCHUP, LOG_DURABLE = 0, 1
+# mpx_replay_durable: getDataFromStableStore reads 12 metadata bytes + one 17-byte Command
+DURABLE_REC_BYTES = 29
 LOG_REC = np.dtype([("ballot", "<i4"), ("status", "<i4"), ("inst_no", "<i4"), ("pad", "<u4")])
 
 assert LOG_REC.itemsize == 16

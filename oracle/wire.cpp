@@ -176,4 +176,40 @@ int orc_encode_log(int format, const mpx_log_rec* recs, size_t n, const uint64_t
     return MPX_OK;
 }
 
+// Durable-log replay: bareminpaxos.(*Replica).getDataFromStableStore bareminpaxos.go:122-161,
+// one record per loop iteration, in file order: 12 metadata bytes (:127-140), one
+// Command.Unmarshal (:142-143, statemarsh.go:21-37), the two watermark updates (:145-151), and
+// instanceSpace[instNo] = the record (:153-157; last_rec[] keeps the index of that record).
+// A trailing partial record is rejected (the reference decodes it zero-padded), and an instNo
+// outside [0, inst_cap) stops the loop where Go's index check panics.
+int orc_replay_durable(const uint8_t* log, size_t len, int32_t inst_cap, mpx_log_rec* recs,
+                       uint8_t* op, int64_t* key, int64_t* val, int32_t* last_rec,
+                       int32_t* scalars) {
+    if (len % MPX_DURABLE_REC_BYTES) return MPX_E_INVAL;
+    auto u32 = [](const uint8_t* b) {
+        return (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) |
+               ((uint32_t)b[3] << 24);
+    };
+    auto u64 = [&](const uint8_t* b) { return (uint64_t)u32(b) | ((uint64_t)u32(b + 4) << 32); };
+    for (int32_t i = 0; i < inst_cap; ++i) last_rec[i] = -1;
+    int32_t& defaultBallot = scalars[0];
+    int32_t& committedUpTo = scalars[1];
+    const size_t n = len / MPX_DURABLE_REC_BYTES;
+    for (size_t i = 0; i < n; ++i) {
+        const uint8_t* bs = log + i * MPX_DURABLE_REC_BYTES;
+        const int32_t ballot = (int32_t)u32(bs);
+        const int32_t status = (int32_t)u32(bs + 4);
+        const int32_t instNo = (int32_t)u32(bs + 8);
+        recs[i] = mpx_log_rec{ballot, status, instNo, 0};
+        op[i] = bs[12];
+        key[i] = (int64_t)u64(bs + 13);
+        val[i] = (int64_t)u64(bs + 21);
+        if (ballot > defaultBallot) defaultBallot = ballot;
+        if (instNo > committedUpTo && status == MPX_COMMITTED) committedUpTo = instNo;
+        if (instNo < 0 || instNo >= inst_cap) return MPX_E_NIL_INSTANCE;
+        last_rec[instNo] = (int32_t)i;
+    }
+    return MPX_OK;
+}
+
 }  // extern "C"

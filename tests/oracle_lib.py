@@ -53,6 +53,7 @@ def load():
         "orc_decode_peer_stream": (C.c_int, [_p, _sz, _p, _sz, _p, _sz, _p]),
         "orc_encode_replies": (C.c_int, [_p, _sz, C.c_uint32, C.c_uint8, _i32, _p, _p]),
         "orc_encode_log": (C.c_int, [C.c_int, _p, _sz, _p, _p, _p, _p, _p, _sz, _p]),
+        "orc_replay_durable": (C.c_int, [_p, _sz, _i32, _p, _p, _p, _p, _p, _p]),
         "orc_bench_group_step": (C.c_int64, [C.c_int, C.c_int, C.POINTER(L.MpxGroupBatch),
                                              C.c_uint32, C.c_int]),
     }
@@ -205,6 +206,22 @@ class Oracle:
         _check(self.lib.orc_encode_log(fmt, _ptr(recs), n, _ptr(off), _ptr(op), _ptr(key),
                                        _ptr(val), _ptr(out), cap, _ptr(ro)), "orc_encode_log")
         return out[:int(ro[-1])], ro
+
+    def replay_durable(self, log, inst_cap, default_ballot=0, committed_up_to=-1):
+        """getDataFromStableStore (bareminpaxos.go:122-161): returns (recs, op, key, val,
+        last_rec, default_ballot, committed_up_to)."""
+        log = np.ascontiguousarray(log, np.uint8)
+        n = len(log) // R.DURABLE_REC_BYTES
+        recs = np.zeros(n, R.LOG_REC)
+        op = np.zeros(n, np.uint8)
+        key = np.zeros(n, np.int64)
+        val = np.zeros(n, np.int64)
+        last = np.zeros(inst_cap, np.int32)
+        sc = np.array([default_ballot, committed_up_to], np.int32)
+        _check(self.lib.orc_replay_durable(_ptr(log), len(log), inst_cap, _ptr(recs), _ptr(op),
+                                           _ptr(key), _ptr(val), _ptr(last), _ptr(sc)),
+               "orc_replay_durable")
+        return recs, op, key, val, last, int(sc[0]), int(sc[1])
 
     def group_step(self, b, kv_cnt=None, kv_key=None, kv_val=None, ret=None, want_conf=True,
                    want_decided=True):
