@@ -10,10 +10,11 @@
 // The two watermarks are running maxima, so they are order-free; the last record naming an
 // instance wins its slot, so the slot keeps the HIGHEST record index (atomicMax).
 //
-// Layout: one workgroup per 256-record tile (7424 bytes = 464 x 16 B, so every tile starts
+// Layout: 256-record tiles (7424 bytes = 464 x 16 B, so every tile starts
 // 16-byte aligned when the log does); the tile is staged into LDS with 16-byte loads and each lane
 // cuts its record out of LDS, then writes the SoA outputs coalesced (16-byte mpx_log_rec, op,
-// key, val). Wave max-reductions feed one atomicMax per wave for each watermark. HBM-bound:
+// key, val); a grid of 8 workgroups per CU walks the tiles, and each workgroup's max-reductions
+// feed one atomicMax per watermark. HBM-bound:
 // 29 B in + 33 B out + one 4-byte slot update per record.
 #include "common.hpp"
 #include "kernels.hpp"
@@ -25,6 +26,7 @@ constexpr int kReplayBlock = 256;
 constexpr int kRecBytes = MPX_DURABLE_REC_BYTES;               // 12 + 17
 constexpr int kTileBytes = kReplayBlock * kRecBytes;           // 7424
 constexpr int kTileVec = kTileBytes / 16;                      // 464
+constexpr uint64_t kReplayGrid = 256 * 8;  // 256 CUs x 8 workgroups
 static_assert(kTileBytes % 16 == 0, "tile must be a whole number of 16-byte vectors");
 
 __device__ __forceinline__ uint32_t ld_u32(const uint8_t* s) {
@@ -48,53 +50,68 @@ __global__ __launch_bounds__(kReplayBlock) void k_replay_durable(
     uint8_t* __restrict__ op, int64_t* __restrict__ key, int64_t* __restrict__ val,
     int32_t* __restrict__ last_rec, int32_t* __restrict__ scalars, uint32_t* __restrict__ err) {
     __shared__ uint4 tile[kTileVec];
-    const uint64_t r0 = (uint64_t)blockIdx.x * kReplayBlock;
-    const uint64_t nrec = n - r0 < (uint64_t)kReplayBlock ? n - r0 : (uint64_t)kReplayBlock;
-    const uint64_t tile_bytes = nrec * kRecBytes;
-    const uint8_t* src = log + r0 * kRecBytes;
-    // stage: whole 16-byte vectors inside the tile's records, the ragged tail byte by byte
-    const uint64_t nvec = tile_bytes / 16;
-    for (int v = threadIdx.x; v < kTileVec; v += kReplayBlock) {
-        if ((uint64_t)v < nvec) {
-            tile[v] = ld_stream(reinterpret_cast<const uint4*>(src) + v);
-        } else if ((uint64_t)v * 16 < tile_bytes) {
-            uint8_t b[16] = {};
-            for (uint64_t k = (uint64_t)v * 16; k < tile_bytes; ++k) b[k - (uint64_t)v * 16] = src[k];
-            tile[v] = *reinterpret_cast<const uint4*>(b);
-        }
-    }
-    __syncthreads();
-
+    __shared__ int32_t red[2][kReplayBlock / kWave];
     const int t = threadIdx.x;
     int32_t ballot = INT32_MIN, committed = INT32_MIN;
-    if ((uint64_t)t < nrec) {
-        const uint8_t* s = reinterpret_cast<const uint8_t*>(tile) + t * kRecBytes;
-        const int32_t b = (int32_t)ld_u32(s);
-        const int32_t st = (int32_t)ld_u32(s + 4);
-        const int32_t inst = (int32_t)ld_u32(s + 8);
-        const uint64_t i = r0 + t;
-        mpx_log_rec r;
-        r.ballot = b;
-        r.status = st;
-        r.inst_no = inst;
-        r.pad = 0;
-        st_stream(reinterpret_cast<int4*>(recs + i), *reinterpret_cast<const int4*>(&r));
-        st_stream(op + i, s[12]);
-        st_stream(key + i, (int64_t)ld_u64(s + 13));
-        st_stream(val + i, (int64_t)ld_u64(s + 21));
-        ballot = b;
-        if (st == MPX_COMMITTED) committed = inst;
-        // instanceSpace[instNo] panics outside the array (Go index check)
-        if (inst < 0 || inst >= inst_cap)
-            raise_err(err, kErrNil);
-        else
-            atomicMax(last_rec + inst, (int32_t)i);
+    const uint64_t n_tiles = (n + kReplayBlock - 1) / kReplayBlock;
+    for (uint64_t tl = blockIdx.x; tl < n_tiles; tl += gridDim.x) {
+        const uint64_t r0 = tl * kReplayBlock;
+        const uint64_t nrec = n - r0 < (uint64_t)kReplayBlock ? n - r0 : (uint64_t)kReplayBlock;
+        const uint64_t tile_bytes = nrec * kRecBytes;
+        const uint8_t* src = log + r0 * kRecBytes;
+        // stage: whole 16-byte vectors inside the tile's records, the ragged tail byte by byte
+        const uint64_t nvec = tile_bytes / 16;
+        __syncthreads();  // the previous tile's readers are done with the LDS image
+        for (int v = t; v < kTileVec; v += kReplayBlock) {
+            if ((uint64_t)v < nvec) {
+                tile[v] = ld_stream(reinterpret_cast<const uint4*>(src) + v);
+            } else if ((uint64_t)v * 16 < tile_bytes) {
+                uint8_t b[16] = {};
+                for (uint64_t k = (uint64_t)v * 16; k < tile_bytes; ++k)
+                    b[k - (uint64_t)v * 16] = src[k];
+                tile[v] = *reinterpret_cast<const uint4*>(b);
+            }
+        }
+        __syncthreads();
+        if ((uint64_t)t < nrec) {
+            const uint8_t* s = reinterpret_cast<const uint8_t*>(tile) + t * kRecBytes;
+            const int32_t b = (int32_t)ld_u32(s);
+            const int32_t st = (int32_t)ld_u32(s + 4);
+            const int32_t inst = (int32_t)ld_u32(s + 8);
+            const uint64_t i = r0 + t;
+            mpx_log_rec r;
+            r.ballot = b;
+            r.status = st;
+            r.inst_no = inst;
+            r.pad = 0;
+            st_stream(reinterpret_cast<int4*>(recs + i), *reinterpret_cast<const int4*>(&r));
+            st_stream(op + i, s[12]);
+            st_stream(key + i, (int64_t)ld_u64(s + 13));
+            st_stream(val + i, (int64_t)ld_u64(s + 21));
+            ballot = b > ballot ? b : ballot;
+            if (st == MPX_COMMITTED && inst > committed) committed = inst;
+            // instanceSpace[instNo] panics outside the array (Go index check)
+            if (inst < 0 || inst >= inst_cap)
+                raise_err(err, kErrNil);
+            else
+                atomicMax(last_rec + inst, (int32_t)i);
+        }
     }
+    // one atomic per workgroup and watermark, skipped when it cannot raise the running value:
+    // per-wave atomics on the two words serialised at L2 (2 x 262k atomics for 2^24 records)
     ballot = wave_max_i32(ballot);
     committed = wave_max_i32(committed);
     if (lane_id() == 0) {
-        if (ballot != INT32_MIN) atomicMax(scalars + 0, ballot);
-        if (committed != INT32_MIN) atomicMax(scalars + 1, committed);
+        red[0][t / kWave] = ballot;
+        red[1][t / kWave] = committed;
+    }
+    __syncthreads();
+    if (t < 2) {
+        int32_t m = INT32_MIN;
+        for (int w = 0; w < kReplayBlock / kWave; ++w) m = red[t][w] > m ? red[t][w] : m;
+        if (m != INT32_MIN && m > __hip_atomic_load(scalars + t, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT))
+            atomicMax(scalars + t, m);
     }
 }
 }  // namespace
@@ -104,7 +121,9 @@ hipError_t launch_replay_durable(const uint8_t* log, uint64_t n, int32_t inst_ca
                                  int32_t* last_rec, int32_t* scalars, uint32_t* err,
                                  hipStream_t stream) {
     if (!n) return hipSuccess;
-    const uint64_t grid = (n + kReplayBlock - 1) / kReplayBlock;
+    // a few workgroups per CU walk the tiles (grid-stride), so the watermark atomics stay few
+    const uint64_t tiles = (n + kReplayBlock - 1) / kReplayBlock;
+    const uint64_t grid = tiles < kReplayGrid ? tiles : kReplayGrid;
     hipLaunchKernelGGL(k_replay_durable, dim3((unsigned)grid), dim3(kReplayBlock), 0, stream, log,
                        n, inst_cap, recs, op, key, val, last_rec, scalars, err);
     return hipGetLastError();

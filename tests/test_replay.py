@@ -122,9 +122,42 @@ def test_replay_round_trip_engine(mk_engine):
     assert np.array_equal(last[recs["inst_no"]], np.arange(n))
 
 
+class _Hip:
+    """Device buffers through the engine's own HIP runtime (/opt/rocm/lib, the library libmpx.so
+    links): torch ships a second HIP runtime that cannot share the device with the first once
+    the engine has initialised it in this process."""
+
+    def __init__(self):
+        import ctypes as C
+        self.C = C
+        self.h = C.CDLL("/opt/rocm/lib/libamdhip64.so")
+        self.live = []
+
+    def put(self, a):
+        C = self.C
+        a = np.ascontiguousarray(a)
+        p = C.c_void_p()
+        assert self.h.hipMalloc(C.byref(p), C.c_size_t(max(a.nbytes, 16))) == 0
+        self.live.append(p)
+        if a.nbytes:
+            assert self.h.hipMemcpy(p, a.ctypes.data_as(C.c_void_p), C.c_size_t(a.nbytes), 1) == 0
+        return p.value
+
+    def get(self, ptr, like):
+        C = self.C
+        out = np.empty_like(like)
+        if out.nbytes:
+            assert self.h.hipMemcpy(out.ctypes.data_as(C.c_void_p), C.c_void_p(ptr),
+                                    C.c_size_t(out.nbytes), 2) == 0
+        return out
+
+    def free(self):
+        for p in self.live:
+            self.h.hipFree(p)
+
+
 @pytest.mark.gpu
 def test_replay_errors_and_dev(mk_engine):
-    import torch
     from minpaxos_amd.engine import MpxError
     e, o = mk_engine(5, R.MODE_MIN), Oracle()
     log = durable_log(1000, 600, 11)
@@ -134,23 +167,20 @@ def test_replay_errors_and_dev(mk_engine):
         e.replay_durable(log, 100)
     # device form: caller-initialised slots, scalars in HBM
     n, cap = 1000, 600
-    d_log = torch.from_numpy(log).cuda()
-    d_recs = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
-    d_op = torch.zeros(n, dtype=torch.uint8, device="cuda")
-    d_key = torch.zeros(n, dtype=torch.int64, device="cuda")
-    d_val = torch.zeros(n, dtype=torch.int64, device="cuda")
-    d_last = torch.full((cap,), -1, dtype=torch.int32, device="cuda")
-    d_sc = torch.tensor([0, -1], dtype=torch.int32, device="cuda")
-    torch.cuda.synchronize()
-    e.replay_durable_dev(d_log.data_ptr(), len(log), cap, d_recs.data_ptr(), d_op.data_ptr(),
-                         d_key.data_ptr(), d_val.data_ptr(), d_last.data_ptr(), d_sc.data_ptr())
-    e.synchronize()
     want = o.replay_durable(log, cap)
-    assert np.array_equal(d_recs.cpu().numpy().view(R.LOG_REC), want[0])
-    assert np.array_equal(d_key.cpu().numpy(), want[2])
-    assert np.array_equal(d_last.cpu().numpy(), want[4])
-    assert d_sc.cpu().tolist() == [want[5], want[6]]
-    with pytest.raises(MpxError):  # misaligned device log
-        e.replay_durable_dev(d_log.data_ptr() + 1, 29, cap, d_recs.data_ptr(), d_op.data_ptr(),
-                             d_key.data_ptr(), d_val.data_ptr(), d_last.data_ptr(),
-                             d_sc.data_ptr())
+    hip = _Hip()
+    try:
+        d_log = hip.put(log)
+        d = [hip.put(np.zeros_like(w)) for w in want[:4]]
+        d_last = hip.put(np.full(cap, -1, np.int32))
+        d_sc = hip.put(np.array([0, -1], np.int32))
+        e.replay_durable_dev(d_log, len(log), cap, *d, d_last, d_sc)
+        e.synchronize()
+        for ptr, w in zip(d, want[:4]):
+            assert np.array_equal(hip.get(ptr, w), w)
+        assert np.array_equal(hip.get(d_last, want[4]), want[4])
+        assert hip.get(d_sc, np.zeros(2, np.int32)).tolist() == [want[5], want[6]]
+        with pytest.raises(MpxError):  # misaligned device log
+            e.replay_durable_dev(d_log + 1, 29, cap, *d, d_last, d_sc)
+    finally:
+        hip.free()
