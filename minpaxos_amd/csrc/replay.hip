@@ -29,13 +29,6 @@ constexpr int kTileVec = kTileBytes / 16;                      // 464
 constexpr uint64_t kReplayGrid = 256 * 8;  // 256 CUs x 8 workgroups
 static_assert(kTileBytes % 16 == 0, "tile must be a whole number of 16-byte vectors");
 
-__device__ __forceinline__ uint32_t ld_u32(const uint8_t* s) {
-    return (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
-}
-__device__ __forceinline__ uint64_t ld_u64(const uint8_t* s) {
-    return (uint64_t)ld_u32(s) | ((uint64_t)ld_u32(s + 4) << 32);
-}
-
 __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
@@ -49,7 +42,7 @@ __global__ __launch_bounds__(kReplayBlock) void k_replay_durable(
     const uint8_t* __restrict__ log, uint64_t n, int32_t inst_cap, mpx_log_rec* __restrict__ recs,
     uint8_t* __restrict__ op, int64_t* __restrict__ key, int64_t* __restrict__ val,
     int32_t* __restrict__ last_rec, int32_t* __restrict__ scalars, uint32_t* __restrict__ err) {
-    __shared__ uint4 tile[kTileVec];
+    __shared__ uint4 tile[kTileVec + 1];  // +1: the last lane's 9th dword reads past the tile
     __shared__ int32_t red[2][kReplayBlock / kWave];
     const int t = threadIdx.x;
     int32_t ballot = INT32_MIN, committed = INT32_MIN;
@@ -74,10 +67,22 @@ __global__ __launch_bounds__(kReplayBlock) void k_replay_durable(
         }
         __syncthreads();
         if ((uint64_t)t < nrec) {
-            const uint8_t* s = reinterpret_cast<const uint8_t*>(tile) + t * kRecBytes;
-            const int32_t b = (int32_t)ld_u32(s);
-            const int32_t st = (int32_t)ld_u32(s + 4);
-            const int32_t inst = (int32_t)ld_u32(s + 8);
+            // the record as 8 realigned dwords from 9 aligned LDS dword reads (not 29 byte reads)
+            const int off = t * kRecBytes;
+            const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(tile) + (off >> 2);
+            const int sh = (off & 3) * 8;
+            uint32_t w[9], d[8];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) w[k] = wsrc[k];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                d[k] = (uint32_t)((((uint64_t)w[k + 1] << 32) | w[k]) >> sh);
+            const int32_t b = (int32_t)d[0];
+            const int32_t st = (int32_t)d[1];
+            const int32_t inst = (int32_t)d[2];
+            const uint8_t opb = (uint8_t)d[3];
+            const uint64_t kv = ((((uint64_t)d[4] << 32) | d[3]) >> 8) | ((uint64_t)(d[5] & 0xff) << 56);
+            const uint64_t vv = ((((uint64_t)d[6] << 32) | d[5]) >> 8) | ((uint64_t)(d[7] & 0xff) << 56);
             const uint64_t i = r0 + t;
             mpx_log_rec r;
             r.ballot = b;
@@ -85,9 +90,9 @@ __global__ __launch_bounds__(kReplayBlock) void k_replay_durable(
             r.inst_no = inst;
             r.pad = 0;
             st_stream(reinterpret_cast<int4*>(recs + i), *reinterpret_cast<const int4*>(&r));
-            st_stream(op + i, s[12]);
-            st_stream(key + i, (int64_t)ld_u64(s + 13));
-            st_stream(val + i, (int64_t)ld_u64(s + 21));
+            st_stream(op + i, opb);
+            st_stream(key + i, (int64_t)kv);
+            st_stream(val + i, (int64_t)vv);
             ballot = b > ballot ? b : ballot;
             if (st == MPX_COMMITTED && inst > committed) committed = inst;
             // instanceSpace[instNo] panics outside the array (Go index check)
