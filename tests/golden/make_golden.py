@@ -75,6 +75,15 @@ def cases():
     for fmt, fname in ((R.LOG_CATCHUP, "catchup"), (R.LOG_DURABLE, "durable")):
         out[f"log_{fname}"] = ("log", dict(fmt=fmt),
                                dict(recs=lrec, cmd_off=loff, op=lop, key=lkey, val=lval))
+    # durable log read back (getDataFromStableStore): 1-command records, repeated instNos, both
+    # statuses, written by the oracle's durable encoder
+    rrec, roff, rop, rkey, rval = synth.log_records(2000, 1, seed=61)
+    rrec = rrec.copy()
+    rng = np.random.default_rng(62)
+    rrec["inst_no"] = rng.integers(0, 1500, 2000)
+    rrec["status"] = np.where(rng.random(2000) < 0.6, R.COMMITTED, R.ACCEPTED)
+    rlog, _ = Oracle(5, R.MODE_MIN).encode_log(R.LOG_DURABLE, rrec, roff, rop, rkey, rval)
+    out["replay_durable"] = ("replay", dict(cap=1500, db=7, cu=-1), dict(log=rlog))
     return out
 
 
@@ -117,6 +126,11 @@ def run_case(kind, p, x, backend_mk):
         b = backend_mk(5, R.MODE_MIN)
         out, ro = b.encode_log(p["fmt"], x["recs"], x["cmd_off"], x["op"], x["key"], x["val"])
         return dict(out=out, rec_off=ro)
+    if kind == "replay":
+        b = backend_mk(5, R.MODE_MIN)
+        rc, op, key, val, last, db, cu = b.replay_durable(x["log"], p["cap"], p["db"], p["cu"])
+        return dict(recs=rc, op=op, key=key, val=val, last_rec=last,
+                    scalars=np.array([db, cu], np.int32))
     raise ValueError(kind)
 
 
