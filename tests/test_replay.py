@@ -123,14 +123,16 @@ def test_replay_round_trip_engine(mk_engine):
 
 
 class _Hip:
-    """Device buffers through the engine's own HIP runtime (/opt/rocm/lib, the library libmpx.so
-    links): torch ships a second HIP runtime that cannot share the device with the first once
-    the engine has initialised it in this process."""
+    """Device buffers through the HIP runtime libmpx.so is bound to in this process (its
+    libamdhip64.so.7, already loaded with the engine: /opt/rocm's, or torch's when torch came
+    first). torch.cuda cannot be used here: once the engine has initialised a runtime that is not
+    torch's, torch finds no device."""
 
     def __init__(self):
         import ctypes as C
+        import os
         self.C = C
-        self.h = C.CDLL("/opt/rocm/lib/libamdhip64.so")
+        self.h = C.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD | os.RTLD_GLOBAL)
         self.live = []
 
     def put(self, a):
