@@ -4,29 +4,39 @@
 Workload (BASELINE.json configs[4], SURVEY §8(d) config 5, per GPU): 65,536 independent Paxos
 groups x 256 instances x 4 AcceptReplies (N = 5) + 4 PUT/GET commands per instance, per-group
 keys uniform on [0,256). One step = for every group: the accept tally (handleAcceptReply, MIN
-by default), executeCommands over the committed prefix against the group's KV table, then ONE
-RCCL all-reduce (max) of the commit/executed watermark vector of all groups of the job.
-Weak scaling: each rank owns its own 65,536 groups (block-partitioned by global group id).
+by default), executeCommands over the committed prefix against the group's KV table, the step
+totals (instances decided / executed, commands executed), then ONE RCCL group per step: max of
+the commit/executed watermark vector of all groups of the job and sum of the totals, issued on a
+second HIP stream so it overlaps the next step's kernel (double-buffered watermark vectors).
+  --scaling weak    each rank owns --groups groups (default)
+  --scaling strong  --groups-total groups split over the ranks (block partition)
+`value` = instances DECIDED by the step (quorum crossings, summed over ranks by the step's
+all-reduce) per second; every one of them is also executed in the same step (MIN executes up to
+committedUpTo, the highest decided instance). Executed instances / commands per second are
+reported beside it.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--mode min|classic]
   torchrun --nproc-per-node N bench.py --gpus N ...
 
 The other single-GPU configurations of BASELINE.json are kernel benches of their own
 (--workload; the default `step` is the headline line above):
-  tally    config 2: accept tally, 16M instances x 4 replies (k_accept_tally), --mode min|classic
-  prepare  config 3: CLASSIC prepare selection, 16M instances x 4 replies (k_prepare_classic)
-  apply    config 4: batched KV apply, 64M PUT/GET over 1M keys (the mpx_apply pipeline),
-           --dist uniform|zipf
-  decode   SURVEY §8(f) rank 1: peer-stream framing + AcceptReply decode of the config-2 replies
-           (16M instances x 4 = 64M frames of 14 B, a Beacon every ~4096 frames, 0.9 GB)
-  fanout   SURVEY §8(f) rank 2: ProposeReplyTS fan-out of the config-4 commands (64M replies
-           over --clients connections, 25-byte records grouped per connection)
-  log      SURVEY §8(f) ranks 3/4: instance-log encoding of 16M committed instances x 4 commands
-           (--log-format catchup = Instance.Marshal for bcastAccept, durable = the stable store)
+  tally       config 2: accept tally, 16M instances x 4 replies (k_accept_tally), --mode min|classic
+  prepare     config 3: CLASSIC prepare selection, 16M instances x 4 replies (k_prepare_classic)
+  prepare_min config 3, MIN variant: one PrepareBookkeeping per group, G = 65,536 (k_prepare_min)
+  apply       config 4: batched KV apply, 64M PUT/GET over 1M keys (mpx_apply), --dist uniform|zipf
+  conflict    state.ConflictBatch of consecutive instances of the config-4 commands, B = 4
+  decode      SURVEY §8(f) rank 1: peer-stream framing + AcceptReply decode of the config-2 replies
+  fanout      SURVEY §8(f) rank 2: ProposeReplyTS fan-out of 64M replies over --clients connections
+  log         SURVEY §8(f) ranks 3/4: instance-log encoding of 16M committed instances x 4 commands
+  replay      SURVEY §8(f) rank 3 (read side): durable-log replay of 16M 29-byte records
 Each prints one JSON line in the same format, with its own roofline, parity and CPU baseline.
 
-Rank 0 prints ONE JSON line. Inputs are generated on the host (synthetic, counter-based
-splitmix64) and copied to HBM before timing; the timed region contains only device work.
+Device memory, streams and events come from the engine's own HIP runtime (mpx_dev_alloc & co):
+libmpx.so is loaded before anything imports torch, so it binds /opt/rocm's HIP and RCCL — the
+runtime the tests run on, recorded in the line's "runtime" field. torch is only imported for the
+gloo group (unique-id broadcast, barriers, max over ranks) when WORLD_SIZE > 1. Inputs are
+generated on the host (counter-based splitmix64) and copied to HBM before timing; the timed
+region contains only device work.
 """
 import argparse
 import ctypes as C
@@ -40,9 +50,12 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from minpaxos_amd import _lib  # noqa: E402  (first: the engine's HIP + RCCL, not torch's)
+
+_lib.load()
 from minpaxos_amd import records as R  # noqa: E402
-from minpaxos_amd import synth  # noqa: E402
-from minpaxos_amd import _lib  # noqa: E402
+from minpaxos_amd import shard, synth  # noqa: E402
+from minpaxos_amd.devbuf import D2D, Arena, DevArray  # noqa: E402
 from minpaxos_amd.engine import Engine  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
@@ -54,255 +67,345 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mode", default="min", choices=["min", "classic"])
-    ap.add_argument("--groups", type=int, default=65536, help="groups per GPU")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--groups", type=int, default=65536, help="groups per GPU (weak scaling)")
+    ap.add_argument("--groups-total", type=int, default=65536,
+                    help="groups of the whole job (strong scaling)")
     ap.add_argument("--ipg", type=int, default=256)
     ap.add_argument("--cmds", type=int, default=4)
     ap.add_argument("--keys", type=int, default=256)
+    ap.add_argument("--replicas", type=int, default=5, help="N (replies per instance = N-1)")
+    ap.add_argument("--kv-per-group", type=int, default=512)
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="issue the step all-reduce on the compute stream (no overlap)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-groups", type=int, default=0,
                     help="groups timed on the CPU baseline (0 = auto, ~10-30 s of CPU work)")
     ap.add_argument("--parity-groups", type=int, default=512)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--workload", default="step", choices=["step", "tally", "prepare", "apply", "decode", "fanout", "log", "replay"])
+    ap.add_argument("--traffic-json", default="")
+    ap.add_argument("--workload", default="step",
+                    choices=["step", "tally", "prepare", "prepare_min", "apply", "conflict",
+                             "decode", "fanout", "log", "replay"])
     ap.add_argument("--log-format", default="catchup", choices=["catchup", "durable"])
     ap.add_argument("--clients", type=int, default=1024, help="fanout: client connections")
     ap.add_argument("--instances", type=int, default=1 << 24, help="tally / prepare: instances")
+    ap.add_argument("--prep-groups", type=int, default=65536, help="prepare_min: groups")
     ap.add_argument("--commands", type=int, default=1 << 26, help="apply: commands")
     ap.add_argument("--apply-keys", type=int, default=1 << 20, help="apply: key space")
     ap.add_argument("--kv-capacity", type=int, default=0,
                     help="apply: engine key capacity (0 = 2 x --apply-keys; the table gets >= 2x slots)")
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
+    ap.add_argument("--replay-dups", action="store_true",
+                    help="replay: instNo drawn with repeats (last record wins) instead of a permutation")
     return ap.parse_args()
 
 
+class Ranks:
+    """The process group of a multi-GPU run, for host-side coordination only (gloo on CPU):
+    the RCCL unique id broadcast, barriers around the timed region and the max over ranks of
+    the elapsed time. Device data moves only through the engine's RCCL communicator."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            import torch.distributed as dist
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x):
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def bcast(self, obj):
+        if not self.dist:
+            return obj
+        box = [obj if self.rank == 0 else None]
+        self.dist.broadcast_object_list(box, src=0)
+        return box[0]
+
+    def close(self):
+        if self.dist:
+            self.dist.barrier()
+            self.dist.destroy_process_group()
+
+
+def host_cores():
+    """the CPU share of this process: its affinity set, capped by OMP_NUM_THREADS (16 on the
+    GPU box, whose nproc reports the whole machine) and by 16"""
+    n = len(os.sched_getaffinity(0))
+    lim = os.environ.get("OMP_NUM_THREADS", "")
+    if lim.isdigit() and int(lim) > 0:
+        n = min(n, int(lim))
+    return max(1, min(n, 16))
+
+
+def traffic_of(path, **want):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary (tools/traffic.py) when it
+    was measured on this exact configuration, else None"""
+    for p in ([path] if path else [os.path.join(ROOT, "profiles", f"traffic_r0{k}.json")
+                                   for k in (2, 1)]):
+        try:
+            tj = json.load(open(p))
+        except Exception:
+            continue
+        if all(tj.get(k) == v for k, v in want.items()):
+            return tj.get("bytes_per_launch")
+    return None
+
+
+# ==================================== headline: config 5 ======================================
 def main():
     a = parse()
-    if a.workload != "step":
-        return kernel_bench(a)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    import torch
-    import torch.distributed as dist
+    rk = Ranks()
+    try:
+        if a.workload == "step":
+            step_bench(a, rk)
+        else:
+            kernel_bench(a, rk)
+    finally:
+        rk.close()
 
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+def step_bench(a, rk):
+    world, rank = rk.world, rk.rank
     mode = R.MODE_MIN if a.mode == "min" else R.MODE_CLASSIC
-    N, G, ipg, B, K = 5, a.groups, a.ipg, a.cmds, 512
-    G_total = G * world
-    eng = Engine(local, n_replicas=N, mode=mode, kv_per_group=K)
+    N, ipg, B, K = a.replicas, a.ipg, a.cmds, a.kv_per_group
+    if a.scaling == "weak":
+        G_total = a.groups * world
+    else:
+        G_total = a.groups_total
+    g0, g1 = shard.block_range(G_total, world, rank)
+    G = g1 - g0
+    eng = Engine(rk.local, n_replicas=N, mode=mode, kv_per_group=K, max_groups=max(G, 1))
+    ar = Arena(eng)
 
     # ---- this rank's block of groups, generated from their global ids --------------------------
     t_gen = time.time()
-    b = synth.group_batch(G, ipg, N, B, a.keys, p_ok=0.7, p_put=0.5, seed=45,
-                          first_group=rank * G)
+    b = synth.group_batch(G, ipg, N, B, a.keys, p_ok=0.7, p_put=0.5, seed=45, first_group=g0)
     t_gen = time.time() - t_gen
-
-    def dt(x, dtype=None):
-        arr = np.ascontiguousarray(x)
-        if arr.dtype.names:
-            arr = arr.view(np.uint8)
-        return torch.from_numpy(arr).to(dev)
-
-    n_rec = len(b["recs"])
     m = len(b["op"])
     d = dict(
-        recs=dt(b["recs"]), off=dt(b["grp_rec_off"]), st_in=dt(b["st_in"]),
-        st_out=torch.empty(G * ipg * 16, dtype=torch.uint8, device=dev),
-        ci=dt(b["committed_in"]), ei=dt(b["executed_in"]), pi=dt(b["peer_in"]),
-        po=torch.empty(G * N, dtype=torch.int32, device=dev),
-        op=dt(b["op"]), key=dt(b["key"]), val=dt(b["val"]), coff=dt(b["cmd_off"]),
-        ret=torch.zeros(m, dtype=torch.int64, device=dev),
-        conf=torch.zeros(m, dtype=torch.uint8, device=dev),
-        kc0=torch.zeros(G, dtype=torch.int32, device=dev),
-        kk0=torch.zeros(G * K, dtype=torch.int64, device=dev),
-        kv0=torch.zeros(G * K, dtype=torch.int64, device=dev),
-        kc1=torch.zeros(G, dtype=torch.int32, device=dev),
-        kk1=torch.zeros(G * K, dtype=torch.int64, device=dev),
-        kv1=torch.zeros(G * K, dtype=torch.int64, device=dev),
-        wm=torch.full((2 * G_total,), -1, dtype=torch.int32, device=dev),
+        recs=ar.put(b["recs"]), off=ar.put(b["grp_rec_off"]), st_in=ar.put(b["st_in"]),
+        st_out=ar.put(b["st_in"]),  # instances without replies keep their input state
+        ci=ar.put(b["committed_in"]), ei=ar.put(b["executed_in"]), pi=ar.put(b["peer_in"]),
+        po=ar.empty(G * N, np.int32), op=ar.put(b["op"]), key=ar.put(b["key"]),
+        val=ar.put(b["val"]), coff=ar.put(b["cmd_off"]),
+        ret=ar.full(m, np.int64, 0), conf=ar.full(m, np.uint8, 0),
+        kc0=ar.full(G, np.uint32, 0), kk0=ar.full(G * K, np.int64, 0),
+        kv0=ar.full(G * K, np.int64, 0), kc1=ar.full(G, np.uint32, 0),
+        kk1=ar.full(G * K, np.int64, 0), kv1=ar.full(G * K, np.int64, 0),
+        nd=ar.full(G, np.uint32, 0),
+        wm=[ar.full(2 * G_total, np.int32, 0xFF) for _ in range(2)],
+        tot=[ar.full(R_TOTALS, np.int64, 0) for _ in range(2)],
     )
-    co = d["wm"][rank * G:(rank + 1) * G]
-    eo = d["wm"][G_total + rank * G:G_total + (rank + 1) * G]
 
-    def batch(kc_in, kk_in, kv_in, kc_out, kk_out, kv_out):
-        p = lambda t: t.data_ptr()  # noqa: E731
+    def batch(buf, tin, tout):
+        wm = d["wm"][buf]
+        kc_i, kk_i, kv_i = tin
+        kc_o, kk_o, kv_o = tout
         return _lib.MpxGroupBatch(
-            G, ipg, p(d["recs"]), p(d["off"]), p(d["st_in"]), p(d["st_out"]), p(d["ci"]), p(co),
-            p(d["ei"]), p(eo), p(d["pi"]), p(d["po"]), p(d["op"]), p(d["key"]), p(d["val"]),
-            p(d["coff"]), None, p(d["ret"]), p(d["conf"]), p(kc_in), p(kk_in), p(kv_in),
-            p(kc_out), p(kk_out), p(kv_out), None)
+            G, ipg, d["recs"].ptr, d["off"].ptr, d["st_in"].ptr, d["st_out"].ptr, d["ci"].ptr,
+            wm.at(g0), d["ei"].ptr, wm.at(G_total + g0), d["pi"].ptr, d["po"].ptr, d["op"].ptr,
+            d["key"].ptr, d["val"].ptr, d["coff"].ptr, None, d["ret"].ptr, d["conf"].ptr,
+            kc_i.ptr, kk_i.ptr, kv_i.ptr, kc_o.ptr, kk_o.ptr, kv_o.ptr, None, d["nd"].ptr)
 
-    # all device work of a step (fill, kernel, all-reduce, events) on the engine's HIP stream
-    stream = torch.cuda.ExternalStream(eng.stream, device=dev)
-    torch.cuda.set_stream(stream)
-    sptr = C.c_void_p(eng.stream)
-    if world > 1:
-        uid = [Engine.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        eng.comm_init(world, rank, uid[0])
-    else:
-        eng.comm_init(1, 0, Engine.comm_unique_id())
+    t0s = (d["kc0"], d["kk0"], d["kv0"])
+    t1s = (d["kc1"], d["kk1"], d["kv1"])
+    comp = eng.stream
+    comm = comp if a.no_overlap else eng.stream_create()
+    uid = rk.bcast(Engine.comm_unique_id() if rank == 0 else None)
+    eng.comm_init(world, rank, uid)
 
     # steady state: the group tables already hold their keys (one untimed step fills them),
     # and every timed step reads that table and writes a fresh one (same work every step)
-    eng.group_step_dev(batch(d["kc1"], d["kk1"], d["kv1"], d["kc0"], d["kk0"], d["kv0"]), sptr)
+    eng.group_step_dev(batch(0, t1s, t0s), comp)
     eng.synchronize()
-    step_batch = batch(d["kc0"], d["kk0"], d["kv0"], d["kc1"], d["kk1"], d["kv1"])
+    steps = [batch(0, t0s, t1s), batch(1, t0s, t1s)]
+    ev_done = [eng.event_create(False) for _ in range(2)]
+    ev_comm = [eng.event_create(False) for _ in range(2)]
+    n_ev = max(a.steps, 1)
+    ev_k = [(eng.event_create(), eng.event_create()) for _ in range(n_ev)]
 
-    def step(ev=None):
-        d["wm"].fill_(-1)
-        if ev is not None:
-            ev[0].record(stream)
-        eng.group_step_dev(step_batch, sptr)
-        if ev is not None:
-            ev[1].record(stream)
-        eng.watermarks_allreduce_dev(d["wm"].data_ptr(), G_total, sptr)
+    def step(i, timed):
+        buf = i & 1
+        if i >= 2:  # buffer `buf` is free once the all-reduce of step i-2 has read it
+            eng.stream_wait_event(comp, ev_comm[buf])
+        eng.memset(d["wm"][buf].ptr, 0xFF, d["wm"][buf].nbytes, comp)  # -1 outside own groups
+        if timed:
+            eng.event_record(ev_k[i][0], comp)
+        eng.group_step_dev(steps[buf], comp)
+        if timed:
+            eng.event_record(ev_k[i][1], comp)
+        eng.step_totals_dev(steps[buf], d["tot"][buf].ptr, comp)
+        eng.event_record(ev_done[buf], comp)
+        eng.stream_wait_event(comm, ev_done[buf])
+        eng.step_allreduce_dev(d["wm"][buf].ptr, G_total, d["tot"][buf].ptr, R_TOTALS, comm)
+        eng.event_record(ev_comm[buf], comm)
 
-    for _ in range(a.warmup):
-        step()
+    for i in range(a.warmup):
+        step(i, False)
     eng.synchronize()
-    torch.cuda.synchronize(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(a.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    rk.barrier()
+    eng.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        step(evs[i])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+        step(i, True)
+    eng.synchronize()  # every stream of the device; raises if a kernel flagged an error
+    rk.barrier()
     t1 = time.perf_counter()
-    eng.synchronize()  # raises if any kernel flagged an error
-    elapsed = t1 - t0
-    kern_ms = [s.elapsed_time(e) for s, e in evs]
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = rk.max(t1 - t0)
+    kern_ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in ev_k[:a.steps]]
 
     # ---- outputs of the (identical) timed steps -------------------------------------------------
-    # instances decided by one step: status COMMITTED after it and not before it
-    st_o = d["st_out"].view(torch.int32).view(-1, 4)[:, 0]
-    st_i = d["st_in"].view(torch.int32).view(-1, 4)[:, 0]
-    n_decided = int(((st_o == R.COMMITTED) & (st_i != R.COMMITTED)).sum().item())
-    wm = d["wm"].cpu().numpy()
-    committed = wm[:G_total]
-    executed = wm[G_total:]
-    own_c = committed[rank * G:(rank + 1) * G]
-    own_e = executed[rank * G:(rank + 1) * G]
+    last = (a.steps - 1) & 1
+    tot = ar.get(d["tot"][last])  # summed over ranks by the step's all-reduce
+    n_decided, n_exec_inst, n_exec_cmds = (int(x) for x in tot)
+    wm = ar.get(d["wm"][last])
+    committed, executed = wm[:G_total], wm[G_total:]
+    own_e = executed[g0:g1].astype(np.int64)
+    kc = ar.get(d["kc1"])
+    wm_ok = bool((committed >= 0).all())  # every rank sees every group's watermark
     coff = b["cmd_off"].astype(np.int64)
     gidx = np.arange(G, dtype=np.int64) * ipg
-    lo = gidx + 0  # executed_in = -1 -> first instance 0
-    hi = gidx + own_e.astype(np.int64) + 1
-    n_exec_cmds = int((coff[hi] - coff[lo]).sum())
-    n_exec_inst = int((own_e.astype(np.int64) + 1).sum())
-    kc = d["kc1"].cpu().numpy()
-    # allreduce check: every rank sees every group's watermark (none left at -1)
-    wm_ok = bool((committed >= 0).all())
+    own_cmds = int((coff[gidx + own_e + 1] - coff[gidx]).sum())
 
-    # algorithmic bytes of one group-step launch (per rank): replies + instance state in/out,
+    # algorithmic bytes of one group-step launch (this rank): replies + instance state in/out,
     # executed commands (op,key,val in; ret,conf out), group table in/out, per-group scalars
-    alg = (n_rec * 16 + G * ipg * 16 * 2 + n_exec_cmds * (17 + 9)
-           + int(kc.sum()) * 16 * 2 + G * (4 * 4 + 2 * N * 4 + 4 * 2 + 8 * 2))
-    kern_avg_ms = float(np.mean(kern_ms))
+    n_rec = len(b["recs"])
+    alg = (n_rec * 16 + G * ipg * 16 * 2 + own_cmds * (17 + 9)
+           + int(kc.sum()) * 16 * 2 + G * (4 * 4 + 2 * N * 4 + 4 * 2 + 8 * 2 + 4))
+    kern_avg_ms = float(np.mean(kern_ms)) if kern_ms else float("nan")
     achieved_gbs = alg / (kern_avg_ms * 1e-3) / 1e9
-
-    traffic = None
-    try:
-        tj = json.load(open(a.traffic_json))
-        if tj.get("mode") == a.mode and tj.get("groups") == G:
-            traffic = tj.get("bytes_per_launch")
-    except Exception:
-        pass
 
     res = {}
     if rank == 0:
         # parity: the first groups of the timed output against the oracle (test infra)
-        res["parity"] = parity_sample(b, d, a, mode, N, K, rank)
+        res["parity"] = parity_sample(b, d, ar, a, mode, N, K, G_total, g0)
         if world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(b, a, mode, N, K)
 
-    units = G_total * ipg * a.steps
-    value = units / elapsed
     if rank == 0:
+        cfg_work = (f"config5: {G_total} groups ({a.scaling} scaling, {G} on rank 0) x {ipg} "
+                    f"instances x {N - 1} AcceptReplies + {B} cmds/instance, keys U[0,{a.keys}) "
+                    f"per group, mode {a.mode}")
         line = {
             "metric": "decided+applied instances/sec (tally + KV apply + RCCL watermark all-reduce)",
-            "value": value,
+            "value": n_decided * a.steps / elapsed,
             "unit": "instances/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": elapsed / a.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": a.scaling,
             "vs_baseline": None,
             "dtype": "int32/int64",
             "data": "synthetic (counter-based splitmix64, SURVEY §8(d) config 5)",
             "config": {
-                "workload": f"config5: {G} groups/GPU x {ipg} instances x {N - 1} AcceptReplies "
-                            f"+ {B} cmds/instance, keys U[0,{a.keys}) per group, mode {a.mode}",
-                "groups_total": G_total, "instances_per_step": G_total * ipg,
+                "workload": cfg_work,
+                "groups_total": G_total, "groups_per_rank": G, "instances_per_step": G_total * ipg,
                 "commands_per_step": G_total * ipg * B, "parallelism": f"groups block-sharded x{world}",
-                "collective": "RCCL all-reduce(max) of 2 x groups_total int32 watermarks per step",
+                "collective": ("one RCCL group per step: all-reduce(max) of 2 x groups_total int32 "
+                               "watermarks + all-reduce(sum) of 3 int64 step totals, "
+                               + ("on the compute stream" if a.no_overlap else
+                                  "on a second stream overlapping the next step's kernel")),
             },
+            "value_counts": "instances decided by the step (quorum crossings), all ranks",
             "roofline": {
                 "bound": "hbm", "kernel": "k_group_fast", "achieved": achieved_gbs,
                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved_gbs / PEAK_HBM_GBS,
-                "traffic": traffic, "alg_bytes_per_launch": alg,
+                "traffic": traffic_of(a.traffic_json, mode=a.mode, groups=G, kernel="k_group_fast"),
+                "alg_bytes_per_launch": alg,
                 "kernel_ms_avg": kern_avg_ms, "kernel_ms_min": float(np.min(kern_ms)),
+                "timing": "HIP events around each k_group_fast launch on the compute stream",
             },
             "decided_instances_per_step": n_decided,
-            "groups_with_commit_watermark": int(((own_c >= 0).sum())),
             "executed_instances_per_step": n_exec_inst,
             "executed_commands_per_step": n_exec_cmds,
+            "instances_processed_per_s": G_total * ipg * a.steps / elapsed,
+            "executed_instances_per_s": n_exec_inst * a.steps / elapsed,
+            "executed_commands_per_s": n_exec_cmds * a.steps / elapsed,
             "watermark_allreduce_ok": wm_ok,
             "gen_s": round(t_gen, 2),
+            "runtime": _lib.runtime_info(),
         }
         line.update(res)
         print(json.dumps(line), flush=True)
+    if comm != comp:
+        eng.stream_destroy(comm)
+    ar.close()
     eng.close()
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
 
 
-def _oracle_sub(b, g0, g1, ipg):
+R_TOTALS = 3  # mpx_step_totals_dev: decided instances, executed instances, executed commands
+
+
+def _oracle_sub(b, g0, g1, ipg, N):
     r0, r1 = int(b["grp_rec_off"][g0]), int(b["grp_rec_off"][g1])
     c0, c1 = int(b["cmd_off"][g0 * ipg]), int(b["cmd_off"][g1 * ipg])
     sub = dict(n_groups=g1 - g0, ipg=ipg, recs=b["recs"][r0:r1],
                grp_rec_off=(b["grp_rec_off"][g0:g1 + 1] - np.uint64(r0)),
                st_in=b["st_in"][g0 * ipg:g1 * ipg], committed_in=b["committed_in"][g0:g1],
-               executed_in=b["executed_in"][g0:g1], peer_in=b["peer_in"][g0 * 5:g1 * 5],
+               executed_in=b["executed_in"][g0:g1], peer_in=b["peer_in"][g0 * N:g1 * N],
                op=b["op"][c0:c1], key=b["key"][c0:c1], val=b["val"][c0:c1],
                cmd_off=(b["cmd_off"][g0 * ipg:g1 * ipg + 1] - np.uint32(c0)))
     return sub, (c0, c1)
 
 
-def parity_sample(b, d, a, mode, N, K, rank):
+def parity_sample(b, d, ar, a, mode, N, K, G_total, g0):
+    """every output of the first --parity-groups groups of the last timed step against the
+    oracle: instance states, decided counts, watermarks (after the all-reduce), peerCommits,
+    Execute results, conflicts and the group tables (count, keys, values)"""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_lib import Oracle  # CPU oracle: the checker, never the measured path
-    S = min(a.parity_groups, a.groups)
+    S = min(a.parity_groups, len(b["committed_in"]))
     ipg = a.ipg
-    sub, (c0, c1) = _oracle_sub(b, 0, S, ipg)
+    sub, (c0, c1) = _oracle_sub(b, 0, S, ipg, N)
     o = Oracle(N, mode, kv_per_group=K)
     # the timed steps started from the table the warm-up step produced
     w0 = o.group_step(sub)
     want = o.group_step(sub, w0["kv_cnt"], w0["kv_key"], w0["kv_val"])
-    ret = d["ret"][c0:c1].cpu().numpy()
-    conf = d["conf"][c0:c1].cpu().numpy()
-    G_total = a.groups * int(os.environ.get("WORLD_SIZE", "1"))
-    wm = d["wm"].cpu().numpy()
-    ok = (np.array_equal(ret, want["ret"]) and np.array_equal(conf, want["conf_prev"])
-          and np.array_equal(wm[:S], want["committed_out"])
-          and np.array_equal(wm[G_total:G_total + S], want["executed_out"])
-          and np.array_equal(d["kc1"][:S].cpu().numpy().astype(np.uint32), want["kv_cnt"]))
-    return {"groups_checked": S, "bit_exact": bool(ok)}
+    wm = ar.get(d["wm"][(a.steps - 1) & 1])
+    kc = ar.get(d["kc1"], S).astype(np.uint32)
+    kk = ar.get(d["kk1"], S * K)
+    kv = ar.get(d["kv1"], S * K)
+    checks = {
+        "st_out": np.array_equal(ar.get(_as(d["st_out"], np.int32), S * ipg * 4),
+                                 want["st_out"].view(np.int32).reshape(-1)),
+        "n_decided": np.array_equal(ar.get(d["nd"], S), want["n_decided"]),
+        "committed": np.array_equal(wm[g0:g0 + S], want["committed_out"]),
+        "executed": np.array_equal(wm[G_total + g0:G_total + g0 + S], want["executed_out"]),
+        "peer_commits": np.array_equal(ar.get(d["po"], S * N), want["peer_out"]),
+        "ret": np.array_equal(ar.get(d["ret"], c1 - c0, c0), want["ret"]),
+        "conf_prev": np.array_equal(ar.get(d["conf"], c1 - c0, c0), want["conf_prev"]),
+        "kv_cnt": np.array_equal(kc, want["kv_cnt"]),
+    }
+    tab = True
+    for g in range(S):
+        n = int(want["kv_cnt"][g])
+        tab &= np.array_equal(kk[g * K:g * K + n], want["kv_key"][g * K:g * K + n])
+        tab &= np.array_equal(kv[g * K:g * K + n], want["kv_val"][g * K:g * K + n])
+    checks["kv_key_val"] = bool(tab)
+    bad = [k for k, v in checks.items() if not v]
+    return {"groups_checked": S, "outputs": sorted(checks), "bit_exact": not bad,
+            "mismatch": bad}
+
+
+def _as(x, dtype):
+    """the same device buffer viewed with another element type"""
+    return DevArray(x.ptr, x.nbytes, dtype, (x.nbytes // np.dtype(dtype).itemsize,))
 
 
 def cpu_baseline(b, a, mode, N, K):
@@ -311,13 +414,14 @@ def cpu_baseline(b, a, mode, N, K):
     import oracle_lib as OL
     lib = OL.load()
     ipg = a.ipg
+    G = len(b["committed_in"])
 
     built = {}  # g_n -> (arrays kept alive, batch struct): inputs are never written
 
     def run(g_n, threads):
         if g_n in built:
             return lib.orc_bench_group_step(N, mode, C.byref(built[g_n][1]), K, threads) * 1e-9
-        sub, _ = _oracle_sub(b, 0, g_n, ipg)
+        sub, _ = _oracle_sub(b, 0, g_n, ipg, N)
         o = OL.Oracle(N, mode, kv_per_group=K)
         warm = o.group_step(sub)  # steady-state tables, as on the GPU
         m = len(sub["op"])
@@ -326,7 +430,7 @@ def cpu_baseline(b, a, mode, N, K):
                 np.zeros(g_n, np.int32), sub["peer_in"], np.zeros(g_n * N, np.int32), sub["op"],
                 sub["key"], sub["val"], sub["cmd_off"], None, np.zeros(m, np.int64), None,
                 warm["kv_cnt"], warm["kv_key"], warm["kv_val"], warm["kv_cnt"].copy(),
-                warm["kv_key"].copy(), warm["kv_val"].copy(), None]
+                warm["kv_key"].copy(), warm["kv_val"].copy(), None, None]
         arrs = [np.ascontiguousarray(x) if isinstance(x, np.ndarray) else x for x in arrs]
         gb = OL.group_batch_struct(arrs)
         built[g_n] = (arrs, gb)
@@ -334,11 +438,11 @@ def cpu_baseline(b, a, mode, N, K):
         return ns * 1e-9
 
     if a.cpu_sample_groups:
-        g_n = min(a.cpu_sample_groups, a.groups)
+        g_n = min(a.cpu_sample_groups, G)
     else:
-        t = run(min(2048, a.groups), 1)
-        per = t / min(2048, a.groups)
-        g_n = int(min(a.groups, max(2048, 15.0 / max(per, 1e-9))))
+        t = run(min(2048, G), 1)
+        per = t / min(2048, G)
+        g_n = int(min(G, max(2048, 15.0 / max(per, 1e-9))))
     secs, reps = 0.0, 0
     while secs < 10.0 and reps < 50:  # about 10 s of CPU work in total
         secs += run(g_n, 1)
@@ -347,221 +451,285 @@ def cpu_baseline(b, a, mode, N, K):
            "sample": f"first {g_n} groups of the same workload ({g_n * ipg} instances, "
                      f"{g_n * ipg * (N - 1)} replies, {g_n * ipg * a.cmds} commands) x {reps} "
                      f"reps, pointer-per-instance log + hash-map State, one thread, "
-                     f"{secs:.1f} s timed"}
-    # the same loop with the groups sharded over host threads (one per core, at
-    # most the box's CPU share of 16), reported beside the one-core reference-faithful figure
-    th = max(1, min(16, os.cpu_count() or 1))
+                     f"{secs:.1f} s timed (instances processed per second)"}
+    # the same loop with the groups sharded over the process's CPU share (its
+    # affinity set, capped by OMP_NUM_THREADS and 16), beside the one-core reference-faithful
+    # figure
+    th = host_cores()
     if th > 1:
-        g_s = min(a.groups, g_n * th)
+        g_s = min(G, g_n * th)
         ssecs, sreps = 0.0, 0
         while ssecs < 4.0 and sreps < 5:  # each rep also rebuilds the per-group maps (untimed)
             ssecs += run(g_s, th)
             sreps += 1
         out["sharded"] = {"value": g_s * ipg * sreps / ssecs, "unit": "instances/s",
-                          "cores": th, "sample": f"first {g_s} groups x {sreps} reps, groups "
-                                                 f"block-sharded over {th} threads"}
+                          "cores": th, "cores_probe": "len(os.sched_getaffinity(0)) capped by "
+                                                      "OMP_NUM_THREADS and 16",
+                          "sample": f"first {g_s} groups x {sreps} reps, groups block-sharded "
+                                    f"over {th} threads"}
     return out
 
 
-# ============================ single-kernel configurations (2, 3, 4) ============================
-def _timed(stream, eng, steps, warmup, launch, before=None):
-    """warmup + steps launches on the engine stream; HIP events around each launch (the stream
-    the kernels run on); wall clock around the timed loop. Returns (wall_s, [ms per launch])."""
-    import torch
+# ============================ single-kernel configurations ===================================
+def _timed(eng, steps, warmup, launch, before=None):
+    """warmup + steps launches on the engine stream; HIP events (engine runtime) around each
+    launch on the stream the kernels run on; wall clock around the timed loop.
+    Returns (wall_s, [ms per launch])."""
     for _ in range(warmup):
         if before:
             before()
         launch()
     eng.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(steps)]
-    torch.cuda.synchronize()
+    evs = [(eng.event_create(), eng.event_create()) for _ in range(steps)]
     t0 = time.perf_counter()
     for e0, e1 in evs:
         if before:
             before()
-        e0.record(stream)
+        eng.event_record(e0)
         launch()
-        e1.record(stream)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
+        eng.event_record(e1)
     eng.synchronize()
-    return wall, [e0.elapsed_time(e1) for e0, e1 in evs]
+    wall = time.perf_counter() - t0
+    ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in evs]
+    for e0, e1 in evs:
+        eng.event_destroy(e0)
+        eng.event_destroy(e1)
+    return wall, ms
 
 
-def kernel_bench(a):
-    """BASELINE.json configs 2-4 on one GPU (replicas only: under torchrun every rank runs its
-    own copy of the workload and `value` sums the ranks)."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    import torch.distributed as dist
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+def _cpu_loop(fn, budget=10.0, max_reps=20):
+    secs, reps = 0.0, 0
+    while secs < budget and reps < max_reps:
+        secs += fn()
+        reps += 1
+    return secs, reps
+
+
+def kernel_bench(a, rk):
+    """BASELINE.json configs 2-4 and the §8(f) rows on one GPU (replicas only: under torchrun
+    every rank runs its own copy of the workload and `value` sums the ranks)."""
+    world, rank = rk.world, rk.rank
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as OL  # CPU oracle: the checker and the CPU baseline, never the measured path
     N = 5
     mode = R.MODE_MIN if a.mode == "min" else R.MODE_CLASSIC
-    eng = Engine(local, n_replicas=N, mode=mode, kv_capacity=a.kv_capacity or 2 * a.apply_keys)
-    stream = torch.cuda.ExternalStream(eng.stream, device=dev)
-    torch.cuda.set_stream(stream)
-
-    def dt(x):
-        arr = np.ascontiguousarray(x)
-        if arr.dtype.names:
-            arr = arr.view(np.uint8)
-        return torch.from_numpy(arr).to(dev)
+    eng = Engine(rk.local, n_replicas=N, mode=mode, kv_capacity=a.kv_capacity or 2 * a.apply_keys)
+    ar = Arena(eng)
+    put, get, sync = ar.put, ar.get, eng.synchronize
+    lib = OL.load()
+    traffic = None
 
     t_gen = time.time()
     if a.workload == "tally":
         I = a.instances
         recs, st = synth.accept_replies(I, N, 0.7, seed=42)
         n = len(recs)
-        d_recs, d_st = dt(recs), dt(st)
-        d_out = torch.empty_like(d_st)
-        d_scal = torch.empty(1 + N, dtype=torch.int32, device=dev)
-        scal0 = torch.tensor([-1] + [0] * N, dtype=torch.int32, device=dev)
-        d_dec = torch.empty(I, dtype=torch.uint8, device=dev)
+        d_recs, d_st = put(recs), put(st)
+        d_out = ar.empty(len(st), R.INST_STATE)
+        d_scal = ar.empty(1 + N, np.int32)
+        scal0 = put(np.array([-1] + [0] * N, np.int32))
+        d_dec = ar.empty(I, np.uint8)
         t_gen = time.time() - t_gen
-        wall, ms = _timed(stream, eng, a.steps, a.warmup,
-                          lambda: eng.accept_tally_dev(d_recs.data_ptr(), n, d_st.data_ptr(),
-                                                       d_out.data_ptr(), I, 0, d_scal.data_ptr(),
-                                                       d_dec.data_ptr(), eng.stream),
-                          before=lambda: d_scal.copy_(scal0))
-        alg = n * 16 + I * 16 * 2 + I  # replies + state in/out + decided flags
+        wall, ms = _timed(eng, a.steps, a.warmup,
+                          lambda: eng.accept_tally_dev(d_recs.ptr, n, d_st.ptr, d_out.ptr, I, 0,
+                                                       d_scal.ptr, d_dec.ptr, eng.stream),
+                          before=lambda: eng.memcpy(d_scal.ptr, scal0.ptr, d_scal.nbytes, D2D))
+        alg = n * 16 + I * 16 * 2  # replies + state in/out (SURVEY 8(d) config 2: 96 B/instance)
         units, unit = I, "instances/s"
         kernel = f"k_accept_tally<{a.mode}>"
         o = OL.Oracle(N, mode)
         w_st, w_cu, w_pc, w_dec = o.accept_tally(recs, st, 0, -1)
-        got_st = d_out.cpu().numpy().view(R.INST_STATE)
-        sc = d_scal.cpu().numpy()
+        got_st = get(d_out)
+        sc = get(d_scal)
         bit_exact = bool(np.array_equal(got_st.view(np.int32), w_st.view(np.int32))
                          and sc[0] == w_cu and np.array_equal(sc[1:], w_pc)
-                         and np.array_equal(d_dec.cpu().numpy(), w_dec))
+                         and np.array_equal(get(d_dec), w_dec))
         parity = {"instances_checked": I, "bit_exact": bit_exact}
-        lib = OL.load()
-        secs, reps = 0.0, 0
-        while secs < 10.0 and reps < 20:
+
+        def cpu_once():
             s2 = st.copy()
             cu = C.c_int32(-1)
             pc = np.zeros(N, np.int32)
-            secs += lib.orc_bench_accept(N, mode, recs.ctypes.data, n, s2.ctypes.data, I, 0,
-                                         C.byref(cu), pc.ctypes.data) * 1e-9
-            reps += 1
+            return lib.orc_bench_accept(N, mode, recs.ctypes.data, n, s2.ctypes.data, I, 0,
+                                        C.byref(cu), pc.ctypes.data) * 1e-9
+        secs, reps = _cpu_loop(cpu_once)
         cpu = {"value": I * reps / secs, "unit": unit, "cores": 1, "kind": "port",
                "sample": f"the full workload ({I} instances, {n} replies) x {reps}, "
                          f"pointer-per-instance log, one thread, {secs:.1f} s timed"}
         workload = f"config2: {I} instances x {N - 1} AcceptReplies, N={N}, p_ok=0.7, mode {a.mode}"
+        traffic = traffic_of(a.traffic_json, kernel=kernel, instances=I)
     elif a.workload == "prepare":
         I = a.instances
         recs, st = synth.prepare_replies(I, N, 0.8, seed=43)
         n = len(recs)
-        d_recs, d_st = dt(recs), dt(st)
-        d_out = torch.empty_like(d_st)
-        d_db = torch.empty(1, dtype=torch.int32, device=dev)
-        db0 = torch.tensor([-1], dtype=torch.int32, device=dev)
-        d_prep = torch.empty(I, dtype=torch.uint8, device=dev)
+        d_recs, d_st = put(recs), put(st)
+        d_out = ar.empty(len(st), R.PREP_STATE)
+        d_db = ar.empty(1, np.int32)
+        db0 = put(np.array([-1], np.int32))
+        d_prep = ar.empty(I, np.uint8)
         t_gen = time.time() - t_gen
-        wall, ms = _timed(stream, eng, a.steps, a.warmup,
-                          lambda: eng.prepare_select_dev(d_recs.data_ptr(), n, d_st.data_ptr(),
-                                                         d_out.data_ptr(), I, 0, d_db.data_ptr(),
-                                                         d_prep.data_ptr(), eng.stream),
-                          before=lambda: d_db.copy_(db0))
-        alg = n * 16 + I * 32 * 2 + I
+        wall, ms = _timed(eng, a.steps, a.warmup,
+                          lambda: eng.prepare_select_dev(d_recs.ptr, n, d_st.ptr, d_out.ptr, I, 0,
+                                                         d_db.ptr, d_prep.ptr, eng.stream),
+                          before=lambda: eng.memcpy(d_db.ptr, db0.ptr, 4, D2D))
+        alg = n * 16 + I * 32 * 2  # SURVEY 8(d) config 3: 128 B/instance
         units, unit = I, "instances/s"
         kernel = "k_prepare_classic"
         o = OL.Oracle(N, R.MODE_CLASSIC)
         t0 = time.perf_counter()
         w_st, w_db, w_prep = o.prepare_select(recs, st, 0, -1)
         t_orc = time.perf_counter() - t0
-        got = d_out.cpu().numpy().view(R.PREP_STATE)
-        bit_exact = bool(np.array_equal(got.view(np.int32), w_st.view(np.int32))
-                         and int(d_db.item()) == w_db
-                         and np.array_equal(d_prep.cpu().numpy(), w_prep))
+        bit_exact = bool(np.array_equal(get(d_out).view(np.int32), w_st.view(np.int32))
+                         and int(get(d_db)[0]) == w_db and np.array_equal(get(d_prep), w_prep))
         parity = {"instances_checked": I, "bit_exact": bit_exact}
-        reps, secs = 1, t_orc
-        while secs < 10.0 and reps < 20:
+
+        def cpu_once():
             t0 = time.perf_counter()
             o.prepare_select(recs, st, 0, -1)
-            secs += time.perf_counter() - t0
-            reps += 1
+            return time.perf_counter() - t0
+        secs, reps = _cpu_loop(cpu_once, 10.0 - t_orc)
+        secs, reps = secs + t_orc, reps + 1
         cpu = {"value": I * reps / secs, "unit": unit, "cores": 1, "kind": "port",
                "sample": f"the full workload ({I} instances, {n} replies) x {reps} through the "
                          f"oracle's sequential handler loop (incl. its numpy copy-in/out), "
                          f"one thread, {secs:.1f} s timed"}
         workload = f"config3: {I} instances x {N - 1} PrepareReplies, N={N}, p_ok=0.8, random ballots"
+    elif a.workload == "prepare_min":
+        Gp = a.prep_groups
+        recs, off, gst = synth.prepare_replies_min(Gp, N, seed=46)
+        n = len(recs)
+        pc = np.zeros(Gp * N, np.int32)
+        d_recs, d_off, d_gst0, d_pc0 = put(recs), put(off), put(gst), put(pc)
+        d_gst = ar.empty(Gp, R.GROUP_PREP_STATE)
+        d_pc = ar.empty(Gp * N, np.int32)
+        d_eff = ar.empty(n, R.PREPARE_EFFECT)
+        t_gen = time.time() - t_gen
+
+        def reset():  # the bookkeeping is updated in place: every launch starts from the input
+            eng.memcpy(d_gst.ptr, d_gst0.ptr, d_gst.nbytes, D2D)
+            eng.memcpy(d_pc.ptr, d_pc0.ptr, d_pc.nbytes, D2D)
+        wall, ms = _timed(eng, a.steps, a.warmup,
+                          lambda: eng.prepare_select_min_dev(d_recs.ptr, n, d_off.ptr, d_gst.ptr,
+                                                             Gp, d_pc.ptr, d_eff.ptr, eng.stream),
+                          before=reset)
+        # replies + offsets in, group state in/out, peerCommits in/out, one effect per reply
+        alg = n * 24 + (Gp + 1) * 8 + Gp * 32 * 2 + Gp * N * 4 * 2 + n * 8
+        units, unit = Gp, "groups/s"
+        kernel = "k_prepare_min"
+        o = OL.Oracle(N, R.MODE_MIN)
+        w_gst, w_pc, w_eff = o.prepare_select_min(recs, off, gst, pc)
+        bit_exact = bool(np.array_equal(get(d_gst).view(np.int32), w_gst.view(np.int32))
+                         and np.array_equal(get(d_pc), w_pc)
+                         and np.array_equal(get(d_eff).view(np.int32), w_eff.view(np.int32)))
+        parity = {"groups_checked": Gp, "bit_exact": bit_exact}
+
+        def cpu_once():
+            t0 = time.perf_counter()
+            o.prepare_select_min(recs, off, gst, pc)
+            return time.perf_counter() - t0
+        secs, reps = _cpu_loop(cpu_once, 10.0, 200)
+        cpu = {"value": Gp * reps / secs, "unit": unit, "cores": 1, "kind": "port",
+               "sample": f"the full workload ({Gp} groups, {n} replies) x {reps} through the "
+                         f"oracle's handlePrepareReply loop (incl. numpy copy-in/out), one "
+                         f"thread, {secs:.1f} s timed"}
+        workload = (f"config3 (MIN): {Gp} groups x {N - 1} PrepareReplies, one PrepareBookkeeping "
+                    f"per group (latency-bound: reported, not roofline-graded)")
     elif a.workload == "apply":
         M, K = a.commands, a.apply_keys
         op, key, val = synth.commands(M, K, 0.5, a.dist, seed=44)
-        d_op, d_key, d_val = dt(op), dt(key), dt(val)
-        d_ret = torch.empty(M, dtype=torch.int64, device=dev)
-        d_conf = torch.empty(M, dtype=torch.uint8, device=dev)
+        d_op, d_key, d_val = put(op), put(key), put(val)
+        d_ret = ar.empty(M, np.int64)
+        d_conf = ar.empty(M, np.uint8)
         t_gen = time.time() - t_gen
-        launch = lambda: eng.apply_dev(d_op.data_ptr(), d_key.data_ptr(), d_val.data_ptr(), M,  # noqa: E731
-                                       d_ret.data_ptr(), d_conf.data_ptr(), eng.stream)
+        launch = lambda: eng.apply_dev(d_op.ptr, d_key.ptr, d_val.ptr, M, d_ret.ptr,  # noqa: E731
+                                       d_conf.ptr, eng.stream)
         eng.apply_reserve(M)
         launch()  # the table holds every key from here on: every timed call does the same work
-        eng.synchronize()
-        wall, ms = _timed(stream, eng, a.steps, a.warmup, launch)
+        sync()
+        wall, ms = _timed(eng, a.steps, a.warmup, launch)
         n_keys = eng.kv_size()
         alg = M * (17 + 9) + n_keys * 16 * 2  # commands in, ret+conf out, table read + written
         units, unit = M, "commands/s"
-        kernel = "mpx_apply pipeline (insert, lookup, radix sort, mark, scan, finish, commit)"
+        kernel = "mpx_apply pipeline"
         o = OL.Oracle(N, mode)
         o.apply(op, key, val)
         w_ret, w_conf = o.apply(op, key, val)
         wk, wv = o.kv_export()
         order = np.argsort(wk, kind="stable")
         gk, gv = eng.kv_export()
-        bit_exact = bool(np.array_equal(d_ret.cpu().numpy(), w_ret)
-                         and np.array_equal(d_conf.cpu().numpy(), w_conf)
+        bit_exact = bool(np.array_equal(get(d_ret), w_ret) and np.array_equal(get(d_conf), w_conf)
                          and np.array_equal(gk, wk[order]) and np.array_equal(gv, wv[order]))
         parity = {"commands_checked": M, "bit_exact": bit_exact}
-        lib = OL.load()
         ret = np.zeros(M, np.int64)
         k0, v0 = np.ascontiguousarray(wk), np.ascontiguousarray(wv)
-        secs, reps = 0.0, 0
-        while secs < 10.0 and reps < 20:
-            secs += lib.orc_bench_apply(k0.ctypes.data, v0.ctypes.data, len(k0), op.ctypes.data,
-                                        key.ctypes.data, val.ctypes.data, M, ret.ctypes.data) * 1e-9
-            reps += 1
+        secs, reps = _cpu_loop(lambda: lib.orc_bench_apply(
+            k0.ctypes.data, v0.ctypes.data, len(k0), op.ctypes.data, key.ctypes.data,
+            val.ctypes.data, M, ret.ctypes.data) * 1e-9)
         cpu = {"value": M * reps / secs, "unit": unit, "cores": 1, "kind": "port",
                "sample": f"the full workload ({M} commands over {K} keys, {a.dist}) x {reps}, "
                          f"Execute per command on an unordered_map, one thread, {secs:.1f} s timed"}
         workload = f"config4: {M} PUT/GET (p_put=0.5) over {K} keys, {a.dist}"
+        traffic = traffic_of(a.traffic_json, kernel=kernel, commands=M, dist=a.dist)
+    elif a.workload == "conflict":
+        M, K, Bc = a.commands, a.apply_keys, 4
+        op, key, _ = synth.commands(M, K, 0.5, a.dist, seed=44)
+        n_inst = M // Bc
+        off = (np.arange(n_inst + 1, dtype=np.uint64) * np.uint64(Bc))
+        d_op, d_key, d_off = put(op), put(key), put(off)
+        d_out = ar.empty(max(n_inst - 1, 1), np.uint8)
+        t_gen = time.time() - t_gen
+        wall, ms = _timed(eng, a.steps, a.warmup,
+                          lambda: eng.conflict_batch_dev(d_op.ptr, d_key.ptr, d_off.ptr, n_inst,
+                                                         d_out.ptr, eng.stream))
+        # every command is read by the pairs it belongs to (twice), offsets once, one flag out
+        alg = M * 9 + (n_inst + 1) * 8 + (n_inst - 1)
+        units, unit = n_inst - 1, "instance pairs/s"
+        kernel = "k_conflict_batch"
+        o = OL.Oracle(N, mode)
+        want = o.conflict_batch(op, key, off)
+        bit_exact = bool(np.array_equal(get(d_out, n_inst - 1), want))
+        parity = {"pairs_checked": n_inst - 1, "bit_exact": bit_exact}
+        cout = np.zeros(max(n_inst - 1, 1), np.uint8)
+
+        def cpu_once():
+            t0 = time.perf_counter()
+            lib.orc_conflict_batch(op.ctypes.data, key.ctypes.data, off.ctypes.data, n_inst,
+                                   cout.ctypes.data)
+            return time.perf_counter() - t0
+        secs, reps = _cpu_loop(cpu_once)
+        cpu = {"value": (n_inst - 1) * reps / secs, "unit": unit, "cores": 1, "kind": "port",
+               "sample": f"the full run ({n_inst} instances of {Bc} commands) x {reps}, the "
+                         f"nested ConflictBatch loop per pair, one thread, {secs:.1f} s timed"}
+        workload = (f"conflict: ConflictBatch(inst i, inst i+1) over {n_inst} instances of {Bc} "
+                    f"config-4 commands ({a.dist} keys over {K})")
     elif a.workload == "fanout":
         M, Cn = a.commands, a.clients
         recs = synth.replies(M, Cn, seed=55)
-        d_recs = dt(recs)
-        d_out = torch.empty(M * R.PROPOSE_REPLY_BYTES, dtype=torch.uint8, device=dev)
-        d_off = torch.empty(Cn + 1, dtype=torch.int64, device=dev)
+        d_recs = put(recs)
+        d_out = ar.empty(M * R.PROPOSE_REPLY_BYTES, np.uint8)
+        d_off = ar.empty(Cn + 1, np.uint64)
         eng.encode_replies_reserve(M)
         t_gen = time.time() - t_gen
-        wall, ms = _timed(stream, eng, a.steps, a.warmup,
-                          lambda: eng.encode_replies_dev(d_recs.data_ptr(), M, Cn, 1, 0,
-                                                         d_out.data_ptr(), d_off.data_ptr(),
-                                                         eng.stream))
+        wall, ms = _timed(eng, a.steps, a.warmup,
+                          lambda: eng.encode_replies_dev(d_recs.ptr, M, Cn, 1, 0, d_out.ptr,
+                                                         d_off.ptr, eng.stream))
         alg = M * (24 + R.PROPOSE_REPLY_BYTES) + (Cn + 1) * 8  # records in, wire bytes out
         units, unit = M, "replies/s"
-        kernel = "mpx_encode_replies pipeline (client keys, radix sort, gather + encode)"
+        kernel = "mpx_encode_replies pipeline"
         o = OL.Oracle(N, mode)
         w_out, w_off = o.encode_replies(recs, Cn, 1, 0)
-        bit_exact = bool(d_out.cpu().numpy().tobytes() == w_out.tobytes()
-                         and np.array_equal(d_off.cpu().numpy().view(np.uint64), w_off))
+        bit_exact = bool(get(d_out).tobytes() == w_out.tobytes()
+                         and np.array_equal(get(d_off), w_off))
         parity = {"replies_checked": M, "bit_exact": bit_exact}
-        lib = OL.load()
         cout = np.zeros(M * R.PROPOSE_REPLY_BYTES, np.uint8)
         coff = np.zeros(Cn + 1, np.uint64)
-        secs, reps = 0.0, 0
-        while secs < 10.0 and reps < 20:
+
+        def cpu_once():
             t0 = time.perf_counter()
             lib.orc_encode_replies(recs.ctypes.data, M, Cn, 1, 0, cout.ctypes.data,
                                    coff.ctypes.data)
-            secs += time.perf_counter() - t0
-            reps += 1
+            return time.perf_counter() - t0
+        secs, reps = _cpu_loop(cpu_once)
         cpu = {"value": M * reps / secs, "unit": unit, "cores": 1, "kind": "port",
                "sample": f"the full batch ({M} replies over {Cn} connections) x {reps}, one "
                          f"Marshal per reply into per-connection buffers, one thread, "
@@ -572,38 +740,36 @@ def kernel_bench(a):
         fmt = R.LOG_CATCHUP if a.log_format == "catchup" else R.LOG_DURABLE
         recs, coff, op, key, val = synth.log_records(I, 4, seed=58)
         M = len(op)
-        d_recs, d_off, d_op, d_key, d_val = dt(recs), dt(coff), dt(op), dt(key), dt(val)
+        d_recs, d_off, d_op, d_key, d_val = put(recs), put(coff), put(op), put(key), put(val)
         bound = eng.lib.mpx_encode_log_bound(I, M)
-        d_out = torch.empty(bound, dtype=torch.uint8, device=dev)
-        d_ro = torch.empty(I + 1, dtype=torch.int64, device=dev)
+        d_out = ar.empty(bound, np.uint8)
+        d_ro = ar.empty(I + 1, np.uint64)
         eng.encode_log_reserve(I, M)
         t_gen = time.time() - t_gen
-        wall, ms = _timed(stream, eng, a.steps, a.warmup,
-                          lambda: eng.encode_log_dev(fmt, d_recs.data_ptr(), I, d_off.data_ptr(),
-                                                     d_op.data_ptr(), d_key.data_ptr(),
-                                                     d_val.data_ptr(), M, d_out.data_ptr(),
-                                                     d_ro.data_ptr(), eng.stream))
+        wall, ms = _timed(eng, a.steps, a.warmup,
+                          lambda: eng.encode_log_dev(fmt, d_recs.ptr, I, d_off.ptr, d_op.ptr,
+                                                     d_key.ptr, d_val.ptr, M, d_out.ptr, d_ro.ptr,
+                                                     eng.stream))
         o = OL.Oracle(N, mode)
         w_out, w_ro = o.encode_log(fmt, recs, coff, op, key, val)
         total = int(w_ro[-1])
         # records + offsets + commands in, the encoding + record offsets out
         alg = I * (16 + 8) + M * 17 + total + (I + 1) * 8
         units, unit = I, "instances/s"
-        kernel = "mpx_encode_log pipeline (record sizes, scan, output-parallel emit)"
-        bit_exact = bool(np.array_equal(d_ro.cpu().numpy().view(np.uint64), w_ro)
-                         and d_out[:total].cpu().numpy().tobytes() == w_out.tobytes())
+        kernel = "mpx_encode_log pipeline"
+        bit_exact = bool(np.array_equal(get(d_ro), w_ro)
+                         and get(d_out, total).tobytes() == w_out.tobytes())
         parity = {"instances_checked": I, "bytes": total, "bit_exact": bit_exact}
-        lib = OL.load()
         cout = np.zeros(total, np.uint8)
         cro = np.zeros(I + 1, np.uint64)
-        secs, reps = 0.0, 0
-        while secs < 10.0 and reps < 20:
+
+        def cpu_once():
             t0 = time.perf_counter()
             lib.orc_encode_log(fmt, recs.ctypes.data, I, coff.ctypes.data, op.ctypes.data,
                                key.ctypes.data, val.ctypes.data, cout.ctypes.data, total,
                                cro.ctypes.data)
-            secs += time.perf_counter() - t0
-            reps += 1
+            return time.perf_counter() - t0
+        secs, reps = _cpu_loop(cpu_once)
         cpu = {"value": I * reps / secs, "unit": unit, "cores": 1, "kind": "port",
                "sample": f"the full run ({I} instances, {M} commands, {total} bytes) x {reps}, "
                          f"one Marshal per instance and command, one thread, {secs:.1f} s timed"}
@@ -612,51 +778,50 @@ def kernel_bench(a):
         I = a.instances
         recs, coff, op, key, val = synth.log_records(I, 1, seed=59)
         recs = recs.copy()
-        recs["inst_no"] = np.random.default_rng(60).permutation(I).astype(np.int32)
+        rng = np.random.default_rng(60)
+        recs["inst_no"] = (rng.integers(0, I // 2, I) if a.replay_dups else rng.permutation(I)
+                           ).astype(np.int32)
         o = OL.Oracle(N, mode)
         log, _ = o.encode_log(R.LOG_DURABLE, recs, coff, op, key, val)
         L = len(log)
-        d_log = dt(log)
-        d_recs = torch.empty(I * 16, dtype=torch.uint8, device=dev)
-        d_op = torch.empty(I, dtype=torch.uint8, device=dev)
-        d_key = torch.empty(I, dtype=torch.int64, device=dev)
-        d_val = torch.empty(I, dtype=torch.int64, device=dev)
-        d_last = torch.full((I,), -1, dtype=torch.int32, device=dev)
-        d_sc = torch.tensor([0, -1], dtype=torch.int32, device=dev)
-        torch.cuda.synchronize()
+        d_log = put(log)
+        d_recs = ar.empty(I, R.LOG_REC)
+        d_op = ar.empty(I, np.uint8)
+        d_key = ar.empty(I, np.int64)
+        d_val = ar.empty(I, np.int64)
+        d_last = ar.full(I, np.int32, 0xFF)
+        d_sc = put(np.array([0, -1], np.int32))
         t_gen = time.time() - t_gen
         # every output is idempotent under repetition (slots and watermarks are maxima)
-        wall, ms = _timed(stream, eng, a.steps, a.warmup,
-                          lambda: eng.replay_durable_dev(d_log.data_ptr(), L, I, d_recs.data_ptr(),
-                                                         d_op.data_ptr(), d_key.data_ptr(),
-                                                         d_val.data_ptr(), d_last.data_ptr(),
-                                                         d_sc.data_ptr(), eng.stream))
+        wall, ms = _timed(eng, a.steps, a.warmup,
+                          lambda: eng.replay_durable_dev(d_log.ptr, L, I, d_recs.ptr, d_op.ptr,
+                                                         d_key.ptr, d_val.ptr, d_last.ptr,
+                                                         d_sc.ptr, eng.stream))
         w = o.replay_durable(log, I)
         # log read once; records, op, key, val written once; one 4-byte slot per record
         alg = L + I * (16 + 1 + 8 + 8) + I * 4
         units, unit = I, "records/s"
         kernel = "k_replay_durable"
-        bit_exact = bool(np.array_equal(d_recs.cpu().numpy().view(R.LOG_REC), w[0])
-                         and np.array_equal(d_op.cpu().numpy(), w[1])
-                         and np.array_equal(d_key.cpu().numpy(), w[2])
-                         and np.array_equal(d_val.cpu().numpy(), w[3])
-                         and np.array_equal(d_last.cpu().numpy(), w[4])
-                         and d_sc.cpu().tolist() == [w[5], w[6]])
+        bit_exact = bool(np.array_equal(get(d_recs), w[0]) and np.array_equal(get(d_op), w[1])
+                         and np.array_equal(get(d_key), w[2]) and np.array_equal(get(d_val), w[3])
+                         and np.array_equal(get(d_last), w[4])
+                         and get(d_sc).tolist() == [w[5], w[6]])
         parity = {"records_checked": I, "bytes": L, "bit_exact": bit_exact}
-        lib = OL.load()
         c = [np.zeros(I, R.LOG_REC), np.zeros(I, np.uint8), np.zeros(I, np.int64),
              np.zeros(I, np.int64), np.zeros(I, np.int32), np.zeros(2, np.int32)]
-        secs, reps = 0.0, 0
-        while secs < 10.0 and reps < 20:
+
+        def cpu_once():
+            c[4][:] = -1
             c[5][:] = (0, -1)
             t0 = time.perf_counter()
-            lib.orc_replay_durable(log.ctypes.data, L, I, *[x.ctypes.data for x in c])
-            secs += time.perf_counter() - t0
-            reps += 1
+            lib.orc_replay_durable(log.ctypes.data, L, I, 0, *[x.ctypes.data for x in c])
+            return time.perf_counter() - t0
+        secs, reps = _cpu_loop(cpu_once)
         cpu = {"value": I * reps / secs, "unit": unit, "cores": 1, "kind": "port",
                "sample": f"the full log ({I} records, {L} bytes) x {reps} through the oracle's "
                          f"getDataFromStableStore loop, one thread, {secs:.1f} s timed"}
-        workload = f"replay (durable): {I} records x 1 command, {L} bytes, instNo a permutation"
+        workload = (f"replay (durable): {I} records x 1 command, {L} bytes, instNo "
+                    + ("drawn with repeats over I/2 slots" if a.replay_dups else "a permutation"))
     else:  # decode
         I = a.instances
         recs, _ = synth.accept_replies(I, N, 0.7, seed=42)
@@ -665,46 +830,40 @@ def kernel_bench(a):
         o = OL.Oracle(N, mode)
         w_ar, w_oth, w_res = o.decode_peer_stream(buf)
         n_ar, n_oth = int(w_res["n_accept_replies"]), int(w_res["n_other"])
-        d_buf = dt(buf)
-        d_ar = torch.empty(n_ar * 16, dtype=torch.uint8, device=dev)
-        d_oth = torch.empty(max(n_oth, 1) * 8, dtype=torch.uint8, device=dev)
-        d_res = torch.empty(32, dtype=torch.uint8, device=dev)
+        d_buf = put(buf)
+        d_ar = ar.empty(n_ar, R.ACCEPT_REPLY)
+        d_oth = ar.empty(max(n_oth, 1), R.PEER_FRAME)
+        d_res = ar.empty(1, R.DECODE_RESULT)
         eng.decode_reserve(L)
         t_gen = time.time() - t_gen
-        wall, ms = _timed(stream, eng, a.steps, a.warmup,
-                          lambda: eng.decode_peer_stream_dev(d_buf.data_ptr(), L, d_ar.data_ptr(),
-                                                             n_ar, d_oth.data_ptr(), n_oth,
-                                                             d_res.data_ptr(), eng.stream))
+        wall, ms = _timed(eng, a.steps, a.warmup,
+                          lambda: eng.decode_peer_stream_dev(d_buf.ptr, L, d_ar.ptr, n_ar,
+                                                             d_oth.ptr, n_oth, d_res.ptr,
+                                                             eng.stream))
         alg = L + n_ar * 16 + n_oth * 8  # stream read once, records written once
         units, unit = n_ar, "AcceptReplies/s"
-        kernel = ("mpx_decode_peer_stream pipeline (tile maps, group maps, walk, tile entries, "
-                  "emit)")
-        got_res = d_res.cpu().numpy().view(R.DECODE_RESULT)[0]
-        bit_exact = bool(got_res.tobytes() == w_res.tobytes()
-                         and d_ar.cpu().numpy().tobytes() == w_ar.tobytes()
-                         and d_oth.cpu().numpy()[:n_oth * 8].tobytes() == w_oth.tobytes())
+        kernel = "mpx_decode_peer_stream pipeline"
+        bit_exact = bool(get(d_res).tobytes() == w_res.tobytes()
+                         and get(d_ar).tobytes() == w_ar.tobytes()
+                         and get(d_oth, n_oth).tobytes() == w_oth.tobytes())
         parity = {"frames_checked": n_ar + n_oth, "bytes": L, "bit_exact": bit_exact}
-        lib = OL.load()
         car = np.zeros(n_ar, R.ACCEPT_REPLY)
         coth = np.zeros(max(n_oth, 1), R.PEER_FRAME)
         cres = np.zeros(1, R.DECODE_RESULT)
-        secs, reps = 0.0, 0
-        while secs < 10.0 and reps < 20:
+
+        def cpu_once():
             t0 = time.perf_counter()
-            lib.orc_decode_peer_stream(buf.ctypes.data, L, car.ctypes.data, n_ar, coth.ctypes.data,
-                                       n_oth, cres.ctypes.data)
-            secs += time.perf_counter() - t0
-            reps += 1
+            lib.orc_decode_peer_stream(buf.ctypes.data, L, car.ctypes.data, n_ar,
+                                       coth.ctypes.data, n_oth, cres.ctypes.data)
+            return time.perf_counter() - t0
+        secs, reps = _cpu_loop(cpu_once)
         cpu = {"value": n_ar * reps / secs, "unit": unit, "cores": 1, "kind": "port",
                "sample": f"the full stream ({L} bytes, {n_ar} AcceptReplies, {n_oth} Beacons) "
                          f"x {reps} through the oracle's replicaListener loop, one thread, "
                          f"{secs:.1f} s timed"}
         workload = (f"decode: {n_ar} AcceptReply frames (config-2 replies, {I} instances) + "
                     f"{n_oth} Beacons, {L} bytes")
-    if world > 1:
-        tt = torch.tensor([wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        wall = float(tt.item())
+    wall = rk.max(wall)
     kern_avg = float(np.mean(ms))
     achieved = alg / (kern_avg * 1e-3) / 1e9
     if rank == 0:
@@ -716,17 +875,15 @@ def kernel_bench(a):
             "config": {"workload": workload, "parallelism": f"replicas x{world}"},
             "roofline": {"bound": "hbm", "kernel": kernel, "achieved": achieved,
                          "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
-                         "traffic": None, "alg_bytes_per_launch": alg, "kernel_ms_avg": kern_avg,
-                         "kernel_ms_min": float(np.min(ms))},
-            "gen_s": round(t_gen, 2), "parity": parity,
+                         "traffic": traffic, "alg_bytes_per_launch": alg,
+                         "kernel_ms_avg": kern_avg, "kernel_ms_min": float(np.min(ms))},
+            "gen_s": round(t_gen, 2), "parity": parity, "runtime": _lib.runtime_info(),
         }
         if world == 1 and not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)
+    ar.close()
     eng.close()
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -40,8 +40,11 @@
  *     MPX_E_* code; mpx_last_error() explains the last failure of a handle.
  *   - records are processed with SEQUENTIAL semantics in array order: the results equal those of
  *     calling the reference handler once per record, in array order. Records must be grouped by
- *     instance (all replies for one instance contiguous); within a group, slot order = arrival
- *     order. MIN watermarks are "last assignment wins" in array order.
+ *     instance (all replies for one instance contiguous) and the groups must appear in ASCENDING
+ *     instance order (what the Go shim's stable sort of a drained batch produces); any other
+ *     order is rejected with MPX_E_INVAL. Within a group, slot order = arrival order. MIN
+ *     watermarks are "last assignment wins" in array order, which under ascending order is the
+ *     highest instance that makes an assignment.
  *   - host-pointer entry points are synchronous: results are in the caller's buffers on return.
  *     *_dev entry points take device pointers and a hipStream_t (passed as void*, NULL = the
  *     engine's stream) and are asynchronous; they never allocate or synchronise, so they can be
@@ -60,7 +63,7 @@
 extern "C" {
 #endif
 
-#define MPX_ABI_VERSION 1
+#define MPX_ABI_VERSION 2
 
 /* ---- error codes ---------------------------------------------------------------------- */
 #define MPX_OK 0
@@ -263,6 +266,10 @@ int mpx_kv_clear(mpx_engine* eng);
  * instance i = commands [inst_off[i], inst_off[i+1]). out has n_inst-1 entries.            */
 int mpx_conflict_batch(mpx_engine* eng, const uint8_t* op, const int64_t* key,
                        const uint64_t* inst_off, size_t n_inst, uint8_t* out);
+/* device form; d_inst_off is trusted (n_inst+1 non-decreasing offsets starting at 0)       */
+int mpx_conflict_batch_dev(mpx_engine* eng, const uint8_t* d_op, const int64_t* d_key,
+                           const uint64_t* d_inst_off, size_t n_inst, uint8_t* d_out,
+                           void* stream);
 
 /* ---- A7: CLASSIC commit watermark (updateCommittedUpTo over a status window) ------------ */
 int mpx_committed_prefix(mpx_engine* eng, const mpx_inst_state* st, size_t n_inst,
@@ -303,11 +310,21 @@ typedef struct mpx_group_batch {
     int64_t* kv_key_out;
     int64_t* kv_val_out;
     uint8_t* decided;              /* optional, n_groups*ipg                                */
+    uint32_t* n_decided;           /* optional, n_groups: instances decided in this call
+                                      (status became COMMITTED at a quorum crossing)        */
 } mpx_group_batch;
 
 /* host pointers (synchronous) / device pointers (asynchronous on stream)                  */
 int mpx_group_step(mpx_engine* eng, const mpx_group_batch* b);
 int mpx_group_step_dev(mpx_engine* eng, const mpx_group_batch* b, void* stream);
+
+/* per-step totals of a group batch after mpx_group_step_dev (device pointers; b->n_decided
+ * required): d_totals[0] = instances decided, d_totals[1] = instances executed
+ * (executeCommands iterations), d_totals[2] = commands executed (Execute calls). Written, not
+ * accumulated; reduce them over ranks with mpx_step_allreduce_dev.                         */
+#define MPX_STEP_TOTALS 3
+int mpx_step_totals_dev(mpx_engine* eng, const mpx_group_batch* b, int64_t* d_totals,
+                        void* stream);
 
 /* ---- multi-GPU: the one collective (RCCL over xGMI) -------------------------------------
  * Each rank owns a block of groups; non-owned entries must hold -1. After the call every
@@ -320,6 +337,10 @@ int mpx_watermarks_allreduce(mpx_engine* eng, int32_t* committed, int32_t* execu
 /* device pointers: committed/executed are one contiguous int32 buffer of 2*n_groups       */
 int mpx_watermarks_allreduce_dev(mpx_engine* eng, int32_t* d_watermarks, size_t n_groups,
                                  void* stream);
+/* the whole per-step exchange as one RCCL group: max over ranks of the 2*n_groups watermark
+ * vector and sum over ranks of n_totals int64 counters (e.g. the mpx_step_totals_dev ones)  */
+int mpx_step_allreduce_dev(mpx_engine* eng, int32_t* d_watermarks, size_t n_groups,
+                           int64_t* d_totals, size_t n_totals, void* stream);
 
 /* ---- peer stream framing + AcceptReply decode ----------------------
  * A peer connection carries frames [code u8][body]. Codes (genericsmrproto.go:7-18 and the
@@ -447,14 +468,45 @@ int mpx_encode_log_dev(mpx_engine* eng, int format, const mpx_log_rec* d_recs, s
  * instNo outside [0, inst_cap) is where the reference's instanceSpace index panics:
  * MPX_E_NIL_INSTANCE, outputs unspecified.                                                   */
 #define MPX_DURABLE_REC_BYTES 29
+/* rec_base: the file index of this call's first record (0 for a whole file; the running record
+ * count when a long store is replayed in chunks): last_rec holds rec_base + i, so a later
+ * chunk's records win over an earlier chunk's. rec_base + len / 29 must stay below 2^31.
+ * last_rec[inst_cap] is in/out: the caller initialises it to -1 before the first chunk.      */
 int mpx_replay_durable(mpx_engine* eng, const uint8_t* log, size_t len, int32_t inst_cap,
-                       mpx_log_rec* recs, uint8_t* op, int64_t* key, int64_t* val,
-                       int32_t* last_rec, int32_t* scalars);
-/* device form: d_log 16-byte aligned; d_last_rec[inst_cap] initialised by the caller (-1, or a
- * previous call's indices shifted below this call's); d_scalars[2] in/out                    */
+                       int32_t rec_base, mpx_log_rec* recs, uint8_t* op, int64_t* key,
+                       int64_t* val, int32_t* last_rec, int32_t* scalars);
+/* device form: d_log 16-byte aligned; d_last_rec[inst_cap] and d_scalars[2] in/out          */
 int mpx_replay_durable_dev(mpx_engine* eng, const uint8_t* d_log, size_t len, int32_t inst_cap,
-                           mpx_log_rec* d_recs, uint8_t* d_op, int64_t* d_key, int64_t* d_val,
-                           int32_t* d_last_rec, int32_t* d_scalars, void* stream);
+                           int32_t rec_base, mpx_log_rec* d_recs, uint8_t* d_op,
+                           int64_t* d_key, int64_t* d_val, int32_t* d_last_rec,
+                           int32_t* d_scalars, void* stream);
+
+/* ---- device memory, streams and events of the engine's HIP runtime -----------------------
+ * For hosts with no HIP binding of their own (a cgo shim, the Python bench and tests): every
+ * buffer the *_dev entry points take can come from here, so caller and engine share one HIP
+ * runtime and one device. Asynchronous calls take a stream (NULL = the engine's).           */
+#define MPX_COPY_H2D 1
+#define MPX_COPY_D2H 2
+#define MPX_COPY_D2D 3
+int mpx_dev_alloc(mpx_engine* eng, size_t bytes, void** d_out);
+int mpx_dev_free(mpx_engine* eng, void* d);
+int mpx_memcpy_async(mpx_engine* eng, void* dst, const void* src, size_t bytes, int kind,
+                     void* stream);
+int mpx_memset_async(mpx_engine* eng, void* d, int byte_value, size_t bytes, void* stream);
+int mpx_stream_create(mpx_engine* eng, void** stream_out);
+int mpx_stream_destroy(mpx_engine* eng, void* stream);
+int mpx_stream_synchronize(mpx_engine* eng, void* stream);
+int mpx_event_create(mpx_engine* eng, int timing, void** event_out);
+int mpx_event_destroy(mpx_engine* eng, void* event);
+int mpx_event_record(mpx_engine* eng, void* event, void* stream);
+int mpx_stream_wait_event(mpx_engine* eng, void* stream, void* event);
+/* milliseconds between two recorded (and completed) timing events                          */
+int mpx_event_elapsed_ms(mpx_engine* eng, void* ev_start, void* ev_end, float* ms);
+
+/* the HIP and RCCL runtimes this library is bound to, as one JSON object (NUL-terminated,
+ * truncated to cap): {"hip_runtime": v, "hip_driver": v, "rccl": v, "hip_path": "...",
+ * "rccl_path": "..."}. Returns the full length (excluding the NUL) or a negative error.    */
+int mpx_runtime_info(char* buf, size_t cap);
 
 #ifdef __cplusplus
 }

@@ -26,7 +26,7 @@ class MpxGroupBatch(C.Structure):
             "recs", "grp_rec_off", "st_in", "st_out", "committed_in", "committed_out",
             "executed_in", "executed_out", "peer_in", "peer_out", "op", "key", "val", "cmd_off",
             "has_cmds", "ret", "conf_prev", "kv_cnt_in", "kv_key_in", "kv_val_in", "kv_cnt_out",
-            "kv_key_out", "kv_val_out", "decided")]
+            "kv_key_out", "kv_val_out", "decided", "n_decided")]
 
 
 # name -> (restype, argtypes); every symbol of include/mpx.h
@@ -52,6 +52,7 @@ SIGNATURES = {
     "mpx_kv_import": (C.c_int, [_p, _p, _p, _sz]),
     "mpx_kv_clear": (C.c_int, [_p]),
     "mpx_conflict_batch": (C.c_int, [_p, _p, _p, _p, _sz, _p]),
+    "mpx_conflict_batch_dev": (C.c_int, [_p, _p, _p, _p, _sz, _p, _p]),
     "mpx_committed_prefix": (C.c_int, [_p, _p, _sz, _i32, _p]),
     "mpx_group_step": (C.c_int, [_p, C.POINTER(MpxGroupBatch)]),
     "mpx_group_step_dev": (C.c_int, [_p, C.POINTER(MpxGroupBatch), _p]),
@@ -69,8 +70,23 @@ SIGNATURES = {
     "mpx_encode_log": (C.c_int, [_p, C.c_int, _p, _sz, _p, _p, _p, _p, _sz, _p, _sz, _p]),
     "mpx_encode_log_reserve": (C.c_int, [_p, _sz, _sz]),
     "mpx_encode_log_dev": (C.c_int, [_p, C.c_int, _p, _sz, _p, _p, _p, _p, _sz, _p, _p, _p]),
-    "mpx_replay_durable": (C.c_int, [_p, _p, _sz, _i32, _p, _p, _p, _p, _p, _p]),
-    "mpx_replay_durable_dev": (C.c_int, [_p, _p, _sz, _i32, _p, _p, _p, _p, _p, _p, _p]),
+    "mpx_replay_durable": (C.c_int, [_p, _p, _sz, _i32, _i32, _p, _p, _p, _p, _p, _p]),
+    "mpx_replay_durable_dev": (C.c_int, [_p, _p, _sz, _i32, _i32, _p, _p, _p, _p, _p, _p, _p]),
+    "mpx_step_totals_dev": (C.c_int, [_p, C.POINTER(MpxGroupBatch), _p, _p]),
+    "mpx_step_allreduce_dev": (C.c_int, [_p, _p, _sz, _p, _sz, _p]),
+    "mpx_dev_alloc": (C.c_int, [_p, _sz, C.POINTER(_p)]),
+    "mpx_dev_free": (C.c_int, [_p, _p]),
+    "mpx_memcpy_async": (C.c_int, [_p, _p, _p, _sz, C.c_int, _p]),
+    "mpx_memset_async": (C.c_int, [_p, _p, C.c_int, _sz, _p]),
+    "mpx_stream_create": (C.c_int, [_p, C.POINTER(_p)]),
+    "mpx_stream_destroy": (C.c_int, [_p, _p]),
+    "mpx_stream_synchronize": (C.c_int, [_p, _p]),
+    "mpx_event_create": (C.c_int, [_p, C.c_int, C.POINTER(_p)]),
+    "mpx_event_destroy": (C.c_int, [_p, _p]),
+    "mpx_event_record": (C.c_int, [_p, _p, _p]),
+    "mpx_stream_wait_event": (C.c_int, [_p, _p, _p]),
+    "mpx_event_elapsed_ms": (C.c_int, [_p, _p, _p, C.POINTER(C.c_float)]),
+    "mpx_runtime_info": (C.c_int, [C.c_char_p, _sz]),
 }
 
 _lib = None
@@ -95,3 +111,12 @@ def load():
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def runtime_info():
+    """The HIP / RCCL runtimes libmpx.so is bound to in this process (dict)."""
+    import json
+    lib = load()
+    buf = C.create_string_buffer(1024)
+    lib.mpx_runtime_info(buf, len(buf))
+    return json.loads(buf.value.decode())

@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -472,7 +474,8 @@ int mpx_apply_dev(mpx_engine* e, const uint8_t* d_op, const int64_t* d_key, cons
 }
 
 int mpx_kv_size(mpx_engine* e, size_t* n) {
-    if (!e || !n) return MPX_E_INVAL;
+    if (!e) return MPX_E_INVAL;
+    if (!n) return fail(e, MPX_E_INVAL, "null or invalid argument");
     CK(begin(e));
     CK(ensure_kv(e));
     unsigned long long c = 0;
@@ -483,7 +486,8 @@ int mpx_kv_size(mpx_engine* e, size_t* n) {
 }
 
 int mpx_kv_export(mpx_engine* e, int64_t* keys, int64_t* vals, size_t cap, size_t* n) {
-    if (!e || !n || (cap && (!keys || !vals))) return MPX_E_INVAL;
+    if (!e) return MPX_E_INVAL;
+    if (!n || (cap && (!keys || !vals))) return fail(e, MPX_E_INVAL, "null or invalid argument");
     CK(begin(e));
     CK(ensure_kv(e));
     unsigned long long c = 0;
@@ -503,7 +507,8 @@ int mpx_kv_export(mpx_engine* e, int64_t* keys, int64_t* vals, size_t cap, size_
 }
 
 int mpx_kv_import(mpx_engine* e, const int64_t* keys, const int64_t* vals, size_t n) {
-    if (!e || (n && (!keys || !vals))) return MPX_E_INVAL;
+    if (!e) return MPX_E_INVAL;
+    if ((n && (!keys || !vals))) return fail(e, MPX_E_INVAL, "null or invalid argument");
     CK(begin(e));
     CK(ensure_kv(e));
     GROW(e, e->b[8], n * 8);
@@ -547,9 +552,20 @@ int mpx_conflict_batch(mpx_engine* e, const uint8_t* op, const int64_t* key,
     return finish(e);
 }
 
+int mpx_conflict_batch_dev(mpx_engine* e, const uint8_t* d_op, const int64_t* d_key,
+                           const uint64_t* d_inst_off, size_t n_inst, uint8_t* d_out,
+                           void* stream) {
+    if (!e) return MPX_E_INVAL;
+    if (n_inst < 2) return MPX_OK;
+    if (!d_op || !d_key || !d_inst_off || !d_out) return fail(e, MPX_E_INVAL, "null argument");
+    HIPCHK(e, mpx::launch_conflict_batch(d_op, d_key, d_inst_off, n_inst, d_out, pick(e, stream)));
+    return MPX_OK;
+}
+
 // ---- fused group step -------------------------------------------------------------------------
 int mpx_group_step_dev(mpx_engine* e, const mpx_group_batch* b, void* stream) {
-    if (!e || !b) return MPX_E_INVAL;
+    if (!e) return MPX_E_INVAL;
+    if (!b) return fail(e, MPX_E_INVAL, "null or invalid argument");
     if (b->n_groups && (!b->recs || !b->grp_rec_off || !b->st_in || !b->st_out ||
                         !b->committed_in || !b->committed_out || !b->executed_in ||
                         !b->executed_out || !b->peer_in || !b->peer_out || !b->op || !b->key ||
@@ -566,8 +582,19 @@ int mpx_group_step_dev(mpx_engine* e, const mpx_group_batch* b, void* stream) {
     return MPX_OK;
 }
 
+int mpx_step_totals_dev(mpx_engine* e, const mpx_group_batch* b, int64_t* d_totals,
+                        void* stream) {
+    if (!e) return MPX_E_INVAL;
+    if (!b || !d_totals) return fail(e, MPX_E_INVAL, "null argument");
+    if (b->n_groups && (!b->n_decided || !b->executed_in || !b->executed_out || !b->cmd_off))
+        return fail(e, MPX_E_INVAL, "mpx_step_totals_dev needs n_decided, executed_in/out, cmd_off");
+    HIPCHK(e, mpx::launch_step_totals(b, d_totals, pick(e, stream)));
+    return MPX_OK;
+}
+
 int mpx_group_step(mpx_engine* e, const mpx_group_batch* hb) {
-    if (!e || !hb) return MPX_E_INVAL;
+    if (!e) return MPX_E_INVAL;
+    if (!hb) return fail(e, MPX_E_INVAL, "null or invalid argument");
     const uint64_t G = hb->n_groups, ipg = hb->ipg, ni = G * ipg;
     const int N = e->cfg.n_replicas;
     const uint64_t K = e->cfg.kv_per_group;
@@ -594,7 +621,7 @@ int mpx_group_step(mpx_engine* e, const mpx_group_batch* hb) {
                  o_pi = take(G * N * 4), o_po = take(G * N * 4), o_op = take(m), o_key = take(m * 8),
                  o_val = take(m * 8), o_coff = take((ni + 1) * 4), o_has = take(ni),
                  o_ret = take(m * 8), o_conf = take(m), o_kc = take(G * 4), o_kk = take(G * K * 8),
-                 o_kvv = take(G * K * 8), o_dec = take(ni);
+                 o_kvv = take(G * K * 8), o_dec = take(ni), o_nd = take(G * 4);
     GROW(e, e->b[0], off);
     char* d = (char*)e->b[0].p;
     mpx_group_batch db{};
@@ -624,6 +651,7 @@ int mpx_group_step(mpx_engine* e, const mpx_group_batch* hb) {
     db.kv_key_out = (int64_t*)(d + o_kk);
     db.kv_val_out = (int64_t*)(d + o_kvv);
     db.decided = hb->decided ? (uint8_t*)(d + o_dec) : nullptr;
+    db.n_decided = hb->n_decided ? (uint32_t*)(d + o_nd) : nullptr;
     CK(h2d(e, d + o_recs, hb->recs, nr * 16));
     CK(h2d(e, d + o_roff, hb->grp_rec_off, (G + 1) * 8));
     CK(h2d(e, d + o_st, hb->st_in, ni * 16));
@@ -654,6 +682,7 @@ int mpx_group_step(mpx_engine* e, const mpx_group_batch* hb) {
     CK(d2h(e, hb->kv_key_out, d + o_kk, G * K * 8));
     CK(d2h(e, hb->kv_val_out, d + o_kvv, G * K * 8));
     if (hb->decided) CK(d2h(e, hb->decided, d + o_dec, ni));
+    if (hb->n_decided) CK(d2h(e, hb->n_decided, d + o_nd, G * 4));
     return finish(e);
 }
 
@@ -668,7 +697,8 @@ int mpx_comm_unique_id(void* out128) {
 }
 
 int mpx_comm_init(mpx_engine* e, int nranks, int rank, const void* unique_id128) {
-    if (!e || !unique_id128 || nranks < 1 || rank < 0 || rank >= nranks) return MPX_E_INVAL;
+    if (!e) return MPX_E_INVAL;
+    if (!unique_id128 || nranks < 1 || rank < 0 || rank >= nranks) return fail(e, MPX_E_INVAL, "null or invalid argument");
     HIPCHK(e, hipSetDevice(e->device));
     if (e->comm) {
         ncclCommDestroy(e->comm);
@@ -687,7 +717,8 @@ int mpx_comm_init(mpx_engine* e, int nranks, int rank, const void* unique_id128)
 }
 
 int mpx_watermarks_allreduce_dev(mpx_engine* e, int32_t* d_wm, size_t n_groups, void* stream) {
-    if (!e || (n_groups && !d_wm)) return MPX_E_INVAL;
+    if (!e) return MPX_E_INVAL;
+    if (n_groups && !d_wm) return fail(e, MPX_E_INVAL, "null d_watermarks");
     if (!e->comm) return fail(e, MPX_E_INVAL, "mpx_comm_init has not been called");
     ncclResult_t r = ncclAllReduce(d_wm, d_wm, 2 * n_groups, ncclInt32, ncclMax, e->comm,
                                    pick(e, stream));
@@ -695,9 +726,28 @@ int mpx_watermarks_allreduce_dev(mpx_engine* e, int32_t* d_wm, size_t n_groups, 
     return MPX_OK;
 }
 
+int mpx_step_allreduce_dev(mpx_engine* e, int32_t* d_wm, size_t n_groups, int64_t* d_totals,
+                           size_t n_totals, void* stream) {
+    if (!e) return MPX_E_INVAL;
+    if ((n_groups && !d_wm) || (n_totals && !d_totals)) return fail(e, MPX_E_INVAL, "null argument");
+    if (!e->comm) return fail(e, MPX_E_INVAL, "mpx_comm_init has not been called");
+    const hipStream_t s = pick(e, stream);
+    ncclResult_t r = ncclGroupStart();
+    if (r == ncclSuccess && n_groups)
+        r = ncclAllReduce(d_wm, d_wm, 2 * n_groups, ncclInt32, ncclMax, e->comm, s);
+    if (r == ncclSuccess && n_totals)
+        r = ncclAllReduce(d_totals, d_totals, n_totals, ncclInt64, ncclSum, e->comm, s);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r == ncclSuccess) r = r2;
+    if (r != ncclSuccess)
+        return fail(e, MPX_E_RCCL, std::string("step all-reduce: ") + ncclGetErrorString(r));
+    return MPX_OK;
+}
+
 int mpx_watermarks_allreduce(mpx_engine* e, int32_t* committed, int32_t* executed,
                              size_t n_groups) {
-    if (!e || (n_groups && (!committed || !executed))) return MPX_E_INVAL;
+    if (!e) return MPX_E_INVAL;
+    if ((n_groups && (!committed || !executed))) return fail(e, MPX_E_INVAL, "null or invalid argument");
     CK(begin(e));
     GROW(e, e->b[5], 2 * n_groups * 4);
     int32_t* d = (int32_t*)e->b[5].p;
@@ -722,8 +772,9 @@ int mpx_decode_reserve(mpx_engine* e, size_t max_len) {
 int mpx_decode_peer_stream_dev(mpx_engine* e, const uint8_t* d_buf, size_t len,
                                mpx_accept_reply* d_ar, size_t ar_cap, mpx_peer_frame* d_other,
                                size_t other_cap, mpx_decode_result* d_res, void* stream) {
-    if (!e || !d_res || (len && !d_buf) || (ar_cap && !d_ar) || (other_cap && !d_other))
-        return MPX_E_INVAL;
+    if (!e) return MPX_E_INVAL;
+    if (!d_res || (len && !d_buf) || (ar_cap && !d_ar) || (other_cap && !d_other))
+        return fail(e, MPX_E_INVAL, "null or invalid argument");
     if (len > MPX_DECODE_MAX_BYTES)
         return fail(e, MPX_E_UNSUPPORTED, "decode buffers are limited to 2^31-1 bytes per call");
     if (e->decode_work.cap < mpx::decode_work_bytes(len))
@@ -739,8 +790,9 @@ int mpx_decode_peer_stream_dev(mpx_engine* e, const uint8_t* d_buf, size_t len,
 int mpx_decode_peer_stream(mpx_engine* e, const uint8_t* buf, size_t len, mpx_accept_reply* ar,
                            size_t ar_cap, mpx_peer_frame* other, size_t other_cap,
                            mpx_decode_result* res) {
-    if (!e || !res || (len && !buf) || (ar_cap && !ar) || (other_cap && !other))
-        return MPX_E_INVAL;
+    if (!e) return MPX_E_INVAL;
+    if (!res || (len && !buf) || (ar_cap && !ar) || (other_cap && !other))
+        return fail(e, MPX_E_INVAL, "null or invalid argument");
     if (len > MPX_DECODE_MAX_BYTES)
         return fail(e, MPX_E_UNSUPPORTED, "decode buffers are limited to 2^31-1 bytes per call");
     CK(begin(e));
@@ -775,7 +827,8 @@ int mpx_encode_replies_reserve(mpx_engine* e, size_t max_n) {
 int mpx_encode_replies_dev(mpx_engine* e, const mpx_reply_rec* d_recs, size_t n,
                            uint32_t n_clients, uint8_t ok, int32_t leader, uint8_t* d_out,
                            uint64_t* d_client_off, void* stream) {
-    if (!e || !n_clients || !d_client_off || (n && (!d_recs || !d_out))) return MPX_E_INVAL;
+    if (!e) return MPX_E_INVAL;
+    if (!n_clients || !d_client_off || (n && (!d_recs || !d_out))) return fail(e, MPX_E_INVAL, "null or invalid argument");
     if (n >= (1ull << 32)) return fail(e, MPX_E_UNSUPPORTED, "at most 2^32-1 replies per call");
     if (e->fan_work.cap < mpx::fanout_work_bytes(n))
         return fail(e, MPX_E_INVAL,
@@ -789,7 +842,8 @@ int mpx_encode_replies_dev(mpx_engine* e, const mpx_reply_rec* d_recs, size_t n,
 
 int mpx_encode_replies(mpx_engine* e, const mpx_reply_rec* recs, size_t n, uint32_t n_clients,
                        uint8_t ok, int32_t leader, uint8_t* out, uint64_t* client_off) {
-    if (!e || !n_clients || !client_off || (n && (!recs || !out))) return MPX_E_INVAL;
+    if (!e) return MPX_E_INVAL;
+    if (!n_clients || !client_off || (n && (!recs || !out))) return fail(e, MPX_E_INVAL, "null or invalid argument");
     if (n >= (1ull << 32)) return fail(e, MPX_E_UNSUPPORTED, "at most 2^32-1 replies per call");
     CK(begin(e));
     GROW(e, e->fan[0], n * sizeof(mpx_reply_rec));
@@ -820,9 +874,9 @@ int mpx_encode_log_dev(mpx_engine* e, int format, const mpx_log_rec* d_recs, siz
                        const uint64_t* d_cmd_off, const uint8_t* d_op, const int64_t* d_key,
                        const int64_t* d_val, size_t m, uint8_t* d_out, uint64_t* d_rec_off,
                        void* stream) {
-    if (!e || !d_rec_off || (n && (!d_recs || !d_cmd_off || !d_out)) ||
-        (m && (!d_op || !d_key || !d_val)))
-        return MPX_E_INVAL;
+    if (!e) return MPX_E_INVAL;
+    if (!d_rec_off || (n && (!d_recs || !d_cmd_off || !d_out)) || (m && (!d_op || !d_key || !d_val)))
+        return fail(e, MPX_E_INVAL, "null or invalid argument");
     if (format != MPX_LOG_CATCHUP && format != MPX_LOG_DURABLE)
         return fail(e, MPX_E_INVAL, "unknown log format");
     if (e->log_work.cap < mpx::logenc_work_bytes(n, m))
@@ -838,9 +892,9 @@ int mpx_encode_log(mpx_engine* e, int format, const mpx_log_rec* recs, size_t n,
                    const uint64_t* cmd_off, const uint8_t* op, const int64_t* key,
                    const int64_t* val, size_t m, uint8_t* out, size_t out_cap,
                    uint64_t* rec_off) {
-    if (!e || !rec_off || (n && (!recs || !cmd_off)) || (m && (!op || !key || !val)) ||
-        (out_cap && !out))
-        return MPX_E_INVAL;
+    if (!e) return MPX_E_INVAL;
+    if (!rec_off || (n && (!recs || !cmd_off)) || (m && (!op || !key || !val)) || (out_cap && !out))
+        return fail(e, MPX_E_INVAL, "null or invalid argument");
     if (format != MPX_LOG_CATCHUP && format != MPX_LOG_DURABLE)
         return fail(e, MPX_E_INVAL, "unknown log format");
     for (size_t i = 0; i < n; ++i)  // the device kernels trust the offsets
@@ -873,32 +927,48 @@ int mpx_encode_log(mpx_engine* e, int format, const mpx_log_rec* recs, size_t n,
 }
 
 // ---- §8(f) rank 3, read side: durable-log replay --------------------------------------------
-int mpx_replay_durable_dev(mpx_engine* e, const uint8_t* d_log, size_t len, int32_t inst_cap,
-                           mpx_log_rec* d_recs, uint8_t* d_op, int64_t* d_key, int64_t* d_val,
-                           int32_t* d_last_rec, int32_t* d_scalars, void* stream) {
-    if (!e || !d_scalars || inst_cap < 0) return MPX_E_INVAL;
+namespace {
+// shared argument checks of both forms; *n_out = number of records
+int replay_args(mpx_engine* e, size_t len, int32_t inst_cap, int32_t rec_base, size_t* n_out) {
+    if (inst_cap < 0) return fail(e, MPX_E_INVAL, "inst_cap must be >= 0");
+    if (rec_base < 0) return fail(e, MPX_E_INVAL, "rec_base must be >= 0");
     if (len % MPX_DURABLE_REC_BYTES)
         return fail(e, MPX_E_INVAL, "durable log ends in a partial record");
     const size_t n = len / MPX_DURABLE_REC_BYTES;
-    if (n > (size_t)INT32_MAX) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 records");
+    if ((uint64_t)rec_base + n > (uint64_t)INT32_MAX)
+        return fail(e, MPX_E_UNSUPPORTED, "rec_base + records must stay below 2^31");
+    // every record indexes instanceSpace[instNo]: with no instance space, the first one panics
+    if (n && inst_cap == 0)
+        return fail(e, MPX_E_NIL_INSTANCE, "a durable record's instNo is outside [0, inst_cap)");
+    *n_out = n;
+    return MPX_OK;
+}
+}  // namespace
+
+int mpx_replay_durable_dev(mpx_engine* e, const uint8_t* d_log, size_t len, int32_t inst_cap,
+                           int32_t rec_base, mpx_log_rec* d_recs, uint8_t* d_op, int64_t* d_key,
+                           int64_t* d_val, int32_t* d_last_rec, int32_t* d_scalars, void* stream) {
+    if (!e) return MPX_E_INVAL;
+    if (!d_scalars) return fail(e, MPX_E_INVAL, "null d_scalars");
+    size_t n = 0;
+    CK(replay_args(e, len, inst_cap, rec_base, &n));
     if (n && (!d_log || !d_recs || !d_op || !d_key || !d_val || !d_last_rec))
-        return MPX_E_INVAL;
+        return fail(e, MPX_E_INVAL, "null device buffer");
     if ((uintptr_t)d_log % 16)
         return fail(e, MPX_E_INVAL, "d_log must be 16-byte aligned (the tiles load 16 B vectors)");
-    HIPCHK(e, mpx::launch_replay_durable(d_log, n, inst_cap, d_recs, d_op, d_key, d_val,
+    HIPCHK(e, mpx::launch_replay_durable(d_log, n, inst_cap, rec_base, d_recs, d_op, d_key, d_val,
                                          d_last_rec, d_scalars, e->d_err, pick(e, stream)));
     return MPX_OK;
 }
 
 int mpx_replay_durable(mpx_engine* e, const uint8_t* log, size_t len, int32_t inst_cap,
-                       mpx_log_rec* recs, uint8_t* op, int64_t* key, int64_t* val,
+                       int32_t rec_base, mpx_log_rec* recs, uint8_t* op, int64_t* key, int64_t* val,
                        int32_t* last_rec, int32_t* scalars) {
-    if (!e || !scalars || inst_cap < 0 || (inst_cap && !last_rec)) return MPX_E_INVAL;
-    if (len % MPX_DURABLE_REC_BYTES)
-        return fail(e, MPX_E_INVAL, "durable log ends in a partial record");
-    const size_t n = len / MPX_DURABLE_REC_BYTES;
-    if (n > (size_t)INT32_MAX) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 records");
-    if (n && (!log || !recs || !op || !key || !val)) return MPX_E_INVAL;
+    if (!e) return MPX_E_INVAL;
+    if (!scalars || (inst_cap > 0 && !last_rec)) return fail(e, MPX_E_INVAL, "null argument");
+    size_t n = 0;
+    CK(replay_args(e, len, inst_cap, rec_base, &n));
+    if (n && (!log || !recs || !op || !key || !val)) return fail(e, MPX_E_INVAL, "null argument");
     CK(begin(e));
     GROW(e, e->rp[0], len);
     GROW(e, e->rp[1], n * sizeof(mpx_log_rec));
@@ -908,12 +978,13 @@ int mpx_replay_durable(mpx_engine* e, const uint8_t* log, size_t len, int32_t in
     GROW(e, e->rp[5], (size_t)inst_cap * 4);
     GROW(e, e->rp[6], 2 * sizeof(int32_t));
     CK(h2d(e, e->rp[0].p, log, len));
-    if (inst_cap) HIPCHK(e, hipMemsetAsync(e->rp[5].p, 0xff, (size_t)inst_cap * 4, e->stream));
+    CK(h2d(e, e->rp[5].p, last_rec, (size_t)inst_cap * 4));
     CK(h2d(e, e->rp[6].p, scalars, 2 * sizeof(int32_t)));
-    CK(mpx_replay_durable_dev(e, (const uint8_t*)e->rp[0].p, len, inst_cap,
-                              (mpx_log_rec*)e->rp[1].p, (uint8_t*)e->rp[2].p,
-                              (int64_t*)e->rp[3].p, (int64_t*)e->rp[4].p, (int32_t*)e->rp[5].p,
-                              (int32_t*)e->rp[6].p, e->stream));
+    if (n)
+        CK(mpx_replay_durable_dev(e, (const uint8_t*)e->rp[0].p, len, inst_cap, rec_base,
+                                  (mpx_log_rec*)e->rp[1].p, (uint8_t*)e->rp[2].p,
+                                  (int64_t*)e->rp[3].p, (int64_t*)e->rp[4].p,
+                                  (int32_t*)e->rp[5].p, (int32_t*)e->rp[6].p, e->stream));
     CK(d2h(e, recs, e->rp[1].p, n * sizeof(mpx_log_rec)));
     CK(d2h(e, op, e->rp[2].p, n));
     CK(d2h(e, key, e->rp[3].p, n * 8));
@@ -924,6 +995,137 @@ int mpx_replay_durable(mpx_engine* e, const uint8_t* log, size_t len, int32_t in
     if (rc == MPX_E_NIL_INSTANCE)
         return fail(e, rc, "a durable record's instNo is outside [0, inst_cap)");
     return rc;
+}
+
+// ---- device memory, streams, events (the engine's HIP runtime) --------------------------------
+int mpx_dev_alloc(mpx_engine* e, size_t bytes, void** out) {
+    if (!e) return MPX_E_INVAL;
+    if (!out) return fail(e, MPX_E_INVAL, "null or invalid argument");
+    *out = nullptr;
+    HIPCHK(e, hipSetDevice(e->device));
+    if (hipMalloc(out, bytes ? bytes : 1) != hipSuccess) {
+        (void)hipGetLastError();
+        *out = nullptr;
+        return fail(e, MPX_E_NOMEM, "device allocation of " + std::to_string(bytes) + " bytes failed");
+    }
+    return MPX_OK;
+}
+
+int mpx_dev_free(mpx_engine* e, void* d) {
+    if (!e) return MPX_E_INVAL;
+    if (!d) return MPX_OK;
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipFree(d));
+    return MPX_OK;
+}
+
+int mpx_memcpy_async(mpx_engine* e, void* dst, const void* src, size_t bytes, int kind,
+                     void* stream) {
+    if (!e) return MPX_E_INVAL;
+    if (!bytes) return MPX_OK;
+    if (!dst || !src) return fail(e, MPX_E_INVAL, "null copy pointer");
+    hipMemcpyKind k;
+    switch (kind) {
+        case MPX_COPY_H2D: k = hipMemcpyHostToDevice; break;
+        case MPX_COPY_D2H: k = hipMemcpyDeviceToHost; break;
+        case MPX_COPY_D2D: k = hipMemcpyDeviceToDevice; break;
+        default: return fail(e, MPX_E_INVAL, "unknown copy kind");
+    }
+    HIPCHK(e, hipMemcpyAsync(dst, src, bytes, k, pick(e, stream)));
+    return MPX_OK;
+}
+
+int mpx_memset_async(mpx_engine* e, void* d, int byte_value, size_t bytes, void* stream) {
+    if (!e) return MPX_E_INVAL;
+    if (!bytes) return MPX_OK;
+    if (!d) return fail(e, MPX_E_INVAL, "null memset pointer");
+    HIPCHK(e, hipMemsetAsync(d, byte_value, bytes, pick(e, stream)));
+    return MPX_OK;
+}
+
+int mpx_stream_create(mpx_engine* e, void** out) {
+    if (!e) return MPX_E_INVAL;
+    if (!out) return fail(e, MPX_E_INVAL, "null or invalid argument");
+    HIPCHK(e, hipSetDevice(e->device));
+    hipStream_t s = nullptr;
+    HIPCHK(e, hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *out = (void*)s;
+    return MPX_OK;
+}
+
+int mpx_stream_destroy(mpx_engine* e, void* s) {
+    if (!e) return MPX_E_INVAL;
+    if (!s || s == (void*)e->stream) return fail(e, MPX_E_INVAL, "not a stream of mpx_stream_create");
+    HIPCHK(e, hipStreamDestroy((hipStream_t)s));
+    return MPX_OK;
+}
+
+int mpx_stream_synchronize(mpx_engine* e, void* s) {
+    if (!e) return MPX_E_INVAL;
+    HIPCHK(e, hipStreamSynchronize(pick(e, s)));
+    return MPX_OK;
+}
+
+int mpx_event_create(mpx_engine* e, int timing, void** out) {
+    if (!e) return MPX_E_INVAL;
+    if (!out) return fail(e, MPX_E_INVAL, "null or invalid argument");
+    HIPCHK(e, hipSetDevice(e->device));
+    hipEvent_t ev = nullptr;
+    HIPCHK(e, hipEventCreateWithFlags(&ev, timing ? hipEventDefault : hipEventDisableTiming));
+    *out = (void*)ev;
+    return MPX_OK;
+}
+
+int mpx_event_destroy(mpx_engine* e, void* ev) {
+    if (!e) return MPX_E_INVAL;
+    if (!ev) return fail(e, MPX_E_INVAL, "null or invalid argument");
+    HIPCHK(e, hipEventDestroy((hipEvent_t)ev));
+    return MPX_OK;
+}
+
+int mpx_event_record(mpx_engine* e, void* ev, void* s) {
+    if (!e) return MPX_E_INVAL;
+    if (!ev) return fail(e, MPX_E_INVAL, "null or invalid argument");
+    HIPCHK(e, hipEventRecord((hipEvent_t)ev, pick(e, s)));
+    return MPX_OK;
+}
+
+int mpx_stream_wait_event(mpx_engine* e, void* s, void* ev) {
+    if (!e) return MPX_E_INVAL;
+    if (!ev) return fail(e, MPX_E_INVAL, "null or invalid argument");
+    HIPCHK(e, hipStreamWaitEvent(pick(e, s), (hipEvent_t)ev, 0));
+    return MPX_OK;
+}
+
+int mpx_event_elapsed_ms(mpx_engine* e, void* ev0, void* ev1, float* ms) {
+    if (!e) return MPX_E_INVAL;
+    if (!ev0 || !ev1 || !ms) return fail(e, MPX_E_INVAL, "null or invalid argument");
+    HIPCHK(e, hipEventElapsedTime(ms, (hipEvent_t)ev0, (hipEvent_t)ev1));
+    return MPX_OK;
+}
+
+int mpx_runtime_info(char* buf, size_t cap) {
+    int rt = 0, drv = 0, nv = 0;
+    (void)hipRuntimeGetVersion(&rt);
+    (void)hipDriverGetVersion(&drv);
+    (void)ncclGetVersion(&nv);
+    (void)hipGetLastError();
+    auto path_of = [](const void* sym) {
+        Dl_info info{};
+        return (sym && dladdr(sym, &info) && info.dli_fname) ? std::string(info.dli_fname)
+                                                              : std::string("?");
+    };
+    const std::string s = "{\"hip_runtime\": " + std::to_string(rt) +
+                          ", \"hip_driver\": " + std::to_string(drv) +
+                          ", \"rccl\": " + std::to_string(nv) + ", \"hip_path\": \"" +
+                          path_of((const void*)&hipRuntimeGetVersion) + "\", \"rccl_path\": \"" +
+                          path_of((const void*)&ncclAllReduce) + "\"}";
+    if (buf && cap) {
+        const size_t k = std::min(cap - 1, s.size());
+        memcpy(buf, s.data(), k);
+        buf[k] = 0;
+    }
+    return (int)s.size();
 }
 
 }  // extern "C"

@@ -51,6 +51,8 @@ hipError_t launch_conflict_batch(const uint8_t* op, const int64_t* key, const ui
 hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
                              const mpx_group_batch* b, uint32_t* worklist, uint32_t* wcount,
                              uint32_t* err, hipStream_t stream);
+// d_totals[0..2] = decided instances, executed instances, executed commands of the batch
+hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, hipStream_t stream);
 
 // ---- global KV table apply (mpx_apply) ----------------------------------------------------
 struct KvTable {
@@ -105,7 +107,7 @@ hipError_t launch_encode_log(int format, const mpx_log_rec* recs, uint64_t n,
 
 // ---- durable-log replay (mpx_replay_durable) ---------------------------------------------
 hipError_t launch_replay_durable(const uint8_t* log, uint64_t n, int32_t inst_cap,
-                                 mpx_log_rec* recs, uint8_t* op, int64_t* key, int64_t* val,
+                                 int32_t rec_base, mpx_log_rec* recs, uint8_t* op, int64_t* key, int64_t* val,
                                  int32_t* last_rec, int32_t* scalars, uint32_t* err,
                                  hipStream_t stream);
 

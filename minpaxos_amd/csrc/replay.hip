@@ -39,7 +39,8 @@ __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
 }
 
 __global__ __launch_bounds__(kReplayBlock) void k_replay_durable(
-    const uint8_t* __restrict__ log, uint64_t n, int32_t inst_cap, mpx_log_rec* __restrict__ recs,
+    const uint8_t* __restrict__ log, uint64_t n, int32_t inst_cap, int32_t rec_base,
+    mpx_log_rec* __restrict__ recs,
     uint8_t* __restrict__ op, int64_t* __restrict__ key, int64_t* __restrict__ val,
     int32_t* __restrict__ last_rec, int32_t* __restrict__ scalars, uint32_t* __restrict__ err) {
     __shared__ uint4 tile[kTileVec + 1];  // +1: the last lane's 9th dword reads past the tile
@@ -99,7 +100,7 @@ __global__ __launch_bounds__(kReplayBlock) void k_replay_durable(
             if (inst < 0 || inst >= inst_cap)
                 raise_err(err, kErrNil);
             else
-                atomicMax(last_rec + inst, (int32_t)i);
+                atomicMax(last_rec + inst, rec_base + (int32_t)i);
         }
     }
     // one atomic per workgroup and watermark, skipped when it cannot raise the running value:
@@ -122,7 +123,7 @@ __global__ __launch_bounds__(kReplayBlock) void k_replay_durable(
 }  // namespace
 
 hipError_t launch_replay_durable(const uint8_t* log, uint64_t n, int32_t inst_cap,
-                                 mpx_log_rec* recs, uint8_t* op, int64_t* key, int64_t* val,
+                                 int32_t rec_base, mpx_log_rec* recs, uint8_t* op, int64_t* key, int64_t* val,
                                  int32_t* last_rec, int32_t* scalars, uint32_t* err,
                                  hipStream_t stream) {
     if (!n) return hipSuccess;
@@ -130,7 +131,7 @@ hipError_t launch_replay_durable(const uint8_t* log, uint64_t n, int32_t inst_ca
     const uint64_t tiles = (n + kReplayBlock - 1) / kReplayBlock;
     const uint64_t grid = tiles < kReplayGrid ? tiles : kReplayGrid;
     hipLaunchKernelGGL(k_replay_durable, dim3((unsigned)grid), dim3(kReplayBlock), 0, stream, log,
-                       n, inst_cap, recs, op, key, val, last_rec, scalars, err);
+                       n, inst_cap, rec_base, recs, op, key, val, last_rec, scalars, err);
     return hipGetLastError();
 }
 

@@ -296,7 +296,7 @@ struct FastLds {
     uint32_t newbits[kFCmds / 32];  // first PUTs of new keys, as a bitmap over command index
     uint16_t coff[kFIpg + 2];       // instance -> first command (group-relative)
     uint32_t red[1 + MPX_MAX_REPLICAS];  // 1 + instance: last crossing, last peerCommits[id] source
-    uint32_t firstnil, firstbad, flags;
+    uint32_t firstnil, firstbad, flags, ndec;
 #ifdef MPX_LDS_PAD
     uint8_t lds_pad[MPX_LDS_PAD];  // A/B builds only: lowers occupancy to price it
 #endif
@@ -397,6 +397,7 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
         S.firstnil = ipg;
         S.firstbad = ipg;
         S.flags = 0;
+        S.ndec = 0;
     }
 #pragma unroll
     for (int k = 0; k < kFRecPer; ++k) {
@@ -529,6 +530,10 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
         }
         dec = deci != 0;
         if (__ballot(dec) && l == 0) atomicMax(&S.red[0], 1u);
+    }
+    {  // instances decided by this step (only a lane's own instance can decide)
+        const unsigned long long dm = __ballot(dec);
+        if (l == 0 && dm) atomicAdd(&S.ndec, (uint32_t)__popcll(dm));
     }
     // executeCommands stops at the first nil instance (nil Cmds); CLASSIC's watermark at the first
     // instance that is not COMMITTED: wave minima, one LDS atomic per wave
@@ -759,6 +764,7 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
         b.committed_out[g] = cu;
         b.executed_out[g] = stop > lo ? (int32_t)(stop - 1) : ex_in;
         b.kv_cnt_out[g] = total < kvpg ? total : kvpg;
+        if (b.n_decided) b.n_decided[g] = S.ndec;
     }
     ebits &= 0x7FFFFFFFu;
     if (ebits) raise_err(err, ebits);
@@ -786,7 +792,7 @@ struct GenLds {
     uint32_t dec_bits[kMaxIpgBits / 32];
     uint32_t wsum[kStepBlock / kWave];
     unsigned long long red[1 + MPX_MAX_REPLICAS];
-    uint32_t dn, n_orig, scal[4];
+    uint32_t dn, n_orig, ndec, scal[4];
 };
 
 template <int MODE>
@@ -802,7 +808,10 @@ __device__ void group_general(GenLds& S, const mpx_group_batch& b, uint32_t g, i
     if (t <= MPX_MAX_REPLICAS) S.red[t] = 0;
     for (int i = t; i < kMaxIpgBits / 32; i += kStepBlock) S.dec_bits[i] = 0;
     for (int i = t; i < kHCap; i += kStepBlock) S.hslot[i] = 0;
-    if (t == 0) S.dn = 0;
+    if (t == 0) {
+        S.dn = 0;
+        S.ndec = 0;
+    }
     __syncthreads();
 
     // ---- 1. tally straight from global memory ------------------------------------------------------
@@ -831,6 +840,11 @@ __device__ void group_general(GenLds& S, const mpx_group_batch& b, uint32_t g, i
     if (b.decided)
         for (uint64_t i = t; i < ipg; i += kStepBlock)
             b.decided[gi0 + i] = (S.dec_bits[i >> 5] >> (i & 31)) & 1u;
+    if (b.n_decided) {  // popcount of the decided bitmap (bits past ipg stay 0)
+        uint32_t c = 0;
+        for (uint64_t i = t; i < (ipg + 31) / 32; i += kStepBlock) c += __popc(S.dec_bits[i]);
+        if (c) atomicAdd(&S.ndec, c);
+    }
 
     // ---- watermarks --------------------------------------------------------------------------------
     const int32_t cu_in = b.committed_in[g];
@@ -884,7 +898,10 @@ __device__ void group_general(GenLds& S, const mpx_group_batch& b, uint32_t g, i
     }
     __syncthreads();
     const int64_t stop = hi >= lo ? (int64_t)S.scal[2] : lo;
-    if (t == 0) b.executed_out[g] = stop > lo ? (int32_t)(stop - 1) : ex_in;
+    if (t == 0) {
+        b.executed_out[g] = stop > lo ? (int32_t)(stop - 1) : ex_in;
+        if (b.n_decided) b.n_decided[g] = S.ndec;
+    }
 
     const Dict D{S.dkey, S.dval, S.dfirst, S.cnt, S.hslot, S.dpresent, S.dseen, &S.dn,
                  (uint32_t)kDCap, (uint32_t)kHCap};
@@ -1008,6 +1025,51 @@ hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
         k_group_general<MPX_MODE_CLASSIC><<<gen_grid, kStepBlock, 0, stream>>>(
             *b, nrep, kv_per_group, worklist, wcount, err);
     }
+    return hipGetLastError();
+}
+
+// per-step totals of a batch: decided instances, executed instances, executed commands. One
+// group per lane, a block reduction, one 64-bit atomic per block and counter (totals zeroed by
+// the launcher on the same stream).
+__global__ __launch_bounds__(256) void k_step_totals(mpx_group_batch b, unsigned long long* totals) {
+    __shared__ unsigned long long red[3][kStepBlock / kWave];
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long d = 0, xi = 0, xc = 0;
+    if (g < b.n_groups) {
+        d = b.n_decided[g];
+        const int64_t ei = b.executed_in[g], eo = b.executed_out[g];
+        const int64_t lo = ei + 1 < 0 ? 0 : ei + 1;
+        if (eo >= lo && eo < (int64_t)b.ipg) {
+            const uint64_t gi0 = (uint64_t)g * b.ipg;
+            xi = (unsigned long long)(eo - lo + 1);
+            xc = b.cmd_off[gi0 + eo + 1] - b.cmd_off[gi0 + lo];
+        }
+    }
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) {
+        d += __shfl_xor(d, k);
+        xi += __shfl_xor(xi, k);
+        xc += __shfl_xor(xc, k);
+    }
+    const int w = threadIdx.x / kWave;
+    if (lane_id() == 0) {
+        red[0][w] = d;
+        red[1][w] = xi;
+        red[2][w] = xc;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        unsigned long long v = 0;
+        for (int k = 0; k < kStepBlock / kWave; ++k) v += red[threadIdx.x][k];
+        if (v) atomicAdd(totals + threadIdx.x, v);
+    }
+}
+
+hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, hipStream_t stream) {
+    hipError_t r = hipMemsetAsync(totals, 0, MPX_STEP_TOTALS * sizeof(int64_t), stream);
+    if (r != hipSuccess || !b->n_groups) return r;
+    k_step_totals<<<(b->n_groups + kStepBlock - 1) / kStepBlock, kStepBlock, 0, stream>>>(
+        *b, reinterpret_cast<unsigned long long*>(totals));
     return hipGetLastError();
 }
 

@@ -211,6 +211,10 @@ class Engine:
                                                 _ptr(out)), "mpx_conflict_batch")
         return out[:max(n_inst - 1, 0)]
 
+    def conflict_batch_dev(self, d_op, d_key, d_inst_off, n_inst, d_out, stream=None):
+        self._check(self.lib.mpx_conflict_batch_dev(self.h, d_op, d_key, d_inst_off, n_inst,
+                                                    d_out, stream), "mpx_conflict_batch_dev")
+
     # ---- fused group step -------------------------------------------------------------------
     def group_step(self, b, kv_cnt=None, kv_key=None, kv_val=None, ret=None, want_conf=True,
                    want_decided=True):
@@ -236,16 +240,22 @@ class Engine:
         eo = np.zeros(G, np.int32)
         po = np.zeros(G * N, np.int32)
         dec = np.zeros(G * ipg, np.uint8) if want_decided else None
+        nd = np.zeros(G, np.uint32)
         gb = _lib.MpxGroupBatch(G, ipg, *[C.cast(_ptr(x), C.c_void_p) if x is not None else None
                                           for x in (recs, off, st, st, ci, co, ei, eo, pi, po, op,
                                                     key, val, coff, has, ret, conf, kc, kk, kv,
-                                                    kc, kk, kv, dec)])
+                                                    kc, kk, kv, dec, nd)])
         self._check(self.lib.mpx_group_step(self.h, C.byref(gb)), "mpx_group_step")
         return dict(st_out=st, committed_out=co, executed_out=eo, peer_out=po, ret=ret,
-                    conf_prev=conf, kv_cnt=kc, kv_key=kk, kv_val=kv, decided=dec)
+                    conf_prev=conf, kv_cnt=kc, kv_key=kk, kv_val=kv, decided=dec, n_decided=nd)
 
     def group_step_dev(self, gb, stream=None):
         self._check(self.lib.mpx_group_step_dev(self.h, C.byref(gb), stream), "mpx_group_step_dev")
+
+    def step_totals_dev(self, gb, d_totals, stream=None):
+        """d_totals[0..2] = decided instances, executed instances, executed commands"""
+        self._check(self.lib.mpx_step_totals_dev(self.h, C.byref(gb), d_totals, stream),
+                    "mpx_step_totals_dev")
 
     # ---- peer stream framing (SURVEY §8(f) rank 1) ------------------------------------------
     def decode_peer_stream(self, buf, ar_cap=None, other_cap=None):
@@ -324,27 +334,33 @@ class Engine:
                     "mpx_encode_log_dev")
 
     # ---- durable-log replay (read side) ---------------------------------
-    def replay_durable(self, log, inst_cap, default_ballot=0, committed_up_to=-1):
+    def replay_durable(self, log, inst_cap, default_ballot=0, committed_up_to=-1, rec_base=0,
+                       last_rec=None):
         """getDataFromStableStore (bareminpaxos.go:122-161) over a durable log of 29-byte
         records. Returns (recs, op, key, val, last_rec, default_ballot, committed_up_to):
-        last_rec[i] is the index of the last record naming instance i (-1: none)."""
+        last_rec[i] is the file index of the last record naming instance i (-1: none). A store
+        replayed in chunks passes each chunk's first file index as rec_base and the previous
+        chunk's last_rec."""
         log = _c(log, np.uint8)
         n = len(log) // R.DURABLE_REC_BYTES
         recs = np.zeros(n, R.LOG_REC)
         op = np.zeros(n, np.uint8)
         key = np.zeros(n, np.int64)
         val = np.zeros(n, np.int64)
-        last = np.zeros(inst_cap, np.int32)
+        last = np.full(inst_cap, -1, np.int32) if last_rec is None else \
+            np.array(last_rec, np.int32, copy=True)
         sc = np.array([default_ballot, committed_up_to], np.int32)
-        self._check(self.lib.mpx_replay_durable(self.h, _ptr(log), len(log), inst_cap, _ptr(recs),
+        self._check(self.lib.mpx_replay_durable(self.h, _ptr(log), len(log), inst_cap, rec_base,
+                                                _ptr(recs),
                                                 _ptr(op), _ptr(key), _ptr(val), _ptr(last),
                                                 _ptr(sc)),
                     "mpx_replay_durable")
         return recs, op, key, val, last, int(sc[0]), int(sc[1])
 
     def replay_durable_dev(self, d_log, nbytes, inst_cap, d_recs, d_op, d_key, d_val, d_last,
-                           d_scalars, stream=None):
-        self._check(self.lib.mpx_replay_durable_dev(self.h, d_log, nbytes, inst_cap, d_recs, d_op,
+                           d_scalars, stream=None, rec_base=0):
+        self._check(self.lib.mpx_replay_durable_dev(self.h, d_log, nbytes, inst_cap, rec_base,
+                                                    d_recs, d_op,
                                                     d_key, d_val, d_last, d_scalars, stream),
                     "mpx_replay_durable_dev")
 
@@ -373,3 +389,57 @@ class Engine:
     def watermarks_allreduce_dev(self, d_wm, n_groups, stream=None):
         self._check(self.lib.mpx_watermarks_allreduce_dev(self.h, d_wm, n_groups, stream),
                     "mpx_watermarks_allreduce_dev")
+
+    def step_allreduce_dev(self, d_wm, n_groups, d_totals, n_totals, stream=None):
+        """max of the watermark vector and sum of the step totals over ranks, one RCCL group"""
+        self._check(self.lib.mpx_step_allreduce_dev(self.h, d_wm, n_groups, d_totals, n_totals,
+                                                    stream), "mpx_step_allreduce_dev")
+
+    # ---- device memory / streams / events of the engine's HIP runtime -----------------------
+    def dev_alloc(self, nbytes):
+        p = C.c_void_p()
+        self._check(self.lib.mpx_dev_alloc(self.h, nbytes, C.byref(p)), "mpx_dev_alloc")
+        return p.value
+
+    def dev_free(self, ptr):
+        self._check(self.lib.mpx_dev_free(self.h, ptr), "mpx_dev_free")
+
+    def memcpy(self, dst, src, nbytes, kind, stream=None):
+        self._check(self.lib.mpx_memcpy_async(self.h, dst, src, nbytes, kind, stream),
+                    "mpx_memcpy_async")
+
+    def memset(self, ptr, byte_value, nbytes, stream=None):
+        self._check(self.lib.mpx_memset_async(self.h, ptr, byte_value, nbytes, stream),
+                    "mpx_memset_async")
+
+    def stream_create(self):
+        s = C.c_void_p()
+        self._check(self.lib.mpx_stream_create(self.h, C.byref(s)), "mpx_stream_create")
+        return s.value
+
+    def stream_destroy(self, s):
+        self._check(self.lib.mpx_stream_destroy(self.h, s), "mpx_stream_destroy")
+
+    def stream_synchronize(self, s=None):
+        self._check(self.lib.mpx_stream_synchronize(self.h, s), "mpx_stream_synchronize")
+
+    def event_create(self, timing=True):
+        ev = C.c_void_p()
+        self._check(self.lib.mpx_event_create(self.h, 1 if timing else 0, C.byref(ev)),
+                    "mpx_event_create")
+        return ev.value
+
+    def event_destroy(self, ev):
+        self._check(self.lib.mpx_event_destroy(self.h, ev), "mpx_event_destroy")
+
+    def event_record(self, ev, stream=None):
+        self._check(self.lib.mpx_event_record(self.h, ev, stream), "mpx_event_record")
+
+    def stream_wait_event(self, stream, ev):
+        self._check(self.lib.mpx_stream_wait_event(self.h, stream, ev), "mpx_stream_wait_event")
+
+    def event_elapsed_ms(self, ev0, ev1):
+        ms = C.c_float(0.0)
+        self._check(self.lib.mpx_event_elapsed_ms(self.h, ev0, ev1, C.byref(ms)),
+                    "mpx_event_elapsed_ms")
+        return ms.value

@@ -305,6 +305,11 @@ int orc_group_step(int N, int mode, const mpx_group_batch* b, uint32_t kv_per_gr
         }
         if (b->decided)
             for (uint32_t i = 0; i < ipg; ++i) b->decided[(size_t)g * ipg + i] = dec[i];
+        if (b->n_decided) {
+            uint32_t nd = 0;
+            for (uint32_t i = 0; i < ipg; ++i) nd += dec[i];
+            b->n_decided[g] = nd;
+        }
         b->committed_out[g] = cu;
         for (int j = 0; j < N; ++j) b->peer_out[(size_t)g * N + j] = pc[j];
 

@@ -181,17 +181,17 @@ int orc_encode_log(int format, const mpx_log_rec* recs, size_t n, const uint64_t
 // Command.Unmarshal (:142-143, statemarsh.go:21-37), the two watermark updates (:145-151), and
 // instanceSpace[instNo] = the record (:153-157; last_rec[] keeps the index of that record).
 // A trailing partial record is rejected (the reference decodes it zero-padded), and an instNo
-// outside [0, inst_cap) stops the loop where Go's index check panics.
-int orc_replay_durable(const uint8_t* log, size_t len, int32_t inst_cap, mpx_log_rec* recs,
-                       uint8_t* op, int64_t* key, int64_t* val, int32_t* last_rec,
-                       int32_t* scalars) {
-    if (len % MPX_DURABLE_REC_BYTES) return MPX_E_INVAL;
+// outside [0, inst_cap) stops the loop where Go's index check panics. Record i of this call is
+// file record rec_base + i (a store replayed in chunks); last_rec is in/out.
+int orc_replay_durable(const uint8_t* log, size_t len, int32_t inst_cap, int32_t rec_base,
+                       mpx_log_rec* recs, uint8_t* op, int64_t* key, int64_t* val,
+                       int32_t* last_rec, int32_t* scalars) {
+    if (len % MPX_DURABLE_REC_BYTES || rec_base < 0) return MPX_E_INVAL;
     auto u32 = [](const uint8_t* b) {
         return (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) |
                ((uint32_t)b[3] << 24);
     };
     auto u64 = [&](const uint8_t* b) { return (uint64_t)u32(b) | ((uint64_t)u32(b + 4) << 32); };
-    for (int32_t i = 0; i < inst_cap; ++i) last_rec[i] = -1;
     int32_t& defaultBallot = scalars[0];
     int32_t& committedUpTo = scalars[1];
     const size_t n = len / MPX_DURABLE_REC_BYTES;
@@ -207,7 +207,7 @@ int orc_replay_durable(const uint8_t* log, size_t len, int32_t inst_cap, mpx_log
         if (ballot > defaultBallot) defaultBallot = ballot;
         if (instNo > committedUpTo && status == MPX_COMMITTED) committedUpTo = instNo;
         if (instNo < 0 || instNo >= inst_cap) return MPX_E_NIL_INSTANCE;
-        last_rec[instNo] = (int32_t)i;
+        last_rec[instNo] = rec_base + (int32_t)i;
     }
     return MPX_OK;
 }

@@ -15,15 +15,19 @@ if TESTS not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP engine)")
     config.addinivalue_line("markers", "slow: larger parity sizes")
-
-
-@pytest.fixture(scope="session", autouse=True)
-def _built():
-    """Build the oracle (g++) and, where hipcc exists, the engine (incremental make)."""
+    # Build the oracle (g++) and, where hipcc exists, the engine (incremental make), then load
+    # libmpx.so BEFORE any test module imports torch: the engine binds /opt/rocm's HIP and RCCL
+    # (the runtime bench.py measures on too), not the copies torch bundles.
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
     if os.path.exists("/opt/rocm/bin/hipcc"):
         subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "minpaxos_amd")], check=True)
-    yield
+    from minpaxos_amd import _lib
+    _lib.load()
+
+
+def pytest_report_header(config):
+    from minpaxos_amd import _lib
+    return f"libmpx.so runtime: {_lib.runtime_info()}"
 
 
 @pytest.fixture(scope="session")

@@ -53,7 +53,7 @@ def load():
         "orc_decode_peer_stream": (C.c_int, [_p, _sz, _p, _sz, _p, _sz, _p]),
         "orc_encode_replies": (C.c_int, [_p, _sz, C.c_uint32, C.c_uint8, _i32, _p, _p]),
         "orc_encode_log": (C.c_int, [C.c_int, _p, _sz, _p, _p, _p, _p, _p, _sz, _p]),
-        "orc_replay_durable": (C.c_int, [_p, _sz, _i32, _p, _p, _p, _p, _p, _p]),
+        "orc_replay_durable": (C.c_int, [_p, _sz, _i32, _i32, _p, _p, _p, _p, _p, _p]),
         "orc_bench_group_step": (C.c_int64, [C.c_int, C.c_int, C.POINTER(L.MpxGroupBatch),
                                              C.c_uint32, C.c_int]),
     }
@@ -207,18 +207,21 @@ class Oracle:
                                        _ptr(val), _ptr(out), cap, _ptr(ro)), "orc_encode_log")
         return out[:int(ro[-1])], ro
 
-    def replay_durable(self, log, inst_cap, default_ballot=0, committed_up_to=-1):
+    def replay_durable(self, log, inst_cap, default_ballot=0, committed_up_to=-1, rec_base=0,
+                       last_rec=None):
         """getDataFromStableStore (bareminpaxos.go:122-161): returns (recs, op, key, val,
-        last_rec, default_ballot, committed_up_to)."""
+        last_rec, default_ballot, committed_up_to); last_rec in/out (default: all -1)."""
         log = np.ascontiguousarray(log, np.uint8)
         n = len(log) // R.DURABLE_REC_BYTES
         recs = np.zeros(n, R.LOG_REC)
         op = np.zeros(n, np.uint8)
         key = np.zeros(n, np.int64)
         val = np.zeros(n, np.int64)
-        last = np.zeros(inst_cap, np.int32)
+        last = np.full(inst_cap, -1, np.int32) if last_rec is None else \
+            np.array(last_rec, np.int32, copy=True)
         sc = np.array([default_ballot, committed_up_to], np.int32)
-        _check(self.lib.orc_replay_durable(_ptr(log), len(log), inst_cap, _ptr(recs), _ptr(op),
+        _check(self.lib.orc_replay_durable(_ptr(log), len(log), inst_cap, rec_base, _ptr(recs),
+                                           _ptr(op),
                                            _ptr(key), _ptr(val), _ptr(last), _ptr(sc)),
                "orc_replay_durable")
         return recs, op, key, val, last, int(sc[0]), int(sc[1])
@@ -249,12 +252,13 @@ class Oracle:
         eo = np.zeros(G, np.int32)
         po = np.zeros(G * N, np.int32)
         dec = np.zeros(G * ipg, np.uint8) if want_decided else None
+        nd = np.zeros(G, np.uint32)
         gb = L.MpxGroupBatch(G, ipg, *[_ptr(x) for x in (recs, off, st, sto, ci, co, ei, eo, pi,
                                                           po, op, key, val, coff, has, ret, conf,
-                                                          kci, kki, kvi, kco, kko, kvo, dec)])
+                                                          kci, kki, kvi, kco, kko, kvo, dec, nd)])
         _check(self.lib.orc_group_step(N, self.mode, C.byref(gb), K), "orc_group_step")
         return dict(st_out=sto, committed_out=co, executed_out=eo, peer_out=po, ret=ret,
-                    conf_prev=conf, kv_cnt=kco, kv_key=kko, kv_val=kvo, decided=dec)
+                    conf_prev=conf, kv_cnt=kco, kv_key=kko, kv_val=kvo, decided=dec, n_decided=nd)
 
 
 def group_batch_struct(arrs):

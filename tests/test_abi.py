@@ -32,7 +32,7 @@ def test_library_exports_every_header_symbol():
                          text=True, check=True).stdout
     exported = set(re.findall(r"\bT (mpx_[a-z0-9_]+)", out))
     assert set(header_functions()) <= exported
-    assert lib.mpx_abi_version() == 1
+    assert lib.mpx_abi_version() == 2
 
 
 def test_no_device_calls_fail_cleanly():
@@ -58,8 +58,8 @@ def test_struct_sizes_match_header():
         sizeof(mpx_inst_state), sizeof(mpx_prepare_reply), sizeof(mpx_prep_state),
         sizeof(mpx_prepare_reply_min), sizeof(mpx_group_prep_state), sizeof(mpx_prepare_effect),
         sizeof(mpx_config), sizeof(mpx_group_batch));
-      printf("%zu %zu %zu\n", offsetof(mpx_accept_reply, ok), offsetof(mpx_prep_state, flags),
-        offsetof(mpx_group_batch, decided));
+      printf("%zu %zu %zu %zu\n", offsetof(mpx_accept_reply, ok), offsetof(mpx_prep_state, flags),
+        offsetof(mpx_group_batch, decided), offsetof(mpx_group_batch, n_decided));
       return 0;
     }"""
     import tempfile
@@ -79,6 +79,24 @@ def test_struct_sizes_match_header():
     assert offs[0] == R.ACCEPT_REPLY.fields["ok"][1]
     assert offs[1] == R.PREP_STATE.fields["flags"][1]
     assert offs[2] == _lib.MpxGroupBatch.decided.offset
+    assert offs[3] == _lib.MpxGroupBatch.n_decided.offset
+
+
+def test_runtime_info_names_the_bound_runtimes():
+    """libmpx.so reports the HIP / RCCL it is bound to (bench.py records it in its JSON line)"""
+    info = _lib.runtime_info()
+    assert info["hip_runtime"] > 0 and info["rccl"] > 0
+    assert "libamdhip64" in info["hip_path"] and "librccl" in info["rccl_path"]
+
+
+def test_no_device_utilities_fail_cleanly():
+    lib = _lib.load()
+    p = C.c_void_p()
+    assert lib.mpx_dev_alloc(None, 16, C.byref(p)) == R.E_INVAL
+    assert lib.mpx_stream_create(None, C.byref(p)) == R.E_INVAL
+    assert lib.mpx_step_allreduce_dev(None, None, 0, None, 0, None) == R.E_INVAL
+    assert lib.mpx_replay_durable(None, None, 0, 0, 0, None, None, None, None, None, None) == \
+        R.E_INVAL
 
 
 def test_product_does_not_reference_oracle():

@@ -85,3 +85,42 @@ def test_rank_block_equals_global_slice():
     assert np.array_equal(full["recs"][5 * 32 * 4:11 * 32 * 4], part["recs"])
     assert np.array_equal(full["key"][5 * 32 * 4:11 * 32 * 4], part["key"])
     assert np.array_equal(full["op"][5 * 32 * 4:11 * 32 * 4], part["op"])
+
+
+def _ranks_worker(rank, world, port, q):
+    """bench.Ranks over gloo: RCCL unique-id broadcast, barrier, max over ranks"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    import bench
+    rk = bench.Ranks()
+    try:
+        uid = rk.bcast(bytes(range(128)) if rank == 0 else None)
+        rk.barrier()
+        q.put((rank, uid, rk.max(1.5 * (rank + 1))))
+    finally:
+        rk.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_ranks_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ranks_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, uid, mx in got:
+        assert uid == bytes(range(128)) and mx == 1.5 * world
+
+
+def test_strong_scaling_partition_covers_groups():
+    """--scaling strong: block ranges of groups_total over P ranks tile [0, G) exactly"""
+    for g_total in (65536, 1000, 7):
+        for world in (1, 2, 4, 8):
+            rs = [shard.block_range(g_total, world, r) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == g_total
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))

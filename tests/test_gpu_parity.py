@@ -227,7 +227,7 @@ def test_conflict_batch(mk_engine):
 # ---- fused group step (config 5 shape) ----------------------------------------------------------
 def _cmp_group(got, want, G, K):
     for f in ("committed_out", "executed_out", "peer_out", "ret", "conf_prev", "kv_cnt",
-              "decided"):
+              "decided", "n_decided"):
         a, b = got[f], want[f]
         bad = np.nonzero(a != b)[0]
         assert len(bad) == 0, f"{f} differs at {bad[:8]}: {a[bad[:5]]} vs {b[bad[:5]]}"

@@ -16,6 +16,7 @@ import pytest
 from oracle_lib import Oracle, OracleError
 from minpaxos_amd import records as R
 from minpaxos_amd import synth
+from minpaxos_amd.devbuf import Arena
 
 
 def durable_log(n, inst_cap, seed, dup=True):
@@ -82,6 +83,20 @@ def test_encode_replay_round_trip():
     assert cu == (int(com.max()) if len(com) else -1)
 
 
+def test_oracle_chunked_replay_matches_whole():
+    """rec_base + carried last_rec: chunked replay == one pass (the ADVICE r1 'last record wins
+    across chunks' case)"""
+    o = Oracle()
+    log = durable_log(900, 120, 31)
+    whole = o.replay_durable(log, 120)
+    last, db, cu = None, 0, -1
+    for a, b in ((0, 300), (300, 301), (301, 900)):
+        r = o.replay_durable(log[a * 29:b * 29], 120, db, cu, rec_base=a, last_rec=last)
+        last, db, cu = r[4], r[5], r[6]
+    assert np.array_equal(last, whole[4]) and (db, cu) == tuple(whole[5:])
+    assert np.array_equal(last, np.array(go_replay(log, 120, 0, -1)[2], np.int32))
+
+
 def test_oracle_errors():
     o = Oracle()
     log = durable_log(10, 16, 6)
@@ -122,42 +137,6 @@ def test_replay_round_trip_engine(mk_engine):
     assert np.array_equal(last[recs["inst_no"]], np.arange(n))
 
 
-class _Hip:
-    """Device buffers through the HIP runtime libmpx.so is bound to in this process (its
-    libamdhip64.so.7, already loaded with the engine: /opt/rocm's, or torch's when torch came
-    first). torch.cuda cannot be used here: once the engine has initialised a runtime that is not
-    torch's, torch finds no device."""
-
-    def __init__(self):
-        import ctypes as C
-        import os
-        self.C = C
-        self.h = C.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD | os.RTLD_GLOBAL)
-        self.live = []
-
-    def put(self, a):
-        C = self.C
-        a = np.ascontiguousarray(a)
-        p = C.c_void_p()
-        assert self.h.hipMalloc(C.byref(p), C.c_size_t(max(a.nbytes, 16))) == 0
-        self.live.append(p)
-        if a.nbytes:
-            assert self.h.hipMemcpy(p, a.ctypes.data_as(C.c_void_p), C.c_size_t(a.nbytes), 1) == 0
-        return p.value
-
-    def get(self, ptr, like):
-        C = self.C
-        out = np.empty_like(like)
-        if out.nbytes:
-            assert self.h.hipMemcpy(out.ctypes.data_as(C.c_void_p), C.c_void_p(ptr),
-                                    C.c_size_t(out.nbytes), 2) == 0
-        return out
-
-    def free(self):
-        for p in self.live:
-            self.h.hipFree(p)
-
-
 @pytest.mark.gpu
 def test_replay_errors_and_dev(mk_engine):
     from minpaxos_amd.engine import MpxError
@@ -167,22 +146,46 @@ def test_replay_errors_and_dev(mk_engine):
         e.replay_durable(log[:-3], 600)
     with pytest.raises(MpxError):
         e.replay_durable(log, 100)
-    # device form: caller-initialised slots, scalars in HBM
-    n, cap = 1000, 600
+    # no instance space at all: the first record is already a panic in the reference
+    with pytest.raises(MpxError) as ei:
+        e.replay_durable(log, 0)
+    assert ei.value.code == R.E_NIL_INSTANCE
+    # device form: caller-initialised slots, scalars in HBM (buffers from the engine's runtime)
+    cap = 600
     want = o.replay_durable(log, cap)
-    hip = _Hip()
-    try:
+    with Arena(e) as hip:
         d_log = hip.put(log)
         d = [hip.put(np.zeros_like(w)) for w in want[:4]]
         d_last = hip.put(np.full(cap, -1, np.int32))
         d_sc = hip.put(np.array([0, -1], np.int32))
-        e.replay_durable_dev(d_log, len(log), cap, *d, d_last, d_sc)
+        e.replay_durable_dev(d_log.ptr, len(log), cap, *[x.ptr for x in d], d_last.ptr, d_sc.ptr)
         e.synchronize()
-        for ptr, w in zip(d, want[:4]):
-            assert np.array_equal(hip.get(ptr, w), w)
-        assert np.array_equal(hip.get(d_last, want[4]), want[4])
-        assert hip.get(d_sc, np.zeros(2, np.int32)).tolist() == [want[5], want[6]]
+        for x, w in zip(d, want[:4]):
+            assert np.array_equal(hip.get(x), w)
+        assert np.array_equal(hip.get(d_last), want[4])
+        assert hip.get(d_sc).tolist() == [want[5], want[6]]
         with pytest.raises(MpxError):  # misaligned device log
-            e.replay_durable_dev(d_log + 1, 29, cap, *d, d_last, d_sc)
-    finally:
-        hip.free()
+            e.replay_durable_dev(d_log.ptr + 1, 29, cap, *[x.ptr for x in d], d_last.ptr, d_sc.ptr)
+        with pytest.raises(MpxError) as ei:  # inst_cap 0 with records: E_NIL_INSTANCE, any history
+            e.replay_durable_dev(d_log.ptr, 29, 0, *[x.ptr for x in d], d_last.ptr, d_sc.ptr)
+        assert ei.value.code == R.E_NIL_INSTANCE
+
+
+@pytest.mark.gpu
+def test_replay_chunked(mk_engine):
+    """a store replayed in chunks (rec_base = the chunk's first file record, last_rec carried):
+    the same slots and watermarks as one call over the whole file, so a later chunk's record
+    wins its instance even where an earlier chunk named it at a higher in-chunk index"""
+    e, o = mk_engine(5, R.MODE_MIN), Oracle()
+    n, cap = 5000, 700
+    log = durable_log(n, cap, 21)
+    whole = o.replay_durable(log, cap, 3, -1)
+    for cuts in ((0, 1, 257, 2600, n), (0, 4096, n), (0, 999, 1000, n)):
+        last, db, cu = None, 3, -1
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            part = log[a * 29:b * 29]
+            got = e.replay_durable(part, cap, db, cu, rec_base=a, last_rec=last)
+            want = o.replay_durable(part, cap, db, cu, rec_base=a, last_rec=last)
+            assert np.array_equal(got[4], want[4]) and got[5:] == want[5:]
+            last, db, cu = got[4], got[5], got[6]
+        assert np.array_equal(last, whole[4]) and (db, cu) == tuple(whole[5:])
