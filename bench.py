@@ -26,6 +26,9 @@ The other single-GPU configurations of BASELINE.json are kernel benches of their
   apply       config 4: batched KV apply, 64M PUT/GET over 1M keys (mpx_apply), --dist uniform|zipf
   conflict    state.ConflictBatch of consecutive instances of the config-4 commands, B = 4
   decode      SURVEY §8(f) rank 1: peer-stream framing + AcceptReply decode of the config-2 replies
+              (fixed-size frames; stops at the first variable-length message)
+  stream      SURVEY §8(f) rank 1, full: a leader's stream with PrepareReplies mixed in
+              (--mode min|classic wire, --prepare-every K, --prep-cmds n), every frame decoded
   fanout      SURVEY §8(f) rank 2: ProposeReplyTS fan-out of 64M replies over --clients connections
   log         SURVEY §8(f) ranks 3/4: instance-log encoding of 16M committed instances x 4 commands
   replay      SURVEY §8(f) rank 3 (read side): durable-log replay of 16M 29-byte records
@@ -85,7 +88,11 @@ def parse():
     ap.add_argument("--traffic-json", default="")
     ap.add_argument("--workload", default="step",
                     choices=["step", "tally", "prepare", "prepare_min", "apply", "conflict",
-                             "decode", "fanout", "log", "replay"])
+                             "decode", "stream", "fanout", "log", "replay"])
+    ap.add_argument("--prepare-every", type=int, default=4096,
+                    help="stream: a PrepareReply before every K-th AcceptReply (0 = none)")
+    ap.add_argument("--prep-cmds", type=int, default=1,
+                    help="stream: Commands carried by each PrepareReply")
     ap.add_argument("--log-format", default="catchup", choices=["catchup", "durable"])
     ap.add_argument("--clients", type=int, default=1024, help="fanout: client connections")
     ap.add_argument("--instances", type=int, default=1 << 24, help="tally / prepare: instances")
@@ -822,6 +829,59 @@ def kernel_bench(a, rk):
                          f"getDataFromStableStore loop, one thread, {secs:.1f} s timed"}
         workload = (f"replay (durable): {I} records x 1 command, {L} bytes, instNo "
                     + ("drawn with repeats over I/2 slots" if a.replay_dups else "a permutation"))
+    elif a.workload == "stream":
+        from minpaxos_amd import wire
+        I = a.instances
+        recs, _ = synth.accept_replies(I, N, 0.7, seed=42)
+        buf = wire.leader_stream(mode, recs, seed=61, prepare_every=a.prepare_every,
+                                 n_cmds=a.prep_cmds)
+        L = len(buf)
+        o = OL.Oracle(N, mode)
+        w = o.decode_stream(buf)
+        n_ar, n_pr, n_var, n_oth = (len(x) for x in w[:4])
+        d_buf = put(buf)
+        d_ar = ar.empty(max(n_ar, 1), R.ACCEPT_REPLY)
+        pdt = R.PREPARE_REPLY_MIN if mode == R.MODE_MIN else R.PREPARE_REPLY
+        d_pr = ar.empty(max(n_pr, 1), pdt)
+        d_var = ar.empty(max(n_var, 1), R.VAR_FRAME)
+        d_oth = ar.empty(max(n_oth, 1), R.PEER_FRAME)
+        d_res = ar.full(1, R.STREAM_RESULT, 0)
+        out = _lib.MpxDecodeOut(d_ar.ptr, n_ar, d_pr.ptr, n_pr, d_var.ptr, n_var, d_oth.ptr, n_oth)
+        eng.decode_stream_reserve(L)
+        t_gen = time.time() - t_gen
+        wall, ms = _timed(eng, a.steps, a.warmup,
+                          lambda: eng.decode_stream_dev(d_buf.ptr, L, 0, out, d_res.ptr,
+                                                        eng.stream),
+                          before=lambda: eng.memset(d_res.ptr, 0, d_res.nbytes))
+        # stream read once, records written once
+        alg = L + n_ar * 16 + n_pr * pdt.itemsize + n_var * 32 + n_oth * 8
+        units, unit = n_ar + n_pr, "replies/s"
+        kernel = "mpx_decode_stream pipeline"
+        got = [get(d_ar, n_ar), get(d_pr, n_pr), get(d_var, n_var), get(d_oth, n_oth), get(d_res)[0]]
+        bit_exact = all(g.tobytes() == x.tobytes() for g, x in zip(got[:4], w[:4])) and all(
+            int(got[4][f]) == int(w[4][f]) for f in ("consumed", "n_accept_replies",
+                                                     "n_prepare_replies", "n_var", "n_other",
+                                                     "stop_reason", "stop_code"))
+        parity = {"frames_checked": n_ar + n_var + n_oth, "bytes": L, "bit_exact": bool(bit_exact)}
+        car = np.zeros(max(n_ar, 1), R.ACCEPT_REPLY)
+        cpr = np.zeros(max(n_pr, 1), pdt)
+        cvar = np.zeros(max(n_var, 1), R.VAR_FRAME)
+        coth = np.zeros(max(n_oth, 1), R.PEER_FRAME)
+        cres = np.zeros(1, R.STREAM_RESULT)
+        cout = _lib.MpxDecodeOut(car.ctypes.data, n_ar, cpr.ctypes.data, n_pr, cvar.ctypes.data,
+                                 n_var, coth.ctypes.data, n_oth)
+
+        def cpu_once():
+            t0 = time.perf_counter()
+            lib.orc_decode_stream(mode, buf.ctypes.data, L, C.byref(cout), cres.ctypes.data)
+            return time.perf_counter() - t0
+        secs, reps = _cpu_loop(cpu_once)
+        cpu = {"value": (n_ar + n_pr) * reps / secs, "unit": unit, "cores": 1, "kind": "port",
+               "sample": f"the full stream ({L} bytes) x {reps} through the oracle's "
+                         f"replicaListener + Unmarshal loop, one thread, {secs:.1f} s timed"}
+        workload = (f"stream ({a.mode} wire): {n_ar} AcceptReplies + {n_pr} PrepareReplies "
+                    f"({a.prep_cmds} Commands each, one per {a.prepare_every} AcceptReplies) + "
+                    f"{n_oth} Beacons, {L} bytes")
     else:  # decode
         I = a.instances
         recs, _ = synth.accept_replies(I, N, 0.7, seed=42)

@@ -394,6 +394,82 @@ int mpx_decode_peer_stream_dev(mpx_engine* eng, const uint8_t* d_buf, size_t len
                                mpx_accept_reply* d_ar, size_t ar_cap, mpx_peer_frame* d_other,
                                size_t other_cap, mpx_decode_result* d_res, void* stream);
 
+/* ---- full peer-stream decode: fixed AND variable-length frames, MIN or CLASSIC wire ------
+ * mpx_decode_stream frames one connection's bytes with the framing of the engine's protocol
+ * (mpx_config.mode): bareminpaxos registers minpaxosproto messages (bareminpaxos.go:108-113),
+ * paxos registers paxosproto messages (paxos.go:93-98), both as codes 8..13 in the order
+ * Prepare, Accept, Commit, CommitShort, PrepareReply, AcceptReply. Body lengths:
+ *                   MIN (minpaxosprotomarsh.go)            CLASSIC (paxosprotomarsh.go)
+ *   6/7 Beacon      8                                        8
+ *   8  Prepare      12 (:259-270)                            13 (:76-87)
+ *   9  Accept       16 + V(n) + 17n + V(m) + m Instances     12 + V(n) + 17n (:244-270)
+ *                   (:470-507)
+ *   10 Commit       12 + V(n) + 17n (:648-672)               12 + V(n) + 17n (:403-430)
+ *   11 CommitShort  16 (:737-749)                            16 (:492-503)
+ *   12 PrepareReply 17 + V(n) + 17n + V(m) + m Instances     9 + V(n) + 17n (:152-176)
+ *                   (:352-387)
+ *   13 AcceptReply  13 (:568-580)                            9 (:324-338)
+ * V(x) is a Go binary.PutVarint (zig-zag, 1..10 bytes); an Instance is 8 + V(k) + 17k bytes
+ * (:126-153); 17 bytes is one state.Command (statemarsh.go:21-37). Every other code is a 1-byte
+ * frame (genericsmr.go:440-442).
+ * Outputs, each in stream order:
+ *   AcceptReply  -> mpx_accept_reply (CLASSIC: id = -1, the wire carries no Id)
+ *   PrepareReply -> mpx_prepare_reply_min (MIN) / mpx_prepare_reply (CLASSIC) with value_id =
+ *                   the index of the frame's mpx_var_frame (its Command slice), AND an
+ *                   mpx_var_frame
+ *   Accept / Commit -> mpx_var_frame (the host unmarshals them from the byte ranges)
+ *   other fixed-size frames -> mpx_peer_frame                                               */
+typedef struct mpx_var_frame {
+    uint32_t offset;      /* the frame's code byte                                          */
+    uint32_t length;      /* code byte included                                            */
+    uint32_t n_cmds;      /* len(Command)                                                   */
+    uint32_t cmds_off;    /* first 17-byte Command                                          */
+    uint32_t n_log;       /* len(CatchUpLog) (MIN Accept / PrepareReply), else 0              */
+    uint32_t log_off;     /* first Instance of the CatchUpLog (end of Command if n_log == 0)  */
+    uint8_t code;
+    uint8_t pad[7];
+} mpx_var_frame; /* 32 B */
+
+typedef struct mpx_decode_out {
+    mpx_accept_reply* ar;     size_t ar_cap;
+    void* prep;               size_t prep_cap; /* mpx_prepare_reply_min[] (MIN) or
+                                                  mpx_prepare_reply[] (CLASSIC)              */
+    mpx_var_frame* var;       size_t var_cap;
+    mpx_peer_frame* other;    size_t other_cap;
+} mpx_decode_out;
+
+#define MPX_DECODE_MALFORMED 3 /* a varint overflows 64 bits (Unmarshal returns an error and
+                                  replicaListener stops, genericsmr.go:433-437) or a slice
+                                  length is negative (make panics)                          */
+#define MPX_DECODE_LONG 4      /* _dev only: the frame at `consumed` ends more than
+                                  MPX_DECODE_WINDOW bytes past the 128-byte chunk it starts
+                                  in; it IS decoded (counted, records written) and the chain
+                                  resumes at `next`: call again with start = next            */
+#define MPX_DECODE_WINDOW 64
+
+typedef struct mpx_stream_result {
+    uint64_t consumed;          /* stop position (len at MPX_DECODE_END)                     */
+    uint64_t next;              /* MPX_DECODE_LONG: where the next frame starts              */
+    uint64_t n_accept_replies;  /* totals over the stream so far (in/out for the _dev form)  */
+    uint64_t n_prepare_replies;
+    uint64_t n_var;
+    uint64_t n_other;
+    int32_t stop_reason;        /* MPX_DECODE_END / PARTIAL / MALFORMED (/ LONG, _dev)       */
+    int32_t stop_code;          /* code byte at `consumed`, -1 at MPX_DECODE_END             */
+} mpx_stream_result; /* 56 B */
+
+/* host pointers, synchronous: the whole buffer (long frames included); res out            */
+int mpx_decode_stream(mpx_engine* eng, const uint8_t* buf, size_t len,
+                      const mpx_decode_out* out, mpx_stream_result* res);
+/* scratch for _dev calls on buffers of up to max_len bytes (grows only)                    */
+int mpx_decode_stream_reserve(mpx_engine* eng, size_t max_len);
+/* device form: frames d_buf[start, len) (start = 0, or a previous call's res.next) and
+ * appends records at the indices the counts in *d_res (in/out: zero it for a new stream)
+ * give; one call stops at the first frame that is a terminal (END / PARTIAL / MALFORMED) or
+ * LONG. `out` is a host struct of device pointers.                                         */
+int mpx_decode_stream_dev(mpx_engine* eng, const uint8_t* d_buf, size_t len, size_t start,
+                          const mpx_decode_out* out, mpx_stream_result* d_res, void* stream);
+
 /* ---- client reply fan-out -----------------------------------------
  * One reply per executed (or decided) command, in execution order: the proposing client's
  * connection index, and the ProposeReplyTS fields the leader fills from

@@ -29,6 +29,11 @@ class MpxGroupBatch(C.Structure):
             "kv_key_out", "kv_val_out", "decided", "n_decided")]
 
 
+class MpxDecodeOut(C.Structure):
+    _fields_ = [("ar", _p), ("ar_cap", _sz), ("prep", _p), ("prep_cap", _sz), ("var", _p),
+                ("var_cap", _sz), ("other", _p), ("other_cap", _sz)]
+
+
 # name -> (restype, argtypes); every symbol of include/mpx.h
 SIGNATURES = {
     "mpx_abi_version": (C.c_int, []),
@@ -63,6 +68,9 @@ SIGNATURES = {
     "mpx_decode_peer_stream": (C.c_int, [_p, _p, _sz, _p, _sz, _p, _sz, _p]),
     "mpx_decode_reserve": (C.c_int, [_p, _sz]),
     "mpx_decode_peer_stream_dev": (C.c_int, [_p, _p, _sz, _p, _sz, _p, _sz, _p, _p]),
+    "mpx_decode_stream": (C.c_int, [_p, _p, _sz, C.POINTER(MpxDecodeOut), _p]),
+    "mpx_decode_stream_reserve": (C.c_int, [_p, _sz]),
+    "mpx_decode_stream_dev": (C.c_int, [_p, _p, _sz, _sz, C.POINTER(MpxDecodeOut), _p, _p]),
     "mpx_encode_replies": (C.c_int, [_p, _p, _sz, C.c_uint32, C.c_uint8, _i32, _p, _p]),
     "mpx_encode_replies_reserve": (C.c_int, [_p, _sz]),
     "mpx_encode_replies_dev": (C.c_int, [_p, _p, _sz, C.c_uint32, C.c_uint8, _i32, _p, _p, _p]),

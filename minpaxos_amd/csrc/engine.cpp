@@ -42,6 +42,10 @@ struct mpx_engine {
     // peer stream decode: staging (bytes, AcceptReplies, other frames, result) + scratch
     DevBuf dec[4];
     DevBuf decode_work;
+    // full stream decode: staging (bytes, AcceptReplies, PrepareReplies, var frames, other,
+    // result) + scratch
+    DevBuf sd[6];
+    DevBuf stream_work;
     // client reply fan-out: staging (records, bytes, offsets) + scratch
     DevBuf fan[3];
     DevBuf fan_work;
@@ -232,6 +236,9 @@ int mpx_close(mpx_engine* e) {
     for (auto& x : e->dec)
         if (x.p) (void)hipFree(x.p);
     if (e->decode_work.p) (void)hipFree(e->decode_work.p);
+    for (auto& x : e->sd)
+        if (x.p) (void)hipFree(x.p);
+    if (e->stream_work.p) (void)hipFree(e->stream_work.p);
     for (auto& x : e->fan)
         if (x.p) (void)hipFree(x.p);
     if (e->fan_work.p) (void)hipFree(e->fan_work.p);
@@ -812,6 +819,100 @@ int mpx_decode_peer_stream(mpx_engine* e, const uint8_t* buf, size_t len, mpx_ac
                                    sizeof(mpx_accept_reply)));
     CK(d2h(e, other, e->dec[2].p, std::min<uint64_t>(res->n_other, other_cap) *
                                       sizeof(mpx_peer_frame)));
+    return finish(e);
+}
+
+// ---- §8(f) rank 1, full: fixed and variable-length frames -------------------------------------
+namespace {
+size_t prep_rec_bytes(const mpx_engine* e) {
+    return e->cfg.mode == MPX_MODE_MIN ? sizeof(mpx_prepare_reply_min) : sizeof(mpx_prepare_reply);
+}
+}  // namespace
+
+int mpx_decode_stream_reserve(mpx_engine* e, size_t max_len) {
+    if (!e) return MPX_E_INVAL;
+    if (max_len > MPX_DECODE_MAX_BYTES)
+        return fail(e, MPX_E_UNSUPPORTED, "decode buffers are limited to 2^31-1 bytes per call");
+    CK(begin(e));
+    GROW(e, e->stream_work, mpx::stream_work_bytes(max_len));
+    return finish(e);
+}
+
+int mpx_decode_stream_dev(mpx_engine* e, const uint8_t* d_buf, size_t len, size_t start,
+                          const mpx_decode_out* out, mpx_stream_result* d_res, void* stream) {
+    if (!e) return MPX_E_INVAL;
+    if (!out || !d_res || (len && !d_buf) || (out->ar_cap && !out->ar) ||
+        (out->prep_cap && !out->prep) || (out->var_cap && !out->var) ||
+        (out->other_cap && !out->other))
+        return fail(e, MPX_E_INVAL, "null or invalid argument");
+    if (len > MPX_DECODE_MAX_BYTES)
+        return fail(e, MPX_E_UNSUPPORTED, "decode buffers are limited to 2^31-1 bytes per call");
+    if (start > len) return fail(e, MPX_E_INVAL, "start is past the end of the buffer");
+    if ((uintptr_t)d_buf % 16)
+        return fail(e, MPX_E_INVAL, "d_buf must be 16-byte aligned (tiles load 16 B vectors)");
+    if (e->stream_work.cap < mpx::stream_work_bytes(len))
+        return fail(e, MPX_E_INVAL,
+                    "mpx_decode_stream_dev: call mpx_decode_stream_reserve(len) first (the dev "
+                    "entry point never allocates)");
+    const mpx::StreamOuts o{out->ar, out->ar_cap, out->prep, out->prep_cap, out->var,
+                            out->var_cap, out->other, out->other_cap};
+    HIPCHK(e, mpx::launch_decode_stream(e->cfg.mode, 0, d_buf, len, start, o, d_res,
+                                        e->stream_work.p, e->stream_work.cap, pick(e, stream)));
+    return MPX_OK;
+}
+
+int mpx_decode_stream(mpx_engine* e, const uint8_t* buf, size_t len, const mpx_decode_out* out,
+                      mpx_stream_result* res) {
+    if (!e) return MPX_E_INVAL;
+    if (!out || !res || (len && !buf) || (out->ar_cap && !out->ar) ||
+        (out->prep_cap && !out->prep) || (out->var_cap && !out->var) ||
+        (out->other_cap && !out->other))
+        return fail(e, MPX_E_INVAL, "null or invalid argument");
+    if (len > MPX_DECODE_MAX_BYTES)
+        return fail(e, MPX_E_UNSUPPORTED, "decode buffers are limited to 2^31-1 bytes per call");
+    const size_t pb = prep_rec_bytes(e);
+    CK(begin(e));
+    GROW(e, e->sd[0], len);
+    GROW(e, e->sd[1], out->ar_cap * sizeof(mpx_accept_reply));
+    GROW(e, e->sd[2], out->prep_cap * pb);
+    GROW(e, e->sd[3], out->var_cap * sizeof(mpx_var_frame));
+    GROW(e, e->sd[4], out->other_cap * sizeof(mpx_peer_frame));
+    GROW(e, e->sd[5], sizeof(mpx_stream_result));
+    GROW(e, e->stream_work, mpx::stream_work_bytes(len));
+    CK(h2d(e, e->sd[0].p, buf, len));
+    const mpx_decode_out d{(mpx_accept_reply*)e->sd[1].p, out->ar_cap, e->sd[2].p, out->prep_cap,
+                           (mpx_var_frame*)e->sd[3].p, out->var_cap,
+                           (mpx_peer_frame*)e->sd[4].p, out->other_cap};
+    mpx_stream_result r;
+    memset(&r, 0, sizeof(r));
+    CK(h2d(e, e->sd[5].p, &r, sizeof(r)));
+    // one call per frame longer than the in-map window (MPX_DECODE_LONG); after one, windows
+    // of the buffer (a PARTIAL stop at a window's end just continues) keep each call short
+    size_t start = 0, window = len;
+    for (;;) {
+        const size_t end = std::min(len, start + window);
+        CK(mpx_decode_stream_dev(e, (const uint8_t*)e->sd[0].p, end, start, &d,
+                                 (mpx_stream_result*)e->sd[5].p, e->stream));
+        CK(d2h(e, &r, e->sd[5].p, sizeof(r)));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        if (r.stop_reason == MPX_DECODE_LONG && r.next <= len) {
+            start = r.next;
+            window = 1u << 18;
+        } else if (r.stop_reason == MPX_DECODE_PARTIAL && end < len) {
+            start = r.consumed;
+            window = std::min<size_t>(window * 2, len);
+        } else {
+            break;
+        }
+    }
+    *res = r;
+    CK(d2h(e, out->ar, e->sd[1].p, std::min<uint64_t>(r.n_accept_replies, out->ar_cap) *
+                                      sizeof(mpx_accept_reply)));
+    CK(d2h(e, out->prep, e->sd[2].p, std::min<uint64_t>(r.n_prepare_replies, out->prep_cap) * pb));
+    CK(d2h(e, out->var, e->sd[3].p, std::min<uint64_t>(r.n_var, out->var_cap) *
+                                       sizeof(mpx_var_frame)));
+    CK(d2h(e, out->other, e->sd[4].p, std::min<uint64_t>(r.n_other, out->other_cap) *
+                                         sizeof(mpx_peer_frame)));
     return finish(e);
 }
 

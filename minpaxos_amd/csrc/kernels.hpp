@@ -89,6 +89,23 @@ hipError_t launch_decode_peer_stream(const uint8_t* buf, uint64_t len, mpx_accep
                                      mpx_decode_result* res, void* work, uint64_t work_bytes,
                                      hipStream_t stream);
 
+// ---- full peer-stream decode (mpx_decode_stream) -----------------------------------------
+struct StreamOuts {
+    mpx_accept_reply* ar;
+    uint64_t ar_cap;
+    void* prep;
+    uint64_t prep_cap;
+    mpx_var_frame* var;
+    uint64_t var_cap;
+    mpx_peer_frame* oth;
+    uint64_t oth_cap;
+};
+uint64_t stream_work_bytes(uint64_t len);
+// frames buf[start, len) with the proto's framing; legacy = stop at variable-length messages
+hipError_t launch_decode_stream(int proto, int legacy, const uint8_t* buf, uint64_t len,
+                                uint64_t start, const StreamOuts& outs, mpx_stream_result* res,
+                                void* work, uint64_t work_bytes, hipStream_t stream);
+
 // ---- client reply fan-out (mpx_encode_replies) -------------------------------------------
 uint64_t fanout_work_bytes(uint64_t n);
 hipError_t launch_encode_replies(const mpx_reply_rec* recs, uint64_t n, uint32_t n_clients,

@@ -1,0 +1,837 @@
+// stream.hip — full peer-stream framing: fixed AND variable-length frames, MIN or CLASSIC wire
+// (mpx_decode_stream, and mpx_decode_peer_stream as its MIN,
+// stop-at-variable special case).
+//
+// Reference: genericsmr.(*Replica).replicaListener src/genericsmr/genericsmr.go:402-446 reads a
+// connection as frames [code u8][body]; the body of a variable-length message (Accept, Commit,
+// PrepareReply) is a fixed header, a binary.PutVarint slice length, 17-byte Commands and, for
+// MIN Accept / PrepareReply, a CatchUpLog of Instances (8 bytes + V(k) + 17k each)
+// (minpaxosprotomarsh.go:126-153, :352-387, :470-507, :648-672; paxosprotomarsh.go:152-176,
+// :244-270, :403-430). Layout table in include/mpx.h.
+//
+// Framing is a chain: each frame's start depends on every earlier length. The engine makes it
+// data parallel with POSITION maps: a 128-byte chunk maps each entry offset e in [0, 64) (where
+// a frame that started before the chunk can end) to the offset its chain leaves the chunk at
+// (an entry of the next chunk), or to "terminal". A lane computes its chunk's map with a backward
+// DP over the chunk's bytes in LDS: D[p] = D[p + len(frame at p)]; a variable-length frame's
+// length comes from a bounded parse of its varints. Terminals are: the end of the buffer, a
+// frame running past it, a malformed varint / negative length, and a frame landing more than
+// 63 bytes into the next chunk (LONG: rare - catch-up logs, large batches). Maps compose
+// associatively: a workgroup reduces its 128 chunk maps to a 16 KB tile map, a group of 256
+// tile maps to a group map, one block walks the group maps from the entry, classifies the
+// terminal it reaches exactly, and the down-sweeps give every tile, then every chunk, its true
+// entry. The emit pass walks each chunk's frames on the true chain, counts them per record
+// kind, takes its output indices from a block scan plus a decoupled look-back across tiles,
+// and writes the records. A LONG terminal is decoded too and ends the call (MPX_DECODE_LONG):
+// the next call starts at its end (the host form loops).
+// HBM traffic per stream byte: 1 read (maps) + 1 read (emit) + 0.5 write + 0.5 read (the 64-byte
+// chunk maps), records written once.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace mpx {
+
+namespace {
+
+constexpr int kC = 128;                 // bytes per chunk (one lane)
+constexpr int kE = MPX_DECODE_WINDOW;   // entry offsets per chunk map
+constexpr int kTL = 128;                // chunks (lanes) per tile
+constexpr int kTB = kC * kTL;           // tile bytes
+constexpr int kGT = 256;                // tiles per group
+constexpr uint8_t kTerm = 0xFF;         // terminal (tree levels >= 1, tile / group maps)
+constexpr uint8_t kDeadE = 0xFF;        // no entry (past the stop)
+static_assert(kE == 64 && kE + kC <= 255, "u8 DP encoding: exit offsets, then terminals");
+
+enum { kOk = 0, kPartial = 1, kMalformed = 2, kBeyond = 3 };
+
+
+// fixed frame length by code (code byte included), 0 = variable-length message
+__device__ __forceinline__ uint32_t flen(uint32_t code, int proto) {
+    switch (code) {
+    case MPX_PEER_BEACON:
+    case MPX_PEER_BEACON_REPLY: return 9;
+    case MPX_PEER_PREPARE: return proto == MPX_MODE_MIN ? 13 : 14;
+    case MPX_PEER_COMMIT_SHORT: return 17;
+    case MPX_PEER_ACCEPT_REPLY: return proto == MPX_MODE_MIN ? 14 : 10;
+    case MPX_PEER_ACCEPT:
+    case MPX_PEER_COMMIT:
+    case MPX_PEER_PREPARE_REPLY: return 0;
+    default: return 1;
+    }
+}
+
+// bytes of the stream: an LDS-staged window [lo, hi) (relative positions), global otherwise
+struct Bytes {
+    const uint8_t* g;
+    const uint8_t* s;
+    uint64_t lo, hi;
+    __host__ __device__ __forceinline__ uint32_t operator()(uint64_t i) const {
+        return (i >= lo && i < hi) ? (uint32_t)s[i - lo] : (uint32_t)g[i];
+    }
+};
+
+struct VarInfo {
+    uint32_t len, n_cmds, cmds_off, n_log, log_off;  // offsets relative to the call's base
+};
+
+// binary.ReadVarint at *pos (len: end of the buffer; limit: give up past it)
+__host__ __device__ __forceinline__ int read_varint(const Bytes& by, uint64_t len, uint64_t limit,
+                                           uint64_t* pos, int64_t* out) {
+    uint64_t x = 0;
+    uint32_t s = 0;
+    for (int i = 0; i < 10; ++i) {
+        if (*pos >= len) return kPartial;
+        if (*pos >= limit) return kBeyond;
+        const uint32_t b = by((*pos)++);
+        if (b < 0x80u) {
+            if (i == 9 && b > 1u) return kMalformed;  // errOverflow
+            x |= (uint64_t)b << s;
+            *out = (int64_t)(x >> 1) ^ -(int64_t)(x & 1ull);
+            return kOk;
+        }
+        x |= (uint64_t)(b & 0x7fu) << s;
+        s += 7;
+    }
+    return kMalformed;
+}
+
+__host__ __device__ __forceinline__ int skip_cmds(uint64_t len, uint64_t limit, uint64_t* pos, int64_t n) {
+    if (n < 0) return kMalformed;  // make() panics
+    if ((uint64_t)n > (len - *pos) / 17) return kPartial;
+    *pos += 17 * (uint64_t)n;
+    return *pos > limit ? kBeyond : kOk;
+}
+
+// the variable-length message at p; the parse gives up (kBeyond) once it passes `limit`.
+// Returns the status in .st and the frame in .f (valid when .st == kOk).
+struct VarRes {
+    int st;
+    VarInfo f;
+};
+// the Command slice: where it starts and how long it is (header + V(n))
+struct VarHead {
+    int st;
+    uint32_t hdr_end, n;
+};
+__host__ __device__ __forceinline__ uint32_t var_hdr(uint32_t code, int proto) {
+    if (proto == MPX_MODE_MIN) return code == MPX_PEER_ACCEPT ? 16 : code == MPX_PEER_COMMIT ? 12 : 17;
+    return code == MPX_PEER_PREPARE_REPLY ? 9 : 12;
+}
+__host__ __device__ __forceinline__ VarHead var_head(const Bytes& by, uint64_t len,
+                                                     uint64_t limit, uint64_t p, int proto) {
+    VarHead h{kOk, 0, 0};
+    uint64_t pos = p + 1 + var_hdr(by(p), proto);
+    if (pos > len) { h.st = kPartial; return h; }
+    if (pos > limit) { h.st = kBeyond; return h; }
+    int64_t n = 0;
+    h.st = read_varint(by, len, limit, &pos, &n);
+    if (h.st == kOk && n < 0) h.st = kMalformed;
+    h.hdr_end = (uint32_t)pos;
+    h.n = (uint32_t)n;
+    return h;
+}
+// the variable-length message at p; the parse gives up (kBeyond) once it passes `limit`.
+// Returns the status in .st and the frame in .f (valid when .st == kOk).
+__host__ __device__ __forceinline__ VarRes parse_var(const Bytes& by, uint64_t len,
+                                                     uint64_t limit, uint64_t p, int proto) {
+    VarRes r{kOk, {0, 0, 0, 0, 0}};
+    const uint32_t code = by(p);
+    const VarHead h = var_head(by, len, limit, p, proto);
+    if (h.st != kOk) {
+        r.st = h.st;
+        return r;
+    }
+    uint64_t pos = h.hdr_end;
+    int st = skip_cmds(len, limit, &pos, (int64_t)h.n);
+    uint64_t log_off = pos;
+    int64_t m = 0;
+    if (st == kOk && proto == MPX_MODE_MIN && code != MPX_PEER_COMMIT) {  // CatchUpLog
+        st = read_varint(by, len, limit, &pos, &m);
+        if (st == kOk && m < 0) st = kMalformed;
+        if (st == kOk && (uint64_t)m > (len - pos) / 9) st = kPartial;
+        log_off = pos;
+        for (int64_t i = 0; st == kOk && i < m; ++i) {  // Instance: Ballot, Status, V(k), k Commands
+            if (pos + 8 > len) {
+                st = kPartial;
+                break;
+            }
+            pos += 8;
+            int64_t k = 0;
+            st = read_varint(by, len, limit, &pos, &k);
+            if (st == kOk) st = skip_cmds(len, limit, &pos, k);
+        }
+    }
+    r.st = st;
+    // the slice header again from its own parse (kept apart from the loop above)
+    const VarHead h2 = var_head(by, len, limit, p, proto);
+    r.f = VarInfo{(uint32_t)(pos - p), h2.n, h2.hdr_end, (uint32_t)m, (uint32_t)log_off};
+    return r;
+}
+
+struct SParams {
+    const uint8_t* buf;  // base of the call (16-byte aligned)
+    uint64_t len;        // bytes from base
+    uint64_t pos_base;   // offset of base in the caller's buffer (for record offsets)
+    uint32_t entry0;     // the chain starts at base + entry0 (< 16)
+    int proto;
+    int legacy;          // stop at variable-length messages (mpx_decode_peer_stream)
+};
+
+// ---- workspace ----------------------------------------------------------------------------
+struct Work {
+    uint8_t* cmap;             // [tiles * kTL][kE] chunk maps
+    uint8_t* tmap;             // [tiles][kE]
+    uint8_t* tent;             // [tiles] true entry (kDeadE past the stop)
+    uint8_t* gmap;             // [groups][kE]
+    uint8_t* gent;             // [groups]
+    unsigned long long* lb;    // [tiles][4] look-back words: status << 32 | count
+    uint32_t* ticket;
+    uint64_t* stop;            // [0] stop position, [1] next, [2] reason, [3..7] VarInfo of a
+                               // LONG stop frame, [8..11] the call's input counts
+};
+
+uint64_t n_tiles_of(uint64_t len) { return (len + kTB - 1) / kTB; }
+
+}  // namespace
+
+// ---- pass A: chunk maps and tile maps --------------------------------------------------------
+// frame length by code from a byte-lane table (codes 6..13; 0 = variable-length message,
+// anything else a 1-byte frame); the two wire formats differ in Prepare and AcceptReply
+constexpr uint64_t kLutMin = 9ull | (9ull << 8) | (13ull << 16) | (0ull << 24) | (0ull << 32) |
+                             (17ull << 40) | (0ull << 48) | (14ull << 56);
+constexpr uint64_t kLutClassic = 9ull | (9ull << 8) | (14ull << 16) | (0ull << 24) |
+                                 (0ull << 32) | (17ull << 40) | (0ull << 48) | (10ull << 56);
+__device__ __forceinline__ uint32_t lut_len(uint64_t lut, uint32_t code) {
+    const uint32_t i = code - (uint32_t)MPX_PEER_BEACON;
+    const uint32_t in = 0u - (uint32_t)(i < 8u);
+    return (((uint32_t)(lut >> ((i & 7u) * 8u)) & 0xFFu) & in) | (1u & ~in);
+}
+
+// Phase 1 (variable-length messages only): the bounded parse of every variable-message code of
+// the lane's chunk (bytes through L2), D[p] = its length if it lands no further than `lim`,
+// else 0 (terminal); the DP reads it back at p before writing D[p].
+__device__ __noinline__ void var_lengths(const uint8_t* g, uint64_t len, uint64_t c0,
+                                         uint64_t lim, int proto, uint64_t m_lo, uint64_t m_hi,
+                                         uint8_t* D) {
+    const Bytes by{g, nullptr, 0, 0};
+    for (int h = 0; h < 2; ++h) {
+        uint64_t m = h ? m_hi : m_lo;
+        while (m) {
+            const int p = __ffsll((long long)m) - 1 + 64 * h;
+            m &= m - 1;
+            const VarRes r = parse_var(by, len, lim, c0 + (uint64_t)p, proto);
+            D[p] = r.st == kOk ? (uint8_t)r.f.len : (uint8_t)0;  // len <= kC + kE
+        }
+    }
+}
+
+// Phase 2: the backward DP over the chunk's positions in registers: w[k] = D[p + 1 + k] (the
+// window of the next kE positions; past the chunk it holds the exit offsets 0..kE-1). A fixed
+// frame takes its successor's value from the window at a compile-time offset; a variable one
+// reads its length and its landing's value from the LDS mirror D (only when some lane of the
+// wave has a variable-message code at p). kEdge: the chunk runs into the end of the buffer.
+template <bool kEdge>
+__device__ __forceinline__ void chunk_dp(const uint32_t (&wd)[kC / 4], uint64_t c0, uint64_t len,
+                                         uint64_t lut, bool legacy, uint8_t* D) {
+    uint32_t w[kE];
+#pragma unroll
+    for (int k = 0; k < kE; ++k) w[k] = (uint32_t)k;  // D[kC + k] = exit offset k
+#pragma unroll
+    for (int p = kC - 1; p >= 0; --p) {
+        const uint32_t code = (wd[p >> 2] >> ((p & 3) * 8)) & 0xFFu;
+        const uint32_t fl = lut_len(lut, code);
+        const uint32_t term = (uint32_t)kE + (uint32_t)p;
+        // fixed lengths 1, 9, 10, 13, 14, 17
+        uint32_t v = (w[0] & (0u - (uint32_t)(fl == 1))) | (w[8] & (0u - (uint32_t)(fl == 9))) |
+                     (w[9] & (0u - (uint32_t)(fl == 10))) | (w[12] & (0u - (uint32_t)(fl == 13))) |
+                     (w[13] & (0u - (uint32_t)(fl == 14))) | (w[16] & (0u - (uint32_t)(fl == 17)));
+        const bool var = fl == 0;
+        uint32_t L = fl;
+        if (__ballot(var && !legacy)) {  // wave-uniform: the slow operands only when needed
+            L = var ? (uint32_t)D[p] : fl;
+            const uint32_t q = (uint32_t)p + L;
+            const uint32_t dq = D[q < (uint32_t)kC ? q : 0];
+            const uint32_t vv = L == 0 ? term
+                                : q < (uint32_t)kC ? dq
+                                : q < (uint32_t)(kC + kE) ? q - (uint32_t)kC : term;
+            v = var ? vv : v;
+        } else if (var) {
+            v = term;  // legacy: stop at variable-length messages
+            L = 0;
+        }
+        if (kEdge) {
+            const uint64_t a = c0 + (uint64_t)p;
+            if (a >= len || a + L > len) v = term;
+        }
+        D[p] = (uint8_t)v;
+#pragma unroll
+        for (int k = kE - 1; k > 0; --k) w[k] = w[k - 1];
+        w[0] = v;
+    }
+}
+
+// 16 groups of 8 chunks: G[g][e] = where entry e of chunk 8g leaves chunk 8g+7 (kTerm: a
+// terminal on the way); X[c][e] are chunk maps with terminals as kTerm or >= kE
+__device__ __forceinline__ void chunk_groups(const uint8_t* X, int xstride, uint8_t (*G)[kE]) {
+    for (int t = threadIdx.x; t < (kTL / 8) * kE; t += kTL) {
+        const int g = t / kE;
+        uint32_t x = (uint32_t)(t % kE);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const uint32_t y = x < (uint32_t)kE ? X[(8 * g + c) * xstride + x] : kTerm;
+            x = y < (uint32_t)kE ? y : kTerm;
+        }
+        G[g][t % kE] = (uint8_t)x;
+    }
+}
+
+__global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
+    __shared__ __attribute__((aligned(16))) uint8_t D[kTL][kC];  // var lengths, then the DP
+    __shared__ uint8_t G[kTL / 8][kE];
+    const int l = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kTB;
+    const uint64_t c0 = t0 + (uint64_t)l * kC;
+    uint32_t wd[kC / 4];
+    if (c0 + kC <= P.len) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(P.buf + c0);
+#pragma unroll
+        for (int i = 0; i < kC / 16; ++i) {
+            const uint4 v = s4[i];  // default policy: the emit pass reads the stream again
+            wd[4 * i] = v.x;
+            wd[4 * i + 1] = v.y;
+            wd[4 * i + 2] = v.z;
+            wd[4 * i + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < kC / 4; ++i) {
+            uint32_t x = 0;
+            for (int b = 0; b < 4; ++b) {
+                const uint64_t a = c0 + 4 * i + b;
+                if (a < P.len) x |= (uint32_t)P.buf[a] << (8 * b);
+            }
+            wd[i] = x;
+        }
+    }
+    const uint64_t lut = P.proto == MPX_MODE_MIN ? kLutMin : kLutClassic;
+    if (!P.legacy) {
+        uint64_t m_lo = 0, m_hi = 0;  // positions of variable-message codes
+#pragma unroll
+        for (int p = 0; p < kC; ++p) {
+            const uint32_t code = (wd[p >> 2] >> ((p & 3) * 8)) & 0xFFu;
+            const uint64_t bit = (uint64_t)(lut_len(lut, code) == 0) << (p & 63);
+            if (p < 64) m_lo |= bit; else m_hi |= bit;
+        }
+        if (m_lo | m_hi)
+            var_lengths(P.buf, P.len, c0, c0 + kC + kE - 1, P.proto, m_lo, m_hi, D[l]);
+    }
+    if (c0 + kC + 17 + kE > P.len)
+        chunk_dp<true>(wd, c0, P.len, lut, P.legacy != 0, D[l]);
+    else
+        chunk_dp<false>(wd, c0, P.len, lut, P.legacy != 0, D[l]);
+    {  // this chunk's map (64 bytes) for the emit pass and the walk
+        const uint4* src = reinterpret_cast<const uint4*>(D[l]);
+        uint4* dst = reinterpret_cast<uint4*>(W.cmap + ((uint64_t)blockIdx.x * kTL + l) * kE);
+#pragma unroll
+        for (int i = 0; i < kE / 16; ++i) dst[i] = src[i];
+    }
+    __syncthreads();
+    chunk_groups(&D[0][0], kC, G);
+    __syncthreads();
+    if (l < kE) {  // the tile map: entry l through the 16 group maps
+        uint32_t x = (uint32_t)l;
+#pragma unroll
+        for (int g = 0; g < kTL / 8; ++g) x = x == kTerm ? kTerm : G[g][x];
+        W.tmap[(uint64_t)blockIdx.x * kE + l] = (uint8_t)x;
+    }
+}
+
+// ---- pass B1: group maps (lane e walks entry e over the group's tile maps) --------------------
+__global__ __launch_bounds__(kE) void k_sd_group_maps(Work W, uint32_t n_tiles) {
+    __shared__ uint8_t S[kGT][kE];
+    const uint32_t g = blockIdx.x, first = g * kGT;
+    const uint32_t nt = min((uint32_t)kGT, n_tiles - first);
+    for (uint32_t i = threadIdx.x; i < nt * kE; i += blockDim.x)
+        (&S[0][0])[i] = W.tmap[(uint64_t)first * kE + i];
+    __syncthreads();
+    uint8_t e = (uint8_t)threadIdx.x;
+    for (uint32_t t = 0; t < nt && e != kTerm; ++t) e = S[t][e];
+    W.gmap[(uint64_t)g * kE + threadIdx.x] = e;
+}
+
+// ---- pass B2: the true chain over the group maps, then the exact stop ------------------------
+// One block: thread 0 walks (maps staged in LDS by the block). At the terminal group it descends
+// to the terminal tile, chunk and byte, classifies the frame there and writes the result.
+__global__ __launch_bounds__(64) void k_sd_walk(SParams P, Work W, uint32_t n_tiles,
+                                                 uint32_t n_groups, mpx_stream_result* res) {
+    __shared__ uint8_t S[kGT][kE];
+    __shared__ uint32_t st[3];  // entry, terminal group (n_groups = none), its entry
+    const int t = threadIdx.x;
+    if (t == 0) {
+        st[0] = P.entry0;
+        st[1] = n_groups;
+        st[2] = 0;
+        // the input counts, for the emit pass (which overwrites *res with the totals)
+        W.stop[8] = res->n_accept_replies;
+        W.stop[9] = res->n_prepare_replies;
+        W.stop[10] = res->n_var;
+        W.stop[11] = res->n_other;
+    }
+    for (uint32_t b0 = 0; b0 < n_groups; b0 += kGT) {
+        const uint32_t nb = min((uint32_t)kGT, n_groups - b0);
+        __syncthreads();
+        if (st[1] != n_groups) {  // past the terminal: the rest is dead
+            for (uint32_t g = t; g < nb; g += blockDim.x) W.gent[b0 + g] = kDeadE;
+            continue;
+        }
+        for (uint32_t i = t; i < nb * kE; i += blockDim.x)
+            (&S[0][0])[i] = W.gmap[(uint64_t)b0 * kE + i];
+        __syncthreads();
+        if (t == 0) {
+            uint32_t e = st[0], stop = st[1];
+            for (uint32_t g = 0; g < nb; ++g) {
+                if (stop != n_groups) {
+                    W.gent[b0 + g] = kDeadE;
+                    continue;
+                }
+                W.gent[b0 + g] = (uint8_t)e;
+                const uint8_t x = S[g][e];
+                if (x == kTerm) {
+                    stop = b0 + g;
+                    st[2] = e;
+                } else {
+                    e = x;
+                }
+            }
+            st[0] = e;
+            st[1] = stop;
+        }
+    }
+    __syncthreads();
+    // the terminal: every chain ends in one (at the latest the end of the buffer)
+    const uint32_t gs = st[1];
+    uint32_t e = st[2];
+    // terminal tile within group gs
+    const uint32_t first = gs * kGT, nt = min((uint32_t)kGT, n_tiles - first);
+    for (uint32_t i = t; i < nt * kE; i += blockDim.x)
+        (&S[0][0])[i] = W.tmap[(uint64_t)first * kE + i];
+    __syncthreads();
+    if (t == 0) {
+        uint32_t ts = first;
+        for (uint32_t k = 0; k < nt; ++k) {
+            const uint8_t x = S[k][e];
+            if (x == kTerm) {
+                ts = first + k;
+                break;
+            }
+            e = x;
+        }
+        st[0] = ts;
+        st[2] = e;
+    }
+    __syncthreads();
+    // terminal chunk within the tile (its 128 chunk maps, 8 KB, over S)
+    const uint32_t ts = st[0];
+    for (uint32_t i = t; i < (uint32_t)kTL * kE / 16; i += blockDim.x)
+        reinterpret_cast<uint4*>(&S[0][0])[i] =
+            reinterpret_cast<const uint4*>(W.cmap + (uint64_t)ts * kTL * kE)[i];
+    __syncthreads();
+    if (t == 0) {
+        e = st[2];
+        uint32_t cs = 0, v = 0;
+        for (uint32_t c = 0; c < (uint32_t)kTL; ++c) {
+            v = S[c][e];
+            if (v >= (uint32_t)kE) {
+                cs = c;
+                break;
+            }
+            e = v;
+        }
+        const uint64_t s = (uint64_t)ts * kTB + (uint64_t)cs * kC + (v - kE);  // terminal byte
+        int32_t why, code = -1;
+        uint64_t next = s;
+        VarInfo f{0, 0, 0, 0, 0};
+        if (s >= P.len) {
+            why = MPX_DECODE_END;
+        } else {
+            code = P.buf[s];
+            const uint32_t fl = flen((uint32_t)code, P.proto);
+            if (fl) {
+                why = MPX_DECODE_PARTIAL;  // a fixed frame past the end (the only fixed terminal)
+            } else if (P.legacy) {
+                why = MPX_DECODE_VARIABLE;
+            } else {
+                const VarRes r = parse_var(Bytes{P.buf, nullptr, 0, 0}, P.len, ~0ull, s, P.proto);
+                why = r.st == kOk ? MPX_DECODE_LONG : r.st == kPartial ? MPX_DECODE_PARTIAL
+                                                                      : MPX_DECODE_MALFORMED;
+                if (r.st == kOk) {
+                    f = r.f;
+                    next = s + f.len;
+                }
+            }
+        }
+        res->consumed = P.pos_base + (why == MPX_DECODE_END ? P.len : s);
+        res->next = P.pos_base + next;
+        res->stop_reason = why;
+        res->stop_code = code;
+        W.stop[0] = s;
+        W.stop[1] = next;
+        W.stop[2] = (uint64_t)(uint32_t)why;
+        W.stop[3] = f.len;
+        W.stop[4] = f.n_cmds;
+        W.stop[5] = f.cmds_off;
+        W.stop[6] = f.n_log;
+        W.stop[7] = f.log_off;
+    }
+}
+
+// ---- pass B3: tile entries inside each group ---------------------------------------------------
+__global__ __launch_bounds__(kE) void k_sd_tile_entries(Work W, uint32_t n_tiles) {
+    __shared__ uint8_t S[kGT][kE];
+    const uint32_t g = blockIdx.x, first = g * kGT;
+    const uint32_t nt = min((uint32_t)kGT, n_tiles - first);
+    const uint8_t r = W.gent[g];
+    if (r == kDeadE) {
+        for (uint32_t t = threadIdx.x; t < nt; t += blockDim.x) W.tent[first + t] = kDeadE;
+        return;
+    }
+    for (uint32_t i = threadIdx.x; i < nt * kE; i += blockDim.x)
+        (&S[0][0])[i] = W.tmap[(uint64_t)first * kE + i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint8_t e = r;
+        for (uint32_t t = 0; t < nt; ++t) {
+            W.tent[first + t] = e;
+            e = e == kDeadE ? kDeadE : S[t][e];  // kTerm == kDeadE: the tiles after are dead
+        }
+    }
+}
+
+// ---- pass C: chunk entries, counts, look-back, records ----------------------------------------
+struct Outs {
+    mpx_accept_reply* ar;
+    uint64_t ar_cap;
+    void* prep;
+    uint64_t prep_cap;
+    mpx_var_frame* var;
+    uint64_t var_cap;
+    mpx_peer_frame* oth;
+    uint64_t oth_cap;
+};
+
+__device__ __forceinline__ int32_t le32(const Bytes& by, uint64_t i) {
+    return (int32_t)(by(i) | (by(i + 1) << 8) | (by(i + 2) << 16) | (by(i + 3) << 24));
+}
+
+__global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint32_t n_tiles,
+                                                 mpx_stream_result* res) {
+    __shared__ __attribute__((aligned(16))) uint8_t B[kTB + kE];
+    __shared__ __attribute__((aligned(16))) uint8_t X[kTL][kE];  // the tile's chunk maps
+    __shared__ uint8_t G[kTL / 8][kE];
+    __shared__ uint8_t GE[kTL / 8];
+    __shared__ uint8_t En[kTL];
+    __shared__ uint32_t tile_s;
+    __shared__ uint32_t wsum[kTL / kWave][4];
+    __shared__ uint32_t pre_s[4];
+    const int l = threadIdx.x;
+    if (l == 0) tile_s = atomicAdd(W.ticket, 1u);  // tiles in dispatch order (look-back)
+    __syncthreads();
+    const uint32_t tile = tile_s;
+    const uint8_t ent = W.tent[tile];
+    if (ent == kDeadE) return;  // every tile after the stop tile, never one before it
+    const uint64_t t0 = (uint64_t)tile * kTB;
+    for (int i = l; i < (kTB + kE) / 16; i += kTL) {
+        const uint64_t a = t0 + (uint64_t)i * 16;
+        uint4 v;
+        if (a + 16 <= P.len) {
+            v = *reinterpret_cast<const uint4*>(P.buf + a);
+        } else {
+            uint32_t q[4] = {0, 0, 0, 0};
+            for (int b = 0; b < 16; ++b)
+                if (a + b < P.len) q[b >> 2] |= (uint32_t)P.buf[a + b] << (8 * (b & 3));
+            v = make_uint4(q[0], q[1], q[2], q[3]);
+        }
+        *reinterpret_cast<uint4*>(&B[i * 16]) = v;
+    }
+    {  // the tile's chunk maps
+        const uint4* src = reinterpret_cast<const uint4*>(W.cmap + (uint64_t)tile * kTL * kE);
+        for (int i = l; i < kTL * kE / 16; i += kTL) reinterpret_cast<uint4*>(&X[0][0])[i] = src[i];
+    }
+    __syncthreads();
+    chunk_groups(&X[0][0], kE, G);
+    __syncthreads();
+    if (l == 0) {  // group entries from the tile's entry
+        uint32_t x = ent;
+        for (int g = 0; g < kTL / 8; ++g) {
+            GE[g] = (uint8_t)x;
+            x = x == kDeadE ? kDeadE : G[g][x];
+        }
+    }
+    __syncthreads();
+    if (l < kTL / 8) {  // chunk entries inside each group
+        uint32_t x = GE[l];
+        for (int c = 0; c < 8; ++c) {
+            En[8 * l + c] = (uint8_t)x;
+            const uint32_t y = x == kDeadE ? kDeadE : X[8 * l + c][x];
+            x = y < (uint32_t)kE ? y : kDeadE;
+        }
+    }
+    __syncthreads();
+    const uint32_t e = En[l];
+    const uint64_t stop = W.stop[0];
+    const int why = (int)W.stop[2];
+    const bool long_stop = why == MPX_DECODE_LONG;
+    const Bytes by{P.buf, B, t0, t0 + kTB + kE < P.len ? t0 + kTB + kE : P.len};
+    const uint64_t c0 = t0 + (uint64_t)l * kC;
+    // walk 1: frames of this chunk on the true chain: AcceptReplies, PrepareReplies, variable
+    // messages, other fixed frames (every frame before the stop is complete and in the window)
+    uint32_t cnt[4] = {0, 0, 0, 0};
+    const uint64_t lut = P.proto == MPX_MODE_MIN ? kLutMin : kLutClassic;
+    if (e != kDeadE) {
+        for (uint64_t a = c0 + e; a < c0 + kC;) {
+            const uint32_t code = B[a - t0];  // a frame on the chain starts inside the tile
+            if (a == stop) {
+                if (long_stop) {
+                    cnt[2]++;
+                    cnt[1] += code == MPX_PEER_PREPARE_REPLY ? 1u : 0u;
+                }
+                break;
+            }
+            uint32_t fl = lut_len(lut, code);
+            if (fl == 0) {
+                fl = parse_var(by, P.len, ~0ull, a, P.proto).f.len;
+                cnt[2]++;
+                cnt[1] += code == MPX_PEER_PREPARE_REPLY ? 1u : 0u;
+            } else {
+                cnt[code == MPX_PEER_ACCEPT_REPLY ? 0 : 3]++;
+            }
+            a += fl;
+        }
+    }
+    // block exclusive scan of the four counts
+    uint32_t incl[4], tot[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t x = cnt[k];
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d);
+            if (lane_id() >= d) x += y;
+        }
+        incl[k] = x;
+        if (lane_id() == kWave - 1) wsum[l / kWave][k] = x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t before = 0, all = 0;
+        for (int w = 0; w < kTL / kWave; ++w) {
+            before += w < l / kWave ? wsum[w][k] : 0u;
+            all += wsum[w][k];
+        }
+        incl[k] = incl[k] - cnt[k] + before;  // exclusive within the tile
+        tot[k] = all;
+    }
+    // decoupled look-back over tiles (wave 0, 64 predecessors per round). Per tile and count
+    // one 64-bit word, status << 32 | value (1: the tile's own count, 2: the inclusive count
+    // up to it), so a word is valid on its own: relaxed device-scope loads and stores, no fences
+    if (l < kWave) {
+        unsigned long long* lb = W.lb;
+        uint32_t pre[4] = {0, 0, 0, 0};
+        if (l < 4 && tile > 0)
+            __hip_atomic_store(lb + 4 * (uint64_t)tile + l, (1ull << 32) | tot[l],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            for (int64_t j0 = (int64_t)tile - 1; j0 >= 0;) {
+                const int64_t j = j0 - l;
+                const unsigned long long w =
+                    j >= 0 ? __hip_atomic_load(lb + 4 * (uint64_t)j + k, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                           : (2ull << 32);  // before tile 0: an inclusive zero
+                const uint32_t f = (uint32_t)(w >> 32);
+                const unsigned long long m_inc = __ballot(f == 2u);
+                const int first = m_inc ? __ffsll((long long)m_inc) - 1 : kWave;
+                const unsigned long long upto =
+                    first >= kWave - 1 ? ~0ull : ((2ull << first) - 1ull);
+                if (__ballot(f == 0u) & upto) continue;  // not published yet: spin
+                uint32_t v = l <= first ? (uint32_t)w : 0u;
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+                pre[k] += v;
+                if (first < kWave) break;
+                j0 -= kWave;
+            }
+        }
+        if (l < 4) {
+            __hip_atomic_store(lb + 4 * (uint64_t)tile + l, (2ull << 32) | (pre[l] + tot[l]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            pre_s[l] = pre[l];
+        }
+    }
+    __syncthreads();
+    uint64_t idx[4];
+    const uint64_t base[4] = {W.stop[8], W.stop[9], W.stop[10], W.stop[11]};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) idx[k] = base[k] + pre_s[k] + incl[k];
+    // the stop tile (the one holding the terminal byte, at the latest position len) owns the
+    // totals: every later tile is dead
+    if (stop / kTB == tile && l == 0) {
+        res->n_accept_replies = base[0] + pre_s[0] + tot[0];
+        res->n_prepare_replies = base[1] + pre_s[1] + tot[1];
+        res->n_var = base[2] + pre_s[2] + tot[2];
+        res->n_other = base[3] + pre_s[3] + tot[3];
+    }
+    if (e == kDeadE) return;
+    // walk 2: the records
+    for (uint64_t a = c0 + e; a < c0 + kC;) {
+        const uint32_t code = B[a - t0];
+        uint32_t fl = lut_len(lut, code);
+        const bool at_stop = a == stop;
+        if (at_stop && !long_stop) break;
+        if (fl == 0) {
+            VarInfo f;
+            if (at_stop) {
+                f = VarInfo{(uint32_t)W.stop[3], (uint32_t)W.stop[4], (uint32_t)W.stop[5],
+                            (uint32_t)W.stop[6], (uint32_t)W.stop[7]};
+            } else {
+                f = parse_var(by, P.len, ~0ull, a, P.proto).f;
+#ifdef MPX_DEBUG_STREAM
+                {
+                    const VarRes d = parse_var(Bytes{P.buf, nullptr, 0, 0}, P.len, ~0ull, a, P.proto);
+                    printf("var@%lu code %u: lds-by len %u n %u co %u m %u lo %u | global st %d len %u n %u co %u m %u lo %u | B[a-t0]=%u g=%u\n",
+                           (unsigned long)a, code, f.len, f.n_cmds, f.cmds_off, f.n_log, f.log_off, d.st, d.f.len,
+                           d.f.n_cmds, d.f.cmds_off, d.f.n_log, d.f.log_off, (unsigned)B[a - t0], (unsigned)P.buf[a]);
+                }
+#endif
+            }
+            fl = f.len;
+            if (code == MPX_PEER_PREPARE_REPLY) {
+                if (idx[1] < O.prep_cap) {
+                    if (P.proto == MPX_MODE_MIN) {  // Id, Instance, OK, Ballot, LastCommitted
+                        mpx_prepare_reply_min r;
+                        r.id = le32(by, a + 1);
+                        r.instance = le32(by, a + 5);
+                        r.ok = by(a + 9);
+                        r.ballot = le32(by, a + 10);
+                        r.last_committed = le32(by, a + 14);
+                        r.value_id = (uint32_t)idx[2];
+                        static_cast<mpx_prepare_reply_min*>(O.prep)[idx[1]] = r;
+                    } else {  // Instance, OK, Ballot
+                        mpx_prepare_reply r;
+                        r.instance = le32(by, a + 1);
+                        r.ok = by(a + 5);
+                        r.ballot = le32(by, a + 6);
+                        r.value_id = (uint32_t)idx[2];
+                        static_cast<mpx_prepare_reply*>(O.prep)[idx[1]] = r;
+                    }
+                }
+                ++idx[1];
+            }
+            if (idx[2] < O.var_cap) {
+                mpx_var_frame v;
+                v.offset = (uint32_t)(P.pos_base + a);
+                v.length = f.len;
+                v.n_cmds = f.n_cmds;
+                v.cmds_off = (uint32_t)(P.pos_base + f.cmds_off);
+                v.n_log = f.n_log;
+                v.log_off = (uint32_t)(P.pos_base + f.log_off);
+                v.code = (uint8_t)code;
+#pragma unroll
+                for (int k = 0; k < 7; ++k) v.pad[k] = 0;
+                O.var[idx[2]] = v;
+            }
+            ++idx[2];
+            if (at_stop) break;
+        } else if (code == MPX_PEER_ACCEPT_REPLY) {
+            if (idx[0] < O.ar_cap) {
+                mpx_accept_reply r;
+                r.instance = le32(by, a + 1);
+                r.ok = by(a + 5);
+                r.ballot = le32(by, a + 6);
+                r.id = P.proto == MPX_MODE_MIN ? le32(by, a + 10) : -1;
+                r.pad[0] = r.pad[1] = r.pad[2] = 0;
+                O.ar[idx[0]] = r;
+            }
+            ++idx[0];
+        } else {
+            if (idx[3] < O.oth_cap) {
+                mpx_peer_frame f;
+                f.offset = (uint32_t)(P.pos_base + a);
+                f.code = (uint8_t)code;
+                f.pad[0] = f.pad[1] = f.pad[2] = 0;
+                O.oth[idx[3]] = f;
+            }
+            ++idx[3];
+        }
+        a += fl;
+    }
+}
+
+// an empty call ([start, len) holds no byte): END, counts unchanged
+__global__ void k_sd_empty(mpx_stream_result* res, uint64_t at) {
+    res->consumed = at;
+    res->next = at;
+    res->stop_reason = MPX_DECODE_END;
+    res->stop_code = -1;
+}
+
+// ---- host side ----------------------------------------------------------------------------
+namespace {
+struct Layout {
+    uint64_t cmap, tmap, tent, gmap, gent, lb, ticket, stop, total;
+};
+Layout layout_of(uint64_t len) {
+    const uint64_t tiles = n_tiles_of(len + 16), groups = (tiles + kGT - 1) / kGT;
+    auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+    Layout L{};
+    uint64_t o = 0;
+    L.cmap = o; o += al(tiles * kTL * kE);
+    L.tmap = o; o += al(tiles * kE);
+    L.tent = o; o += al(tiles);
+    L.gmap = o; o += al(groups * kE);
+    L.gent = o; o += al(groups);
+    L.lb = o; o += al(tiles * 32);
+    L.ticket = o; o += al(4);
+    L.stop = o; o += al(12 * 8);
+    L.total = o;
+    return L;
+}
+}  // namespace
+
+uint64_t stream_work_bytes(uint64_t len) { return layout_of(len).total; }
+
+hipError_t launch_decode_stream(int proto, int legacy, const uint8_t* buf, uint64_t len,
+                                uint64_t start, const StreamOuts& outs, mpx_stream_result* res,
+                                void* work, uint64_t work_bytes, hipStream_t stream) {
+    if (len > (uint64_t)MPX_DECODE_MAX_BYTES || start > len) return hipErrorInvalidValue;
+    if (work_bytes < stream_work_bytes(len)) return hipErrorInvalidValue;
+    if (start == len) {
+        k_sd_empty<<<1, 1, 0, stream>>>(res, start);
+        return hipGetLastError();
+    }
+    const uint64_t base = start & ~15ull;
+    SParams P{buf + base, len - base, base, (uint32_t)(start - base), proto, legacy};
+    // one tile more when len is a multiple of the tile: position len is a terminal the chain
+    // must be able to land on
+    const uint32_t tiles = (uint32_t)n_tiles_of(P.len + 1);
+    const uint32_t groups = (tiles + kGT - 1) / kGT;
+    const Layout L = layout_of(len);
+    char* w = (char*)work;
+    Work W{(uint8_t*)(w + L.cmap), (uint8_t*)(w + L.tmap), (uint8_t*)(w + L.tent),
+           (uint8_t*)(w + L.gmap), (uint8_t*)(w + L.gent), (unsigned long long*)(w + L.lb),
+           (uint32_t*)(w + L.ticket), (uint64_t*)(w + L.stop)};
+    hipError_t r = hipMemsetAsync(w + L.lb, 0, (uint64_t)tiles * 32, stream);
+    if (r == hipSuccess) r = hipMemsetAsync(w + L.ticket, 0, 4, stream);
+    if (r != hipSuccess) return r;
+    Outs O{outs.ar, outs.ar_cap, outs.prep, outs.prep_cap, outs.var, outs.var_cap, outs.oth,
+           outs.oth_cap};
+    k_sd_tile_maps<<<tiles, kTL, 0, stream>>>(P, W);
+    k_sd_group_maps<<<groups, kE, 0, stream>>>(W, tiles);
+    k_sd_walk<<<1, 64, 0, stream>>>(P, W, tiles, groups, res);
+    k_sd_tile_entries<<<groups, kE, 0, stream>>>(W, tiles);
+    k_sd_emit<<<tiles, kTL, 0, stream>>>(P, W, O, tiles, res);
+    return hipGetLastError();
+}
+
+}  // namespace mpx

@@ -277,6 +277,36 @@ class Engine:
         return (ar[:min(int(r["n_accept_replies"]), ar_cap)],
                 oth[:min(int(r["n_other"]), other_cap)], r)
 
+    def decode_stream(self, buf, caps=None):
+        """Frame one peer connection's bytes with the engine's protocol (MIN / CLASSIC),
+        variable-length messages included. Returns (accept_replies, prepare_replies,
+        var_frames, other_frames, mpx_stream_result)."""
+        buf = np.frombuffer(buf, np.uint8) if isinstance(buf, (bytes, bytearray)) else \
+            _c(buf, np.uint8)
+        n = len(buf)
+        ca, cp, cv, co = caps or (n // 10 + 1, n // 10 + 1, n // 13 + 1, n + 1)
+        ar = np.zeros(max(ca, 1), R.ACCEPT_REPLY)
+        pr = np.zeros(max(cp, 1), R.PREPARE_REPLY_MIN if self.mode == R.MODE_MIN
+                      else R.PREPARE_REPLY)
+        var = np.zeros(max(cv, 1), R.VAR_FRAME)
+        oth = np.zeros(max(co, 1), R.PEER_FRAME)
+        res = np.zeros(1, R.STREAM_RESULT)
+        out = _lib.MpxDecodeOut(_ptr(ar), ca, _ptr(pr), cp, _ptr(var), cv, _ptr(oth), co)
+        self._check(self.lib.mpx_decode_stream(self.h, _ptr(buf), n, C.byref(out), _ptr(res)),
+                    "mpx_decode_stream")
+        r = res[0]
+        return (ar[:min(int(r["n_accept_replies"]), ca)], pr[:min(int(r["n_prepare_replies"]), cp)],
+                var[:min(int(r["n_var"]), cv)], oth[:min(int(r["n_other"]), co)], r)
+
+    def decode_stream_reserve(self, max_len):
+        self._check(self.lib.mpx_decode_stream_reserve(self.h, max_len),
+                    "mpx_decode_stream_reserve")
+
+    def decode_stream_dev(self, d_buf, n, start, out, d_res, stream=None):
+        """out: _lib.MpxDecodeOut of device pointers; d_res: device mpx_stream_result (in/out)"""
+        self._check(self.lib.mpx_decode_stream_dev(self.h, d_buf, n, start, C.byref(out), d_res,
+                                                   stream), "mpx_decode_stream_dev")
+
     def decode_reserve(self, max_len):
         self._check(self.lib.mpx_decode_reserve(self.h, max_len), "mpx_decode_reserve")
 

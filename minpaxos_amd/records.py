@@ -60,8 +60,18 @@ PEER_COMMIT_SHORT, PEER_PREPARE_REPLY, PEER_ACCEPT_REPLY = 11, 12, 13
 # body bytes after the code byte (None = variable length; unknown codes have none)
 PEER_BODY = {PEER_BEACON: 8, PEER_BEACON_REPLY: 8, PEER_PREPARE: 12, PEER_COMMIT_SHORT: 16,
              PEER_ACCEPT_REPLY: 13, PEER_ACCEPT: None, PEER_COMMIT: None, PEER_PREPARE_REPLY: None}
-DECODE_END, DECODE_PARTIAL, DECODE_VARIABLE = 0, 1, 2
+# CLASSIC framing (paxosproto, registration order paxos.go:93-98): Prepare 13, AcceptReply 9
+PEER_BODY_CLASSIC = {**PEER_BODY, PEER_PREPARE: 13, PEER_ACCEPT_REPLY: 9}
+DECODE_END, DECODE_PARTIAL, DECODE_VARIABLE, DECODE_MALFORMED, DECODE_LONG = 0, 1, 2, 3, 4
+DECODE_WINDOW = 64
 DECODE_MAX_BYTES = 0x7FFFFFFF
+# mpx_var_frame / mpx_stream_result (mpx_decode_stream)
+VAR_FRAME = np.dtype([("offset", "<u4"), ("length", "<u4"), ("n_cmds", "<u4"),
+                      ("cmds_off", "<u4"), ("n_log", "<u4"), ("log_off", "<u4"), ("code", "u1"),
+                      ("pad", "u1", (7,))])
+STREAM_RESULT = np.dtype([("consumed", "<u8"), ("next", "<u8"), ("n_accept_replies", "<u8"),
+                          ("n_prepare_replies", "<u8"), ("n_var", "<u8"), ("n_other", "<u8"),
+                          ("stop_reason", "<i4"), ("stop_code", "<i4")])
 # mpx_peer_frame / mpx_decode_result
 PEER_FRAME = np.dtype([("offset", "<u4"), ("code", "u1"), ("pad", "u1", (3,))])
 DECODE_RESULT = np.dtype([("consumed", "<u8"), ("n_accept_replies", "<u8"), ("n_other", "<u8"),
@@ -81,6 +91,7 @@ LOG_REC = np.dtype([("ballot", "<i4"), ("status", "<i4"), ("inst_no", "<i4"), ("
 assert LOG_REC.itemsize == 16
 assert REPLY_REC.itemsize == 24
 assert PEER_FRAME.itemsize == 8 and DECODE_RESULT.itemsize == 32
+assert VAR_FRAME.itemsize == 32 and STREAM_RESULT.itemsize == 56
 assert ACCEPT_REPLY.itemsize == 16 and INST_STATE.itemsize == 16
 assert PREPARE_REPLY.itemsize == 16 and PREP_STATE.itemsize == 32
 assert PREPARE_REPLY_MIN.itemsize == 24 and GROUP_PREP_STATE.itemsize == 32

@@ -94,6 +94,187 @@ int orc_decode_peer_stream(const uint8_t* buf, size_t len, mpx_accept_reply* ar,
     return MPX_OK;
 }
 
+// Full peer-stream framing (mpx_decode_stream): replicaListener (genericsmr.go:402-446) with the
+// rpcTable of bareminpaxos (MIN, bareminpaxos.go:108-113) or paxos (CLASSIC, paxos.go:93-98),
+// every message Unmarshal()ed as its Go code reads it:
+//   binary.ReadVarint = ReadUvarint (10 bytes at most; a 10th byte > 1 overflows) + zig-zag;
+//   a negative slice length makes make() panic; a Command / Instance / header whose bytes are
+//   not all in the buffer yet is a partial frame (on the socket, Unmarshal would block).
+namespace {
+
+enum VarStatus { kVarOk = 0, kVarPartial = 1, kVarMalformed = 2 };
+
+// binary.ReadVarint at *pos; advances *pos
+int read_varint(const uint8_t* buf, size_t len, size_t* pos, int64_t* out) {
+    uint64_t x = 0;
+    unsigned s = 0;
+    for (int i = 0; i < 10; ++i) {
+        if (*pos >= len) return kVarPartial;
+        const uint8_t b = buf[(*pos)++];
+        if (b < 0x80) {
+            if (i == 9 && b > 1) return kVarMalformed;  // errOverflow
+            x |= (uint64_t)b << s;
+            *out = (int64_t)(x >> 1) ^ -(int64_t)(x & 1);  // zig-zag: ux>>1, ^ if ux&1
+            return kVarOk;
+        }
+        x |= (uint64_t)(b & 0x7f) << s;
+        s += 7;
+    }
+    return kVarMalformed;
+}
+
+// a slice of n 17-byte Commands at *pos (make([]state.Command, n) + n Command.Unmarshal)
+int skip_cmds(size_t len, size_t* pos, int64_t n) {
+    if (n < 0) return kVarMalformed;  // makeslice: len out of range
+    if ((uint64_t)n > (len - *pos) / 17) return kVarPartial;
+    *pos += 17 * (size_t)n;
+    return kVarOk;
+}
+
+// body of a variable-length message at p (code byte at p); fills f
+int parse_var(int proto, const uint8_t* buf, size_t len, size_t p, mpx_var_frame* f) {
+    const uint8_t code = buf[p];
+    size_t hdr;
+    bool log = false;
+    if (proto == MPX_MODE_MIN) {
+        hdr = code == MPX_PEER_ACCEPT ? 16 : code == MPX_PEER_COMMIT ? 12 : 17;
+        log = code != MPX_PEER_COMMIT;  // Accept and PrepareReply carry a CatchUpLog
+    } else {
+        hdr = code == MPX_PEER_PREPARE_REPLY ? 9 : 12;
+    }
+    memset(f, 0, sizeof(*f));
+    f->offset = (uint32_t)p;
+    f->code = code;
+    size_t pos = p + 1 + hdr;
+    if (pos > len) return kVarPartial;  // ReadAtLeast(header)
+    int64_t n = 0;
+    int st = read_varint(buf, len, &pos, &n);
+    if (st) return st;
+    if (n < 0) return kVarMalformed;
+    f->cmds_off = (uint32_t)pos;
+    if ((st = skip_cmds(len, &pos, n))) return st;
+    f->n_cmds = (uint32_t)n;
+    f->log_off = (uint32_t)pos;
+    if (log) {
+        int64_t m = 0;
+        if ((st = read_varint(buf, len, &pos, &m))) return st;
+        if (m < 0) return kVarMalformed;
+        if ((uint64_t)m > (len - pos) / 9) return kVarPartial;  // >= 9 bytes per Instance
+        f->log_off = (uint32_t)pos;
+        for (int64_t i = 0; i < m; ++i) {  // Instance.Unmarshal: Ballot, Status, Cmds
+            if (pos + 8 > len) return kVarPartial;
+            pos += 8;
+            int64_t k = 0;
+            if ((st = read_varint(buf, len, &pos, &k))) return st;
+            if ((st = skip_cmds(len, &pos, k))) return st;
+        }
+        f->n_log = (uint32_t)m;
+    }
+    f->length = (uint32_t)(pos - p);
+    return kVarOk;
+}
+
+// fixed body length (0 = unknown code, 1-byte frame), or -1 = variable-length message
+int fixed_body(int proto, uint8_t code) {
+    switch (code) {
+    case MPX_PEER_BEACON:
+    case MPX_PEER_BEACON_REPLY: return 8;
+    case MPX_PEER_PREPARE: return proto == MPX_MODE_MIN ? 12 : 13;
+    case MPX_PEER_COMMIT_SHORT: return 16;
+    case MPX_PEER_ACCEPT_REPLY: return proto == MPX_MODE_MIN ? 13 : 9;
+    case MPX_PEER_ACCEPT:
+    case MPX_PEER_COMMIT:
+    case MPX_PEER_PREPARE_REPLY: return -1;
+    default: return 0;
+    }
+}
+
+}  // namespace
+
+int orc_decode_stream(int proto, const uint8_t* buf, size_t len, const mpx_decode_out* out,
+                      mpx_stream_result* res) {
+    if (proto != MPX_MODE_MIN && proto != MPX_MODE_CLASSIC) return MPX_E_INVAL;
+    size_t p = 0;
+    uint64_t n_ar = 0, n_prep = 0, n_var = 0, n_oth = 0;
+    int32_t why = MPX_DECODE_END, code_at = -1;
+    while (p < len) {
+        const uint8_t code = buf[p];
+        const int bl = fixed_body(proto, code);
+        const uint8_t* b = buf + p + 1;
+        if (bl < 0) {
+            mpx_var_frame f;
+            const int st = parse_var(proto, buf, len, p, &f);
+            if (st) {
+                why = st == kVarPartial ? MPX_DECODE_PARTIAL : MPX_DECODE_MALFORMED;
+                code_at = code;
+                break;
+            }
+            if (code == MPX_PEER_PREPARE_REPLY) {
+                if (n_prep < out->prep_cap) {
+                    if (proto == MPX_MODE_MIN) {  // Id, Instance, OK, Ballot, LastCommitted
+                        mpx_prepare_reply_min r;
+                        r.id = le32(b);
+                        r.instance = le32(b + 4);
+                        r.ok = b[8];
+                        r.ballot = le32(b + 9);
+                        r.last_committed = le32(b + 13);
+                        r.value_id = (uint32_t)n_var;
+                        ((mpx_prepare_reply_min*)out->prep)[n_prep] = r;
+                    } else {  // Instance, OK, Ballot
+                        mpx_prepare_reply r;
+                        r.instance = le32(b);
+                        r.ok = b[4];
+                        r.ballot = le32(b + 5);
+                        r.value_id = (uint32_t)n_var;
+                        ((mpx_prepare_reply*)out->prep)[n_prep] = r;
+                    }
+                }
+                ++n_prep;
+            }
+            if (n_var < out->var_cap) out->var[n_var] = f;
+            ++n_var;
+            p += f.length;
+            continue;
+        }
+        if (p + 1 + (size_t)bl > len) {
+            why = MPX_DECODE_PARTIAL;
+            code_at = code;
+            break;
+        }
+        if (code == MPX_PEER_ACCEPT_REPLY) {
+            if (n_ar < out->ar_cap) {
+                mpx_accept_reply r;
+                memset(&r, 0, sizeof(r));
+                r.instance = le32(b);  // Instance, OK, Ballot (+ Id for MIN)
+                r.ok = b[4];
+                r.ballot = le32(b + 5);
+                r.id = proto == MPX_MODE_MIN ? le32(b + 9) : -1;
+                out->ar[n_ar] = r;
+            }
+            ++n_ar;
+        } else {
+            if (n_oth < out->other_cap) {
+                mpx_peer_frame f;
+                memset(&f, 0, sizeof(f));
+                f.offset = (uint32_t)p;
+                f.code = code;
+                out->other[n_oth] = f;
+            }
+            ++n_oth;
+        }
+        p += 1 + (size_t)bl;
+    }
+    res->consumed = p;
+    res->next = p;
+    res->n_accept_replies = n_ar;
+    res->n_prepare_replies = n_prep;
+    res->n_var = n_var;
+    res->n_other = n_oth;
+    res->stop_reason = why;
+    res->stop_code = code_at;
+    return MPX_OK;
+}
+
 // Client reply fan-out: every reply, in execution order, is one
 // genericsmr.(*Replica).ReplyProposeTS(reply, client writer) (genericsmr.go:529-535), i.e.
 // ProposeReplyTS.Marshal (gsmrprotomarsh.go:702-732) appended to that client's stream:

@@ -53,6 +53,7 @@ def load():
         "orc_decode_peer_stream": (C.c_int, [_p, _sz, _p, _sz, _p, _sz, _p]),
         "orc_encode_replies": (C.c_int, [_p, _sz, C.c_uint32, C.c_uint8, _i32, _p, _p]),
         "orc_encode_log": (C.c_int, [C.c_int, _p, _sz, _p, _p, _p, _p, _p, _sz, _p]),
+        "orc_decode_stream": (C.c_int, [C.c_int, _p, _sz, C.POINTER(L.MpxDecodeOut), _p]),
         "orc_replay_durable": (C.c_int, [_p, _sz, _i32, _i32, _p, _p, _p, _p, _p, _p]),
         "orc_bench_group_step": (C.c_int64, [C.c_int, C.c_int, C.POINTER(L.MpxGroupBatch),
                                              C.c_uint32, C.c_int]),
@@ -206,6 +207,27 @@ class Oracle:
         _check(self.lib.orc_encode_log(fmt, _ptr(recs), n, _ptr(off), _ptr(op), _ptr(key),
                                        _ptr(val), _ptr(out), cap, _ptr(ro)), "orc_encode_log")
         return out[:int(ro[-1])], ro
+
+    def decode_stream(self, buf, protocol=None):
+        """mpx_decode_stream restated (replicaListener + every Unmarshal): returns
+        (accept_replies, prepare_replies, var_frames, other_frames, result)"""
+        proto = self.mode if protocol is None else protocol
+        buf = np.ascontiguousarray(np.frombuffer(buf, np.uint8) if isinstance(buf, bytes) else buf,
+                                   np.uint8)
+        n = len(buf)
+        ar = np.zeros(n // 10 + 1, R.ACCEPT_REPLY)
+        pdt = R.PREPARE_REPLY_MIN if proto == R.MODE_MIN else R.PREPARE_REPLY
+        pr = np.zeros(n // 10 + 1, pdt)
+        var = np.zeros(n // 13 + 1, R.VAR_FRAME)
+        oth = np.zeros(n + 1, R.PEER_FRAME)
+        res = np.zeros(1, R.STREAM_RESULT)
+        out = L.MpxDecodeOut(_ptr(ar), len(ar), _ptr(pr), len(pr), _ptr(var), len(var),
+                             _ptr(oth), len(oth))
+        _check(self.lib.orc_decode_stream(proto, _ptr(buf), n, C.byref(out), _ptr(res)),
+               "orc_decode_stream")
+        r = res[0]
+        return (ar[:int(r["n_accept_replies"])], pr[:int(r["n_prepare_replies"])],
+                var[:int(r["n_var"])], oth[:int(r["n_other"])], r)
 
     def replay_durable(self, log, inst_cap, default_ballot=0, committed_up_to=-1, rec_base=0,
                        last_rec=None):
