@@ -78,7 +78,8 @@ def parse():
     ap.add_argument("--cmds", type=int, default=4)
     ap.add_argument("--keys", type=int, default=256)
     ap.add_argument("--replicas", type=int, default=5, help="N (replies per instance = N-1)")
-    ap.add_argument("--kv-per-group", type=int, default=512)
+    ap.add_argument("--kv-per-group", type=int, default=256,
+                    help="group table capacity (config 5: the per-group key space, 256)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="issue the step all-reduce on the compute stream (no overlap)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

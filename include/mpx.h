@@ -189,7 +189,10 @@ typedef struct mpx_config {
     int32_t n_replicas;     /* N, 1..16                                                     */
     int32_t mode;           /* MPX_MODE_MIN / MPX_MODE_CLASSIC                              */
     uint64_t kv_capacity;   /* key capacity of the engine's KV table (mpx_apply); 0 = 1<<20 */
-    uint32_t kv_per_group;  /* max live keys per group table (mpx_group_step); 0 = 512      */
+    uint32_t kv_per_group;  /* max live keys per group table (mpx_group_step), <= 1024;
+                               0 = 512. Also picks the fused step's fast-path variant (256:
+                               the config-5 kernel); a group whose call touches more than
+                               2048 distinct keys fails with MPX_E_KV_FULL                  */
     uint32_t flags;         /* reserved, 0                                                  */
     uint64_t max_groups;    /* groups per mpx_group_step_dev call (work list); 0 = 1<<20    */
 } mpx_config;

@@ -253,10 +253,28 @@ __device__ __forceinline__ void table_writeback(const Dict& D, uint32_t norig, u
 // present at the start iff it is one of the table's entries. Nothing reaches global memory
 // before the group is known to fit; otherwise it goes to k_group_general via the work list
 // (also for the one key the free-slot marker cannot hold, INT64_MIN).
-constexpr int kFRecs = 1024, kFIpg = 256, kFCmds = 1024, kFTab = 256, kFH = 512;
-constexpr int kFPer = kFCmds / kStepBlock;   // commands per thread
-constexpr int kFRecPer = kFRecs / kStepBlock;
-constexpr int kFWaves = kStepBlock / kWave;
+// Capacities of one fast-path variant: T threads = T instance slots, R replies, C commands,
+// TB table entries at the start of the step, 2^HB hash slots (table + new keys). The launcher
+// picks the smallest variant a batch's shape (N, ipg, kv_per_group) fits; a group that still
+// overflows one at run time goes to the general kernel.
+template <int T_, int R_, int C_, int TB_, int HB_>
+struct FastCfg {
+    static constexpr int kFT = T_, kFRecs = R_, kFIpg = T_, kFCmds = C_, kFTab = TB_;
+    static constexpr int kFHB = HB_, kFH = 1 << HB_;
+    static constexpr int kFPer = kFCmds / kFT;    // commands per thread
+    static constexpr int kFRecPer = kFRecs / kFT; // replies per thread
+    static constexpr int kFTabPer = (kFTab + kFT - 1) / kFT;
+    static constexpr int kFWaves = kFT / kWave;
+    static constexpr int kWaveCmds = kFCmds / kFWaves;  // commands per wave
+    static_assert(kFCmds % kFT == 0 && kFRecs % kFT == 0, "whole items per thread");
+    static_assert(kFCmds / 32 <= kWave, "the new-key bitmap is scanned by one wave");
+    static_assert(kWaveCmds < 2047, "kTabLp holds 1 + a wave-relative command index");
+    static_assert(kFH % (2 * kFT) == 0 && (kFH * 2) % (kWave * 16) == 0, "init strides");
+};
+using FastBase = FastCfg<256, 1024, 1024, 256, 9>;   // config 5: N <= 5, keys per group <= 256
+using FastRecs = FastCfg<256, 2048, 1024, 256, 9>;   // N <= 9
+using FastKeys = FastCfg<256, 1024, 1024, 1024, 10>; // group tables of up to 1024 keys
+using FastWide = FastCfg<512, 2048, 2048, 512, 10>;  // 512 instances per group
 constexpr uint16_t kNone16 = 0xFFFF;
 constexpr uint8_t kIdBad = 31;
 constexpr unsigned long long kFreeKey = 0x8000000000000000ull;  // INT64_MIN marks a free slot
@@ -267,9 +285,20 @@ constexpr uint32_t kOverflow = 0x80000000u;                      // ebits: group
 constexpr uint32_t kTabAny = 0x8000u;  // some earlier command used the slot
 constexpr uint32_t kTabPut = 0x4000u;  // ... and the latest of them is a PUT
 constexpr uint32_t kTabLp = 0x07FFu;
-constexpr int kWaveCmds = kFCmds / kFWaves;  // commands per wave (256)
 
+#define MPX_FAST_CONSTS                                                      \
+    constexpr int kFT = Cfg::kFT, kFRecs = Cfg::kFRecs, kFIpg = Cfg::kFIpg;    \
+    constexpr int kFCmds = Cfg::kFCmds, kFTab = Cfg::kFTab, kFH = Cfg::kFH;    \
+    constexpr int kFPer = Cfg::kFPer, kFRecPer = Cfg::kFRecPer;                \
+    constexpr int kFTabPer = Cfg::kFTabPer, kFWaves = Cfg::kFWaves;            \
+    constexpr int kWaveCmds = Cfg::kWaveCmds;                                   \
+    (void)kFT; (void)kFRecs; (void)kFIpg; (void)kFCmds; (void)kFTab; (void)kFH; \
+    (void)kFPer; (void)kFRecPer; (void)kFTabPer; (void)kFWaves; (void)kWaveCmds;
+
+template <class Cfg>
 struct FastLds {
+    static constexpr int kFRecs = Cfg::kFRecs, kFIpg = Cfg::kFIpg, kFCmds = Cfg::kFCmds;
+    static constexpr int kFTab = Cfg::kFTab, kFH = Cfg::kFH, kFWaves = Cfg::kFWaves;
     union {
         struct {                 // until the tally: the group's replies (SoA) + reply ranges
             int32_t inst[kFRecs];
@@ -313,18 +342,20 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 }
 
 // home slot of a key in the fast path's table: Fibonacci hashing of the folded key (the top
-// log2(kFH) bits of a 32-bit multiplicative hash)
+// HB bits of a 32-bit multiplicative hash)
+template <int HB>
 __device__ __forceinline__ uint32_t fhash(int64_t k) {
     const uint32_t x = (uint32_t)(uint64_t)k ^ (uint32_t)((uint64_t)k >> 32);
-    return (x * 0x9E3779B1u) >> (32 - 9);
+    return (x * 0x9E3779B1u) >> (32 - HB);
 }
-static_assert(kFH == 512, "fhash returns 9 bits");
 
 // slot of key in the group's table, claiming a free slot if the key is absent (*fresh = 1);
 // -1 when the table is full. Linear probing; the CAS returns the slot's key, so a probe that
 // meets the key (inserted earlier or concurrently by another lane) ends there too.
-__device__ __forceinline__ int fast_slot(FastLds& S, unsigned long long key, uint32_t h,
+template <class Cfg>
+__device__ __forceinline__ int fast_slot(FastLds<Cfg>& S, unsigned long long key, uint32_t h,
                                          int& fresh) {
+    constexpr int kFH = Cfg::kFH;
     uint32_t i = h & (kFH - 1);
     for (int probe = 0; probe < kFH; ++probe) {
         const unsigned long long old = atomicCAS(&S.hkey[i], kFreeKey, key);
@@ -337,11 +368,12 @@ __device__ __forceinline__ int fast_slot(FastLds& S, unsigned long long key, uin
     return -1;
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, int32_t nrep,
-                                                           uint32_t kvpg, uint32_t* worklist,
-                                                           uint32_t* wcount, uint32_t* err) {
-    __shared__ FastLds S;
+template <int MODE, class Cfg>
+__global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int32_t nrep,
+                                                         uint32_t kvpg, uint32_t* worklist,
+                                                         uint32_t* wcount, uint32_t* err) {
+    MPX_FAST_CONSTS
+    __shared__ FastLds<Cfg> S;
     STAMP_DECL
     const uint32_t g = blockIdx.x;
     const int t = threadIdx.x, l = lane_id();
@@ -369,7 +401,7 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
         const uint32_t last = (uint32_t)nrec - 1;
 #pragma unroll
         for (int k = 0; k < kFRecPer; ++k) {
-            const uint32_t p = t + k * kStepBlock;
+            const uint32_t p = t + k * kFT;
             rr[k] = ld_stream(reinterpret_cast<const int4*>(b.recs) + r0 + (p < last ? p : last));
         }
     } else {
@@ -381,13 +413,20 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     int4 st = ld_stream(reinterpret_cast<const int4*>(b.st_in) + gi0 + ti);
     const uint32_t co = b.cmd_off[gi0 + ti];
     const uint8_t hs = b.has_cmds ? b.has_cmds[gi0 + ti] : (uint8_t)1;
-    const uint64_t ei = (uint64_t)g * kvpg + ((uint32_t)t < kcnt ? (uint32_t)t : (kcnt ? kcnt - 1 : 0));
-    const int64_t tk = b.kv_key_in[ei];
-    const int64_t tv = b.kv_val_in[ei];
+    int64_t tk[kFTabPer], tv[kFTabPer];  // this lane's table entries t, t + T, ...
+#pragma unroll
+    for (int k = 0; k < kFTabPer; ++k) {
+        const uint32_t e = (uint32_t)t + k * kFT;
+        const uint64_t ei = (uint64_t)g * kvpg + (e < kcnt ? e : (kcnt ? kcnt - 1 : 0));
+        tk[k] = b.kv_key_in[ei];
+        tv[k] = b.kv_val_in[ei];
+    }
     // LDS initialisation (regions outside the reply image)
-    S.hkey[t] = kFreeKey;
-    S.hkey[t + kStepBlock] = kFreeKey;
-    reinterpret_cast<uint32_t*>(S.tabidx)[t] = 0xFFFFFFFFu;  // kNone16 pairs
+#pragma unroll
+    for (int k = 0; k < kFH / kFT; ++k) S.hkey[t + k * kFT] = kFreeKey;
+#pragma unroll
+    for (int k = 0; k < kFH / (2 * kFT); ++k)
+        reinterpret_cast<uint32_t*>(S.tabidx)[t + k * kFT] = 0xFFFFFFFFu;  // kNone16 pairs
     if (t < kFCmds / 32) S.newbits[t] = 0u;
     S.u.a.rstart[t] = kNone16;
     S.coff[t] = (uint16_t)(own ? co - c_lo : ncmd);
@@ -401,7 +440,7 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     }
 #pragma unroll
     for (int k = 0; k < kFRecPer; ++k) {
-        const uint32_t p = t + k * kStepBlock;
+        const uint32_t p = t + k * kFT;
         const uint32_t idc = (rr[k].z >= 0 && rr[k].z < nrep) ? (uint32_t)rr[k].z : kIdBad;
         S.u.a.inst[p] = rr[k].x;
         S.u.a.bal[p] = rr[k].y;
@@ -429,7 +468,7 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     // ---- phase 1: reply ranges from head flags; the group's table into the dictionary ----------
 #pragma unroll
     for (int k = 0; k < kFRecPer; ++k) {
-        const uint32_t p = t + k * kStepBlock;
+        const uint32_t p = t + k * kFT;
         const bool valid = p < nrec;
         const int32_t inst = S.u.a.inst[p];
         const int32_t prev = S.u.a.inst[p ? p - 1 : 0];
@@ -442,15 +481,22 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
         if (head && p && pinwin) S.u.a.rend[prev] = (uint16_t)p;
         if (valid && p + 1 == nrec && inwin) S.u.a.rend[inst] = (uint16_t)nrec;
     }
-    int tslot = 0;  // slot of this lane's table entry
-    if ((uint32_t)t < kcnt) {
-        int fresh = 0;
-        const int sl = (unsigned long long)tk == kFreeKey
-                           ? -1 : fast_slot(S, (unsigned long long)tk, fhash(tk), fresh);
-        ebits |= sl < 0 ? kOverflow : 0u;
-        tslot = sl < 0 ? 0 : sl;
-        if (fresh) S.tabidx[sl] = (uint16_t)t;  // (a duplicate entry of a malformed table
-        S.dval[t] = tv;                          //  shares the first one's slot)
+    int tslot[kFTabPer];  // slots of this lane's table entries
+#pragma unroll
+    for (int k = 0; k < kFTabPer; ++k) {
+        const uint32_t e = (uint32_t)t + k * kFT;
+        tslot[k] = 0;
+        if (e < kcnt) {
+            int fresh = 0;
+            const int sl = (unsigned long long)tk[k] == kFreeKey
+                               ? -1
+                               : fast_slot(S, (unsigned long long)tk[k], fhash<Cfg::kFHB>(tk[k]),
+                                           fresh);
+            ebits |= sl < 0 ? kOverflow : 0u;
+            tslot[k] = sl < 0 ? 0 : sl;
+            if (fresh) S.tabidx[sl] = (uint16_t)e;  // (a duplicate entry of a malformed table
+            S.dval[e] = tv[k];                      //  shares the first one's slot)
+        }
     }
     __syncthreads();  // B2
     STAMP(1);
@@ -587,8 +633,9 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     for (int k = 0; k < kFPer; ++k) ops |= (uint32_t)o[k] << (8 * k);
     const int wv = __builtin_amdgcn_readfirstlane(t / kWave);
     uint16_t* T = S.u.b.tab + wv * kFH;  // this wave's table (the reply image is dead)
-    static_assert(kFH * 2 == kWave * 16, "one 16-byte store per lane clears a wave's table");
-    reinterpret_cast<uint4*>(T)[l] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int k = 0; k < kFH * 2 / (kWave * 16); ++k)  // 16-byte stores clear the wave's table
+        reinterpret_cast<uint4*>(T)[l + k * kWave] = make_uint4(0u, 0u, 0u, 0u);
     // volatile LDS pointers: every access below is a real ds_* instruction, in program order
     typedef __attribute__((address_space(3))) volatile uint8_t lds_u8;
     typedef __attribute__((address_space(3))) volatile unsigned long long lds_u64;
@@ -607,11 +654,11 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
         const unsigned long long key = (unsigned long long)ck[k];
         int kd = -1;
 #if MPX_ABLATE & 2
-        if (act) kd = (int)fhash(ck[k]);
+        if (act) kd = (int)fhash<Cfg::kFHB>(ck[k]);
 #else
         if (act && key != kFreeKey) {
             int fresh = 0;
-            kd = fast_slot(S, key, fhash(ck[k]), fresh);
+            kd = fast_slot(S, key, fhash<Cfg::kFHB>(ck[k]), fresh);
         }
 #endif
         ebits |= (act && kd < 0) ? kOverflow : 0u;  // table full, or the key INT64_MIN
@@ -725,10 +772,14 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
     };
     int64_t* kko = b.kv_key_out + (uint64_t)g * kvpg;
     int64_t* kvo = b.kv_val_out + (uint64_t)g * kvpg;
-    if (!(MPX_ABLATE & 16) && (uint32_t)t < kcnt) {  // original entries stay in place
-        const uint32_t dl = last_put((uint32_t)tslot);
-        kko[t] = (int64_t)S.hkey[tslot];
-        kvo[t] = dl ? S.u.b.cval[dl - 1] : S.dval[t];
+#pragma unroll
+    for (int k = 0; k < kFTabPer; ++k) {  // original entries stay in place
+        const uint32_t e = (uint32_t)t + k * kFT;
+        if (!(MPX_ABLATE & 16) && e < kcnt) {
+            const uint32_t dl = last_put((uint32_t)tslot[k]);
+            kko[e] = (int64_t)S.hkey[tslot[k]];
+            kvo[e] = dl ? S.u.b.cval[dl - 1] : S.dval[e];
+        }
     }
     // keys new to the table that hold a value: appended in order of their first PUT, whose
     // rank is a popcount over the first-PUT bitmap (each wave scans the 32 words itself)
@@ -772,7 +823,7 @@ __global__ __launch_bounds__(kStepBlock) void k_group_fast(mpx_group_batch b, in
 }
 
 // ======================================= general path =========================================
-constexpr int kDCap = 1024;
+constexpr int kDCap = 2048;  // distinct keys a group's call may touch (table included)
 constexpr int kHCap = 2 * kDCap;
 constexpr int kChunk = 1024;
 constexpr int kPer = kChunk / kStepBlock;
@@ -998,6 +1049,40 @@ __global__ void k_fill_worklist(uint32_t* worklist, uint32_t* wcount, uint32_t n
     if (i == 0) *wcount = n;
 }
 
+namespace {
+template <int MODE, class Cfg>
+void launch_fast(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t* worklist,
+                 uint32_t* wcount, uint32_t* err, hipStream_t stream) {
+    k_group_fast<MODE, Cfg><<<b->n_groups, Cfg::kFT, 0, stream>>>(*b, nrep, kvpg, worklist, wcount,
+                                                                   err);
+}
+// the smallest fast-path variant the batch's shape fits (0 = none: every group is general)
+int fast_variant(int32_t nrep, uint32_t ipg, uint32_t kvpg) {
+    const uint64_t recs = (uint64_t)(nrep > 1 ? nrep - 1 : 1) * ipg;  // replies of a full group
+    if (ipg <= 256 && recs <= 1024 && kvpg <= 256) return 1;
+    if (ipg <= 256 && recs <= 2048 && kvpg <= 256) return 2;
+    if (ipg <= 256 && recs <= 1024 && kvpg <= 1024) return 3;
+    if (ipg <= 512 && recs <= 2048 && kvpg <= 512) return 4;
+    return 0;
+}
+template <int MODE>
+void launch_step(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t* worklist,
+                 uint32_t* wcount, uint32_t* err, hipStream_t stream) {
+    switch (fast_variant(nrep, b->ipg, kvpg)) {
+    case 1: launch_fast<MODE, FastBase>(b, nrep, kvpg, worklist, wcount, err, stream); break;
+    case 2: launch_fast<MODE, FastRecs>(b, nrep, kvpg, worklist, wcount, err, stream); break;
+    case 3: launch_fast<MODE, FastKeys>(b, nrep, kvpg, worklist, wcount, err, stream); break;
+    case 4: launch_fast<MODE, FastWide>(b, nrep, kvpg, worklist, wcount, err, stream); break;
+    default:
+        k_fill_worklist<<<(b->n_groups + 255) / 256, 256, 0, stream>>>(worklist, wcount,
+                                                                       b->n_groups);
+    }
+    const unsigned gen_grid = b->n_groups < 1024 ? b->n_groups : 1024;
+    k_group_general<MODE><<<gen_grid, kStepBlock, 0, stream>>>(*b, nrep, kvpg, worklist, wcount,
+                                                               err);
+}
+}  // namespace
+
 hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
                              const mpx_group_batch* b, uint32_t* worklist, uint32_t* wcount,
                              uint32_t* err, hipStream_t stream) {
@@ -1006,25 +1091,10 @@ hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
     if (b->ipg > (uint32_t)kMaxIpgBits) return hipErrorInvalidValue;
     hipError_t r = hipMemsetAsync(wcount, 0, sizeof(uint32_t), stream);
     if (r != hipSuccess) return r;
-    const bool fast_ok = b->ipg <= (uint32_t)kFIpg;
-    const unsigned gen_grid = b->n_groups < 1024 ? b->n_groups : 1024;
-    if (mode == MPX_MODE_MIN) {
-        if (fast_ok)
-            k_group_fast<MPX_MODE_MIN><<<b->n_groups, kStepBlock, 0, stream>>>(*b, nrep, kv_per_group,
-                                                                             worklist, wcount, err);
-        else
-            k_fill_worklist<<<(b->n_groups + 255) / 256, 256, 0, stream>>>(worklist, wcount, b->n_groups);
-        k_group_general<MPX_MODE_MIN><<<gen_grid, kStepBlock, 0, stream>>>(*b, nrep, kv_per_group,
-                                                                          worklist, wcount, err);
-    } else {
-        if (fast_ok)
-            k_group_fast<MPX_MODE_CLASSIC><<<b->n_groups, kStepBlock, 0, stream>>>(
-                *b, nrep, kv_per_group, worklist, wcount, err);
-        else
-            k_fill_worklist<<<(b->n_groups + 255) / 256, 256, 0, stream>>>(worklist, wcount, b->n_groups);
-        k_group_general<MPX_MODE_CLASSIC><<<gen_grid, kStepBlock, 0, stream>>>(
-            *b, nrep, kv_per_group, worklist, wcount, err);
-    }
+    if (mode == MPX_MODE_MIN)
+        launch_step<MPX_MODE_MIN>(b, nrep, kv_per_group, worklist, wcount, err, stream);
+    else
+        launch_step<MPX_MODE_CLASSIC>(b, nrep, kv_per_group, worklist, wcount, err, stream);
     return hipGetLastError();
 }
 

@@ -19,6 +19,8 @@ def pytest_configure(config):
     # libmpx.so BEFORE any test module imports torch: the engine binds /opt/rocm's HIP and RCCL
     # (the runtime bench.py measures on too), not the copies torch bundles.
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    if os.environ.get("MPX_TESTS_NO_ENGINE"):  # oracle-only runs (the sanitizer subprocess)
+        return
     if os.path.exists("/opt/rocm/bin/hipcc"):
         subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "minpaxos_amd")], check=True)
     from minpaxos_amd import _lib
@@ -26,6 +28,8 @@ def pytest_configure(config):
 
 
 def pytest_report_header(config):
+    if os.environ.get("MPX_TESTS_NO_ENGINE"):
+        return "oracle only"
     from minpaxos_amd import _lib
     return f"libmpx.so runtime: {_lib.runtime_info()}"
 

@@ -14,7 +14,8 @@ from minpaxos_amd import _lib as L
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
-ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
+# MPX_ORACLE_SO selects another build of the same oracle (the ASan/UBSan one, test_sanitize.py)
+ORACLE_SO = os.environ.get("MPX_ORACLE_SO") or os.path.join(ORACLE_DIR, "liboracle.so")
 
 _p = C.c_void_p
 _sz = C.c_size_t

@@ -286,3 +286,32 @@ def test_group_step_ragged(mk_engine):
         got = e.group_step(b, ret=ret0)
         want = o.group_step(b, ret=ret0)
         _cmp_group(got, want, G, K)
+
+
+@pytest.mark.parametrize("shape", [
+    dict(N=5, ipg=256, K=256, keys=256, B=4),      # FastBase
+    dict(N=7, ipg=256, K=256, keys=256, B=4),      # FastRecs (6 x 256 replies)
+    dict(N=9, ipg=256, K=256, keys=200, B=3),      # FastRecs, 8 replies per instance
+    dict(N=5, ipg=256, K=1024, keys=1024, B=4),    # FastKeys (tables of up to 1024 keys)
+    dict(N=5, ipg=512, K=512, keys=256, B=4),      # FastWide (512 instances per group)
+    dict(N=5, ipg=384, K=512, keys=400, B=5),      # FastWide with a partial instance space
+    dict(N=3, ipg=128, K=1024, keys=5000, B=9),    # FastKeys -> general (1152 commands)
+], ids=lambda d: "N{N}_ipg{ipg}_K{K}_keys{keys}_B{B}".format(**d))
+@pytest.mark.parametrize("mode", [R.MODE_MIN, R.MODE_CLASSIC])
+def test_group_step_variants(mk_engine, shape, mode):
+    """every fast-path capacity variant (and its run-time fallback to the general kernel),
+    two steps: from empty tables, then from the tables the first step produced"""
+    G, N, ipg, K = 128, shape["N"], shape["ipg"], shape["K"]
+    b = synth.group_batch(G, ipg, N, shape["B"], shape["keys"], seed=90 + N + ipg)
+    e, o = mk_engine(N, mode, kv_per_group=K), Oracle(N, mode, kv_per_group=K)
+    try:
+        want = o.group_step(b)
+    except OracleError:
+        pytest.skip("oracle: table full for this shape")
+    _cmp_group(e.group_step(b), want, G, K)
+    b2 = synth.group_batch(G, ipg, N, shape["B"], shape["keys"], seed=91 + N + ipg)
+    try:
+        want2 = o.group_step(b2, want["kv_cnt"], want["kv_key"], want["kv_val"])
+    except OracleError:
+        return
+    _cmp_group(e.group_step(b2, want["kv_cnt"], want["kv_key"], want["kv_val"]), want2, G, K)
