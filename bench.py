@@ -246,11 +246,16 @@ def step_bench(a, rk):
     n_ev = max(a.steps, 1)
     ev_k = [(eng.event_create(), eng.event_create()) for _ in range(n_ev)]
 
+    # watermark ranges other ranks own: [0, g0) and [g1, G_total) of both halves
+    wm_foreign = [(h + lo, h + hi) for h in (0, G_total) for lo, hi in ((0, g0), (g1, G_total))
+                  if hi > lo]
+
     def step(i, timed):
         buf = i & 1
         if i >= 2:  # buffer `buf` is free once the all-reduce of step i-2 has read it
             eng.stream_wait_event(comp, ev_comm[buf])
-        eng.memset(d["wm"][buf].ptr, 0xFF, d["wm"][buf].nbytes, comp)  # -1 outside own groups
+        for lo, hi in wm_foreign:  # -1 outside own groups (the step writes every own group)
+            eng.memset(d["wm"][buf].at(lo), 0xFF, (hi - lo) * 4, comp)
         if timed:
             eng.event_record(ev_k[i][0], comp)
         eng.group_step_dev(steps[buf], comp)

@@ -192,9 +192,22 @@ __device__ __forceinline__ uint32_t op_class(uint8_t o) {
     return o == MPX_OP_PUT ? kClsPut : (o == MPX_OP_GET ? kClsGet : kClsOther);
 }
 
-// probes while other lanes insert use relaxed loads. A slot's key changes at most once per call
-// (empty -> key), so a hit is final; a miss may be an insert the probe did not see yet and is
-// re-probed by k_kv_reprobe after the pass.
+// probes while other lanes insert read the key words with plain (L2-cached) loads: a slot's key
+// changes at most once per call (empty -> key), so a key read is final and only "empty" can be
+// stale - an insert then claims the slot with the CAS (which returns the true word), a probe's
+// miss is re-probed by k_kv_reprobe after the pass. MPX_INDEX_PLAIN=0: relaxed agent-scope
+// atomic loads instead (they bypass the XCD's L2).
+#ifndef MPX_INDEX_PLAIN
+#define MPX_INDEX_PLAIN 0
+#endif
+__device__ __forceinline__ unsigned long long probe_load(const int64_t* p) {
+#if MPX_INDEX_PLAIN
+    return (unsigned long long)*p;
+#else
+    return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
 // the two probe loops resumed at slot s whose key `cur` was already loaded (k_kv_index issues
 // the first probe of several commands together)
 __device__ __forceinline__ int64_t kv_insert_from(const KvTable& t, int64_t key, uint64_t s,
@@ -202,7 +215,7 @@ __device__ __forceinline__ int64_t kv_insert_from(const KvTable& t, int64_t key,
     const uint64_t mask = t.cap - 1;
     for (uint64_t probe = 0; probe < t.cap; ++probe) {
         unsigned long long* slot = reinterpret_cast<unsigned long long*>(t.keys + s);
-        if (probe) cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (probe) cur = probe_load(t.keys + s);
         if (cur == (unsigned long long)kSentinel) {
             cur = atomicCAS(slot, (unsigned long long)kSentinel, (unsigned long long)key);
             if (cur == (unsigned long long)kSentinel) return (int64_t)s;  // claimed
@@ -218,9 +231,7 @@ __device__ __forceinline__ int64_t kv_probe_racy_from(const KvTable& t, int64_t 
                                                       unsigned long long cur) {
     const uint64_t mask = t.cap - 1;
     for (uint64_t probe = 0; probe < t.cap; ++probe) {
-        if (probe)
-            cur = __hip_atomic_load(reinterpret_cast<unsigned long long*>(t.keys + s),
-                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (probe) cur = probe_load(t.keys + s);
         if ((int64_t)cur == key) return (int64_t)s;
         if ((int64_t)cur == kSentinel) return -1;
         s = (s + 1) & mask;
@@ -258,10 +269,7 @@ __global__ __launch_bounds__(256) void k_kv_index(KvTable t, const uint8_t* __re
         for (int u = 0; u < kIndexUnroll; ++u) {
             const uint64_t i = i0 + (uint64_t)u * blockDim.x + threadIdx.x;
             h[u] = hash64((uint64_t)k[u]) & mask;
-            cur[u] = i < m && k[u] != kSentinel
-                         ? __hip_atomic_load(reinterpret_cast<unsigned long long*>(t.keys + h[u]),
-                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                         : 0ull;
+            cur[u] = i < m && k[u] != kSentinel ? probe_load(t.keys + h[u]) : 0ull;
         }
 #pragma unroll
         for (int u = 0; u < kIndexUnroll; ++u) {
@@ -640,37 +648,116 @@ hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const
 }
 
 // ---- state.ConflictBatch over consecutive instances ------------------------------------------
-// one wave per instance pair; lanes stride over the |A| x |B| pairs, early exit on a hit
-__global__ __launch_bounds__(256) void k_conflict_batch(const uint8_t* __restrict__ op,
-                                                        const int64_t* __restrict__ key,
-                                                        const uint64_t* __restrict__ off,
-                                                        uint64_t n_pairs, uint8_t* __restrict__ out) {
-    const uint64_t pair = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
-    if (pair >= n_pairs) return;
-    const int l = lane_id();
-    const uint64_t a0 = off[pair], a1 = off[pair + 1], b1 = off[pair + 2];
-    const uint64_t na = a1 - a0, nb = b1 - a1, tot = na * nb;
-    bool hit = false;
-    for (uint64_t base = 0; base < tot; base += kWave) {
-        const uint64_t x = base + l;
-        if (x < tot) {
-            const uint64_t a = a0 + x / nb, b = a1 + x % nb;
-            hit = key[a] == key[b] && (op[a] == MPX_OP_PUT || op[b] == MPX_OP_PUT);
-        }
-        if (ballot(hit)) {
-            hit = true;
-            break;
-        }
+// ConflictBatch(b1, b2) (state.go:62-71) = some pair (c1 in b1, c2 in b2) with the same key and a
+// PUT among the two. A workgroup takes 256 consecutive pairs, i.e. one contiguous command range;
+// when it fits kStage commands it is staged in LDS with coalesced loads (every command is read
+// from HBM once, not once per pair it belongs to). A lane then takes one pair when both
+// instances have at most kSmall commands (MAX_BATCH-sized instances are rare) and tests all
+// |b1| x |b2| products in registers. The wave then takes its larger pairs one at a time, lanes
+// striding over the products with an early exit on the first hit.
+constexpr int kSmall = 8;
+constexpr int kConfBlock = 256;
+constexpr int kStage = 2560;
+
+template <typename KeyAt, typename PutAt>
+__device__ __forceinline__ bool small_pair(uint64_t a0, uint64_t na, uint64_t a1, uint64_t nb,
+                                           KeyAt key_at, PutAt put_at) {
+    int64_t ka[kSmall], kb[kSmall];
+    uint32_t pa = 0, pb = 0;  // PUT bits
+#pragma unroll
+    for (int i = 0; i < kSmall; ++i) {
+        const bool ia = (uint64_t)i < na, ib = (uint64_t)i < nb;
+        ka[i] = ia ? key_at(a0 + i) : 0;
+        kb[i] = ib ? key_at(a1 + i) : 0;
+        pa |= (ia && put_at(a0 + i) ? 1u : 0u) << i;
+        pb |= (ib && put_at(a1 + i) ? 1u : 0u) << i;
     }
-    if (l == 0) out[pair] = hit ? 1 : 0;
+    bool hit = false;
+#pragma unroll
+    for (int i = 0; i < kSmall; ++i)
+#pragma unroll
+        for (int j = 0; j < kSmall; ++j)
+            hit |= (uint64_t)i < na && (uint64_t)j < nb && ka[i] == kb[j] &&
+                   (((pa >> i) | (pb >> j)) & 1u);
+    return hit;
+}
+
+__global__ __launch_bounds__(kConfBlock) void k_conflict_batch(const uint8_t* __restrict__ op,
+                                                               const int64_t* __restrict__ key,
+                                                               const uint64_t* __restrict__ off,
+                                                               uint64_t n_pairs,
+                                                               uint8_t* __restrict__ out) {
+    __shared__ int64_t sk[kStage];
+    __shared__ uint8_t so[kStage];
+    __shared__ uint64_t range[2];
+    const uint64_t p0 = (uint64_t)blockIdx.x * kConfBlock;
+    const uint64_t pair = p0 + threadIdx.x;
+    const uint64_t pe = n_pairs - p0 < (uint64_t)kConfBlock ? n_pairs : p0 + kConfBlock;
+    const int l = lane_id();
+    const bool live = pair < n_pairs;
+    uint64_t a0 = 0, a1 = 0, b1 = 0;
+    if (live) {
+        a0 = off[pair];
+        a1 = off[pair + 1];
+        b1 = off[pair + 2];
+    }
+    if (pair == p0) range[0] = a0;
+    if (pair + 1 == pe) range[1] = b1;
+    __syncthreads();
+    const uint64_t c_lo = range[0], span = range[1] - range[0];
+    const bool staged = span <= (uint64_t)kStage;  // uniform over the workgroup
+    if (staged) {
+        for (uint32_t i = threadIdx.x; i < (uint32_t)span; i += kConfBlock) {
+            sk[i] = key[c_lo + i];
+            so[i] = op[c_lo + i];
+        }
+        __syncthreads();
+    }
+    const uint64_t na = a1 - a0, nb = b1 - a1;
+    const bool small = live && na <= (uint64_t)kSmall && nb <= (uint64_t)kSmall;
+    if (small) {
+        bool hit;
+        if (staged)
+            hit = small_pair(a0 - c_lo, na, a1 - c_lo, nb, [&](uint64_t i) { return sk[i]; },
+                             [&](uint64_t i) { return so[i] == MPX_OP_PUT; });
+        else
+            hit = small_pair(a0, na, a1, nb, [&](uint64_t i) { return key[i]; },
+                             [&](uint64_t i) { return op[i] == MPX_OP_PUT; });
+        out[pair] = hit ? 1 : 0;
+    }
+    // the wave's larger pairs, one at a time
+    unsigned long long big = __ballot(live && !small);
+    while (big) {
+        const int src = __ffsll((long long)big) - 1;
+        big &= big - 1;
+        const uint64_t p = (uint64_t)__shfl((long long)pair, src);
+        const uint64_t x0 = (uint64_t)__shfl((long long)a0, src);
+        const uint64_t x1 = (uint64_t)__shfl((long long)a1, src);
+        const uint64_t y1 = (uint64_t)__shfl((long long)b1, src);
+        const uint64_t xa = x1 - x0, xb = y1 - x1, tot = xa * xb;
+        bool hit = false;
+        for (uint64_t base = 0; base < tot; base += kWave) {
+            const uint64_t x = base + l;
+            bool h = false;
+            if (x < tot) {
+                const uint64_t i = x0 + x / xb, j = x1 + x % xb;
+                h = key[i] == key[j] && (op[i] == MPX_OP_PUT || op[j] == MPX_OP_PUT);
+            }
+            if (__ballot(h)) {
+                hit = true;
+                break;
+            }
+        }
+        if (l == src) out[p] = hit ? 1 : 0;
+    }
 }
 
 hipError_t launch_conflict_batch(const uint8_t* op, const int64_t* key, const uint64_t* inst_off,
                                  uint64_t n_inst, uint8_t* out, hipStream_t stream) {
     if (n_inst < 2) return hipSuccess;
     const uint64_t pairs = n_inst - 1;
-    const uint64_t blocks = (pairs * kWave + 255) / 256;
-    k_conflict_batch<<<dim3((unsigned)blocks), 256, 0, stream>>>(op, key, inst_off, pairs, out);
+    k_conflict_batch<<<dim3((unsigned)((pairs + kConfBlock - 1) / kConfBlock)), kConfBlock, 0,
+                       stream>>>(op, key, inst_off, pairs, out);
     return hipGetLastError();
 }
 

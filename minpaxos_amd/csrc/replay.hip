@@ -8,14 +8,22 @@
 //   committedUpTo = instNo            if instNo > committedUpTo && COMMITTED        (:149-151)
 //   instanceSpace[instNo] = {ballot, status, {0,0,0,nil}, [command]}               (:153-157)
 // The two watermarks are running maxima, so they are order-free; the last record naming an
-// instance wins its slot, so the slot keeps the HIGHEST record index (atomicMax).
+// instance wins its slot, so the slot keeps the HIGHEST record index.
+// The slot maximum without a device-scope atomic per record (MPX_REPLAY_ATOMIC=0, default):
+//   pass 1 (k_replay_durable) raises a slot with a plain load + store when its record index is
+//          higher: racing records of one instance may leave a lower index, never a value below
+//          the slot's value at call start (memory holds it when the kernel begins);
+//   pass 2 (k_replay_fix) re-reads every record's instNo from the SoA output and lifts a slot
+//          that still holds a lower index with atomicMax - only where records of one instance
+//          raced, so (almost) no atomics.
+// MPX_REPLAY_ATOMIC=1 keeps the single pass with one atomicMax per record (A/B builds).
 //
 // Layout: 256-record tiles (7424 bytes = 464 x 16 B, so every tile starts
 // 16-byte aligned when the log does); the tile is staged into LDS with 16-byte loads and each lane
 // cuts its record out of LDS, then writes the SoA outputs coalesced (16-byte mpx_log_rec, op,
 // key, val); a grid of 8 workgroups per CU walks the tiles, and each workgroup's max-reductions
 // feed one atomicMax per watermark. HBM-bound:
-// 29 B in + 33 B out + one 4-byte slot update per record.
+// 29 B in + 33 B out + one 4-byte slot update per record (+ pass 2's 16-byte re-read).
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -27,6 +35,9 @@ constexpr int kRecBytes = MPX_DURABLE_REC_BYTES;               // 12 + 17
 constexpr int kTileBytes = kReplayBlock * kRecBytes;           // 7424
 constexpr int kTileVec = kTileBytes / 16;                      // 464
 constexpr uint64_t kReplayGrid = 256 * 8;  // 256 CUs x 8 workgroups
+#ifndef MPX_REPLAY_ATOMIC
+#define MPX_REPLAY_ATOMIC 1
+#endif
 static_assert(kTileBytes % 16 == 0, "tile must be a whole number of 16-byte vectors");
 
 __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
@@ -99,8 +110,10 @@ __global__ __launch_bounds__(kReplayBlock) void k_replay_durable(
             // instanceSpace[instNo] panics outside the array (Go index check)
             if (inst < 0 || inst >= inst_cap)
                 raise_err(err, kErrNil);
-            else
+            else if (MPX_REPLAY_ATOMIC)
                 atomicMax(last_rec + inst, rec_base + (int32_t)i);
+            else if (last_rec[inst] < rec_base + (int32_t)i)
+                last_rec[inst] = rec_base + (int32_t)i;
         }
     }
     // one atomic per workgroup and watermark, skipped when it cannot raise the running value:
@@ -120,6 +133,20 @@ __global__ __launch_bounds__(kReplayBlock) void k_replay_durable(
             atomicMax(scalars + t, m);
     }
 }
+
+// pass 2: a slot below one of its records' indices lost a race in pass 1
+__global__ __launch_bounds__(256) void k_replay_fix(const mpx_log_rec* __restrict__ recs,
+                                                    uint64_t n, int32_t inst_cap,
+                                                    int32_t rec_base,
+                                                    int32_t* __restrict__ last_rec) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int32_t inst = reinterpret_cast<const int32_t*>(recs + i)[2];  // inst_no
+        if (inst < 0 || inst >= inst_cap) continue;
+        const int32_t me = rec_base + (int32_t)i;
+        if (last_rec[inst] < me) atomicMax(last_rec + inst, me);
+    }
+}
 }  // namespace
 
 hipError_t launch_replay_durable(const uint8_t* log, uint64_t n, int32_t inst_cap,
@@ -132,6 +159,11 @@ hipError_t launch_replay_durable(const uint8_t* log, uint64_t n, int32_t inst_ca
     const uint64_t grid = tiles < kReplayGrid ? tiles : kReplayGrid;
     hipLaunchKernelGGL(k_replay_durable, dim3((unsigned)grid), dim3(kReplayBlock), 0, stream, log,
                        n, inst_cap, rec_base, recs, op, key, val, last_rec, scalars, err);
+    if (!MPX_REPLAY_ATOMIC) {
+        const uint64_t g = (n + 255) / 256;
+        hipLaunchKernelGGL(k_replay_fix, dim3((unsigned)(g < 8192 ? g : 8192)), dim3(256), 0,
+                           stream, recs, n, inst_cap, rec_base, last_rec);
+    }
     return hipGetLastError();
 }
 

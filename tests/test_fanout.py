@@ -44,8 +44,10 @@ def test_kat_empty_and_bad_client():
 @pytest.mark.gpu
 def test_fanout_parity(mk_engine):
     e, o = mk_engine(5, R.MODE_MIN), Oracle()
+    # counting-sort path (<= 1024 connections; 5M replies = several tiles per workgroup) and the
+    # radix path (65536 connections)
     for n, c in ((1, 1), (255, 2), (256, 7), (257, 7), (1000, 1024), (4099, 3),
-                 (300000, 1024), (200000, 65536), (70000, 1)):
+                 (300000, 1024), (200000, 65536), (70000, 1), (5000000, 1000), (4500001, 2)):
         rec = synth.replies(n, c, seed=n + c)
         for ok, leader in ((1, 0), (0, 7)):
             got = e.encode_replies(rec, c, ok, leader)
@@ -68,3 +70,25 @@ def test_fanout_empty_and_bad_client(mk_engine):
     got = e.encode_replies(rec, 4)
     want = Oracle().encode_replies(rec, 4)
     assert got[0].tobytes() == want[0].tobytes() and np.array_equal(got[1], want[1])
+
+
+@pytest.mark.gpu
+def test_fanout_skewed_and_unaligned_output(mk_engine):
+    """one hot connection among many, into output buffers at every address mod 4"""
+    from minpaxos_amd.devbuf import Arena
+    e, o = mk_engine(5, R.MODE_MIN), Oracle()
+    n, c = 600000, 1024
+    rec = synth.replies(n, c, seed=5)
+    rec["client"][np.random.default_rng(6).random(n) < 0.7] = 517
+    want = o.encode_replies(rec, c, 1, 3)
+    e.encode_replies_reserve(n)
+    with Arena(e) as ar:
+        d_rec = ar.put(rec)
+        d_out = ar.empty(25 * n + 8, np.uint8)
+        d_off = ar.empty(c + 1, np.uint64)
+        for mis in range(4):
+            e.encode_replies_dev(d_rec.ptr, n, c, 1, 3, d_out.ptr + mis, d_off.ptr)
+            e.synchronize()
+            got = ar.get(d_out)[mis:mis + 25 * n]
+            assert got.tobytes() == want[0].tobytes(), mis
+            assert np.array_equal(ar.get(d_off), want[1])

@@ -217,11 +217,13 @@ def test_apply_chunked(mk_engine, monkeypatch, chunk):
 def test_conflict_batch(mk_engine):
     rng = np.random.default_rng(9)
     e, o = mk_engine(5, R.MODE_MIN), Oracle(5, R.MODE_MIN)
-    sizes = rng.integers(0, 12, 4000)
-    sizes[::500] = 700
-    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
-    op, key, _ = gen_cases.commands_mixed(rng, int(off[-1]), 2000, neg_keys=False)
-    assert np.array_equal(e.conflict_batch(op, key, off), o.conflict_batch(op, key, off))
+    # LDS-staged workgroups (with a few big instances), then ranges too long to stage
+    for every, big in ((500, 700), (90, 400)):
+        sizes = rng.integers(0, 12, 4000)
+        sizes[::every] = big
+        off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+        op, key, _ = gen_cases.commands_mixed(rng, int(off[-1]), 2000, neg_keys=False)
+        assert np.array_equal(e.conflict_batch(op, key, off), o.conflict_batch(op, key, off))
 
 
 # ---- fused group step (config 5 shape) ----------------------------------------------------------
