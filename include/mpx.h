@@ -317,7 +317,9 @@ typedef struct mpx_group_batch {
                                       (status became COMMITTED at a quorum crossing)        */
 } mpx_group_batch;
 
-/* host pointers (synchronous) / device pointers (asynchronous on stream)                  */
+/* host pointers (synchronous) / device pointers (asynchronous on stream). One handle runs
+ * its group steps (and step totals) one at a time in stream order: they share the handle's
+ * work-list and accumulator words.                                                         */
 int mpx_group_step(mpx_engine* eng, const mpx_group_batch* b);
 int mpx_group_step_dev(mpx_engine* eng, const mpx_group_batch* b, void* stream);
 

@@ -214,7 +214,8 @@ int mpx_open(int device, const mpx_config* cfg, mpx_engine** out) {
         hipMalloc(&e->d_red, mpx::kRedWords * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&e->d_part, (size_t)mpx::kTileGrid * mpx::kPartStride * sizeof(uint32_t)) !=
             hipSuccess ||
-        hipMalloc(&e->d_wcount, sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&e->d_wcount, mpx::kStepCtlWords * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(e->d_wcount, 0, mpx::kStepCtlWords * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&e->worklist.p, e->worklist.cap) != hipSuccess ||
         hipMemset(e->d_err, 0, sizeof(uint32_t)) != hipSuccess) {
         (void)hipGetLastError();
@@ -595,7 +596,7 @@ int mpx_step_totals_dev(mpx_engine* e, const mpx_group_batch* b, int64_t* d_tota
     if (!b || !d_totals) return fail(e, MPX_E_INVAL, "null argument");
     if (b->n_groups && (!b->n_decided || !b->executed_in || !b->executed_out || !b->cmd_off))
         return fail(e, MPX_E_INVAL, "mpx_step_totals_dev needs n_decided, executed_in/out, cmd_off");
-    HIPCHK(e, mpx::launch_step_totals(b, d_totals, pick(e, stream)));
+    HIPCHK(e, mpx::launch_step_totals(b, d_totals, e->d_wcount, pick(e, stream)));
     return MPX_OK;
 }
 

@@ -52,7 +52,12 @@ hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
                              const mpx_group_batch* b, uint32_t* worklist, uint32_t* wcount,
                              uint32_t* err, hipStream_t stream);
 // d_totals[0..2] = decided instances, executed instances, executed commands of the batch
-hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, hipStream_t stream);
+// step control words (engine-owned, zeroed once): [0] work-list count, [1] its ticket, [4..9]
+// the totals' 64-bit accumulators, [10] their ticket. Both kernels that consume a count reset
+// it in their last workgroup, so a step launches no memset.
+constexpr int kStepCtlWords = 16;
+hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, uint32_t* ctl,
+                              hipStream_t stream);
 
 // ---- global KV table apply (mpx_apply) ----------------------------------------------------
 struct KvTable {

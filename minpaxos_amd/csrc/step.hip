@@ -1034,12 +1034,17 @@ template <int MODE>
 __global__ __launch_bounds__(kStepBlock) void k_group_general(mpx_group_batch b, int32_t nrep,
                                                               uint32_t kvpg,
                                                               const uint32_t* worklist,
-                                                              const uint32_t* wcount, uint32_t* err) {
+                                                              uint32_t* wcount, uint32_t* err) {
     __shared__ GenLds S;
     const uint32_t n = *wcount;
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         group_general<MODE>(S, b, worklist[i], nrep, kvpg, err);
         __syncthreads();
+    }
+    // the last workgroup to finish (every one has read the count) zeroes it for the next step
+    if (threadIdx.x == 0 && atomicAdd(wcount + 1, 1u) == gridDim.x - 1) {
+        wcount[0] = 0;
+        wcount[1] = 0;
     }
 }
 
@@ -1077,7 +1082,7 @@ void launch_step(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t
         k_fill_worklist<<<(b->n_groups + 255) / 256, 256, 0, stream>>>(worklist, wcount,
                                                                        b->n_groups);
     }
-    const unsigned gen_grid = b->n_groups < 1024 ? b->n_groups : 1024;
+    const unsigned gen_grid = b->n_groups < 256 ? b->n_groups : 256;  // one per CU (LDS)
     k_group_general<MODE><<<gen_grid, kStepBlock, 0, stream>>>(*b, nrep, kvpg, worklist, wcount,
                                                                err);
 }
@@ -1089,8 +1094,6 @@ hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
     if (!b->n_groups) return hipSuccess;
     if (kv_per_group > (uint32_t)kDCap) return hipErrorInvalidValue;
     if (b->ipg > (uint32_t)kMaxIpgBits) return hipErrorInvalidValue;
-    hipError_t r = hipMemsetAsync(wcount, 0, sizeof(uint32_t), stream);
-    if (r != hipSuccess) return r;
     if (mode == MPX_MODE_MIN)
         launch_step<MPX_MODE_MIN>(b, nrep, kv_per_group, worklist, wcount, err, stream);
     else
@@ -1099,9 +1102,12 @@ hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
 }
 
 // per-step totals of a batch: decided instances, executed instances, executed commands. One
-// group per lane, a block reduction, one 64-bit atomic per block and counter (totals zeroed by
-// the launcher on the same stream).
-__global__ __launch_bounds__(256) void k_step_totals(mpx_group_batch b, unsigned long long* totals) {
+// group per lane, a block reduction, one 64-bit atomic per block and counter into the engine's
+// accumulators; the last workgroup writes the totals and zeroes the accumulators.
+__global__ __launch_bounds__(256) void k_step_totals(mpx_group_batch b, unsigned long long* totals,
+                                                     uint32_t* ctl) {
+    unsigned long long* acc = reinterpret_cast<unsigned long long*>(ctl + 4);
+    __shared__ bool last;
     __shared__ unsigned long long red[3][kStepBlock / kWave];
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long d = 0, xi = 0, xc = 0;
@@ -1131,15 +1137,26 @@ __global__ __launch_bounds__(256) void k_step_totals(mpx_group_batch b, unsigned
     if (threadIdx.x < 3) {
         unsigned long long v = 0;
         for (int k = 0; k < kStepBlock / kWave; ++k) v += red[threadIdx.x][k];
-        if (v) atomicAdd(totals + threadIdx.x, v);
+        if (v) atomicAdd(acc + threadIdx.x, v);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();  // this block's sums before its ticket
+        last = atomicAdd(ctl + 10, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x < 3) {
+        __threadfence();
+        totals[threadIdx.x] = atomicExch(acc + threadIdx.x, 0ull);
+        if (threadIdx.x == 0) ctl[10] = 0;
     }
 }
 
-hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, hipStream_t stream) {
-    hipError_t r = hipMemsetAsync(totals, 0, MPX_STEP_TOTALS * sizeof(int64_t), stream);
-    if (r != hipSuccess || !b->n_groups) return r;
-    k_step_totals<<<(b->n_groups + kStepBlock - 1) / kStepBlock, kStepBlock, 0, stream>>>(
-        *b, reinterpret_cast<unsigned long long*>(totals));
+hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, uint32_t* ctl,
+                              hipStream_t stream) {
+    const uint32_t blocks = b->n_groups ? (b->n_groups + kStepBlock - 1) / kStepBlock : 1;
+    k_step_totals<<<blocks, kStepBlock, 0, stream>>>(*b, reinterpret_cast<unsigned long long*>(totals),
+                                                     ctl);
     return hipGetLastError();
 }
 
