@@ -38,6 +38,7 @@ constexpr int kE = MPX_DECODE_WINDOW;   // entry offsets per chunk map
 constexpr int kTL = 128;                // chunks (lanes) per tile
 constexpr int kTB = kC * kTL;           // tile bytes
 constexpr int kGT = 256;                // tiles per group
+constexpr int kDRow = kC + 4;           // LDS row of a chunk's DP (bank-conflict padding)
 constexpr uint8_t kTerm = 0xFF;         // terminal (tree levels >= 1, tile / group maps)
 constexpr uint8_t kDeadE = 0xFF;        // no entry (past the stop)
 static_assert(kE == 64 && kE + kC <= 255, "u8 DP encoding: exit offsets, then terminals");
@@ -286,7 +287,9 @@ __device__ __forceinline__ void chunk_groups(const uint8_t* X, int xstride, uint
 }
 
 __global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
-    __shared__ __attribute__((aligned(16))) uint8_t D[kTL][kC];  // var lengths, then the DP
+    // var lengths, then the DP; rows padded to 33 dwords so the 64 lanes of a wave, each on its
+    // own row, hit 64 different banks (a 128-byte stride put every lane on two banks)
+    __shared__ __attribute__((aligned(16))) uint8_t D[kTL][kDRow];
     __shared__ uint8_t G[kTL / 8][kE];
     const int l = threadIdx.x;
     const uint64_t t0 = (uint64_t)blockIdx.x * kTB;
@@ -330,13 +333,14 @@ __global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
     else
         chunk_dp<false>(wd, c0, P.len, lut, P.legacy != 0, D[l]);
     {  // this chunk's map (64 bytes) for the emit pass and the walk
-        const uint4* src = reinterpret_cast<const uint4*>(D[l]);
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(D[l]);
         uint4* dst = reinterpret_cast<uint4*>(W.cmap + ((uint64_t)blockIdx.x * kTL + l) * kE);
 #pragma unroll
-        for (int i = 0; i < kE / 16; ++i) dst[i] = src[i];
+        for (int i = 0; i < kE / 16; ++i)
+            dst[i] = make_uint4(src[4 * i], src[4 * i + 1], src[4 * i + 2], src[4 * i + 3]);
     }
     __syncthreads();
-    chunk_groups(&D[0][0], kC, G);
+    chunk_groups(&D[0][0], kDRow, G);
     __syncthreads();
     if (l < kE) {  // the tile map: entry l through the 16 group maps
         uint32_t x = (uint32_t)l;
@@ -522,10 +526,17 @@ struct Outs {
 __device__ __forceinline__ int32_t le32(const Bytes& by, uint64_t i) {
     return (int32_t)(by(i) | (by(i + 1) << 8) | (by(i + 2) << 16) | (by(i + 3) << 24));
 }
+// 4 bytes at LDS byte offset o from two aligned dword reads (o + 8 inside the buffer)
+__device__ __forceinline__ int32_t lds_le32(const uint8_t* B, uint32_t o) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(B) + (o >> 2);
+    const uint32_t sh = o & 3u;
+    const uint64_t x = ((uint64_t)w[1] << 32) | w[0];
+    return (int32_t)(uint32_t)(x >> (8 * sh));
+}
 
 __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint32_t n_tiles,
                                                  mpx_stream_result* res) {
-    __shared__ __attribute__((aligned(16))) uint8_t B[kTB + kE];
+    __shared__ __attribute__((aligned(16))) uint8_t B[kTB + kE + 16];  // + lds_le32's 2nd dword
     __shared__ __attribute__((aligned(16))) uint8_t X[kTL][kE];  // the tile's chunk maps
     __shared__ uint8_t G[kTL / 8][kE];
     __shared__ uint8_t GE[kTL / 8];
@@ -744,12 +755,13 @@ __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint
             ++idx[2];
             if (at_stop) break;
         } else if (code == MPX_PEER_ACCEPT_REPLY) {
-            if (idx[0] < O.ar_cap) {
+            if (idx[0] < O.ar_cap) {  // a complete fixed frame: inside the LDS window
+                const uint32_t o = (uint32_t)(a - t0);
                 mpx_accept_reply r;
-                r.instance = le32(by, a + 1);
-                r.ok = by(a + 5);
-                r.ballot = le32(by, a + 6);
-                r.id = P.proto == MPX_MODE_MIN ? le32(by, a + 10) : -1;
+                r.instance = lds_le32(B, o + 1);
+                r.ok = B[o + 5];
+                r.ballot = lds_le32(B, o + 6);
+                r.id = P.proto == MPX_MODE_MIN ? lds_le32(B, o + 10) : -1;
                 r.pad[0] = r.pad[1] = r.pad[2] = 0;
                 O.ar[idx[0]] = r;
             }
