@@ -185,8 +185,13 @@ struct Work {
     uint8_t* tent;             // [tiles] true entry (kDeadE past the stop)
     uint8_t* gmap;             // [groups][kE]
     uint8_t* gent;             // [groups]
-    unsigned long long* lb;    // [tiles][4] look-back words: status << 32 | count
-    uint32_t* ticket;
+    uint32_t* tcnt;            // [tiles][4] records of each kind the tile emits (k_sd_count)
+    uint32_t* tpre;            // [tiles][4] exclusive prefixes of tcnt within 1024 tiles
+    uint32_t* btot;            // [tiles / 1024][4] totals of the scan's workgroups
+    uint32_t* boff;            // [tiles / 1024][4] their exclusive prefixes
+    uint32_t* ticket;          // the scan's last-workgroup ticket (zeroed per call)
+    uint2* cinfo;              // [tiles][kTL] per chunk: .x = entry, .y = its 4 record counts
+                               // (u8 each; k_sd_count -> k_sd_emit)
     uint64_t* stop;            // [0] stop position, [1] next, [2] reason, [3..7] VarInfo of a
                                // LONG stop frame, [8..11] the call's input counts
 };
@@ -534,41 +539,10 @@ __device__ __forceinline__ int32_t lds_le32(const uint8_t* B, uint32_t o) {
     return (int32_t)(uint32_t)(x >> (8 * sh));
 }
 
-__global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint32_t n_tiles,
-                                                 mpx_stream_result* res) {
-    __shared__ __attribute__((aligned(16))) uint8_t B[kTB + kE + 16];  // + lds_le32's 2nd dword
-    __shared__ __attribute__((aligned(16))) uint8_t X[kTL][kE];  // the tile's chunk maps
-    __shared__ uint8_t G[kTL / 8][kE];
-    __shared__ uint8_t GE[kTL / 8];
-    __shared__ uint8_t En[kTL];
-    __shared__ uint32_t tile_s;
-    __shared__ uint32_t wsum[kTL / kWave][4];
-    __shared__ uint32_t pre_s[4];
+// the tile's chunk entries: the tile's true entry through its chunk maps (X, in LDS)
+__device__ __forceinline__ void chunk_entries(uint32_t ent, uint8_t (*X)[kE], uint8_t (*G)[kE],
+                                              uint8_t* GE, uint8_t* En) {
     const int l = threadIdx.x;
-    if (l == 0) tile_s = atomicAdd(W.ticket, 1u);  // tiles in dispatch order (look-back)
-    __syncthreads();
-    const uint32_t tile = tile_s;
-    const uint8_t ent = W.tent[tile];
-    if (ent == kDeadE) return;  // every tile after the stop tile, never one before it
-    const uint64_t t0 = (uint64_t)tile * kTB;
-    for (int i = l; i < (kTB + kE) / 16; i += kTL) {
-        const uint64_t a = t0 + (uint64_t)i * 16;
-        uint4 v;
-        if (a + 16 <= P.len) {
-            v = *reinterpret_cast<const uint4*>(P.buf + a);
-        } else {
-            uint32_t q[4] = {0, 0, 0, 0};
-            for (int b = 0; b < 16; ++b)
-                if (a + b < P.len) q[b >> 2] |= (uint32_t)P.buf[a + b] << (8 * (b & 3));
-            v = make_uint4(q[0], q[1], q[2], q[3]);
-        }
-        *reinterpret_cast<uint4*>(&B[i * 16]) = v;
-    }
-    {  // the tile's chunk maps
-        const uint4* src = reinterpret_cast<const uint4*>(W.cmap + (uint64_t)tile * kTL * kE);
-        for (int i = l; i < kTL * kE / 16; i += kTL) reinterpret_cast<uint4*>(&X[0][0])[i] = src[i];
-    }
-    __syncthreads();
     chunk_groups(&X[0][0], kE, G);
     __syncthreads();
     if (l == 0) {  // group entries from the tile's entry
@@ -588,37 +562,192 @@ __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint
         }
     }
     __syncthreads();
-    const uint32_t e = En[l];
+}
+
+__device__ __forceinline__ void load_chunk_maps(const Work& W, uint32_t tile, uint8_t (*X)[kE]) {
+    const uint4* src = reinterpret_cast<const uint4*>(W.cmap + (uint64_t)tile * kTL * kE);
+    for (int i = threadIdx.x; i < kTL * kE / 16; i += kTL) reinterpret_cast<uint4*>(&X[0][0])[i] = src[i];
+}
+
+// frames of the lane's chunk on the true chain, by kind: AcceptReplies, PrepareReplies, variable
+// messages, other fixed frames (every frame before the stop is complete and in the window).
+// code_at(a): the byte at stream position a.
+template <class CodeAt>
+__device__ __forceinline__ void chunk_counts(uint32_t e, uint64_t c0, uint64_t stop, bool long_stop,
+                                             const SParams& P, const Bytes& by, CodeAt code_at,
+                                             uint32_t (&cnt)[4]) {
+    const uint64_t lut = P.proto == MPX_MODE_MIN ? kLutMin : kLutClassic;
+    if (e == kDeadE) return;
+    for (uint64_t a = c0 + e; a < c0 + kC;) {
+        const uint32_t code = code_at(a);
+        if (a == stop) {
+            if (long_stop) {
+                cnt[2]++;
+                cnt[1] += code == MPX_PEER_PREPARE_REPLY ? 1u : 0u;
+            }
+            break;
+        }
+        uint32_t fl = lut_len(lut, code);
+        if (fl == 0) {
+            fl = parse_var(by, P.len, ~0ull, a, P.proto).f.len;
+            cnt[2]++;
+            cnt[1] += code == MPX_PEER_PREPARE_REPLY ? 1u : 0u;
+        } else {
+            cnt[code == MPX_PEER_ACCEPT_REPLY ? 0 : 3]++;
+        }
+        a += fl;
+    }
+}
+
+// pass C1: every tile's record counts (the emit pass takes its output indices from their
+// exclusive scan; a decoupled look-back across the ~1500 tiles in flight waited on device-scope
+// loads, which bypass the XCDs' L2s)
+// the tile's bytes [t0, t0 + kTB + kE) into LDS (zero past len)
+__device__ __forceinline__ void stage_tile(const SParams& P, uint64_t t0, uint8_t* B) {
+    for (int i = threadIdx.x; i < (kTB + kE) / 16; i += kTL) {
+        const uint64_t a = t0 + (uint64_t)i * 16;
+        uint4 v;
+        if (a + 16 <= P.len) {
+            v = *reinterpret_cast<const uint4*>(P.buf + a);
+        } else {
+            uint32_t q[4] = {0, 0, 0, 0};
+            for (int b = 0; b < 16; ++b)
+                if (a + b < P.len) q[b >> 2] |= (uint32_t)P.buf[a + b] << (8 * (b & 3));
+            v = make_uint4(q[0], q[1], q[2], q[3]);
+        }
+        *reinterpret_cast<uint4*>(&B[i * 16]) = v;
+    }
+}
+
+__global__ __launch_bounds__(kTL) void k_sd_count(SParams P, Work W) {
+    __shared__ __attribute__((aligned(16))) uint8_t B[kTB + kE];
+    __shared__ __attribute__((aligned(16))) uint8_t X[kTL][kE];
+    __shared__ uint8_t G[kTL / 8][kE];
+    __shared__ uint8_t GE[kTL / 8];
+    __shared__ uint8_t En[kTL];
+    __shared__ uint32_t wsum[kTL / kWave][4];
+    const int l = threadIdx.x;
+    const uint32_t tile = blockIdx.x;
+    const uint8_t ent = W.tent[tile];
+    if (ent == kDeadE) {
+        if (l < 4) W.tcnt[4 * (uint64_t)tile + l] = 0;
+        return;
+    }
+    const uint64_t t0 = (uint64_t)tile * kTB;
+    stage_tile(P, t0, B);
+    load_chunk_maps(W, tile, X);
+    __syncthreads();
+    chunk_entries(ent, X, G, GE, En);
+    const uint64_t c0 = t0 + (uint64_t)l * kC;
+    const Bytes by{P.buf, B, t0, t0 + kTB + kE < P.len ? t0 + kTB + kE : P.len};
+    uint32_t cnt[4] = {0, 0, 0, 0};
+    chunk_counts(En[l], c0, W.stop[0], (int)W.stop[2] == MPX_DECODE_LONG, P, by,
+                 [&](uint64_t a) { return (uint32_t)B[a - t0]; }, cnt);
+    W.cinfo[(uint64_t)tile * kTL + l] =
+        make_uint2(En[l], cnt[0] | (cnt[1] << 8) | (cnt[2] << 16) | (cnt[3] << 24));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t x = cnt[k];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+        if (lane_id() == 0) wsum[l / kWave][k] = x;
+    }
+    __syncthreads();
+    if (l < 4) {
+        uint32_t x = 0;
+        for (int w = 0; w < kTL / kWave; ++w) x += wsum[w][l];
+        W.tcnt[4 * (uint64_t)tile + l] = x;
+    }
+}
+
+// pass C2: exclusive scan of the tile counts: a workgroup scans 1024 tiles (coalesced) and
+// publishes its total; the last workgroup to finish scans the totals into per-workgroup offsets
+// (tile prefix = tpre[tile] + boff[tile / kScanT])
+constexpr int kScanT = 1024;
+__global__ __launch_bounds__(kScanT) void k_sd_scan(Work W, uint32_t n_tiles) {
+    __shared__ uint32_t ws[kScanT / kWave][4];
+    __shared__ bool last;
+    const int t = threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * kScanT + t;
+    uint4 c = make_uint4(0, 0, 0, 0);
+    if (i < n_tiles) c = reinterpret_cast<const uint4*>(W.tcnt)[i];
+    uint32_t v[4] = {c.x, c.y, c.z, c.w}, ex[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t x = v[k];
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d);
+            if (lane_id() >= d) x += y;
+        }
+        if (lane_id() == kWave - 1) ws[t / kWave][k] = x;
+        ex[k] = x - v[k];
+    }
+    __syncthreads();
+    uint32_t tot[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        for (int w = 0; w < kScanT / kWave; ++w) {
+            ex[k] += w < t / kWave ? ws[w][k] : 0u;
+            tot[k] += ws[w][k];
+        }
+    if (i < n_tiles) reinterpret_cast<uint4*>(W.tpre)[i] = make_uint4(ex[0], ex[1], ex[2], ex[3]);
+    if (t == 0) {
+        reinterpret_cast<uint4*>(W.btot)[blockIdx.x] = make_uint4(tot[0], tot[1], tot[2], tot[3]);
+        __threadfence();
+        last = atomicAdd(W.ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    // the workgroup offsets (at most 128 workgroups: 2^31 bytes / 16 KB tiles / 1024)
+    const uint32_t nb = gridDim.x;
+    uint32_t b[4] = {0, 0, 0, 0};
+    if ((uint32_t)t < nb)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            b[k] = __hip_atomic_load(W.btot + 4 * t + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t x = b[k];
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d);
+            if (lane_id() >= d) x += y;
+        }
+        if (lane_id() == kWave - 1) ws[t / kWave][k] = x;
+        ex[k] = x - b[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        for (int w = 0; w < t / kWave; ++w) ex[k] += ws[w][k];
+    if ((uint32_t)t < nb)
+        reinterpret_cast<uint4*>(W.boff)[t] = make_uint4(ex[0], ex[1], ex[2], ex[3]);
+    if (t == 0) *W.ticket = 0;
+}
+
+__global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint32_t n_tiles,
+                                                 mpx_stream_result* res) {
+    __shared__ __attribute__((aligned(16))) uint8_t B[kTB + kE + 16];  // + lds_le32's 2nd dword
+    __shared__ uint32_t wsum[kTL / kWave][4];
+    const int l = threadIdx.x;
+    const uint32_t tile = blockIdx.x;
+    const uint8_t ent = W.tent[tile];
+    if (ent == kDeadE) return;  // every tile after the stop tile, never one before it
+    const uint64_t t0 = (uint64_t)tile * kTB;
+    stage_tile(P, t0, B);
+    const uint2 ci = W.cinfo[(uint64_t)tile * kTL + l];  // entry and counts (k_sd_count)
+    __syncthreads();
+    const uint32_t e = ci.x;
     const uint64_t stop = W.stop[0];
     const int why = (int)W.stop[2];
     const bool long_stop = why == MPX_DECODE_LONG;
     const Bytes by{P.buf, B, t0, t0 + kTB + kE < P.len ? t0 + kTB + kE : P.len};
     const uint64_t c0 = t0 + (uint64_t)l * kC;
-    // walk 1: frames of this chunk on the true chain: AcceptReplies, PrepareReplies, variable
-    // messages, other fixed frames (every frame before the stop is complete and in the window)
-    uint32_t cnt[4] = {0, 0, 0, 0};
+    const uint32_t cnt[4] = {ci.y & 0xFFu, (ci.y >> 8) & 0xFFu, (ci.y >> 16) & 0xFFu, ci.y >> 24};
     const uint64_t lut = P.proto == MPX_MODE_MIN ? kLutMin : kLutClassic;
-    if (e != kDeadE) {
-        for (uint64_t a = c0 + e; a < c0 + kC;) {
-            const uint32_t code = B[a - t0];  // a frame on the chain starts inside the tile
-            if (a == stop) {
-                if (long_stop) {
-                    cnt[2]++;
-                    cnt[1] += code == MPX_PEER_PREPARE_REPLY ? 1u : 0u;
-                }
-                break;
-            }
-            uint32_t fl = lut_len(lut, code);
-            if (fl == 0) {
-                fl = parse_var(by, P.len, ~0ull, a, P.proto).f.len;
-                cnt[2]++;
-                cnt[1] += code == MPX_PEER_PREPARE_REPLY ? 1u : 0u;
-            } else {
-                cnt[code == MPX_PEER_ACCEPT_REPLY ? 0 : 3]++;
-            }
-            a += fl;
-        }
-    }
     // block exclusive scan of the four counts
     uint32_t incl[4], tot[4];
 #pragma unroll
@@ -643,55 +772,21 @@ __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint
         incl[k] = incl[k] - cnt[k] + before;  // exclusive within the tile
         tot[k] = all;
     }
-    // decoupled look-back over tiles (wave 0, 64 predecessors per round). Per tile and count
-    // one 64-bit word, status << 32 | value (1: the tile's own count, 2: the inclusive count
-    // up to it), so a word is valid on its own: relaxed device-scope loads and stores, no fences
-    if (l < kWave) {
-        unsigned long long* lb = W.lb;
-        uint32_t pre[4] = {0, 0, 0, 0};
-        if (l < 4 && tile > 0)
-            __hip_atomic_store(lb + 4 * (uint64_t)tile + l, (1ull << 32) | tot[l],
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            for (int64_t j0 = (int64_t)tile - 1; j0 >= 0;) {
-                const int64_t j = j0 - l;
-                const unsigned long long w =
-                    j >= 0 ? __hip_atomic_load(lb + 4 * (uint64_t)j + k, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT)
-                           : (2ull << 32);  // before tile 0: an inclusive zero
-                const uint32_t f = (uint32_t)(w >> 32);
-                const unsigned long long m_inc = __ballot(f == 2u);
-                const int first = m_inc ? __ffsll((long long)m_inc) - 1 : kWave;
-                const unsigned long long upto =
-                    first >= kWave - 1 ? ~0ull : ((2ull << first) - 1ull);
-                if (__ballot(f == 0u) & upto) continue;  // not published yet: spin
-                uint32_t v = l <= first ? (uint32_t)w : 0u;
-#pragma unroll
-                for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-                pre[k] += v;
-                if (first < kWave) break;
-                j0 -= kWave;
-            }
-        }
-        if (l < 4) {
-            __hip_atomic_store(lb + 4 * (uint64_t)tile + l, (2ull << 32) | (pre[l] + tot[l]),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            pre_s[l] = pre[l];
-        }
-    }
-    __syncthreads();
     uint64_t idx[4];
     const uint64_t base[4] = {W.stop[8], W.stop[9], W.stop[10], W.stop[11]};
+    uint32_t tp[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) idx[k] = base[k] + pre_s[k] + incl[k];
+    for (int k = 0; k < 4; ++k) {
+        tp[k] = W.tpre[4 * (uint64_t)tile + k] + W.boff[4 * (uint64_t)(tile / kScanT) + k];
+        idx[k] = base[k] + tp[k] + incl[k];
+    }
     // the stop tile (the one holding the terminal byte, at the latest position len) owns the
     // totals: every later tile is dead
     if (stop / kTB == tile && l == 0) {
-        res->n_accept_replies = base[0] + pre_s[0] + tot[0];
-        res->n_prepare_replies = base[1] + pre_s[1] + tot[1];
-        res->n_var = base[2] + pre_s[2] + tot[2];
-        res->n_other = base[3] + pre_s[3] + tot[3];
+        res->n_accept_replies = base[0] + tp[0] + tot[0];
+        res->n_prepare_replies = base[1] + tp[1] + tot[1];
+        res->n_var = base[2] + tp[2] + tot[2];
+        res->n_other = base[3] + tp[3] + tot[3];
     }
     if (e == kDeadE) return;
     // walk 2: the records
@@ -791,7 +886,7 @@ __global__ void k_sd_empty(mpx_stream_result* res, uint64_t at) {
 // ---- host side ----------------------------------------------------------------------------
 namespace {
 struct Layout {
-    uint64_t cmap, tmap, tent, gmap, gent, lb, ticket, stop, total;
+    uint64_t cmap, tmap, tent, gmap, gent, tcnt, tpre, btot, boff, ticket, cinfo, stop, total;
 };
 Layout layout_of(uint64_t len) {
     const uint64_t tiles = n_tiles_of(len + 16), groups = (tiles + kGT - 1) / kGT;
@@ -803,8 +898,12 @@ Layout layout_of(uint64_t len) {
     L.tent = o; o += al(tiles);
     L.gmap = o; o += al(groups * kE);
     L.gent = o; o += al(groups);
-    L.lb = o; o += al(tiles * 32);
+    L.tcnt = o; o += al(tiles * 16);
+    L.tpre = o; o += al(tiles * 16);
+    L.btot = o; o += al((tiles / 1024 + 1) * 16);
+    L.boff = o; o += al((tiles / 1024 + 1) * 16);
     L.ticket = o; o += al(4);
+    L.cinfo = o; o += al(tiles * kTL * 8);
     L.stop = o; o += al(12 * 8);
     L.total = o;
     return L;
@@ -831,10 +930,10 @@ hipError_t launch_decode_stream(int proto, int legacy, const uint8_t* buf, uint6
     const Layout L = layout_of(len);
     char* w = (char*)work;
     Work W{(uint8_t*)(w + L.cmap), (uint8_t*)(w + L.tmap), (uint8_t*)(w + L.tent),
-           (uint8_t*)(w + L.gmap), (uint8_t*)(w + L.gent), (unsigned long long*)(w + L.lb),
-           (uint32_t*)(w + L.ticket), (uint64_t*)(w + L.stop)};
-    hipError_t r = hipMemsetAsync(w + L.lb, 0, (uint64_t)tiles * 32, stream);
-    if (r == hipSuccess) r = hipMemsetAsync(w + L.ticket, 0, 4, stream);
+           (uint8_t*)(w + L.gmap), (uint8_t*)(w + L.gent), (uint32_t*)(w + L.tcnt),
+           (uint32_t*)(w + L.tpre), (uint32_t*)(w + L.btot), (uint32_t*)(w + L.boff),
+           (uint32_t*)(w + L.ticket), (uint2*)(w + L.cinfo), (uint64_t*)(w + L.stop)};
+    const hipError_t r = hipMemsetAsync(w + L.ticket, 0, 4, stream);
     if (r != hipSuccess) return r;
     Outs O{outs.ar, outs.ar_cap, outs.prep, outs.prep_cap, outs.var, outs.var_cap, outs.oth,
            outs.oth_cap};
@@ -842,6 +941,8 @@ hipError_t launch_decode_stream(int proto, int legacy, const uint8_t* buf, uint6
     k_sd_group_maps<<<groups, kE, 0, stream>>>(W, tiles);
     k_sd_walk<<<1, 64, 0, stream>>>(P, W, tiles, groups, res);
     k_sd_tile_entries<<<groups, kE, 0, stream>>>(W, tiles);
+    k_sd_count<<<tiles, kTL, 0, stream>>>(P, W);
+    k_sd_scan<<<(tiles + kScanT - 1) / kScanT, kScanT, 0, stream>>>(W, tiles);
     k_sd_emit<<<tiles, kTL, 0, stream>>>(P, W, O, tiles, res);
     return hipGetLastError();
 }
