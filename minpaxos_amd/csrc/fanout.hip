@@ -239,23 +239,31 @@ __global__ __launch_bounds__(kFanThreads) void k_fan_scatter(
     const uint64_t r0 = (uint64_t)blockIdx.x * per_slice;
     const uint64_t r1 = n - r0 < per_slice ? n : r0 + per_slice;
     const uint32_t out_mis = (uint32_t)((uintptr_t)out & 3u);
+    // the wave's segment of a tile: reply k*64+l of segment w, coalesced per k; the next tile's
+    // replies are loaded while this tile is ranked, encoded and written
+    mpx_reply_rec nxt[kFanPer];
+    auto load_tile = [&](uint64_t t0) {
+        const uint32_t nt = (uint32_t)(r1 - t0 < (uint64_t)kFanTile ? r1 - t0 : kFanTile);
+#pragma unroll
+        for (int k = 0; k < kFanPer; ++k) {
+            const uint32_t j = w * kFanSeg + k * kWave + l;
+            if (j < nt) nxt[k] = recs[t0 + j];
+        }
+    };
+    if (r0 < r1) load_tile(r0);
     for (uint64_t t0 = r0; t0 < r1; t0 += kFanTile) {
         const uint32_t nt = (uint32_t)(r1 - t0 < (uint64_t)kFanTile ? r1 - t0 : kFanTile);
         for (uint32_t x = t; x < kFanWaves * C; x += kFanThreads) wcnt[x / C][x % C] = 0;
-        __syncthreads();
-        // load the wave's segment: reply k*64+l of segment w, coalesced per k
         mpx_reply_rec rec[kFanPer];
         uint32_t cl[kFanPer], lr[kFanPer];
 #pragma unroll
         for (int k = 0; k < kFanPer; ++k) {
             const uint32_t j = w * kFanSeg + k * kWave + l;
-            if (j < nt) {
-                rec[k] = recs[t0 + j];
-                cl[k] = fan_client(rec[k].client, C, err);
-            } else {
-                cl[k] = 0;
-            }
+            rec[k] = nxt[k];
+            cl[k] = j < nt ? fan_client(rec[k].client, C, err) : 0u;
         }
+        if (t0 + kFanTile < r1) load_tile(t0 + kFanTile);
+        __syncthreads();
         // stable rank within the wave's segment: lanes with the same client in one round
         // (match over the client bits), rounds in order, per-wave LDS counters
 #pragma unroll
@@ -322,8 +330,9 @@ __global__ __launch_bounds__(kFanThreads) void k_fan_scatter(
             const uint32_t c = sc[s];
             const uint32_t S = tstart[c];                        // run's first image slot
             const uint64_t d = ((uint64_t)base[c] + (s - S)) * kRecBytes;  // output offset
-            const uint64_t run_end = ((uint64_t)base[c] + tcnt[c]) * kRecBytes;
+            const uint32_t rem = (tcnt[c] - (s - S)) * kRecBytes;  // bytes from d to the run end
             const uint32_t head = (4u - (uint32_t)((d + out_mis) & 3u)) & 3u;
+            uint8_t* const od = out + d;
             // B = the reply's 25 bytes then 7 bytes of the next slot (pad when s is last)
             uint32_t B[8];
             const uint32_t* r = img + s * kSlotWords;
@@ -337,25 +346,25 @@ __global__ __launch_bounds__(kFanThreads) void k_fan_scatter(
                 if (cin >> 31) {  // carry bytes [d-(4-head), d) + the first head bytes
                     const uint32_t pre = 4 - head;
                     const uint32_t v = (cin & ((1u << (8 * pre)) - 1u)) | (B[0] << (8 * pre));
-                    *reinterpret_cast<uint32_t*>(out + d - pre) = v;
+                    *reinterpret_cast<uint32_t*>(od - pre) = v;
                 } else {
-                    for (uint32_t q = 0; q < head; ++q) out[d + q] = (uint8_t)(B[0] >> (8 * q));
+                    for (uint32_t q = 0; q < head; ++q) od[q] = (uint8_t)(B[0] >> (8 * q));
                 }
             }
 #pragma unroll
             for (uint32_t q = 0; q < 7; ++q) {
                 const uint32_t o = head + 4 * q;  // output dword at d + o (aligned)
                 if (o >= (uint32_t)kRecBytes) break;
-                const uint32_t v = head ? (uint32_t)((((uint64_t)B[q + 1] << 32) | B[q]) >> (8 * head))
-                                        : B[q];
-                if (d + o + 4 <= run_end) {
-                    if (!(MPX_FAN_ABLATE & 8)) *reinterpret_cast<uint32_t*>(out + d + o) = v;
-                } else if (d + o < run_end) {  // the run's last reply: its partial dword waits
-                    const uint32_t nb = (uint32_t)(run_end - (d + o));
+                const uint32_t v = __builtin_amdgcn_alignbyte(B[q + 1], B[q], head);
+                if (o + 4 <= rem) {
+                    if (!(MPX_FAN_ABLATE & 8)) *reinterpret_cast<uint32_t*>(od + o) = v;
+                } else if (o < rem) {  // the run's last reply: its partial dword waits
+                    const uint32_t nb = rem - o;
                     carry[c] = 0x80000000u | (v & ((1u << (8 * nb)) - 1u));
                 }
             }
-            if (s + 1 == S + tcnt[c] && ((run_end + out_mis) & 3u) == 0) carry[c] = 0x80000000u;
+            if (rem == (uint32_t)kRecBytes && ((d + kRecBytes + out_mis) & 3u) == 0)
+                carry[c] = 0x80000000u;
         }
         __syncthreads();
         for (uint32_t c = t; c < C; c += kFanThreads) base[c] += tcnt[c];
