@@ -1,4 +1,6 @@
-// apply.hip — batched state-machine apply against the engine's device KV table (A5/A6).
+// apply.hip — the engine's device KV table (clear / import / export), the sort-based apply
+// pipeline used for tables past apply_fast.hip's bin limit (and as its A/B reference, env
+// MPX_APPLY_FALLBACK=1), the dispatcher of mpx_apply, and state.ConflictBatch (A5/A6).
 //
 // Reference: (*state.Command).Execute  src/state/state.go:77-103, applied in log order by
 // executeCommands  src/bareminpaxos/bareminpaxos.go:1066-1098; state.Conflict state.go:53-60;
@@ -38,63 +40,17 @@
 // command (2), one per PUT (1) and one value gather per GET (8), all reads. Chunks only bound
 // the scratch memory.
 // Steps 3, 5 and 7 use rocPRIM device primitives (stable LSD radix sort, look-back scan_by_key).
+#include <cstdlib>
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
 
-#include "common.hpp"
-#include "kernels.hpp"
+#include "kvtab.hpp"
 
 namespace mpx {
 
-constexpr int64_t kSentinel = INT64_MIN;
-// per-slot state word: bit 0 present (has a value); bit 1 the last command on the slot in call
-// epoch (word >> 2) was a PUT. Epochs start at 1, so a cleared word (0) is "untouched".
-constexpr uint32_t kPresent = 1u;
-constexpr uint32_t kLastPut = 2u;
-constexpr uint32_t kEpochMax = 1u << 30;
 // op class carried in the low 2 bits of a sort key
 constexpr uint32_t kClsOther = 0, kClsPut = 1, kClsGet = 2;
-
-__device__ __forceinline__ uint64_t hash64(uint64_t x) {
-    x ^= x >> 30;
-    x *= 0xBF58476D1CE4E5B9ull;
-    x ^= x >> 27;
-    x *= 0x94D049BB133111EBull;
-    x ^= x >> 31;
-    return x;
-}
-
-// table arrays hold cap+1 entries; entry cap is the side slot of key INT64_MIN
-__device__ __forceinline__ int64_t kv_insert(const KvTable& t, int64_t key, uint32_t* err) {
-    if (key == kSentinel) return (int64_t)t.cap;
-    const uint64_t mask = t.cap - 1;
-    uint64_t s = hash64((uint64_t)key) & mask;
-    for (uint64_t probe = 0; probe < t.cap; ++probe, s = (s + 1) & mask) {
-        unsigned long long* slot = reinterpret_cast<unsigned long long*>(t.keys + s);
-        unsigned long long cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (cur == (unsigned long long)kSentinel) {
-            cur = atomicCAS(slot, (unsigned long long)kSentinel, (unsigned long long)key);
-            if (cur == (unsigned long long)kSentinel) return (int64_t)s;  // claimed
-        }
-        if ((int64_t)cur == key) return (int64_t)s;
-    }
-    raise_err(err, kErrKvFull);
-    return -1;
-}
-
-// lookup after all inserts of this call have finished (previous kernel): plain loads
-__device__ __forceinline__ int64_t kv_lookup(const KvTable& t, int64_t key) {
-    if (key == kSentinel) return (int64_t)t.cap;
-    const uint64_t mask = t.cap - 1;
-    uint64_t s = hash64((uint64_t)key) & mask;
-    for (uint64_t probe = 0; probe < t.cap; ++probe, s = (s + 1) & mask) {
-        const int64_t cur = t.keys[s];
-        if (cur == key) return (int64_t)s;
-        if (cur == kSentinel) return -1;
-    }
-    return -1;
-}
 
 __global__ void k_kv_fill(KvTable t) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -210,10 +166,17 @@ __device__ __forceinline__ unsigned long long probe_load(const int64_t* p) {
 }
 // the two probe loops resumed at slot s whose key `cur` was already loaded (k_kv_index issues
 // the first probe of several commands together)
+// (probes stay inside the key's 256-slot bucket, kvtab.hpp)
+__device__ __forceinline__ uint64_t next_in_bucket(uint64_t s) {
+    return (s & ~(uint64_t)(kSB - 1)) | ((s + 1) & (kSB - 1));
+}
+__device__ __forceinline__ uint64_t first_slot(const KvTable& t, int64_t key) {
+    const uint64_t h = hash64((uint64_t)key);
+    return ((uint64_t)bucket_of(h, t.lgnb) << kLgSB) | home_of(h);
+}
 __device__ __forceinline__ int64_t kv_insert_from(const KvTable& t, int64_t key, uint64_t s,
                                                   unsigned long long cur, uint32_t* err) {
-    const uint64_t mask = t.cap - 1;
-    for (uint64_t probe = 0; probe < t.cap; ++probe) {
+    for (int probe = 0; probe < kSB; ++probe) {
         unsigned long long* slot = reinterpret_cast<unsigned long long*>(t.keys + s);
         if (probe) cur = probe_load(t.keys + s);
         if (cur == (unsigned long long)kSentinel) {
@@ -221,7 +184,7 @@ __device__ __forceinline__ int64_t kv_insert_from(const KvTable& t, int64_t key,
             if (cur == (unsigned long long)kSentinel) return (int64_t)s;  // claimed
         }
         if ((int64_t)cur == key) return (int64_t)s;
-        s = (s + 1) & mask;
+        s = next_in_bucket(s);
     }
     raise_err(err, kErrKvFull);
     return -1;
@@ -229,12 +192,11 @@ __device__ __forceinline__ int64_t kv_insert_from(const KvTable& t, int64_t key,
 
 __device__ __forceinline__ int64_t kv_probe_racy_from(const KvTable& t, int64_t key, uint64_t s,
                                                       unsigned long long cur) {
-    const uint64_t mask = t.cap - 1;
-    for (uint64_t probe = 0; probe < t.cap; ++probe) {
+    for (int probe = 0; probe < kSB; ++probe) {
         if (probe) cur = probe_load(t.keys + s);
         if ((int64_t)cur == key) return (int64_t)s;
         if ((int64_t)cur == kSentinel) return -1;
-        s = (s + 1) & mask;
+        s = next_in_bucket(s);
     }
     return -1;
 }
@@ -253,7 +215,6 @@ __global__ __launch_bounds__(256) void k_kv_index(KvTable t, const uint8_t* __re
                                                   uint32_t* __restrict__ miss,
                                                   uint32_t* __restrict__ n_miss) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * kIndexUnroll;
-    const uint64_t mask = t.cap - 1;
     for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x * kIndexUnroll; i0 < m; i0 += stride) {
         uint8_t o[kIndexUnroll];
         int64_t k[kIndexUnroll];
@@ -268,7 +229,7 @@ __global__ __launch_bounds__(256) void k_kv_index(KvTable t, const uint8_t* __re
 #pragma unroll
         for (int u = 0; u < kIndexUnroll; ++u) {
             const uint64_t i = i0 + (uint64_t)u * blockDim.x + threadIdx.x;
-            h[u] = hash64((uint64_t)k[u]) & mask;
+            h[u] = first_slot(t, k[u]);
             cur[u] = i < m && k[u] != kSentinel ? probe_load(t.keys + h[u]) : 0ull;
         }
 #pragma unroll
@@ -573,8 +534,22 @@ uint64_t apply_chunk_commands(uint64_t chunk, uint64_t m) {
     return m < c ? (m ? m : 1) : c;
 }
 
-uint64_t apply_work_bytes(uint64_t chunk, uint64_t m) {
-    return layout(apply_chunk_commands(chunk, m)).total;
+namespace {
+// env MPX_APPLY_FALLBACK=1: the sort-based pipeline even where the partitioned one applies (A/B)
+bool use_fast(const KvTable& t) {
+    const char* f = getenv("MPX_APPLY_FALLBACK");
+    return apply_fast_ok(t) && !(f && f[0] == '1');
+}
+// env MPX_APPLY_HOT_MIN: sample count (of 32K) that makes a key hot; 0 = no hot keys
+uint32_t hot_min() {
+    const char* h = getenv("MPX_APPLY_HOT_MIN");
+    return h ? (uint32_t)strtoul(h, nullptr, 10) : 4u;
+}
+}  // namespace
+
+uint64_t apply_work_bytes(const KvTable& t, uint64_t chunk, uint64_t m) {
+    const uint64_t C = apply_chunk_commands(chunk, m);
+    return use_fast(t) ? apply_fast_work_bytes(t, C) : layout(C).total;
 }
 
 hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
@@ -582,6 +557,8 @@ hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const
                         uint32_t* err, hipStream_t stream) {
     if (!m) return hipSuccess;
     const uint64_t C = apply_chunk_commands(chunk, m);
+    if (use_fast(t))
+        return launch_apply_fast(t, op, key, val, m, ret, conf, C, w, hot_min(), err, stream);
     // result codes carry a chunk index or a slot in 29 bits
     if (C > kPayloadMask || t.cap + 1 > kPayloadMask) return hipErrorInvalidValue;
     const WorkLayout L = layout(C);

@@ -1,0 +1,1058 @@
+// apply_fast.hip — the partitioned apply pipeline of mpx_apply (A5/A6).
+//
+// Reference: (*state.Command).Execute  src/state/state.go:77-103, applied in log order by
+// executeCommands  src/bareminpaxos/bareminpaxos.go:1066-1098; state.Conflict state.go:53-60.
+//
+// Sequential semantics restated per key: for command i on key k,
+//   ret[i]  = PUT: val[i]; GET: val of the last PUT on k before i in this call, else the table
+//             value at call start if k is present, else NIL (0); other ops: 0
+//   conf[i] = Conflict(previous command on k in this call, command i)
+//   table   : k <- val of the last PUT on k in this call
+// Commands of different keys never interact, and the table (kvtab.hpp) is cut into 256-slot
+// buckets that each hold a closed set of keys. So the log is partitioned by bucket and every
+// bucket is resolved in LDS by one wave, against its own slice of the table, in log order:
+//   k_ap_select   one workgroup samples the chunk's keys; the most frequent keys seen at least
+//                 hot_min times in 32K samples (at most 63) are HOT: they skip the partition and are resolved in log order by a
+//                 per-key max-scan (below), so a skewed key space cannot pile onto one wave.
+//                 Index 0 is always the key INT64_MIN (the table's sentinel, kept in a side slot).
+//   k_ap_count    per 4096-command log tile: commands per bin (16 buckets) of the cold keys, and
+//                 per hot key the last position of any command and of a PUT in the tile
+//   scans         3-kernel scan of the tile rows: bin offsets per tile (sum), hot positions
+//                 before each tile (max)
+//   k_ap_scatter  per tile: a stable per-bin ranking (per-wave peer masks + wave prefix), the
+//                 tile's cold commands as a bin-sorted image in LDS, copied out as one contiguous
+//                 run per bin (16-byte key/value records + op bytes); each command's position in
+//                 the partition (pos1) is stored in log order
+//   k_ap_resolve  one workgroup per bin: its 16 bucket tables in LDS (keys, values, state), the
+//                 bin's records streamed in log order 1024 at a time, ranked by bucket, each
+//                 bucket's records resolved by its wave 64 at a time (peer masks within the 64, the
+//                 bucket table between rounds); results land at the record's partition position;
+//                 touched slots written back once
+//   k_ap_hot_commit  the hot keys' final value and state
+//   k_ap_emit     per tile, log order: a cold command's result is gathered from its partition
+//                 position (pos1), a hot command's from the per-wave peer scan, the earlier waves'
+//                 tables and the tile's incoming positions; ret / conf stored coalesced
+// Table traffic is one read and one write of each bin's slice per call instead of one random probe
+// per command. New keys: a bin whose records both PUT a key absent from the table and GET (or
+// run another op on) an absent key re-runs in two passes (insert every PUT key, then resolve), so
+// a GET before the first PUT of a new key still sees that later PUT as its successor. Calls of
+// several chunks insert every PUT key of the call first, as the fallback pipeline does.
+#include "kvtab.hpp"
+
+namespace mpx {
+
+constexpr int kTL = 4096;          // commands per log tile
+constexpr int kTT = 1024;          // threads of the tile and bin workgroups
+constexpr int kTW = kTT / kWave;   // 16 waves
+constexpr int kTPer = kTL / kTT;   // 4 commands per thread; wave w owns [256 w, 256 w + 256)
+constexpr int kHMax = 64;          // hot keys per chunk, index 0 = INT64_MIN
+constexpr int kHotTab = 128;       // LDS hash of the hot keys
+constexpr int kMaxBins = 1024;
+constexpr int kMaxBPB = 16;        // buckets per bin = waves of the resolve workgroup
+constexpr int kSampTab = 8192;     // k_ap_select's LDS count table
+constexpr uint32_t kSamples = 1u << 15;
+constexpr uint32_t kHotBit = 0x80000000u;
+constexpr uint32_t kNoSlot = ~0u;
+constexpr unsigned kScatterGrid = 256;  // persistent partition grid: one workgroup per CU
+
+// LDS slot state of k_ap_resolve
+constexpr uint8_t kSPresent = 1, kSLastPut = 2, kSTouched = 4, kSValDirty = 8, kSNew = 16,
+                  kSWasPresent = 32;
+// k_ap_resolve flags
+constexpr uint32_t kFAbsentOther = 1u, kFNewPut = 2u;
+
+struct ApHot {               // per chunk; written by k_ap_select (+ the scan's totals)
+    int64_t key[kHMax];
+    int64_t val0[kHMax];     // value at chunk start (present keys)
+    uint32_t slot[kHMax];    // table slot, kNoSlot when absent and never inserted
+    uint32_t flags[kHMax];   // bit 0 present, bit 1 last op PUT (if touched), bit 2 touched in call
+    uint32_t fin_any[kHMax]; // 1 + chunk position of the key's last command (0: none)
+    uint32_t fin_put[kHMax]; // 1 + chunk position of the key's last PUT (0: none)
+    uint32_t n;              // hot keys, >= 1
+    uint32_t restarts;       // bins that ran the two-pass form (diagnostic)
+};
+
+struct ApGeo {
+    uint32_t lgnb, lgbpb, nbin, rowlen, tiles, ng, tpg;
+};
+
+__device__ __forceinline__ uint32_t bin_of(uint64_t h, const ApGeo& g) {
+    return bucket_of(h, g.lgnb) >> g.lgbpb;
+}
+
+typedef __attribute__((address_space(3))) volatile uint8_t lds_u8;
+typedef __attribute__((address_space(3))) volatile uint16_t lds_u16;
+typedef __attribute__((address_space(3))) volatile unsigned long long lds_u64;
+
+// peers of this lane among the active lanes of the wave with the same class id c (< width of W):
+// every lane writes its lane id into W[c], reads back the id that remained (one per class), ORs
+// its bit into that id's mask and reads the mask back, then the mask is cleared for the next use.
+// LDS executes a wave's instructions in order, so each step sees the previous one complete.
+__device__ __forceinline__ unsigned long long wave_peers(lds_u8* W, lds_u64* PM, uint32_t c,
+                                                         bool act) {
+    unsigned long long peers = 0;
+    if (act) {
+        const int l = lane_id();
+        W[c] = (uint8_t)l;
+        const uint32_t cls = W[c];
+        __hip_atomic_fetch_or((__attribute__((address_space(3))) unsigned long long*)&PM[cls],
+                              1ull << l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        peers = PM[cls];
+        PM[cls] = 0ull;
+    }
+    return peers;
+}
+
+// the same without LDS, one ballot per distinct class among the active lanes: for the hot keys,
+// where most of a wave's lanes share a few classes and the LDS OR above would serialise on one word
+__device__ __forceinline__ unsigned long long wave_match(uint32_t c, bool act) {
+    unsigned long long rem = __ballot(act), mine = 0;
+    while (rem) {
+        const int lead = __ffsll((long long)rem) - 1;
+        const uint32_t cl = (uint32_t)__builtin_amdgcn_readlane((int)c, lead);
+        const bool in = act && c == cl;
+        const unsigned long long m = __ballot(in);
+        if (in) mine = m;
+        rem &= ~m;
+    }
+    return mine;
+}
+
+__device__ __forceinline__ int64_t shfl64(int64_t v, int src) {
+    return (int64_t)__shfl((long long)v, src);
+}
+
+// XCD-aware tile order of a persistent grid (gridDim a multiple of 8): workgroup b runs on XCD
+// b % 8; XCD x owns the contiguous tiles [xs, xe) and its workgroups walk them together, so the
+// runs that neighbouring tiles read or write in the same partition bin meet in one L2
+struct TileWalk {
+    uint32_t tile, end, step;
+};
+__device__ __forceinline__ TileWalk tile_walk(uint32_t tiles) {
+    const uint32_t x = blockIdx.x & 7u, i = blockIdx.x >> 3, nper = gridDim.x >> 3;
+    const uint32_t per = tiles >> 3, rem = tiles & 7u;
+    const uint32_t xs = x * per + (x < rem ? x : rem);
+    return TileWalk{xs + i, xs + per + (x < rem ? 1u : 0u), nper};
+}
+// the same for a one-tile-per-workgroup grid (gridDim == tiles)
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t tiles) {
+    const uint32_t x = blockIdx.x & 7u, i = blockIdx.x >> 3;
+    const uint32_t per = tiles >> 3, rem = tiles & 7u;
+    return x * per + (x < rem ? x : rem) + i;
+}
+
+// ---- hot keys ---------------------------------------------------------------------------------
+struct HotLds {
+    int64_t k[kHotTab];
+    int8_t h[kHotTab];
+};
+
+__device__ __forceinline__ void hot_build(HotLds& s, const ApHot* hot, uint32_t nh) {
+    for (int i = threadIdx.x; i < kHotTab; i += blockDim.x) s.k[i] = kSentinel;
+    __syncthreads();
+    for (uint32_t h = 1 + threadIdx.x; h < nh; h += blockDim.x) {
+        const int64_t key = hot->key[h];
+        uint32_t p = (uint32_t)(hash64((uint64_t)key) >> 8) & (kHotTab - 1);
+        for (;;) {
+            const unsigned long long cur =
+                atomicCAS(reinterpret_cast<unsigned long long*>(&s.k[p]),
+                          (unsigned long long)kSentinel, (unsigned long long)key);
+            if (cur == (unsigned long long)kSentinel) {
+                s.h[p] = (int8_t)h;
+                break;
+            }
+            p = (p + 1) & (kHotTab - 1);
+        }
+    }
+    __syncthreads();
+}
+
+// hot index of a key (hash hk), -1 if cold
+__device__ __forceinline__ int hot_find(const HotLds& s, uint32_t nh, int64_t key, uint64_t hk) {
+    if (key == kSentinel) return 0;
+    if (nh <= 1) return -1;
+    uint32_t p = (uint32_t)(hk >> 8) & (kHotTab - 1);
+    for (;;) {
+        const int64_t cur = s.k[p];
+        if (cur == key) return s.h[p];
+        if (cur == kSentinel) return -1;
+        p = (p + 1) & (kHotTab - 1);
+    }
+}
+
+// one workgroup: sample up to 32K keys of the chunk, pick the hot ones (the most frequent keys
+// seen at least hot_min times, at most kHMax - 1 of them), read their start state
+__global__ __launch_bounds__(kTT) void k_ap_select(KvTable t, const int64_t* __restrict__ key,
+                                                   uint32_t n, uint32_t hot_min, ApHot* hot) {
+    __shared__ int64_t sk[kSampTab];
+    __shared__ uint32_t sc[kSampTab];
+    __shared__ int64_t hk[kHMax];
+    __shared__ uint32_t nh, nge, thr;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kSampTab; i += kTT) {
+        sk[i] = kSentinel;
+        sc[i] = 0;
+    }
+    if (tid == 0) nh = 1;
+    __syncthreads();
+    const uint32_t S = n < kSamples ? n : kSamples;
+    if (hot_min) {
+        constexpr int kB = 8;  // loads in flight per thread
+        for (uint32_t i0 = tid; i0 < S; i0 += kTT * kB) {
+            int64_t k[kB];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const uint32_t i = i0 + u * kTT;
+                const uint32_t j = S == n ? i : (uint32_t)(((uint64_t)i * n) / S);
+                k[u] = i < S ? key[j] : kSentinel;
+            }
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                if (k[u] == kSentinel) continue;
+                // frequent keys arrive early; once the probe window is full a sample is dropped
+                uint32_t p = (uint32_t)hash64((uint64_t)k[u]) & (kSampTab - 1);
+                for (int probe = 0; probe < 16; ++probe, p = (p + 1) & (kSampTab - 1)) {
+                    int64_t cur = sk[p];
+                    if (cur == kSentinel)
+                        cur = (int64_t)atomicCAS(reinterpret_cast<unsigned long long*>(&sk[p]),
+                                                 (unsigned long long)kSentinel,
+                                                 (unsigned long long)k[u]);
+                    if (cur == kSentinel || cur == k[u]) {
+                        atomicAdd(&sc[p], 1u);
+                        break;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // the smallest threshold >= hot_min that leaves at most kHMax - 1 keys (binary search)
+        uint32_t lo = hot_min, hi = S + 1;  // count(>= hi) == 0 <= kHMax - 1
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if (tid == 0) nge = 0;
+            __syncthreads();
+            uint32_t c = 0;
+            for (int i = tid; i < kSampTab; i += kTT) c += sc[i] >= mid ? 1u : 0u;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
+            if (lane_id() == 0 && c) atomicAdd(&nge, c);
+            __syncthreads();
+            if (nge <= (uint32_t)kHMax - 1) hi = mid;
+            else lo = mid + 1;
+            __syncthreads();
+        }
+        if (tid == 0) thr = lo;
+        __syncthreads();
+        for (int i = tid; i < kSampTab; i += kTT)
+            if (sc[i] >= thr) {
+                const uint32_t x = atomicAdd(&nh, 1u);
+                if (x < kHMax) hk[x] = sk[i];
+            }
+        __syncthreads();
+    }
+    const uint32_t H = nh < (uint32_t)kHMax ? nh : (uint32_t)kHMax;
+    if (tid == 0) {
+        hot->n = H;
+        hot->restarts = 0;
+    }
+    const uint32_t ep = t.epoch[0];
+    for (uint32_t h = tid; h < H; h += kTT) {
+        const int64_t k = h == 0 ? kSentinel : hk[h];
+        const int64_t s = kv_lookup(t, k);
+        const uint32_t w = s >= 0 ? t.state[s] : 0u;
+        const uint32_t pres = w & kPresent;
+        hot->key[h] = k;
+        hot->slot[h] = s >= 0 ? (uint32_t)s : kNoSlot;
+        hot->flags[h] = pres | ((w >> 2) == ep ? (4u | (w & kLastPut)) : 0u);
+        hot->val0[h] = pres ? t.vals[s] : 0;
+    }
+}
+
+// ---- per-tile counts --------------------------------------------------------------------------
+__global__ __launch_bounds__(kTT) void k_ap_count(ApGeo g, const uint8_t* __restrict__ op,
+                                                  const int64_t* __restrict__ key, uint32_t n,
+                                                  uint32_t* __restrict__ rows,
+                                                  const ApHot* __restrict__ hot) {
+    __shared__ HotLds hl;
+    __shared__ uint32_t hist[kMaxBins];
+    __shared__ uint32_t ha[kHMax], hp[kHMax];
+    const int tid = threadIdx.x;
+    const uint32_t nh = hot->n;
+    for (uint32_t b = tid; b < g.nbin; b += kTT) hist[b] = 0;
+    if (tid < kHMax) {
+        ha[tid] = 0;
+        hp[tid] = 0;
+    }
+    hot_build(hl, hot, nh);
+    const uint32_t tile = xcd_tile(g.tiles);
+    const uint32_t j0 = tile * (uint32_t)kTL;
+    int64_t k[kTPer];
+#pragma unroll
+    for (int u = 0; u < kTPer; ++u) {
+        const uint32_t j = j0 + u * kTT + tid;
+        k[u] = j < n ? key[j] : 0;
+    }
+    const int l = lane_id();
+#pragma unroll
+    for (int u = 0; u < kTPer; ++u) {
+        const uint32_t j = j0 + u * kTT + tid;
+        const bool in = j < n;
+        const uint64_t h = hash64((uint64_t)k[u]);
+        const int hh = in ? hot_find(hl, nh, k[u], h) : -1;
+        if (in && hh < 0) atomicAdd(&hist[bin_of(h, g)], 1u);
+        const bool hotc = in && hh >= 0;
+        if (!__ballot(hotc)) continue;
+        // per hot key of the round: its last command and its last PUT, one LDS atomic each
+        const bool put = hotc && op[j] == MPX_OP_PUT;
+        const unsigned long long peers = wave_match((uint32_t)hh, hotc);
+        const unsigned long long puts = peers & __ballot(put);
+        if (hotc && hi_bit(peers) == l) atomicMax(&ha[hh], j + 1);
+        if (put && hi_bit(puts) == l) atomicMax(&hp[hh], j + 1);
+    }
+    __syncthreads();
+    uint32_t* row = rows + (uint64_t)tile * g.rowlen;
+    for (uint32_t b = tid; b < g.nbin; b += kTT) row[b] = hist[b];
+    if (tid < kHMax) {
+        row[g.nbin + 2 * tid] = ha[tid];
+        row[g.nbin + 2 * tid + 1] = hp[tid];
+    }
+}
+
+// ---- scan of the tile rows: columns < nbin exclusive sums, the rest exclusive maxima ----------
+__device__ __forceinline__ uint32_t col_op(bool sum, uint32_t a, uint32_t b) {
+    return sum ? a + b : (a > b ? a : b);
+}
+
+// (columns of hot keys past hot->n are all zero and skipped)
+__global__ __launch_bounds__(256) void k_ap_scan_part(ApGeo g, const uint32_t* __restrict__ rows,
+                                                      uint32_t* __restrict__ part,
+                                                      const ApHot* __restrict__ hot) {
+    const uint32_t gi = blockIdx.x;
+    const uint32_t t0 = gi * g.tpg, t1 = t0 + g.tpg < g.tiles ? t0 + g.tpg : g.tiles;
+    const uint32_t cols = g.nbin + 2 * hot->n;
+    for (uint32_t c = threadIdx.x; c < cols; c += 256) {
+        const bool sum = c < g.nbin;
+        uint32_t acc = 0;
+        uint32_t tt = t0;
+        for (; tt + 8 <= t1; tt += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = rows[(uint64_t)(tt + u) * g.rowlen + c];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc = col_op(sum, acc, v[u]);
+        }
+        for (; tt < t1; ++tt) acc = col_op(sum, acc, rows[(uint64_t)tt * g.rowlen + c]);
+        part[(uint64_t)gi * g.rowlen + c] = acc;
+    }
+}
+
+__global__ __launch_bounds__(kTT) void k_ap_scan_top(ApGeo g, uint32_t* __restrict__ part,
+                                                     uint32_t* __restrict__ bin_start,
+                                                     ApHot* __restrict__ hot) {
+    __shared__ uint32_t tot[kMaxBins];
+    __shared__ uint32_t wsum[kTW];
+    const int tid = threadIdx.x;
+    const uint32_t cols = g.nbin + 2 * hot->n;
+    for (uint32_t c = tid; c < g.rowlen; c += kTT) {
+        const bool sum = c < g.nbin;
+        uint32_t acc = 0;
+        for (uint32_t g0 = 0; c < cols && g0 < g.ng; g0 += 16) {  // 16 loads in flight
+            uint32_t v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                v[u] = g0 + u < g.ng ? part[(uint64_t)(g0 + u) * g.rowlen + c] : 0u;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                if (g0 + u < g.ng) part[(uint64_t)(g0 + u) * g.rowlen + c] = acc;
+                acc = col_op(sum, acc, v[u]);
+            }
+        }
+        if (sum) {
+            tot[c] = acc;
+        } else {
+            const uint32_t h = (c - g.nbin) >> 1;
+            if ((c - g.nbin) & 1) hot->fin_put[h] = acc;
+            else hot->fin_any[h] = acc;
+        }
+    }
+    __syncthreads();
+    // exclusive scan of the bin totals (nbin <= 1024: one per thread)
+    const uint32_t v = (uint32_t)tid < g.nbin ? tot[tid] : 0u;
+    uint32_t x = v;
+    const int l = lane_id();
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (l >= d) x += y;
+    }
+    if (l == kWave - 1) wsum[tid / kWave] = x;
+    __syncthreads();
+    uint32_t wb = 0;
+    for (int w2 = 0; w2 < tid / kWave; ++w2) wb += wsum[w2];
+    const uint32_t excl = wb + x - v;
+    if ((uint32_t)tid < g.nbin) {
+        bin_start[tid] = excl;
+        if ((uint32_t)tid == g.nbin - 1) bin_start[g.nbin] = excl + v;
+        for (uint32_t gi = 0; gi < g.ng; ++gi) part[(uint64_t)gi * g.rowlen + tid] += excl;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_ap_scan_rows(ApGeo g, uint32_t* __restrict__ rows,
+                                                      const uint32_t* __restrict__ part,
+                                                      const ApHot* __restrict__ hot) {
+    const uint32_t gi = blockIdx.x;
+    const uint32_t t0 = gi * g.tpg, t1 = t0 + g.tpg < g.tiles ? t0 + g.tpg : g.tiles;
+    const uint32_t cols = g.nbin + 2 * hot->n;
+    for (uint32_t c = threadIdx.x; c < cols; c += 256) {
+        const bool sum = c < g.nbin;
+        uint32_t acc = part[(uint64_t)gi * g.rowlen + c];
+        uint32_t tt = t0;
+        for (; tt + 8 <= t1; tt += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = rows[(uint64_t)(tt + u) * g.rowlen + c];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                rows[(uint64_t)(tt + u) * g.rowlen + c] = acc;
+                acc = col_op(sum, acc, v[u]);
+            }
+        }
+        for (; tt < t1; ++tt) {
+            uint32_t* p = rows + (uint64_t)tt * g.rowlen + c;
+            const uint32_t x = *p;
+            *p = acc;
+            acc = col_op(sum, acc, x);
+        }
+    }
+}
+
+// ---- partition ----------------------------------------------------------------------------------
+struct ScatterLds {
+    HotLds hl;
+    uint32_t roff[kMaxBins];    // this tile's run start per bin (partition position)
+    uint32_t lstart[kMaxBins];  // bin start inside the tile image
+    uint16_t cw[kTW][kMaxBins]; // per-wave counts -> exclusive prefix over the waves
+    uint8_t W[kTW][kMaxBins];
+    unsigned long long PM[kTW][kWave];
+    int4 img[kTL];              // bin-sorted (key, val) of the tile's cold commands
+    uint8_t iop[kTL];
+    uint16_t ibin[kTL];
+    uint32_t wsum[kTW];
+    uint32_t ncold;
+};
+
+__global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __restrict__ op,
+                                                    const int64_t* __restrict__ key,
+                                                    const int64_t* __restrict__ val, uint32_t n,
+                                                    const uint32_t* __restrict__ rows,
+                                                    const ApHot* __restrict__ hot,
+                                                    int4* __restrict__ rec_kv,
+                                                    uint8_t* __restrict__ rec_op,
+                                                    uint32_t* __restrict__ pos1) {
+    __shared__ ScatterLds S;
+    const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
+    const uint32_t nh = hot->n;
+    uint32_t* cw32 = reinterpret_cast<uint32_t*>(&S.cw[0][0]);
+    for (int i = tid; i < kTW * kMaxBins / 2; i += kTT) cw32[i] = 0u;
+    S.PM[w][l] = 0ull;
+    hot_build(S.hl, hot, nh);
+    TileWalk tw = tile_walk(g.tiles);
+    const uint32_t wofs = (uint32_t)w * (kWave * kTPer) + (uint32_t)l;
+    // this tile's commands in registers; the next tile's are loaded while this one is ranked
+    uint8_t o[kTPer];
+    int64_t k[kTPer], v[kTPer];
+    auto load = [&](uint32_t tile, uint8_t* o_, int64_t* k_, int64_t* v_) {
+#pragma unroll
+        for (int r = 0; r < kTPer; ++r) {
+            const uint32_t j = tile * (uint32_t)kTL + wofs + r * kWave;
+            const bool in = tile < tw.end && j < n;
+            o_[r] = in ? op[j] : 0;
+            k_[r] = in ? key[j] : 0;
+            v_[r] = in ? val[j] : 0;
+        }
+    };
+    load(tw.tile, o, k, v);
+    lds_u8* W = (lds_u8*)&S.W[w][0];
+    lds_u64* PM = (lds_u64*)&S.PM[w][0];
+    lds_u16* CW = (lds_u16*)&S.cw[w][0];
+    const unsigned long long below = (1ull << l) - 1ull;
+    for (; tw.tile < tw.end; tw.tile += tw.step) {
+        const uint32_t tile = tw.tile;
+        const uint32_t j0 = tile * (uint32_t)kTL + wofs;
+        uint8_t no[kTPer];
+        int64_t nk[kTPer], nv[kTPer];
+        load(tile + tw.step, no, nk, nv);
+        uint32_t bin[kTPer], rank[kTPer];
+        bool cold[kTPer];
+#pragma unroll
+        for (int r = 0; r < kTPer; ++r) {
+            const uint32_t j = j0 + r * kWave;
+            const bool in = j < n;
+            const uint64_t h = hash64((uint64_t)k[r]);
+            const int hh = in ? hot_find(S.hl, nh, k[r], h) : -1;
+            if (in && hh >= 0) pos1[j] = kHotBit | (uint32_t)hh;
+            cold[r] = in && hh < 0;
+            bin[r] = cold[r] ? bin_of(h, g) : 0u;
+            rank[r] = 0;
+            if (!__ballot(cold[r])) continue;
+            const unsigned long long peers = wave_peers(W, PM, bin[r], cold[r]);
+            if (cold[r]) {
+                const uint32_t base = CW[bin[r]];
+                rank[r] = base + (uint32_t)__popcll(peers & below);
+                if ((peers >> l) == 1ull) CW[bin[r]] = (uint16_t)(base + (uint32_t)__popcll(peers));
+            }
+        }
+        __syncthreads();
+        // per bin: exclusive prefix over the waves, the tile's count per bin
+        for (uint32_t b = tid; b < g.nbin; b += kTT) {
+            uint32_t s = 0;
+#pragma unroll
+            for (int w2 = 0; w2 < kTW; ++w2) {
+                const uint32_t x = S.cw[w2][b];
+                S.cw[w2][b] = (uint16_t)s;
+                s += x;
+            }
+            S.lstart[b] = s;
+        }
+        __syncthreads();
+        {  // exclusive scan of the counts over the bins (nbin <= 1024: one per thread)
+            const uint32_t c = (uint32_t)tid < g.nbin ? S.lstart[tid] : 0u;
+            const uint32_t ro = (uint32_t)tid < g.nbin ? rows[(uint64_t)tile * g.rowlen + tid] : 0u;
+            uint32_t x = c;
+#pragma unroll
+            for (int d = 1; d < kWave; d <<= 1) {
+                const uint32_t y = __shfl_up(x, d);
+                if (l >= d) x += y;
+            }
+            if (l == kWave - 1) S.wsum[w] = x;
+            __syncthreads();
+            uint32_t wb = 0;
+            for (int w2 = 0; w2 < w; ++w2) wb += S.wsum[w2];
+            if ((uint32_t)tid < g.nbin) {
+                S.lstart[tid] = wb + x - c;
+                S.roff[tid] = ro;
+            }
+            if (tid == kTT - 1) S.ncold = wb + x;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kTPer; ++r) {
+            if (!cold[r]) continue;
+            const uint32_t b = bin[r];
+            const uint32_t wr = S.cw[w][b] + rank[r];
+            const uint32_t ip = S.lstart[b] + wr;
+            S.img[ip] = make_int4((int)(uint32_t)k[r], (int)(uint32_t)((uint64_t)k[r] >> 32),
+                                  (int)(uint32_t)v[r], (int)(uint32_t)((uint64_t)v[r] >> 32));
+            S.iop[ip] = o[r];
+            S.ibin[ip] = (uint16_t)b;
+            pos1[j0 + r * kWave] = S.roff[b] + wr;
+        }
+        __syncthreads();
+        const uint32_t nc = S.ncold;
+        for (uint32_t i = tid; i < nc; i += kTT) {
+            const uint32_t b = S.ibin[i];
+            const uint32_t dst = S.roff[b] + (i - S.lstart[b]);
+            rec_kv[dst] = S.img[i];
+            rec_op[dst] = S.iop[i];
+        }
+        for (int i = tid; i < kTW * kMaxBins / 2; i += kTT) cw32[i] = 0u;  // next tile's counts
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kTPer; ++r) {
+            o[r] = no[r];
+            k[r] = nk[r];
+            v[r] = nv[r];
+        }
+    }
+}
+
+// ---- per-bin resolve ------------------------------------------------------------------------------
+struct ResolveLds {
+    int64_t tk[kMaxBPB * kSB];
+    int64_t tv[kMaxBPB * kSB];
+    uint8_t ts[kMaxBPB * kSB];
+    uint8_t W[kTW][kSB];
+    unsigned long long PM[kTW][kWave];
+    int4 skv[kTT];
+    uint8_t sop[kTT];
+    uint8_t sh[kTT];
+    uint16_t lst[kTT];
+    uint32_t cw[kTW][kMaxBPB];
+    uint32_t bcnt[kMaxBPB], bst[kMaxBPB];
+    int64_t rret[kTT];
+    uint8_t rconf[kTT];
+    uint32_t flags;
+    uint32_t nnew[kTW];
+};
+
+__device__ __forceinline__ int64_t kv_lo_hi(int lo, int hi) {
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// bucket b of the bin (wave b): its cnt records of this tile, in log order, 64 per round
+__device__ __forceinline__ void resolve_bucket(ResolveLds& S, int b, uint32_t cnt, uint32_t st0,
+                                              int mode, uint32_t* err) {
+    const int l = lane_id();
+    const unsigned long long below = (1ull << l) - 1ull;
+    int64_t* T = S.tk + b * kSB;
+    int64_t* V = S.tv + b * kSB;
+    uint8_t* TS = S.ts + b * kSB;
+    lds_u8* W = (lds_u8*)&S.W[b][0];
+    lds_u64* PM = (lds_u64*)&S.PM[b][0];
+    for (uint32_t r = 0; r < cnt; r += kWave) {
+        const bool live = r + l < cnt;
+        const uint32_t idx = live ? S.lst[st0 + r + l] : 0u;
+        const int4 kv = S.skv[idx];
+        const int64_t k = kv_lo_hi(kv.x, kv.y), v = kv_lo_hi(kv.z, kv.w);
+        const uint8_t o = S.sop[idx];
+        const bool isput = o == MPX_OP_PUT, isget = o == MPX_OP_GET;
+        // lookup in the bucket
+        int s = -1;
+        uint32_t p = S.sh[idx];
+        if (live) {
+            for (int probe = 0; probe < kSB; ++probe) {
+                const int64_t cur = T[p];
+                if (cur == k) {
+                    s = (int)p;
+                    break;
+                }
+                if (cur == kSentinel) break;
+                p = (p + 1) & (kSB - 1);
+            }
+        }
+        if (live && s < 0 && isput) {  // a key new to the table: claim a slot
+            if (mode == 0) atomicOr(&S.flags, kFNewPut);
+            for (int probe = 0; probe < kSB; ++probe) {
+                const unsigned long long cur =
+                    atomicCAS(reinterpret_cast<unsigned long long*>(&T[p]),
+                              (unsigned long long)kSentinel, (unsigned long long)k);
+                if (cur == (unsigned long long)kSentinel) {
+                    s = (int)p;
+                    TS[p] |= kSNew;
+                    break;
+                }
+                if ((int64_t)cur == k) {
+                    s = (int)p;
+                    break;
+                }
+                p = (p + 1) & (kSB - 1);
+            }
+            if (s < 0) raise_err(err, kErrKvFull);
+        }
+        if (live && s < 0 && !isput && mode == 0) atomicOr(&S.flags, kFAbsentOther);
+        const bool act = live && s >= 0;
+        int64_t ret = 0;
+        bool conf = false;
+        if (__ballot(act)) {
+            const uint32_t sl = act ? (uint32_t)s : 0u;
+            const unsigned long long peers = wave_peers(W, PM, sl, act);
+            const unsigned long long putm = __ballot(act && isput);
+            const unsigned long long lp = peers & below, lput = lp & putm;
+            const unsigned long long allput = peers & putm;
+            const uint8_t stt = act ? TS[sl] : 0;
+            const bool hasprev = lp ? true : (stt & kSTouched) != 0;
+            const bool prevput = lp ? ((putm >> hi_bit(lp)) & 1ull) != 0 : (stt & kSLastPut) != 0;
+            const int64_t vget = shfl64(v, lput ? hi_bit(lput) : l);
+            const int64_t vlast = shfl64(v, allput ? hi_bit(allput) : l);
+            const int64_t tab = act ? V[sl] : 0;
+            ret = !act ? 0 : isput ? v : (isget ? (lput ? vget : ((stt & kSPresent) ? tab : 0)) : 0);
+            conf = act && hasprev && (prevput || isput);
+            if (act && (peers >> l) == 1ull) {  // the round's last command on this slot
+                uint8_t ns = (uint8_t)((stt & (kSPresent | kSValDirty | kSNew | kSWasPresent)) |
+                                       kSTouched | (isput ? kSLastPut : 0));
+                if (allput) {
+                    V[sl] = vlast;
+                    ns |= kSPresent | kSValDirty;
+                }
+                TS[sl] = ns;
+            }
+        }
+        if (live) {
+            S.rret[idx] = ret;
+            S.rconf[idx] = conf ? 1 : 0;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
+                                                    const uint32_t* __restrict__ bin_start,
+                                                    const int4* __restrict__ rec_kv,
+                                                    const uint8_t* __restrict__ rec_op,
+                                                    int64_t* __restrict__ r_ret,
+                                                    uint8_t* __restrict__ r_conf, ApHot* hot,
+                                                    uint32_t* err) {
+    __shared__ ResolveLds S;
+    const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
+    const uint32_t bin = blockIdx.x;
+    const uint32_t bpb = 1u << g.lgbpb, nslot = bpb * kSB;
+    const uint64_t gbase = (uint64_t)bin * nslot;
+    const uint32_t ep = t.epoch[0];
+    const uint32_t r0 = bin_start[bin], r1 = bin_start[bin + 1];
+    const unsigned long long below = (1ull << l) - 1ull;
+    auto load_tables = [&]() {
+        for (uint32_t i = tid; i < nslot; i += kTT) {
+            S.tk[i] = t.keys[gbase + i];
+            S.tv[i] = t.vals[gbase + i];
+            const uint32_t x = t.state[gbase + i];
+            const uint8_t pres = (uint8_t)(x & kPresent);
+            S.ts[i] = (uint8_t)(pres | (pres ? kSWasPresent : 0) |
+                                ((x >> 2) == ep ? (kSTouched | (x & kLastPut)) : 0u));
+        }
+    };
+    load_tables();
+    S.PM[w][l] = 0ull;
+    if (tid == 0) S.flags = 0;
+    __syncthreads();
+    for (int mode = 0; mode < 2; ++mode) {
+        if (mode == 1) {
+            // two-pass form: insert every PUT key of the bin, then resolve again from the start
+            if ((S.flags & (kFAbsentOther | kFNewPut)) != (kFAbsentOther | kFNewPut)) break;
+            __syncthreads();
+            load_tables();
+            if (tid == 0) atomicAdd(&hot->restarts, 1u);
+            __syncthreads();
+            for (uint32_t q = r0 + tid; q < r1; q += kTT) {
+                if (rec_op[q] != MPX_OP_PUT) continue;
+                const int4 kv = rec_kv[q];
+                const int64_t k = kv_lo_hi(kv.x, kv.y);
+                const uint64_t h = hash64((uint64_t)k);
+                const uint32_t b = bucket_of(h, g.lgnb) & (bpb - 1);
+                int64_t* T = S.tk + b * kSB;
+                uint32_t p = home_of(h);
+                bool done = false;
+                for (int probe = 0; probe < kSB && !done; ++probe) {
+                    const unsigned long long cur =
+                        atomicCAS(reinterpret_cast<unsigned long long*>(&T[p]),
+                                  (unsigned long long)kSentinel, (unsigned long long)k);
+                    if (cur == (unsigned long long)kSentinel) {
+                        S.ts[b * kSB + p] |= kSNew;
+                        done = true;
+                    } else if ((int64_t)cur == k) {
+                        done = true;
+                    }
+                    p = (p + 1) & (kSB - 1);
+                }
+                if (!done) raise_err(err, kErrKvFull);
+            }
+            __syncthreads();
+        }
+        // the next 1024 records are loaded while this batch is resolved
+        int4 kv = r0 + tid < r1 ? rec_kv[r0 + tid] : make_int4(0, 0, 0, 0);
+        uint8_t o = r0 + tid < r1 ? rec_op[r0 + tid] : 0;
+        for (uint32_t base = r0; base < r1; base += kTT) {
+            const uint32_t q = base + tid;
+            const bool live = q < r1;
+            const uint32_t qn = q + kTT;
+            const int4 nkv = qn < r1 ? rec_kv[qn] : make_int4(0, 0, 0, 0);
+            const uint8_t no = qn < r1 ? rec_op[qn] : 0;
+            const uint64_t h = hash64((uint64_t)kv_lo_hi(kv.x, kv.y));
+            const uint32_t bl = bucket_of(h, g.lgnb) & (bpb - 1);
+            S.skv[tid] = kv;
+            S.sop[tid] = o;
+            S.sh[tid] = (uint8_t)home_of(h);
+            uint32_t rk = 0;
+            for (uint32_t b = 0; b < bpb; ++b) {
+                const unsigned long long m = __ballot(live && bl == b);
+                if (live && bl == b) rk = (uint32_t)__popcll(m & below);
+                if (l == 0) S.cw[w][b] = (uint32_t)__popcll(m);
+            }
+            __syncthreads();
+            if ((uint32_t)tid < bpb) {
+                uint32_t s = 0;
+                for (int w2 = 0; w2 < kTW; ++w2) {
+                    const uint32_t x = S.cw[w2][tid];
+                    S.cw[w2][tid] = s;
+                    s += x;
+                }
+                S.bcnt[tid] = s;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                uint32_t s = 0;
+                for (uint32_t b = 0; b < bpb; ++b) {
+                    S.bst[b] = s;
+                    s += S.bcnt[b];
+                }
+            }
+            __syncthreads();
+            if (live) S.lst[S.bst[bl] + S.cw[w][bl] + rk] = (uint16_t)tid;
+            __syncthreads();
+            if ((uint32_t)w < bpb) resolve_bucket(S, w, S.bcnt[w], S.bst[w], mode, err);
+            __syncthreads();
+            if (live) {
+                r_ret[q] = S.rret[tid];
+                r_conf[q] = S.rconf[tid];
+            }
+            kv = nkv;
+            o = no;
+        }
+        __syncthreads();
+    }
+    // write back the touched slots; count the keys that became present
+    uint32_t added = 0;
+    for (uint32_t i = tid; i < nslot; i += kTT) {
+        const uint8_t s = S.ts[i];
+        if (s & kSNew) t.keys[gbase + i] = S.tk[i];
+        if (s & kSValDirty) t.vals[gbase + i] = S.tv[i];
+        if (s & kSTouched) t.state[gbase + i] = (ep << 2) | (s & (kPresent | kLastPut));
+        added += ((s & kSPresent) && !(s & kSWasPresent)) ? 1u : 0u;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) added += __shfl_xor(added, d);
+    if (l == 0 && added) atomicAdd(t.n_present, (unsigned long long)added);
+}
+
+// ---- hot keys: final state ----------------------------------------------------------------------
+__global__ void k_ap_hot_commit(KvTable t, const int64_t* __restrict__ val, const ApHot* hot,
+                                uint32_t* err) {
+    const uint32_t h = threadIdx.x;
+    if (h >= hot->n) return;
+    const uint32_t a = hot->fin_any[h], p = hot->fin_put[h];
+    if (!a) return;
+    uint32_t slot = hot->slot[h];
+    const uint32_t fl = hot->flags[h];
+    if (slot == kNoSlot) {
+        if (!p) return;  // GET / other ops of an absent key: nothing to record
+        const int64_t s = kv_insert(t, hot->key[h], err);
+        if (s < 0) return;
+        slot = (uint32_t)s;
+    }
+    const uint32_t ep = t.epoch[0];
+    if (p) t.vals[slot] = val[p - 1];
+    t.state[slot] = (ep << 2) | (a == p ? kLastPut : 0u) | ((fl & kPresent) || p ? kPresent : 0u);
+    if (!(fl & kPresent) && p) atomicAdd(t.n_present, 1ull);
+}
+
+// ---- log-order results --------------------------------------------------------------------------
+struct EmitLds {
+    uint2 T[kTW][kHMax];   // per wave and hot key: 1 + position of the last command / last PUT
+    uint2 TP[kTW][kHMax];  // the same over the earlier waves of the tile
+    uint2 inc[kHMax];      // over the earlier tiles
+    int64_t hval[kHMax];
+    uint32_t hfl[kHMax];
+};
+
+__global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restrict__ op,
+                                                 const int64_t* __restrict__ val, uint32_t n,
+                                                 const uint32_t* __restrict__ pos1,
+                                                 const int64_t* __restrict__ r_ret,
+                                                 const uint8_t* __restrict__ r_conf,
+                                                 const uint32_t* __restrict__ rows,
+                                                 const ApHot* __restrict__ hot,
+                                                 int64_t* __restrict__ ret,
+                                                 uint8_t* __restrict__ conf) {
+    __shared__ EmitLds S;
+    const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
+    reinterpret_cast<uint2*>(&S.T[0][0])[tid] = make_uint2(0u, 0u);  // kTW * kHMax == kTT
+    const uint32_t tile = xcd_tile(g.tiles);
+    if (tid < kHMax) {
+        const uint32_t* row = rows + (uint64_t)tile * g.rowlen + g.nbin;
+        S.inc[tid] = make_uint2(row[2 * tid], row[2 * tid + 1]);
+        S.hval[tid] = hot->val0[tid];
+        S.hfl[tid] = hot->flags[tid];
+    }
+    __syncthreads();
+    const uint32_t jw = tile * (uint32_t)kTL + (uint32_t)w * (kWave * kTPer);
+    uint32_t p[kTPer];
+#pragma unroll
+    for (int r = 0; r < kTPer; ++r) {
+        const uint32_t j = jw + r * kWave + l;
+        p[r] = j < n ? pos1[j] : 0u;
+    }
+    int64_t rv[kTPer];
+    uint8_t cf[kTPer], o[kTPer];
+#pragma unroll
+    for (int r = 0; r < kTPer; ++r) {
+        const uint32_t j = jw + r * kWave + l;
+        const bool in = j < n;
+        const bool hotc = in && (p[r] & kHotBit);
+        rv[r] = 0;
+        cf[r] = 0;
+        o[r] = 0;
+        if (in && !hotc) {
+            rv[r] = r_ret[p[r]];
+            cf[r] = r_conf[p[r]];
+        }
+        if (hotc) {
+            o[r] = op[j];
+            rv[r] = val[j];
+        }
+    }
+    const unsigned long long below = (1ull << l) - 1ull;
+    uint32_t pa[kTPer], pp[kTPer];
+#pragma unroll
+    for (int r = 0; r < kTPer; ++r) {
+        const uint32_t j = jw + r * kWave + l;
+        const bool hotc = j < n && (p[r] & kHotBit);
+        pa[r] = 0;
+        pp[r] = 0;
+        if (!__ballot(hotc)) continue;
+        const uint32_t h = hotc ? (p[r] & ~kHotBit) : 0u;
+        const unsigned long long peers = wave_match(h, hotc);
+        const unsigned long long putm = __ballot(hotc && o[r] == MPX_OP_PUT);
+        if (hotc) {
+            const uint2 tr = S.T[w][h];
+            const unsigned long long lp = peers & below, lput = lp & putm;
+            const uint32_t jb = jw + r * kWave + 1;  // 1 + position of lane 0
+            pa[r] = lp ? jb + (uint32_t)hi_bit(lp) : tr.x;
+            pp[r] = lput ? jb + (uint32_t)hi_bit(lput) : tr.y;
+            if ((peers >> l) == 1ull) {
+                const unsigned long long allput = peers & putm;
+                S.T[w][h] = make_uint2(jb + (uint32_t)l, allput ? jb + (uint32_t)hi_bit(allput) : tr.y);
+            }
+        }
+    }
+    __syncthreads();
+    {
+        const int ww = tid / kHMax, hh = tid % kHMax;
+        uint2 m = make_uint2(0u, 0u);
+        for (int w2 = 0; w2 < ww; ++w2) {
+            const uint2 x = S.T[w2][hh];
+            m.x = m.x > x.x ? m.x : x.x;
+            m.y = m.y > x.y ? m.y : x.y;
+        }
+        S.TP[ww][hh] = m;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kTPer; ++r) {
+        const uint32_t j = jw + r * kWave + l;
+        if (j >= n) continue;
+        if (p[r] & kHotBit) {
+            const uint32_t h = p[r] & ~kHotBit;
+            const uint2 tp = S.TP[w][h], ic = S.inc[h];
+            uint32_t a = pa[r] > tp.x ? pa[r] : tp.x;
+            a = a > ic.x ? a : ic.x;
+            uint32_t q = pp[r] > tp.y ? pp[r] : tp.y;
+            q = q > ic.y ? q : ic.y;
+            const uint32_t fl = S.hfl[h];
+            const bool hasprev = a != 0 || (fl & 4u);
+            const bool prevput = a ? a == q : (fl & kLastPut) != 0;
+            const bool isput = o[r] == MPX_OP_PUT, isget = o[r] == MPX_OP_GET;
+            const int64_t x = isput ? rv[r]
+                                    : (isget ? (q ? val[q - 1] : ((fl & kPresent) ? S.hval[h] : 0))
+                                             : 0);
+            rv[r] = x;
+            cf[r] = hasprev && (prevput || isput) ? 1 : 0;
+        }
+        st_stream(ret + j, rv[r]);
+        if (conf) st_stream(conf + j, cf[r]);
+    }
+}
+
+// ---- launcher ---------------------------------------------------------------------------------
+namespace {
+struct FastLayout {
+    uint64_t rows, part, bin_start, rec_kv, rec_op, pos1, r_ret, r_conf, hot, total;
+};
+
+ApGeo geo_for(const KvTable& t, uint64_t n) {
+    ApGeo g{};
+    g.lgnb = t.lgnb;
+    g.lgbpb = t.lgnb < 4 ? t.lgnb : 4;
+    g.nbin = 1u << (t.lgnb - g.lgbpb);
+    g.rowlen = g.nbin + 2 * kHMax;
+    g.tiles = (uint32_t)((n + kTL - 1) / kTL);
+    if (!g.tiles) g.tiles = 1;
+    g.ng = g.tiles < 128 ? g.tiles : 128;
+    g.tpg = (g.tiles + g.ng - 1) / g.ng;
+    g.ng = (g.tiles + g.tpg - 1) / g.tpg;
+    return g;
+}
+
+FastLayout fast_layout(const KvTable& t, uint64_t c) {
+    const ApGeo g = geo_for(t, c);
+    auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+    FastLayout L{};
+    uint64_t o = 0;
+    L.rows = o; o += al((uint64_t)g.tiles * g.rowlen * 4);
+    L.part = o; o += al((uint64_t)128 * g.rowlen * 4);
+    L.bin_start = o; o += al(((uint64_t)g.nbin + 1) * 4);
+    L.rec_kv = o; o += al(c * 16);
+    L.rec_op = o; o += al(c);
+    L.pos1 = o; o += al(c * 4);
+    L.r_ret = o; o += al(c * 8);
+    L.r_conf = o; o += al(c);
+    L.hot = o; o += al(sizeof(ApHot));
+    L.total = o;
+    return L;
+}
+}  // namespace
+
+bool apply_fast_ok(const KvTable& t) {
+    const uint32_t lgbpb = t.lgnb < 4 ? t.lgnb : 4;
+    return (1u << (t.lgnb - lgbpb)) <= (uint32_t)kMaxBins;
+}
+
+uint64_t apply_fast_work_bytes(const KvTable& t, uint64_t c) { return fast_layout(t, c).total; }
+
+__global__ void k_epoch_bump2(uint32_t* epoch) {
+    uint32_t e = epoch[0] + 1;
+    epoch[1] = 0;
+    if (e >= kEpochMax) {
+        e = 1;
+        epoch[1] = 1;
+    }
+    epoch[0] = e;
+}
+
+__global__ void k_epoch_wrap2(KvTable t) {
+    if (!t.epoch[1]) return;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= t.cap; s += stride)
+        t.state[s] &= kPresent;
+}
+
+__global__ __launch_bounds__(256) void k_ap_preinsert(KvTable t, const uint8_t* __restrict__ op,
+                                                      const int64_t* __restrict__ key, uint64_t m,
+                                                      uint32_t* err) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride)
+        if (op[i] == MPX_OP_PUT && key[i] != kSentinel) kv_insert(t, key[i], err);
+}
+
+hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
+                             uint64_t m, int64_t* ret, uint8_t* conf, uint64_t C, ApplyWork& w,
+                             uint32_t hot_min, uint32_t* err, hipStream_t stream) {
+    if (C >= (1ull << 31)) return hipErrorInvalidValue;
+    const FastLayout L = fast_layout(t, C);
+    if (w.bytes < L.total) return hipErrorInvalidValue;
+    char* b = (char*)w.base;
+    uint32_t* rows = (uint32_t*)(b + L.rows);
+    uint32_t* part = (uint32_t*)(b + L.part);
+    uint32_t* bin_start = (uint32_t*)(b + L.bin_start);
+    int4* rec_kv = (int4*)(b + L.rec_kv);
+    uint8_t* rec_op = (uint8_t*)(b + L.rec_op);
+    uint32_t* pos1 = (uint32_t*)(b + L.pos1);
+    int64_t* r_ret = (int64_t*)(b + L.r_ret);
+    uint8_t* r_conf = (uint8_t*)(b + L.r_conf);
+    ApHot* hot = (ApHot*)(b + L.hot);
+
+    k_epoch_bump2<<<1, 1, 0, stream>>>(t.epoch);
+    k_epoch_wrap2<<<1024, 256, 0, stream>>>(t);
+    if (C < m) {
+        const uint64_t blocks = (m + 255) / 256;
+        k_ap_preinsert<<<(unsigned)(blocks > 8192 ? 8192 : blocks), 256, 0, stream>>>(t, op, key,
+                                                                                     m, err);
+    }
+    // scratch for the r_conf writes when the caller wants no conf: still written (cheap)
+    for (uint64_t c0 = 0; c0 < m; c0 += C) {
+        const uint32_t n = (uint32_t)(m - c0 < C ? m - c0 : C);
+        const ApGeo g = geo_for(t, n);
+        k_ap_select<<<1, kTT, 0, stream>>>(t, key + c0, n, hot_min, hot);
+        k_ap_count<<<g.tiles, kTT, 0, stream>>>(g, op + c0, key + c0, n, rows, hot);
+        k_ap_scan_part<<<g.ng, 256, 0, stream>>>(g, rows, part, hot);
+        k_ap_scan_top<<<1, kTT, 0, stream>>>(g, part, bin_start, hot);
+        k_ap_scan_rows<<<g.ng, 256, 0, stream>>>(g, rows, part, hot);
+        k_ap_scatter<<<kScatterGrid, kTT, 0, stream>>>(g, op + c0, key + c0, val + c0, n, rows, hot,
+                                                  rec_kv, rec_op, pos1);
+        k_ap_resolve<<<g.nbin, kTT, 0, stream>>>(g, t, bin_start, rec_kv, rec_op, r_ret, r_conf,
+                                                 hot, err);
+        k_ap_hot_commit<<<1, kHMax, 0, stream>>>(t, val + c0, hot, err);
+        k_ap_emit<<<g.tiles, kTT, 0, stream>>>(g, op + c0, val + c0, n, pos1, r_ret, r_conf, rows,
+                                               hot, ret + c0, conf ? conf + c0 : nullptr);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace mpx

@@ -151,6 +151,8 @@ int ensure_kv(mpx_engine* e) {
     while (cap < 2 * want) cap <<= 1;
     mpx::KvTable t{};
     t.cap = cap;
+    t.lgnb = 0;
+    while ((1ull << (t.lgnb + 8)) < cap) ++t.lgnb;
     // cap hash slots + one side slot for the key INT64_MIN (the empty-slot sentinel)
     if (hipMalloc(&t.keys, (cap + 1) * 8) != hipSuccess ||
         hipMalloc(&t.vals, (cap + 1) * 8) != hipSuccess ||
@@ -443,7 +445,7 @@ int mpx_apply(mpx_engine* e, const uint8_t* op, const int64_t* key, const int64_
     GROW(e, e->b[9], m * 8);
     GROW(e, e->b[10], m * 8);
     GROW(e, e->b[11], m);
-    GROW(e, e->apply_work, mpx::apply_work_bytes(e->apply_chunk, m));
+    GROW(e, e->apply_work, mpx::apply_work_bytes(e->kv, e->apply_chunk, m));
     CK(h2d(e, e->b[7].p, op, m));
     CK(h2d(e, e->b[8].p, key, m * 8));
     CK(h2d(e, e->b[9].p, val, m * 8));
@@ -462,7 +464,7 @@ int mpx_apply_reserve(mpx_engine* e, size_t max_cmds) {
     if (max_cmds >= (1ull << 31)) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 commands");
     CK(begin(e));
     CK(ensure_kv(e));
-    GROW(e, e->apply_work, mpx::apply_work_bytes(e->apply_chunk, max_cmds));
+    GROW(e, e->apply_work, mpx::apply_work_bytes(e->kv, e->apply_chunk, max_cmds));
     return finish(e);
 }
 
@@ -471,7 +473,7 @@ int mpx_apply_dev(mpx_engine* e, const uint8_t* d_op, const int64_t* d_key, cons
     if (!e) return MPX_E_INVAL;
     if (m && (!d_op || !d_key || !d_val || !d_ret)) return fail(e, MPX_E_INVAL, "null argument");
     if (m >= (1ull << 31)) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 commands per call");
-    if (!e->kv_ready || e->apply_work.cap < mpx::apply_work_bytes(e->apply_chunk, m))
+    if (!e->kv_ready || e->apply_work.cap < mpx::apply_work_bytes(e->kv, e->apply_chunk, m))
         return fail(e, MPX_E_INVAL,
                     "mpx_apply_dev: call mpx_apply_reserve(m) first (the dev entry point never "
                     "allocates)");

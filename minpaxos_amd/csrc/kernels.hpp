@@ -64,7 +64,8 @@ struct KvTable {
     int64_t* keys;       // [cap]
     int64_t* vals;       // [cap]
     uint32_t* state;     // [cap] bit 0 present, bit 1 last command of epoch (>> 2) was a PUT
-    uint64_t cap;        // power of two
+    uint64_t cap;        // power of two, >= 1024
+    uint32_t lgnb;       // log2(cap / 256): buckets of 256 slots (kvtab.hpp)
     unsigned long long* n_present;  // device counter
     uint32_t* epoch;     // device: [0] call epoch of mpx_apply, [1] wrap flag
 };
@@ -73,11 +74,18 @@ struct ApplyWork {      // scratch sized for m commands (see apply_work_bytes)
     void* base;
     uint64_t bytes;
 };
-// commands per apply chunk (0 = default): bounds the pipeline's scratch (48 B per command);
+// commands per apply chunk (0 = default): bounds the pipeline's scratch (30 B per command on the
+// partitioned path, 48 B on the sort-based one);
 // env MPX_APPLY_CHUNK overrides it per engine (tests use tiny chunks to cross boundaries)
 constexpr uint64_t kApplyChunkDefault = 1ull << 26;
 uint64_t apply_chunk_commands(uint64_t chunk, uint64_t m);
-uint64_t apply_work_bytes(uint64_t chunk, uint64_t m);
+uint64_t apply_work_bytes(const KvTable& t, uint64_t chunk, uint64_t m);
+// the partitioned pipeline (apply_fast.hip): tables of at most 1024 bins of 16 buckets
+bool apply_fast_ok(const KvTable& t);
+uint64_t apply_fast_work_bytes(const KvTable& t, uint64_t c);
+hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
+                             uint64_t m, int64_t* ret, uint8_t* conf, uint64_t C, ApplyWork& w,
+                             uint32_t hot_min, uint32_t* err, hipStream_t stream);
 hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
                         uint64_t m, int64_t* ret, uint8_t* conf, uint64_t chunk, ApplyWork& w,
                         uint32_t* err, hipStream_t stream);

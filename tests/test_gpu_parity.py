@@ -214,6 +214,52 @@ def test_apply_chunked(mk_engine, monkeypatch, chunk):
         assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
 
 
+@pytest.mark.parametrize("fallback", ["0", "1"])
+@pytest.mark.parametrize("hot_min", ["0", "2", "8"])
+def test_apply_paths(mk_engine, monkeypatch, hot_min, fallback):
+    """the partitioned pipeline with no hot keys (every key through the bins), with as many hot
+    keys as fit (MPX_APPLY_HOT_MIN=2), with the sampled default, and the sort-based fallback:
+    every call bit-exact, table state carried across calls. Fresh key ranges per call put GETs
+    of absent keys before their first PUT in the same bin (the two-pass bins); the small table
+    (32 buckets of 256 slots) is driven to ~70% occupancy"""
+    monkeypatch.setenv("MPX_APPLY_HOT_MIN", hot_min)
+    monkeypatch.setenv("MPX_APPLY_FALLBACK", fallback)
+    rng = np.random.default_rng(31 + int(hot_min) + 10 * int(fallback))
+    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=4096), Oracle(5, R.MODE_MIN)
+    calls = []
+    for t in range(3):
+        op, key, val = gen_cases.commands_mixed(rng, 30000, 1500)
+        calls.append((op, np.where(key > 0, key + t * 1_000_003, key), val))
+    calls.append(synth.commands(50000, 300, 0.5, "zipf", seed=5))
+    calls.append(synth.commands(9000, 1 << 40, 0.2, "uniform", seed=6))  # mostly absent GETs
+    calls.append(synth.commands(70000, 1200, 0.6, "uniform", seed=7))
+    calls.append((np.full(5000, R.OP_GET, np.uint8), np.full(5000, 9, np.int64),
+                  np.arange(5000, dtype=np.int64)))  # one hot key, GETs only
+    for op, key, val in calls:
+        gr, gc = e.apply(op, key, val)
+        wr, wc = o.apply(op, key, val)
+        assert np.array_equal(gr, wr) and np.array_equal(gc, wc)
+        gk, gv = e.kv_export()
+        wk, wv = o.kv_export()
+        assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
+        assert e.kv_size() == len(wk)
+
+
+def test_apply_large_table_fallback(mk_engine):
+    """a table past the partitioned pipeline's 1024 bins (kv_capacity 4M keys: 8M slots) takes
+    the sort-based pipeline; same results"""
+    rng = np.random.default_rng(41)
+    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 22), Oracle(5, R.MODE_MIN)
+    for t in range(2):
+        op, key, val = gen_cases.commands_mixed(rng, 60000, 20000)
+        gr, gc = e.apply(op, key, val)
+        wr, wc = o.apply(op, key, val)
+        assert np.array_equal(gr, wr) and np.array_equal(gc, wc)
+    gk, gv = e.kv_export()
+    wk, wv = o.kv_export()
+    assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
+
+
 def test_conflict_batch(mk_engine):
     rng = np.random.default_rng(9)
     e, o = mk_engine(5, R.MODE_MIN), Oracle(5, R.MODE_MIN)
