@@ -41,6 +41,16 @@
 
 namespace mpx {
 
+// diagnostic ablations of k_ap_resolve (variant builds only): 1 no bucket resolve, 2 no result
+// stores, 4 no batch ranking
+#ifndef MPX_RS_ABL
+#define MPX_RS_ABL 0
+#endif
+// diagnostic build: per-phase clock64() totals of k_ap_resolve printed by bin 0 (-DMPX_RS_STAMP=1)
+#ifndef MPX_RS_STAMP
+#define MPX_RS_STAMP 0
+#endif
+
 constexpr int kTL = 4096;          // commands per log tile
 constexpr int kTT = 1024;          // threads of the tile and bin workgroups
 constexpr int kTW = kTT / kWave;   // 16 waves
@@ -118,6 +128,18 @@ __device__ __forceinline__ unsigned long long wave_match(uint32_t c, bool act) {
     return mine;
 }
 
+// the same from one ballot per bit of the class id (c < 2^nbits): for few classes, or where the
+// LDS round trips above are the critical path
+__device__ __forceinline__ unsigned long long match_bits(uint32_t c, int nbits, bool act) {
+    unsigned long long m = __ballot(act);
+    for (int i = 0; i < nbits; ++i) {
+        const bool bit = (c >> i) & 1u;
+        const unsigned long long b = __ballot(bit);
+        m &= bit ? b : ~b;
+    }
+    return act ? m : 0ull;
+}
+
 __device__ __forceinline__ int64_t shfl64(int64_t v, int src) {
     return (int64_t)__shfl((long long)v, src);
 }
@@ -187,7 +209,9 @@ __global__ __launch_bounds__(kTT) void k_ap_select(KvTable t, const int64_t* __r
     __shared__ int64_t sk[kSampTab];
     __shared__ uint32_t sc[kSampTab];
     __shared__ int64_t hk[kHMax];
-    __shared__ uint32_t nh, nge, thr;
+    __shared__ uint32_t sc_hist[kTT];
+    __shared__ uint32_t wsum_s[kTW];
+    __shared__ uint32_t nh, thr_s, thr;
     const int tid = threadIdx.x;
     for (int i = tid; i < kSampTab; i += kTT) {
         sk[i] = kSentinel;
@@ -211,7 +235,7 @@ __global__ __launch_bounds__(kTT) void k_ap_select(KvTable t, const int64_t* __r
                 if (k[u] == kSentinel) continue;
                 // frequent keys arrive early; once the probe window is full a sample is dropped
                 uint32_t p = (uint32_t)hash64((uint64_t)k[u]) & (kSampTab - 1);
-                for (int probe = 0; probe < 16; ++probe, p = (p + 1) & (kSampTab - 1)) {
+                for (int probe = 0; probe < 4; ++probe, p = (p + 1) & (kSampTab - 1)) {
                     int64_t cur = sk[p];
                     if (cur == kSentinel)
                         cur = (int64_t)atomicCAS(reinterpret_cast<unsigned long long*>(&sk[p]),
@@ -225,22 +249,34 @@ __global__ __launch_bounds__(kTT) void k_ap_select(KvTable t, const int64_t* __r
             }
         }
         __syncthreads();
-        // the smallest threshold >= hot_min that leaves at most kHMax - 1 keys (binary search)
-        uint32_t lo = hot_min, hi = S + 1;  // count(>= hi) == 0 <= kHMax - 1
-        while (lo < hi) {
-            const uint32_t mid = lo + (hi - lo) / 2;
-            if (tid == 0) nge = 0;
-            __syncthreads();
-            uint32_t c = 0;
-            for (int i = tid; i < kSampTab; i += kTT) c += sc[i] >= mid ? 1u : 0u;
+        // the smallest threshold >= hot_min that leaves at most kHMax - 1 keys: a histogram of
+        // the counts (capped at kTT - 1; more than kHMax - 1 keys cannot reach that), then a
+        // suffix sum over it
+        sc_hist[tid] = 0;
+        if (tid == 0) thr_s = kTT;
+        __syncthreads();
+        for (int i = tid; i < kSampTab; i += kTT)
+            if (sc[i]) atomicAdd(&sc_hist[sc[i] < (uint32_t)kTT ? sc[i] : kTT - 1], 1u);
+        __syncthreads();
+        {
+            // inclusive suffix sum: reverse the index, scan forward
+            const int ri = kTT - 1 - tid;
+            uint32_t x = sc_hist[ri];
+            const int l = lane_id();
 #pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
-            if (lane_id() == 0 && c) atomicAdd(&nge, c);
+            for (int d = 1; d < kWave; d <<= 1) {
+                const uint32_t y = __shfl_up(x, d);
+                if (l >= d) x += y;
+            }
+            if (l == kWave - 1) wsum_s[tid / kWave] = x;
             __syncthreads();
-            if (nge <= (uint32_t)kHMax - 1) hi = mid;
-            else lo = mid + 1;
-            __syncthreads();
+            uint32_t wb = 0;
+            for (int w2 = 0; w2 < tid / kWave; ++w2) wb += wsum_s[w2];
+            const uint32_t ge = wb + x;  // keys with count >= ri
+            if ((uint32_t)ri >= hot_min && ge <= (uint32_t)kHMax - 1) atomicMin(&thr_s, (uint32_t)ri);
         }
+        __syncthreads();
+        const uint32_t lo = thr_s;
         if (tid == 0) thr = lo;
         __syncthreads();
         for (int i = tid; i < kSampTab; i += kTT)
@@ -287,10 +323,12 @@ __global__ __launch_bounds__(kTT) void k_ap_count(ApGeo g, const uint8_t* __rest
     const uint32_t tile = xcd_tile(g.tiles);
     const uint32_t j0 = tile * (uint32_t)kTL;
     int64_t k[kTPer];
+    uint8_t o[kTPer];
 #pragma unroll
     for (int u = 0; u < kTPer; ++u) {
         const uint32_t j = j0 + u * kTT + tid;
         k[u] = j < n ? key[j] : 0;
+        o[u] = j < n ? op[j] : 0;
     }
     const int l = lane_id();
 #pragma unroll
@@ -303,7 +341,7 @@ __global__ __launch_bounds__(kTT) void k_ap_count(ApGeo g, const uint8_t* __rest
         const bool hotc = in && hh >= 0;
         if (!__ballot(hotc)) continue;
         // per hot key of the round: its last command and its last PUT, one LDS atomic each
-        const bool put = hotc && op[j] == MPX_OP_PUT;
+        const bool put = hotc && o[u] == MPX_OP_PUT;
         const unsigned long long peers = wave_match((uint32_t)hh, hotc);
         const unsigned long long puts = peers & __ballot(put);
         if (hotc && hi_bit(peers) == l) atomicMax(&ha[hh], j + 1);
@@ -459,9 +497,9 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
     TileWalk tw = tile_walk(g.tiles);
     const uint32_t wofs = (uint32_t)w * (kWave * kTPer) + (uint32_t)l;
     // this tile's commands in registers; the next tile's are loaded while this one is ranked
-    uint8_t o[kTPer];
+    uint32_t o[kTPer];  // 32-bit: byte-packed ops make the compiler wait for the prefetch early
     int64_t k[kTPer], v[kTPer];
-    auto load = [&](uint32_t tile, uint8_t* o_, int64_t* k_, int64_t* v_) {
+    auto load = [&](uint32_t tile, uint32_t* o_, int64_t* k_, int64_t* v_) {
 #pragma unroll
         for (int r = 0; r < kTPer; ++r) {
             const uint32_t j = tile * (uint32_t)kTL + wofs + r * kWave;
@@ -472,6 +510,10 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
         }
     };
     load(tw.tile, o, k, v);
+    auto load_roff = [&](uint32_t tile) {
+        return tile < tw.end && (uint32_t)tid < g.nbin ? rows[(uint64_t)tile * g.rowlen + tid] : 0u;
+    };
+    uint32_t roff_cur = load_roff(tw.tile);
     lds_u8* W = (lds_u8*)&S.W[w][0];
     lds_u64* PM = (lds_u64*)&S.PM[w][0];
     lds_u16* CW = (lds_u16*)&S.cw[w][0];
@@ -479,9 +521,10 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
     for (; tw.tile < tw.end; tw.tile += tw.step) {
         const uint32_t tile = tw.tile;
         const uint32_t j0 = tile * (uint32_t)kTL + wofs;
-        uint8_t no[kTPer];
+        uint32_t no[kTPer];
         int64_t nk[kTPer], nv[kTPer];
         load(tile + tw.step, no, nk, nv);
+        const uint32_t roff_nxt = load_roff(tile + tw.step);
         uint32_t bin[kTPer], rank[kTPer];
         bool cold[kTPer];
 #pragma unroll
@@ -505,19 +548,21 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
         __syncthreads();
         // per bin: exclusive prefix over the waves, the tile's count per bin
         for (uint32_t b = tid; b < g.nbin; b += kTT) {
+            uint32_t x[kTW];  // all loads first: the stores below may alias them
+#pragma unroll
+            for (int w2 = 0; w2 < kTW; ++w2) x[w2] = S.cw[w2][b];
             uint32_t s = 0;
 #pragma unroll
             for (int w2 = 0; w2 < kTW; ++w2) {
-                const uint32_t x = S.cw[w2][b];
                 S.cw[w2][b] = (uint16_t)s;
-                s += x;
+                s += x[w2];
             }
             S.lstart[b] = s;
         }
         __syncthreads();
         {  // exclusive scan of the counts over the bins (nbin <= 1024: one per thread)
             const uint32_t c = (uint32_t)tid < g.nbin ? S.lstart[tid] : 0u;
-            const uint32_t ro = (uint32_t)tid < g.nbin ? rows[(uint64_t)tile * g.rowlen + tid] : 0u;
+            const uint32_t ro = roff_cur;
             uint32_t x = c;
 #pragma unroll
             for (int d = 1; d < kWave; d <<= 1) {
@@ -543,7 +588,7 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
             const uint32_t ip = S.lstart[b] + wr;
             S.img[ip] = make_int4((int)(uint32_t)k[r], (int)(uint32_t)((uint64_t)k[r] >> 32),
                                   (int)(uint32_t)v[r], (int)(uint32_t)((uint64_t)v[r] >> 32));
-            S.iop[ip] = o[r];
+            S.iop[ip] = (uint8_t)o[r];
             S.ibin[ip] = (uint16_t)b;
             pos1[j0 + r * kWave] = S.roff[b] + wr;
         }
@@ -563,26 +608,28 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
             k[r] = nk[r];
             v[r] = nv[r];
         }
+        roff_cur = roff_nxt;
     }
 }
 
 // ---- per-bin resolve ------------------------------------------------------------------------------
+constexpr int kRH = 2;             // records per thread per resolve batch
+constexpr int kRT = kTT * kRH;     // 2048 records per batch
 struct ResolveLds {
     int64_t tk[kMaxBPB * kSB];
     int64_t tv[kMaxBPB * kSB];
     uint8_t ts[kMaxBPB * kSB];
     uint8_t W[kTW][kSB];
     unsigned long long PM[kTW][kWave];
-    int4 skv[kTT];
-    uint8_t sop[kTT];
-    uint8_t sh[kTT];
-    uint16_t lst[kTT];
-    uint32_t cw[kTW][kMaxBPB];
+    int4 skv[kRT];                    // the batch's records in bucket order (log order inside)
+    uint8_t sop[kRT];
+    uint16_t sidx[kRT];               // their index in the batch
+    uint32_t cw[kRH * kTW][kMaxBPB];  // per (half, wave): records per bucket -> exclusive prefix
     uint32_t bcnt[kMaxBPB], bst[kMaxBPB];
-    int64_t rret[kTT];
-    uint8_t rconf[kTT];
     uint32_t flags;
-    uint32_t nnew[kTW];
+#if MPX_RS_STAMP
+    unsigned long long ph[8], rb[kTW];
+#endif
 };
 
 __device__ __forceinline__ int64_t kv_lo_hi(int lo, int hi) {
@@ -590,8 +637,11 @@ __device__ __forceinline__ int64_t kv_lo_hi(int lo, int hi) {
 }
 
 // bucket b of the bin (wave b): its cnt records of this tile, in log order, 64 per round
+// (results go straight to the batch's partition positions: a batch covers 2048 consecutive ones,
+// so the scattered 8-byte stores of its waves meet in L2)
 __device__ __forceinline__ void resolve_bucket(ResolveLds& S, int b, uint32_t cnt, uint32_t st0,
-                                              int mode, uint32_t* err) {
+                                              int mode, uint32_t base, int64_t* __restrict__ r_ret,
+                                              uint8_t* __restrict__ r_conf, uint32_t* err) {
     const int l = lane_id();
     const unsigned long long below = (1ull << l) - 1ull;
     int64_t* T = S.tk + b * kSB;
@@ -601,23 +651,36 @@ __device__ __forceinline__ void resolve_bucket(ResolveLds& S, int b, uint32_t cn
     lds_u64* PM = (lds_u64*)&S.PM[b][0];
     for (uint32_t r = 0; r < cnt; r += kWave) {
         const bool live = r + l < cnt;
-        const uint32_t idx = live ? S.lst[st0 + r + l] : 0u;
-        const int4 kv = S.skv[idx];
+        const uint32_t x = live ? st0 + r + l : 0u;
+        const int4 kv = S.skv[x];
+        const uint32_t idx = S.sidx[x];
         const int64_t k = kv_lo_hi(kv.x, kv.y), v = kv_lo_hi(kv.z, kv.w);
-        const uint8_t o = S.sop[idx];
+        const uint8_t o = S.sop[x];
         const bool isput = o == MPX_OP_PUT, isget = o == MPX_OP_GET;
-        // lookup in the bucket
+        // lookup in the bucket, 4 slots per step: the worst probe length among the wave's 64 lanes
+        // sets the number of dependent LDS reads
         int s = -1;
-        uint32_t p = S.sh[idx];
+        uint32_t p = home_of(hash64((uint64_t)k));
         if (live) {
-            for (int probe = 0; probe < kSB; ++probe) {
-                const int64_t cur = T[p];
-                if (cur == k) {
-                    s = (int)p;
+            for (int step = 0; step < kSB / 4; ++step) {
+                int64_t c[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) c[u] = T[(p + u) & (kSB - 1)];
+                int hit = -1, stop = -1;
+#pragma unroll
+                for (int u = 3; u >= 0; --u) {
+                    if (c[u] == k) hit = u;
+                    if (c[u] == kSentinel) stop = u;
+                }
+                if (hit >= 0 && (stop < 0 || hit < stop)) {
+                    s = (int)((p + hit) & (kSB - 1));
                     break;
                 }
-                if (cur == kSentinel) break;
-                p = (p + 1) & (kSB - 1);
+                if (stop >= 0) {
+                    p = (p + stop) & (kSB - 1);  // the first empty slot: an insert starts here
+                    break;
+                }
+                p = (p + 4) & (kSB - 1);
             }
         }
         if (live && s < 0 && isput) {  // a key new to the table: claim a slot
@@ -645,7 +708,14 @@ __device__ __forceinline__ void resolve_bucket(ResolveLds& S, int b, uint32_t cn
         bool conf = false;
         if (__ballot(act)) {
             const uint32_t sl = act ? (uint32_t)s : 0u;
+#ifndef MPX_RS_PEERS_LDS
+#define MPX_RS_PEERS_LDS 1
+#endif
+#if MPX_RS_PEERS_LDS
             const unsigned long long peers = wave_peers(W, PM, sl, act);
+#else
+            const unsigned long long peers = match_bits(sl, kLgSB, act);
+#endif
             const unsigned long long putm = __ballot(act && isput);
             const unsigned long long lp = peers & below, lput = lp & putm;
             const unsigned long long allput = peers & putm;
@@ -667,9 +737,9 @@ __device__ __forceinline__ void resolve_bucket(ResolveLds& S, int b, uint32_t cn
                 TS[sl] = ns;
             }
         }
-        if (live) {
-            S.rret[idx] = ret;
-            S.rconf[idx] = conf ? 1 : 0;
+        if (live && !(MPX_RS_ABL & 2)) {
+            r_ret[base + idx] = ret;
+            r_conf[base + idx] = conf ? 1 : 0;
         }
     }
 }
@@ -736,58 +806,115 @@ __global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
             }
             __syncthreads();
         }
-        // the next 1024 records are loaded while this batch is resolved
-        int4 kv = r0 + tid < r1 ? rec_kv[r0 + tid] : make_int4(0, 0, 0, 0);
-        uint8_t o = r0 + tid < r1 ? rec_op[r0 + tid] : 0;
-        for (uint32_t base = r0; base < r1; base += kTT) {
-            const uint32_t q = base + tid;
-            const bool live = q < r1;
-            const uint32_t qn = q + kTT;
-            const int4 nkv = qn < r1 ? rec_kv[qn] : make_int4(0, 0, 0, 0);
-            const uint8_t no = qn < r1 ? rec_op[qn] : 0;
-            const uint64_t h = hash64((uint64_t)kv_lo_hi(kv.x, kv.y));
-            const uint32_t bl = bucket_of(h, g.lgnb) & (bpb - 1);
-            S.skv[tid] = kv;
-            S.sop[tid] = o;
-            S.sh[tid] = (uint8_t)home_of(h);
-            uint32_t rk = 0;
-            for (uint32_t b = 0; b < bpb; ++b) {
-                const unsigned long long m = __ballot(live && bl == b);
-                if (live && bl == b) rk = (uint32_t)__popcll(m & below);
-                if (l == 0) S.cw[w][b] = (uint32_t)__popcll(m);
+        // the next batch is loaded while this one is resolved
+        for (int i = tid; i < kRH * kTW * kMaxBPB; i += kTT) (&S.cw[0][0])[i] = 0u;
+        __syncthreads();
+        // (ops held as 32-bit values: packed into one register as bytes, the compiler waits for the
+        // prefetch at the loop back-edge)
+        int4 kv[kRH];
+        uint32_t o[kRH];
+#pragma unroll
+        for (int hh = 0; hh < kRH; ++hh) {
+            const uint32_t q = r0 + hh * kTT + tid;
+            kv[hh] = q < r1 ? rec_kv[q] : make_int4(0, 0, 0, 0);
+            o[hh] = q < r1 ? rec_op[q] : 0;
+        }
+#if MPX_RS_STAMP
+        if (tid < 8) S.ph[tid] = 0;
+        if (tid < kTW) S.rb[tid] = 0;
+        __syncthreads();
+        unsigned long long c0 = clock64(), c1;
+#define RS_STAMP(i) do { c1 = clock64(); if (tid == 0) S.ph[i] += c1 - c0; c0 = c1; } while (0)
+#else
+#define RS_STAMP(i) do {} while (0)
+#endif
+        for (uint32_t base = r0; base < r1; base += kRT) {
+            uint32_t bl[kRH], rk[kRH];
+            bool live[kRH];
+#pragma unroll
+            for (int hh = 0; hh < kRH; ++hh) {
+                const uint32_t i = hh * kTT + tid;
+                live[hh] = base + i < r1;
+                const uint64_t h = hash64((uint64_t)kv_lo_hi(kv[hh].x, kv[hh].y));
+                bl[hh] = bucket_of(h, g.lgnb) & (bpb - 1);
+                rk[hh] = 0;
+                if (MPX_RS_ABL & 4) continue;
+                const unsigned long long m = match_bits(bl[hh], (int)g.lgbpb, live[hh]);
+                rk[hh] = (uint32_t)__popcll(m & below);
+                if (live[hh] && (m >> l) == 1ull)  // the last lane of its bucket: the count
+                    S.cw[hh * kTW + w][bl[hh]] = (uint32_t)__popcll(m);
             }
+            RS_STAMP(0);
             __syncthreads();
-            if ((uint32_t)tid < bpb) {
-                uint32_t s = 0;
-                for (int w2 = 0; w2 < kTW; ++w2) {
-                    const uint32_t x = S.cw[w2][tid];
-                    S.cw[w2][tid] = s;
-                    s += x;
+            RS_STAMP(1);
+            if (w == 0) {  // lane b < bpb: prefix of bucket b over the (half, wave) groups
+                const uint32_t b = (uint32_t)l;
+                uint32_t x[kRH * kTW];
+#pragma unroll
+                for (int v = 0; v < kRH * kTW; ++v) x[v] = b < bpb ? S.cw[v][b] : 0u;
+                uint32_t tot = 0;
+#pragma unroll
+                for (int v = 0; v < kRH * kTW; ++v) {
+                    if (b < bpb) S.cw[v][b] = tot;
+                    tot += x[v];
                 }
-                S.bcnt[tid] = s;
-            }
-            __syncthreads();
-            if (tid == 0) {
-                uint32_t s = 0;
-                for (uint32_t b = 0; b < bpb; ++b) {
-                    S.bst[b] = s;
-                    s += S.bcnt[b];
+                uint32_t sc = tot;  // inclusive scan over the buckets
+#pragma unroll
+                for (int d = 1; d < kMaxBPB; d <<= 1) {
+                    const uint32_t y = __shfl_up(sc, d);
+                    if (l >= d) sc += y;
+                }
+                if (b < bpb) {
+                    S.bcnt[b] = tot;
+                    S.bst[b] = sc - tot;
                 }
             }
             __syncthreads();
-            if (live) S.lst[S.bst[bl] + S.cw[w][bl] + rk] = (uint16_t)tid;
-            __syncthreads();
-            if ((uint32_t)w < bpb) resolve_bucket(S, w, S.bcnt[w], S.bst[w], mode, err);
-            __syncthreads();
-            if (live) {
-                r_ret[q] = S.rret[tid];
-                r_conf[q] = S.rconf[tid];
+#pragma unroll
+            for (int hh = 0; hh < kRH; ++hh)
+                if (live[hh]) {
+                    const uint32_t x = S.bst[bl[hh]] + S.cw[hh * kTW + w][bl[hh]] + rk[hh];
+                    S.skv[x] = kv[hh];
+                    S.sop[x] = (uint8_t)o[hh];
+                    S.sidx[x] = (uint16_t)(hh * kTT + tid);
+                }
+            // the next batch's records load while this one resolves (issued only now: a wait for
+            // them must not be needed before this batch's records are in LDS)
+#pragma unroll
+            for (int hh = 0; hh < kRH; ++hh) {
+                const uint32_t q = base + kRT + hh * kTT + tid;
+                kv[hh] = q < r1 ? rec_kv[q] : make_int4(0, 0, 0, 0);
+                o[hh] = q < r1 ? rec_op[q] : 0;
             }
-            kv = nkv;
-            o = no;
+            RS_STAMP(2);
+            __syncthreads();
+            RS_STAMP(3);
+            for (int i = tid; i < kRH * kTW * kMaxBPB; i += kTT) (&S.cw[0][0])[i] = 0u;
+#if MPX_RS_STAMP
+            const unsigned long long rb0 = clock64();
+#endif
+            if (!(MPX_RS_ABL & 1) && (uint32_t)w < bpb)
+                resolve_bucket(S, w, S.bcnt[w], S.bst[w], mode, base, r_ret, r_conf, err);
+#if MPX_RS_STAMP
+            if (l == 0) S.rb[w] += clock64() - rb0;
+#endif
+            RS_STAMP(4);
+            __syncthreads();
+            RS_STAMP(5);
         }
         __syncthreads();
     }
+#if MPX_RS_STAMP
+    if (bin == 0 && tid == 0) {
+        unsigned long long mx = 0, sm = 0;
+        for (int i = 0; i < kTW; ++i) {
+            mx = S.rb[i] > mx ? S.rb[i] : mx;
+            sm += S.rb[i];
+        }
+        printf("RS_STAMP bin0 recs=%u rank=%llu bar1=%llu prefix+sorted=%llu bar2=%llu resolve(w0)=%llu bar3=%llu rb_max=%llu rb_mean=%llu\n",
+               r1 - r0, S.ph[0], S.ph[1], S.ph[2], S.ph[3], S.ph[4], S.ph[5], mx, sm / kTW);
+    }
+#endif
     // write back the touched slots; count the keys that became present
     uint32_t added = 0;
     for (uint32_t i = tid; i < nslot; i += kTT) {
