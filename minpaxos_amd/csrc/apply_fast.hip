@@ -21,16 +21,16 @@
 //                 before each tile (max)
 //   k_ap_scatter  per tile: a stable per-bin ranking (per-wave peer masks + wave prefix), the
 //                 tile's cold commands as a bin-sorted image in LDS, copied out as one contiguous
-//                 run per bin (16-byte key/value records + op bytes); each command's position in
-//                 the partition (pos1) is stored in log order
+//                 run per bin (16-byte key/value records + op bytes); per command its index in
+//                 the tile image (ipos, log order), per image position its partition position (cpos)
 //   k_ap_resolve  one workgroup per bin: its 16 bucket tables in LDS (keys, values, state), the
 //                 bin's records streamed in log order 1024 at a time, ranked by bucket, each
 //                 bucket's records resolved by its wave 64 at a time (peer masks within the 64, the
 //                 bucket table between rounds); results land at the record's partition position;
 //                 touched slots written back once
 //   k_ap_hot_commit  the hot keys' final value and state
-//   k_ap_emit     per tile, log order: a cold command's result is gathered from its partition
-//                 position (pos1), a hot command's from the per-wave peer scan, the earlier waves'
+//   k_ap_emit     per tile, log order: the tile's cold results gathered run by run into an LDS
+//                 image (cpos), read back by ipos; a hot command's from the per-wave peer scan, the earlier waves'
 //                 tables and the tile's incoming positions; ret / conf stored coalesced
 // Table traffic is one read and one write of each bin's slice per call instead of one random probe
 // per command. New keys: a bin whose records both PUT a key absent from the table and GET (or
@@ -56,12 +56,13 @@ constexpr int kTT = 1024;          // threads of the tile and bin workgroups
 constexpr int kTW = kTT / kWave;   // 16 waves
 constexpr int kTPer = kTL / kTT;   // 4 commands per thread; wave w owns [256 w, 256 w + 256)
 constexpr int kHMax = 64;          // hot keys per chunk, index 0 = INT64_MIN
-constexpr int kHotTab = 128;       // LDS hash of the hot keys
+constexpr int kLgHMax = 6;
+constexpr int kHotTab = 512;       // LDS hash of the hot keys (load <= 1/8: probes stay short)
 constexpr int kMaxBins = 1024;
 constexpr int kMaxBPB = 16;        // buckets per bin = waves of the resolve workgroup
 constexpr int kSampTab = 8192;     // k_ap_select's LDS count table
 constexpr uint32_t kSamples = 1u << 15;
-constexpr uint32_t kHotBit = 0x80000000u;
+constexpr uint32_t kHotIdx = 0x8000u;  // ipos: hot command (| hot index), else image index
 constexpr uint32_t kNoSlot = ~0u;
 constexpr unsigned kScatterGrid = 256;  // persistent partition grid: one workgroup per CU
 
@@ -113,23 +114,8 @@ __device__ __forceinline__ unsigned long long wave_peers(lds_u8* W, lds_u64* PM,
     return peers;
 }
 
-// the same without LDS, one ballot per distinct class among the active lanes: for the hot keys,
-// where most of a wave's lanes share a few classes and the LDS OR above would serialise on one word
-__device__ __forceinline__ unsigned long long wave_match(uint32_t c, bool act) {
-    unsigned long long rem = __ballot(act), mine = 0;
-    while (rem) {
-        const int lead = __ffsll((long long)rem) - 1;
-        const uint32_t cl = (uint32_t)__builtin_amdgcn_readlane((int)c, lead);
-        const bool in = act && c == cl;
-        const unsigned long long m = __ballot(in);
-        if (in) mine = m;
-        rem &= ~m;
-    }
-    return mine;
-}
-
-// the same from one ballot per bit of the class id (c < 2^nbits): for few classes, or where the
-// LDS round trips above are the critical path
+// the same from one ballot per bit of the class id (c < 2^nbits), without LDS: for few classes,
+// or where most lanes share a class (the LDS OR above would serialise on one word)
 __device__ __forceinline__ unsigned long long match_bits(uint32_t c, int nbits, bool act) {
     unsigned long long m = __ballot(act);
     for (int i = 0; i < nbits; ++i) {
@@ -189,16 +175,18 @@ __device__ __forceinline__ void hot_build(HotLds& s, const ApHot* hot, uint32_t 
     __syncthreads();
 }
 
-// hot index of a key (hash hk), -1 if cold
+// hot index of a key (hash hk), -1 if cold; two slots per step
 __device__ __forceinline__ int hot_find(const HotLds& s, uint32_t nh, int64_t key, uint64_t hk) {
     if (key == kSentinel) return 0;
     if (nh <= 1) return -1;
     uint32_t p = (uint32_t)(hk >> 8) & (kHotTab - 1);
     for (;;) {
-        const int64_t cur = s.k[p];
-        if (cur == key) return s.h[p];
-        if (cur == kSentinel) return -1;
-        p = (p + 1) & (kHotTab - 1);
+        const int64_t c0 = s.k[p], c1 = s.k[(p + 1) & (kHotTab - 1)];
+        if (c0 == key) return s.h[p];
+        if (c0 == kSentinel) return -1;
+        if (c1 == key) return s.h[(p + 1) & (kHotTab - 1)];
+        if (c1 == kSentinel) return -1;
+        p = (p + 2) & (kHotTab - 1);
     }
 }
 
@@ -342,7 +330,7 @@ __global__ __launch_bounds__(kTT) void k_ap_count(ApGeo g, const uint8_t* __rest
         if (!__ballot(hotc)) continue;
         // per hot key of the round: its last command and its last PUT, one LDS atomic each
         const bool put = hotc && o[u] == MPX_OP_PUT;
-        const unsigned long long peers = wave_match((uint32_t)hh, hotc);
+        const unsigned long long peers = match_bits((uint32_t)hh, kLgHMax, hotc);
         const unsigned long long puts = peers & __ballot(put);
         if (hotc && hi_bit(peers) == l) atomicMax(&ha[hh], j + 1);
         if (put && hi_bit(puts) == l) atomicMax(&hp[hh], j + 1);
@@ -486,7 +474,9 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
                                                     const ApHot* __restrict__ hot,
                                                     int4* __restrict__ rec_kv,
                                                     uint8_t* __restrict__ rec_op,
-                                                    uint32_t* __restrict__ pos1) {
+                                                    uint16_t* __restrict__ ipos,
+                                                    uint32_t* __restrict__ cpos,
+                                                    uint32_t* __restrict__ tcold) {
     __shared__ ScatterLds S;
     const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
     const uint32_t nh = hot->n;
@@ -533,7 +523,7 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
             const bool in = j < n;
             const uint64_t h = hash64((uint64_t)k[r]);
             const int hh = in ? hot_find(S.hl, nh, k[r], h) : -1;
-            if (in && hh >= 0) pos1[j] = kHotBit | (uint32_t)hh;
+            if (in && hh >= 0) ipos[j] = (uint16_t)(kHotIdx | (uint32_t)hh);
             cold[r] = in && hh < 0;
             bin[r] = cold[r] ? bin_of(h, g) : 0u;
             rank[r] = 0;
@@ -590,15 +580,17 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
                                   (int)(uint32_t)v[r], (int)(uint32_t)((uint64_t)v[r] >> 32));
             S.iop[ip] = (uint8_t)o[r];
             S.ibin[ip] = (uint16_t)b;
-            pos1[j0 + r * kWave] = S.roff[b] + wr;
+            ipos[j0 + r * kWave] = (uint16_t)ip;
         }
         __syncthreads();
         const uint32_t nc = S.ncold;
+        if (tid == 0) tcold[tile] = nc;
         for (uint32_t i = tid; i < nc; i += kTT) {
             const uint32_t b = S.ibin[i];
             const uint32_t dst = S.roff[b] + (i - S.lstart[b]);
             rec_kv[dst] = S.img[i];
             rec_op[dst] = S.iop[i];
+            cpos[(uint64_t)tile * kTL + i] = dst;  // image order: emit gathers run by run
         }
         for (int i = tid; i < kTW * kMaxBins / 2; i += kTT) cw32[i] = 0u;  // next tile's counts
         __syncthreads();
@@ -636,111 +628,146 @@ __device__ __forceinline__ int64_t kv_lo_hi(int lo, int hi) {
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
-// bucket b of the bin (wave b): its cnt records of this tile, in log order, 64 per round
+// bucket b of the bin (wave b): its cnt records of this batch, in log order, 64 per round.
+// A round is two stages: A = the slot lookup (claiming slots for new keys) and the peer masks;
+// B = the slot state read, the results, the state update. (Issuing A of round r+1 before B of
+// round r, which it does not depend on, measured slower: the volatile peer-mask accesses keep
+// program order, so nothing overlapped and registers grew.)
 // (results go straight to the batch's partition positions: a batch covers 2048 consecutive ones,
 // so the scattered 8-byte stores of its waves meet in L2)
-__device__ __forceinline__ void resolve_bucket(ResolveLds& S, int b, uint32_t cnt, uint32_t st0,
-                                              int mode, uint32_t base, int64_t* __restrict__ r_ret,
-                                              uint8_t* __restrict__ r_conf, uint32_t* err) {
+struct RoundA {
+    unsigned long long peers, putm;
+    int64_t v;
+    uint32_t idx, sl;
+    bool live, act, isput, isget;
+};
+
+__device__ __forceinline__ RoundA resolve_stage_a(ResolveLds& S, int b, uint32_t cnt, uint32_t st0,
+                                                  uint32_t r, int mode, uint32_t* err) {
     const int l = lane_id();
-    const unsigned long long below = (1ull << l) - 1ull;
     int64_t* T = S.tk + b * kSB;
-    int64_t* V = S.tv + b * kSB;
     uint8_t* TS = S.ts + b * kSB;
     lds_u8* W = (lds_u8*)&S.W[b][0];
     lds_u64* PM = (lds_u64*)&S.PM[b][0];
-    for (uint32_t r = 0; r < cnt; r += kWave) {
-        const bool live = r + l < cnt;
-        const uint32_t x = live ? st0 + r + l : 0u;
-        const int4 kv = S.skv[x];
-        const uint32_t idx = S.sidx[x];
-        const int64_t k = kv_lo_hi(kv.x, kv.y), v = kv_lo_hi(kv.z, kv.w);
-        const uint8_t o = S.sop[x];
-        const bool isput = o == MPX_OP_PUT, isget = o == MPX_OP_GET;
-        // lookup in the bucket, 4 slots per step: the worst probe length among the wave's 64 lanes
-        // sets the number of dependent LDS reads
-        int s = -1;
-        uint32_t p = home_of(hash64((uint64_t)k));
-        if (live) {
-            for (int step = 0; step < kSB / 4; ++step) {
-                int64_t c[4];
+    RoundA a;
+    a.live = r + l < cnt;
+    const uint32_t x = a.live ? st0 + r + l : 0u;
+    const int4 kv = S.skv[x];
+    a.idx = S.sidx[x];
+    const int64_t k = kv_lo_hi(kv.x, kv.y);
+    a.v = kv_lo_hi(kv.z, kv.w);
+    const uint8_t o = S.sop[x];
+    a.isput = o == MPX_OP_PUT;
+    a.isget = o == MPX_OP_GET;
+    // lookup in the bucket, 4 slots per step: the worst probe length among the wave's 64 lanes
+    // sets the number of dependent LDS reads
+    int s = -1;
+    uint32_t p = home_of(hash64((uint64_t)k));
+    if (a.live) {
+        for (int step = 0; step < kSB / 4; ++step) {
+            int64_t c[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) c[u] = T[(p + u) & (kSB - 1)];
-                int hit = -1, stop = -1;
+            for (int u = 0; u < 4; ++u) c[u] = T[(p + u) & (kSB - 1)];
+            int hit = -1, stop = -1;
 #pragma unroll
-                for (int u = 3; u >= 0; --u) {
-                    if (c[u] == k) hit = u;
-                    if (c[u] == kSentinel) stop = u;
-                }
-                if (hit >= 0 && (stop < 0 || hit < stop)) {
-                    s = (int)((p + hit) & (kSB - 1));
-                    break;
-                }
-                if (stop >= 0) {
-                    p = (p + stop) & (kSB - 1);  // the first empty slot: an insert starts here
-                    break;
-                }
-                p = (p + 4) & (kSB - 1);
+            for (int u = 3; u >= 0; --u) {
+                if (c[u] == k) hit = u;
+                if (c[u] == kSentinel) stop = u;
             }
-        }
-        if (live && s < 0 && isput) {  // a key new to the table: claim a slot
-            if (mode == 0) atomicOr(&S.flags, kFNewPut);
-            for (int probe = 0; probe < kSB; ++probe) {
-                const unsigned long long cur =
-                    atomicCAS(reinterpret_cast<unsigned long long*>(&T[p]),
-                              (unsigned long long)kSentinel, (unsigned long long)k);
-                if (cur == (unsigned long long)kSentinel) {
-                    s = (int)p;
-                    TS[p] |= kSNew;
-                    break;
-                }
-                if ((int64_t)cur == k) {
-                    s = (int)p;
-                    break;
-                }
-                p = (p + 1) & (kSB - 1);
+            if (hit >= 0 && (stop < 0 || hit < stop)) {
+                s = (int)((p + hit) & (kSB - 1));
+                break;
             }
-            if (s < 0) raise_err(err, kErrKvFull);
+            if (stop >= 0) {
+                p = (p + stop) & (kSB - 1);  // the first empty slot: an insert starts here
+                break;
+            }
+            p = (p + 4) & (kSB - 1);
         }
-        if (live && s < 0 && !isput && mode == 0) atomicOr(&S.flags, kFAbsentOther);
-        const bool act = live && s >= 0;
-        int64_t ret = 0;
-        bool conf = false;
-        if (__ballot(act)) {
-            const uint32_t sl = act ? (uint32_t)s : 0u;
+    }
+    if (a.live && s < 0 && a.isput) {  // a key new to the table: claim a slot
+        if (mode == 0) atomicOr(&S.flags, kFNewPut);
+        for (int probe = 0; probe < kSB; ++probe) {
+            const unsigned long long cur =
+                atomicCAS(reinterpret_cast<unsigned long long*>(&T[p]),
+                          (unsigned long long)kSentinel, (unsigned long long)k);
+            if (cur == (unsigned long long)kSentinel) {
+                s = (int)p;
+                TS[p] |= kSNew;
+                break;
+            }
+            if ((int64_t)cur == k) {
+                s = (int)p;
+                break;
+            }
+            p = (p + 1) & (kSB - 1);
+        }
+        if (s < 0) raise_err(err, kErrKvFull);
+    }
+    if (a.live && s < 0 && !a.isput && mode == 0) atomicOr(&S.flags, kFAbsentOther);
+    a.act = a.live && s >= 0;
+    a.sl = a.act ? (uint32_t)s : 0u;
+    a.peers = 0;
+    a.putm = 0;
+    if (__ballot(a.act)) {
 #ifndef MPX_RS_PEERS_LDS
 #define MPX_RS_PEERS_LDS 1
 #endif
 #if MPX_RS_PEERS_LDS
-            const unsigned long long peers = wave_peers(W, PM, sl, act);
+        a.peers = wave_peers(W, PM, a.sl, a.act);
 #else
-            const unsigned long long peers = match_bits(sl, kLgSB, act);
+        a.peers = match_bits(a.sl, kLgSB, a.act);
 #endif
-            const unsigned long long putm = __ballot(act && isput);
-            const unsigned long long lp = peers & below, lput = lp & putm;
-            const unsigned long long allput = peers & putm;
-            const uint8_t stt = act ? TS[sl] : 0;
-            const bool hasprev = lp ? true : (stt & kSTouched) != 0;
-            const bool prevput = lp ? ((putm >> hi_bit(lp)) & 1ull) != 0 : (stt & kSLastPut) != 0;
-            const int64_t vget = shfl64(v, lput ? hi_bit(lput) : l);
-            const int64_t vlast = shfl64(v, allput ? hi_bit(allput) : l);
-            const int64_t tab = act ? V[sl] : 0;
-            ret = !act ? 0 : isput ? v : (isget ? (lput ? vget : ((stt & kSPresent) ? tab : 0)) : 0);
-            conf = act && hasprev && (prevput || isput);
-            if (act && (peers >> l) == 1ull) {  // the round's last command on this slot
-                uint8_t ns = (uint8_t)((stt & (kSPresent | kSValDirty | kSNew | kSWasPresent)) |
-                                       kSTouched | (isput ? kSLastPut : 0));
-                if (allput) {
-                    V[sl] = vlast;
-                    ns |= kSPresent | kSValDirty;
-                }
-                TS[sl] = ns;
+        a.putm = __ballot(a.act && a.isput);
+    }
+    return a;
+}
+
+__device__ __forceinline__ void resolve_stage_b(ResolveLds& S, int b, const RoundA& a,
+                                                uint32_t base, int64_t* __restrict__ r_ret,
+                                                uint8_t* __restrict__ r_conf) {
+    const int l = lane_id();
+    const unsigned long long below = (1ull << l) - 1ull;
+    int64_t* V = S.tv + b * kSB;
+    uint8_t* TS = S.ts + b * kSB;
+    int64_t ret = 0;
+    bool conf = false;
+    if (__ballot(a.act)) {
+        const uint32_t sl = a.sl;
+        const unsigned long long lp = a.peers & below, lput = lp & a.putm;
+        const unsigned long long allput = a.peers & a.putm;
+        const uint8_t stt = a.act ? TS[sl] : 0;
+        const bool hasprev = lp ? true : (stt & kSTouched) != 0;
+        const bool prevput = lp ? ((a.putm >> hi_bit(lp)) & 1ull) != 0 : (stt & kSLastPut) != 0;
+        const int64_t vget = shfl64(a.v, lput ? hi_bit(lput) : l);
+        const int64_t vlast = shfl64(a.v, allput ? hi_bit(allput) : l);
+        const int64_t tab = a.act ? V[sl] : 0;
+        ret = !a.act ? 0
+                     : a.isput ? a.v
+                               : (a.isget ? (lput ? vget : ((stt & kSPresent) ? tab : 0)) : 0);
+        conf = a.act && hasprev && (prevput || a.isput);
+        if (a.act && (a.peers >> l) == 1ull) {  // the round's last command on this slot
+            uint8_t ns = (uint8_t)((stt & (kSPresent | kSValDirty | kSNew | kSWasPresent)) |
+                                   kSTouched | (a.isput ? kSLastPut : 0));
+            if (allput) {
+                V[sl] = vlast;
+                ns |= kSPresent | kSValDirty;
             }
+            TS[sl] = ns;
         }
-        if (live && !(MPX_RS_ABL & 2)) {
-            r_ret[base + idx] = ret;
-            r_conf[base + idx] = conf ? 1 : 0;
-        }
+    }
+    if (a.live && !(MPX_RS_ABL & 2)) {
+        r_ret[base + a.idx] = ret;
+        r_conf[base + a.idx] = conf ? 1 : 0;
+    }
+}
+
+__device__ __forceinline__ void resolve_bucket(ResolveLds& S, int b, uint32_t cnt, uint32_t st0,
+                                              int mode, uint32_t base, int64_t* __restrict__ r_ret,
+                                              uint8_t* __restrict__ r_conf, uint32_t* err) {
+    for (uint32_t r = 0; r < cnt; r += kWave) {
+        const RoundA a = resolve_stage_a(S, b, cnt, st0, r, mode, err);
+        resolve_stage_b(S, b, a, base, r_ret, r_conf);
     }
 }
 
@@ -847,37 +874,52 @@ __global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
             RS_STAMP(0);
             __syncthreads();
             RS_STAMP(1);
-            if (w == 0) {  // lane b < bpb: prefix of bucket b over the (half, wave) groups
-                const uint32_t b = (uint32_t)l;
-                uint32_t x[kRH * kTW];
+            // every wave computes the prefixes its own records need (lane b: bucket b), so no wave
+            // waits for another between the ranking and the staging
+            {
+                const uint32_t b = (uint32_t)l & (kMaxBPB - 1);
+                uint32_t c0[kTW], c1[kTW];
 #pragma unroll
-                for (int v = 0; v < kRH * kTW; ++v) x[v] = b < bpb ? S.cw[v][b] : 0u;
-                uint32_t tot = 0;
-#pragma unroll
-                for (int v = 0; v < kRH * kTW; ++v) {
-                    if (b < bpb) S.cw[v][b] = tot;
-                    tot += x[v];
+                for (int v = 0; v < kTW; ++v) {
+                    c0[v] = b < bpb ? S.cw[v][b] : 0u;
+                    c1[v] = b < bpb ? S.cw[kTW + v][b] : 0u;
                 }
-                uint32_t sc = tot;  // inclusive scan over the buckets
+                uint32_t all0 = 0, all1 = 0, pre0 = 0, pre1 = 0;
+#pragma unroll
+                for (int v = 0; v < kTW; ++v) {
+                    pre0 += v < w ? c0[v] : 0u;
+                    pre1 += v < w ? c1[v] : 0u;
+                    all0 += c0[v];
+                    all1 += c1[v];
+                }
+                const uint32_t tot = all0 + all1;
+                uint32_t sc = tot;  // inclusive scan over the buckets (lanes 0..15)
 #pragma unroll
                 for (int d = 1; d < kMaxBPB; d <<= 1) {
                     const uint32_t y = __shfl_up(sc, d);
-                    if (l >= d) sc += y;
+                    if ((l & (kMaxBPB - 1)) >= d) sc += y;
                 }
-                if (b < bpb) {
+                const uint32_t st = sc - tot;
+                if (w == 0 && l < kMaxBPB && b < bpb) {
                     S.bcnt[b] = tot;
-                    S.bst[b] = sc - tot;
+                    S.bst[b] = st;
+                }
+                // position of each record: bucket start + earlier groups + rank in its group
+#pragma unroll
+                for (int hh = 0; hh < kRH; ++hh) {
+                    const uint32_t bb = bl[hh];
+                    const uint32_t stb = (uint32_t)__shfl((int)st, (int)bb);
+                    const uint32_t p0 = (uint32_t)__shfl((int)pre0, (int)bb);
+                    const uint32_t a0 = (uint32_t)__shfl((int)all0, (int)bb);
+                    const uint32_t p1 = (uint32_t)__shfl((int)pre1, (int)bb);
+                    if (live[hh]) {
+                        const uint32_t x = stb + (hh == 0 ? p0 : a0 + p1) + rk[hh];
+                        S.skv[x] = kv[hh];
+                        S.sop[x] = (uint8_t)o[hh];
+                        S.sidx[x] = (uint16_t)(hh * kTT + tid);
+                    }
                 }
             }
-            __syncthreads();
-#pragma unroll
-            for (int hh = 0; hh < kRH; ++hh)
-                if (live[hh]) {
-                    const uint32_t x = S.bst[bl[hh]] + S.cw[hh * kTW + w][bl[hh]] + rk[hh];
-                    S.skv[x] = kv[hh];
-                    S.sop[x] = (uint8_t)o[hh];
-                    S.sidx[x] = (uint16_t)(hh * kTT + tid);
-                }
             // the next batch's records load while this one resolves (issued only now: a wait for
             // them must not be needed before this batch's records are in LDS)
 #pragma unroll
@@ -957,11 +999,15 @@ struct EmitLds {
     uint2 inc[kHMax];      // over the earlier tiles
     int64_t hval[kHMax];
     uint32_t hfl[kHMax];
+    int64_t iret[kTL];     // the tile's cold results in image order (bin runs)
+    uint8_t iconf[kTL];
 };
 
 __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restrict__ op,
                                                  const int64_t* __restrict__ val, uint32_t n,
-                                                 const uint32_t* __restrict__ pos1,
+                                                 const uint16_t* __restrict__ ipos,
+                                                 const uint32_t* __restrict__ cpos,
+                                                 const uint32_t* __restrict__ tcold,
                                                  const int64_t* __restrict__ r_ret,
                                                  const uint8_t* __restrict__ r_conf,
                                                  const uint32_t* __restrict__ rows,
@@ -978,44 +1024,60 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
         S.hval[tid] = hot->val0[tid];
         S.hfl[tid] = hot->flags[tid];
     }
-    __syncthreads();
+    // the cold results, lanes over the tile image: consecutive lanes read consecutive positions of
+    // one bin run (the gather in command order touched one line per lane)
+    {
+        const uint32_t nc = tcold[tile];
+        const uint32_t* cp = cpos + (uint64_t)tile * kTL;
+        uint32_t q[kTPer];
+#pragma unroll
+        for (int u = 0; u < kTPer; ++u) {
+            const uint32_t i = tid + u * kTT;
+            q[u] = i < nc ? cp[i] : 0u;
+        }
+        int64_t x[kTPer];
+        uint8_t c[kTPer];
+#pragma unroll
+        for (int u = 0; u < kTPer; ++u) {
+            const uint32_t i = tid + u * kTT;
+            x[u] = i < nc ? r_ret[q[u]] : 0;
+            c[u] = i < nc ? r_conf[q[u]] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kTPer; ++u) {
+            const uint32_t i = tid + u * kTT;
+            if (i < nc) {
+                S.iret[i] = x[u];
+                S.iconf[i] = c[u];
+            }
+        }
+    }
     const uint32_t jw = tile * (uint32_t)kTL + (uint32_t)w * (kWave * kTPer);
     uint32_t p[kTPer];
-#pragma unroll
-    for (int r = 0; r < kTPer; ++r) {
-        const uint32_t j = jw + r * kWave + l;
-        p[r] = j < n ? pos1[j] : 0u;
-    }
     int64_t rv[kTPer];
-    uint8_t cf[kTPer], o[kTPer];
+    uint8_t cf[kTPer];
+    uint32_t o[kTPer];
 #pragma unroll
     for (int r = 0; r < kTPer; ++r) {
         const uint32_t j = jw + r * kWave + l;
         const bool in = j < n;
-        const bool hotc = in && (p[r] & kHotBit);
-        rv[r] = 0;
+        p[r] = in ? ipos[j] : 0u;
+        const bool hotc = in && (p[r] & kHotIdx);
+        o[r] = hotc ? op[j] : 0u;
+        rv[r] = hotc ? val[j] : 0;
         cf[r] = 0;
-        o[r] = 0;
-        if (in && !hotc) {
-            rv[r] = r_ret[p[r]];
-            cf[r] = r_conf[p[r]];
-        }
-        if (hotc) {
-            o[r] = op[j];
-            rv[r] = val[j];
-        }
     }
     const unsigned long long below = (1ull << l) - 1ull;
     uint32_t pa[kTPer], pp[kTPer];
 #pragma unroll
     for (int r = 0; r < kTPer; ++r) {
         const uint32_t j = jw + r * kWave + l;
-        const bool hotc = j < n && (p[r] & kHotBit);
+        const bool hotc = j < n && (p[r] & kHotIdx);
         pa[r] = 0;
         pp[r] = 0;
         if (!__ballot(hotc)) continue;
-        const uint32_t h = hotc ? (p[r] & ~kHotBit) : 0u;
-        const unsigned long long peers = wave_match(h, hotc);
+        const uint32_t h = hotc ? (p[r] & ~kHotIdx) : 0u;
+        const unsigned long long peers = match_bits(h, kLgHMax, hotc);
         const unsigned long long putm = __ballot(hotc && o[r] == MPX_OP_PUT);
         if (hotc) {
             const uint2 tr = S.T[w][h];
@@ -1045,8 +1107,8 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
     for (int r = 0; r < kTPer; ++r) {
         const uint32_t j = jw + r * kWave + l;
         if (j >= n) continue;
-        if (p[r] & kHotBit) {
-            const uint32_t h = p[r] & ~kHotBit;
+        if (p[r] & kHotIdx) {
+            const uint32_t h = p[r] & ~kHotIdx;
             const uint2 tp = S.TP[w][h], ic = S.inc[h];
             uint32_t a = pa[r] > tp.x ? pa[r] : tp.x;
             a = a > ic.x ? a : ic.x;
@@ -1061,6 +1123,9 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
                                              : 0);
             rv[r] = x;
             cf[r] = hasprev && (prevput || isput) ? 1 : 0;
+        } else {
+            rv[r] = S.iret[p[r]];
+            cf[r] = S.iconf[p[r]];
         }
         st_stream(ret + j, rv[r]);
         if (conf) st_stream(conf + j, cf[r]);
@@ -1070,7 +1135,7 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
 // ---- launcher ---------------------------------------------------------------------------------
 namespace {
 struct FastLayout {
-    uint64_t rows, part, bin_start, rec_kv, rec_op, pos1, r_ret, r_conf, hot, total;
+    uint64_t rows, part, bin_start, rec_kv, rec_op, ipos, cpos, tcold, r_ret, r_conf, hot, total;
 };
 
 ApGeo geo_for(const KvTable& t, uint64_t n) {
@@ -1097,7 +1162,9 @@ FastLayout fast_layout(const KvTable& t, uint64_t c) {
     L.bin_start = o; o += al(((uint64_t)g.nbin + 1) * 4);
     L.rec_kv = o; o += al(c * 16);
     L.rec_op = o; o += al(c);
-    L.pos1 = o; o += al(c * 4);
+    L.ipos = o; o += al(c * 2);
+    L.cpos = o; o += al((uint64_t)g.tiles * kTL * 4);
+    L.tcold = o; o += al((uint64_t)g.tiles * 4);
     L.r_ret = o; o += al(c * 8);
     L.r_conf = o; o += al(c);
     L.hot = o; o += al(sizeof(ApHot));
@@ -1150,7 +1217,9 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
     uint32_t* bin_start = (uint32_t*)(b + L.bin_start);
     int4* rec_kv = (int4*)(b + L.rec_kv);
     uint8_t* rec_op = (uint8_t*)(b + L.rec_op);
-    uint32_t* pos1 = (uint32_t*)(b + L.pos1);
+    uint16_t* ipos = (uint16_t*)(b + L.ipos);
+    uint32_t* cpos = (uint32_t*)(b + L.cpos);
+    uint32_t* tcold = (uint32_t*)(b + L.tcold);
     int64_t* r_ret = (int64_t*)(b + L.r_ret);
     uint8_t* r_conf = (uint8_t*)(b + L.r_conf);
     ApHot* hot = (ApHot*)(b + L.hot);
@@ -1172,11 +1241,12 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
         k_ap_scan_top<<<1, kTT, 0, stream>>>(g, part, bin_start, hot);
         k_ap_scan_rows<<<g.ng, 256, 0, stream>>>(g, rows, part, hot);
         k_ap_scatter<<<kScatterGrid, kTT, 0, stream>>>(g, op + c0, key + c0, val + c0, n, rows, hot,
-                                                  rec_kv, rec_op, pos1);
+                                                  rec_kv, rec_op, ipos, cpos, tcold);
         k_ap_resolve<<<g.nbin, kTT, 0, stream>>>(g, t, bin_start, rec_kv, rec_op, r_ret, r_conf,
                                                  hot, err);
         k_ap_hot_commit<<<1, kHMax, 0, stream>>>(t, val + c0, hot, err);
-        k_ap_emit<<<g.tiles, kTT, 0, stream>>>(g, op + c0, val + c0, n, pos1, r_ret, r_conf, rows,
+        k_ap_emit<<<g.tiles, kTT, 0, stream>>>(g, op + c0, val + c0, n, ipos, cpos, tcold, r_ret,
+                                               r_conf, rows,
                                                hot, ret + c0, conf ? conf + c0 : nullptr);
     }
     return hipGetLastError();
