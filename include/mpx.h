@@ -188,7 +188,12 @@ typedef struct mpx_prepare_effect {
 typedef struct mpx_config {
     int32_t n_replicas;     /* N, 1..16                                                     */
     int32_t mode;           /* MPX_MODE_MIN / MPX_MODE_CLASSIC                              */
-    uint64_t kv_capacity;   /* key capacity of the engine's KV table (mpx_apply); 0 = 1<<20 */
+    uint64_t kv_capacity;   /* key capacity of the engine's KV table (mpx_apply); 0 = 1<<20.
+                               The table has the next power of two >= 2 x kv_capacity slots
+                               (at least 1024), cut by key hash into buckets of 256 slots;
+                               a key whose bucket is full fails the call with MPX_E_KV_FULL
+                               (at the default load of <= 1/2 a practical impossibility
+                               for non-adversarial keys)                                  */
     uint32_t kv_per_group;  /* max live keys per group table (mpx_group_step), <= 1024;
                                0 = 512. Also picks the fused step's fast-path variant (256:
                                the config-5 kernel); a group whose call touches more than
@@ -250,7 +255,8 @@ int mpx_prepare_select_min_dev(mpx_engine* eng, const mpx_prepare_reply_min* d_r
 /* ---- A5/A6: batched KV apply on the engine's State ---------------------------------------
  * Executes the m commands in array (log) order against the engine's persistent table:
  * ret[i] = Execute's return value; conf_prev[i] (optional) = state.Conflict(previous command
- * on the same key in this call, command i), 0 if there is none.                            */
+ * on the same key in this call, command i), 0 if there is none. Only keys PUT at some point
+ * occupy the table: GETs (and other ops) of absent keys return NIL and leave it unchanged.   */
 int mpx_apply(mpx_engine* eng, const uint8_t* op, const int64_t* key, const int64_t* val,
               size_t m, int64_t* ret, uint8_t* conf_prev);
 /* allocate the KV table and the apply workspace for calls of up to max_cmds commands, so

@@ -74,7 +74,7 @@ struct ApplyWork {      // scratch sized for m commands (see apply_work_bytes)
     void* base;
     uint64_t bytes;
 };
-// commands per apply chunk (0 = default): bounds the pipeline's scratch (30 B per command on the
+// commands per apply chunk (0 = default): bounds the pipeline's scratch (34 B per command on the
 // partitioned path, 48 B on the sort-based one);
 // env MPX_APPLY_CHUNK overrides it per engine (tests use tiny chunks to cross boundaries)
 constexpr uint64_t kApplyChunkDefault = 1ull << 26;
