@@ -61,7 +61,7 @@ constexpr int kHotTab = 512;       // LDS hash of the hot keys (load <= 1/8: pro
 constexpr int kMaxBins = 1024;
 constexpr int kMaxBPB = 16;        // buckets per bin = waves of the resolve workgroup
 constexpr int kSampTab = 8192;     // k_ap_select's LDS count table
-constexpr uint32_t kSamples = 1u << 15;
+constexpr uint32_t kSamples = 1u << 15;  // (k_ap_select divides by a shift)
 constexpr uint32_t kHotIdx = 0x8000u;  // ipos: hot command (| hot index), else image index
 constexpr uint32_t kNoSlot = ~0u;
 constexpr unsigned kScatterGrid = 256;  // persistent partition grid: one workgroup per CU
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(kTT) void k_ap_select(KvTable t, const int64_t* __r
 #pragma unroll
             for (int u = 0; u < kB; ++u) {
                 const uint32_t i = i0 + u * kTT;
-                const uint32_t j = S == n ? i : (uint32_t)(((uint64_t)i * n) / S);
+                const uint32_t j = S == n ? i : (uint32_t)(((uint64_t)i * n) >> 15);  // S = 2^15
                 k[u] = i < S ? key[j] : kSentinel;
             }
 #pragma unroll
@@ -311,12 +311,12 @@ __global__ __launch_bounds__(kTT) void k_ap_count(ApGeo g, const uint8_t* __rest
     const uint32_t tile = xcd_tile(g.tiles);
     const uint32_t j0 = tile * (uint32_t)kTL;
     int64_t k[kTPer];
-    uint8_t o[kTPer];
+    uint32_t o[kTPer];  // ops: loaded up front when hot keys exist, else only for INT64_MIN keys
 #pragma unroll
     for (int u = 0; u < kTPer; ++u) {
         const uint32_t j = j0 + u * kTT + tid;
         k[u] = j < n ? key[j] : 0;
-        o[u] = j < n ? op[j] : 0;
+        o[u] = j < n && nh > 1 ? op[j] : 0u;
     }
     const int l = lane_id();
 #pragma unroll
@@ -328,6 +328,7 @@ __global__ __launch_bounds__(kTT) void k_ap_count(ApGeo g, const uint8_t* __rest
         if (in && hh < 0) atomicAdd(&hist[bin_of(h, g)], 1u);
         const bool hotc = in && hh >= 0;
         if (!__ballot(hotc)) continue;
+        if (nh <= 1 && hotc) o[u] = op[j];
         // per hot key of the round: its last command and its last PUT, one LDS atomic each
         const bool put = hotc && o[u] == MPX_OP_PUT;
         const unsigned long long peers = match_bits((uint32_t)hh, kLgHMax, hotc);
@@ -605,8 +606,8 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
 }
 
 // ---- per-bin resolve ------------------------------------------------------------------------------
-constexpr int kRH = 2;             // records per thread per resolve batch
-constexpr int kRT = kTT * kRH;     // 2048 records per batch
+constexpr int kRH = 3;             // records per thread per resolve batch
+constexpr int kRT = kTT * kRH;     // 3072 records per batch
 struct ResolveLds {
     int64_t tk[kMaxBPB * kSB];
     int64_t tv[kMaxBPB * kSB];
@@ -633,7 +634,7 @@ __device__ __forceinline__ int64_t kv_lo_hi(int lo, int hi) {
 // B = the slot state read, the results, the state update. (Issuing A of round r+1 before B of
 // round r, which it does not depend on, measured slower: the volatile peer-mask accesses keep
 // program order, so nothing overlapped and registers grew.)
-// (results go straight to the batch's partition positions: a batch covers 2048 consecutive ones,
+// (results go straight to the batch's partition positions: a batch covers 3072 consecutive ones,
 // so the scattered 8-byte stores of its waves meet in L2)
 struct RoundA {
     unsigned long long peers, putm;
@@ -878,22 +879,28 @@ __global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
             // waits for another between the ranking and the staging
             {
                 const uint32_t b = (uint32_t)l & (kMaxBPB - 1);
-                uint32_t c0[kTW], c1[kTW];
+                // per half: the records of this wave's earlier groups, and of all groups
+                uint32_t pre[kRH], all[kRH];
 #pragma unroll
-                for (int v = 0; v < kTW; ++v) {
-                    c0[v] = b < bpb ? S.cw[v][b] : 0u;
-                    c1[v] = b < bpb ? S.cw[kTW + v][b] : 0u;
-                }
-                uint32_t all0 = 0, all1 = 0, pre0 = 0, pre1 = 0;
+                for (int hh = 0; hh < kRH; ++hh) {
+                    uint32_t c[kTW];
 #pragma unroll
-                for (int v = 0; v < kTW; ++v) {
-                    pre0 += v < w ? c0[v] : 0u;
-                    pre1 += v < w ? c1[v] : 0u;
-                    all0 += c0[v];
-                    all1 += c1[v];
+                    for (int v = 0; v < kTW; ++v) c[v] = b < bpb ? S.cw[hh * kTW + v][b] : 0u;
+                    pre[hh] = 0;
+                    all[hh] = 0;
+#pragma unroll
+                    for (int v = 0; v < kTW; ++v) {
+                        pre[hh] += v < w ? c[v] : 0u;
+                        all[hh] += c[v];
+                    }
                 }
-                const uint32_t tot = all0 + all1;
-                uint32_t sc = tot;  // inclusive scan over the buckets (lanes 0..15)
+                uint32_t tot = 0;
+#pragma unroll
+                for (int hh = 0; hh < kRH; ++hh) {  // earlier halves come first in log order
+                    pre[hh] += tot;
+                    tot += all[hh];
+                }
+                uint32_t sc = tot;  // inclusive scan over the buckets (each 16-lane segment)
 #pragma unroll
                 for (int d = 1; d < kMaxBPB; d <<= 1) {
                     const uint32_t y = __shfl_up(sc, d);
@@ -907,13 +914,9 @@ __global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
                 // position of each record: bucket start + earlier groups + rank in its group
 #pragma unroll
                 for (int hh = 0; hh < kRH; ++hh) {
-                    const uint32_t bb = bl[hh];
-                    const uint32_t stb = (uint32_t)__shfl((int)st, (int)bb);
-                    const uint32_t p0 = (uint32_t)__shfl((int)pre0, (int)bb);
-                    const uint32_t a0 = (uint32_t)__shfl((int)all0, (int)bb);
-                    const uint32_t p1 = (uint32_t)__shfl((int)pre1, (int)bb);
+                    const int bb = (int)bl[hh];
+                    const uint32_t x = (uint32_t)__shfl((int)(st + pre[hh]), bb) + rk[hh];
                     if (live[hh]) {
-                        const uint32_t x = stb + (hh == 0 ? p0 : a0 + p1) + rk[hh];
                         S.skv[x] = kv[hh];
                         S.sop[x] = (uint8_t)o[hh];
                         S.sidx[x] = (uint16_t)(hh * kTT + tid);
@@ -1024,6 +1027,16 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
         S.hval[tid] = hot->val0[tid];
         S.hfl[tid] = hot->flags[tid];
     }
+    const uint32_t jw = tile * (uint32_t)kTL + (uint32_t)w * (kWave * kTPer);
+    uint32_t p[kTPer];
+    int64_t rv[kTPer];
+    uint8_t cf[kTPer];
+    uint32_t o[kTPer];
+#pragma unroll
+    for (int r = 0; r < kTPer; ++r) {
+        const uint32_t j = jw + r * kWave + l;
+        p[r] = j < n ? ipos[j] : 0u;
+    }
     // the cold results, lanes over the tile image: consecutive lanes read consecutive positions of
     // one bin run (the gather in command order touched one line per lane)
     {
@@ -1052,16 +1065,10 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
             }
         }
     }
-    const uint32_t jw = tile * (uint32_t)kTL + (uint32_t)w * (kWave * kTPer);
-    uint32_t p[kTPer];
-    int64_t rv[kTPer];
-    uint8_t cf[kTPer];
-    uint32_t o[kTPer];
 #pragma unroll
     for (int r = 0; r < kTPer; ++r) {
         const uint32_t j = jw + r * kWave + l;
         const bool in = j < n;
-        p[r] = in ? ipos[j] : 0u;
         const bool hotc = in && (p[r] & kHotIdx);
         o[r] = hotc ? op[j] : 0u;
         rv[r] = hotc ? val[j] : 0;
