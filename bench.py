@@ -162,8 +162,11 @@ def host_cores():
 def traffic_of(path, **want):
     """HBM bytes per launch from a committed rocprofv3 PMC summary (tools/traffic.py) when it
     was measured on this exact configuration, else None"""
-    for p in ([path] if path else [os.path.join(ROOT, "profiles", f"traffic_r0{k}.json")
-                                   for k in (2, 1)]):
+    cands = [path] if path else (
+        [os.path.join(ROOT, "profiles", f"traffic_r0{k}.json") for k in (2, 1)] +
+        [os.path.join(ROOT, "profiles", "r02", "apply_pmc", f"traffic_{d}.json")
+         for d in ("uniform", "zipf")])
+    for p in cands:
         try:
             tj = json.load(open(p))
         except Exception:

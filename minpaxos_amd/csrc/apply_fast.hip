@@ -50,6 +50,11 @@ namespace mpx {
 #ifndef MPX_RS_STAMP
 #define MPX_RS_STAMP 0
 #endif
+// diagnostic ablations of k_ap_scatter: 1 no partition writes, 2 no image either, 4 bin ranks
+// from ballots (match_bits) instead of the LDS peer masks
+#ifndef MPX_SC_ABL
+#define MPX_SC_ABL 0
+#endif
 
 constexpr int kTL = 4096;          // commands per log tile
 constexpr int kTT = 1024;          // threads of the tile and bin workgroups
@@ -65,6 +70,7 @@ constexpr uint32_t kSamples = 1u << 15;  // (k_ap_select divides by a shift)
 constexpr uint32_t kHotIdx = 0x8000u;  // ipos: hot command (| hot index), else image index
 constexpr uint32_t kNoSlot = ~0u;
 constexpr unsigned kScatterGrid = 256;  // persistent partition grid: one workgroup per CU
+constexpr uint32_t kScanGroups = 256;   // tile groups of the row scan (one workgroup per CU)
 
 // LDS slot state of k_ap_resolve
 constexpr uint8_t kSPresent = 1, kSLastPut = 2, kSTouched = 4, kSValDirty = 8, kSNew = 16,
@@ -529,7 +535,9 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
             bin[r] = cold[r] ? bin_of(h, g) : 0u;
             rank[r] = 0;
             if (!__ballot(cold[r])) continue;
-            const unsigned long long peers = wave_peers(W, PM, bin[r], cold[r]);
+            const unsigned long long peers = (MPX_SC_ABL & 4)
+                                                 ? match_bits(bin[r], 31 - __clz((int)g.nbin), cold[r])
+                                                 : wave_peers(W, PM, bin[r], cold[r]);
             if (cold[r]) {
                 const uint32_t base = CW[bin[r]];
                 rank[r] = base + (uint32_t)__popcll(peers & below);
@@ -573,7 +581,7 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < kTPer; ++r) {
-            if (!cold[r]) continue;
+            if (!cold[r] || (MPX_SC_ABL & 2)) continue;
             const uint32_t b = bin[r];
             const uint32_t wr = S.cw[w][b] + rank[r];
             const uint32_t ip = S.lstart[b] + wr;
@@ -586,12 +594,12 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
         __syncthreads();
         const uint32_t nc = S.ncold;
         if (tid == 0) tcold[tile] = nc;
-        for (uint32_t i = tid; i < nc; i += kTT) {
+        for (uint32_t i = tid; i < ((MPX_SC_ABL & 3) ? 0u : nc); i += kTT) {
             const uint32_t b = S.ibin[i];
             const uint32_t dst = S.roff[b] + (i - S.lstart[b]);
-            rec_kv[dst] = S.img[i];
-            rec_op[dst] = S.iop[i];
-            cpos[(uint64_t)tile * kTL + i] = dst;  // image order: emit gathers run by run
+            if (!(MPX_SC_ABL & 32)) rec_kv[dst] = S.img[i];
+            if (!(MPX_SC_ABL & 8)) rec_op[dst] = S.iop[i];
+            if (!(MPX_SC_ABL & 16)) cpos[(uint64_t)tile * kTL + i] = dst;  // image order: emit gathers run by run
         }
         for (int i = tid; i < kTW * kMaxBins / 2; i += kTT) cw32[i] = 0u;  // next tile's counts
         __syncthreads();
@@ -1153,7 +1161,7 @@ ApGeo geo_for(const KvTable& t, uint64_t n) {
     g.rowlen = g.nbin + 2 * kHMax;
     g.tiles = (uint32_t)((n + kTL - 1) / kTL);
     if (!g.tiles) g.tiles = 1;
-    g.ng = g.tiles < 128 ? g.tiles : 128;
+    g.ng = g.tiles < kScanGroups ? g.tiles : kScanGroups;
     g.tpg = (g.tiles + g.ng - 1) / g.ng;
     g.ng = (g.tiles + g.tpg - 1) / g.tpg;
     return g;
@@ -1165,7 +1173,7 @@ FastLayout fast_layout(const KvTable& t, uint64_t c) {
     FastLayout L{};
     uint64_t o = 0;
     L.rows = o; o += al((uint64_t)g.tiles * g.rowlen * 4);
-    L.part = o; o += al((uint64_t)128 * g.rowlen * 4);
+    L.part = o; o += al((uint64_t)kScanGroups * g.rowlen * 4);
     L.bin_start = o; o += al(((uint64_t)g.nbin + 1) * 4);
     L.rec_kv = o; o += al(c * 16);
     L.rec_op = o; o += al(c);
