@@ -70,7 +70,13 @@ constexpr uint32_t kSamples = 1u << 15;  // (k_ap_select divides by a shift)
 constexpr uint32_t kHotIdx = 0x8000u;  // ipos: hot command (| hot index), else image index
 constexpr uint32_t kNoSlot = ~0u;
 constexpr unsigned kScatterGrid = 256;  // persistent partition grid: one workgroup per CU
-constexpr uint32_t kScanGroups = 256;   // tile groups of the row scan (one workgroup per CU)
+constexpr uint32_t kScanGroups = 256;   // tile groups of the row scan (one workgroup per CU);
+                                        // k_ap_scan_top covers 16 x 16 of them per column
+
+static_assert(kScanGroups <= 256, "k_ap_scan_top covers 16 chunks of 16 groups per column");
+static_assert((1 << kLgHMax) == kHMax, "hot indices are matched on kLgHMax bits");
+static_assert(kTW * kHMax == kTT, "k_ap_emit clears / scans its per-wave hot tables one per thread");
+static_assert(kMaxBins <= kTT, "the bin scans take one bin per thread");
 
 // LDS slot state of k_ap_resolve
 constexpr uint8_t kSPresent = 1, kSLastPut = 2, kSTouched = 4, kSValDirty = 8, kSNew = 16,
@@ -379,40 +385,59 @@ __global__ __launch_bounds__(256) void k_ap_scan_part(ApGeo g, const uint32_t* _
     }
 }
 
+// exclusive prefix over the tile groups, 64 columns per workgroup: lane (c, k) of the 16 lanes
+// of column c holds groups [16k, 16k + 16); a 16-lane scan of the chunk sums links them
+constexpr int kTopCols = kTT / 16;
 __global__ __launch_bounds__(kTT) void k_ap_scan_top(ApGeo g, uint32_t* __restrict__ part,
-                                                     uint32_t* __restrict__ bin_start,
+                                                     uint32_t* __restrict__ ctot,
                                                      ApHot* __restrict__ hot) {
-    __shared__ uint32_t tot[kMaxBins];
-    __shared__ uint32_t wsum[kTW];
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, l = lane_id();
+    const int k = l & 15;
+    const uint32_t c = blockIdx.x * kTopCols + (uint32_t)(tid / kWave) * 4 + (uint32_t)(l >> 4);
     const uint32_t cols = g.nbin + 2 * hot->n;
-    for (uint32_t c = tid; c < g.rowlen; c += kTT) {
-        const bool sum = c < g.nbin;
-        uint32_t acc = 0;
-        for (uint32_t g0 = 0; c < cols && g0 < g.ng; g0 += 16) {  // 16 loads in flight
-            uint32_t v[16];
+    const bool sum = c < g.nbin;
+    const bool live = c < cols;
+    uint32_t v[16];
 #pragma unroll
-            for (int u = 0; u < 16; ++u)
-                v[u] = g0 + u < g.ng ? part[(uint64_t)(g0 + u) * g.rowlen + c] : 0u;
+    for (int u = 0; u < 16; ++u) {
+        const uint32_t gi = (uint32_t)k * 16 + u;
+        v[u] = live && gi < g.ng ? part[(uint64_t)gi * g.rowlen + c] : 0u;
+    }
+    uint32_t acc = 0;
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                if (g0 + u < g.ng) part[(uint64_t)(g0 + u) * g.rowlen + c] = acc;
-                acc = col_op(sum, acc, v[u]);
-            }
-        }
+    for (int u = 0; u < 16; ++u) acc = col_op(sum, acc, v[u]);
+    uint32_t x = acc;  // inclusive scan of the chunk results over the 16 lanes of the column
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (k >= d) x = col_op(sum, x, y);
+    }
+    uint32_t run = (uint32_t)__shfl_up(x, 1);
+    if (k == 0) run = 0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const uint32_t gi = (uint32_t)k * 16 + u;
+        if (live && gi < g.ng) part[(uint64_t)gi * g.rowlen + c] = run;
+        run = col_op(sum, run, v[u]);
+    }
+    if (live && k == 15) {
         if (sum) {
-            tot[c] = acc;
+            ctot[c] = x;
         } else {
             const uint32_t h = (c - g.nbin) >> 1;
-            if ((c - g.nbin) & 1) hot->fin_put[h] = acc;
-            else hot->fin_any[h] = acc;
+            if ((c - g.nbin) & 1) hot->fin_put[h] = x;
+            else hot->fin_any[h] = x;
         }
     }
-    __syncthreads();
-    // exclusive scan of the bin totals (nbin <= 1024: one per thread)
-    const uint32_t v = (uint32_t)tid < g.nbin ? tot[tid] : 0u;
+}
+
+// bin starts: exclusive scan of the bin totals (nbin <= 1024: one per thread)
+__global__ __launch_bounds__(kTT) void k_ap_scan_bins(ApGeo g, const uint32_t* __restrict__ ctot,
+                                                      uint32_t* __restrict__ bin_start) {
+    __shared__ uint32_t wsum[kTW];
+    const int tid = threadIdx.x, l = lane_id();
+    const uint32_t v = (uint32_t)tid < g.nbin ? ctot[tid] : 0u;
     uint32_t x = v;
-    const int l = lane_id();
 #pragma unroll
     for (int d = 1; d < kWave; d <<= 1) {
         const uint32_t y = __shfl_up(x, d);
@@ -422,23 +447,22 @@ __global__ __launch_bounds__(kTT) void k_ap_scan_top(ApGeo g, uint32_t* __restri
     __syncthreads();
     uint32_t wb = 0;
     for (int w2 = 0; w2 < tid / kWave; ++w2) wb += wsum[w2];
-    const uint32_t excl = wb + x - v;
     if ((uint32_t)tid < g.nbin) {
-        bin_start[tid] = excl;
-        if ((uint32_t)tid == g.nbin - 1) bin_start[g.nbin] = excl + v;
-        for (uint32_t gi = 0; gi < g.ng; ++gi) part[(uint64_t)gi * g.rowlen + tid] += excl;
+        bin_start[tid] = wb + x - v;
+        if ((uint32_t)tid == g.nbin - 1) bin_start[g.nbin] = wb + x;
     }
 }
 
 __global__ __launch_bounds__(256) void k_ap_scan_rows(ApGeo g, uint32_t* __restrict__ rows,
                                                       const uint32_t* __restrict__ part,
+                                                      const uint32_t* __restrict__ bin_start,
                                                       const ApHot* __restrict__ hot) {
     const uint32_t gi = blockIdx.x;
     const uint32_t t0 = gi * g.tpg, t1 = t0 + g.tpg < g.tiles ? t0 + g.tpg : g.tiles;
     const uint32_t cols = g.nbin + 2 * hot->n;
     for (uint32_t c = threadIdx.x; c < cols; c += 256) {
         const bool sum = c < g.nbin;
-        uint32_t acc = part[(uint64_t)gi * g.rowlen + c];
+        uint32_t acc = part[(uint64_t)gi * g.rowlen + c] + (sum ? bin_start[c] : 0u);
         uint32_t tt = t0;
         for (; tt + 8 <= t1; tt += 8) {
             uint32_t v[8];
@@ -1150,7 +1174,7 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
 // ---- launcher ---------------------------------------------------------------------------------
 namespace {
 struct FastLayout {
-    uint64_t rows, part, bin_start, rec_kv, rec_op, ipos, cpos, tcold, r_ret, r_conf, hot, total;
+    uint64_t rows, part, ctot, bin_start, rec_kv, rec_op, ipos, cpos, tcold, r_ret, r_conf, hot, total;
 };
 
 ApGeo geo_for(const KvTable& t, uint64_t n) {
@@ -1174,6 +1198,7 @@ FastLayout fast_layout(const KvTable& t, uint64_t c) {
     uint64_t o = 0;
     L.rows = o; o += al((uint64_t)g.tiles * g.rowlen * 4);
     L.part = o; o += al((uint64_t)kScanGroups * g.rowlen * 4);
+    L.ctot = o; o += al((uint64_t)g.nbin * 4);
     L.bin_start = o; o += al(((uint64_t)g.nbin + 1) * 4);
     L.rec_kv = o; o += al(c * 16);
     L.rec_op = o; o += al(c);
@@ -1229,6 +1254,7 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
     char* b = (char*)w.base;
     uint32_t* rows = (uint32_t*)(b + L.rows);
     uint32_t* part = (uint32_t*)(b + L.part);
+    uint32_t* ctot = (uint32_t*)(b + L.ctot);
     uint32_t* bin_start = (uint32_t*)(b + L.bin_start);
     int4* rec_kv = (int4*)(b + L.rec_kv);
     uint8_t* rec_op = (uint8_t*)(b + L.rec_op);
@@ -1253,8 +1279,9 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
         k_ap_select<<<1, kTT, 0, stream>>>(t, key + c0, n, hot_min, hot);
         k_ap_count<<<g.tiles, kTT, 0, stream>>>(g, op + c0, key + c0, n, rows, hot);
         k_ap_scan_part<<<g.ng, 256, 0, stream>>>(g, rows, part, hot);
-        k_ap_scan_top<<<1, kTT, 0, stream>>>(g, part, bin_start, hot);
-        k_ap_scan_rows<<<g.ng, 256, 0, stream>>>(g, rows, part, hot);
+        k_ap_scan_top<<<(g.rowlen + kTopCols - 1) / kTopCols, kTT, 0, stream>>>(g, part, ctot, hot);
+        k_ap_scan_bins<<<1, kTT, 0, stream>>>(g, ctot, bin_start);
+        k_ap_scan_rows<<<g.ng, 256, 0, stream>>>(g, rows, part, bin_start, hot);
         k_ap_scatter<<<kScatterGrid, kTT, 0, stream>>>(g, op + c0, key + c0, val + c0, n, rows, hot,
                                                   rec_kv, rec_op, ipos, cpos, tcold);
         k_ap_resolve<<<g.nbin, kTT, 0, stream>>>(g, t, bin_start, rec_kv, rec_op, r_ret, r_conf,
