@@ -101,7 +101,7 @@ def parse():
     ap.add_argument("--commands", type=int, default=1 << 26, help="apply: commands")
     ap.add_argument("--apply-keys", type=int, default=1 << 20, help="apply: key space")
     ap.add_argument("--kv-capacity", type=int, default=0,
-                    help="apply: engine key capacity (0 = 2 x --apply-keys; the table gets >= 2x slots)")
+                    help="apply: engine key capacity (0 = --apply-keys; the table gets >= 2x slots, load <= 1/2)")
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
     ap.add_argument("--replay-dups", action="store_true",
                     help="replay: instNo drawn with repeats (last record wins) instead of a permutation")
@@ -529,7 +529,7 @@ def kernel_bench(a, rk):
     import oracle_lib as OL  # CPU oracle: the checker and the CPU baseline, never the measured path
     N = 5
     mode = R.MODE_MIN if a.mode == "min" else R.MODE_CLASSIC
-    eng = Engine(rk.local, n_replicas=N, mode=mode, kv_capacity=a.kv_capacity or 2 * a.apply_keys)
+    eng = Engine(rk.local, n_replicas=N, mode=mode, kv_capacity=a.kv_capacity or a.apply_keys)
     ar = Arena(eng)
     put, get, sync = ar.put, ar.get, eng.synchronize
     lib = OL.load()
@@ -685,7 +685,8 @@ def kernel_bench(a, rk):
                "sample": f"the full workload ({M} commands over {K} keys, {a.dist}) x {reps}, "
                          f"Execute per command on an unordered_map, one thread, {secs:.1f} s timed"}
         workload = f"config4: {M} PUT/GET (p_put=0.5) over {K} keys, {a.dist}"
-        traffic = traffic_of(a.traffic_json, kernel=kernel, commands=M, dist=a.dist)
+        traffic = traffic_of(a.traffic_json, kernel=kernel, commands=M, dist=a.dist,
+                             kv_capacity=a.kv_capacity or K)
     elif a.workload == "conflict":
         M, K, Bc = a.commands, a.apply_keys, 4
         op, key, _ = synth.commands(M, K, 0.5, a.dist, seed=44)
