@@ -29,7 +29,7 @@ def load(sub, counter):
 fe, wr = load("fetch", "FETCH_SIZE"), load("write", "WRITE_SIZE")
 rows, tf, tw = [], 0.0, 0.0
 for k in sorted(set(fe) | set(wr)):
-    if "k_ap_" not in k and "k_kv_" not in k and "k_apply" not in k:
+    if "k_ap_" not in k and "k_apply" not in k:  # the call's kernels (not export / fill)
         continue
     f = statistics.median(fe.get(k, [0])) * 1024
     w = statistics.median(wr.get(k, [0])) * 1024
