@@ -245,6 +245,25 @@ def test_apply_paths(mk_engine, monkeypatch, hot_min, fallback):
         assert e.kv_size() == len(wk)
 
 
+@pytest.mark.parametrize("fallback", ["0", "1"])
+def test_apply_bucket_full(mk_engine, monkeypatch, fallback):
+    """more distinct PUT keys than a table of 4 buckets x 256 slots holds: MPX_E_KV_FULL (the
+    oracle's Go map never fills; the engine's capacity is documented in mpx.h); a call that fits
+    still matches the oracle afterwards on a fresh engine"""
+    monkeypatch.setenv("MPX_APPLY_FALLBACK", fallback)
+    e = mk_engine(5, R.MODE_MIN, kv_capacity=512)  # 1024 slots
+    keys = np.arange(1, 1501, dtype=np.int64)
+    with pytest.raises(MpxError) as ei:
+        e.apply(np.full(len(keys), R.OP_PUT, np.uint8), keys, keys * 3)
+    assert ei.value.code == R.E_KV_FULL
+    e2, o = mk_engine(5, R.MODE_MIN, kv_capacity=512), Oracle(5, R.MODE_MIN)
+    rng = np.random.default_rng(3)
+    op, key, val = gen_cases.commands_mixed(rng, 20000, 400)
+    gr, gc = e2.apply(op, key, val)
+    wr, wc = o.apply(op, key, val)
+    assert np.array_equal(gr, wr) and np.array_equal(gc, wc)
+
+
 def test_apply_large_table_fallback(mk_engine):
     """a table past the partitioned pipeline's 1024 bins (kv_capacity 4M keys: 8M slots) takes
     the sort-based pipeline; same results"""
