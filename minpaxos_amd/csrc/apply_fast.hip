@@ -11,8 +11,8 @@
 // Commands of different keys never interact, and the table (kvtab.hpp) is cut into 256-slot
 // buckets that each hold a closed set of keys. So the log is partitioned by bucket and every
 // bucket is resolved in LDS by one wave, against its own slice of the table, in log order:
-//   k_ap_select   one workgroup samples the chunk's keys; the most frequent keys seen at least
-//                 hot_min times in 32K samples (at most 63) are HOT: they skip the partition and are resolved in log order by a
+//   k_ap_sample / k_ap_select  32K of the chunk's keys are sampled into a hash of counts; the most
+//                 frequent keys seen at least hot_min times (at most 63) are HOT: they skip the partition and are resolved in log order by a
 //                 per-key max-scan (below), so a skewed key space cannot pile onto one wave.
 //                 Index 0 is always the key INT64_MIN (the table's sentinel, kept in a side slot).
 //   k_ap_count    per 4096-command log tile: commands per bin (16 buckets) of the cold keys, and
@@ -65,8 +65,7 @@ constexpr int kLgHMax = 6;
 constexpr int kHotTab = 512;       // LDS hash of the hot keys (load <= 1/8: probes stay short)
 constexpr int kMaxBins = 1024;
 constexpr int kMaxBPB = 16;        // buckets per bin = waves of the resolve workgroup
-constexpr int kSampTab = 8192;     // k_ap_select's LDS count table
-constexpr uint32_t kSamples = 1u << 15;  // (k_ap_select divides by a shift)
+constexpr uint32_t kSamples = 1u << 15;  // (k_ap_sample divides by a shift)
 constexpr uint32_t kHotIdx = 0x8000u;  // ipos: hot command (| hot index), else image index
 constexpr uint32_t kNoSlot = ~0u;
 constexpr unsigned kScatterGrid = 256;  // persistent partition grid: one workgroup per CU
@@ -77,6 +76,7 @@ static_assert(kScanGroups <= 256, "k_ap_scan_top covers 16 chunks of 16 groups p
 static_assert((1 << kLgHMax) == kHMax, "hot indices are matched on kLgHMax bits");
 static_assert(kTW * kHMax == kTT, "k_ap_emit clears / scans its per-wave hot tables one per thread");
 static_assert(kMaxBins <= kTT, "the bin scans take one bin per thread");
+static_assert(kSamples % (64 * 256) == 0, "k_ap_sample: whole samples per thread");
 
 // LDS slot state of k_ap_resolve
 constexpr uint8_t kSPresent = 1, kSLastPut = 2, kSTouched = 4, kSValDirty = 8, kSNew = 16,
@@ -202,61 +202,91 @@ __device__ __forceinline__ int hot_find(const HotLds& s, uint32_t nh, int64_t ke
     }
 }
 
-// one workgroup: sample up to 32K keys of the chunk, pick the hot ones (the most frequent keys
-// seen at least hot_min times, at most kHMax - 1 of them), read their start state
-__global__ __launch_bounds__(kTT) void k_ap_select(KvTable t, const int64_t* __restrict__ key,
-                                                   uint32_t n, uint32_t hot_min, ApHot* hot) {
-    __shared__ int64_t sk[kSampTab];
-    __shared__ uint32_t sc[kSampTab];
+// Hot-key selection, three small kernels: k_ap_sclear empties the sample table, k_ap_sample
+// counts up to 32K sampled keys of the chunk in it (64 workgroups, device-scope CAS / add; a
+// sample whose 8-slot probe window is full is dropped: frequent keys arrive early), k_ap_select
+// (one workgroup) picks the most frequent keys seen at least hot_min times (at most kHMax - 1)
+// and reads their start state
+constexpr int kGTab = 1 << 16;       // sample table slots
+constexpr unsigned kSampGrid = 64;
+
+__global__ __launch_bounds__(256) void k_ap_sclear(int64_t* __restrict__ gk,
+                                                   uint32_t* __restrict__ gc) {
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < (uint32_t)kGTab; i += gridDim.x * 256) {
+        gk[i] = kSentinel;
+        gc[i] = 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_ap_sample(const int64_t* __restrict__ key, uint32_t n,
+                                                   uint32_t hot_min, int64_t* __restrict__ gk,
+                                                   uint32_t* __restrict__ gc) {
+    if (!hot_min) return;
+    const uint32_t S = n < kSamples ? n : kSamples;
+    constexpr int kB = (int)(kSamples / (kSampGrid * 256));  // samples per thread
+    int64_t k[kB];
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+        const uint32_t i = (blockIdx.x * 256 + threadIdx.x) * kB + u;
+        const uint32_t j = S == n ? i : (uint32_t)(((uint64_t)i * n) >> 15);  // S = 2^15
+        k[u] = i < S ? key[j] : kSentinel;
+    }
+    const int l = lane_id();
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+        // lanes of the wave with the same key act once: the lowest lane of each home-slot class
+        // takes every lane whose key equals its own (a hot key is most of the samples, and
+        // device-scope atomics on one word serialise); a colliding other key acts alone
+        const bool valid = k[u] != kSentinel;
+        const uint32_t h0 = (uint32_t)hash64((uint64_t)k[u]) & (kGTab - 1);
+        const unsigned long long cls = match_bits(h0, 16, valid);
+        const int lead = valid ? lo_bit(cls) : l;
+        const int64_t lk = shfl64(k[u], lead);
+        const bool follower = valid && lead != l && lk == k[u];
+        const unsigned long long fol = __ballot(follower);
+        if (!valid || follower) continue;
+        const uint32_t cnt = lead == l ? 1u + (uint32_t)__popcll(fol & cls) : 1u;
+        uint32_t p = h0;
+        for (int probe = 0; probe < 8; ++probe, p = (p + 1) & (kGTab - 1)) {
+            // agent-scope load: a plain one can hit a stale L2 copy of an empty slot that the
+            // memory-side CAS has filled
+            unsigned long long cur =
+                __hip_atomic_load(reinterpret_cast<unsigned long long*>(&gk[p]),
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cur == (unsigned long long)kSentinel)
+                cur = atomicCAS(reinterpret_cast<unsigned long long*>(&gk[p]),
+                                (unsigned long long)kSentinel, (unsigned long long)k[u]);
+            if (cur == (unsigned long long)kSentinel || (int64_t)cur == k[u]) {
+                atomicAdd(&gc[p], cnt);
+                break;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kTT) void k_ap_select(KvTable t, const int64_t* __restrict__ gk,
+                                                   const uint32_t* __restrict__ gc,
+                                                   uint32_t hot_min, ApHot* hot) {
     __shared__ int64_t hk[kHMax];
     __shared__ uint32_t sc_hist[kTT];
     __shared__ uint32_t wsum_s[kTW];
-    __shared__ uint32_t nh, thr_s, thr;
+    __shared__ uint32_t nh, thr_s;
     const int tid = threadIdx.x;
-    for (int i = tid; i < kSampTab; i += kTT) {
-        sk[i] = kSentinel;
-        sc[i] = 0;
-    }
+    constexpr int kPer = kGTab / kTT;
     if (tid == 0) nh = 1;
-    __syncthreads();
-    const uint32_t S = n < kSamples ? n : kSamples;
     if (hot_min) {
-        constexpr int kB = 8;  // loads in flight per thread
-        for (uint32_t i0 = tid; i0 < S; i0 += kTT * kB) {
-            int64_t k[kB];
+        uint32_t c[kPer];
 #pragma unroll
-            for (int u = 0; u < kB; ++u) {
-                const uint32_t i = i0 + u * kTT;
-                const uint32_t j = S == n ? i : (uint32_t)(((uint64_t)i * n) >> 15);  // S = 2^15
-                k[u] = i < S ? key[j] : kSentinel;
-            }
-#pragma unroll
-            for (int u = 0; u < kB; ++u) {
-                if (k[u] == kSentinel) continue;
-                // frequent keys arrive early; once the probe window is full a sample is dropped
-                uint32_t p = (uint32_t)hash64((uint64_t)k[u]) & (kSampTab - 1);
-                for (int probe = 0; probe < 4; ++probe, p = (p + 1) & (kSampTab - 1)) {
-                    int64_t cur = sk[p];
-                    if (cur == kSentinel)
-                        cur = (int64_t)atomicCAS(reinterpret_cast<unsigned long long*>(&sk[p]),
-                                                 (unsigned long long)kSentinel,
-                                                 (unsigned long long)k[u]);
-                    if (cur == kSentinel || cur == k[u]) {
-                        atomicAdd(&sc[p], 1u);
-                        break;
-                    }
-                }
-            }
-        }
-        __syncthreads();
+        for (int u = 0; u < kPer; ++u) c[u] = gc[u * kTT + tid];
         // the smallest threshold >= hot_min that leaves at most kHMax - 1 keys: a histogram of
         // the counts (capped at kTT - 1; more than kHMax - 1 keys cannot reach that), then a
         // suffix sum over it
         sc_hist[tid] = 0;
         if (tid == 0) thr_s = kTT;
         __syncthreads();
-        for (int i = tid; i < kSampTab; i += kTT)
-            if (sc[i]) atomicAdd(&sc_hist[sc[i] < (uint32_t)kTT ? sc[i] : kTT - 1], 1u);
+#pragma unroll
+        for (int u = 0; u < kPer; ++u)  // counts below hot_min never decide the threshold
+            if (c[u] >= hot_min) atomicAdd(&sc_hist[c[u] < (uint32_t)kTT ? c[u] : kTT - 1], 1u);
         __syncthreads();
         {
             // inclusive suffix sum: reverse the index, scan forward
@@ -276,16 +306,15 @@ __global__ __launch_bounds__(kTT) void k_ap_select(KvTable t, const int64_t* __r
             if ((uint32_t)ri >= hot_min && ge <= (uint32_t)kHMax - 1) atomicMin(&thr_s, (uint32_t)ri);
         }
         __syncthreads();
-        const uint32_t lo = thr_s;
-        if (tid == 0) thr = lo;
-        __syncthreads();
-        for (int i = tid; i < kSampTab; i += kTT)
-            if (sc[i] >= thr) {
+        const uint32_t thr = thr_s;
+#pragma unroll
+        for (int u = 0; u < kPer; ++u)
+            if (c[u] >= thr) {
                 const uint32_t x = atomicAdd(&nh, 1u);
-                if (x < kHMax) hk[x] = sk[i];
+                if (x < kHMax) hk[x] = gk[u * kTT + tid];
             }
-        __syncthreads();
     }
+    __syncthreads();
     const uint32_t H = nh < (uint32_t)kHMax ? nh : (uint32_t)kHMax;
     if (tid == 0) {
         hot->n = H;
@@ -1174,7 +1203,7 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
 // ---- launcher ---------------------------------------------------------------------------------
 namespace {
 struct FastLayout {
-    uint64_t rows, part, ctot, bin_start, rec_kv, rec_op, ipos, cpos, tcold, r_ret, r_conf, hot, total;
+    uint64_t gk, gc, rows, part, ctot, bin_start, rec_kv, rec_op, ipos, cpos, tcold, r_ret, r_conf, hot, total;
 };
 
 ApGeo geo_for(const KvTable& t, uint64_t n) {
@@ -1196,6 +1225,8 @@ FastLayout fast_layout(const KvTable& t, uint64_t c) {
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
     FastLayout L{};
     uint64_t o = 0;
+    L.gk = o; o += al((uint64_t)kGTab * 8);
+    L.gc = o; o += al((uint64_t)kGTab * 4);
     L.rows = o; o += al((uint64_t)g.tiles * g.rowlen * 4);
     L.part = o; o += al((uint64_t)kScanGroups * g.rowlen * 4);
     L.ctot = o; o += al((uint64_t)g.nbin * 4);
@@ -1252,6 +1283,8 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
     const FastLayout L = fast_layout(t, C);
     if (w.bytes < L.total) return hipErrorInvalidValue;
     char* b = (char*)w.base;
+    int64_t* gk = (int64_t*)(b + L.gk);
+    uint32_t* gc = (uint32_t*)(b + L.gc);
     uint32_t* rows = (uint32_t*)(b + L.rows);
     uint32_t* part = (uint32_t*)(b + L.part);
     uint32_t* ctot = (uint32_t*)(b + L.ctot);
@@ -1276,7 +1309,11 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
     for (uint64_t c0 = 0; c0 < m; c0 += C) {
         const uint32_t n = (uint32_t)(m - c0 < C ? m - c0 : C);
         const ApGeo g = geo_for(t, n);
-        k_ap_select<<<1, kTT, 0, stream>>>(t, key + c0, n, hot_min, hot);
+        if (hot_min) {
+            k_ap_sclear<<<kSampGrid, 256, 0, stream>>>(gk, gc);
+            k_ap_sample<<<kSampGrid, 256, 0, stream>>>(key + c0, n, hot_min, gk, gc);
+        }
+        k_ap_select<<<1, kTT, 0, stream>>>(t, gk, gc, hot_min, hot);
         k_ap_count<<<g.tiles, kTT, 0, stream>>>(g, op + c0, key + c0, n, rows, hot);
         k_ap_scan_part<<<g.ng, 256, 0, stream>>>(g, rows, part, hot);
         k_ap_scan_top<<<(g.rowlen + kTopCols - 1) / kTopCols, kTT, 0, stream>>>(g, part, ctot, hot);
