@@ -726,13 +726,17 @@ __device__ __forceinline__ RoundA resolve_stage_a(ResolveLds& S, int b, uint32_t
     int s = -1;
     uint32_t p = home_of(hash64((uint64_t)k));
     if (a.live) {
-        for (int step = 0; step < kSB / 4; ++step) {
-            int64_t c[4];
+#ifndef MPX_RS_PROBE
+#define MPX_RS_PROBE 8
+#endif
+        constexpr int kPS = MPX_RS_PROBE;  // slots per probe step
+        for (int step = 0; step < kSB / kPS; ++step) {
+            int64_t c[kPS];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) c[u] = T[(p + u) & (kSB - 1)];
+            for (int u = 0; u < kPS; ++u) c[u] = T[(p + u) & (kSB - 1)];
             int hit = -1, stop = -1;
 #pragma unroll
-            for (int u = 3; u >= 0; --u) {
+            for (int u = kPS - 1; u >= 0; --u) {
                 if (c[u] == k) hit = u;
                 if (c[u] == kSentinel) stop = u;
             }
@@ -744,7 +748,7 @@ __device__ __forceinline__ RoundA resolve_stage_a(ResolveLds& S, int b, uint32_t
                 p = (p + stop) & (kSB - 1);  // the first empty slot: an insert starts here
                 break;
             }
-            p = (p + 4) & (kSB - 1);
+            p = (p + kPS) & (kSB - 1);
         }
     }
     if (a.live && s < 0 && a.isput) {  // a key new to the table: claim a slot
