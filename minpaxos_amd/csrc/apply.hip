@@ -540,10 +540,10 @@ bool use_fast(const KvTable& t) {
     const char* f = getenv("MPX_APPLY_FALLBACK");
     return apply_fast_ok(t) && !(f && f[0] == '1');
 }
-// env MPX_APPLY_HOT_MIN: sample count (of 32K) that makes a key hot; 0 = no hot keys
+// env MPX_APPLY_HOT_MIN: sample count (of 64K) that makes a key hot; 0 = no hot keys
 uint32_t hot_min() {
     const char* h = getenv("MPX_APPLY_HOT_MIN");
-    return h ? (uint32_t)strtoul(h, nullptr, 10) : 4u;
+    return h ? (uint32_t)strtoul(h, nullptr, 10) : 5u;
 }
 }  // namespace
 

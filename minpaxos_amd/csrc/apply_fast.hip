@@ -11,8 +11,8 @@
 // Commands of different keys never interact, and the table (kvtab.hpp) is cut into 256-slot
 // buckets that each hold a closed set of keys. So the log is partitioned by bucket and every
 // bucket is resolved in LDS by one wave, against its own slice of the table, in log order:
-//   k_ap_sample / k_ap_select  32K of the chunk's keys are sampled into a hash of counts; the most
-//                 frequent keys seen at least hot_min times (at most 63) are HOT: they skip the partition and are resolved in log order by a
+//   k_ap_sample / k_ap_select  64K of the chunk's keys are sampled into a hash of counts; the
+//                 most frequent keys seen at least hot_min times (at most 127) are HOT: they skip the partition and are resolved in log order by a
 //                 per-key max-scan (below), so a skewed key space cannot pile onto one wave.
 //                 Index 0 is always the key INT64_MIN (the table's sentinel, kept in a side slot).
 //   k_ap_count    per 4096-command log tile: commands per bin (16 buckets) of the cold keys, and
@@ -60,12 +60,13 @@ constexpr int kTL = 4096;          // commands per log tile
 constexpr int kTT = 1024;          // threads of the tile and bin workgroups
 constexpr int kTW = kTT / kWave;   // 16 waves
 constexpr int kTPer = kTL / kTT;   // 4 commands per thread; wave w owns [256 w, 256 w + 256)
-constexpr int kHMax = 64;          // hot keys per chunk, index 0 = INT64_MIN
-constexpr int kLgHMax = 6;
+constexpr int kHMax = 128;         // hot keys per chunk, index 0 = INT64_MIN
+constexpr int kLgHMax = 7;
 constexpr int kHotTab = 512;       // LDS hash of the hot keys (load <= 1/8: probes stay short)
 constexpr int kMaxBins = 1024;
 constexpr int kMaxBPB = 16;        // buckets per bin = waves of the resolve workgroup
-constexpr uint32_t kSamples = 1u << 15;  // (k_ap_sample divides by a shift)
+constexpr int kLgSamples = 16;
+constexpr uint32_t kSamples = 1u << kLgSamples;  // (k_ap_sample divides by a shift)
 constexpr uint32_t kHotIdx = 0x8000u;  // ipos: hot command (| hot index), else image index
 constexpr uint32_t kNoSlot = ~0u;
 constexpr unsigned kScatterGrid = 256;  // persistent partition grid: one workgroup per CU
@@ -74,9 +75,10 @@ constexpr uint32_t kScanGroups = 256;   // tile groups of the row scan (one work
 
 static_assert(kScanGroups <= 256, "k_ap_scan_top covers 16 chunks of 16 groups per column");
 static_assert((1 << kLgHMax) == kHMax, "hot indices are matched on kLgHMax bits");
-static_assert(kTW * kHMax == kTT, "k_ap_emit clears / scans its per-wave hot tables one per thread");
+static_assert((kTW * kHMax) % kTT == 0, "k_ap_emit clears / scans its per-wave hot tables");
 static_assert(kMaxBins <= kTT, "the bin scans take one bin per thread");
 static_assert(kSamples % (64 * 256) == 0, "k_ap_sample: whole samples per thread");
+static_assert((1 << 17) % (16 * kTT) == 0, "k_ap_select reads the sample table 16 counts per thread at a time");
 
 // LDS slot state of k_ap_resolve
 constexpr uint8_t kSPresent = 1, kSLastPut = 2, kSTouched = 4, kSValDirty = 8, kSNew = 16,
@@ -203,11 +205,11 @@ __device__ __forceinline__ int hot_find(const HotLds& s, uint32_t nh, int64_t ke
 }
 
 // Hot-key selection, three small kernels: k_ap_sclear empties the sample table, k_ap_sample
-// counts up to 32K sampled keys of the chunk in it (64 workgroups, device-scope CAS / add; a
-// sample whose 8-slot probe window is full is dropped: frequent keys arrive early), k_ap_select
+// counts up to 64K sampled keys of the chunk in it (64 workgroups, device-scope CAS / add; a
+// sample whose 4-slot probe window is full is dropped: frequent keys arrive early), k_ap_select
 // (one workgroup) picks the most frequent keys seen at least hot_min times (at most kHMax - 1)
 // and reads their start state
-constexpr int kGTab = 1 << 16;       // sample table slots
+constexpr int kGTab = 1 << 17;       // sample table slots
 constexpr unsigned kSampGrid = 64;
 
 __global__ __launch_bounds__(256) void k_ap_sclear(int64_t* __restrict__ gk,
@@ -228,7 +230,7 @@ __global__ __launch_bounds__(256) void k_ap_sample(const int64_t* __restrict__ k
 #pragma unroll
     for (int u = 0; u < kB; ++u) {
         const uint32_t i = (blockIdx.x * 256 + threadIdx.x) * kB + u;
-        const uint32_t j = S == n ? i : (uint32_t)(((uint64_t)i * n) >> 15);  // S = 2^15
+        const uint32_t j = S == n ? i : (uint32_t)(((uint64_t)i * n) >> kLgSamples);
         k[u] = i < S ? key[j] : kSentinel;
     }
     const int l = lane_id();
@@ -247,7 +249,7 @@ __global__ __launch_bounds__(256) void k_ap_sample(const int64_t* __restrict__ k
         if (!valid || follower) continue;
         const uint32_t cnt = lead == l ? 1u + (uint32_t)__popcll(fol & cls) : 1u;
         uint32_t p = h0;
-        for (int probe = 0; probe < 8; ++probe, p = (p + 1) & (kGTab - 1)) {
+        for (int probe = 0; probe < 4; ++probe, p = (p + 1) & (kGTab - 1)) {
             // agent-scope load: a plain one can hit a stale L2 copy of an empty slot that the
             // memory-side CAS has filled
             unsigned long long cur =
@@ -275,18 +277,21 @@ __global__ __launch_bounds__(kTT) void k_ap_select(KvTable t, const int64_t* __r
     constexpr int kPer = kGTab / kTT;
     if (tid == 0) nh = 1;
     if (hot_min) {
-        uint32_t c[kPer];
-#pragma unroll
-        for (int u = 0; u < kPer; ++u) c[u] = gc[u * kTT + tid];
         // the smallest threshold >= hot_min that leaves at most kHMax - 1 keys: a histogram of
         // the counts (capped at kTT - 1; more than kHMax - 1 keys cannot reach that), then a
         // suffix sum over it
         sc_hist[tid] = 0;
         if (tid == 0) thr_s = kTT;
         __syncthreads();
+#pragma unroll 1
+        for (int u0 = 0; u0 < kPer; u0 += 16) {  // two passes over the counts (L2): 16 loads in flight
+            uint32_t c[16];
 #pragma unroll
-        for (int u = 0; u < kPer; ++u)  // counts below hot_min never decide the threshold
-            if (c[u] >= hot_min) atomicAdd(&sc_hist[c[u] < (uint32_t)kTT ? c[u] : kTT - 1], 1u);
+            for (int u = 0; u < 16; ++u) c[u] = gc[(u0 + u) * kTT + tid];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)  // counts below hot_min never decide the threshold
+                if (c[u] >= hot_min) atomicAdd(&sc_hist[c[u] < (uint32_t)kTT ? c[u] : kTT - 1], 1u);
+        }
         __syncthreads();
         {
             // inclusive suffix sum: reverse the index, scan forward
@@ -307,12 +312,18 @@ __global__ __launch_bounds__(kTT) void k_ap_select(KvTable t, const int64_t* __r
         }
         __syncthreads();
         const uint32_t thr = thr_s;
+#pragma unroll 1
+        for (int u0 = 0; u0 < kPer; u0 += 16) {
+            uint32_t c[16];
 #pragma unroll
-        for (int u = 0; u < kPer; ++u)
-            if (c[u] >= thr) {
-                const uint32_t x = atomicAdd(&nh, 1u);
-                if (x < kHMax) hk[x] = gk[u * kTT + tid];
-            }
+            for (int u = 0; u < 16; ++u) c[u] = gc[(u0 + u) * kTT + tid];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (c[u] >= thr) {
+                    const uint32_t x = atomicAdd(&nh, 1u);
+                    if (x < kHMax) hk[x] = gk[(u0 + u) * kTT + tid];
+                }
+        }
     }
     __syncthreads();
     const uint32_t H = nh < (uint32_t)kHMax ? nh : (uint32_t)kHMax;
@@ -1084,7 +1095,7 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
                                                  uint8_t* __restrict__ conf) {
     __shared__ EmitLds S;
     const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
-    reinterpret_cast<uint2*>(&S.T[0][0])[tid] = make_uint2(0u, 0u);  // kTW * kHMax == kTT
+    for (int i = l; i < kHMax; i += kWave) S.T[w][i] = make_uint2(0u, 0u);  // own row: no barrier
     const uint32_t tile = xcd_tile(g.tiles);
     if (tid < kHMax) {
         const uint32_t* row = rows + (uint64_t)tile * g.rowlen + g.nbin;
@@ -1163,9 +1174,12 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
             }
         }
     }
-    __syncthreads();
-    {
-        const int ww = tid / kHMax, hh = tid % kHMax;
+    bool mine = false;  // any hot command among this thread's
+#pragma unroll
+    for (int r = 0; r < kTPer; ++r) mine |= jw + r * kWave + l < n && (p[r] & kHotIdx);
+    if (!__syncthreads_or(mine)) goto emit_out;  // also publishes the staged cold results
+    for (int i = tid; i < kTW * kHMax; i += kTT) {
+        const int ww = i / kHMax, hh = i % kHMax;
         uint2 m = make_uint2(0u, 0u);
         for (int w2 = 0; w2 < ww; ++w2) {
             const uint2 x = S.T[w2][hh];
@@ -1175,6 +1189,7 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
         S.TP[ww][hh] = m;
     }
     __syncthreads();
+emit_out:
 #pragma unroll
     for (int r = 0; r < kTPer; ++r) {
         const uint32_t j = jw + r * kWave + l;
