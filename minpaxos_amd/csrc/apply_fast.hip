@@ -11,27 +11,30 @@
 // Commands of different keys never interact, and the table (kvtab.hpp) is cut into 256-slot
 // buckets that each hold a closed set of keys. So the log is partitioned by bucket and every
 // bucket is resolved in LDS by one wave, against its own slice of the table, in log order:
-//   k_ap_sample / k_ap_select  64K of the chunk's keys are sampled into a hash of counts; the
-//                 most frequent keys seen at least hot_min times (at most 127) are HOT: they skip the partition and are resolved in log order by a
-//                 per-key max-scan (below), so a skewed key space cannot pile onto one wave.
-//                 Index 0 is always the key INT64_MIN (the table's sentinel, kept in a side slot).
+//   k_ap_sclear / k_ap_sample / k_ap_select  64K of the chunk's keys are sampled into a hash of
+//                 counts; the most frequent keys seen at least hot_min times (at most 127) are HOT:
+//                 they skip the partition and are resolved in log order by a per-key max-scan
+//                 (below), so a skewed key space cannot pile onto one wave. Index 0 is always the
+//                 key INT64_MIN (the table's sentinel, kept in a side slot).
 //   k_ap_count    per 4096-command log tile: commands per bin (16 buckets) of the cold keys, and
 //                 per hot key the last position of any command and of a PUT in the tile
-//   scans         3-kernel scan of the tile rows: bin offsets per tile (sum), hot positions
-//                 before each tile (max)
-//   k_ap_scatter  per tile: a stable per-bin ranking (per-wave peer masks + wave prefix), the
+//   scans         k_ap_scan_part / _top / _bins / _rows over the tile rows: bin offsets per tile
+//                 (sums), hot positions before each tile (maxima)
+//   k_ap_scatter  persistent (one workgroup per CU, XCD-contiguous tiles, the next tile
+//                 prefetched): a stable per-bin ranking (per-wave peer masks + wave prefix), the
 //                 tile's cold commands as a bin-sorted image in LDS, copied out as one contiguous
 //                 run per bin (16-byte key/value records + op bytes); per command its index in
-//                 the tile image (ipos, log order), per image position its partition position (cpos)
+//                 the tile image (ipos, log order), per image position its partition slot (cpos)
 //   k_ap_resolve  one workgroup per bin: its 16 bucket tables in LDS (keys, values, state), the
-//                 bin's records streamed in log order 1024 at a time, ranked by bucket, each
-//                 bucket's records resolved by its wave 64 at a time (peer masks within the 64, the
-//                 bucket table between rounds); results land at the record's partition position;
-//                 touched slots written back once
+//                 bin's records streamed in log order 3072 at a time (the next batch prefetched),
+//                 staged in bucket order, each bucket's records resolved by its wave 64 at a time
+//                 (peer masks within the 64, the bucket table between rounds); results land at
+//                 the record's partition slot; touched slots written back once
 //   k_ap_hot_commit  the hot keys' final value and state
 //   k_ap_emit     per tile, log order: the tile's cold results gathered run by run into an LDS
-//                 image (cpos), read back by ipos; a hot command's from the per-wave peer scan, the earlier waves'
-//                 tables and the tile's incoming positions; ret / conf stored coalesced
+//                 image (cpos), read back by ipos; a hot command's from the per-wave peer scan,
+//                 the earlier waves' tables and the tile's incoming positions; ret / conf stored
+//                 coalesced
 // Table traffic is one read and one write of each bin's slice per call instead of one random probe
 // per command. New keys: a bin whose records both PUT a key absent from the table and GET (or
 // run another op on) an absent key re-runs in two passes (insert every PUT key, then resolve), so
