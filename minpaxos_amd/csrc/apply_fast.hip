@@ -865,6 +865,7 @@ __global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
     const uint64_t gbase = (uint64_t)bin * nslot;
     const uint32_t ep = t.epoch[0];
     const uint32_t r0 = bin_start[bin], r1 = bin_start[bin + 1];
+    if (r0 == r1) return;  // no records: nothing read, nothing touched (small calls, hot-heavy chunks)
     const unsigned long long below = (1ull << l) - 1ull;
     auto load_tables = [&]() {
         for (uint32_t i = tid; i < nslot; i += kTT) {
