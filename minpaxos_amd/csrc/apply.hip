@@ -40,6 +40,7 @@
 // command (2), one per PUT (1) and one value gather per GET (8), all reads. Chunks only bound
 // the scratch memory.
 // Steps 3, 5 and 7 use rocPRIM device primitives (stable LSD radix sort, look-back scan_by_key).
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -535,11 +536,21 @@ uint64_t apply_chunk_commands(uint64_t chunk, uint64_t m) {
 }
 
 namespace {
-// env MPX_APPLY_FALLBACK=1: the sort-based pipeline even where the partitioned one applies (A/B)
-bool use_fast(const KvTable& t) {
+// Which pipeline runs a call of m commands. The partitioned pipeline has a fixed cost of about a
+// dozen dependent launches plus a pass over every bin that received records, so calls below
+// MPX_APPLY_FAST_MIN commands (default kFastMinDefault, the measured crossover) take the sort-based
+// one. env MPX_APPLY_FALLBACK=1 forces the sort-based pipeline, =0 the partitioned one (where the
+// table geometry allows it) at any size; unset = by size. Both give identical results.
+constexpr uint64_t kFastMinDefault = 16384;
+uint64_t fast_min(const KvTable& t) {  // calls of at least this many commands run partitioned
+    if (!apply_fast_ok(t)) return UINT64_MAX;
     const char* f = getenv("MPX_APPLY_FALLBACK");
-    return apply_fast_ok(t) && !(f && f[0] == '1');
+    if (f && f[0] == '1') return UINT64_MAX;
+    if (f && f[0] == '0') return 0;
+    const char* n = getenv("MPX_APPLY_FAST_MIN");
+    return n ? strtoull(n, nullptr, 10) : kFastMinDefault;
 }
+bool use_fast(const KvTable& t, uint64_t m) { return m >= fast_min(t); }
 // env MPX_APPLY_HOT_MIN: sample count (of 64K) that makes a key hot; 0 = no hot keys
 uint32_t hot_min() {
     const char* h = getenv("MPX_APPLY_HOT_MIN");
@@ -549,7 +560,14 @@ uint32_t hot_min() {
 
 uint64_t apply_work_bytes(const KvTable& t, uint64_t chunk, uint64_t m) {
     const uint64_t C = apply_chunk_commands(chunk, m);
-    return use_fast(t) ? apply_fast_work_bytes(t, C) : layout(C).total;
+    return use_fast(t, m) ? apply_fast_work_bytes(t, C) : layout(C).total;
+}
+
+// Every m <= max_m must fit: each pipeline's need grows with m, so the largest call on either
+// side of the size switch bounds them all.
+uint64_t apply_reserve_bytes(const KvTable& t, uint64_t chunk, uint64_t max_m) {
+    const uint64_t b = apply_work_bytes(t, chunk, max_m), thr = fast_min(t);
+    return thr > 1 && thr <= max_m ? std::max(b, apply_work_bytes(t, chunk, thr - 1)) : b;
 }
 
 hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
@@ -557,7 +575,7 @@ hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const
                         uint32_t* err, hipStream_t stream) {
     if (!m) return hipSuccess;
     const uint64_t C = apply_chunk_commands(chunk, m);
-    if (use_fast(t))
+    if (use_fast(t, m))
         return launch_apply_fast(t, op, key, val, m, ret, conf, C, w, hot_min(), err, stream);
     // result codes carry a chunk index or a slot in 29 bits
     if (C > kPayloadMask || t.cap + 1 > kPayloadMask) return hipErrorInvalidValue;

@@ -211,13 +211,22 @@ __device__ __forceinline__ int hot_find(const HotLds& s, uint32_t nh, int64_t ke
 // counts up to 64K sampled keys of the chunk in it (64 workgroups, device-scope CAS / add; a
 // sample whose 4-slot probe window is full is dropped: frequent keys arrive early), k_ap_select
 // (one workgroup) picks the most frequent keys seen at least hot_min times (at most kHMax - 1)
-// and reads their start state
-constexpr int kGTab = 1 << 17;       // sample table slots
+// and reads their start state. The table has 2x as many slots as the chunk has samples (a power
+// of two, at least kGTabMin: select reads it in 16 columns of kTT), so small chunks scan less
+constexpr int kGTab = 1 << 17;       // sample table slots, largest
+constexpr int kGTabMin = 16 * 1024;  // smallest (kTT threads x 16 loads)
 constexpr unsigned kSampGrid = 64;
+static_assert(kGTab >= 2 * (int)kSamples && kGTabMin % (16 * 1024) == 0, "sample table sizing");
+inline uint32_t gtab_for(uint32_t n) {
+    const uint32_t S = n < kSamples ? n : kSamples;
+    uint32_t tab = kGTabMin;
+    while (tab < 2 * S) tab <<= 1;
+    return tab;
+}
 
 __global__ __launch_bounds__(256) void k_ap_sclear(int64_t* __restrict__ gk,
-                                                   uint32_t* __restrict__ gc) {
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < (uint32_t)kGTab; i += gridDim.x * 256) {
+                                                   uint32_t* __restrict__ gc, uint32_t tab) {
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < tab; i += gridDim.x * 256) {
         gk[i] = kSentinel;
         gc[i] = 0;
     }
@@ -225,8 +234,9 @@ __global__ __launch_bounds__(256) void k_ap_sclear(int64_t* __restrict__ gk,
 
 __global__ __launch_bounds__(256) void k_ap_sample(const int64_t* __restrict__ key, uint32_t n,
                                                    uint32_t hot_min, int64_t* __restrict__ gk,
-                                                   uint32_t* __restrict__ gc) {
+                                                   uint32_t* __restrict__ gc, uint32_t tab) {
     if (!hot_min) return;
+    const uint32_t tmask = tab - 1;
     const uint32_t S = n < kSamples ? n : kSamples;
     constexpr int kB = (int)(kSamples / (kSampGrid * 256));  // samples per thread
     int64_t k[kB];
@@ -243,7 +253,7 @@ __global__ __launch_bounds__(256) void k_ap_sample(const int64_t* __restrict__ k
         // takes every lane whose key equals its own (a hot key is most of the samples, and
         // device-scope atomics on one word serialise); a colliding other key acts alone
         const bool valid = k[u] != kSentinel;
-        const uint32_t h0 = (uint32_t)hash64((uint64_t)k[u]) & (kGTab - 1);
+        const uint32_t h0 = (uint32_t)hash64((uint64_t)k[u]) & tmask;
         const unsigned long long cls = match_bits(h0, 16, valid);
         const int lead = valid ? lo_bit(cls) : l;
         const int64_t lk = shfl64(k[u], lead);
@@ -252,7 +262,7 @@ __global__ __launch_bounds__(256) void k_ap_sample(const int64_t* __restrict__ k
         if (!valid || follower) continue;
         const uint32_t cnt = lead == l ? 1u + (uint32_t)__popcll(fol & cls) : 1u;
         uint32_t p = h0;
-        for (int probe = 0; probe < 4; ++probe, p = (p + 1) & (kGTab - 1)) {
+        for (int probe = 0; probe < 4; ++probe, p = (p + 1) & tmask) {
             // agent-scope load: a plain one can hit a stale L2 copy of an empty slot that the
             // memory-side CAS has filled
             unsigned long long cur =
@@ -271,13 +281,13 @@ __global__ __launch_bounds__(256) void k_ap_sample(const int64_t* __restrict__ k
 
 __global__ __launch_bounds__(kTT) void k_ap_select(KvTable t, const int64_t* __restrict__ gk,
                                                    const uint32_t* __restrict__ gc,
-                                                   uint32_t hot_min, ApHot* hot) {
+                                                   uint32_t hot_min, uint32_t tab, ApHot* hot) {
     __shared__ int64_t hk[kHMax];
     __shared__ uint32_t sc_hist[kTT];
     __shared__ uint32_t wsum_s[kTW];
     __shared__ uint32_t nh, thr_s;
     const int tid = threadIdx.x;
-    constexpr int kPer = kGTab / kTT;
+    const int kPer = (int)(tab / kTT);  // a multiple of 16
     if (tid == 0) nh = 1;
     if (hot_min) {
         // the smallest threshold >= hot_min that leaves at most kHMax - 1 keys: a histogram of
@@ -1332,11 +1342,12 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
     for (uint64_t c0 = 0; c0 < m; c0 += C) {
         const uint32_t n = (uint32_t)(m - c0 < C ? m - c0 : C);
         const ApGeo g = geo_for(t, n);
+        const uint32_t tab = gtab_for(n);
         if (hot_min) {
-            k_ap_sclear<<<kSampGrid, 256, 0, stream>>>(gk, gc);
-            k_ap_sample<<<kSampGrid, 256, 0, stream>>>(key + c0, n, hot_min, gk, gc);
+            k_ap_sclear<<<kSampGrid, 256, 0, stream>>>(gk, gc, tab);
+            k_ap_sample<<<kSampGrid, 256, 0, stream>>>(key + c0, n, hot_min, gk, gc, tab);
         }
-        k_ap_select<<<1, kTT, 0, stream>>>(t, gk, gc, hot_min, hot);
+        k_ap_select<<<1, kTT, 0, stream>>>(t, gk, gc, hot_min, tab, hot);
         k_ap_count<<<g.tiles, kTT, 0, stream>>>(g, op + c0, key + c0, n, rows, hot);
         k_ap_scan_part<<<g.ng, 256, 0, stream>>>(g, rows, part, hot);
         k_ap_scan_top<<<(g.rowlen + kTopCols - 1) / kTopCols, kTT, 0, stream>>>(g, part, ctot, hot);

@@ -464,7 +464,7 @@ int mpx_apply_reserve(mpx_engine* e, size_t max_cmds) {
     if (max_cmds >= (1ull << 31)) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 commands");
     CK(begin(e));
     CK(ensure_kv(e));
-    GROW(e, e->apply_work, mpx::apply_work_bytes(e->kv, e->apply_chunk, max_cmds));
+    GROW(e, e->apply_work, mpx::apply_reserve_bytes(e->kv, e->apply_chunk, max_cmds));
     return finish(e);
 }
 

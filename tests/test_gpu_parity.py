@@ -264,6 +264,36 @@ def test_apply_bucket_full(mk_engine, monkeypatch, fallback):
     assert np.array_equal(gr, wr) and np.array_equal(gc, wc)
 
 
+def test_apply_size_dispatch(mk_engine, monkeypatch):
+    """with MPX_APPLY_FALLBACK unset the call size picks the pipeline (MPX_APPLY_FAST_MIN, here
+    10000 commands): calls on both sides of the switch carry one table, bit-exact. The
+    device-pointer entry point reserved for the largest call also runs the smaller calls, which
+    take the other pipeline with its own scratch layout (mpx_apply_reserve covers both)"""
+    from minpaxos_amd.devbuf import Arena
+    monkeypatch.delenv("MPX_APPLY_FALLBACK", raising=False)
+    monkeypatch.setenv("MPX_APPLY_FAST_MIN", "10000")
+    rng = np.random.default_rng(57)
+    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 16), Oracle(5, R.MODE_MIN)
+    sizes = [40000, 9999, 10000, 37, 25000, 1]
+    e.apply_reserve(max(sizes))
+    with Arena(e) as ar:
+        for i, m in enumerate(sizes):
+            op, key, val = gen_cases.commands_mixed(rng, m, 3000)
+            if i % 2:
+                gr, gc = e.apply(op, key, val)
+            else:
+                d_op, d_key, d_val = ar.put(op), ar.put(key), ar.put(val)
+                d_ret, d_conf = ar.empty(m, np.int64), ar.empty(m, np.uint8)
+                e.apply_dev(d_op.ptr, d_key.ptr, d_val.ptr, m, d_ret.ptr, d_conf.ptr, e.stream)
+                e.stream_synchronize(e.stream)
+                gr, gc = ar.get(d_ret), ar.get(d_conf)
+            wr, wc = o.apply(op, key, val)
+            assert np.array_equal(gr, wr) and np.array_equal(gc, wc), m
+    gk, gv = e.kv_export()
+    wk, wv = o.kv_export()
+    assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
+
+
 def test_apply_large_table_fallback(mk_engine):
     """a table past the partitioned pipeline's 1024 bins (kv_capacity 4M keys: 8M slots) takes
     the sort-based pipeline; same results"""
