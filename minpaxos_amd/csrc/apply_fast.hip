@@ -67,7 +67,15 @@ constexpr int kHMax = 128;         // hot keys per chunk, index 0 = INT64_MIN
 constexpr int kLgHMax = 7;
 constexpr int kHotTab = 512;       // LDS hash of the hot keys (load <= 1/8: probes stay short)
 constexpr int kMaxBins = 1024;
-constexpr int kMaxBPB = 16;        // buckets per bin = waves of the resolve workgroup
+// buckets per bin = waves of the resolve workgroup (MPX_RS_LGBPB: 3 = 8-wave workgroups of half
+// the LDS, two per CU; 4 = 16 waves, one per CU)
+#ifndef MPX_RS_LGBPB
+#define MPX_RS_LGBPB 4
+#endif
+constexpr int kLgMaxBPB = MPX_RS_LGBPB;
+constexpr int kMaxBPB = 1 << kLgMaxBPB;
+constexpr int kRTT = kMaxBPB * kWave;  // threads of the resolve workgroup
+constexpr int kRTW = kMaxBPB;
 constexpr int kLgSamples = 16;
 constexpr uint32_t kSamples = 1u << kLgSamples;  // (k_ap_sample divides by a shift)
 constexpr uint32_t kHotIdx = 0x8000u;  // ipos: hot command (| hot index), else image index
@@ -692,21 +700,21 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
 
 // ---- per-bin resolve ------------------------------------------------------------------------------
 constexpr int kRH = 3;             // records per thread per resolve batch
-constexpr int kRT = kTT * kRH;     // 3072 records per batch
+constexpr int kRT = kRTT * kRH;    // records per batch (3072 at 16 buckets per bin)
 struct ResolveLds {
     int64_t tk[kMaxBPB * kSB];
     int64_t tv[kMaxBPB * kSB];
     uint8_t ts[kMaxBPB * kSB];
-    uint8_t W[kTW][kSB];
-    unsigned long long PM[kTW][kWave];
+    uint8_t W[kRTW][kSB];
+    unsigned long long PM[kRTW][kWave];
     int4 skv[kRT];                    // the batch's records in bucket order (log order inside)
     uint8_t sop[kRT];
     uint16_t sidx[kRT];               // their index in the batch
-    uint32_t cw[kRH * kTW][kMaxBPB];  // per (half, wave): records per bucket -> exclusive prefix
+    uint32_t cw[kRH * kRTW][kMaxBPB];  // per (half, wave): records per bucket -> exclusive prefix
     uint32_t bcnt[kMaxBPB], bst[kMaxBPB];
     uint32_t flags;
 #if MPX_RS_STAMP
-    unsigned long long ph[8], rb[kTW];
+    unsigned long long ph[8], rb[kRTW];
 #endif
 };
 
@@ -861,7 +869,7 @@ __device__ __forceinline__ void resolve_bucket(ResolveLds& S, int b, uint32_t cn
     }
 }
 
-__global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
+__global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
                                                     const uint32_t* __restrict__ bin_start,
                                                     const int4* __restrict__ rec_kv,
                                                     const uint8_t* __restrict__ rec_op,
@@ -878,7 +886,7 @@ __global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
     if (r0 == r1) return;  // no records: nothing read, nothing touched (small calls, hot-heavy chunks)
     const unsigned long long below = (1ull << l) - 1ull;
     auto load_tables = [&]() {
-        for (uint32_t i = tid; i < nslot; i += kTT) {
+        for (uint32_t i = tid; i < nslot; i += kRTT) {
             S.tk[i] = t.keys[gbase + i];
             S.tv[i] = t.vals[gbase + i];
             const uint32_t x = t.state[gbase + i];
@@ -899,7 +907,7 @@ __global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
             load_tables();
             if (tid == 0) atomicAdd(&hot->restarts, 1u);
             __syncthreads();
-            for (uint32_t q = r0 + tid; q < r1; q += kTT) {
+            for (uint32_t q = r0 + tid; q < r1; q += kRTT) {
                 if (rec_op[q] != MPX_OP_PUT) continue;
                 const int4 kv = rec_kv[q];
                 const int64_t k = kv_lo_hi(kv.x, kv.y);
@@ -925,7 +933,7 @@ __global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
             __syncthreads();
         }
         // the next batch is loaded while this one is resolved
-        for (int i = tid; i < kRH * kTW * kMaxBPB; i += kTT) (&S.cw[0][0])[i] = 0u;
+        for (int i = tid; i < kRH * kRTW * kMaxBPB; i += kRTT) (&S.cw[0][0])[i] = 0u;
         __syncthreads();
         // (ops held as 32-bit values: packed into one register as bytes, the compiler waits for the
         // prefetch at the loop back-edge)
@@ -933,13 +941,13 @@ __global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
         uint32_t o[kRH];
 #pragma unroll
         for (int hh = 0; hh < kRH; ++hh) {
-            const uint32_t q = r0 + hh * kTT + tid;
+            const uint32_t q = r0 + hh * kRTT + tid;
             kv[hh] = q < r1 ? rec_kv[q] : make_int4(0, 0, 0, 0);
             o[hh] = q < r1 ? rec_op[q] : 0;
         }
 #if MPX_RS_STAMP
         if (tid < 8) S.ph[tid] = 0;
-        if (tid < kTW) S.rb[tid] = 0;
+        if (tid < kRTW) S.rb[tid] = 0;
         __syncthreads();
         unsigned long long c0 = clock64(), c1;
 #define RS_STAMP(i) do { c1 = clock64(); if (tid == 0) S.ph[i] += c1 - c0; c0 = c1; } while (0)
@@ -951,7 +959,7 @@ __global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
             bool live[kRH];
 #pragma unroll
             for (int hh = 0; hh < kRH; ++hh) {
-                const uint32_t i = hh * kTT + tid;
+                const uint32_t i = hh * kRTT + tid;
                 live[hh] = base + i < r1;
                 const uint64_t h = hash64((uint64_t)kv_lo_hi(kv[hh].x, kv[hh].y));
                 bl[hh] = bucket_of(h, g.lgnb) & (bpb - 1);
@@ -960,7 +968,7 @@ __global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
                 const unsigned long long m = match_bits(bl[hh], (int)g.lgbpb, live[hh]);
                 rk[hh] = (uint32_t)__popcll(m & below);
                 if (live[hh] && (m >> l) == 1ull)  // the last lane of its bucket: the count
-                    S.cw[hh * kTW + w][bl[hh]] = (uint32_t)__popcll(m);
+                    S.cw[hh * kRTW + w][bl[hh]] = (uint32_t)__popcll(m);
             }
             RS_STAMP(0);
             __syncthreads();
@@ -973,13 +981,13 @@ __global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
                 uint32_t pre[kRH], all[kRH];
 #pragma unroll
                 for (int hh = 0; hh < kRH; ++hh) {
-                    uint32_t c[kTW];
+                    uint32_t c[kRTW];
 #pragma unroll
-                    for (int v = 0; v < kTW; ++v) c[v] = b < bpb ? S.cw[hh * kTW + v][b] : 0u;
+                    for (int v = 0; v < kRTW; ++v) c[v] = b < bpb ? S.cw[hh * kRTW + v][b] : 0u;
                     pre[hh] = 0;
                     all[hh] = 0;
 #pragma unroll
-                    for (int v = 0; v < kTW; ++v) {
+                    for (int v = 0; v < kRTW; ++v) {
                         pre[hh] += v < w ? c[v] : 0u;
                         all[hh] += c[v];
                     }
@@ -1009,7 +1017,7 @@ __global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
                     if (live[hh]) {
                         S.skv[x] = kv[hh];
                         S.sop[x] = (uint8_t)o[hh];
-                        S.sidx[x] = (uint16_t)(hh * kTT + tid);
+                        S.sidx[x] = (uint16_t)(hh * kRTT + tid);
                     }
                 }
             }
@@ -1017,14 +1025,14 @@ __global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
             // them must not be needed before this batch's records are in LDS)
 #pragma unroll
             for (int hh = 0; hh < kRH; ++hh) {
-                const uint32_t q = base + kRT + hh * kTT + tid;
+                const uint32_t q = base + kRT + hh * kRTT + tid;
                 kv[hh] = q < r1 ? rec_kv[q] : make_int4(0, 0, 0, 0);
                 o[hh] = q < r1 ? rec_op[q] : 0;
             }
             RS_STAMP(2);
             __syncthreads();
             RS_STAMP(3);
-            for (int i = tid; i < kRH * kTW * kMaxBPB; i += kTT) (&S.cw[0][0])[i] = 0u;
+            for (int i = tid; i < kRH * kRTW * kMaxBPB; i += kRTT) (&S.cw[0][0])[i] = 0u;
 #if MPX_RS_STAMP
             const unsigned long long rb0 = clock64();
 #endif
@@ -1042,17 +1050,17 @@ __global__ __launch_bounds__(kTT) void k_ap_resolve(ApGeo g, KvTable t,
 #if MPX_RS_STAMP
     if (bin == 0 && tid == 0) {
         unsigned long long mx = 0, sm = 0;
-        for (int i = 0; i < kTW; ++i) {
+        for (int i = 0; i < kRTW; ++i) {
             mx = S.rb[i] > mx ? S.rb[i] : mx;
             sm += S.rb[i];
         }
         printf("RS_STAMP bin0 recs=%u rank=%llu bar1=%llu prefix+sorted=%llu bar2=%llu resolve(w0)=%llu bar3=%llu rb_max=%llu rb_mean=%llu\n",
-               r1 - r0, S.ph[0], S.ph[1], S.ph[2], S.ph[3], S.ph[4], S.ph[5], mx, sm / kTW);
+               r1 - r0, S.ph[0], S.ph[1], S.ph[2], S.ph[3], S.ph[4], S.ph[5], mx, sm / kRTW);
     }
 #endif
     // write back the touched slots; count the keys that became present
     uint32_t added = 0;
-    for (uint32_t i = tid; i < nslot; i += kTT) {
+    for (uint32_t i = tid; i < nslot; i += kRTT) {
         const uint8_t s = S.ts[i];
         if (s & kSNew) t.keys[gbase + i] = S.tk[i];
         if (s & kSValDirty) t.vals[gbase + i] = S.tv[i];
@@ -1242,7 +1250,7 @@ struct FastLayout {
 ApGeo geo_for(const KvTable& t, uint64_t n) {
     ApGeo g{};
     g.lgnb = t.lgnb;
-    g.lgbpb = t.lgnb < 4 ? t.lgnb : 4;
+    g.lgbpb = t.lgnb < (uint32_t)kLgMaxBPB ? t.lgnb : (uint32_t)kLgMaxBPB;
     g.nbin = 1u << (t.lgnb - g.lgbpb);
     g.rowlen = g.nbin + 2 * kHMax;
     g.tiles = (uint32_t)((n + kTL - 1) / kTL);
@@ -1278,7 +1286,7 @@ FastLayout fast_layout(const KvTable& t, uint64_t c) {
 }  // namespace
 
 bool apply_fast_ok(const KvTable& t) {
-    const uint32_t lgbpb = t.lgnb < 4 ? t.lgnb : 4;
+    const uint32_t lgbpb = t.lgnb < (uint32_t)kLgMaxBPB ? t.lgnb : (uint32_t)kLgMaxBPB;
     return (1u << (t.lgnb - lgbpb)) <= (uint32_t)kMaxBins;
 }
 
@@ -1355,7 +1363,7 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
         k_ap_scan_rows<<<g.ng, 256, 0, stream>>>(g, rows, part, bin_start, hot);
         k_ap_scatter<<<kScatterGrid, kTT, 0, stream>>>(g, op + c0, key + c0, val + c0, n, rows, hot,
                                                   rec_kv, rec_op, ipos, cpos, tcold);
-        k_ap_resolve<<<g.nbin, kTT, 0, stream>>>(g, t, bin_start, rec_kv, rec_op, r_ret, r_conf,
+        k_ap_resolve<<<g.nbin, kRTT, 0, stream>>>(g, t, bin_start, rec_kv, rec_op, r_ret, r_conf,
                                                  hot, err);
         k_ap_hot_commit<<<1, kHMax, 0, stream>>>(t, val + c0, hot, err);
         k_ap_emit<<<g.tiles, kTT, 0, stream>>>(g, op + c0, val + c0, n, ipos, cpos, tcold, r_ret,
