@@ -366,6 +366,9 @@ __global__ __launch_bounds__(kTT) void k_ap_select(KvTable t, const int64_t* __r
 }
 
 // ---- per-tile counts --------------------------------------------------------------------------
+// persistent (kCountGrid workgroups, XCD-contiguous tiles): the hot table is built once per
+// workgroup, and the next tile's keys load while this one is counted
+constexpr unsigned kCountGrid = 512;  // two 1024-thread workgroups per CU
 __global__ __launch_bounds__(kTT) void k_ap_count(ApGeo g, const uint8_t* __restrict__ op,
                                                   const int64_t* __restrict__ key, uint32_t n,
                                                   uint32_t* __restrict__ rows,
@@ -375,46 +378,65 @@ __global__ __launch_bounds__(kTT) void k_ap_count(ApGeo g, const uint8_t* __rest
     __shared__ uint32_t ha[kHMax], hp[kHMax];
     const int tid = threadIdx.x;
     const uint32_t nh = hot->n;
-    for (uint32_t b = tid; b < g.nbin; b += kTT) hist[b] = 0;
-    if (tid < kHMax) {
-        ha[tid] = 0;
-        hp[tid] = 0;
-    }
-    hot_build(hl, hot, nh);
-    const uint32_t tile = xcd_tile(g.tiles);
-    const uint32_t j0 = tile * (uint32_t)kTL;
+    const TileWalk tw = tile_walk(g.tiles);
     int64_t k[kTPer];
     uint32_t o[kTPer];  // ops: loaded up front when hot keys exist, else only for INT64_MIN keys
+    auto load = [&](uint32_t tile) {
+        const uint32_t j0 = tile * (uint32_t)kTL;
 #pragma unroll
-    for (int u = 0; u < kTPer; ++u) {
-        const uint32_t j = j0 + u * kTT + tid;
-        k[u] = j < n ? key[j] : 0;
-        o[u] = j < n && nh > 1 ? op[j] : 0u;
-    }
+        for (int u = 0; u < kTPer; ++u) {
+            const uint32_t j = j0 + u * kTT + tid;
+            const bool in = tile < tw.end && j < n;
+            k[u] = in ? key[j] : 0;
+            o[u] = in && nh > 1 ? op[j] : 0u;
+        }
+    };
+    load(tw.tile);  // in flight while the hot table is built (its key loads and barriers)
+    hot_build(hl, hot, nh);
     const int l = lane_id();
+    for (uint32_t tile = tw.tile; tile < tw.end; tile += tw.step) {
+        for (uint32_t b = tid; b < g.nbin; b += kTT) hist[b] = 0;
+        if (tid < kHMax) {
+            ha[tid] = 0;
+            hp[tid] = 0;
+        }
+        __syncthreads();
+        const uint32_t j0 = tile * (uint32_t)kTL;
+        uint64_t h[kTPer];
+        int hh[kTPer];
 #pragma unroll
-    for (int u = 0; u < kTPer; ++u) {
-        const uint32_t j = j0 + u * kTT + tid;
-        const bool in = j < n;
-        const uint64_t h = hash64((uint64_t)k[u]);
-        const int hh = in ? hot_find(hl, nh, k[u], h) : -1;
-        if (in && hh < 0) atomicAdd(&hist[bin_of(h, g)], 1u);
-        const bool hotc = in && hh >= 0;
-        if (!__ballot(hotc)) continue;
-        if (nh <= 1 && hotc) o[u] = op[j];
-        // per hot key of the round: its last command and its last PUT, one LDS atomic each
-        const bool put = hotc && o[u] == MPX_OP_PUT;
-        const unsigned long long peers = match_bits((uint32_t)hh, kLgHMax, hotc);
-        const unsigned long long puts = peers & __ballot(put);
-        if (hotc && hi_bit(peers) == l) atomicMax(&ha[hh], j + 1);
-        if (put && hi_bit(puts) == l) atomicMax(&hp[hh], j + 1);
-    }
-    __syncthreads();
-    uint32_t* row = rows + (uint64_t)tile * g.rowlen;
-    for (uint32_t b = tid; b < g.nbin; b += kTT) row[b] = hist[b];
-    if (tid < kHMax) {
-        row[g.nbin + 2 * tid] = ha[tid];
-        row[g.nbin + 2 * tid + 1] = hp[tid];
+        for (int u = 0; u < kTPer; ++u) {
+            const uint32_t j = j0 + u * kTT + tid;
+            h[u] = hash64((uint64_t)k[u]);
+            hh[u] = j < n ? hot_find(hl, nh, k[u], h[u]) : -1;
+        }
+        uint32_t oc[kTPer];
+#pragma unroll
+        for (int u = 0; u < kTPer; ++u) oc[u] = o[u];
+        load(tile + tw.step);  // the next tile's keys, while this one is counted
+#pragma unroll
+        for (int u = 0; u < kTPer; ++u) {
+            const uint32_t j = j0 + u * kTT + tid;
+            const bool in = j < n;
+            if (in && hh[u] < 0) atomicAdd(&hist[bin_of(h[u], g)], 1u);
+            const bool hotc = in && hh[u] >= 0;
+            if (!__ballot(hotc)) continue;
+            if (nh <= 1 && hotc) oc[u] = op[j];
+            // per hot key of the round: its last command and its last PUT, one LDS atomic each
+            const bool put = hotc && oc[u] == MPX_OP_PUT;
+            const unsigned long long peers = match_bits((uint32_t)hh[u], kLgHMax, hotc);
+            const unsigned long long puts = peers & __ballot(put);
+            if (hotc && hi_bit(peers) == l) atomicMax(&ha[hh[u]], j + 1);
+            if (put && hi_bit(puts) == l) atomicMax(&hp[hh[u]], j + 1);
+        }
+        __syncthreads();
+        uint32_t* row = rows + (uint64_t)tile * g.rowlen;
+        for (uint32_t b = tid; b < g.nbin; b += kTT) row[b] = hist[b];
+        if (tid < kHMax) {
+            row[g.nbin + 2 * tid] = ha[tid];
+            row[g.nbin + 2 * tid + 1] = hp[tid];
+        }
+        __syncthreads();
     }
 }
 
@@ -1356,7 +1378,7 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
             k_ap_sample<<<kSampGrid, 256, 0, stream>>>(key + c0, n, hot_min, gk, gc, tab);
         }
         k_ap_select<<<1, kTT, 0, stream>>>(t, gk, gc, hot_min, tab, hot);
-        k_ap_count<<<g.tiles, kTT, 0, stream>>>(g, op + c0, key + c0, n, rows, hot);
+        k_ap_count<<<kCountGrid, kTT, 0, stream>>>(g, op + c0, key + c0, n, rows, hot);
         k_ap_scan_part<<<g.ng, 256, 0, stream>>>(g, rows, part, hot);
         k_ap_scan_top<<<(g.rowlen + kTopCols - 1) / kTopCols, kTT, 0, stream>>>(g, part, ctot, hot);
         k_ap_scan_bins<<<1, kTT, 0, stream>>>(g, ctot, bin_start);
