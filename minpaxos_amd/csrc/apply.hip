@@ -12,7 +12,7 @@
 //   conf[i] = Conflict(previous command on k in this call, command i)
 //   table   : k <- val of the last PUT on k in this call
 // Only keys that are PUT in this call or already present can change any output, so:
-//   0. k_epoch_bump       a new call epoch (device counter, so captured graphs stay correct)
+//   0. k_epoch_next       a new call epoch (device counter, so captured graphs stay correct)
 //   1. k_kv_insert_puts   insert every PUT key of the whole call (one 64-bit CAS per probe; the
 //                         key INT64_MIN is kept in a side slot so the table needs no key state)
 // then the log is cut into chunks of C commands, processed in order; per chunk:
@@ -62,24 +62,34 @@ __global__ void k_kv_fill(KvTable t) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *t.n_present = 0;
 }
 
-// epoch[0] = current call epoch, epoch[1] = wrap flag (the next kernel clears every slot's tag);
-// also zeroes the call's miss counter (k_kv_index)
-__global__ void k_epoch_bump(uint32_t* epoch, uint32_t* n_miss) {
-    *n_miss = 0;
-    uint32_t e = epoch[0] + 1;
-    epoch[1] = 0;
-    if (e >= kEpochMax) {
-        e = 1;
-        epoch[1] = 1;
+// A new call epoch in one launch: epoch[0] = the current call epoch; when it would reach
+// kEpochMax every slot's tag is cleared and it restarts at 1. Every block reads the old epoch
+// before it counts itself done in epoch[1] (0 between calls); the last block to finish writes the
+// new one, so no block can see it early. Also zeroes the call's miss counter (k_kv_index).
+__global__ void k_epoch_next(KvTable t, uint32_t* n_miss) {
+    if (n_miss && blockIdx.x == 0 && threadIdx.x == 0) *n_miss = 0;
+    const uint32_t e0 = t.epoch[0];
+    const bool wrap = e0 + 1 >= kEpochMax;
+    if (wrap) {
+        const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+        for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= t.cap; s += stride)
+            t.state[s] &= kPresent;
     }
-    epoch[0] = e;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&t.epoch[1], 1u) == gridDim.x - 1) {
+            atomicExch(&t.epoch[1], 0u);
+            atomicExch(&t.epoch[0], wrap ? 1u : e0 + 1);
+        }
+    }
 }
 
-__global__ void k_epoch_wrap(KvTable t) {
-    if (!t.epoch[1]) return;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= t.cap; s += stride)
-        t.state[s] &= kPresent;
+hipError_t launch_epoch_next(KvTable& t, uint32_t* n_miss, hipStream_t stream) {
+    // few blocks: their completion atomics on one word serialise (1024 blocks cost ~15 us per
+    // call); the sweep they share runs once per 2^30 calls
+    k_epoch_next<<<32, 256, 0, stream>>>(t, n_miss);
+    return hipGetLastError();
 }
 
 hipError_t launch_kv_clear(KvTable& t, hipStream_t stream) {
@@ -593,8 +603,7 @@ hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const
     const unsigned slot_bits = bits_for(t.cap + 2);
 
     uint32_t* n_miss = (uint32_t*)(b + L.n_miss);
-    k_epoch_bump<<<1, 1, 0, stream>>>(t.epoch, n_miss);
-    k_epoch_wrap<<<1024, 256, 0, stream>>>(t);
+    if (const hipError_t er = launch_epoch_next(t, n_miss, stream); er != hipSuccess) return er;
     // one chunk: one pass writes every sort key (PUTs insert, the rest probe; misses re-probed
     // after the pass, through lps as the miss list - lps is not live until the scan)
     const bool one = C >= m;

@@ -1314,23 +1314,6 @@ bool apply_fast_ok(const KvTable& t) {
 
 uint64_t apply_fast_work_bytes(const KvTable& t, uint64_t c) { return fast_layout(t, c).total; }
 
-__global__ void k_epoch_bump2(uint32_t* epoch) {
-    uint32_t e = epoch[0] + 1;
-    epoch[1] = 0;
-    if (e >= kEpochMax) {
-        e = 1;
-        epoch[1] = 1;
-    }
-    epoch[0] = e;
-}
-
-__global__ void k_epoch_wrap2(KvTable t) {
-    if (!t.epoch[1]) return;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= t.cap; s += stride)
-        t.state[s] &= kPresent;
-}
-
 __global__ __launch_bounds__(256) void k_ap_preinsert(KvTable t, const uint8_t* __restrict__ op,
                                                       const int64_t* __restrict__ key, uint64_t m,
                                                       uint32_t* err) {
@@ -1361,8 +1344,7 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
     uint8_t* r_conf = (uint8_t*)(b + L.r_conf);
     ApHot* hot = (ApHot*)(b + L.hot);
 
-    k_epoch_bump2<<<1, 1, 0, stream>>>(t.epoch);
-    k_epoch_wrap2<<<1024, 256, 0, stream>>>(t);
+    if (const hipError_t er = launch_epoch_next(t, nullptr, stream); er != hipSuccess) return er;
     if (C < m) {
         const uint64_t blocks = (m + 255) / 256;
         k_ap_preinsert<<<(unsigned)(blocks > 8192 ? 8192 : blocks), 256, 0, stream>>>(t, op, key,

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -162,6 +163,16 @@ int ensure_kv(mpx_engine* e) {
         hipMemsetAsync(t.epoch, 0, 2 * sizeof(uint32_t), e->stream) != hipSuccess) {
         (void)hipGetLastError();
         return fail(e, MPX_E_NOMEM, "KV table allocation failed");
+    }
+    // test hook: MPX_KV_EPOCH_START starts the call epoch of a new table near its wrap (kEpochMax
+    // = 2^30 calls), so a test can drive calls across it
+    if (const char* es = getenv("MPX_KV_EPOCH_START")) {
+        const uint32_t e0 = (uint32_t)strtoul(es, nullptr, 10);
+        if (hipMemcpyAsync(t.epoch, &e0, sizeof e0, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+            hipStreamSynchronize(e->stream) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(e, MPX_E_NOMEM, "KV table epoch setup failed");
+        }
     }
     e->kv = t;
     HIPCHK(e, mpx::launch_kv_clear(e->kv, e->stream));

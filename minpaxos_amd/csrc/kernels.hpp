@@ -80,6 +80,8 @@ struct ApplyWork {      // scratch sized for m commands (see apply_work_bytes)
 constexpr uint64_t kApplyChunkDefault = 1ull << 26;
 uint64_t apply_chunk_commands(uint64_t chunk, uint64_t m);
 uint64_t apply_work_bytes(const KvTable& t, uint64_t chunk, uint64_t m);
+// a new call epoch for the table (both apply pipelines); zeroes *n_miss when given
+hipError_t launch_epoch_next(KvTable& t, uint32_t* n_miss, hipStream_t stream);
 // scratch for any call of at most max_m commands (mpx_apply_reserve)
 uint64_t apply_reserve_bytes(const KvTable& t, uint64_t chunk, uint64_t max_m);
 // the partitioned pipeline (apply_fast.hip): tables of at most 1024 bins of 16 buckets

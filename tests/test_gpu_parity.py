@@ -294,6 +294,26 @@ def test_apply_size_dispatch(mk_engine, monkeypatch):
     assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
 
 
+@pytest.mark.parametrize("fallback", ["0", "1"])
+def test_apply_epoch_wrap(mk_engine, monkeypatch, fallback):
+    """the call epoch tags every slot a call touched (state.Conflict against the same call's
+    earlier commands); 2^30 calls wrap it to 1 after clearing every tag. A table whose epoch
+    starts three calls before the wrap (MPX_KV_EPOCH_START) runs six calls across it on each
+    pipeline: every call and the final table bit-exact"""
+    monkeypatch.setenv("MPX_APPLY_FALLBACK", fallback)
+    monkeypatch.setenv("MPX_KV_EPOCH_START", str((1 << 30) - 3))
+    rng = np.random.default_rng(71 + int(fallback))
+    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=4096), Oracle(5, R.MODE_MIN)
+    for _ in range(6):
+        op, key, val = gen_cases.commands_mixed(rng, 20000, 1500)
+        gr, gc = e.apply(op, key, val)
+        wr, wc = o.apply(op, key, val)
+        assert np.array_equal(gr, wr) and np.array_equal(gc, wc)
+    gk, gv = e.kv_export()
+    wk, wv = o.kv_export()
+    assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
+
+
 def test_apply_large_table_fallback(mk_engine):
     """a table past the partitioned pipeline's 1024 bins (kv_capacity 4M keys: 8M slots) takes
     the sort-based pipeline; same results"""
