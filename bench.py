@@ -18,6 +18,13 @@ reported beside it.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--mode min|classic]
   torchrun --nproc-per-node N bench.py --gpus N ...
 
+`--gpus N` (N > 1) without a launcher (no WORLD_SIZE in the environment) starts N fresh rank
+processes itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT), before
+anything loads the engine or touches a GPU, waits for all of them, forwards rank 0's JSON line
+and exits non-zero if any rank fails. Under torchrun the ranks come from the environment.
+The default is BASELINE config 5 as written: 65,536 groups in total, strong scaling (block
+partition over the ranks); `--scaling weak --groups G` keeps G groups per GPU instead.
+
 The other single-GPU configurations of BASELINE.json are kernel benches of their own
 (--workload; the default `step` is the headline line above):
   tally       config 2: accept tally, 16M instances x 4 replies (k_accept_tally), --mode min|classic
@@ -53,9 +60,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from minpaxos_amd import _lib  # noqa: E402  (first: the engine's HIP + RCCL, not torch's)
-
-_lib.load()
+# _lib.load() runs in main(), after the rank launcher and before torch is imported (the engine's
+# HIP + RCCL, not torch's); importing this module loads nothing
+from minpaxos_amd import _lib  # noqa: E402
 from minpaxos_amd import records as R  # noqa: E402
 from minpaxos_amd import shard, synth  # noqa: E402
 from minpaxos_amd.devbuf import D2D, Arena, DevArray  # noqa: E402
@@ -70,7 +77,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mode", default="min", choices=["min", "classic"])
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="strong (default): --groups-total split over the ranks (BASELINE "
+                         "config 5); weak: --groups per rank")
     ap.add_argument("--groups", type=int, default=65536, help="groups per GPU (weak scaling)")
     ap.add_argument("--groups-total", type=int, default=65536,
                     help="groups of the whole job (strong scaling)")
@@ -143,10 +152,19 @@ class Ranks:
         self.dist.broadcast_object_list(box, src=0)
         return box[0]
 
-    def close(self):
+    def gather(self, obj):
+        """obj of every rank, in rank order, on every rank"""
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def close(self, barrier=True):
         if self.dist:
-            self.dist.barrier()
-            self.dist.destroy_process_group()
+            if barrier:
+                self.dist.barrier()
+                self.dist.destroy_process_group()
 
 
 def host_cores():
@@ -176,17 +194,71 @@ def traffic_of(path, **want):
     return None
 
 
+def launch_ranks(n):
+    """--gpus n without a launcher: n fresh child processes of this script, one per GPU. The
+    parent never loads the engine or touches a GPU (no HIP call precedes the children); it
+    forwards rank 0's stdout, sends the other ranks' stdout to stderr, and ends every rank as
+    soon as one fails. Returns the exit status."""
+    import socket
+    import subprocess
+    import threading
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr))
+
+    def forward(pipe):
+        for ln in iter(pipe.readline, b""):
+            sys.stdout.write(ln.decode(errors="replace"))
+            sys.stdout.flush()
+    fw = threading.Thread(target=forward, args=(procs[0].stdout,), daemon=True)
+    fw.start()
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                print(f"bench.py: rank {procs.index(p)} exited with status {c}; stopping the "
+                      f"other ranks", file=sys.stderr, flush=True)
+                for q in live:
+                    q.kill()  # the exact child PIDs this parent started
+        time.sleep(0.05)
+    fw.join(timeout=10)
+    return rc
+
+
 # ==================================== headline: config 5 ======================================
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a.gpus))
+    _lib.load()
     rk = Ranks()
+    if a.gpus != rk.world and rk.rank == 0:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={rk.world}; running {rk.world} ranks",
+              file=sys.stderr, flush=True)
+    ok = False
     try:
         if a.workload == "step":
             step_bench(a, rk)
         else:
             kernel_bench(a, rk)
+        ok = True
     finally:
-        rk.close()
+        # a failed rank leaves without the closing barrier (its peers may be blocked in another
+        # collective): it exits non-zero and the launcher ends the others
+        rk.close(barrier=ok)
 
 
 def step_bench(a, rk):
@@ -218,7 +290,9 @@ def step_bench(a, rk):
         kv0=ar.full(G * K, np.int64, 0), kc1=ar.full(G, np.uint32, 0),
         kk1=ar.full(G * K, np.int64, 0), kv1=ar.full(G * K, np.int64, 0),
         nd=ar.full(G, np.uint32, 0),
-        wm=[ar.full(2 * G_total, np.int32, 0xFF) for _ in range(2)],
+        # poisoned (0x7F7F7F7F > any instance): the per-step -1 fill of the ranges other ranks
+        # own is what makes the max-all-reduce correct, a missing or short fill shows up
+        wm=[ar.full(2 * G_total, np.int32, 0x7F) for _ in range(2)],
         tot=[ar.full(R_TOTALS, np.int64, 0) for _ in range(2)],
     )
 
@@ -292,7 +366,12 @@ def step_bench(a, rk):
     committed, executed = wm[:G_total], wm[G_total:]
     own_e = executed[g0:g1].astype(np.int64)
     kc = ar.get(d["kc1"])
-    wm_ok = bool((committed >= 0).all())  # every rank sees every group's watermark
+    # every rank sees every group's watermark (no -1 or poison left) and all ranks hold the
+    # same vector after the all-reduce
+    wm_ok = bool((committed >= 0).all() and (wm < ipg).all())
+    import hashlib
+    wm_sha = hashlib.sha256(wm.tobytes()).hexdigest()
+    shas = rk.gather(wm_sha)
     coff = b["cmd_off"].astype(np.int64)
     gidx = np.arange(G, dtype=np.int64) * ipg
     own_cmds = int((coff[gidx + own_e + 1] - coff[gidx]).sum())
@@ -354,6 +433,8 @@ def step_bench(a, rk):
             "executed_instances_per_s": n_exec_inst * a.steps / elapsed,
             "executed_commands_per_s": n_exec_cmds * a.steps / elapsed,
             "watermark_allreduce_ok": wm_ok,
+            "watermarks_sha256": wm_sha,
+            "watermarks_identical_on_all_ranks": len(set(shas)) == 1,
             "gen_s": round(t_gen, 2),
             "runtime": _lib.runtime_info(),
         }

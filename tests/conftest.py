@@ -63,3 +63,24 @@ def mk_engine():
     yield mk
     for e in made:
         e.close()
+
+
+@pytest.fixture(scope="session")
+def stub_lib():
+    """libmpx_stub.so: engine.cpp (the real C ABI host code) over tests/san/hip_stub.cpp built
+    with MPX_STUB_ORACLE=1 — host-memory "devices", the group step through the CPU oracle and
+    RCCL all-reduces that really reduce across processes (shared memory). TEST INFRASTRUCTURE:
+    lets the multi-rank path of bench.py / engine.cpp run on a CPU; never shipped."""
+    out_dir = os.path.join(TESTS, "san", "_build")
+    os.makedirs(out_dir, exist_ok=True)
+    so = os.path.join(out_dir, "libmpx_stub.so")
+    srcs = [os.path.join(ROOT, "minpaxos_amd", "csrc", "engine.cpp"),
+            os.path.join(TESTS, "san", "hip_stub.cpp"), os.path.join(ROOT, "oracle", "oracle.cpp")]
+    deps = srcs + [os.path.join(ROOT, "include", "mpx.h"),
+                   os.path.join(ROOT, "minpaxos_amd", "csrc", "kernels.hpp")]
+    if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(d) for d in deps):
+        subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-fPIC", "-shared",
+                        "-D__HIP_PLATFORM_AMD__", "-DMPX_STUB_ORACLE=1", "-I/opt/rocm/include",
+                        "-I" + os.path.join(ROOT, "include"), *srcs, "-ldl", "-lrt", "-o", so],
+                       check=True)
+    return so

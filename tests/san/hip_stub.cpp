@@ -1,19 +1,111 @@
 // tests/san/hip_stub.cpp — TEST INFRASTRUCTURE ONLY: a host-memory stand-in for the HIP / RCCL
-// runtime calls engine.cpp makes, plus no-op kernel launchers, so the C ABI's host-side code
-// (argument validation, staging, the decode loop, error reporting) can be built and run under
-// AddressSanitizer + UBSan on a CPU. "Device" memory is host memory; copies are
-// memcpy; launchers enqueue nothing.
+// runtime calls engine.cpp makes, so the C ABI's host side can be built and run on a CPU.
+// "Device" memory is host memory, copies are memcpy, every call completes before it returns
+// (so stream and event order hold trivially) and events carry a host timestamp.
+//
+// Two builds (never shipped, never loaded by the product path):
+//   * default (tests/test_sanitize.py): kernel launchers enqueue nothing; engine.cpp's argument
+//     validation, staging and error paths run under ASan + UBSan.
+//   * -DMPX_STUB_ORACLE=1 (tests/test_dist.py, libmpx_stub.so): the group-step launchers run the
+//     CPU oracle (oracle/oracle.cpp, linked into the stub) and the RCCL calls really reduce across
+//     PROCESSES — every rank maps one /dev/shm segment named after the unique id, deposits its
+//     buffer in its slot, waits at a barrier, and reads the reduction of all slots. That is what
+//     lets bench.py's multi-rank step (engine.cpp's nranks > 1 path: comm init, the fused
+//     max + sum group, double-buffered watermark vectors) run end to end without a GPU.
+// MPX_STUB_DEVICES (default 1) sets the device count the stub reports.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "../../minpaxos_amd/csrc/kernels.hpp"
 
+namespace {
+double now_s() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + t.tv_nsec * 1e-9;
+}
+
+// ---- cross-process communicator: one shared segment per unique id ---------------------------
+constexpr size_t kSlotBytes = 64ull << 20;  // per rank (sparse: only touched pages use memory)
+constexpr int kMaxRanks = 16;
+struct ShmHeader {
+    std::atomic<uint32_t> arrived;
+    std::atomic<uint32_t> generation;
+    std::atomic<uint32_t> joined;
+    uint32_t nranks;
+};
+struct StubComm {
+    ShmHeader* hdr = nullptr;
+    char* slots = nullptr;
+    size_t map_bytes = 0;
+    int nranks = 1, rank = 0;
+    char name[64] = {0};
+};
+
+// sense-reversing barrier over the segment; false after 120 s (a peer died)
+bool barrier(StubComm* c) {
+    if (c->nranks == 1) return true;
+    const uint32_t gen = c->hdr->generation.load(std::memory_order_acquire);
+    if (c->hdr->arrived.fetch_add(1, std::memory_order_acq_rel) == (uint32_t)c->nranks - 1) {
+        c->hdr->arrived.store(0, std::memory_order_relaxed);
+        c->hdr->generation.fetch_add(1, std::memory_order_acq_rel);
+        return true;
+    }
+    const double t0 = now_s();
+    while (c->hdr->generation.load(std::memory_order_acquire) == gen) {
+        sched_yield();
+        if (now_s() - t0 > 120.0) return false;
+    }
+    return true;
+}
+
+template <typename T>
+void reduce_into(T* d, const char* slots, int nranks, size_t n, ncclRedOp_t op) {
+    for (size_t i = 0; i < n; ++i) {
+        T acc = reinterpret_cast<const T*>(slots)[i];
+        for (int r = 1; r < nranks; ++r) {
+            const T v = reinterpret_cast<const T*>(slots + (size_t)r * kSlotBytes)[i];
+            switch (op) {
+                case ncclMax: acc = v > acc ? v : acc; break;
+                case ncclMin: acc = v < acc ? v : acc; break;
+                default: acc = (T)(acc + v); break;
+            }
+        }
+        d[i] = acc;
+    }
+}
+
+size_t el_size(ncclDataType_t t) {
+    switch (t) {
+        case ncclInt8: case ncclUint8: return 1;
+        case ncclInt64: case ncclUint64: case ncclFloat64: return 8;
+        default: return 4;
+    }
+}
+
+int stub_devices() {
+    const char* s = getenv("MPX_STUB_DEVICES");
+    const int n = s ? atoi(s) : 1;
+    return n > 0 ? n : 1;
+}
+}  // namespace
+
 extern "C" {
-hipError_t hipSetDevice(int) { return hipSuccess; }
-hipError_t hipGetDeviceCount(int* c) { *c = 1; return hipSuccess; }
+hipError_t hipSetDevice(int d) { return d >= 0 && d < stub_devices() ? hipSuccess : hipErrorInvalidDevice; }
+hipError_t hipGetDeviceCount(int* c) { *c = stub_devices(); return hipSuccess; }
 hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned int) {
     *s = reinterpret_cast<hipStream_t>(malloc(8));
     return hipSuccess;
@@ -33,31 +125,97 @@ hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipSt
 hipError_t hipGetLastError(void) { return hipSuccess; }
 const char* hipGetErrorString(hipError_t) { return "stub"; }
 hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) {
-    *e = reinterpret_cast<hipEvent_t>(malloc(8));
+    *e = reinterpret_cast<hipEvent_t>(calloc(1, sizeof(double)));
     return hipSuccess;
 }
 hipError_t hipEventDestroy(hipEvent_t e) { free(e); return hipSuccess; }
-hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
-hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
+hipError_t hipEventRecord(hipEvent_t e, hipStream_t) {
+    *reinterpret_cast<double*>(e) = now_s();  // the work before it has completed (synchronous)
+    return hipSuccess;
+}
+hipError_t hipEventElapsedTime(float* ms, hipEvent_t a, hipEvent_t b) {
+    *ms = (float)((*reinterpret_cast<double*>(b) - *reinterpret_cast<double*>(a)) * 1e3);
+    return hipSuccess;
+}
 hipError_t hipRuntimeGetVersion(int* v) { *v = 1; return hipSuccess; }
 hipError_t hipDriverGetVersion(int* v) { *v = 1; return hipSuccess; }
-ncclResult_t ncclGetUniqueId(ncclUniqueId* id) { memset(id, 7, sizeof(*id)); return ncclSuccess; }
-ncclResult_t ncclCommInitRank(ncclComm_t* c, int, ncclUniqueId, int) {
-    *c = reinterpret_cast<ncclComm_t>(malloc(8));
+
+ncclResult_t ncclGetUniqueId(ncclUniqueId* id) {
+    memset(id, 0, sizeof(*id));
+    int fd = open("/dev/urandom", O_RDONLY);
+    if (fd < 0 || read(fd, id->internal, 16) != 16) {
+        if (fd >= 0) close(fd);
+        return ncclSystemError;
+    }
+    close(fd);
     return ncclSuccess;
 }
-ncclResult_t ncclCommDestroy(ncclComm_t c) { free(c); return ncclSuccess; }
-ncclResult_t ncclAllReduce(const void* s, void* d, size_t n, ncclDataType_t t, ncclRedOp_t,
-                           ncclComm_t, hipStream_t) {
-    const size_t el = t == ncclInt64 ? 8 : 4;
-    memmove(d, s, n * el);  // one rank: the reduction is the identity
+ncclResult_t ncclCommInitRank(ncclComm_t* out, int nranks, ncclUniqueId id, int rank) {
+    if (nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks) return ncclInvalidArgument;
+    StubComm* c = new StubComm();
+    c->nranks = nranks;
+    c->rank = rank;
+    char* p = c->name + snprintf(c->name, sizeof c->name, "/mpxstub_");
+    for (int i = 0; i < 16; ++i) p += sprintf(p, "%02x", (unsigned char)id.internal[i]);
+    c->map_bytes = 4096 + (size_t)nranks * kSlotBytes;
+    int fd = shm_open(c->name, O_CREAT | O_RDWR, 0600);
+    if (fd < 0 || ftruncate(fd, (off_t)c->map_bytes) != 0) {
+        if (fd >= 0) close(fd);
+        delete c;
+        return ncclSystemError;
+    }
+    void* m = mmap(nullptr, c->map_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) {
+        delete c;
+        return ncclSystemError;
+    }
+    c->hdr = reinterpret_cast<ShmHeader*>(m);  // a fresh segment is zero-filled
+    c->slots = reinterpret_cast<char*>(m) + 4096;
+    c->hdr->joined.fetch_add(1);
+    if (!barrier(c)) {
+        munmap(m, c->map_bytes);
+        delete c;
+        return ncclSystemError;
+    }
+    if (rank == 0) shm_unlink(c->name);  // every rank has it mapped: nothing left in /dev/shm
+    *out = reinterpret_cast<ncclComm_t>(c);
     return ncclSuccess;
 }
+ncclResult_t ncclCommDestroy(ncclComm_t h) {
+    StubComm* c = reinterpret_cast<StubComm*>(h);
+    if (c) {
+        munmap(c->hdr, c->map_bytes);
+        delete c;
+    }
+    return ncclSuccess;
+}
+ncclResult_t ncclAllReduce(const void* s, void* d, size_t n, ncclDataType_t t, ncclRedOp_t op,
+                           ncclComm_t h, hipStream_t) {
+    StubComm* c = reinterpret_cast<StubComm*>(h);
+    const size_t bytes = n * el_size(t);
+    if (!c || bytes > kSlotBytes) return ncclInvalidArgument;
+    memcpy(c->slots + (size_t)c->rank * kSlotBytes, s, bytes);
+    if (!barrier(c)) return ncclSystemError;  // every rank has deposited its buffer
+    switch (t) {
+        case ncclInt64: reduce_into((int64_t*)d, c->slots, c->nranks, n, op); break;
+        case ncclUint64: reduce_into((uint64_t*)d, c->slots, c->nranks, n, op); break;
+        case ncclUint32: reduce_into((uint32_t*)d, c->slots, c->nranks, n, op); break;
+        default: reduce_into((int32_t*)d, c->slots, c->nranks, n, op); break;
+    }
+    if (!barrier(c)) return ncclSystemError;  // every rank has read the slots
+    return ncclSuccess;
+}
+// the calls inside a group complete one by one, in the same order on every rank
 ncclResult_t ncclGroupStart(void) { return ncclSuccess; }
 ncclResult_t ncclGroupEnd(void) { return ncclSuccess; }
 const char* ncclGetErrorString(ncclResult_t) { return "stub"; }
 ncclResult_t ncclGetVersion(int* v) { *v = 1; return ncclSuccess; }
 }
+
+#if MPX_STUB_ORACLE
+extern "C" int orc_group_step(int N, int mode, const mpx_group_batch* b, uint32_t kv_per_group);
+#endif
 
 namespace mpx {
 hipError_t launch_accept_tally(int, const mpx_accept_reply*, uint64_t, const mpx_inst_state*,
@@ -73,9 +231,40 @@ hipError_t launch_prepare_min(const mpx_prepare_reply_min*, uint64_t, const uint
                               mpx_prepare_effect*, uint32_t*, hipStream_t) { return hipSuccess; }
 hipError_t launch_conflict_batch(const uint8_t*, const int64_t*, const uint64_t*, uint64_t,
                                  uint8_t*, hipStream_t) { return hipSuccess; }
+#if MPX_STUB_ORACLE
+// the group step through the oracle; its error codes become the kernels' error-word bits
+hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group, const mpx_group_batch* b,
+                             uint32_t*, uint32_t*, uint32_t* err, hipStream_t) {
+    const int rc = orc_group_step(nrep, mode, b, kv_per_group);
+    if (rc == MPX_E_NIL_INSTANCE) *err |= kErrNil;
+    else if (rc == MPX_E_BAD_ID) *err |= kErrBadId;
+    else if (rc == MPX_E_KV_FULL) *err |= kErrKvFull;
+    else if (rc) *err |= kErrInval;
+    return hipSuccess;
+}
+// k_step_totals (step.hip) over host memory
+hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, uint32_t*, hipStream_t) {
+    int64_t d = 0, xi = 0, xc = 0;
+    for (uint32_t g = 0; g < b->n_groups; ++g) {
+        d += b->n_decided[g];
+        const int64_t ei = b->executed_in[g], eo = b->executed_out[g];
+        const int64_t lo = ei + 1 < 0 ? 0 : ei + 1;
+        if (eo >= lo && eo < (int64_t)b->ipg) {
+            const uint64_t gi0 = (uint64_t)g * b->ipg;
+            xi += eo - lo + 1;
+            xc += b->cmd_off[gi0 + eo + 1] - b->cmd_off[gi0 + lo];
+        }
+    }
+    totals[0] = d;
+    totals[1] = xi;
+    totals[2] = xc;
+    return hipSuccess;
+}
+#else
 hipError_t launch_group_step(int, int32_t, uint32_t, const mpx_group_batch*, uint32_t*, uint32_t*,
                              uint32_t*, hipStream_t) { return hipSuccess; }
 hipError_t launch_step_totals(const mpx_group_batch*, int64_t*, uint32_t*, hipStream_t) { return hipSuccess; }
+#endif
 uint64_t apply_chunk_commands(uint64_t c, uint64_t m) { return c ? c : m; }
 uint64_t apply_work_bytes(const KvTable&, uint64_t, uint64_t m) { return 48 * m + 256; }
 uint64_t apply_reserve_bytes(const KvTable&, uint64_t, uint64_t m) { return 48 * m + 256; }

@@ -124,3 +124,92 @@ def test_strong_scaling_partition_covers_groups():
             rs = [shard.block_range(g_total, world, r) for r in range(world)]
             assert rs[0][0] == 0 and rs[-1][1] == g_total
             assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+
+
+# ---- bench.py --gpus N: the launcher and the engine's multi-rank step (nranks > 1) ----------
+def _bench(stub_lib, *args, devices=2, timeout=240):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MPX_LIB=stub_lib, MPX_STUB_DEVICES=str(devices))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args],
+                          capture_output=True, text=True, env=env, timeout=timeout, cwd=root)
+
+
+def _expected_step(g_total, ipg=256, n=5, b=4, keys=256):
+    """one step of every group of the job in ONE process through the oracle: the fused
+    watermark vector every rank must hold after the all-reduce, and the summed totals"""
+    import hashlib
+
+    from oracle_lib import Oracle
+    full = synth.group_batch(g_total, ipg, n, b, keys, p_ok=0.7, p_put=0.5, seed=45)
+    want = Oracle(n, R.MODE_MIN, kv_per_group=256).group_step(full)
+    wm = np.concatenate([want["committed_out"], want["executed_out"]]).astype(np.int32)
+    ei = full["executed_in"].astype(np.int64)
+    eo = want["executed_out"].astype(np.int64)
+    lo = np.maximum(ei + 1, 0)
+    coff = full["cmd_off"].astype(np.int64)
+    g0 = np.arange(g_total, dtype=np.int64) * ipg
+    ran = eo >= lo
+    xi = int(np.where(ran, eo - lo + 1, 0).sum())
+    xc = int(np.where(ran, coff[g0 + np.where(ran, eo, 0) + 1] - coff[g0 + lo], 0).sum())
+    return (hashlib.sha256(wm.tobytes()).hexdigest(),
+            (int(want["n_decided"].sum()), xi, xc))
+
+
+@pytest.mark.parametrize("scaling,extra,g_total", [
+    ("strong", ["--groups-total", "64"], 64),
+    ("weak", ["--groups", "24"], 48),
+    ("strong", ["--groups-total", "37"], 37),  # ragged blocks: 18 + 19 groups
+])
+def test_bench_gpus2_multirank_step(stub_lib, scaling, extra, g_total):
+    """`bench.py --gpus 2` starts two rank processes itself; each runs the engine's real
+    multi-rank step sequence (engine.cpp: comm init over the broadcast unique id, group step,
+    step totals, the fused max + sum RCCL group on a second stream, double-buffered watermark
+    vectors reset to -1 outside the rank's block) for 1 + 1 warm-up + 3 timed steps, so both
+    buffers are reused. The buffers start poisoned, so a missing -1 fill would survive the max.
+    Every rank must end with the single-process oracle's vector and the line's totals must be
+    the oracle's sums."""
+    r = _bench(stub_lib, "--gpus", "2", "--scaling", scaling, *extra, "--steps", "3",
+               "--warmup", "1", "--no-cpu-baseline")
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    import json
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == scaling
+    assert line["config"]["groups_total"] == g_total
+    assert line["parity"]["bit_exact"], line["parity"]
+    sha, (nd, xi, xc) = _expected_step(g_total)
+    assert line["watermarks_identical_on_all_ranks"]
+    assert line["watermarks_sha256"] == sha
+    assert line["watermark_allreduce_ok"]
+    assert (line["decided_instances_per_step"], line["executed_instances_per_step"],
+            line["executed_commands_per_step"]) == (nd, xi, xc)
+
+
+def test_bench_gpus1_line_shape(stub_lib):
+    """--gpus 1 runs in-process (no launcher) and prints the same keys as the 2-rank line"""
+    r1 = _bench(stub_lib, "--gpus", "1", "--groups-total", "16", "--steps", "2", "--warmup", "1",
+                "--no-cpu-baseline", devices=1)
+    r2 = _bench(stub_lib, "--gpus", "2", "--groups-total", "16", "--steps", "2", "--warmup", "1",
+                "--no-cpu-baseline")
+    assert r1.returncode == 0 and r2.returncode == 0, r1.stderr[-2000:] + r2.stderr[-2000:]
+    import json
+    l1, l2 = (json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+              for r in (r1, r2))
+    assert l1["n_gpus"] == 1 and l2["n_gpus"] == 2
+    assert sorted(l1) == sorted(l2)
+    sha, _ = _expected_step(16)
+    assert l1["watermarks_sha256"] == sha == l2["watermarks_sha256"]
+
+
+def test_bench_launcher_rank_failure_exits_nonzero(stub_lib):
+    """one rank failing (rank 1 has no device: the stub reports one) ends the job non-zero
+    instead of leaving rank 0 blocked in a collective"""
+    r = _bench(stub_lib, "--gpus", "2", "--groups-total", "16", "--steps", "2", "--warmup", "1",
+               "--no-cpu-baseline", devices=1, timeout=180)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
