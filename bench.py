@@ -112,6 +112,9 @@ def parse():
     ap.add_argument("--kv-capacity", type=int, default=0,
                     help="apply: engine key capacity (0 = --apply-keys; the table gets >= 2x slots, load <= 1/2)")
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
+    ap.add_argument("--apply-path", default="auto",
+                    choices=["auto", "small", "sorted", "partitioned"],
+                    help="apply: mpx_config.apply_path (auto = by call size)")
     ap.add_argument("--replay-dups", action="store_true",
                     help="replay: instNo drawn with repeats (last record wins) instead of a permutation")
     return ap.parse_args()
@@ -610,7 +613,9 @@ def kernel_bench(a, rk):
     import oracle_lib as OL  # CPU oracle: the checker and the CPU baseline, never the measured path
     N = 5
     mode = R.MODE_MIN if a.mode == "min" else R.MODE_CLASSIC
-    eng = Engine(rk.local, n_replicas=N, mode=mode, kv_capacity=a.kv_capacity or a.apply_keys)
+    eng = Engine(rk.local, n_replicas=N, mode=mode, kv_capacity=a.kv_capacity or a.apply_keys,
+                 apply_path={"auto": R.APPLY_AUTO, "small": R.APPLY_SMALL, "sorted": R.APPLY_SORTED,
+                             "partitioned": R.APPLY_PARTITIONED}[a.apply_path])
     ar = Arena(eng)
     put, get, sync = ar.put, ar.get, eng.synchronize
     lib = OL.load()

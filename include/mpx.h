@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define MPX_ABI_VERSION 2
+#define MPX_ABI_VERSION 3
 
 /* ---- error codes ---------------------------------------------------------------------- */
 #define MPX_OK 0
@@ -200,7 +200,29 @@ typedef struct mpx_config {
                                2048 distinct keys fails with MPX_E_KV_FULL                  */
     uint32_t flags;         /* reserved, 0                                                  */
     uint64_t max_groups;    /* groups per mpx_group_step_dev call (work list); 0 = 1<<20    */
-} mpx_config;
+    /* mpx_apply tuning, fixed for the handle's life (0 = default everywhere). Every setting
+     * gives identical results; they move time and scratch only.                            */
+    uint64_t apply_chunk;   /* commands per pipeline chunk (bounds the scratch of one call:
+                               34 B / command partitioned, 48 B sorted); 0 = 1<<26          */
+    uint32_t apply_path;    /* MPX_APPLY_AUTO: by call size (single-launch kernel up to
+                               MPX_APPLY_SMALL_MAX commands, the sort-based pipeline below
+                               apply_fast_min, the partitioned one from there, sort-based
+                               again for tables past 1024 bins); or force one of
+                               MPX_APPLY_SMALL / _SORTED / _PARTITIONED (SMALL and
+                               PARTITIONED where the call / table allow, else AUTO's pick)  */
+    uint32_t apply_fast_min;  /* AUTO: calls of at least this many commands run
+                                 partitioned; 0 = 16384 (the measured crossover)            */
+    uint32_t apply_hot_min;   /* partitioned: samples (of 64K) that make a key hot and keep
+                                 its commands in place; 0 = 5; MPX_APPLY_NO_HOT = none      */
+    uint32_t reserved;        /* 0                                                          */
+} mpx_config; /* 56 B */
+
+#define MPX_APPLY_AUTO 0
+#define MPX_APPLY_SORTED 1
+#define MPX_APPLY_PARTITIONED 2
+#define MPX_APPLY_SMALL 3
+#define MPX_APPLY_NO_HOT 0xFFFFFFFFu
+#define MPX_APPLY_SMALL_MAX 8192
 
 typedef struct mpx_engine mpx_engine;
 
@@ -594,6 +616,14 @@ int mpx_event_elapsed_ms(mpx_engine* eng, void* ev_start, void* ev_end, float* m
  * truncated to cap): {"hip_runtime": v, "hip_driver": v, "rccl": v, "hip_path": "...",
  * "rccl_path": "..."}. Returns the full length (excluding the NUL) or a negative error.    */
 int mpx_runtime_info(char* buf, size_t cap);
+
+/* ---- diagnostics: TEST-ONLY entry points (the product path never calls them) -----------
+ * mpx_debug_kv_set_epoch: set the KV table's call epoch (1 <= epoch < 2^30) without touching
+ * its slots, so a test can drive calls across the epoch wrap on a table whose slots carry
+ * older tags. mpx_debug_kv_state: copy the table's per-slot state words (bit 0 present, bit 1
+ * last command of the tagged call was a PUT, bits 2.. the tag); *n = slots (cap + 1).       */
+int mpx_debug_kv_set_epoch(mpx_engine* eng, uint32_t epoch);
+int mpx_debug_kv_state(mpx_engine* eng, uint32_t* state, size_t cap, size_t* n);
 
 #ifdef __cplusplus
 }

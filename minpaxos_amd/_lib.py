@@ -17,7 +17,10 @@ _sz = C.c_size_t
 
 class MpxConfig(C.Structure):
     _fields_ = [("n_replicas", C.c_int32), ("mode", C.c_int32), ("kv_capacity", C.c_uint64),
-                ("kv_per_group", C.c_uint32), ("flags", C.c_uint32), ("max_groups", C.c_uint64)]
+                ("kv_per_group", C.c_uint32), ("flags", C.c_uint32), ("max_groups", C.c_uint64),
+                ("apply_chunk", C.c_uint64), ("apply_path", C.c_uint32),
+                ("apply_fast_min", C.c_uint32), ("apply_hot_min", C.c_uint32),
+                ("reserved", C.c_uint32)]
 
 
 class MpxGroupBatch(C.Structure):
@@ -95,6 +98,8 @@ SIGNATURES = {
     "mpx_stream_wait_event": (C.c_int, [_p, _p, _p]),
     "mpx_event_elapsed_ms": (C.c_int, [_p, _p, _p, C.POINTER(C.c_float)]),
     "mpx_runtime_info": (C.c_int, [C.c_char_p, _sz]),
+    "mpx_debug_kv_set_epoch": (C.c_int, [_p, C.c_uint32]),
+    "mpx_debug_kv_state": (C.c_int, [_p, _p, _sz, C.POINTER(_sz)]),
 }
 
 _lib = None

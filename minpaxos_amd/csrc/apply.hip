@@ -1,6 +1,7 @@
 // apply.hip — the engine's device KV table (clear / import / export), the sort-based apply
-// pipeline used for tables past apply_fast.hip's bin limit (and as its A/B reference, env
-// MPX_APPLY_FALLBACK=1), the dispatcher of mpx_apply, and state.ConflictBatch (A5/A6).
+// pipeline used for tables past apply_fast.hip's bin limit and small calls (and as its A/B
+// reference, mpx_config.apply_path = MPX_APPLY_SORTED), the dispatcher of mpx_apply, and
+// state.ConflictBatch (A5/A6).
 //
 // Reference: (*state.Command).Execute  src/state/state.go:77-103, applied in log order by
 // executeCommands  src/bareminpaxos/bareminpaxos.go:1066-1098; state.Conflict state.go:53-60;
@@ -59,7 +60,10 @@ __global__ void k_kv_fill(KvTable t) {
         t.keys[s] = kSentinel;
         t.state[s] = 0;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) *t.n_present = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *t.n_present = 0;
+        t.epoch[1] = 0;  // k_epoch_next's completion counter (a stale count after a fault)
+    }
 }
 
 // A new call epoch in one launch: epoch[0] = the current call epoch; when it would reach
@@ -546,47 +550,42 @@ uint64_t apply_chunk_commands(uint64_t chunk, uint64_t m) {
 }
 
 namespace {
-// Which pipeline runs a call of m commands. The partitioned pipeline has a fixed cost of about a
-// dozen dependent launches plus a pass over every bin that received records, so calls below
-// MPX_APPLY_FAST_MIN commands (default kFastMinDefault, the measured crossover) take the sort-based
-// one. env MPX_APPLY_FALLBACK=1 forces the sort-based pipeline, =0 the partitioned one (where the
-// table geometry allows it) at any size; unset = by size. Both give identical results.
+// Which pipeline runs a call of m commands (the handle's ApplyOpts). The partitioned pipeline has
+// a fixed cost of about a dozen dependent launches plus a pass over every bin that received
+// records, so AUTO sends calls below fast_min commands (default kFastMinDefault, the measured
+// crossover) to the sort-based one. SORTED / PARTITIONED force a pipeline at any size (the
+// partitioned one where the table geometry allows it). All give identical results.
 constexpr uint64_t kFastMinDefault = 16384;
-uint64_t fast_min(const KvTable& t) {  // calls of at least this many commands run partitioned
-    if (!apply_fast_ok(t)) return UINT64_MAX;
-    const char* f = getenv("MPX_APPLY_FALLBACK");
-    if (f && f[0] == '1') return UINT64_MAX;
-    if (f && f[0] == '0') return 0;
-    const char* n = getenv("MPX_APPLY_FAST_MIN");
-    return n ? strtoull(n, nullptr, 10) : kFastMinDefault;
+uint64_t fast_min(const KvTable& t, const ApplyOpts& o) {  // partitioned from this many commands
+    if (!apply_fast_ok(t) || o.path == MPX_APPLY_SORTED) return UINT64_MAX;
+    if (o.path == MPX_APPLY_PARTITIONED) return 0;
+    return o.fast_min ? o.fast_min : kFastMinDefault;
 }
-bool use_fast(const KvTable& t, uint64_t m) { return m >= fast_min(t); }
-// env MPX_APPLY_HOT_MIN: sample count (of 64K) that makes a key hot; 0 = no hot keys
-uint32_t hot_min() {
-    const char* h = getenv("MPX_APPLY_HOT_MIN");
-    return h ? (uint32_t)strtoul(h, nullptr, 10) : 5u;
+bool use_fast(const KvTable& t, const ApplyOpts& o, uint64_t m) { return m >= fast_min(t, o); }
+uint32_t hot_min(const ApplyOpts& o) {  // sample count (of 64K) that makes a key hot; 0 = none
+    return o.hot_min == MPX_APPLY_NO_HOT ? 0u : (o.hot_min ? o.hot_min : 5u);
 }
 }  // namespace
 
-uint64_t apply_work_bytes(const KvTable& t, uint64_t chunk, uint64_t m) {
-    const uint64_t C = apply_chunk_commands(chunk, m);
-    return use_fast(t, m) ? apply_fast_work_bytes(t, C) : layout(C).total;
+uint64_t apply_work_bytes(const KvTable& t, const ApplyOpts& o, uint64_t m) {
+    const uint64_t C = apply_chunk_commands(o.chunk, m);
+    return use_fast(t, o, m) ? apply_fast_work_bytes(t, C) : layout(C).total;
 }
 
 // Every m <= max_m must fit: each pipeline's need grows with m, so the largest call on either
 // side of the size switch bounds them all.
-uint64_t apply_reserve_bytes(const KvTable& t, uint64_t chunk, uint64_t max_m) {
-    const uint64_t b = apply_work_bytes(t, chunk, max_m), thr = fast_min(t);
-    return thr > 1 && thr <= max_m ? std::max(b, apply_work_bytes(t, chunk, thr - 1)) : b;
+uint64_t apply_reserve_bytes(const KvTable& t, const ApplyOpts& o, uint64_t max_m) {
+    const uint64_t b = apply_work_bytes(t, o, max_m), thr = fast_min(t, o);
+    return thr > 1 && thr <= max_m ? std::max(b, apply_work_bytes(t, o, thr - 1)) : b;
 }
 
 hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
-                        uint64_t m, int64_t* ret, uint8_t* conf, uint64_t chunk, ApplyWork& w,
+                        uint64_t m, int64_t* ret, uint8_t* conf, const ApplyOpts& o, ApplyWork& w,
                         uint32_t* err, hipStream_t stream) {
     if (!m) return hipSuccess;
-    const uint64_t C = apply_chunk_commands(chunk, m);
-    if (use_fast(t, m))
-        return launch_apply_fast(t, op, key, val, m, ret, conf, C, w, hot_min(), err, stream);
+    const uint64_t C = apply_chunk_commands(o.chunk, m);
+    if (use_fast(t, o, m))
+        return launch_apply_fast(t, op, key, val, m, ret, conf, C, w, hot_min(o), err, stream);
     // result codes carry a chunk index or a slot in 29 bits
     if (C > kPayloadMask || t.cap + 1 > kPayloadMask) return hipErrorInvalidValue;
     const WorkLayout L = layout(C);

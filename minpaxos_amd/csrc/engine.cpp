@@ -33,7 +33,7 @@ struct mpx_engine {
     std::string err;
     uint32_t* d_err = nullptr;
     unsigned long long* d_red = nullptr;
-    uint32_t* d_part = nullptr;  // tile kernels' per-workgroup partials
+    uint32_t* d_tctl = nullptr;  // tile kernels' control words (kTileCtlWords, zero between calls)
     // host-API staging
     DevBuf b[12];
     // global KV table (mpx_apply)
@@ -55,7 +55,7 @@ struct mpx_engine {
     DevBuf log_work;
     // durable-log replay staging: log bytes, records, op, key, val, last_rec, scalars
     DevBuf rp[7];
-    uint64_t apply_chunk = 0;  // commands per apply chunk (0 = kApplyChunkDefault)
+    mpx::ApplyOpts apply{};  // mpx_config.apply_* (fixed for the handle's life)
     // group-step work list (groups the fast kernel hands to the general kernel) + its count
     DevBuf worklist;
     uint32_t* d_wcount = nullptr;
@@ -145,6 +145,15 @@ int d2h(mpx_engine* e, void* h, const void* d, size_t bytes) {
         if (_c) return _c;     \
     } while (0)
 
+void free_kv(mpx::KvTable& t) {
+    if (t.keys) (void)hipFree(t.keys);
+    if (t.vals) (void)hipFree(t.vals);
+    if (t.state) (void)hipFree(t.state);
+    if (t.n_present) (void)hipFree(t.n_present);
+    if (t.epoch) (void)hipFree(t.epoch);
+    t = mpx::KvTable{};
+}
+
 int ensure_kv(mpx_engine* e) {
     if (e->kv_ready) return MPX_OK;
     uint64_t want = e->cfg.kv_capacity ? e->cfg.kv_capacity : (1ull << 20);
@@ -159,23 +168,19 @@ int ensure_kv(mpx_engine* e) {
         hipMalloc(&t.vals, (cap + 1) * 8) != hipSuccess ||
         hipMalloc(&t.state, (cap + 1) * 4) != hipSuccess ||
         hipMalloc(&t.n_present, sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&t.epoch, 2 * sizeof(uint32_t)) != hipSuccess ||
-        hipMemsetAsync(t.epoch, 0, 2 * sizeof(uint32_t), e->stream) != hipSuccess) {
+        hipMalloc(&t.epoch, 2 * sizeof(uint32_t)) != hipSuccess) {
         (void)hipGetLastError();
+        free_kv(t);
         return fail(e, MPX_E_NOMEM, "KV table allocation failed");
     }
-    // test hook: MPX_KV_EPOCH_START starts the call epoch of a new table near its wrap (kEpochMax
-    // = 2^30 calls), so a test can drive calls across it
-    if (const char* es = getenv("MPX_KV_EPOCH_START")) {
-        const uint32_t e0 = (uint32_t)strtoul(es, nullptr, 10);
-        if (hipMemcpyAsync(t.epoch, &e0, sizeof e0, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
-            hipStreamSynchronize(e->stream) != hipSuccess) {
-            (void)hipGetLastError();
-            return fail(e, MPX_E_NOMEM, "KV table epoch setup failed");
-        }
+    const hipError_t r0 = hipMemsetAsync(t.epoch, 0, 2 * sizeof(uint32_t), e->stream);
+    const hipError_t r1 = r0 == hipSuccess ? mpx::launch_kv_clear(t, e->stream) : r0;
+    if (r1 != hipSuccess) {
+        (void)hipGetLastError();
+        free_kv(t);
+        return hip_fail(e, "KV table initialisation", r1);
     }
     e->kv = t;
-    HIPCHK(e, mpx::launch_kv_clear(e->kv, e->stream));
     e->kv_ready = true;
     return MPX_OK;
 }
@@ -204,6 +209,7 @@ int mpx_open(int device, const mpx_config* cfg, mpx_engine** out) {
     *out = nullptr;
     if (cfg->n_replicas < 1 || cfg->n_replicas > MPX_MAX_REPLICAS) return MPX_E_INVAL;
     if (cfg->mode != MPX_MODE_MIN && cfg->mode != MPX_MODE_CLASSIC) return MPX_E_INVAL;
+    if (cfg->apply_path > MPX_APPLY_SMALL || cfg->flags || cfg->reserved) return MPX_E_INVAL;
     int c = 0;
     if (hipGetDeviceCount(&c) != hipSuccess || device < 0 || device >= c) {
         (void)hipGetLastError();
@@ -214,7 +220,8 @@ int mpx_open(int device, const mpx_config* cfg, mpx_engine** out) {
     e->device = device;
     e->cfg = *cfg;
     if (!e->cfg.kv_per_group) e->cfg.kv_per_group = 512;
-    if (const char* c = getenv("MPX_APPLY_CHUNK")) e->apply_chunk = strtoull(c, nullptr, 10);
+    e->apply = mpx::ApplyOpts{cfg->apply_chunk, cfg->apply_path, cfg->apply_fast_min,
+                              cfg->apply_hot_min};
     if (!e->cfg.max_groups) e->cfg.max_groups = 1ull << 20;
     if (e->cfg.kv_per_group > 1024) {
         delete e;
@@ -225,8 +232,9 @@ int mpx_open(int device, const mpx_config* cfg, mpx_engine** out) {
         hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&e->d_err, sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&e->d_red, mpx::kRedWords * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&e->d_part, (size_t)mpx::kTileGrid * mpx::kPartStride * sizeof(uint32_t)) !=
-            hipSuccess ||
+        hipMalloc(&e->d_tctl, mpx::kTileCtlWords * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(e->d_tctl, 0, mpx::kTileCtlWords * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(e->d_red, 0, mpx::kRedWords * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&e->d_wcount, mpx::kStepCtlWords * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(e->d_wcount, 0, mpx::kStepCtlWords * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&e->worklist.p, e->worklist.cap) != hipSuccess ||
@@ -263,16 +271,10 @@ int mpx_close(mpx_engine* e) {
         if (x.p) (void)hipFree(x.p);
     if (e->worklist.p) (void)hipFree(e->worklist.p);
     if (e->d_wcount) (void)hipFree(e->d_wcount);
-    if (e->kv_ready) {
-        (void)hipFree(e->kv.keys);
-        (void)hipFree(e->kv.vals);
-        (void)hipFree(e->kv.state);
-        (void)hipFree(e->kv.n_present);
-        (void)hipFree(e->kv.epoch);
-    }
+    if (e->kv_ready) free_kv(e->kv);
     if (e->d_err) (void)hipFree(e->d_err);
     if (e->d_red) (void)hipFree(e->d_red);
-    if (e->d_part) (void)hipFree(e->d_part);
+    if (e->d_tctl) (void)hipFree(e->d_tctl);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return MPX_OK;
@@ -309,12 +311,11 @@ int mpx_accept_tally(mpx_engine* e, const mpx_accept_reply* recs, size_t n, mpx_
     CK(h2d(e, e->b[0].p, recs, n * sizeof(mpx_accept_reply)));
     CK(h2d(e, e->b[1].p, st, n_inst * sizeof(mpx_inst_state)));
     CK(h2d(e, e->b[3].p, sc, (1 + N) * sizeof(int32_t)));
-    const bool want_dec = decided_out || e->cfg.mode == MPX_MODE_CLASSIC;
-    uint8_t* d_dec = want_dec ? (uint8_t*)e->b[2].p : nullptr;
+    uint8_t* d_dec = decided_out ? (uint8_t*)e->b[2].p : nullptr;
     HIPCHK(e, mpx::launch_accept_tally(e->cfg.mode, (const mpx_accept_reply*)e->b[0].p, n,
                                        (const mpx_inst_state*)e->b[1].p,
                                        (mpx_inst_state*)e->b[1].p, n_inst, inst_base, N,
-                                       (int32_t*)e->b[3].p, d_dec, e->d_red, e->d_part,
+                                       (int32_t*)e->b[3].p, d_dec, e->d_red, e->d_tctl,
                                        e->d_err, e->stream));
     CK(d2h(e, st, e->b[1].p, n_inst * sizeof(mpx_inst_state)));
     CK(d2h(e, sc, e->b[3].p, (1 + N) * sizeof(int32_t)));
@@ -332,12 +333,10 @@ int mpx_accept_tally_dev(mpx_engine* e, const mpx_accept_reply* d_recs, size_t n
     if (!e) return MPX_E_INVAL;
     if ((n && !d_recs) || (n_inst && (!d_st_in || !d_st_out)) || !d_scalars)
         return fail(e, MPX_E_INVAL, "null argument");
-    if (e->cfg.mode == MPX_MODE_CLASSIC && !d_decided)
-        return fail(e, MPX_E_INVAL, "CLASSIC mode needs d_decided (the commit watermark reads it)");
     if (n >= 0xFFFFFFFFull) return fail(e, MPX_E_UNSUPPORTED, "more than 2^32-2 records");
     HIPCHK(e, mpx::launch_accept_tally(e->cfg.mode, d_recs, n, d_st_in, d_st_out, n_inst,
                                        inst_base, e->cfg.n_replicas, d_scalars, d_decided,
-                                       e->d_red, e->d_part, e->d_err, pick(e, stream)));
+                                       e->d_red, e->d_tctl, e->d_err, pick(e, stream)));
     return MPX_OK;
 }
 
@@ -376,7 +375,7 @@ int mpx_prepare_select(mpx_engine* e, const mpx_prepare_reply* recs, size_t n, m
                                           (const mpx_prep_state*)e->b[1].p,
                                           (mpx_prep_state*)e->b[1].p, n_inst, inst_base,
                                           e->cfg.n_replicas, (int32_t*)e->b[3].p, d_prep,
-                                          e->d_part, e->d_err, e->stream));
+                                          e->d_tctl, e->d_err, e->stream));
     CK(d2h(e, st, e->b[1].p, n_inst * sizeof(mpx_prep_state)));
     CK(d2h(e, default_ballot, e->b[3].p, sizeof(int32_t)));
     if (prepared_out) CK(d2h(e, prepared_out, d_prep, n_inst));
@@ -392,7 +391,7 @@ int mpx_prepare_select_dev(mpx_engine* e, const mpx_prepare_reply* d_recs, size_
         return fail(e, MPX_E_INVAL, "null argument");
     HIPCHK(e, mpx::launch_prepare_classic(d_recs, n, d_st_in, d_st_out, n_inst, inst_base,
                                           e->cfg.n_replicas, d_default_ballot, d_prepared,
-                                          e->d_part, e->d_err, pick(e, stream)));
+                                          e->d_tctl, e->d_err, pick(e, stream)));
     return MPX_OK;
 }
 
@@ -456,7 +455,7 @@ int mpx_apply(mpx_engine* e, const uint8_t* op, const int64_t* key, const int64_
     GROW(e, e->b[9], m * 8);
     GROW(e, e->b[10], m * 8);
     GROW(e, e->b[11], m);
-    GROW(e, e->apply_work, mpx::apply_work_bytes(e->kv, e->apply_chunk, m));
+    GROW(e, e->apply_work, mpx::apply_work_bytes(e->kv, e->apply, m));
     CK(h2d(e, e->b[7].p, op, m));
     CK(h2d(e, e->b[8].p, key, m * 8));
     CK(h2d(e, e->b[9].p, val, m * 8));
@@ -464,7 +463,7 @@ int mpx_apply(mpx_engine* e, const uint8_t* op, const int64_t* key, const int64_
     uint8_t* d_conf = conf_prev ? (uint8_t*)e->b[11].p : nullptr;
     HIPCHK(e, mpx::launch_apply(e->kv, (const uint8_t*)e->b[7].p, (const int64_t*)e->b[8].p,
                                 (const int64_t*)e->b[9].p, m, (int64_t*)e->b[10].p, d_conf,
-                                e->apply_chunk, w, e->d_err, e->stream));
+                                e->apply, w, e->d_err, e->stream));
     CK(d2h(e, ret, e->b[10].p, m * 8));
     if (conf_prev) CK(d2h(e, conf_prev, d_conf, m));
     return finish(e);
@@ -475,7 +474,7 @@ int mpx_apply_reserve(mpx_engine* e, size_t max_cmds) {
     if (max_cmds >= (1ull << 31)) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 commands");
     CK(begin(e));
     CK(ensure_kv(e));
-    GROW(e, e->apply_work, mpx::apply_reserve_bytes(e->kv, e->apply_chunk, max_cmds));
+    GROW(e, e->apply_work, mpx::apply_reserve_bytes(e->kv, e->apply, max_cmds));
     return finish(e);
 }
 
@@ -484,13 +483,13 @@ int mpx_apply_dev(mpx_engine* e, const uint8_t* d_op, const int64_t* d_key, cons
     if (!e) return MPX_E_INVAL;
     if (m && (!d_op || !d_key || !d_val || !d_ret)) return fail(e, MPX_E_INVAL, "null argument");
     if (m >= (1ull << 31)) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 commands per call");
-    if (!e->kv_ready || e->apply_work.cap < mpx::apply_work_bytes(e->kv, e->apply_chunk, m))
+    if (!e->kv_ready || e->apply_work.cap < mpx::apply_work_bytes(e->kv, e->apply, m))
         return fail(e, MPX_E_INVAL,
                     "mpx_apply_dev: call mpx_apply_reserve(m) first (the dev entry point never "
                     "allocates)");
     mpx::ApplyWork w{e->apply_work.p, e->apply_work.cap};
     HIPCHK(e, mpx::launch_apply(e->kv, d_op, d_key, d_val, m, d_ret, d_conf_prev,
-                                e->apply_chunk, w, e->d_err, pick(e, stream)));
+                                e->apply, w, e->d_err, pick(e, stream)));
     return MPX_OK;
 }
 
@@ -1110,6 +1109,27 @@ int mpx_replay_durable(mpx_engine* e, const uint8_t* log, size_t len, int32_t in
     if (rc == MPX_E_NIL_INSTANCE)
         return fail(e, rc, "a durable record's instNo is outside [0, inst_cap)");
     return rc;
+}
+
+// ---- diagnostics (test-only; never called on the product path) -----------------------------
+int mpx_debug_kv_set_epoch(mpx_engine* e, uint32_t epoch) {
+    if (!e) return MPX_E_INVAL;
+    if (epoch < 1 || epoch >= mpx::kKvEpochMax)
+        return fail(e, MPX_E_INVAL, "epoch must lie in [1, 2^30)");
+    CK(begin(e));
+    CK(ensure_kv(e));
+    HIPCHK(e, hipMemcpyAsync(e->kv.epoch, &epoch, sizeof epoch, hipMemcpyHostToDevice, e->stream));
+    return finish(e);
+}
+
+int mpx_debug_kv_state(mpx_engine* e, uint32_t* state, size_t cap, size_t* n) {
+    if (!e) return MPX_E_INVAL;
+    if (!n || (cap && !state)) return fail(e, MPX_E_INVAL, "null or invalid argument");
+    CK(begin(e));
+    CK(ensure_kv(e));
+    *n = (size_t)e->kv.cap + 1;
+    CK(d2h(e, state, e->kv.state, std::min<size_t>(cap, *n) * sizeof(uint32_t)));
+    return finish(e);
 }
 
 // ---- device memory, streams, events (the engine's HIP runtime) --------------------------------

@@ -18,15 +18,19 @@ constexpr uint32_t kErrInval = 16u;  // other malformed input (offsets, sizes)
 
 // reduction scratch: kRedWords u64 per engine
 constexpr int kRedWords = 64;
-// per-workgroup partials of the tile kernels (tile.hpp): at most kTileGrid workgroups, each
-// writing kPartStride u32
+// the tile kernels (tile.hpp) run a persistent grid of at most kTileGrid workgroups; their
+// control words (kTileCtlWords u32, engine-owned, zeroed at mpx_open) carry the call's
+// device-scope maxima and the last-workgroup ticket, and are back to zero after every call
 constexpr int kTileGrid = 2048;
-constexpr int kPartStride = 32;
+constexpr int kTileCtlWords = 64;
+// workgroups of a persistent launch of `kernel` (block threads) over `tiles` units: the number
+// resident at once on the device (occupancy x CUs, cached per kernel), at most kTileGrid
+uint32_t resident_grid(const void* kernel, int block, uint64_t tiles);
 
 hipError_t launch_accept_tally(int mode, const mpx_accept_reply* recs, uint64_t n,
                                const mpx_inst_state* st_in, mpx_inst_state* st_out,
                                uint64_t n_inst, int32_t base, int32_t nrep, int32_t* scalars,
-                               uint8_t* decided, unsigned long long* red, uint32_t* part,
+                               uint8_t* decided, unsigned long long* red, uint32_t* ctl,
                                uint32_t* err, hipStream_t stream);
 
 hipError_t launch_committed_prefix(const mpx_inst_state* st, uint64_t n_inst, int32_t base,
@@ -35,7 +39,7 @@ hipError_t launch_committed_prefix(const mpx_inst_state* st, uint64_t n_inst, in
 hipError_t launch_prepare_classic(const mpx_prepare_reply* recs, uint64_t n,
                                   const mpx_prep_state* st_in, mpx_prep_state* st_out,
                                   uint64_t n_inst, int32_t base, int32_t nrep,
-                                  int32_t* default_ballot, uint8_t* prepared, uint32_t* part,
+                                  int32_t* default_ballot, uint8_t* prepared, uint32_t* ctl,
                                   uint32_t* err, hipStream_t stream);
 
 hipError_t launch_prepare_min(const mpx_prepare_reply_min* recs, uint64_t n,
@@ -67,23 +71,32 @@ struct KvTable {
     uint64_t cap;        // power of two, >= 1024
     uint32_t lgnb;       // log2(cap / 256): buckets of 256 slots (kvtab.hpp)
     unsigned long long* n_present;  // device counter
-    uint32_t* epoch;     // device: [0] call epoch of mpx_apply, [1] wrap flag
+    uint32_t* epoch;     // device: [0] call epoch of mpx_apply (1 .. kKvEpochMax-1), [1] k_epoch_next's
+                         // completion counter (0 between calls)
 };
+
+constexpr uint32_t kKvEpochMax = 1u << 30;  // = kvtab.hpp kEpochMax (state bits 2..31)
 
 struct ApplyWork {      // scratch sized for m commands (see apply_work_bytes)
     void* base;
     uint64_t bytes;
 };
+// the handle's apply settings (mpx_config.apply_*)
+struct ApplyOpts {
+    uint64_t chunk;     // commands per chunk, 0 = kApplyChunkDefault
+    uint32_t path;      // MPX_APPLY_AUTO / _SMALL / _SORTED / _PARTITIONED
+    uint32_t fast_min;  // AUTO: partitioned from this many commands, 0 = kFastMinDefault
+    uint32_t hot_min;   // partitioned: hot-key sample threshold, 0 = 5, MPX_APPLY_NO_HOT = none
+};
 // commands per apply chunk (0 = default): bounds the pipeline's scratch (34 B per command on the
-// partitioned path, 48 B on the sort-based one);
-// env MPX_APPLY_CHUNK overrides it per engine (tests use tiny chunks to cross boundaries)
+// partitioned path, 48 B on the sort-based one)
 constexpr uint64_t kApplyChunkDefault = 1ull << 26;
 uint64_t apply_chunk_commands(uint64_t chunk, uint64_t m);
-uint64_t apply_work_bytes(const KvTable& t, uint64_t chunk, uint64_t m);
+uint64_t apply_work_bytes(const KvTable& t, const ApplyOpts& o, uint64_t m);
 // a new call epoch for the table (both apply pipelines); zeroes *n_miss when given
 hipError_t launch_epoch_next(KvTable& t, uint32_t* n_miss, hipStream_t stream);
 // scratch for any call of at most max_m commands (mpx_apply_reserve)
-uint64_t apply_reserve_bytes(const KvTable& t, uint64_t chunk, uint64_t max_m);
+uint64_t apply_reserve_bytes(const KvTable& t, const ApplyOpts& o, uint64_t max_m);
 // the partitioned pipeline (apply_fast.hip): tables of at most 1024 bins of 16 buckets
 bool apply_fast_ok(const KvTable& t);
 uint64_t apply_fast_work_bytes(const KvTable& t, uint64_t c);
@@ -91,7 +104,7 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
                              uint64_t m, int64_t* ret, uint8_t* conf, uint64_t C, ApplyWork& w,
                              uint32_t hot_min, uint32_t* err, hipStream_t stream);
 hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
-                        uint64_t m, int64_t* ret, uint8_t* conf, uint64_t chunk, ApplyWork& w,
+                        uint64_t m, int64_t* ret, uint8_t* conf, const ApplyOpts& o, ApplyWork& w,
                         uint32_t* err, hipStream_t stream);
 hipError_t launch_kv_clear(KvTable& t, hipStream_t stream);
 hipError_t launch_kv_import(KvTable& t, const int64_t* keys, const int64_t* vals, uint64_t n,

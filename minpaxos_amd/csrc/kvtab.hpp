@@ -18,7 +18,7 @@ constexpr int kLgSB = 8;
 // epoch (word >> 2) was a PUT. Epochs start at 1, so a cleared word (0) is "untouched".
 constexpr uint32_t kPresent = 1u;
 constexpr uint32_t kLastPut = 2u;
-constexpr uint32_t kEpochMax = 1u << 30;
+constexpr uint32_t kEpochMax = kKvEpochMax;
 
 __device__ __forceinline__ uint64_t hash64(uint64_t x) {
     x ^= x >> 30;

@@ -22,14 +22,18 @@
 
 namespace mpx {
 
-// CLASSIC prepare of one instance log: tile_walk (tile.hpp) gives every lane one instance and its
-// replies in arrival order, and the lane runs paxos.go:580-627 on each with the 32-byte state
-// in registers. defaultBallot (:606-608) is a max over the newly prepared instances' ballots:
-// per workgroup an LDS max, then one partial per workgroup and a one-block reduction.
+// CLASSIC prepare of one instance log, ONE launch: tile_walk (tile.hpp) gives every lane one
+// instance and its replies in arrival order, and the lane runs paxos.go:580-627 on each with the
+// 32-byte state in registers. defaultBallot (:606-608) is a max over the newly prepared
+// instances' ballots: per workgroup an LDS max, one device-scope max per workgroup into the
+// control words, and the workgroup that finishes last (ticket) raises defaultBallot and resets
+// them. Instances without replies get prepared = 0 in the gap pass (no memset).
+// Control words: [0] ticket, [1] ballot key (ballot ^ 0x80000000, 0 = none).
 __global__ __launch_bounds__(kTileBlock) void k_prepare_tile(
     const mpx_prepare_reply* __restrict__ recs, uint64_t n, const mpx_prep_state* __restrict__ st_in,
     mpx_prep_state* __restrict__ st_out, uint64_t n_inst, int32_t base, int32_t half,
-    uint32_t* __restrict__ part, uint8_t* __restrict__ prepared, uint32_t* err) {
+    int32_t* __restrict__ default_ballot, uint32_t* __restrict__ ctl, uint8_t* __restrict__ prepared,
+    uint32_t* err) {
     __shared__ TileLds S;
     __shared__ uint32_t red;
     const int t = threadIdx.x, l = lane_id();
@@ -38,7 +42,8 @@ __global__ __launch_bounds__(kTileBlock) void k_prepare_tile(
     const int4* r4 = reinterpret_cast<const int4*>(recs);
     const int4* s4 = reinterpret_cast<const int4*>(st_in);
     int4* o4 = reinterpret_cast<int4*>(st_out);
-    tile_walk(S, r4, n, err, [&](uint32_t a, uint32_t cnt, uint64_t after, uint64_t oend, bool own) {
+    tile_walk(S, r4, n, err, [&](uint32_t a, uint32_t cnt, uint64_t after, uint64_t oend, bool own,
+                                 int64_t nxt, bool first) {
         const int32_t inst = own ? S.rec[a].x : 0;
         const int64_t idx = (int64_t)inst - base;
         const bool inwin = own && idx >= 0 && (uint64_t)idx < n_inst;
@@ -92,6 +97,9 @@ __global__ __launch_bounds__(kTileBlock) void k_prepare_tile(
             st_stream(o4 + 2 * idx + 1, B);
             if (prepared) st_stream(prepared + idx, (uint8_t)(prep ? 1 : 0));
         }
+        if (prepared)  // instances without replies (and nil ones between them) stay unprepared
+            tile_gaps(own, idx, nxt == kNoNext ? INT64_MAX : nxt - base, first, n_inst,
+                      [&](uint64_t q) { prepared[q] = 0; });
         // defaultBallot = max(defaultBallot, inst.ballot) over newly prepared instances
         uint32_t key = (live_inst && prep) ? ((uint32_t)A.x ^ 0x80000000u) : 0u;
 #pragma unroll
@@ -101,25 +109,12 @@ __global__ __launch_bounds__(kTileBlock) void k_prepare_tile(
         }
         if (l == 0 && key) atomicMax(&red, key);
     });
-    __syncthreads();
-    if (t == 0) part[(uint64_t)blockIdx.x * kPartStride] = red;
     if (ebits) raise_err(err, ebits);
-}
-
-__global__ void k_prepare_reduce(const uint32_t* __restrict__ part, uint32_t n_part,
-                                 int32_t* default_ballot) {
-    const int l = lane_id();
-    uint32_t m = 0;
-    for (uint32_t i = l; i < n_part; i += kWave) {
-        const uint32_t x = part[(uint64_t)i * kPartStride];
-        m = m > x ? m : x;
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint32_t x = (uint32_t)__shfl_xor((int)m, d);
-        m = m > x ? m : x;
-    }
-    if (l == 0 && m) {
+    __syncthreads();
+    if (t == 0 && red) atomic_max_done(&ctl[1], red);
+    if (!last_workgroup(&ctl[0]) || t != 0) return;
+    const uint32_t m = atomic_take(&ctl[1]);
+    if (m) {
         const int32_t b = (int32_t)(m ^ 0x80000000u);
         if (b > *default_ballot) *default_ballot = b;
     }
@@ -128,16 +123,16 @@ __global__ void k_prepare_reduce(const uint32_t* __restrict__ part, uint32_t n_p
 hipError_t launch_prepare_classic(const mpx_prepare_reply* recs, uint64_t n,
                                   const mpx_prep_state* st_in, mpx_prep_state* st_out,
                                   uint64_t n_inst, int32_t base, int32_t nrep,
-                                  int32_t* default_ballot, uint8_t* prepared, uint32_t* part,
+                                  int32_t* default_ballot, uint8_t* prepared, uint32_t* ctl,
                                   uint32_t* err, hipStream_t stream) {
-    if (prepared && n_inst) (void)hipMemsetAsync(prepared, 0, n_inst, stream);
-    if (n) {
-        const uint64_t tiles = (n + kTileRecs - 1) / kTileRecs;
-        const uint32_t grid = (uint32_t)(tiles < (uint64_t)kTileGrid ? tiles : kTileGrid);
-        k_prepare_tile<<<grid, kTileBlock, 0, stream>>>(recs, n, st_in, st_out, n_inst, base,
-                                                         nrep >> 1, part, prepared, err);
-        k_prepare_reduce<<<1, kWave, 0, stream>>>(part, grid, default_ballot);
+    if (!n) {  // no replies: nothing changes, no instance prepared
+        if (prepared && n_inst) (void)hipMemsetAsync(prepared, 0, n_inst, stream);
+        return hipGetLastError();
     }
+    const uint64_t tiles = (n + kTileRecs - 1) / kTileRecs;
+    const uint32_t grid = resident_grid((const void*)k_prepare_tile, kTileBlock, tiles);
+    k_prepare_tile<<<grid, kTileBlock, 0, stream>>>(recs, n, st_in, st_out, n_inst, base,
+                                                     nrep >> 1, default_ballot, ctl, prepared, err);
     return hipGetLastError();
 }
 

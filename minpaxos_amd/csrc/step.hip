@@ -1107,7 +1107,6 @@ hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
 __global__ __launch_bounds__(256) void k_step_totals(mpx_group_batch b, unsigned long long* totals,
                                                      uint32_t* ctl) {
     unsigned long long* acc = reinterpret_cast<unsigned long long*>(ctl + 4);
-    __shared__ bool last;
     __shared__ unsigned long long red[3][kStepBlock / kWave];
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long d = 0, xi = 0, xc = 0;
@@ -1137,19 +1136,10 @@ __global__ __launch_bounds__(256) void k_step_totals(mpx_group_batch b, unsigned
     if (threadIdx.x < 3) {
         unsigned long long v = 0;
         for (int k = 0; k < kStepBlock / kWave; ++k) v += red[threadIdx.x][k];
-        if (v) atomicAdd(acc + threadIdx.x, v);
+        if (v) atomic_add_done(acc + threadIdx.x, v);
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();  // this block's sums before its ticket
-        last = atomicAdd(ctl + 10, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (last && threadIdx.x < 3) {
-        __threadfence();
-        totals[threadIdx.x] = atomicExch(acc + threadIdx.x, 0ull);
-        if (threadIdx.x == 0) ctl[10] = 0;
-    }
+    if (last_workgroup(ctl + 10) && threadIdx.x < 3)
+        totals[threadIdx.x] = atomic_take(acc + threadIdx.x);
 }
 
 hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, uint32_t* ctl,

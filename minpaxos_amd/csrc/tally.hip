@@ -1,33 +1,48 @@
 // tally.hip — accept tally kernels for one instance log (configs 2 and the single-group API).
+#include <mutex>
+
 #include "kernels.hpp"
 #include "tally.hpp"
 #include "tile.hpp"
 
 namespace mpx {
 
-// Accept tally of one instance log: tile_walk (tile.hpp) hands every lane one instance and its
-// replies in arrival order; the lane applies handleAcceptReply to each (state in registers).
+// Accept tally of one instance log, ONE launch: tile_walk (tile.hpp) hands every lane one
+// instance and its replies in arrival order; the lane applies handleAcceptReply to each (state in
+// registers).
 //   MIN      bareminpaxos.go:1023-1053: OK replies only, no status check
 //   CLASSIC  paxos.go:634-673: replies to instances not PREPARED/ACCEPTED are ignored
 // The "last assignment wins" scalars of MIN (committedUpTo :1048, peerCommits[id] :1050) come
 // from the highest instance that assigns them (instances ascend in array order; all of an
 // instance's assignments of one scalar write the same value): per round a wave ballot finds the
-// highest lane, one LDS max per wave, one partial per workgroup, a final one-block reduction.
-// Window-relative keys idx+1 (0 = none) keep them unsigned.
-constexpr int kRedFirstBad = 1 + MPX_MAX_REPLICAS;
-
+// highest lane, one LDS max per wave, one device-scope max per workgroup. CLASSIC's
+// updateCommittedUpTo (paxos.go:259-264) is the first instance >= committedUpTo+1 whose final
+// status is not COMMITTED: a minimum over the owned instances (final status in registers) and
+// the instances without replies (their input status, read in the gap pass). Window-relative
+// keys idx+1 (0 = none) keep the maxima unsigned; the minimum is kept as a max of ~idx.
+// The workgroup that finishes last (ticket) turns the maxima into the scalars and resets the
+// control words, so a call is one kernel and no memset: the decided flags of instances without
+// replies are written 0 in the gap pass.
+// Control words (engine-owned, zero between calls): [0] ticket, [1..1+N) MIN keys / [1] CLASSIC
+// "some instance committed", [2] CLASSIC ~first_bad.
 template <int MODE>
 __global__ __launch_bounds__(kTileBlock) void k_accept_tile(
     const mpx_accept_reply* __restrict__ recs, uint64_t n, const mpx_inst_state* __restrict__ st_in,
     mpx_inst_state* __restrict__ st_out, uint64_t n_inst, int32_t base, int32_t half, int32_t nrep,
-    uint32_t* __restrict__ part, uint8_t* __restrict__ decided, uint32_t* err) {
+    int32_t* __restrict__ scalars, uint32_t* __restrict__ ctl, uint8_t* __restrict__ decided,
+    uint32_t* err) {
     __shared__ TileLds S;
     __shared__ uint32_t red[1 + MPX_MAX_REPLICAS];
     const int t = threadIdx.x, l = lane_id();
     if (t <= MPX_MAX_REPLICAS) red[t] = 0;
     uint32_t ebits = 0;
+    // CLASSIC: updateCommittedUpTo scans from committedUpTo+1 (the call's input; the last
+    // workgroup writes scalars[0] only after every workgroup has read it)
+    const int64_t j0 = MODE == MPX_MODE_CLASSIC ? (int64_t)scalars[0] + 1 - base : 0;
+    uint32_t fb_key = 0;  // ~(first non-committed instance >= j0) seen by this lane, 0 = none
     const int4* r4 = reinterpret_cast<const int4*>(recs);
-    tile_walk(S, r4, n, err, [&](uint32_t a, uint32_t cnt, uint64_t after, uint64_t oend, bool own) {
+    tile_walk(S, r4, n, err, [&](uint32_t a, uint32_t cnt, uint64_t after, uint64_t oend, bool own,
+                                 int64_t nxt, bool first) {
         const int32_t inst = own ? S.rec[a].x : 0;
         const int64_t idx = (int64_t)inst - base;
         const bool inwin = own && idx >= 0 && (uint64_t)idx < n_inst;
@@ -81,7 +96,20 @@ __global__ __launch_bounds__(kTileBlock) void k_accept_tile(
         if (inwin) {
             st_stream(reinterpret_cast<int4*>(st_out) + idx, st);
             if (decided) st_stream(decided + idx, (uint8_t)(deci ? 1 : 0));
+            if (MODE == MPX_MODE_CLASSIC && idx >= j0 && st.x != MPX_COMMITTED) {
+                const uint32_t k = ~(uint32_t)idx;
+                fb_key = fb_key > k ? fb_key : k;
+            }
         }
+        // instances without replies: not decided; CLASSIC also reads their (final = input)
+        // status for updateCommittedUpTo, until this lane has a smaller candidate
+        tile_gaps(own, idx, nxt == kNoNext ? INT64_MAX : nxt - base, first, n_inst,
+                  [&](uint64_t q) {
+                      if (decided) decided[q] = 0;
+                      if (MODE == MPX_MODE_CLASSIC && (int64_t)q >= j0 && ~(uint32_t)q > fb_key &&
+                          st_in[q].status != MPX_COMMITTED)
+                          fb_key = ~(uint32_t)q;
+                  });
         const uint32_t key = (uint32_t)(idx + 1);
         if (MODE == MPX_MODE_MIN) {
             const unsigned long long dm = __ballot(inwin && deci);
@@ -100,38 +128,36 @@ __global__ __launch_bounds__(kTileBlock) void k_accept_tile(
             if (__ballot(inwin && deci) && l == 0) atomicMax(&red[0], 1u);
         }
     });
-    __syncthreads();
-    if (t <= nrep) part[(uint64_t)blockIdx.x * kPartStride + t] = red[t];
-    if (ebits) raise_err(err, ebits);
-}
-
-// reduce the workgroups' partials; MIN: write committedUpTo / peerCommits; CLASSIC: set red[0]
-// (some instance committed) and red[kRedFirstBad] for k_classic_first_bad
-template <int MODE>
-__global__ void k_accept_reduce(const uint32_t* __restrict__ part, uint32_t n_part, int32_t nrep,
-                                int32_t base, uint64_t n_inst, int32_t* scalars,
-                                unsigned long long* red) {
-    const int l = lane_id();  // each wave takes every (blockDim/64)-th scalar
-    for (int w = threadIdx.x / kWave; w <= nrep; w += blockDim.x / kWave) {
-        uint32_t m = 0;
-        for (uint32_t i = l; i < n_part; i += kWave) {
-            const uint32_t x = part[(uint64_t)i * kPartStride + w];
-            m = m > x ? m : x;
-        }
+    if (MODE == MPX_MODE_CLASSIC) {
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) {
-            const uint32_t x = (uint32_t)__shfl_xor((int)m, d);
-            m = m > x ? m : x;
+            const uint32_t x = (uint32_t)__shfl_xor((int)fb_key, d);
+            fb_key = fb_key > x ? fb_key : x;
         }
-        if (l != 0) continue;
-        if (MODE == MPX_MODE_MIN) {
-            if (m) scalars[w] = (int32_t)((int64_t)base + m - 1 - (w ? 1 : 0));  // peerCommits: inst-1
-        } else if (w == 0) {
-            red[0] = m;
-            red[kRedFirstBad] = n_inst;
-        }
+        if (l == 0 && fb_key) atomicMax(&red[1], fb_key);
+    }
+    if (ebits) raise_err(err, ebits);
+    __syncthreads();
+    // this workgroup's maxima into the call's (device scope), then its ticket
+    const int nw = MODE == MPX_MODE_MIN ? 1 + nrep : 2;
+    if (t < nw && red[t]) atomic_max_done(&ctl[1 + t], red[t]);
+    if (!last_workgroup(&ctl[0])) return;
+    if (t < nw) red[t] = atomic_take(&ctl[1 + t]);  // read and reset for the next call
+    __syncthreads();
+    if (t != 0) return;
+    if (MODE == MPX_MODE_MIN) {
+        for (int w = 0; w <= nrep; ++w)  // committedUpTo = inst; peerCommits[id] = inst - 1
+            if (red[w]) scalars[w] = (int32_t)((int64_t)base + red[w] - 1 - (w ? 1 : 0));
+    } else if (red[0] && j0 >= 0 && (uint64_t)j0 < n_inst) {
+        // some instance committed: committedUpTo = first non-committed - 1 (n_inst if none)
+        const uint64_t fb = red[1] ? (uint64_t)~red[1] : n_inst;
+        scalars[0] = (int32_t)(base + (int64_t)fb - 1);
     }
 }
+
+// mpx_committed_prefix's reduction words: [0] some instance counts as committed, then the
+// first non-committed instance (a running minimum)
+constexpr int kRedFirstBad = 1 + MPX_MAX_REPLICAS;
 
 __global__ void k_tally_init(unsigned long long* red, uint64_t n_inst) {
     const int t = threadIdx.x;
@@ -139,9 +165,9 @@ __global__ void k_tally_init(unsigned long long* red, uint64_t n_inst) {
     if (t == kRedFirstBad) red[t] = n_inst;
 }
 
-// CLASSIC updateCommittedUpTo (paxos.go:259-264) over the final statuses: find the first
-// instance >= committedUpTo+1 that is not COMMITTED (final COMMITTED <=> st_in COMMITTED or
-// decided in this call).
+// CLASSIC updateCommittedUpTo (paxos.go:259-264) over a status window (mpx_committed_prefix):
+// find the first instance >= committedUpTo+1 that is not COMMITTED (final COMMITTED <=> st
+// COMMITTED or decided).
 // The first non-committed instance is almost always a few instances past committedUpTo, so one
 // block scans the head window [j0, j0 + kHeadWindow) in order and stops at the first hit; the
 // grid-wide kernel below then covers the rest of the window only if the head found nothing.
@@ -197,54 +223,68 @@ __global__ __launch_bounds__(256) void k_classic_first_bad(
     }
 }
 
-template <int MODE>
-__global__ void k_tally_finalize(const unsigned long long* __restrict__ red, int32_t* scalars,
-                                 int32_t nrep, uint64_t n_inst, int32_t base) {
-    if (threadIdx.x != 0) return;
-    if (MODE == MPX_MODE_MIN) {
-        if (red[0]) scalars[0] = (int32_t)(uint32_t)(red[0] & 0xffffffffull);
-        for (int j = 0; j < nrep; ++j)
-            if (red[1 + j]) scalars[1 + j] = (int32_t)(uint32_t)(red[1 + j] & 0xffffffffull);
-    } else {
-        if (red[0] == 0) return;
-        const int64_t j0 = (int64_t)scalars[0] + 1 - base;
-        if (j0 < 0 || (uint64_t)j0 >= n_inst) return;
-        const uint64_t fb = red[kRedFirstBad];  // first non-committed (n_inst if none)
-        scalars[0] = (int32_t)(base + (int64_t)fb - 1);
+__global__ void k_prefix_finalize(const unsigned long long* __restrict__ red, int32_t* scalars,
+                                  uint64_t n_inst, int32_t base) {
+    if (threadIdx.x != 0 || red[0] == 0) return;
+    const int64_t j0 = (int64_t)scalars[0] + 1 - base;
+    if (j0 < 0 || (uint64_t)j0 >= n_inst) return;
+    const uint64_t fb = red[kRedFirstBad];  // first non-committed (n_inst if none)
+    scalars[0] = (int32_t)(base + (int64_t)fb - 1);
+}
+
+uint32_t resident_grid(const void* kernel, int block, uint64_t tiles) {
+    // the kernels are the engine's own, one gfx950 device type: per kernel, the count is cached
+    static std::mutex mu;
+    static const void* keys[16];
+    static uint32_t vals[16];
+    static int used = 0;
+    uint32_t g = 0;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (int i = 0; i < used; ++i)
+            if (keys[i] == kernel) g = vals[i];
+        if (!g) {
+            int dev = 0, nb = 0, cus = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, block, 0);
+            (void)hipGetLastError();
+            const uint64_t r = (uint64_t)(nb > 0 ? nb : 1) * (uint64_t)(cus > 0 ? cus : 256);
+            g = (uint32_t)(r < (uint64_t)kTileGrid ? r : kTileGrid);
+#ifdef MPX_TILE_GRID  // A/B builds: a fixed grid
+            g = MPX_TILE_GRID;
+#endif
+            if (used < 16) {
+                keys[used] = kernel;
+                vals[used++] = g;
+            }
+        }
     }
+    return (uint32_t)(tiles < g ? (tiles ? tiles : 1) : g);
 }
 
 hipError_t launch_accept_tally(int mode, const mpx_accept_reply* recs, uint64_t n,
                                const mpx_inst_state* st_in, mpx_inst_state* st_out,
                                uint64_t n_inst, int32_t base, int32_t nrep, int32_t* scalars,
-                               uint8_t* decided, unsigned long long* red, uint32_t* part,
+                               uint8_t* decided, unsigned long long* red, uint32_t* ctl,
                                uint32_t* err, hipStream_t stream) {
     const int32_t half = nrep >> 1;
-    if (decided && n_inst) (void)hipMemsetAsync(decided, 0, n_inst, stream);
     const uint64_t tiles = (n + kTileRecs - 1) / kTileRecs;
-    const uint32_t grid = (uint32_t)(tiles < (uint64_t)kTileGrid ? (tiles ? tiles : 1) : kTileGrid);
-    const unsigned rblock = (unsigned)(kWave * (1 + nrep) < 256 ? kWave * (1 + nrep) : 256);
-    if (mode == MPX_MODE_MIN) {
-        k_accept_tile<MPX_MODE_MIN><<<grid, kTileBlock, 0, stream>>>(
-            recs, n, st_in, st_out, n_inst, base, half, nrep, part, decided, err);
-        k_accept_reduce<MPX_MODE_MIN><<<1, rblock, 0, stream>>>(part, grid, nrep, base, n_inst,
-                                                                scalars, red);
-    } else {
-        k_accept_tile<MPX_MODE_CLASSIC><<<grid, kTileBlock, 0, stream>>>(
-            recs, n, st_in, st_out, n_inst, base, half, nrep, part, decided, err);
-        k_accept_reduce<MPX_MODE_CLASSIC><<<1, kWave, 0, stream>>>(part, grid, 0, base, n_inst,
-                                                                   scalars, red);
-        if (n_inst) {
-            uint64_t blocks = (n_inst + 255) / 256;
-            if (blocks > 2048) blocks = 2048;
-            k_classic_first_bad_head<<<1, 256, 0, stream>>>(st_in, decided, n_inst, base,
-                                                            scalars, red);
-            k_classic_first_bad<<<dim3((unsigned)blocks), 256, 0, stream>>>(st_in, decided, n_inst,
-                                                                             base, scalars, red);
-        }
-        k_tally_finalize<MPX_MODE_CLASSIC><<<1, 64, 0, stream>>>(red, scalars, nrep, n_inst,
-                                                                 base);
+    if (n == 0) {
+        // no replies: nothing changes but the decided flags (all 0)
+        if (decided && n_inst) (void)hipMemsetAsync(decided, 0, n_inst, stream);
+        return hipGetLastError();
     }
+    if (mode == MPX_MODE_MIN) {
+        const uint32_t grid = resident_grid((const void*)k_accept_tile<MPX_MODE_MIN>, kTileBlock, tiles);
+        k_accept_tile<MPX_MODE_MIN><<<grid, kTileBlock, 0, stream>>>(
+            recs, n, st_in, st_out, n_inst, base, half, nrep, scalars, ctl, decided, err);
+    } else {
+        const uint32_t grid = resident_grid((const void*)k_accept_tile<MPX_MODE_CLASSIC>, kTileBlock, tiles);
+        k_accept_tile<MPX_MODE_CLASSIC><<<grid, kTileBlock, 0, stream>>>(
+            recs, n, st_in, st_out, n_inst, base, half, nrep, scalars, ctl, decided, err);
+    }
+    (void)red;
     return hipGetLastError();
 }
 
@@ -262,7 +302,7 @@ hipError_t launch_committed_prefix(const mpx_inst_state* st, uint64_t n_inst, in
         k_classic_first_bad<<<dim3((unsigned)blocks), 256, 0, stream>>>(st, nullptr, n_inst, base,
                                                                          scalars, red);
     }
-    k_tally_finalize<MPX_MODE_CLASSIC><<<1, 64, 0, stream>>>(red, scalars, 0, n_inst, base);
+    k_prefix_finalize<<<1, 64, 0, stream>>>(red, scalars, n_inst, base);
     return hipGetLastError();
 }
 

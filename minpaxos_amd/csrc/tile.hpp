@@ -29,18 +29,24 @@ struct TileLds {
     uint32_t wcnt[kTilePer * kTileWaves];  // heads per (register k, wave), then their offsets
     uint32_t nh;                         // owned instances in the tile
     uint64_t oend;                       // end of the last owned instance's overhang
+    int64_t onext;                       // instance of the record at oend (kNoNext: none)
 };
+
+constexpr int64_t kNoNext = INT64_MAX;  // no record follows the instance in the log
 
 __device__ __forceinline__ int4 tile_load(const int4* __restrict__ recs, uint64_t n, uint64_t p) {
     return p < n ? ld_stream(recs + p) : make_int4(0, 0, 0, 0);
 }
 
-// Runs body(pos_first, count, overhang_end, t_round) for every owned instance of every tile this
-// workgroup takes. Records of the instance are S.rec[pos_first .. pos_first+count) followed, for
-// the tile's last instance, by global records [tile_end, overhang_end). Every lane of the
-// workgroup calls `body` the same number of times per tile (rounds of 256 instances; lanes
-// without an instance in a round get count = 0), so `body` may use wave-level ballots.
-// `err` receives kErrOrder when instances are not ascending.
+// Runs body(pos_first, count, tile_end, overhang_end, own, next_inst, first) for every owned
+// instance of every tile this workgroup takes. Records of the instance are
+// S.rec[pos_first .. pos_first+count) followed, for the tile's last instance, by global records
+// [tile_end, overhang_end). next_inst is the instance of the next record in the log after the
+// instance's records (kNoNext after the last one) and `first` marks the instance of the log's
+// first record: together they tell a lane which instances without records border its own
+// (tile_gaps). Every lane of the workgroup calls `body` the same number of times per tile
+// (rounds of 256 instances; lanes without an instance in a round get count = 0), so `body` may
+// use wave-level ballots. `err` receives kErrOrder when instances are not ascending.
 template <typename Body>
 __device__ __forceinline__ void tile_walk(TileLds& S, const int4* __restrict__ recs, uint64_t n,
                                           uint32_t* err, Body&& body) {
@@ -102,19 +108,26 @@ __device__ __forceinline__ void tile_walk(TileLds& S, const int4* __restrict__ r
         // instance ends, 64 records per step
         if (w == 0) {
             uint64_t oend = after;
+            int64_t onext = after < n ? (int64_t)after_inst : kNoNext;
             if (after < n && cnt && after_inst == S.rec[cnt - 1].x) {
                 const int32_t inst = after_inst;
                 for (uint64_t q = after + 1;; q += kWave) {
                     const uint64_t p = q + l;
-                    const bool stop = p >= n || recs[p].x != inst;
+                    const int32_t pi = p < n ? recs[p].x : 0;
+                    const bool stop = p >= n || pi != inst;
                     const unsigned long long m = __ballot(stop);
                     if (m) {
-                        oend = q + (uint64_t)__ffsll((long long)m) - 1;
+                        const int src = __ffsll((long long)m) - 1;
+                        oend = q + (uint64_t)src;
+                        onext = oend < n ? (int64_t)__builtin_amdgcn_readlane(pi, src) : kNoNext;
                         break;
                     }
                 }
             }
-            if (l == 0) S.oend = oend;
+            if (l == 0) {
+                S.oend = oend;
+                S.onext = onext;
+            }
         }
 #pragma unroll
         for (int k = 0; k < kTilePer; ++k) {
@@ -124,19 +137,58 @@ __device__ __forceinline__ void tile_walk(TileLds& S, const int4* __restrict__ r
         __syncthreads();
         const uint32_t nh = S.nh;
         const uint64_t oend_t = S.oend;
+        const int64_t onext_t = S.onext;
         const uint32_t rounds = (nh + kTileBlock - 1) / kTileBlock;
         for (uint32_t r = 0; r < rounds; ++r) {
             const uint32_t j = (uint32_t)t + r * kTileBlock;
             const bool own = j < nh;
+            const bool last = own && j + 1 == nh;
             const uint32_t a = own ? S.hpos[j] : 0u;
-            const uint32_t z = own ? (j + 1 < nh ? (uint32_t)S.hpos[j + 1] : cnt) : 0u;
+            const uint32_t z = own ? (!last ? (uint32_t)S.hpos[j + 1] : cnt) : 0u;
             // end of the overhang (global position), == after if none
-            const uint64_t oend = (own && j + 1 == nh) ? oend_t : after;
-            body(a, z - a, after, oend, own);
+            const uint64_t oend = last ? oend_t : after;
+            const int64_t nxt = !own ? kNoNext : (!last ? (int64_t)S.rec[z].x : onext_t);
+            body(a, z - a, after, oend, own, nxt, own && p0 + a == 0);
         }
         __syncthreads();  // the LDS tile is rewritten next
     }
     if (ebits) raise_err(err, ebits);
+}
+
+}  // namespace mpx
+
+namespace mpx {
+
+// The instances without records that border an owned instance (window-relative index idx, next
+// instance with records nxt, both from tile_walk): (idx, nxt) clamped to the window [0, n_inst),
+// and for the log's first instance also [0, idx). Such instances receive no reply, so a lane
+// that writes per-instance outputs for the whole window covers them here: fn(q) runs once for
+// every such q, the wave's 64 lanes striding over one range at a time (coalesced). Wave-uniform:
+// all lanes must call. Every instance of the window is then either owned by exactly one lane or
+// in exactly one such range (records grouped in ascending order; on kErrOrder the outputs are
+// unspecified anyway).
+template <typename Fn>
+__device__ __forceinline__ void tile_gaps(bool own, int64_t idx, int64_t nxt_idx, bool first,
+                                          uint64_t n_inst, Fn&& fn) {
+    const int l = lane_id();
+    const int64_t ni = (int64_t)n_inst;
+    for (int pass = 0; pass < 2; ++pass) {
+        int64_t lo = 0, hi = 0;
+        if (own && pass == 0) {  // after the instance
+            lo = idx + 1 < 0 ? 0 : idx + 1;
+            hi = nxt_idx < ni ? nxt_idx : ni;
+        } else if (own && first) {  // before the log's first instance
+            hi = idx < ni ? idx : ni;
+        }
+        unsigned long long m = __ballot(hi > lo);
+        while (m) {
+            const int src = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const int64_t a = (int64_t)__shfl((long long)lo, src);
+            const int64_t b = (int64_t)__shfl((long long)hi, src);
+            for (int64_t q = a + l; q < b; q += kWave) fn((uint64_t)q);
+        }
+    }
 }
 
 }  // namespace mpx

@@ -49,14 +49,19 @@ def device_count():
 
 class Engine:
     def __init__(self, device=0, n_replicas=5, mode=R.MODE_MIN, kv_capacity=0, kv_per_group=0,
-                 max_groups=0):
+                 max_groups=0, apply_path=R.APPLY_AUTO, apply_fast_min=0, apply_hot_min=0,
+                 apply_chunk=0):
+        """apply_* are the handle's mpx_apply settings (mpx_config): the pipeline choice
+        (R.APPLY_AUTO / _SMALL / _SORTED / _PARTITIONED), AUTO's partitioned threshold, the hot
+        key sample threshold (R.APPLY_NO_HOT: none) and the chunk size; 0 = default"""
         self.lib = _lib.load()
         if isinstance(mode, str):
             mode = {"min": R.MODE_MIN, "classic": R.MODE_CLASSIC}[mode.lower()]
         self.n_replicas = n_replicas
         self.mode = mode
         self.kv_per_group = kv_per_group or 512
-        cfg = _lib.MpxConfig(n_replicas, mode, kv_capacity, kv_per_group, 0, max_groups)
+        cfg = _lib.MpxConfig(n_replicas, mode, kv_capacity, kv_per_group, 0, max_groups,
+                             apply_chunk, apply_path, apply_fast_min, apply_hot_min, 0)
         h = C.c_void_p()
         rc = self.lib.mpx_open(device, C.byref(cfg), C.byref(h))
         if rc != 0:
@@ -167,6 +172,19 @@ class Engine:
         rc = self.lib.mpx_apply(self.h, _ptr(op), _ptr(key), _ptr(val), m, _ptr(ret), _ptr(conf))
         self._check(rc, "mpx_apply")
         return ret, conf
+
+    def debug_kv_set_epoch(self, epoch):
+        """TEST-ONLY: the KV table's call epoch, its slots untouched (mpx_debug_kv_set_epoch)"""
+        self._check(self.lib.mpx_debug_kv_set_epoch(self.h, epoch), "mpx_debug_kv_set_epoch")
+
+    def debug_kv_state(self):
+        """TEST-ONLY: the KV table's per-slot state words (uint32, cap + 1 of them)"""
+        n = C.c_size_t(0)
+        self._check(self.lib.mpx_debug_kv_state(self.h, None, 0, C.byref(n)), "mpx_debug_kv_state")
+        out = np.zeros(n.value, np.uint32)
+        self._check(self.lib.mpx_debug_kv_state(self.h, _ptr(out), len(out), C.byref(n)),
+                    "mpx_debug_kv_state")
+        return out
 
     def apply_reserve(self, max_cmds):
         self._check(self.lib.mpx_apply_reserve(self.h, max_cmds), "mpx_apply_reserve")

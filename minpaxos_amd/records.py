@@ -96,3 +96,8 @@ assert ACCEPT_REPLY.itemsize == 16 and INST_STATE.itemsize == 16
 assert PREPARE_REPLY.itemsize == 16 and PREP_STATE.itemsize == 32
 assert PREPARE_REPLY_MIN.itemsize == 24 and GROUP_PREP_STATE.itemsize == 32
 assert PREPARE_EFFECT.itemsize == 8
+
+# mpx_config.apply_path / apply_hot_min (include/mpx.h)
+APPLY_AUTO, APPLY_SORTED, APPLY_PARTITIONED, APPLY_SMALL = 0, 1, 2, 3
+APPLY_NO_HOT = 0xFFFFFFFF
+APPLY_SMALL_MAX = 8192

@@ -266,10 +266,10 @@ hipError_t launch_group_step(int, int32_t, uint32_t, const mpx_group_batch*, uin
 hipError_t launch_step_totals(const mpx_group_batch*, int64_t*, uint32_t*, hipStream_t) { return hipSuccess; }
 #endif
 uint64_t apply_chunk_commands(uint64_t c, uint64_t m) { return c ? c : m; }
-uint64_t apply_work_bytes(const KvTable&, uint64_t, uint64_t m) { return 48 * m + 256; }
-uint64_t apply_reserve_bytes(const KvTable&, uint64_t, uint64_t m) { return 48 * m + 256; }
+uint64_t apply_work_bytes(const KvTable&, const ApplyOpts&, uint64_t m) { return 48 * m + 256; }
+uint64_t apply_reserve_bytes(const KvTable&, const ApplyOpts&, uint64_t m) { return 48 * m + 256; }
 hipError_t launch_apply(KvTable&, const uint8_t*, const int64_t*, const int64_t*, uint64_t,
-                        int64_t*, uint8_t*, uint64_t, ApplyWork&, uint32_t*, hipStream_t) { return hipSuccess; }
+                        int64_t*, uint8_t*, const ApplyOpts&, ApplyWork&, uint32_t*, hipStream_t) { return hipSuccess; }
 hipError_t launch_kv_clear(KvTable&, hipStream_t) { return hipSuccess; }
 hipError_t launch_kv_import(KvTable&, const int64_t*, const int64_t*, uint64_t, uint32_t*,
                             hipStream_t) { return hipSuccess; }

@@ -60,6 +60,64 @@ def test_accept_tally_config2_shape(mk_engine, mode):
     assert np.array_equal(got[3], want[3])
 
 
+@pytest.mark.parametrize("mode", [R.MODE_MIN, R.MODE_CLASSIC])
+def test_accept_tally_gaps(mk_engine, mode):
+    """sparse replies: instances without replies before the first, between (gaps of 1 to 9000
+    instances, longer than a wave and than a tile) and after the last one. Their decided flags
+    are 0 (the kernel writes them in its gap pass; nothing is memset) and, CLASSIC, the
+    committedUpTo scan (updateCommittedUpTo, paxos.go:259-264) runs through them: most input
+    statuses are COMMITTED, so the first non-committed instance lies deep in a gap or past
+    every record, or does not exist (all committed)."""
+    rng = np.random.default_rng(77 + mode)
+    for trial in range(6):
+        n_inst = 30000
+        picks = np.unique(np.concatenate([rng.integers(3000, 26000, 40), [3000, 26000]]))
+        if trial == 5:
+            picks = np.array([n_inst - 1])  # one instance, at the window's end
+        counts = rng.integers(1, 6, len(picks))
+        rec = np.zeros(int(counts.sum()), R.ACCEPT_REPLY)
+        rec["instance"] = np.repeat(picks.astype(np.int32), counts) + trial
+        rec["id"] = rng.integers(0, 5, len(rec))
+        rec["ok"] = (rng.random(len(rec)) < 0.8).astype(np.uint8)
+        rec["ballot"] = rng.integers(0, 300, len(rec))
+        st = kat_cases.inst_states(n_inst, R.COMMITTED)
+        st["status"][picks] = R.PREPARED  # the replied-to instances can commit now
+        if trial in (1, 2):  # one non-committed instance inside a long gap / after the records
+            st["status"][[12345, 28000][trial - 1]] = R.ACCEPTED
+        if trial == 3:
+            st["status"][:] = R.COMMITTED  # nothing to decide, nothing bad: watermark stays
+        e, o = mk_engine(5, mode), Oracle(5, mode)
+        # a dense call first leaves decided = 1 almost everywhere in the engine's staging buffer
+        dense = kat_cases.acc(0, [(1, 1, 16), (2, 1, 16)])
+        dense = np.concatenate([dense] * n_inst)
+        dense["instance"] = np.repeat(np.arange(n_inst, dtype=np.int32), 2) + trial
+        assert e.accept_tally(dense, kat_cases.inst_states(n_inst), trial, -1)[3].all()
+        for cu0 in (-1, 2999 + trial, 20000):
+            got = e.accept_tally(rec, st, trial, cu0, np.zeros(5, np.int32))
+            want = o.accept_tally(rec, st, trial, cu0, np.zeros(5, np.int32))
+            eq_struct(got[0], want[0])
+            assert got[1] == want[1], (trial, cu0, got[1], want[1])
+            assert np.array_equal(got[2], want[2])
+            assert np.array_equal(got[3], want[3])
+
+
+def test_prepare_classic_gaps(mk_engine):
+    """CLASSIC prepare with sparse replies: the prepared flags of instances without replies are
+    0 and defaultBallot is the max over the prepared ones (one launch, no memset)"""
+    rng = np.random.default_rng(5)
+    rec, st = gen_cases.ragged_prepare(rng, 20000, 5, max_r=6)
+    keep = np.isin(rec["instance"], np.unique(rng.integers(0, 20000, 300)))
+    rec = rec[keep]
+    e, o = mk_engine(5, R.MODE_CLASSIC), Oracle(5, R.MODE_CLASSIC)
+    full_rec, full_st = gen_cases.ragged_prepare(np.random.default_rng(6), 20000, 5, max_r=6)
+    e.prepare_select(full_rec, full_st, 0, -1)  # leaves prepared flags in the staging buffer
+    for db in (-1, 100, 1 << 20):
+        got = e.prepare_select(rec, st, 0, db)
+        want = o.prepare_select(rec, st, 0, db)
+        eq_struct(got[0], want[0])
+        assert got[1] == want[1] and np.array_equal(got[2], want[2])
+
+
 def test_accept_tally_edges(mk_engine):
     e = mk_engine(5, R.MODE_MIN)
     # empty batch
@@ -193,13 +251,12 @@ def test_apply_mixed_ops_and_special_keys(mk_engine):
 
 
 @pytest.mark.parametrize("chunk", [1, 7, 777, 4096])
-def test_apply_chunked(mk_engine, monkeypatch, chunk):
-    """the apply pipeline cuts a call into chunks (MPX_APPLY_CHUNK commands): slot state and
-    conflicts carry across chunk boundaries and calls; a GET in one chunk on a key that is
+def test_apply_chunked(mk_engine, chunk):
+    """the apply pipeline cuts a call into chunks (mpx_config.apply_chunk commands): slot state
+    and conflicts carry across chunk boundaries and calls; a GET in one chunk on a key that is
     only PUT in a later chunk still conflicts with that PUT"""
-    monkeypatch.setenv("MPX_APPLY_CHUNK", str(chunk))
     rng = np.random.default_rng(77 + chunk)
-    e, o = mk_engine(5, R.MODE_MIN), Oracle(5, R.MODE_MIN)
+    e, o = mk_engine(5, R.MODE_MIN, apply_chunk=chunk), Oracle(5, R.MODE_MIN)
     handmade = (np.array([R.OP_GET, R.OP_DELETE, R.OP_GET, R.OP_PUT, R.OP_GET, R.OP_PUT, R.OP_GET],
                          np.uint8),
                 np.array([5, 6, 5, 5, 7, 6, 6], np.int64), np.arange(7, dtype=np.int64) + 100)
@@ -214,18 +271,17 @@ def test_apply_chunked(mk_engine, monkeypatch, chunk):
         assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
 
 
-@pytest.mark.parametrize("fallback", ["0", "1"])
-@pytest.mark.parametrize("hot_min", ["0", "2", "8"])
-def test_apply_paths(mk_engine, monkeypatch, hot_min, fallback):
+@pytest.mark.parametrize("path", [R.APPLY_PARTITIONED, R.APPLY_SORTED])
+@pytest.mark.parametrize("hot_min", [R.APPLY_NO_HOT, 2, 8])
+def test_apply_paths(mk_engine, hot_min, path):
     """the partitioned pipeline with no hot keys (every key through the bins), with as many hot
-    keys as fit (MPX_APPLY_HOT_MIN=2), with the sampled default, and the sort-based fallback:
+    keys as fit (apply_hot_min=2), with the sampled default, and the sort-based pipeline:
     every call bit-exact, table state carried across calls. Fresh key ranges per call put GETs
     of absent keys before their first PUT in the same bin (the two-pass bins); the small table
     (32 buckets of 256 slots) is driven to ~70% occupancy"""
-    monkeypatch.setenv("MPX_APPLY_HOT_MIN", hot_min)
-    monkeypatch.setenv("MPX_APPLY_FALLBACK", fallback)
-    rng = np.random.default_rng(31 + int(hot_min) + 10 * int(fallback))
-    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=4096), Oracle(5, R.MODE_MIN)
+    rng = np.random.default_rng(31 + hot_min % 97 + 10 * path)
+    e = mk_engine(5, R.MODE_MIN, kv_capacity=4096, apply_path=path, apply_hot_min=hot_min)
+    o = Oracle(5, R.MODE_MIN)
     calls = []
     for t in range(3):
         op, key, val = gen_cases.commands_mixed(rng, 30000, 1500)
@@ -245,18 +301,17 @@ def test_apply_paths(mk_engine, monkeypatch, hot_min, fallback):
         assert e.kv_size() == len(wk)
 
 
-@pytest.mark.parametrize("fallback", ["0", "1"])
-def test_apply_bucket_full(mk_engine, monkeypatch, fallback):
+@pytest.mark.parametrize("path", [R.APPLY_PARTITIONED, R.APPLY_SORTED])
+def test_apply_bucket_full(mk_engine, path):
     """more distinct PUT keys than a table of 4 buckets x 256 slots holds: MPX_E_KV_FULL (the
     oracle's Go map never fills; the engine's capacity is documented in mpx.h); a call that fits
     still matches the oracle afterwards on a fresh engine"""
-    monkeypatch.setenv("MPX_APPLY_FALLBACK", fallback)
-    e = mk_engine(5, R.MODE_MIN, kv_capacity=512)  # 1024 slots
+    e = mk_engine(5, R.MODE_MIN, kv_capacity=512, apply_path=path)  # 1024 slots
     keys = np.arange(1, 1501, dtype=np.int64)
     with pytest.raises(MpxError) as ei:
         e.apply(np.full(len(keys), R.OP_PUT, np.uint8), keys, keys * 3)
     assert ei.value.code == R.E_KV_FULL
-    e2, o = mk_engine(5, R.MODE_MIN, kv_capacity=512), Oracle(5, R.MODE_MIN)
+    e2, o = mk_engine(5, R.MODE_MIN, kv_capacity=512, apply_path=path), Oracle(5, R.MODE_MIN)
     rng = np.random.default_rng(3)
     op, key, val = gen_cases.commands_mixed(rng, 20000, 400)
     gr, gc = e2.apply(op, key, val)
@@ -264,16 +319,15 @@ def test_apply_bucket_full(mk_engine, monkeypatch, fallback):
     assert np.array_equal(gr, wr) and np.array_equal(gc, wc)
 
 
-def test_apply_size_dispatch(mk_engine, monkeypatch):
-    """with MPX_APPLY_FALLBACK unset the call size picks the pipeline (MPX_APPLY_FAST_MIN, here
-    10000 commands): calls on both sides of the switch carry one table, bit-exact. The
+def test_apply_size_dispatch(mk_engine):
+    """with apply_path AUTO the call size picks the pipeline (apply_fast_min, here 10000
+    commands): calls on both sides of the switch carry one table, bit-exact. The
     device-pointer entry point reserved for the largest call also runs the smaller calls, which
     take the other pipeline with its own scratch layout (mpx_apply_reserve covers both)"""
     from minpaxos_amd.devbuf import Arena
-    monkeypatch.delenv("MPX_APPLY_FALLBACK", raising=False)
-    monkeypatch.setenv("MPX_APPLY_FAST_MIN", "10000")
     rng = np.random.default_rng(57)
-    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 16), Oracle(5, R.MODE_MIN)
+    e = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 16, apply_fast_min=10000)
+    o = Oracle(5, R.MODE_MIN)
     sizes = [40000, 9999, 10000, 37, 25000, 1]
     e.apply_reserve(max(sizes))
     with Arena(e) as ar:
@@ -294,24 +348,39 @@ def test_apply_size_dispatch(mk_engine, monkeypatch):
     assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
 
 
-@pytest.mark.parametrize("fallback", ["0", "1"])
-def test_apply_epoch_wrap(mk_engine, monkeypatch, fallback):
+@pytest.mark.parametrize("path", [R.APPLY_PARTITIONED, R.APPLY_SORTED])
+def test_apply_epoch_wrap(mk_engine, path):
     """the call epoch tags every slot a call touched (state.Conflict against the same call's
-    earlier commands); 2^30 calls wrap it to 1 after clearing every tag. A table whose epoch
-    starts three calls before the wrap (MPX_KV_EPOCH_START) runs six calls across it on each
-    pipeline: every call and the final table bit-exact"""
-    monkeypatch.setenv("MPX_APPLY_FALLBACK", fallback)
-    monkeypatch.setenv("MPX_KV_EPOCH_START", str((1 << 30) - 3))
-    rng = np.random.default_rng(71 + int(fallback))
-    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=4096), Oracle(5, R.MODE_MIN)
-    for _ in range(6):
-        op, key, val = gen_cases.commands_mixed(rng, 20000, 1500)
+    earlier commands); 2^30 calls wrap it to 1 after clearing every tag. Calls at epochs 1..3
+    tag the slots of key set A; the epoch then moves to three calls before the wrap
+    (mpx_debug_kv_set_epoch, slots untouched); two calls on a disjoint key set B run at
+    2^30-2 and 2^30-1, and three calls on A at the wrapped epochs 1..3: without the wrap sweep
+    A's slots would still carry tags 1..3 and read as touched earlier in the same call. Every
+    call and the final table bit-exact; after the wrap no slot carries a pre-wrap tag."""
+    rng = np.random.default_rng(71 + path)
+    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=4096, apply_path=path), Oracle(5, R.MODE_MIN)
+
+    def call(key_lo):
+        op, key, val = gen_cases.commands_mixed(rng, 20000, 700)
+        key = np.where(key > 0, key % 700 + key_lo, key)
         gr, gc = e.apply(op, key, val)
         wr, wc = o.apply(op, key, val)
         assert np.array_equal(gr, wr) and np.array_equal(gc, wc)
+
+    for _ in range(3):
+        call(1)                       # epochs 1, 2, 3 on key set A
+    e.debug_kv_set_epoch((1 << 30) - 3)
+    for _ in range(2):
+        call(1_000_000)               # epochs 2^30-2, 2^30-1 on key set B
+    for _ in range(3):
+        call(1)                       # the wrap: epochs 1, 2, 3 on A again
+    tags = e.debug_kv_state() >> 2
+    assert tags.max() <= 3 and set(np.unique(tags)) <= {0, 1, 2, 3}
     gk, gv = e.kv_export()
     wk, wv = o.kv_export()
     assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
+    with pytest.raises(MpxError):
+        e.debug_kv_set_epoch(1 << 30)  # outside [1, 2^30)
 
 
 def test_apply_large_table_fallback(mk_engine):
