@@ -293,14 +293,17 @@ def step_bench(a, rk):
         kv0=ar.full(G * K, np.int64, 0), kc1=ar.full(G, np.uint32, 0),
         kk1=ar.full(G * K, np.int64, 0), kv1=ar.full(G * K, np.int64, 0),
         nd=ar.full(G, np.uint32, 0),
-        # poisoned (0x7F7F7F7F > any instance): the per-step -1 fill of the ranges other ranks
-        # own is what makes the max-all-reduce correct, a missing or short fill shows up
-        wm=[ar.full(2 * G_total, np.int32, 0x7F) for _ in range(2)],
+        # the step's watermark vectors, double-buffered: the group step writes this rank's
+        # groups into a send vector whose other ranges hold -1 for good (filled once below;
+        # the buffers start poisoned, 0x7F7F7F7F > any instance, so a missing fill or a group
+        # the step skipped shows up), the max over ranks lands in the receive vector
+        wms=[ar.full(2 * G_total, np.int32, 0x7F) for _ in range(2)],
+        wmr=[ar.full(2 * G_total, np.int32, 0x7F) for _ in range(2)],
         tot=[ar.full(R_TOTALS, np.int64, 0) for _ in range(2)],
     )
 
     def batch(buf, tin, tout):
-        wm = d["wm"][buf]
+        wm = d["wms"][buf]
         kc_i, kk_i, kv_i = tin
         kc_o, kk_o, kv_o = tout
         return _lib.MpxGroupBatch(
@@ -326,16 +329,17 @@ def step_bench(a, rk):
     n_ev = max(a.steps, 1)
     ev_k = [(eng.event_create(), eng.event_create()) for _ in range(n_ev)]
 
-    # watermark ranges other ranks own: [0, g0) and [g1, G_total) of both halves
-    wm_foreign = [(h + lo, h + hi) for h in (0, G_total) for lo, hi in ((0, g0), (g1, G_total))
-                  if hi > lo]
+    # watermark ranges other ranks own, [0, g0) and [g1, G_total) of both halves: -1 once
+    for lo, hi in [(h + lo, h + hi) for h in (0, G_total) for lo, hi in ((0, g0), (g1, G_total))
+                   if hi > lo]:
+        for wb in d["wms"]:
+            eng.memset(wb.at(lo), 0xFF, (hi - lo) * 4, comp)
+    eng.synchronize()
 
     def step(i, timed):
         buf = i & 1
-        if i >= 2:  # buffer `buf` is free once the all-reduce of step i-2 has read it
+        if i >= 2:  # buffers `buf` are free once the all-reduce of step i-2 has used them
             eng.stream_wait_event(comp, ev_comm[buf])
-        for lo, hi in wm_foreign:  # -1 outside own groups (the step writes every own group)
-            eng.memset(d["wm"][buf].at(lo), 0xFF, (hi - lo) * 4, comp)
         if timed:
             eng.event_record(ev_k[i][0], comp)
         eng.group_step_dev(steps[buf], comp)
@@ -344,7 +348,8 @@ def step_bench(a, rk):
         eng.step_totals_dev(steps[buf], d["tot"][buf].ptr, comp)
         eng.event_record(ev_done[buf], comp)
         eng.stream_wait_event(comm, ev_done[buf])
-        eng.step_allreduce_dev(d["wm"][buf].ptr, G_total, d["tot"][buf].ptr, R_TOTALS, comm)
+        eng.step_allreduce_oop_dev(d["wms"][buf].ptr, d["wmr"][buf].ptr, G_total,
+                                   d["tot"][buf].ptr, R_TOTALS, comm)
         eng.event_record(ev_comm[buf], comm)
 
     for i in range(a.warmup):
@@ -365,7 +370,7 @@ def step_bench(a, rk):
     last = (a.steps - 1) & 1
     tot = ar.get(d["tot"][last])  # summed over ranks by the step's all-reduce
     n_decided, n_exec_inst, n_exec_cmds = (int(x) for x in tot)
-    wm = ar.get(d["wm"][last])
+    wm = ar.get(d["wmr"][last])
     committed, executed = wm[:G_total], wm[G_total:]
     own_e = executed[g0:g1].astype(np.int64)
     kc = ar.get(d["kc1"])
@@ -415,8 +420,9 @@ def step_bench(a, rk):
                 "workload": cfg_work,
                 "groups_total": G_total, "groups_per_rank": G, "instances_per_step": G_total * ipg,
                 "commands_per_step": G_total * ipg * B, "parallelism": f"groups block-sharded x{world}",
-                "collective": ("one RCCL group per step: all-reduce(max) of 2 x groups_total int32 "
-                               "watermarks + all-reduce(sum) of 3 int64 step totals, "
+                "collective": ("one RCCL group per step: out-of-place all-reduce(max) of 2 x "
+                               "groups_total int32 watermarks + all-reduce(sum) of 3 int64 step "
+                               "totals, "
                                + ("on the compute stream" if a.no_overlap else
                                   "on a second stream overlapping the next step's kernel")),
             },
@@ -477,7 +483,7 @@ def parity_sample(b, d, ar, a, mode, N, K, G_total, g0):
     # the timed steps started from the table the warm-up step produced
     w0 = o.group_step(sub)
     want = o.group_step(sub, w0["kv_cnt"], w0["kv_key"], w0["kv_val"])
-    wm = ar.get(d["wm"][(a.steps - 1) & 1])
+    wm = ar.get(d["wmr"][(a.steps - 1) & 1])
     kc = ar.get(d["kc1"], S).astype(np.uint32)
     kk = ar.get(d["kk1"], S * K)
     kv = ar.get(d["kv1"], S * K)

@@ -374,6 +374,12 @@ int mpx_watermarks_allreduce_dev(mpx_engine* eng, int32_t* d_watermarks, size_t 
  * vector and sum over ranks of n_totals int64 counters (e.g. the mpx_step_totals_dev ones)  */
 int mpx_step_allreduce_dev(mpx_engine* eng, int32_t* d_watermarks, size_t n_groups,
                            int64_t* d_totals, size_t n_totals, void* stream);
+/* the same exchange out of place: d_wm_send keeps -1 on the groups other ranks own for good
+ * (set once; the group step writes only the rank's own range), so a step needs no refill of
+ * the foreign ranges; the max over ranks lands in d_wm_recv (2*n_groups). d_totals is reduced
+ * in place.                                                                                 */
+int mpx_step_allreduce_oop_dev(mpx_engine* eng, const int32_t* d_wm_send, int32_t* d_wm_recv,
+                               size_t n_groups, int64_t* d_totals, size_t n_totals, void* stream);
 
 /* ---- peer stream framing + AcceptReply decode ----------------------
  * A peer connection carries frames [code u8][body]. Codes (genericsmrproto.go:7-18 and the

@@ -562,12 +562,18 @@ uint64_t fast_min(const KvTable& t, const ApplyOpts& o) {  // partitioned from t
     return o.fast_min ? o.fast_min : kFastMinDefault;
 }
 bool use_fast(const KvTable& t, const ApplyOpts& o, uint64_t m) { return m >= fast_min(t, o); }
+// calls of at most MPX_APPLY_SMALL_MAX commands run the one-launch kernel (apply_small.hip)
+// unless a multi-launch pipeline is forced
+bool use_small(const ApplyOpts& o, uint64_t m) {
+    return m <= MPX_APPLY_SMALL_MAX && (o.path == MPX_APPLY_AUTO || o.path == MPX_APPLY_SMALL);
+}
 uint32_t hot_min(const ApplyOpts& o) {  // sample count (of 64K) that makes a key hot; 0 = none
     return o.hot_min == MPX_APPLY_NO_HOT ? 0u : (o.hot_min ? o.hot_min : 5u);
 }
 }  // namespace
 
 uint64_t apply_work_bytes(const KvTable& t, const ApplyOpts& o, uint64_t m) {
+    if (use_small(o, m)) return 0;
     const uint64_t C = apply_chunk_commands(o.chunk, m);
     return use_fast(t, o, m) ? apply_fast_work_bytes(t, C) : layout(C).total;
 }
@@ -575,14 +581,20 @@ uint64_t apply_work_bytes(const KvTable& t, const ApplyOpts& o, uint64_t m) {
 // Every m <= max_m must fit: each pipeline's need grows with m, so the largest call on either
 // side of the size switch bounds them all.
 uint64_t apply_reserve_bytes(const KvTable& t, const ApplyOpts& o, uint64_t max_m) {
-    const uint64_t b = apply_work_bytes(t, o, max_m), thr = fast_min(t, o);
-    return thr > 1 && thr <= max_m ? std::max(b, apply_work_bytes(t, o, thr - 1)) : b;
+    uint64_t b = apply_work_bytes(t, o, max_m);
+    const uint64_t thr = fast_min(t, o);
+    if (thr > 1 && thr <= max_m) b = std::max(b, apply_work_bytes(t, o, thr - 1));
+    const uint64_t small_end = MPX_APPLY_SMALL_MAX;  // the first size past the small kernel
+    if (use_small(o, small_end) && small_end < max_m)
+        b = std::max(b, apply_work_bytes(t, o, small_end + 1));
+    return b;
 }
 
 hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
                         uint64_t m, int64_t* ret, uint8_t* conf, const ApplyOpts& o, ApplyWork& w,
                         uint32_t* err, hipStream_t stream) {
     if (!m) return hipSuccess;
+    if (use_small(o, m)) return launch_apply_small(t, op, key, val, m, ret, conf, err, stream);
     const uint64_t C = apply_chunk_commands(o.chunk, m);
     if (use_fast(t, o, m))
         return launch_apply_fast(t, op, key, val, m, ret, conf, C, w, hot_min(o), err, stream);

@@ -1,0 +1,373 @@
+// apply_small.hip — mpx_apply for replica-sized calls (at most 8192 commands) in ONE launch.
+//
+// Reference: executeCommands (src/bareminpaxos/bareminpaxos.go:1066-1098) drains one committed
+// batch (MAX_BATCH = 5000 commands, :22) and runs (*state.Command).Execute (src/state/state.go:
+// 77-103) on each in log order; conf_prev[i] = state.Conflict (state.go:53-60) of command i with
+// the previous command on the same key in the call. The replica shim calls mpx_apply once per
+// drained batch, so the call's cost is its latency, not its bandwidth: the multi-launch
+// pipelines (about ten dependent launches, ~60 us) are replaced by one 1024-thread workgroup
+// that keeps the call in LDS:
+//   1. commands -> registers (8 per thread, wave w holds positions [512w, 512w + 512));
+//      PUTs find or claim their slot in the engine's table (kvtab.hpp, 64-bit CAS), then the
+//      other commands look theirs up. A command whose key has no slot (never PUT, absent) is
+//      final already: Execute returns NIL (0) and, as no PUT of its key precedes it, it
+//      conflicts with nothing. Every command's default result goes out now: PUT its value, GET
+//      the table value at call start (present ? value : 0), the rest 0.
+//   2. each slot gets a dense group id (LDS open-addressing table, id = table index < 16383);
+//      (id, position) pairs are sorted by id, stably, with two 7-bit LSD passes (wave-level
+//      bit-sliced ballot matching ranks each wave's 64 lanes, per-wave digit counts, one
+//      2048-entry scan) - positions stay in log order within a group.
+//   3. over the sorted groups: the previous command on the key is the left neighbour (conf),
+//      the last PUT before a command a segmented exclusive max-scan of PUT positions (GET
+//      results), and each group's last PUT is committed to the table (value, present bit,
+//      n_present).
+// The call epoch is neither read nor advanced: conflicts never reach across calls (orc_apply),
+// and the tags other pipelines compare stay older than their next epoch.
+#include "common.hpp"
+#include "kernels.hpp"
+#include "kvtab.hpp"
+
+namespace mpx {
+
+namespace {
+constexpr int kSmT = 1024;                 // threads of the workgroup
+constexpr int kSmWaves = kSmT / kWave;     // 16
+constexpr int kSmPer = 8;                  // commands per thread
+constexpr int kSmMax = kSmT * kSmPer;      // 8192 = MPX_APPLY_SMALL_MAX
+constexpr int kSmHash = 16384;             // LDS id table
+constexpr uint32_t kNoId = kSmHash - 1;    // reserved: commands without a slot sort last
+constexpr int kPosBits = 13;
+constexpr uint32_t kPosMask = (1u << kPosBits) - 1;
+constexpr int kDigit = 7;                  // radix digit bits (2 passes cover the 14-bit id)
+constexpr int kDigits = 1 << kDigit;
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+static_assert(kSmMax == MPX_APPLY_SMALL_MAX, "small apply capacity");
+
+struct SmallLds {
+    uint32_t tab[kSmHash];          // group id -> slot + 1 (0 = free)            64 KB
+    uint32_t buf[2][kSmMax];        // (id << 13 | position), radix ping-pong      64 KB
+    uint16_t cnt[kDigits][kSmWaves];  // per digit and wave: counts, then offsets  4 KB
+    uint8_t op[kSmMax];             // op by position                              8 KB
+    uint32_t wsum[kSmWaves];        // block scan: wave totals
+    int32_t wv[kSmWaves];           // segmented scan: wave values
+    uint32_t wf[kSmWaves];          //                 and head flags
+    uint32_t n_new;                 // slots that became present
+};
+
+__device__ __forceinline__ uint32_t hash_slot(uint32_t s) {
+    s ^= s >> 16;
+    s *= 0x7feb352dU;
+    s ^= s >> 15;
+    s *= 0x846ca68bU;
+    s ^= s >> 16;
+    return s;
+}
+
+// exclusive prefix sum of v over the workgroup (thread order); all threads call
+__device__ __forceinline__ uint32_t block_excl_sum(SmallLds& S, uint32_t v) {
+    const int l = lane_id(), w = threadIdx.x / kWave;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (l >= d) x += y;
+    }
+    if (l == kWave - 1) S.wsum[w] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    for (int i = 0; i < w; ++i) before += S.wsum[i];
+    __syncthreads();  // wsum is reused by the next call
+    return before + x - v;
+}
+}  // namespace
+
+__global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* __restrict__ op,
+                                                      const int64_t* __restrict__ key,
+                                                      const int64_t* __restrict__ val, uint32_t m,
+                                                      int64_t* __restrict__ ret,
+                                                      uint8_t* __restrict__ conf, uint32_t* err) {
+    __shared__ SmallLds S;
+    const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
+    const uint64_t below = lanes_below(l);
+    for (int i = tid; i < kSmHash; i += kSmT) S.tab[i] = 0;
+    if (tid == 0) S.n_new = 0;
+
+    // ---- 1. commands, slots, default results --------------------------------------------
+    // the keys wait in LDS (the sort buffers' space, free until step 2), not in registers
+    int64_t* const kl = reinterpret_cast<int64_t*>(&S.buf[0][0]);
+    uint8_t o8[kSmPer];
+    uint32_t slot[kSmPer];  // kNoSlot: none (the table has fewer than 2^32 - 1 slots)
+    uint32_t pos8[kSmPer];
+#pragma unroll
+    for (int k = 0; k < kSmPer; ++k) {
+        pos8[k] = (uint32_t)(w * (kSmPer * kWave) + k * kWave + l);
+        const bool v = pos8[k] < m;
+        if (v) kl[pos8[k]] = key[pos8[k]];
+        o8[k] = v ? op[pos8[k]] : (uint8_t)MPX_OP_NONE;
+        slot[k] = kNoSlot;
+    }
+    // PUTs find or claim their slot: all of a thread's probes in flight together, one step of
+    // the linear probe per round (kv_insert, unrolled over the thread's commands)
+    {
+        uint32_t base[kSmPer], s[kSmPer];
+        bool act[kSmPer];
+#pragma unroll
+        for (int k = 0; k < kSmPer; ++k) {
+            act[k] = pos8[k] < m && o8[k] == MPX_OP_PUT;
+            const int64_t kk = act[k] ? kl[pos8[k]] : 0;
+            if (act[k] && kk == kSentinel) {
+                slot[k] = (uint32_t)t.cap;
+                act[k] = false;
+            }
+            const uint64_t h = hash64((uint64_t)kk);
+            base[k] = bucket_of(h, t.lgnb) << kLgSB;
+            s[k] = home_of(h);
+        }
+        for (int step = 0; step < kSB; ++step) {
+            unsigned long long cur[kSmPer];
+#pragma unroll
+            for (int k = 0; k < kSmPer; ++k)
+                cur[k] = act[k] ? __hip_atomic_load(reinterpret_cast<unsigned long long*>(
+                                                         t.keys + base[k] + s[k]),
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : 0ull;
+#pragma unroll
+            for (int k = 0; k < kSmPer; ++k)
+                if (act[k] && cur[k] == (unsigned long long)kSentinel)
+                    cur[k] = atomicCAS(reinterpret_cast<unsigned long long*>(t.keys + base[k] + s[k]),
+                                       (unsigned long long)kSentinel,
+                                       (unsigned long long)kl[pos8[k]]);
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < kSmPer; ++k) {
+                if (!act[k]) continue;
+                if (cur[k] == (unsigned long long)kSentinel || (int64_t)cur[k] == kl[pos8[k]]) {
+                    slot[k] = base[k] + s[k];  // claimed, or the key's slot
+                    act[k] = false;
+                } else {
+                    s[k] = (s[k] + 1) & (kSB - 1);
+                    any = true;
+                }
+            }
+            if (!__syncthreads_or(any)) break;
+        }
+#pragma unroll
+        for (int k = 0; k < kSmPer; ++k)
+            if (act[k]) raise_err(err, kErrKvFull);  // the key's bucket is full
+    }
+    __syncthreads();  // every claim is in the table before the lookups
+    // the other commands look their key up (absent and never PUT in this call: no slot)
+    {
+        uint32_t base[kSmPer], s[kSmPer];
+        bool act[kSmPer];
+#pragma unroll
+        for (int k = 0; k < kSmPer; ++k) {
+            act[k] = pos8[k] < m && o8[k] != MPX_OP_PUT;
+            const int64_t kk = act[k] ? kl[pos8[k]] : 0;
+            if (act[k] && kk == kSentinel) {
+                slot[k] = (uint32_t)t.cap;
+                act[k] = false;
+            }
+            const uint64_t h = hash64((uint64_t)kk);
+            base[k] = bucket_of(h, t.lgnb) << kLgSB;
+            s[k] = home_of(h);
+        }
+        for (int step = 0; step < kSB; ++step) {
+            unsigned long long cur[kSmPer];
+#pragma unroll
+            for (int k = 0; k < kSmPer; ++k)
+                cur[k] = act[k] ? __hip_atomic_load(reinterpret_cast<unsigned long long*>(
+                                                         t.keys + base[k] + s[k]),
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : 0ull;
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < kSmPer; ++k) {
+                if (!act[k]) continue;
+                if ((int64_t)cur[k] == kl[pos8[k]]) {
+                    slot[k] = base[k] + s[k];
+                    act[k] = false;
+                } else if (cur[k] == (unsigned long long)kSentinel) {
+                    act[k] = false;  // absent
+                } else {
+                    s[k] = (s[k] + 1) & (kSB - 1);
+                    any = true;
+                }
+            }
+            if (!__ballot(any)) break;
+        }
+    }
+    // default results: PUT -> its value, GET -> the value at call start, others -> NIL; the
+    // GETs that follow a PUT of their key in this call are rewritten in step 3
+    {
+        int64_t r[kSmPer];
+#pragma unroll
+        for (int k = 0; k < kSmPer; ++k) {
+            r[k] = 0;
+            if (pos8[k] >= m) continue;
+            if (o8[k] == MPX_OP_PUT) {
+                r[k] = val[pos8[k]];
+            } else if (o8[k] == MPX_OP_GET && slot[k] != kNoSlot) {
+                const uint32_t st = t.state[slot[k]];
+                const int64_t v = t.vals[slot[k]];
+                r[k] = (st & kPresent) ? v : 0;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kSmPer; ++k) {
+            if (pos8[k] >= m) continue;
+            ret[pos8[k]] = r[k];
+            if (conf && slot[k] == kNoSlot) conf[pos8[k]] = 0;
+            S.op[pos8[k]] = o8[k];
+        }
+    }
+    // ---- 2. group ids and the stable sort by id ---------------------------------------------
+    __syncthreads();  // tab cleared
+#pragma unroll
+    for (int k = 0; k < kSmPer; ++k) {
+        if (pos8[k] >= m) continue;
+        uint32_t id = kNoId;
+        if (slot[k] != kNoSlot) {
+            const uint32_t want = slot[k] + 1u;
+            uint32_t h = hash_slot(want) & (kSmHash - 1);
+            for (;;) {
+                if (h == kNoId) h = 0;
+                const uint32_t cur = atomicCAS(&S.tab[h], 0u, want);
+                if (cur == 0u || cur == want) break;
+                h = (h + 1) & (kSmHash - 1);
+            }
+            id = h;
+        }
+        S.buf[0][pos8[k]] = (id << kPosBits) | pos8[k];
+    }
+    // the stores of the default results have completed before step 3 may overwrite one
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int pass = 0; pass < 2; ++pass) {
+        const uint32_t* src = S.buf[pass];
+        uint32_t* dst = S.buf[pass ^ 1];
+        for (int i = tid; i < kDigits * kSmWaves; i += kSmT) (&S.cnt[0][0])[i] = 0;
+        __syncthreads();
+        uint32_t e[kSmPer], rk[kSmPer], dg[kSmPer];
+        // wave w ranks its 512 positions in order, 64 at a time: lanes with the same digit by
+        // bit-sliced ballots, the wave's running count per digit in its own cnt column
+#pragma unroll
+        for (int k = 0; k < kSmPer; ++k) {
+            const bool v = pos8[k] < m;
+            e[k] = v ? src[pos8[k]] : 0xFFFFFFFFu;
+            const uint32_t d = (e[k] >> (kPosBits + kDigit * pass)) & (kDigits - 1);
+            dg[k] = d;
+            uint64_t peers = __ballot(v);
+#pragma unroll
+            for (int b = 0; b < kDigit; ++b) {
+                const uint64_t mb = __ballot((d >> b) & 1u);
+                peers &= ((d >> b) & 1u) ? mb : ~mb;
+            }
+            const uint32_t run = S.cnt[d][w];
+            rk[k] = run + (uint32_t)popc(peers & below);
+            if (v && !(peers >> l >> 1))  // the group's last lane
+                S.cnt[d][w] = (uint16_t)(run + popc(peers));
+        }
+        __syncthreads();
+        // offsets: exclusive scan of the counts in (digit, wave) order, two entries per thread
+        {
+            uint16_t* c = &S.cnt[0][0];
+            const uint32_t a = c[2 * tid], b = c[2 * tid + 1];
+            const uint32_t ex = block_excl_sum(S, a + b);
+            c[2 * tid] = (uint16_t)ex;
+            c[2 * tid + 1] = (uint16_t)(ex + a);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kSmPer; ++k)
+            if (pos8[k] < m) dst[S.cnt[dg[k]][w] + rk[k]] = e[k];
+        __syncthreads();
+    }
+    // ---- 3. per group, in log order ----------------------------------------------------------
+    // thread tid takes sorted entries q = 8 tid + j (blocked); groups of kNoId (no slot) last
+    const uint32_t* srt = S.buf[0];
+    uint32_t e[kSmPer];
+    int32_t ex[kSmPer];
+    bool hd[kSmPer];
+    bool seen = false;  // a group starts in this thread at or before j
+    int32_t run = -1;
+#pragma unroll
+    for (int j = 0; j < kSmPer; ++j) {
+        const uint32_t q = (uint32_t)tid * kSmPer + j;
+        const bool v = q < m;
+        e[j] = v ? srt[q] : 0xFFFFFFFFu;
+        hd[j] = v && (q == 0 || (srt[q - 1] >> kPosBits) != (e[j] >> kPosBits));
+        if (hd[j]) {
+            run = -1;
+            seen = true;
+        }
+        ex[j] = run;  // last PUT before it in the group, within this thread
+        const uint32_t p = e[j] & kPosMask;
+        if (v && S.op[p] == MPX_OP_PUT) run = (int32_t)p;
+    }
+    // carry of the last PUT from earlier threads into this thread's open group: segmented scan
+    // of (group starts in thread, last PUT) over the threads
+    uint32_t f = seen ? 1u : 0u;
+    int32_t x = run;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t fu = __shfl_up(f, d);
+        const int32_t xu = __shfl_up(x, d);
+        if (l >= d && !f) x = x > xu ? x : xu;
+        if (l >= d) f |= fu;
+    }
+    if (l == kWave - 1) {
+        S.wf[w] = f;
+        S.wv[w] = x;
+    }
+    __syncthreads();
+    int32_t cin = -1;  // inclusive scan of the earlier waves
+    for (int i = 0; i < w; ++i) {
+        if (S.wf[i]) cin = S.wv[i];
+        else cin = cin > S.wv[i] ? cin : S.wv[i];
+    }
+    {  // exclusive value for this thread: the previous lane's inclusive, else the waves'
+        const uint32_t fp = __shfl_up(f, 1);
+        const int32_t xp = __shfl_up(x, 1);
+        if (l > 0) cin = fp ? xp : (cin > xp ? cin : xp);
+    }
+    uint32_t n_new = 0;
+#pragma unroll
+    for (int j = 0; j < kSmPer; ++j) {
+        const uint32_t q = (uint32_t)tid * kSmPer + j;
+        if (q >= m) continue;
+        const uint32_t id = e[j] >> kPosBits, p = e[j] & kPosMask;
+        if (id == kNoId) continue;
+        bool before_head = true;  // no group starts in this thread at or before j
+#pragma unroll
+        for (int i = 0; i <= j; ++i) before_head &= !hd[i];
+        const int32_t pp = before_head ? (ex[j] > cin ? ex[j] : cin) : ex[j];
+        const uint8_t o = S.op[p];
+        if (conf) {
+            const bool c = !hd[j] && (S.op[srt[q - 1] & kPosMask] == MPX_OP_PUT || o == MPX_OP_PUT);
+            conf[p] = c ? 1 : 0;
+        }
+        if (o == MPX_OP_GET && pp >= 0) ret[p] = val[pp];  // the last PUT before it
+        const bool tail = q + 1 == m || (srt[q + 1] >> kPosBits) != id;
+        const int32_t lp = o == MPX_OP_PUT ? (int32_t)p : pp;
+        if (tail && lp >= 0) {  // the group's last PUT: the key's value after the call
+            const uint32_t sl = S.tab[id] - 1u;
+            t.vals[sl] = val[lp];
+            if (!(atomicOr(&t.state[sl], kPresent) & kPresent)) ++n_new;
+        }
+    }
+    if (n_new) atomicAdd(&S.n_new, n_new);
+    __syncthreads();
+    if (tid == 0 && S.n_new) atomicAdd(t.n_present, (unsigned long long)S.n_new);
+}
+
+hipError_t launch_apply_small(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
+                              uint64_t m, int64_t* ret, uint8_t* conf, uint32_t* err,
+                              hipStream_t stream) {
+    if (!m) return hipSuccess;
+    if (m > (uint64_t)kSmMax || t.cap >= 0xFFFFFFFEull) return hipErrorInvalidValue;
+    k_apply_small<<<1, kSmT, 0, stream>>>(t, op, key, val, (uint32_t)m, ret, conf, err);
+    return hipGetLastError();
+}
+
+}  // namespace mpx

@@ -764,6 +764,28 @@ int mpx_step_allreduce_dev(mpx_engine* e, int32_t* d_wm, size_t n_groups, int64_
     return MPX_OK;
 }
 
+int mpx_step_allreduce_oop_dev(mpx_engine* e, const int32_t* d_wm_send, int32_t* d_wm_recv,
+                               size_t n_groups, int64_t* d_totals, size_t n_totals, void* stream) {
+    if (!e) return MPX_E_INVAL;
+    if ((n_groups && (!d_wm_send || !d_wm_recv)) || (n_totals && !d_totals))
+        return fail(e, MPX_E_INVAL, "null argument");
+    if (n_groups && d_wm_send == d_wm_recv)
+        return fail(e, MPX_E_INVAL, "d_wm_send and d_wm_recv must differ (mpx_step_allreduce_dev "
+                                    "is the in-place form)");
+    if (!e->comm) return fail(e, MPX_E_INVAL, "mpx_comm_init has not been called");
+    const hipStream_t s = pick(e, stream);
+    ncclResult_t r = ncclGroupStart();
+    if (r == ncclSuccess && n_groups)
+        r = ncclAllReduce(d_wm_send, d_wm_recv, 2 * n_groups, ncclInt32, ncclMax, e->comm, s);
+    if (r == ncclSuccess && n_totals)
+        r = ncclAllReduce(d_totals, d_totals, n_totals, ncclInt64, ncclSum, e->comm, s);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r == ncclSuccess) r = r2;
+    if (r != ncclSuccess)
+        return fail(e, MPX_E_RCCL, std::string("step all-reduce: ") + ncclGetErrorString(r));
+    return MPX_OK;
+}
+
 int mpx_watermarks_allreduce(mpx_engine* e, int32_t* committed, int32_t* executed,
                              size_t n_groups) {
     if (!e) return MPX_E_INVAL;

@@ -103,6 +103,10 @@ uint64_t apply_fast_work_bytes(const KvTable& t, uint64_t c);
 hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
                              uint64_t m, int64_t* ret, uint8_t* conf, uint64_t C, ApplyWork& w,
                              uint32_t hot_min, uint32_t* err, hipStream_t stream);
+// one-launch apply of at most MPX_APPLY_SMALL_MAX commands (apply_small.hip), no scratch
+hipError_t launch_apply_small(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
+                              uint64_t m, int64_t* ret, uint8_t* conf, uint32_t* err,
+                              hipStream_t stream);
 hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
                         uint64_t m, int64_t* ret, uint8_t* conf, const ApplyOpts& o, ApplyWork& w,
                         uint32_t* err, hipStream_t stream);

@@ -443,6 +443,14 @@ class Engine:
         self._check(self.lib.mpx_step_allreduce_dev(self.h, d_wm, n_groups, d_totals, n_totals,
                                                     stream), "mpx_step_allreduce_dev")
 
+    def step_allreduce_oop_dev(self, d_wm_send, d_wm_recv, n_groups, d_totals, n_totals,
+                               stream=None):
+        """the step exchange out of place: max over ranks of d_wm_send (foreign groups -1 for
+        good) into d_wm_recv, sum of d_totals in place (mpx_step_allreduce_oop_dev)"""
+        self._check(self.lib.mpx_step_allreduce_oop_dev(self.h, d_wm_send, d_wm_recv, n_groups,
+                                                        d_totals, n_totals, stream),
+                    "mpx_step_allreduce_oop_dev")
+
     # ---- device memory / streams / events of the engine's HIP runtime -----------------------
     def dev_alloc(self, nbytes):
         p = C.c_void_p()

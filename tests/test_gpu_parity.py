@@ -256,7 +256,8 @@ def test_apply_chunked(mk_engine, chunk):
     and conflicts carry across chunk boundaries and calls; a GET in one chunk on a key that is
     only PUT in a later chunk still conflicts with that PUT"""
     rng = np.random.default_rng(77 + chunk)
-    e, o = mk_engine(5, R.MODE_MIN, apply_chunk=chunk), Oracle(5, R.MODE_MIN)
+    e = mk_engine(5, R.MODE_MIN, apply_chunk=chunk, apply_path=R.APPLY_SORTED)
+    o = Oracle(5, R.MODE_MIN)
     handmade = (np.array([R.OP_GET, R.OP_DELETE, R.OP_GET, R.OP_PUT, R.OP_GET, R.OP_PUT, R.OP_GET],
                          np.uint8),
                 np.array([5, 6, 5, 5, 7, 6, 6], np.int64), np.arange(7, dtype=np.int64) + 100)
@@ -269,6 +270,59 @@ def test_apply_chunked(mk_engine, chunk):
         gk, gv = e.kv_export()
         wk, wv = o.kv_export()
         assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
+
+
+@pytest.mark.parametrize("path", [R.APPLY_SMALL, R.APPLY_AUTO, R.APPLY_SORTED])
+def test_apply_small_calls(mk_engine, path):
+    """replica-sized calls (one drained executeCommands batch, MAX_BATCH = 5000 commands,
+    bareminpaxos.go:22,1071-1089): sizes around the wave (64), the workgroup (1024) and the
+    small kernel's limit (8192), mixed ops, the special keys, a hot key, GETs of absent keys
+    before their first PUT, and one table carried through all calls; every call's results,
+    the table and its size bit-exact. AUTO and SMALL run the one-launch kernel (apply_small.hip)
+    here, SORTED the multi-launch pipeline"""
+    rng = np.random.default_rng(91 + path)
+    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 14, apply_path=path), Oracle(5, R.MODE_MIN)
+    sizes = [1, 2, 63, 64, 65, 1000, 1023, 1024, 1025, 4095, 5000, 8191, 8192]
+    for i, m in enumerate(sizes):
+        op, key, val = gen_cases.commands_mixed(rng, m, 50 + 37 * i)
+        key = np.where(key > 0, key + (i % 3) * 1_000_003, key)  # fresh keys every third call
+        if i % 4 == 1:
+            key[rng.random(m) < 0.5] = 424242  # a hot key
+        gr, gc = e.apply(op, key, val)
+        wr, wc = o.apply(op, key, val)
+        assert np.array_equal(gr, wr), (m, np.nonzero(gr != wr)[0][:5])
+        assert np.array_equal(gc, wc), (m, np.nonzero(gc != wc)[0][:5])
+        gk, gv = e.kv_export()
+        wk, wv = o.kv_export()
+        assert np.array_equal(gk, wk) and np.array_equal(gv, wv), m
+        assert e.kv_size() == len(wk)
+    # the device-pointer form, one MAX_BATCH call
+    from minpaxos_amd.devbuf import Arena
+    op, key, val = synth.commands(5000, 1 << 12, 0.5, "uniform", seed=92)
+    e.apply_reserve(5000)
+    with Arena(e) as ar:
+        d_op, d_key, d_val = ar.put(op), ar.put(key), ar.put(val)
+        d_ret, d_conf = ar.empty(5000, np.int64), ar.empty(5000, np.uint8)
+        e.apply_dev(d_op.ptr, d_key.ptr, d_val.ptr, 5000, d_ret.ptr, d_conf.ptr, e.stream)
+        e.stream_synchronize(e.stream)
+        wr, wc = o.apply(op, key, val)
+        assert np.array_equal(ar.get(d_ret), wr) and np.array_equal(ar.get(d_conf), wc)
+
+
+def test_apply_small_then_pipelines(mk_engine):
+    """the one-launch kernel neither reads nor advances the call epoch: calls on it between
+    calls of the partitioned and sorted pipelines (which tag slots with the epoch) leave
+    every later call bit-exact"""
+    rng = np.random.default_rng(93)
+    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 14), Oracle(5, R.MODE_MIN)
+    for i, m in enumerate([20000, 3000, 30000, 100, 9000, 8000, 40000]):
+        op, key, val = gen_cases.commands_mixed(rng, m, 2000)
+        gr, gc = e.apply(op, key, val)
+        wr, wc = o.apply(op, key, val)
+        assert np.array_equal(gr, wr) and np.array_equal(gc, wc), m
+    gk, gv = e.kv_export()
+    wk, wv = o.kv_export()
+    assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
 
 
 @pytest.mark.parametrize("path", [R.APPLY_PARTITIONED, R.APPLY_SORTED])
