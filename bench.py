@@ -180,21 +180,26 @@ def host_cores():
     return max(1, min(n, 16))
 
 
-def traffic_of(path, **want):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary (tools/traffic.py) when it
-    was measured on this exact configuration, else None"""
-    cands = [path] if path else (
-        [os.path.join(ROOT, "profiles", f"traffic_r0{k}.json") for k in (2, 1)] +
-        [os.path.join(ROOT, "profiles", "r02", "apply_pmc", f"traffic_{d}.json")
-         for d in ("uniform", "zipf")])
-    for p in cands:
-        try:
-            tj = json.load(open(p))
-        except Exception:
-            continue
-        if all(tj.get(k) == v for k, v in want.items()):
-            return tj.get("bytes_per_launch")
-    return None
+TRAFFIC_DB = os.path.join(ROOT, "profiles", "traffic_r03.json")
+
+
+def traffic_for(key, alg, path=""):
+    """HBM bytes per launch of the measured call from a committed rocprofv3 counter pass
+    (tools/pmc_collect.py: FETCH_SIZE x 2 + WRITE_SIZE, separate --pmc passes, summed over the
+    call's kernels) taken on EXACTLY this configuration (`key`: workload and every parameter
+    that changes the kernel variant or the bytes moved). Returns (bytes or None, note); a
+    figure below the algorithmic bytes cannot be this configuration's and is rejected."""
+    try:
+        db = json.load(open(path or TRAFFIC_DB))
+    except Exception:
+        return None, "no counter database"
+    for ent in db.get("entries", []):
+        if ent.get("key") == key:
+            b = ent["bytes_per_launch"]
+            if b < alg:
+                return None, f"counter pass ({b:.4g} B) below the algorithmic bytes: rejected"
+            return b, ent.get("source", "")
+    return None, "no counter pass for this exact configuration"
 
 
 def launch_ranks(n):
@@ -391,6 +396,9 @@ def step_bench(a, rk):
            + int(kc.sum()) * 16 * 2 + G * (4 * 4 + 2 * N * 4 + 4 * 2 + 8 * 2 + 4))
     kern_avg_ms = float(np.mean(kern_ms)) if kern_ms else float("nan")
     achieved_gbs = alg / (kern_avg_ms * 1e-3) / 1e9
+    tkey = {"workload": "step", "mode": a.mode, "groups": G, "ipg": ipg, "replicas": N,
+            "cmds": B, "keys": a.keys, "kv_per_group": K}
+    traffic, tnote = traffic_for(tkey, alg, a.traffic_json)
 
     res = {}
     if rank == 0:
@@ -430,7 +438,8 @@ def step_bench(a, rk):
             "roofline": {
                 "bound": "hbm", "kernel": "k_group_fast", "achieved": achieved_gbs,
                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved_gbs / PEAK_HBM_GBS,
-                "traffic": traffic_of(a.traffic_json, mode=a.mode, groups=G, kernel="k_group_fast"),
+                "traffic": traffic, "traffic_note": tnote, "traffic_key": tkey,
+                "traffic_kernels": ["k_group_fast"],
                 "alg_bytes_per_launch": alg,
                 "kernel_ms_avg": kern_avg_ms, "kernel_ms_min": float(np.min(kern_ms)),
                 "timing": "HIP events around each k_group_fast launch on the compute stream",
@@ -441,6 +450,7 @@ def step_bench(a, rk):
             "instances_processed_per_s": G_total * ipg * a.steps / elapsed,
             "executed_instances_per_s": n_exec_inst * a.steps / elapsed,
             "executed_commands_per_s": n_exec_cmds * a.steps / elapsed,
+            "launches_in_process": 1 + a.warmup + a.steps,  # table fill + warm-up + timed
             "watermark_allreduce_ok": wm_ok,
             "watermarks_sha256": wm_sha,
             "watermarks_identical_on_all_ranks": len(set(shas)) == 1,
@@ -625,7 +635,6 @@ def kernel_bench(a, rk):
     ar = Arena(eng)
     put, get, sync = ar.put, ar.get, eng.synchronize
     lib = OL.load()
-    traffic = None
 
     t_gen = time.time()
     if a.workload == "tally":
@@ -644,7 +653,8 @@ def kernel_bench(a, rk):
                           before=lambda: eng.memcpy(d_scal.ptr, scal0.ptr, d_scal.nbytes, D2D))
         alg = n * 16 + I * 16 * 2  # replies + state in/out (96 B/instance)
         units, unit = I, "instances/s"
-        kernel = f"k_accept_tally<{a.mode}>"
+        kernel = f"k_accept_tile<{a.mode}>"
+        kernel_pat = ["k_accept_tile"]
         o = OL.Oracle(N, mode)
         w_st, w_cu, w_pc, w_dec = o.accept_tally(recs, st, 0, -1)
         got_st = get(d_out)
@@ -665,7 +675,6 @@ def kernel_bench(a, rk):
                "sample": f"the full workload ({I} instances, {n} replies) x {reps}, "
                          f"pointer-per-instance log, one thread, {secs:.1f} s timed"}
         workload = f"config2: {I} instances x {N - 1} AcceptReplies, N={N}, p_ok=0.7, mode {a.mode}"
-        traffic = traffic_of(a.traffic_json, kernel=kernel, instances=I)
     elif a.workload == "prepare":
         I = a.instances
         recs, st = synth.prepare_replies(I, N, 0.8, seed=43)
@@ -682,7 +691,8 @@ def kernel_bench(a, rk):
                           before=lambda: eng.memcpy(d_db.ptr, db0.ptr, 4, D2D))
         alg = n * 16 + I * 32 * 2  # 128 B/instance
         units, unit = I, "instances/s"
-        kernel = "k_prepare_classic"
+        kernel = "k_prepare_tile"
+        kernel_pat = ["k_prepare_tile"]
         o = OL.Oracle(N, R.MODE_CLASSIC)
         t0 = time.perf_counter()
         w_st, w_db, w_prep = o.prepare_select(recs, st, 0, -1)
@@ -724,6 +734,7 @@ def kernel_bench(a, rk):
         alg = n * 24 + (Gp + 1) * 8 + Gp * 32 * 2 + Gp * N * 4 * 2 + n * 8
         units, unit = Gp, "groups/s"
         kernel = "k_prepare_min"
+        kernel_pat = ["k_prepare_min"]
         o = OL.Oracle(N, R.MODE_MIN)
         w_gst, w_pc, w_eff = o.prepare_select_min(recs, off, gst, pc)
         bit_exact = bool(np.array_equal(get(d_gst).view(np.int32), w_gst.view(np.int32))
@@ -759,6 +770,7 @@ def kernel_bench(a, rk):
         alg = M * (17 + 9) + n_keys * 16 * 2  # commands in, ret+conf out, table read + written
         units, unit = M, "commands/s"
         kernel = "mpx_apply pipeline"
+        kernel_pat = ["mpx::", "rocprim"]
         o = OL.Oracle(N, mode)
         o.apply(op, key, val)
         w_ret, w_conf = o.apply(op, key, val)
@@ -777,8 +789,6 @@ def kernel_bench(a, rk):
                "sample": f"the full workload ({M} commands over {K} keys, {a.dist}) x {reps}, "
                          f"Execute per command on an unordered_map, one thread, {secs:.1f} s timed"}
         workload = f"config4: {M} PUT/GET (p_put=0.5) over {K} keys, {a.dist}"
-        traffic = traffic_of(a.traffic_json, kernel=kernel, commands=M, dist=a.dist,
-                             kv_capacity=a.kv_capacity or K)
     elif a.workload == "conflict":
         M, K, Bc = a.commands, a.apply_keys, 4
         op, key, _ = synth.commands(M, K, 0.5, a.dist, seed=44)
@@ -794,6 +804,7 @@ def kernel_bench(a, rk):
         alg = M * 9 + (n_inst + 1) * 8 + (n_inst - 1)
         units, unit = n_inst - 1, "instance pairs/s"
         kernel = "k_conflict_batch"
+        kernel_pat = ["k_conflict_batch"]
         o = OL.Oracle(N, mode)
         want = o.conflict_batch(op, key, off)
         bit_exact = bool(np.array_equal(get(d_out, n_inst - 1), want))
@@ -825,6 +836,7 @@ def kernel_bench(a, rk):
         alg = M * (24 + R.PROPOSE_REPLY_BYTES) + (Cn + 1) * 8  # records in, wire bytes out
         units, unit = M, "replies/s"
         kernel = "mpx_encode_replies pipeline"
+        kernel_pat = ["mpx::", "rocprim"]
         o = OL.Oracle(N, mode)
         w_out, w_off = o.encode_replies(recs, Cn, 1, 0)
         bit_exact = bool(get(d_out).tobytes() == w_out.tobytes()
@@ -866,6 +878,7 @@ def kernel_bench(a, rk):
         alg = I * (16 + 8) + M * 17 + total + (I + 1) * 8
         units, unit = I, "instances/s"
         kernel = "mpx_encode_log pipeline"
+        kernel_pat = ["mpx::", "rocprim"]
         bit_exact = bool(np.array_equal(get(d_ro), w_ro)
                          and get(d_out, total).tobytes() == w_out.tobytes())
         parity = {"instances_checked": I, "bytes": total, "bit_exact": bit_exact}
@@ -911,6 +924,7 @@ def kernel_bench(a, rk):
         alg = L + I * (16 + 1 + 8 + 8) + I * 4
         units, unit = I, "records/s"
         kernel = "k_replay_durable"
+        kernel_pat = ["k_replay_durable"]
         bit_exact = bool(np.array_equal(get(d_recs), w[0]) and np.array_equal(get(d_op), w[1])
                          and np.array_equal(get(d_key), w[2]) and np.array_equal(get(d_val), w[3])
                          and np.array_equal(get(d_last), w[4])
@@ -959,6 +973,7 @@ def kernel_bench(a, rk):
         alg = L + n_ar * 16 + n_pr * pdt.itemsize + n_var * 32 + n_oth * 8
         units, unit = n_ar + n_pr, "replies/s"
         kernel = "mpx_decode_stream pipeline"
+        kernel_pat = ["mpx::"]
         got = [get(d_ar, n_ar), get(d_pr, n_pr), get(d_var, n_var), get(d_oth, n_oth), get(d_res)[0]]
         bit_exact = all(g.tobytes() == x.tobytes() for g, x in zip(got[:4], w[:4])) and all(
             int(got[4][f]) == int(w[4][f]) for f in ("consumed", "n_accept_replies",
@@ -1005,6 +1020,7 @@ def kernel_bench(a, rk):
         alg = L + n_ar * 16 + n_oth * 8  # stream read once, records written once
         units, unit = n_ar, "AcceptReplies/s"
         kernel = "mpx_decode_peer_stream pipeline"
+        kernel_pat = ["mpx::"]
         bit_exact = bool(get(d_res).tobytes() == w_res.tobytes()
                          and get(d_ar).tobytes() == w_ar.tobytes()
                          and get(d_oth, n_oth).tobytes() == w_oth.tobytes())
@@ -1028,6 +1044,23 @@ def kernel_bench(a, rk):
     wall = rk.max(wall)
     kern_avg = float(np.mean(ms))
     achieved = alg / (kern_avg * 1e-3) / 1e9
+    # the exact configuration a counter pass must have been taken on
+    tkey = {"workload": a.workload, "mode": a.mode}
+    tkey.update({
+        "tally": lambda: {"instances": a.instances, "replicas": N},
+        "prepare": lambda: {"instances": a.instances},
+        "prepare_min": lambda: {"groups": a.prep_groups},
+        "apply": lambda: {"commands": a.commands, "apply_keys": a.apply_keys, "dist": a.dist,
+                          "kv_capacity": a.kv_capacity or a.apply_keys, "apply_path": a.apply_path},
+        "conflict": lambda: {"commands": a.commands, "apply_keys": a.apply_keys, "dist": a.dist},
+        "decode": lambda: {"instances": a.instances},
+        "stream": lambda: {"instances": a.instances, "prepare_every": a.prepare_every,
+                           "prep_cmds": a.prep_cmds},
+        "fanout": lambda: {"commands": a.commands, "clients": a.clients},
+        "log": lambda: {"instances": a.instances, "log_format": a.log_format},
+        "replay": lambda: {"instances": a.instances, "replay_dups": bool(a.replay_dups)},
+    }[a.workload]())
+    traffic, tnote = traffic_for(tkey, alg, a.traffic_json)
     if rank == 0:
         line = {
             "metric": f"{a.workload} throughput ({unit})", "value": units * a.steps * world / wall,
@@ -1037,9 +1070,13 @@ def kernel_bench(a, rk):
             "config": {"workload": workload, "parallelism": f"replicas x{world}"},
             "roofline": {"bound": "hbm", "kernel": kernel, "achieved": achieved,
                          "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
-                         "traffic": traffic, "alg_bytes_per_launch": alg,
+                         "traffic": traffic, "traffic_note": tnote, "traffic_key": tkey,
+                         "traffic_kernels": kernel_pat, "alg_bytes_per_launch": alg,
                          "kernel_ms_avg": kern_avg, "kernel_ms_min": float(np.min(ms))},
             "gen_s": round(t_gen, 2), "parity": parity, "runtime": _lib.runtime_info(),
+            # calls of the measured pipeline this process made (the counter collector divides
+            # by it): warm-up + timed, plus apply's table-filling first call
+            "launches_in_process": a.warmup + a.steps + (1 if a.workload == "apply" else 0),
         }
         if world == 1 and not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu

@@ -29,6 +29,27 @@
 
 namespace mpx {
 
+// Diagnostic build only (-DMPX_SMALL_STAMP=1, tools/stamp_small.py): thread 0 adds the
+// s_memrealtime (100 MHz) delta of each phase to a global accumulator.
+#ifndef MPX_SMALL_STAMP
+#define MPX_SMALL_STAMP 0
+#endif
+#if MPX_SMALL_STAMP
+__device__ unsigned long long mpx_small_stamp[16];
+#define SM_STAMP(k)                                                              \
+    do {                                                                         \
+        if (threadIdx.x == 0) {                                                  \
+            const unsigned long long _n = __builtin_amdgcn_s_memrealtime();       \
+            atomicAdd(&mpx_small_stamp[k], _n - _sm_prev);                       \
+            _sm_prev = _n;                                                       \
+        }                                                                        \
+    } while (0)
+#else
+#define SM_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
+
 namespace {
 constexpr int kSmT = 1024;                 // threads of the workgroup
 constexpr int kSmWaves = kSmT / kWave;     // 16
@@ -46,7 +67,7 @@ static_assert(kSmMax == MPX_APPLY_SMALL_MAX, "small apply capacity");
 struct SmallLds {
     uint32_t tab[kSmHash];          // group id -> slot + 1 (0 = free)            64 KB
     uint32_t buf[2][kSmMax];        // (id << 13 | position), radix ping-pong      64 KB
-    uint16_t cnt[kDigits][kSmWaves];  // per digit and wave: counts, then offsets  4 KB
+    uint32_t cnt[kSmWaves][kDigits];  // per wave and digit: counts, then offsets  8 KB
     uint8_t op[kSmMax];             // op by position                              8 KB
     uint32_t wsum[kSmWaves];        // block scan: wave totals
     int32_t wv[kSmWaves];           // segmented scan: wave values
@@ -87,6 +108,9 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
                                                       int64_t* __restrict__ ret,
                                                       uint8_t* __restrict__ conf, uint32_t* err) {
     __shared__ SmallLds S;
+#if MPX_SMALL_STAMP
+    unsigned long long _sm_prev = __builtin_amdgcn_s_memrealtime();
+#endif
     const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
     const uint64_t below = lanes_below(l);
     for (int i = tid; i < kSmHash; i += kSmT) S.tab[i] = 0;
@@ -97,25 +121,42 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
     int64_t* const kl = reinterpret_cast<int64_t*>(&S.buf[0][0]);
     uint8_t o8[kSmPer];
     uint32_t slot[kSmPer];  // kNoSlot: none (the table has fewer than 2^32 - 1 slots)
-    uint32_t pos8[kSmPer];
+    const uint32_t p0 = (uint32_t)(w * (kSmPer * kWave) + l);  // position of k: p0 + 64 k
+    {
+        int64_t kr[kSmPer], vr[kSmPer];  // every load in flight before the first use
 #pragma unroll
-    for (int k = 0; k < kSmPer; ++k) {
-        pos8[k] = (uint32_t)(w * (kSmPer * kWave) + k * kWave + l);
-        const bool v = pos8[k] < m;
-        if (v) kl[pos8[k]] = key[pos8[k]];
-        o8[k] = v ? op[pos8[k]] : (uint8_t)MPX_OP_NONE;
-        slot[k] = kNoSlot;
+        for (int k = 0; k < kSmPer; ++k) {
+            const uint32_t p = p0 + k * kWave;
+            const bool v = p < m;
+            o8[k] = v ? op[p] : (uint8_t)MPX_OP_NONE;
+            kr[k] = v ? key[p] : 0;
+            vr[k] = v ? val[p] : 0;
+            slot[k] = kNoSlot;
+        }
+#pragma unroll
+        for (int k = 0; k < kSmPer; ++k) {
+            const uint32_t p = p0 + k * kWave;
+            if (p >= m) continue;
+            kl[p] = kr[k];
+            if (o8[k] == MPX_OP_PUT) ret[p] = vr[k];  // a PUT returns its value
+        }
     }
-    // PUTs find or claim their slot: all of a thread's probes in flight together, one step of
-    // the linear probe per round (kv_insert, unrolled over the thread's commands)
+    SM_STAMP(0);
+    // Every command probes its key at once (one step of the bucket's linear probe per round,
+    // all of a thread's probes in flight together): a PUT claims the first free slot (64-bit
+    // CAS, kv_insert), another command stops at its key or at a free slot; those that saw a
+    // free slot probe again once every claim is in (a PUT of the same call may have taken it).
+    bool miss[kSmPer];
     {
         uint32_t base[kSmPer], s[kSmPer];
         bool act[kSmPer];
 #pragma unroll
         for (int k = 0; k < kSmPer; ++k) {
-            act[k] = pos8[k] < m && o8[k] == MPX_OP_PUT;
-            const int64_t kk = act[k] ? kl[pos8[k]] : 0;
-            if (act[k] && kk == kSentinel) {
+            const uint32_t p = p0 + k * kWave;
+            act[k] = p < m;
+            miss[k] = false;
+            const int64_t kk = act[k] ? kl[p] : 0;
+            if (act[k] && kk == kSentinel) {  // the sentinel key lives in the side slot
                 slot[k] = (uint32_t)t.cap;
                 act[k] = false;
             }
@@ -133,62 +174,21 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
                                 : 0ull;
 #pragma unroll
             for (int k = 0; k < kSmPer; ++k)
-                if (act[k] && cur[k] == (unsigned long long)kSentinel)
+                if (act[k] && o8[k] == MPX_OP_PUT && cur[k] == (unsigned long long)kSentinel)
                     cur[k] = atomicCAS(reinterpret_cast<unsigned long long*>(t.keys + base[k] + s[k]),
                                        (unsigned long long)kSentinel,
-                                       (unsigned long long)kl[pos8[k]]);
+                                       (unsigned long long)kl[p0 + k * kWave]);
             bool any = false;
 #pragma unroll
             for (int k = 0; k < kSmPer; ++k) {
                 if (!act[k]) continue;
-                if (cur[k] == (unsigned long long)kSentinel || (int64_t)cur[k] == kl[pos8[k]]) {
-                    slot[k] = base[k] + s[k];  // claimed, or the key's slot
+                const bool free_ = cur[k] == (unsigned long long)kSentinel;
+                if ((int64_t)cur[k] == kl[p0 + k * kWave] || (free_ && o8[k] == MPX_OP_PUT)) {
+                    slot[k] = base[k] + s[k];  // the key's slot, or claimed
                     act[k] = false;
-                } else {
-                    s[k] = (s[k] + 1) & (kSB - 1);
-                    any = true;
-                }
-            }
-            if (!__syncthreads_or(any)) break;
-        }
-#pragma unroll
-        for (int k = 0; k < kSmPer; ++k)
-            if (act[k]) raise_err(err, kErrKvFull);  // the key's bucket is full
-    }
-    __syncthreads();  // every claim is in the table before the lookups
-    // the other commands look their key up (absent and never PUT in this call: no slot)
-    {
-        uint32_t base[kSmPer], s[kSmPer];
-        bool act[kSmPer];
-#pragma unroll
-        for (int k = 0; k < kSmPer; ++k) {
-            act[k] = pos8[k] < m && o8[k] != MPX_OP_PUT;
-            const int64_t kk = act[k] ? kl[pos8[k]] : 0;
-            if (act[k] && kk == kSentinel) {
-                slot[k] = (uint32_t)t.cap;
-                act[k] = false;
-            }
-            const uint64_t h = hash64((uint64_t)kk);
-            base[k] = bucket_of(h, t.lgnb) << kLgSB;
-            s[k] = home_of(h);
-        }
-        for (int step = 0; step < kSB; ++step) {
-            unsigned long long cur[kSmPer];
-#pragma unroll
-            for (int k = 0; k < kSmPer; ++k)
-                cur[k] = act[k] ? __hip_atomic_load(reinterpret_cast<unsigned long long*>(
-                                                         t.keys + base[k] + s[k]),
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                : 0ull;
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < kSmPer; ++k) {
-                if (!act[k]) continue;
-                if ((int64_t)cur[k] == kl[pos8[k]]) {
-                    slot[k] = base[k] + s[k];
+                } else if (free_) {
+                    miss[k] = true;  // not in the table yet: again after the claims
                     act[k] = false;
-                } else if (cur[k] == (unsigned long long)kSentinel) {
-                    act[k] = false;  // absent
                 } else {
                     s[k] = (s[k] + 1) & (kSB - 1);
                     any = true;
@@ -196,36 +196,67 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
             }
             if (!__ballot(any)) break;
         }
-    }
-    // default results: PUT -> its value, GET -> the value at call start, others -> NIL; the
-    // GETs that follow a PUT of their key in this call are rewritten in step 3
-    {
-        int64_t r[kSmPer];
 #pragma unroll
-        for (int k = 0; k < kSmPer; ++k) {
-            r[k] = 0;
-            if (pos8[k] >= m) continue;
-            if (o8[k] == MPX_OP_PUT) {
-                r[k] = val[pos8[k]];
-            } else if (o8[k] == MPX_OP_GET && slot[k] != kNoSlot) {
-                const uint32_t st = t.state[slot[k]];
-                const int64_t v = t.vals[slot[k]];
-                r[k] = (st & kPresent) ? v : 0;
+        for (int k = 0; k < kSmPer; ++k)
+            if (act[k]) raise_err(err, kErrKvFull);  // a full bucket (never for a lookup)
+        SM_STAMP(1);
+        __syncthreads();  // every claim is in the table
+        // misses: from the free slot they saw (the slots before it hold other keys for good)
+        bool again = false;
+#pragma unroll
+        for (int k = 0; k < kSmPer; ++k) again |= miss[k];
+        for (int step = 0; step < kSB && __ballot(again); ++step) {
+            again = false;
+#pragma unroll
+            for (int k = 0; k < kSmPer; ++k) {
+                if (!miss[k]) continue;
+                const unsigned long long c = __hip_atomic_load(
+                    reinterpret_cast<unsigned long long*>(t.keys + base[k] + s[k]),
+                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((int64_t)c == kl[p0 + k * kWave]) {
+                    slot[k] = base[k] + s[k];
+                    miss[k] = false;
+                } else if (c == (unsigned long long)kSentinel) {
+                    miss[k] = false;  // absent, and no PUT of this call: no slot
+                } else {
+                    s[k] = (s[k] + 1) & (kSB - 1);
+                    again = true;
+                }
             }
         }
+    }
+    SM_STAMP(2);
+    // default results of the other commands: GET -> the value at call start, the rest NIL;
+    // the GETs that follow a PUT of their key in this call are rewritten in step 3
+    {
+        uint32_t st[kSmPer];
+        int64_t tv[kSmPer];
 #pragma unroll
         for (int k = 0; k < kSmPer; ++k) {
-            if (pos8[k] >= m) continue;
-            ret[pos8[k]] = r[k];
-            if (conf && slot[k] == kNoSlot) conf[pos8[k]] = 0;
-            S.op[pos8[k]] = o8[k];
+            const bool g = p0 + k * kWave < m && o8[k] == MPX_OP_GET && slot[k] != kNoSlot;
+            st[k] = g ? t.state[slot[k]] : 0u;
+            tv[k] = g ? t.vals[slot[k]] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < kSmPer; ++k) {
+            const uint32_t p = p0 + k * kWave;
+            if (p < m && o8[k] != MPX_OP_PUT) ret[p] = (st[k] & kPresent) ? tv[k] : 0;
         }
     }
-    // ---- 2. group ids and the stable sort by id ---------------------------------------------
-    __syncthreads();  // tab cleared
 #pragma unroll
     for (int k = 0; k < kSmPer; ++k) {
-        if (pos8[k] >= m) continue;
+        const uint32_t p = p0 + k * kWave;
+        if (p >= m) continue;
+        if (conf && slot[k] == kNoSlot) conf[p] = 0;  // nothing precedes it on a PUT-less key
+        S.op[p] = o8[k];
+    }
+    SM_STAMP(3);
+    // ---- 2. group ids and the stable sort by id ---------------------------------------------
+    __syncthreads();  // tab cleared; the keys in the sort buffers are dead
+#pragma unroll
+    for (int k = 0; k < kSmPer; ++k) {
+        const uint32_t p = p0 + k * kWave;
+        if (p >= m) continue;
         uint32_t id = kNoId;
         if (slot[k] != kNoSlot) {
             const uint32_t want = slot[k] + 1u;
@@ -238,11 +269,9 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
             }
             id = h;
         }
-        S.buf[0][pos8[k]] = (id << kPosBits) | pos8[k];
+        S.buf[0][p] = (id << kPosBits) | p;
     }
-    // the stores of the default results have completed before step 3 may overwrite one
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    SM_STAMP(4);
     for (int pass = 0; pass < 2; ++pass) {
         const uint32_t* src = S.buf[pass];
         uint32_t* dst = S.buf[pass ^ 1];
@@ -250,11 +279,12 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
         __syncthreads();
         uint32_t e[kSmPer], rk[kSmPer], dg[kSmPer];
         // wave w ranks its 512 positions in order, 64 at a time: lanes with the same digit by
-        // bit-sliced ballots, the wave's running count per digit in its own cnt column
+        // bit-sliced ballots, the wave's running count per digit in its own cnt row
 #pragma unroll
         for (int k = 0; k < kSmPer; ++k) {
-            const bool v = pos8[k] < m;
-            e[k] = v ? src[pos8[k]] : 0xFFFFFFFFu;
+            const uint32_t p = p0 + k * kWave;
+            const bool v = p < m;
+            e[k] = v ? src[p] : 0xFFFFFFFFu;
             const uint32_t d = (e[k] >> (kPosBits + kDigit * pass)) & (kDigits - 1);
             dg[k] = d;
             uint64_t peers = __ballot(v);
@@ -263,47 +293,62 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
                 const uint64_t mb = __ballot((d >> b) & 1u);
                 peers &= ((d >> b) & 1u) ? mb : ~mb;
             }
-            const uint32_t run = S.cnt[d][w];
+            const uint32_t run = S.cnt[w][d];
             rk[k] = run + (uint32_t)popc(peers & below);
             if (v && !(peers >> l >> 1))  // the group's last lane
-                S.cnt[d][w] = (uint16_t)(run + popc(peers));
+                S.cnt[w][d] = run + (uint32_t)popc(peers);
         }
         __syncthreads();
         // offsets: exclusive scan of the counts in (digit, wave) order, two entries per thread
         {
-            uint16_t* c = &S.cnt[0][0];
-            const uint32_t a = c[2 * tid], b = c[2 * tid + 1];
+            const uint32_t d = (uint32_t)tid >> 3, w0 = ((uint32_t)tid & 7) * 2;
+            const uint32_t a = S.cnt[w0][d], b = S.cnt[w0 + 1][d];
             const uint32_t ex = block_excl_sum(S, a + b);
-            c[2 * tid] = (uint16_t)ex;
-            c[2 * tid + 1] = (uint16_t)(ex + a);
+            S.cnt[w0][d] = ex;
+            S.cnt[w0 + 1][d] = ex + a;
         }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < kSmPer; ++k)
-            if (pos8[k] < m) dst[S.cnt[dg[k]][w] + rk[k]] = e[k];
+            if (p0 + k * kWave < m) dst[S.cnt[w][dg[k]] + rk[k]] = e[k];
         __syncthreads();
     }
+    SM_STAMP(5);
     // ---- 3. per group, in log order ----------------------------------------------------------
-    // thread tid takes sorted entries q = 8 tid + j (blocked); groups of kNoId (no slot) last
+    // thread tid takes sorted entries q = 8 tid + j (blocked, two 16-byte LDS reads); groups of
+    // kNoId (no slot) come last. The default results' stores are complete before any rewrite.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     const uint32_t* srt = S.buf[0];
+    const uint32_t q0 = (uint32_t)tid * kSmPer;
     uint32_t e[kSmPer];
-    int32_t ex[kSmPer];
+    {
+        const uint4 a = reinterpret_cast<const uint4*>(srt)[2 * tid];
+        const uint4 b = reinterpret_cast<const uint4*>(srt)[2 * tid + 1];
+        e[0] = a.x; e[1] = a.y; e[2] = a.z; e[3] = a.w;
+        e[4] = b.x; e[5] = b.y; e[6] = b.z; e[7] = b.w;
+    }
+    const uint32_t e_prev = q0 > 0 && q0 - 1 < m ? srt[q0 - 1] : 0xFFFFFFFFu;
+    const uint32_t e_next = q0 + kSmPer < m ? srt[q0 + kSmPer] : 0xFFFFFFFFu;
+    uint8_t o[kSmPer];
+#pragma unroll
+    for (int j = 0; j < kSmPer; ++j) o[j] = q0 + j < m ? S.op[e[j] & kPosMask] : (uint8_t)0;
+    const uint8_t o_prev = q0 > 0 && q0 - 1 < m ? S.op[e_prev & kPosMask] : (uint8_t)0;
     bool hd[kSmPer];
+    int32_t ex[kSmPer];
     bool seen = false;  // a group starts in this thread at or before j
     int32_t run = -1;
 #pragma unroll
     for (int j = 0; j < kSmPer; ++j) {
-        const uint32_t q = (uint32_t)tid * kSmPer + j;
-        const bool v = q < m;
-        e[j] = v ? srt[q] : 0xFFFFFFFFu;
-        hd[j] = v && (q == 0 || (srt[q - 1] >> kPosBits) != (e[j] >> kPosBits));
+        const bool v = q0 + j < m;
+        const uint32_t before = j ? e[j - 1] : e_prev;
+        hd[j] = v && (q0 + j == 0 || (before >> kPosBits) != (e[j] >> kPosBits));
         if (hd[j]) {
             run = -1;
             seen = true;
         }
         ex[j] = run;  // last PUT before it in the group, within this thread
-        const uint32_t p = e[j] & kPosMask;
-        if (v && S.op[p] == MPX_OP_PUT) run = (int32_t)p;
+        if (v && o[j] == MPX_OP_PUT) run = (int32_t)(e[j] & kPosMask);
     }
     // carry of the last PUT from earlier threads into this thread's open group: segmented scan
     // of (group starts in thread, last PUT) over the threads
@@ -331,35 +376,54 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
         const int32_t xp = __shfl_up(x, 1);
         if (l > 0) cin = fp ? xp : (cin > xp ? cin : xp);
     }
-    uint32_t n_new = 0;
+    uint32_t cslot[kSmPer];  // commits: slot, or kNoSlot
+    bool before_head = true;  // no group starts in this thread at or before j
 #pragma unroll
     for (int j = 0; j < kSmPer; ++j) {
-        const uint32_t q = (uint32_t)tid * kSmPer + j;
-        if (q >= m) continue;
+        cslot[j] = kNoSlot;
+        before_head &= !hd[j];
+        const uint32_t q = q0 + j;
         const uint32_t id = e[j] >> kPosBits, p = e[j] & kPosMask;
-        if (id == kNoId) continue;
-        bool before_head = true;  // no group starts in this thread at or before j
-#pragma unroll
-        for (int i = 0; i <= j; ++i) before_head &= !hd[i];
+        if (q >= m || id == kNoId) continue;
         const int32_t pp = before_head ? (ex[j] > cin ? ex[j] : cin) : ex[j];
-        const uint8_t o = S.op[p];
         if (conf) {
-            const bool c = !hd[j] && (S.op[srt[q - 1] & kPosMask] == MPX_OP_PUT || o == MPX_OP_PUT);
-            conf[p] = c ? 1 : 0;
+            const uint8_t ob = j ? o[j - 1] : o_prev;
+            conf[p] = (!hd[j] && (ob == MPX_OP_PUT || o[j] == MPX_OP_PUT)) ? 1 : 0;
         }
-        if (o == MPX_OP_GET && pp >= 0) ret[p] = val[pp];  // the last PUT before it
-        const bool tail = q + 1 == m || (srt[q + 1] >> kPosBits) != id;
-        const int32_t lp = o == MPX_OP_PUT ? (int32_t)p : pp;
+        if (o[j] == MPX_OP_GET && pp >= 0) ret[p] = val[pp];  // the last PUT before it
+        const uint32_t after = j + 1 < kSmPer ? e[j + 1] : e_next;
+        const bool tail = q + 1 == m || (after >> kPosBits) != id;
+        const int32_t lp = o[j] == MPX_OP_PUT ? (int32_t)p : pp;
         if (tail && lp >= 0) {  // the group's last PUT: the key's value after the call
-            const uint32_t sl = S.tab[id] - 1u;
-            t.vals[sl] = val[lp];
-            if (!(atomicOr(&t.state[sl], kPresent) & kPresent)) ++n_new;
+            cslot[j] = S.tab[id] - 1u;
+            t.vals[cslot[j]] = val[lp];
         }
     }
+    uint32_t olds[kSmPer];
+#pragma unroll
+    for (int j = 0; j < kSmPer; ++j)
+        olds[j] = cslot[j] != kNoSlot ? atomicOr(&t.state[cslot[j]], kPresent) : kPresent;
+    uint32_t n_new = 0;
+#pragma unroll
+    for (int j = 0; j < kSmPer; ++j) n_new += (olds[j] & kPresent) ? 0u : 1u;
     if (n_new) atomicAdd(&S.n_new, n_new);
     __syncthreads();
     if (tid == 0 && S.n_new) atomicAdd(t.n_present, (unsigned long long)S.n_new);
+    SM_STAMP(6);
 }
+
+#if MPX_SMALL_STAMP
+extern "C" int mpx_debug_small_stamps(unsigned long long* out16, int reset) {
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(mpx_small_stamp), 16 * sizeof(unsigned long long)) !=
+        hipSuccess)
+        return -3;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(mpx_small_stamp), z, sizeof(z)) != hipSuccess) return -3;
+    }
+    return 0;
+}
+#endif
 
 hipError_t launch_apply_small(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
                               uint64_t m, int64_t* ret, uint8_t* conf, uint32_t* err,

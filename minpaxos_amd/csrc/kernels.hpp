@@ -23,8 +23,9 @@ constexpr int kRedWords = 64;
 // device-scope maxima and the last-workgroup ticket, and are back to zero after every call
 constexpr int kTileGrid = 2048;
 constexpr int kTileCtlWords = 64;
-// workgroups of a persistent launch of `kernel` (block threads) over `tiles` units: the number
-// resident at once on the device (occupancy x CUs, cached per kernel), at most kTileGrid
+// workgroups of a persistent launch of `kernel` (block threads) over `tiles` units: two rounds
+// of the number resident at once on the device (occupancy x CUs, cached per kernel), at most
+// kTileGrid
 uint32_t resident_grid(const void* kernel, int block, uint64_t tiles);
 
 hipError_t launch_accept_tally(int mode, const mpx_accept_reply* recs, uint64_t n,
