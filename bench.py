@@ -181,6 +181,7 @@ def host_cores():
 
 
 TRAFFIC_DB = os.path.join(ROOT, "profiles", "traffic_r03.json")
+ISSUE_BOUND = ("decode", "stream", "fanout")
 
 
 def traffic_for(key, alg, path=""):
@@ -195,11 +196,55 @@ def traffic_for(key, alg, path=""):
         return None, "no counter database"
     for ent in db.get("entries", []):
         if ent.get("key") == key:
-            b = ent["bytes_per_launch"]
+            b = ent.get("bytes_per_launch")
+            if b is None:
+                return None, "no FETCH/WRITE pass for this exact configuration"
             if b < alg:
                 return None, f"counter pass ({b:.4g} B) below the algorithmic bytes: rejected"
             return b, ent.get("source", "")
     return None, "no counter pass for this exact configuration"
+
+
+# issue peaks for the rows bound by instruction issue rather than HBM (MI355X_MICROARCH.md:
+# a wave64 VALU instruction issues over 2 cycles on its SIMD; an LDS wave-instruction takes at
+# least 2 LDS-array cycles per CU, ds_read_b32/b64 rate), 256 CUs x 4 SIMDs at 2.4 GHz
+PEAK_VALU_GIPS = 256 * 4 * 0.5 * 2.4   # G wave-instructions / s
+PEAK_LDS_GIPS = 256 * 0.5 * 2.4
+
+
+def instr_for(key, path=""):
+    """SQ instruction counts per launch (tools/pmc_collect.py --instr) of exactly this
+    configuration, or None"""
+    try:
+        db = json.load(open(path or TRAFFIC_DB))
+    except Exception:
+        return None
+    for ent in db.get("entries", []):
+        if ent.get("key") == key and ent.get("instr"):
+            return ent["instr"]
+    return None
+
+
+def issue_roofline(kernel, key, kern_ms, hbm, path=""):
+    """the roofline object of a row bound by instruction issue: VALU (and LDS) wave-instructions
+    per launch from the counter database / the call's kernel time, against the issue peaks; the
+    HBM figures stay beside it under "hbm". The bound is whichever fraction is higher; without a
+    counter pass it stays "valu" (measured bound) with achieved null."""
+    ins = instr_for(key, path) or {}
+    t = kern_ms * 1e-3
+    valu, lds = ins.get("SQ_INSTS_VALU"), ins.get("SQ_INSTS_LDS")
+    fv = valu / t / 1e9 / PEAK_VALU_GIPS if valu else None
+    fl = lds / t / 1e9 / PEAK_LDS_GIPS if lds else None
+    use_lds = fl is not None and (fv is None or fl > fv)
+    return {"bound": "lds" if use_lds else "valu", "kernel": kernel,
+            "achieved": (lds if use_lds else valu) / t / 1e9 if (valu or lds) else None,
+            "peak": PEAK_LDS_GIPS if use_lds else PEAK_VALU_GIPS, "unit": "G wave-instr/s",
+            "frac": fl if use_lds else fv, "valu_frac": fv, "lds_frac": fl,
+            "valu_instr_per_launch": valu, "lds_instr_per_launch": lds,
+            "instr_note": "SQ_INSTS_VALU / SQ_INSTS_LDS rocprofv3 passes (tools/pmc_collect.py "
+                          "--instr) of this exact configuration" if ins else
+                          "no instruction-counter pass for this exact configuration",
+            "hbm": hbm}
 
 
 def launch_ranks(n):
@@ -637,6 +682,7 @@ def kernel_bench(a, rk):
     lib = OL.load()
 
     t_gen = time.time()
+    host_call = None
     if a.workload == "tally":
         I = a.instances
         recs, st = synth.accept_replies(I, N, 0.7, seed=42)
@@ -780,6 +826,20 @@ def kernel_bench(a, rk):
         bit_exact = bool(np.array_equal(get(d_ret), w_ret) and np.array_equal(get(d_conf), w_conf)
                          and np.array_equal(gk, wk[order]) and np.array_equal(gv, wv[order]))
         parity = {"commands_checked": M, "bit_exact": bit_exact}
+        if M <= 1 << 16:
+            # a replica-sized call (one drained executeCommands batch, MAX_BATCH = 5000,
+            # bareminpaxos.go:22): the synchronous host-pointer form the cgo shim calls, per
+            # call (H2D of the commands, the launch(es), D2H of ret / conf), same table
+            hc = []
+            for _ in range(max(20, 4 * a.steps)):
+                t0 = time.perf_counter()
+                hr, hcf = eng.apply(op, key, val)
+                hc.append(time.perf_counter() - t0)
+            parity["host_form_bit_exact"] = bool(np.array_equal(hr, w_ret)
+                                                 and np.array_equal(hcf, w_conf))
+            host_call = {"median_us": float(np.median(hc)) * 1e6,
+                         "min_us": float(np.min(hc)) * 1e6, "calls": len(hc),
+                         "form": "mpx_apply (host pointers, synchronous)"}
         ret = np.zeros(M, np.int64)
         k0, v0 = np.ascontiguousarray(wk), np.ascontiguousarray(wv)
         secs, reps = _cpu_loop(lambda: lib.orc_bench_apply(
@@ -789,6 +849,9 @@ def kernel_bench(a, rk):
                "sample": f"the full workload ({M} commands over {K} keys, {a.dist}) x {reps}, "
                          f"Execute per command on an unordered_map, one thread, {secs:.1f} s timed"}
         workload = f"config4: {M} PUT/GET (p_put=0.5) over {K} keys, {a.dist}"
+        if M <= 1 << 16:
+            workload = (f"apply (replica batch): {M} PUT/GET (p_put=0.5) over {K} keys, "
+                        f"{a.dist}, path {a.apply_path}")
     elif a.workload == "conflict":
         M, K, Bc = a.commands, a.apply_keys, 4
         op, key, _ = synth.commands(M, K, 0.5, a.dist, seed=44)
@@ -1061,6 +1124,18 @@ def kernel_bench(a, rk):
         "replay": lambda: {"instances": a.instances, "replay_dups": bool(a.replay_dups)},
     }[a.workload]())
     traffic, tnote = traffic_for(tkey, alg, a.traffic_json)
+    rl = {"bound": "hbm", "kernel": kernel, "achieved": achieved,
+          "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+          "traffic": traffic, "traffic_note": tnote, "traffic_key": tkey,
+          "traffic_kernels": kernel_pat, "alg_bytes_per_launch": alg,
+          "kernel_ms_avg": kern_avg, "kernel_ms_min": float(np.min(ms))}
+    if a.workload in ISSUE_BOUND:
+        # the framing DP (decode, stream) and the fan-out's per-reply LDS ranking are bound by
+        # instruction issue, not HBM: graded against the issue peaks
+        rl = dict(issue_roofline(kernel, tkey, kern_avg, {k: rl[k] for k in (
+            "achieved", "peak", "unit", "frac", "traffic", "traffic_note")}, a.traffic_json),
+                  traffic_key=tkey, traffic_kernels=kernel_pat, alg_bytes_per_launch=alg,
+                  kernel_ms_avg=kern_avg, kernel_ms_min=float(np.min(ms)))
     if rank == 0:
         line = {
             "metric": f"{a.workload} throughput ({unit})", "value": units * a.steps * world / wall,
@@ -1068,12 +1143,9 @@ def kernel_bench(a, rk):
             "ms_per_step": wall / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "int32/int64", "data": "synthetic (splitmix64)",
             "config": {"workload": workload, "parallelism": f"replicas x{world}"},
-            "roofline": {"bound": "hbm", "kernel": kernel, "achieved": achieved,
-                         "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
-                         "traffic": traffic, "traffic_note": tnote, "traffic_key": tkey,
-                         "traffic_kernels": kernel_pat, "alg_bytes_per_launch": alg,
-                         "kernel_ms_avg": kern_avg, "kernel_ms_min": float(np.min(ms))},
+            "roofline": rl,
             "gen_s": round(t_gen, 2), "parity": parity, "runtime": _lib.runtime_info(),
+            **({"host_call": host_call} if host_call else {}),
             # calls of the measured pipeline this process made (the counter collector divides
             # by it): warm-up + timed, plus apply's table-filling first call
             "launches_in_process": a.warmup + a.steps + (1 if a.workload == "apply" else 0),

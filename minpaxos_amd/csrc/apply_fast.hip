@@ -66,7 +66,9 @@ constexpr int kTPer = kTL / kTT;   // 4 commands per thread; wave w owns [256 w,
 constexpr int kHMax = 128;         // hot keys per chunk, index 0 = INT64_MIN
 constexpr int kLgHMax = 7;
 constexpr int kHotTab = 512;       // LDS hash of the hot keys (load <= 1/8: probes stay short)
-constexpr int kMaxBins = 1024;
+constexpr int kLgMaxBins = 10;
+constexpr int kMaxBins = 1 << kLgMaxBins;  // partition bins (super-bins past it)
+constexpr int kLgMaxSub = 4;   // bins per super-bin, at most (tables to 2^10 x 2^4 x 4096 slots)
 // buckets per bin = waves of the resolve workgroup (MPX_RS_LGBPB: 3 = 8-wave workgroups of half
 // the LDS, two per CU; 4 = 16 waves, one per CU)
 #ifndef MPX_RS_LGBPB
@@ -108,12 +110,15 @@ struct ApHot {               // per chunk; written by k_ap_select (+ the scan's 
     uint32_t restarts;       // bins that ran the two-pass form (diagnostic)
 };
 
+// lgsub: tables past kMaxBins bins of 2^lgbpb buckets partition the log into kMaxBins super-bins
+// of 2^lgsub bins each; the resolve workgroup of a super-bin takes its bins one after another
+// (each pass streams the super-bin's records and resolves those of its bin)
 struct ApGeo {
-    uint32_t lgnb, lgbpb, nbin, rowlen, tiles, ng, tpg;
+    uint32_t lgnb, lgbpb, lgsub, nbin, rowlen, tiles, ng, tpg;
 };
 
 __device__ __forceinline__ uint32_t bin_of(uint64_t h, const ApGeo& g) {
-    return bucket_of(h, g.lgnb) >> g.lgbpb;
+    return bucket_of(h, g.lgnb) >> (g.lgbpb + g.lgsub);
 }
 
 typedef __attribute__((address_space(3))) volatile uint8_t lds_u8;
@@ -900,13 +905,19 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
                                                     uint32_t* err) {
     __shared__ ResolveLds S;
     const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
-    const uint32_t bin = blockIdx.x;
     const uint32_t bpb = 1u << g.lgbpb, nslot = bpb * kSB;
-    const uint64_t gbase = (uint64_t)bin * nslot;
+    const uint32_t nsub = 1u << g.lgsub;
     const uint32_t ep = t.epoch[0];
-    const uint32_t r0 = bin_start[bin], r1 = bin_start[bin + 1];
+    const uint32_t r0 = bin_start[blockIdx.x], r1 = bin_start[blockIdx.x + 1];
     if (r0 == r1) return;  // no records: nothing read, nothing touched (small calls, hot-heavy chunks)
     const unsigned long long below = (1ull << l) - 1ull;
+    for (uint32_t sub = 0; sub < nsub; ++sub) {
+    // bin (blockIdx.x << lgsub) | sub: its records are those of the super-bin's log whose bucket
+    // falls in it (every pass streams the super-bin's records)
+    const uint64_t gbase = (((uint64_t)blockIdx.x << g.lgsub) | sub) * nslot;
+    auto member = [&](uint64_t h) {
+        return ((bucket_of(h, g.lgnb) >> g.lgbpb) & (nsub - 1)) == sub;
+    };
     auto load_tables = [&]() {
         for (uint32_t i = tid; i < nslot; i += kRTT) {
             S.tk[i] = t.keys[gbase + i];
@@ -934,6 +945,7 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
                 const int4 kv = rec_kv[q];
                 const int64_t k = kv_lo_hi(kv.x, kv.y);
                 const uint64_t h = hash64((uint64_t)k);
+                if (!member(h)) continue;
                 const uint32_t b = bucket_of(h, g.lgnb) & (bpb - 1);
                 int64_t* T = S.tk + b * kSB;
                 uint32_t p = home_of(h);
@@ -982,8 +994,8 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
 #pragma unroll
             for (int hh = 0; hh < kRH; ++hh) {
                 const uint32_t i = hh * kRTT + tid;
-                live[hh] = base + i < r1;
                 const uint64_t h = hash64((uint64_t)kv_lo_hi(kv[hh].x, kv[hh].y));
+                live[hh] = base + i < r1 && member(h);
                 bl[hh] = bucket_of(h, g.lgnb) & (bpb - 1);
                 rk[hh] = 0;
                 if (MPX_RS_ABL & 4) continue;
@@ -1070,7 +1082,7 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
         __syncthreads();
     }
 #if MPX_RS_STAMP
-    if (bin == 0 && tid == 0) {
+    if (blockIdx.x == 0 && sub == 0 && tid == 0) {
         unsigned long long mx = 0, sm = 0;
         for (int i = 0; i < kRTW; ++i) {
             mx = S.rb[i] > mx ? S.rb[i] : mx;
@@ -1092,6 +1104,8 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) added += __shfl_xor(added, d);
     if (l == 0 && added) atomicAdd(t.n_present, (unsigned long long)added);
+    __syncthreads();  // the next bin reloads the LDS tables
+    }
 }
 
 // ---- hot keys: final state ----------------------------------------------------------------------
@@ -1273,7 +1287,9 @@ ApGeo geo_for(const KvTable& t, uint64_t n) {
     ApGeo g{};
     g.lgnb = t.lgnb;
     g.lgbpb = t.lgnb < (uint32_t)kLgMaxBPB ? t.lgnb : (uint32_t)kLgMaxBPB;
-    g.nbin = 1u << (t.lgnb - g.lgbpb);
+    const uint32_t lgbins = t.lgnb - g.lgbpb;
+    g.lgsub = lgbins > (uint32_t)kLgMaxBins ? lgbins - (uint32_t)kLgMaxBins : 0u;
+    g.nbin = 1u << (lgbins - g.lgsub);
     g.rowlen = g.nbin + 2 * kHMax;
     g.tiles = (uint32_t)((n + kTL - 1) / kTL);
     if (!g.tiles) g.tiles = 1;
@@ -1309,7 +1325,7 @@ FastLayout fast_layout(const KvTable& t, uint64_t c) {
 
 bool apply_fast_ok(const KvTable& t) {
     const uint32_t lgbpb = t.lgnb < (uint32_t)kLgMaxBPB ? t.lgnb : (uint32_t)kLgMaxBPB;
-    return (1u << (t.lgnb - lgbpb)) <= (uint32_t)kMaxBins;
+    return t.lgnb - lgbpb <= (uint32_t)(kLgMaxBins + kLgMaxSub);
 }
 
 uint64_t apply_fast_work_bytes(const KvTable& t, uint64_t c) { return fast_layout(t, c).total; }

@@ -437,19 +437,28 @@ def test_apply_epoch_wrap(mk_engine, path):
         e.debug_kv_set_epoch(1 << 30)  # outside [1, 2^30)
 
 
-def test_apply_large_table_fallback(mk_engine):
-    """a table past the partitioned pipeline's 1024 bins (kv_capacity 4M keys: 8M slots) takes
-    the sort-based pipeline; same results"""
-    rng = np.random.default_rng(41)
-    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 22), Oracle(5, R.MODE_MIN)
-    for t in range(2):
-        op, key, val = gen_cases.commands_mixed(rng, 60000, 20000)
+@pytest.mark.parametrize("cap_lg", [22, 23, 25, 26])
+def test_apply_large_table(mk_engine, cap_lg):
+    """tables past the partition's 1024 bins: kv_capacity 2^22 / 2^23 / 2^25 keys (2^23..2^26
+    slots) split the log into 1024 super-bins of 2 / 4 / 16 bins, which the resolve workgroup
+    takes one after another (partitioned pipeline forced); 2^26 keys is past the 16-bin limit and
+    takes the sort-based pipeline. Every call and the final table bit-exact, across calls, with
+    GETs of new keys before their first PUT (the two-pass bins) and a zipf call (hot keys)"""
+    rng = np.random.default_rng(41 + cap_lg)
+    path = R.APPLY_PARTITIONED if cap_lg < 26 else R.APPLY_AUTO
+    e = mk_engine(5, R.MODE_MIN, kv_capacity=1 << cap_lg, apply_path=path)
+    o = Oracle(5, R.MODE_MIN)
+    calls = [gen_cases.commands_mixed(rng, 60000, 20000) for _ in range(2)]
+    calls.append(synth.commands(200000, 1 << 40, 0.5, "uniform", seed=cap_lg))
+    calls.append(synth.commands(100000, 5000, 0.5, "zipf", seed=cap_lg + 1))
+    for op, key, val in calls:
         gr, gc = e.apply(op, key, val)
         wr, wc = o.apply(op, key, val)
         assert np.array_equal(gr, wr) and np.array_equal(gc, wc)
     gk, gv = e.kv_export()
     wk, wv = o.kv_export()
     assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
+    assert e.kv_size() == len(wk)
 
 
 def test_conflict_batch(mk_engine):

@@ -61,6 +61,10 @@ def main():
     ap.add_argument("sets", nargs="+", help="bench.py argument strings")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pmc", "traffic.json"))
     ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--instr", default="",
+                    help="comma list of SQ instruction counters (e.g. SQ_INSTS_VALU,SQ_INSTS_LDS) "
+                         "to add to the entries instead of the FETCH/WRITE passes: per launch, "
+                         "summed over the call's kernels, one --pmc pass each")
     a = ap.parse_args()
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     db = {"entries": []}
@@ -72,6 +76,23 @@ def main():
         key, pats = rf["traffic_key"], rf["traffic_kernels"]
         launches = line["launches_in_process"]
         d = os.path.join(os.path.dirname(a.out), f"set{i}")
+        if a.instr:
+            old = [e for e in db["entries"] if e["key"] == key]
+            ent = old[0] if old else {"key": key, "kernels": pats, "bytes_per_launch": None,
+                                      "alg_bytes_per_launch": rf["alg_bytes_per_launch"]}
+            ins = ent.setdefault("instr", {})
+            for c in a.instr.split(","):
+                vals = per_kernel(pmc_pass(args, c, os.path.join(d, c), a.steps), pats)
+                tot = 0.0
+                for name, v in vals.items():
+                    tot += statistics.median(v) * max(1, round(len(v) / launches))
+                ins[c] = tot
+            ent["instr_source"] = (f"rocprofv3 --pmc passes ({a.instr}) of bench.py {args} "
+                                   f"(tools/pmc_collect.py --instr)")
+            db["entries"] = [e for e in db["entries"] if e["key"] != key] + [ent]
+            json.dump(db, open(a.out, "w"), indent=1)
+            print(json.dumps({"key": key, "instr": ins}), flush=True)
+            continue
         got = {}
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
             got[c] = per_kernel(pmc_pass(args, c, os.path.join(d, c), a.steps), pats)
@@ -85,11 +106,13 @@ def main():
                                "write_kib_median": statistics.median(w), "per_launch": k,
                                "bytes": b}
             total += b
-        ent = {"key": key, "kernels": pats, "bytes_per_launch": total,
+        old = [e for e in db["entries"] if e["key"] == key]
+        ent = dict(old[0]) if old else {}
+        ent.update({"key": key, "kernels": pats, "bytes_per_launch": total,
                "alg_bytes_per_launch": rf["alg_bytes_per_launch"],
                "ratio_to_alg": total / rf["alg_bytes_per_launch"], "per_kernel": per,
                "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py {args} "
-                         f"(tools/pmc_collect.py)"}
+                         f"(tools/pmc_collect.py)"})
         db["entries"] = [e for e in db["entries"] if e["key"] != key] + [ent]
         json.dump(db, open(a.out, "w"), indent=1)
         print(json.dumps({"key": key, "bytes_per_launch": total,
