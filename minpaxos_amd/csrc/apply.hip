@@ -572,6 +572,8 @@ uint32_t hot_min(const ApplyOpts& o) {  // sample count (of 64K) that makes a ke
 }
 }  // namespace
 
+bool apply_is_one_launch(const ApplyOpts& o, uint64_t m) { return m && use_small(o, m); }
+
 uint64_t apply_work_bytes(const KvTable& t, const ApplyOpts& o, uint64_t m) {
     if (use_small(o, m)) return 0;
     const uint64_t C = apply_chunk_commands(o.chunk, m);

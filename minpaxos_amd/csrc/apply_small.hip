@@ -62,6 +62,8 @@ constexpr uint32_t kPosMask = (1u << kPosBits) - 1;
 constexpr int kDigit = 7;                  // radix digit bits (2 passes cover the 14-bit id)
 constexpr int kDigits = 1 << kDigit;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+constexpr uint32_t kShared = 0x80000000u;  // tab: a second command joined the slot
+constexpr uint8_t kOpPresent = 0x80;       // LDS op byte: the key was present at call start
 static_assert(kSmMax == MPX_APPLY_SMALL_MAX, "small apply capacity");
 
 struct SmallLds {
@@ -120,10 +122,12 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
     // the keys wait in LDS (the sort buffers' space, free until step 2), not in registers
     int64_t* const kl = reinterpret_cast<int64_t*>(&S.buf[0][0]);
     uint8_t o8[kSmPer];
-    uint32_t slot[kSmPer];  // kNoSlot: none (the table has fewer than 2^32 - 1 slots)
+    uint32_t slot[kSmPer];  // kNoSlot: none (the table has fewer than 2^31 - 1 slots)
+    uint32_t slot_st[kSmPer];  // the slot's state word after the call (present set)
+    int64_t vr[kSmPer];     // values (a lone PUT commits its own in step 2)
     const uint32_t p0 = (uint32_t)(w * (kSmPer * kWave) + l);  // position of k: p0 + 64 k
     {
-        int64_t kr[kSmPer], vr[kSmPer];  // every load in flight before the first use
+        int64_t kr[kSmPer];  // every load in flight before the first use
 #pragma unroll
         for (int k = 0; k < kSmPer; ++k) {
             const uint32_t p = p0 + k * kWave;
@@ -228,50 +232,101 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
     SM_STAMP(2);
     // default results of the other commands: GET -> the value at call start, the rest NIL;
     // the GETs that follow a PUT of their key in this call are rewritten in step 3
+    // (the state word of every slot, so the commits know which keys become present: one plain
+    // store each, no atomic; only this call's workgroup touches the table while it runs)
+    bool pres[kSmPer];
     {
         uint32_t st[kSmPer];
         int64_t tv[kSmPer];
 #pragma unroll
         for (int k = 0; k < kSmPer; ++k) {
-            const bool g = p0 + k * kWave < m && o8[k] == MPX_OP_GET && slot[k] != kNoSlot;
-            st[k] = g ? t.state[slot[k]] : 0u;
-            tv[k] = g ? t.vals[slot[k]] : 0;
+            const bool h = p0 + k * kWave < m && slot[k] != kNoSlot;
+            st[k] = h ? t.state[slot[k]] : 0u;
+            tv[k] = h && o8[k] == MPX_OP_GET ? t.vals[slot[k]] : 0;
         }
 #pragma unroll
         for (int k = 0; k < kSmPer; ++k) {
             const uint32_t p = p0 + k * kWave;
-            if (p < m && o8[k] != MPX_OP_PUT) ret[p] = (st[k] & kPresent) ? tv[k] : 0;
+            pres[k] = (st[k] & kPresent) != 0;
+            if (p < m && o8[k] != MPX_OP_PUT) ret[p] = pres[k] ? tv[k] : 0;
+            if (p >= m) continue;
+            if (conf && slot[k] == kNoSlot) conf[p] = 0;  // nothing precedes it on a PUT-less key
+            S.op[p] = (uint8_t)(o8[k] | (pres[k] ? kOpPresent : 0));  // op + present at call start
+            pres[k] = pres[k] || slot[k] == kNoSlot;
+            if (!pres[k]) st[k] |= kPresent;
+            slot_st[k] = st[k];
         }
-    }
-#pragma unroll
-    for (int k = 0; k < kSmPer; ++k) {
-        const uint32_t p = p0 + k * kWave;
-        if (p >= m) continue;
-        if (conf && slot[k] == kNoSlot) conf[p] = 0;  // nothing precedes it on a PUT-less key
-        S.op[p] = o8[k];
     }
     SM_STAMP(3);
-    // ---- 2. group ids and the stable sort by id ---------------------------------------------
+    // ---- 2. group ids, lone commands, the stable sort by id ----------------------------------
+    // Each slot gets a dense id (LDS open addressing: tab[id] = slot + 1, bit 31 set once a
+    // second command of the call joins the slot). A command alone on its key in the call - the
+    // common case of a replica batch over a large key space - is final after step 1 but for
+    // its commit (a PUT's value and present bit); only the commands of shared keys are sorted
+    // and scanned, compacted in log order.
     __syncthreads();  // tab cleared; the keys in the sort buffers are dead
+    uint32_t id[kSmPer];
 #pragma unroll
     for (int k = 0; k < kSmPer; ++k) {
         const uint32_t p = p0 + k * kWave;
-        if (p >= m) continue;
-        uint32_t id = kNoId;
-        if (slot[k] != kNoSlot) {
-            const uint32_t want = slot[k] + 1u;
-            uint32_t h = hash_slot(want) & (kSmHash - 1);
-            for (;;) {
-                if (h == kNoId) h = 0;
-                const uint32_t cur = atomicCAS(&S.tab[h], 0u, want);
-                if (cur == 0u || cur == want) break;
-                h = (h + 1) & (kSmHash - 1);
+        id[k] = kNoId;
+        if (p >= m || slot[k] == kNoSlot) continue;
+        const uint32_t want = slot[k] + 1u;
+        uint32_t h = hash_slot(want) & (kSmHash - 1);
+        for (;;) {
+            if (h == kNoId) h = 0;
+            const uint32_t cur = atomicCAS(&S.tab[h], 0u, want);
+            if (cur == 0u) break;
+            if ((cur & ~kShared) == want) {
+                if (!(cur & kShared)) atomicOr(&S.tab[h], kShared);
+                break;
             }
-            id = h;
+            h = (h + 1) & (kSmHash - 1);
         }
-        S.buf[0][p] = (id << kPosBits) | p;
+        id[k] = h;
+    }
+    __syncthreads();
+    // lone commands: conf 0 (nothing before them on the key in this call), a PUT commits;
+    // shared ones get their rank in log order (wave w holds positions [512 w, 512 w + 512),
+    // round k of it the 64 positions 512 w + 64 k + lane)
+    uint32_t m2, rank[kSmPer];
+    bool shared[kSmPer];
+    uint32_t n_new = 0;
+    {
+        uint32_t before = 0;
+#pragma unroll
+        for (int k = 0; k < kSmPer; ++k) {
+            const uint32_t p = p0 + k * kWave;
+            shared[k] = id[k] != kNoId && (S.tab[id[k]] & kShared);
+            const uint64_t b = __ballot(shared[k]);
+            rank[k] = before + (uint32_t)popc(b & below);
+            before += (uint32_t)popc(b);
+            const bool lone = id[k] != kNoId && !shared[k];
+            if (lone && conf) conf[p] = 0;
+            if (lone && o8[k] == MPX_OP_PUT) {
+                t.vals[slot[k]] = vr[k];
+                if (!pres[k]) {
+                    t.state[slot[k]] = slot_st[k];
+                    ++n_new;
+                }
+            }
+        }
+        if (l == 0) S.wsum[w] = before;
+        __syncthreads();
+        uint32_t off = 0;
+        m2 = 0;
+        for (int i = 0; i < kSmWaves; ++i) {
+            off += i < w ? S.wsum[i] : 0u;
+            m2 += S.wsum[i];
+        }
+#pragma unroll
+        for (int k = 0; k < kSmPer; ++k) {
+            if (shared[k]) S.buf[0][off + rank[k]] = (id[k] << kPosBits) | (p0 + k * kWave);
+        }
     }
     SM_STAMP(4);
+    // the shared commands' (id, position) pairs, stably by id: two 7-bit LSD passes; entry j of
+    // a pass is held by thread (j / 512) * 64 + j % 64, like the positions above
     for (int pass = 0; pass < 2; ++pass) {
         const uint32_t* src = S.buf[pass];
         uint32_t* dst = S.buf[pass ^ 1];
@@ -283,7 +338,7 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
 #pragma unroll
         for (int k = 0; k < kSmPer; ++k) {
             const uint32_t p = p0 + k * kWave;
-            const bool v = p < m;
+            const bool v = p < m2;
             e[k] = v ? src[p] : 0xFFFFFFFFu;
             const uint32_t d = (e[k] >> (kPosBits + kDigit * pass)) & (kDigits - 1);
             dg[k] = d;
@@ -310,7 +365,7 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < kSmPer; ++k)
-            if (p0 + k * kWave < m) dst[S.cnt[w][dg[k]] + rk[k]] = e[k];
+            if (p0 + k * kWave < m2) dst[S.cnt[w][dg[k]] + rk[k]] = e[k];
         __syncthreads();
     }
     SM_STAMP(5);
@@ -328,19 +383,26 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
         e[0] = a.x; e[1] = a.y; e[2] = a.z; e[3] = a.w;
         e[4] = b.x; e[5] = b.y; e[6] = b.z; e[7] = b.w;
     }
-    const uint32_t e_prev = q0 > 0 && q0 - 1 < m ? srt[q0 - 1] : 0xFFFFFFFFu;
-    const uint32_t e_next = q0 + kSmPer < m ? srt[q0 + kSmPer] : 0xFFFFFFFFu;
+    const uint32_t e_prev = q0 > 0 && q0 - 1 < m2 ? srt[q0 - 1] : 0xFFFFFFFFu;
+    const uint32_t e_next = q0 + kSmPer < m2 ? srt[q0 + kSmPer] : 0xFFFFFFFFu;
     uint8_t o[kSmPer];
 #pragma unroll
-    for (int j = 0; j < kSmPer; ++j) o[j] = q0 + j < m ? S.op[e[j] & kPosMask] : (uint8_t)0;
-    const uint8_t o_prev = q0 > 0 && q0 - 1 < m ? S.op[e_prev & kPosMask] : (uint8_t)0;
+    for (int j = 0; j < kSmPer; ++j) o[j] = q0 + j < m2 ? S.op[e[j] & kPosMask] : (uint8_t)0;
+    const uint8_t o_prev =
+        q0 > 0 && q0 - 1 < m2 ? (uint8_t)(S.op[e_prev & kPosMask] & ~kOpPresent) : (uint8_t)0;
+    bool tpres[kSmPer];  // the key was present at call start
+#pragma unroll
+    for (int j = 0; j < kSmPer; ++j) {
+        tpres[j] = (o[j] & kOpPresent) != 0;
+        o[j] &= (uint8_t)~kOpPresent;
+    }
     bool hd[kSmPer];
     int32_t ex[kSmPer];
     bool seen = false;  // a group starts in this thread at or before j
     int32_t run = -1;
 #pragma unroll
     for (int j = 0; j < kSmPer; ++j) {
-        const bool v = q0 + j < m;
+        const bool v = q0 + j < m2;
         const uint32_t before = j ? e[j - 1] : e_prev;
         hd[j] = v && (q0 + j == 0 || (before >> kPosBits) != (e[j] >> kPosBits));
         if (hd[j]) {
@@ -384,7 +446,7 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
         before_head &= !hd[j];
         const uint32_t q = q0 + j;
         const uint32_t id = e[j] >> kPosBits, p = e[j] & kPosMask;
-        if (q >= m || id == kNoId) continue;
+        if (q >= m2 || id == kNoId) continue;
         const int32_t pp = before_head ? (ex[j] > cin ? ex[j] : cin) : ex[j];
         if (conf) {
             const uint8_t ob = j ? o[j - 1] : o_prev;
@@ -392,20 +454,17 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
         }
         if (o[j] == MPX_OP_GET && pp >= 0) ret[p] = val[pp];  // the last PUT before it
         const uint32_t after = j + 1 < kSmPer ? e[j + 1] : e_next;
-        const bool tail = q + 1 == m || (after >> kPosBits) != id;
+        const bool tail = q + 1 == m2 || (after >> kPosBits) != id;
         const int32_t lp = o[j] == MPX_OP_PUT ? (int32_t)p : pp;
         if (tail && lp >= 0) {  // the group's last PUT: the key's value after the call
-            cslot[j] = S.tab[id] - 1u;
+            cslot[j] = (S.tab[id] & ~kShared) - 1u;
             t.vals[cslot[j]] = val[lp];
+            if (!tpres[j]) {  // present from now on (the state word was read in step 1)
+                atomicOr(&t.state[cslot[j]], kPresent);
+                ++n_new;
+            }
         }
     }
-    uint32_t olds[kSmPer];
-#pragma unroll
-    for (int j = 0; j < kSmPer; ++j)
-        olds[j] = cslot[j] != kNoSlot ? atomicOr(&t.state[cslot[j]], kPresent) : kPresent;
-    uint32_t n_new = 0;
-#pragma unroll
-    for (int j = 0; j < kSmPer; ++j) n_new += (olds[j] & kPresent) ? 0u : 1u;
     if (n_new) atomicAdd(&S.n_new, n_new);
     __syncthreads();
     if (tid == 0 && S.n_new) atomicAdd(t.n_present, (unsigned long long)S.n_new);
@@ -429,7 +488,7 @@ hipError_t launch_apply_small(KvTable& t, const uint8_t* op, const int64_t* key,
                               uint64_t m, int64_t* ret, uint8_t* conf, uint32_t* err,
                               hipStream_t stream) {
     if (!m) return hipSuccess;
-    if (m > (uint64_t)kSmMax || t.cap >= 0xFFFFFFFEull) return hipErrorInvalidValue;
+    if (m > (uint64_t)kSmMax || t.cap >= 0x7FFFFFFEull) return hipErrorInvalidValue;
     k_apply_small<<<1, kSmT, 0, stream>>>(t, op, key, val, (uint32_t)m, ret, conf, err);
     return hipGetLastError();
 }

@@ -56,6 +56,10 @@ struct mpx_engine {
     // durable-log replay staging: log bytes, records, op, key, val, last_rec, scalars
     DevBuf rp[7];
     mpx::ApplyOpts apply{};  // mpx_config.apply_* (fixed for the handle's life)
+    // replica-sized mpx_apply calls: pinned, GPU-mapped staging the one-launch kernel reads the
+    // commands from and writes the results to (no DMA copies on the call's path)
+    uint8_t* pin = nullptr;
+    size_t pin_cap = 0;
     // group-step work list (groups the fast kernel hands to the general kernel) + its count
     DevBuf worklist;
     uint32_t* d_wcount = nullptr;
@@ -255,6 +259,7 @@ int mpx_close(mpx_engine* e) {
     for (auto& x : e->b)
         if (x.p) (void)hipFree(x.p);
     if (e->apply_work.p) (void)hipFree(e->apply_work.p);
+    if (e->pin) (void)hipHostFree(e->pin);
     for (auto& x : e->dec)
         if (x.p) (void)hipFree(x.p);
     if (e->decode_work.p) (void)hipFree(e->decode_work.p);
@@ -450,6 +455,42 @@ int mpx_apply(mpx_engine* e, const uint8_t* op, const int64_t* key, const int64_
     if (m >= (1ull << 31)) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 commands per call");
     CK(begin(e));
     CK(ensure_kv(e));
+    if (mpx::apply_is_one_launch(e->apply, m)) {
+        // one drained executeCommands batch: the commands go into pinned host memory the kernel
+        // reads over the link, the results come back the same way; a CPU copy on each side
+        const size_t a16 = (m + 15) & ~(size_t)15, need = a16 * 2 + m * 24;
+        if (e->pin_cap < need) {
+            if (e->pin) (void)hipHostFree(e->pin);
+            e->pin = nullptr;
+            e->pin_cap = 0;
+            void* hp = nullptr;
+            if (hipHostMalloc(&hp, need, hipHostMallocDefault) != hipSuccess || !hp)
+                return fail(e, MPX_E_NOMEM, "pinned staging for mpx_apply");
+            e->pin = (uint8_t*)hp;
+            e->pin_cap = need;
+        }
+        uint8_t* h_op = e->pin;
+        int64_t* h_key = (int64_t*)(e->pin + a16);
+        int64_t* h_val = h_key + m;
+        int64_t* h_ret = h_val + m;
+        uint8_t* h_conf = (uint8_t*)(h_ret + m);
+        std::memcpy(h_op, op, m);
+        std::memcpy(h_key, key, m * 8);
+        std::memcpy(h_val, val, m * 8);
+        void* dp = nullptr;
+        HIPCHK(e, hipHostGetDevicePointer(&dp, e->pin, 0));
+        uint8_t* d0 = (uint8_t*)dp;
+        mpx::ApplyWork w{nullptr, 0};
+        HIPCHK(e, mpx::launch_apply(e->kv, d0, (const int64_t*)(d0 + a16),
+                                    (const int64_t*)(d0 + a16) + m, m,
+                                    (int64_t*)(d0 + a16) + 2 * m,
+                                    conf_prev ? d0 + a16 + m * 24 : nullptr, e->apply, w,
+                                    e->d_err, e->stream));
+        const int rc = finish(e);
+        std::memcpy(ret, h_ret, m * 8);
+        if (conf_prev) std::memcpy(conf_prev, h_conf, m);
+        return rc;
+    }
     GROW(e, e->b[7], m);
     GROW(e, e->b[8], m * 8);
     GROW(e, e->b[9], m * 8);

@@ -100,6 +100,8 @@ hipError_t launch_epoch_next(KvTable& t, uint32_t* n_miss, hipStream_t stream);
 uint64_t apply_reserve_bytes(const KvTable& t, const ApplyOpts& o, uint64_t max_m);
 // the partitioned pipeline (apply_fast.hip): tables of at most 1024 bins of 16 buckets
 bool apply_fast_ok(const KvTable& t);
+// the call runs the one-launch kernel (apply_small.hip): no scratch, inputs read once
+bool apply_is_one_launch(const ApplyOpts& o, uint64_t m);
 uint64_t apply_fast_work_bytes(const KvTable& t, uint64_t c);
 hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
                              uint64_t m, int64_t* ret, uint8_t* conf, uint64_t C, ApplyWork& w,

@@ -116,6 +116,12 @@ hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned int) { return hi
 hipError_t hipDeviceSynchronize(void) { return hipSuccess; }
 hipError_t hipMalloc(void** p, size_t n) { *p = calloc(1, n ? n : 1); return *p ? hipSuccess : hipErrorOutOfMemory; }
 hipError_t hipFree(void* p) { free(p); return hipSuccess; }
+hipError_t hipHostMalloc(void** p, size_t n, unsigned int) {
+    *p = calloc(1, n ? n : 1);
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipHostFree(void* p) { free(p); return hipSuccess; }
+hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned int) { *d = h; return hipSuccess; }
 hipError_t hipMemset(void* p, int v, size_t n) { memset(p, v, n); return hipSuccess; }
 hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) { memset(p, v, n); return hipSuccess; }
 hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t) {
@@ -266,6 +272,10 @@ hipError_t launch_group_step(int, int32_t, uint32_t, const mpx_group_batch*, uin
 hipError_t launch_step_totals(const mpx_group_batch*, int64_t*, uint32_t*, hipStream_t) { return hipSuccess; }
 #endif
 uint64_t apply_chunk_commands(uint64_t c, uint64_t m) { return c ? c : m; }
+// the engine's pinned-staging branch for replica-sized calls (same rule as apply.hip)
+bool apply_is_one_launch(const ApplyOpts& o, uint64_t m) {
+    return m && m <= MPX_APPLY_SMALL_MAX && (o.path == MPX_APPLY_AUTO || o.path == MPX_APPLY_SMALL);
+}
 uint64_t apply_work_bytes(const KvTable&, const ApplyOpts&, uint64_t m) { return 48 * m + 256; }
 uint64_t apply_reserve_bytes(const KvTable&, const ApplyOpts&, uint64_t m) { return 48 * m + 256; }
 hipError_t launch_apply(KvTable&, const uint8_t*, const int64_t*, const int64_t*, uint64_t,

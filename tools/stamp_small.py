@@ -10,7 +10,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-PHASES = ["load", "PUT claim", "lookup", "defaults", "ids", "radix x2", "groups+commit"]
+PHASES = ["load", "PUT claim", "lookup", "defaults", "ids+lone", "radix x2", "groups+commit"]
 
 
 def main():
