@@ -207,7 +207,7 @@ typedef struct mpx_config {
     uint32_t apply_path;    /* MPX_APPLY_AUTO: by call size (single-launch kernel up to
                                MPX_APPLY_SMALL_MAX commands, the sort-based pipeline below
                                apply_fast_min, the partitioned one from there, sort-based
-                               again for tables past 1024 bins); or force one of
+                               again for tables past 2^26 slots); or force one of
                                MPX_APPLY_SMALL / _SORTED / _PARTITIONED (SMALL and
                                PARTITIONED where the call / table allow, else AUTO's pick)  */
     uint32_t apply_fast_min;  /* AUTO: calls of at least this many commands run

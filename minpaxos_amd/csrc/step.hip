@@ -266,6 +266,10 @@ struct FastCfg {
     static constexpr int kFTabPer = (kFTab + kFT - 1) / kFT;
     static constexpr int kFWaves = kFT / kWave;
     static constexpr int kWaveCmds = kFCmds / kFWaves;  // commands per wave
+    // the table's start values in LDS (GETs of keys present at the start read them there);
+    // the 1024-key variant reads them from the input table instead: its 8 KB would hold the
+    // workgroup at 3 per CU (41.7 KB), without them 4 fit (33.5 KB)
+    static constexpr bool kFDvalLds = TB_ <= 512;
     static_assert(kFCmds % kFT == 0 && kFRecs % kFT == 0, "whole items per thread");
     static_assert(kFCmds / 32 <= kWave, "the new-key bitmap is scanned by one wave");
     static_assert(kWaveCmds < 2047, "kTabLp holds 1 + a wave-relative command index");
@@ -320,7 +324,7 @@ struct FastLds {
         } b;
     } u;
     unsigned long long hkey[kFH];  // slot -> key; kFreeKey = free
-    int64_t dval[kFTab];     // table entry values at the start of the step
+    int64_t dval[Cfg::kFDvalLds ? kFTab : 1];  // table entry values at the start of the step
     uint16_t tabidx[kFH];    // table entry holding the slot's key; kNone16 = new to the table
     uint32_t newbits[kFCmds / 32];  // first PUTs of new keys, as a bitmap over command index
     uint16_t coff[kFIpg + 2];       // instance -> first command (group-relative)
@@ -495,7 +499,7 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
             ebits |= sl < 0 ? kOverflow : 0u;
             tslot[k] = sl < 0 ? 0 : sl;
             if (fresh) S.tabidx[sl] = (uint16_t)e;  // (a duplicate entry of a malformed table
-            S.dval[e] = tv[k];                      //  shares the first one's slot)
+            if (Cfg::kFDvalLds) S.dval[e] = tv[k];  //  shares the first one's slot)
         }
     }
     __syncthreads();  // B2
@@ -744,7 +748,11 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
         const int64_t sv = S.u.b.cval[src >= 0 ? src : 0];
         const uint32_t ti = S.tabidx[sl];
         const bool intab = ti != kNone16;                       // present at the start
-        const int64_t at_start = S.dval[intab ? ti : 0];
+        const int64_t at_start =
+            Cfg::kFDvalLds ? S.dval[intab ? ti : 0]
+                           : (intab && op == MPX_OP_GET && lastput < 0
+                                  ? b.kv_val_in[(uint64_t)g * kvpg + ti]
+                                  : 0);
         const int64_t r = isput ? sv : (op == MPX_OP_GET ? (lastput >= 0 ? sv : (intab ? at_start : 0)) : 0);
         const bool conf = hasprev && (prevput || isput);      // state.Conflict(prev, this)
         if (act) {
@@ -778,7 +786,7 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
         if (!(MPX_ABLATE & 16) && e < kcnt) {
             const uint32_t dl = last_put((uint32_t)tslot[k]);
             kko[e] = (int64_t)S.hkey[tslot[k]];
-            kvo[e] = dl ? S.u.b.cval[dl - 1] : S.dval[e];
+            kvo[e] = dl ? S.u.b.cval[dl - 1] : (Cfg::kFDvalLds ? S.dval[e] : tv[k]);
         }
     }
     // keys new to the table that hold a value: appended in order of their first PUT, whose

@@ -32,12 +32,16 @@ def main(src: str, dst: str) -> None:
         d = json.loads(open(os.path.join(dst, f)).read())
         rf, cb = d.get("roofline") or {}, d.get("cpu_baseline") or {}
         par = d.get("parity", {})
-        rows.append("| %s | %s | %.3g %s | %.3f | %.0f | %.3f | %.3g (%s core) | %s |" % (
+        hbm = rf.get("hbm") or rf  # issue-bound rows keep their HBM figures under "hbm"
+        bound = rf.get("bound", "hbm")
+        issue = ("%.3f of %s issue" % (rf["frac"], bound)) if bound != "hbm" and rf.get("frac") \
+            else ("%s (no counter pass)" % bound if bound != "hbm" else "-")
+        cpu = ("%.3g (%s core)" % (cb["value"], cb.get("cores", "?"))) if cb.get("value") else "-"
+        rows.append("| %s | %s | %.3g %s | %.3f | %.0f | %.3f | %s | %s | %s |" % (
             name, d["config"]["workload"], d["value"], d["unit"], d["ms_per_step"],
-            rf.get("achieved", 0.0), rf.get("frac", 0.0), cb.get("value", 0.0),
-            cb.get("cores", "?"), par.get("bit_exact")))
-    print("| workload | shape | value | ms / launch | GB/s | frac of 8 TB/s | CPU port | bit-exact |")
-    print("|---|---|---|---|---|---|---|---|")
+            hbm.get("achieved") or 0.0, hbm.get("frac") or 0.0, issue, cpu, par.get("bit_exact")))
+    print("| workload | shape | value | ms / launch | GB/s | frac of 8 TB/s | issue bound | CPU port | bit-exact |")
+    print("|---|---|---|---|---|---|---|---|---|")
     print("\n".join(rows))
 
 
