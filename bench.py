@@ -486,6 +486,11 @@ def step_bench(a, rk):
                 "traffic": traffic, "traffic_note": tnote, "traffic_key": tkey,
                 "traffic_kernels": ["k_group_fast"],
                 "alg_bytes_per_launch": alg,
+                "alg_table_bytes": int(kc.sum()) * 16 * 2,
+                "alg_note": ("replies 16 B + instance state 16 B in + 16 B out, executed commands "
+                             "17 B in + 9 B out, per-group scalars, and the group KV tables 16 B "
+                             "per live key in + out (the step re-reads its unchanged table: "
+                             "alg_table_bytes of the total)"),
                 "kernel_ms_avg": kern_avg_ms, "kernel_ms_min": float(np.min(kern_ms)),
                 "timing": "HIP events around each k_group_fast launch on the compute stream",
             },
