@@ -36,6 +36,8 @@ constexpr int kLogBlockBytes = kLogBlock * 16 * kLogWindowVec;
 // the fewest bytes a record can take (catch-up: 8 + a 1-byte varint; durable: 12)
 constexpr int kLogMinRec = 9;
 constexpr int kLogMaxRecs = kLogBlockBytes / kLogMinRec + 2;
+// commands overlapping one window: at most a whole 17 bytes each, plus a partial one per end
+constexpr int kLogMaxCmds = kLogBlockBytes / 17 + 3;
 
 __device__ __forceinline__ uint64_t zigzag(int64_t x) {  // binary.PutVarint's mapping
     return x < 0 ? ~((uint64_t)x << 1) : (uint64_t)x << 1;
@@ -82,11 +84,33 @@ __global__ __launch_bounds__(256) void k_log_block_first(const uint64_t* __restr
     }
 }
 
+// OR the n bytes of w (little-endian dwords, bytes past n zero) into the zeroed LDS window W at
+// byte offset s (may be negative: the part before the window is dropped, as is anything past
+// it): one ds_or_b32 per touched dword, so two writers of one dword (a record boundary inside
+// it) meet in the OR
+template <int ND>
+__device__ __forceinline__ void or_bytes(uint32_t* W, int64_t s, const uint32_t (&w)[ND],
+                                         uint32_t n) {
+    const int64_t d0 = s >> 2;  // floor
+    const uint32_t sh = (uint32_t)(s & 3) * 8u;
+    const uint32_t nout = (uint32_t)(((s & 3) + n + 3) >> 2);
+#pragma unroll
+    for (int i = 0; i <= ND; ++i) {
+        if ((uint32_t)i >= nout) break;
+        const int64_t d = d0 + i;
+        if (d < 0 || d >= kLogBlockBytes / 4) continue;
+        const uint64_t pair = ((uint64_t)(i < ND ? w[i] : 0u) << 32) | (i ? w[i - 1] : 0u);
+        const uint32_t v = (uint32_t)(pair >> (32 - sh));
+        if (v) atomicOr(&W[d], v);
+    }
+}
+
 // rec_off: n+1 record offsets (rec_off[n] = total bytes). One block per 8 KB output window:
-// the records overlapping it are first .. first+nr-1 (blk_first of this block and the next);
-// their headers and the commands overlapping the window are written into an LDS image of the
-// window (a thread per header, a thread per command: op/key/val loads are coalesced across
-// threads), which then goes out as 16-byte vector stores.
+// the records overlapping it are first .. first+nr-1 (blk_first of this block and the next).
+// The window is an LDS image, zeroed, into which every header (a thread per record) and every
+// command overlapping the window (a thread per command: op/key/val loads coalesced across
+// threads; the command -> record map built by the record threads, so no search) is ORed as
+// dwords (17 bytes = 5 dwords shifted into at most 6), then stored as 16-byte vectors.
 __global__ __launch_bounds__(kLogBlock) void k_log_emit(
     int format, const mpx_log_rec* __restrict__ recs, const uint64_t* __restrict__ cmd_off,
     const uint8_t* __restrict__ op, const int64_t* __restrict__ key,
@@ -94,7 +118,8 @@ __global__ __launch_bounds__(kLogBlock) void k_log_emit(
     const uint64_t* __restrict__ blk_first, uint32_t n_blocks, uint8_t* __restrict__ out) {
     __shared__ uint64_t off[kLogMaxRecs + 1];
     __shared__ uint64_t coff[kLogMaxRecs + 1];
-    __shared__ __attribute__((aligned(16))) uint8_t S[kLogBlockBytes];
+    __shared__ uint16_t cmap[kLogMaxCmds];  // command - j_lo -> record index in the window
+    __shared__ __attribute__((aligned(16))) uint32_t W[kLogBlockBytes / 4];
     const uint64_t total = rec_off[n];
     const uint64_t b0 = (uint64_t)blockIdx.x * kLogBlockBytes;
     if (b0 >= total) return;  // uniform per block
@@ -107,25 +132,10 @@ __global__ __launch_bounds__(kLogBlock) void k_log_emit(
         off[k] = rec_off[first + k];
         coff[k] = cmd_off[first + k];
     }
+#pragma unroll
+    for (int i = 0; i < kLogWindowVec; ++i)
+        reinterpret_cast<uint4*>(W)[threadIdx.x + i * kLogBlock] = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    // headers
-    for (uint64_t k = threadIdx.x; k < nr; k += kLogBlock) {
-        const uint64_t rs = off[k], nc = coff[k + 1] - coff[k];
-        const uint32_t hb = (uint32_t)(off[k + 1] - rs - 17 * nc);
-        if (rs + hb <= b0 || rs >= b1) continue;
-        const mpx_log_rec m = recs[first + k];
-        const uint64_t zz = zigzag((int64_t)nc);
-        for (uint32_t h = 0; h < hb; ++h) {
-            const uint64_t o = rs + h;
-            if (o < b0 || o >= b1) continue;
-            uint32_t v;
-            if (h < 4) v = ((uint32_t)m.ballot >> (8 * h)) & 0xFF;
-            else if (h < 8) v = ((uint32_t)m.status >> (8 * (h - 4))) & 0xFF;
-            else if (format == MPX_LOG_DURABLE) v = ((uint32_t)m.inst_no >> (8 * (h - 8))) & 0xFF;
-            else v = uvarint_byte(zz, h - 8);
-            S[o - b0] = (uint8_t)v;
-        }
-    }
     // commands overlapping [b0, b1): [j_lo, j_hi) (all commands of the records strictly
     // inside, the tail of the first record, the head of the last)
     uint64_t j_lo, j_hi;
@@ -139,35 +149,45 @@ __global__ __launch_bounds__(kLogBlock) void k_log_emit(
         const uint64_t c = b1 > csl ? (b1 - csl + 16) / 17 : 0;
         j_hi = coff[L] + c < coff[L + 1] ? coff[L] + c : coff[L + 1];
     }
-    for (uint64_t j = j_lo + threadIdx.x; j < j_hi; j += kLogBlock) {
-        uint32_t lo = 0, hi = (uint32_t)nr;  // the record holding command j
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) / 2;
-            if (coff[mid] <= j) lo = mid;
-            else hi = mid;
+    // headers, and the command -> record map
+    for (uint64_t k = threadIdx.x; k < nr; k += kLogBlock) {
+        const uint64_t rs = off[k], c0 = coff[k], c1 = coff[k + 1], nc = c1 - c0;
+        for (uint64_t j = c0 > j_lo ? c0 : j_lo; j < c1 && j < j_hi; ++j)
+            cmap[j - j_lo] = (uint16_t)k;
+        const uint32_t hb = (uint32_t)(off[k + 1] - rs - 17 * nc);
+        if (rs + hb <= b0 || rs >= b1) continue;
+        const mpx_log_rec m = recs[first + k];
+        uint32_t h[5] = {(uint32_t)m.ballot, (uint32_t)m.status, 0u, 0u, 0u};
+        if (format == MPX_LOG_DURABLE) {
+            h[2] = (uint32_t)m.inst_no;
+        } else {
+            const uint64_t zz = zigzag((int64_t)nc);
+            for (uint32_t q = 0; q + 8 < hb; ++q) h[2 + (q >> 2)] |= uvarint_byte(zz, q) << (8 * (q & 3));
         }
-        while (lo + 1 < nr && coff[lo + 1] <= j) ++lo;  // skip records without commands
+        or_bytes(W, (int64_t)(rs - b0), h, hb);
+    }
+    __syncthreads();
+    for (uint64_t j = j_lo + threadIdx.x; j < j_hi; j += kLogBlock) {
+        const uint32_t lo = cmap[j - j_lo];
         const uint64_t nc = coff[lo + 1] - coff[lo];
         const uint64_t cs = off[lo + 1] - 17 * nc;  // commands of record lo start here
         const uint64_t pos = cs + 17 * (j - coff[lo]);
         const uint32_t o8 = op[j];
         const uint64_t k8 = (uint64_t)key[j], v8 = (uint64_t)val[j];
-#pragma unroll
-        for (int f = 0; f < 17; ++f) {
-            const uint64_t o = pos + f;
-            if (o < b0 || o >= b1) continue;
-            const uint32_t v = f == 0 ? o8 : f < 9 ? (uint32_t)(k8 >> (8 * (f - 1))) & 0xFF
-                                                   : (uint32_t)(v8 >> (8 * (f - 9))) & 0xFF;
-            S[o - b0] = (uint8_t)v;
-        }
+        const uint32_t kl = (uint32_t)k8, kh = (uint32_t)(k8 >> 32);
+        const uint32_t vl = (uint32_t)v8, vh = (uint32_t)(v8 >> 32);
+        const uint32_t c[5] = {o8 | (kl << 8), (kl >> 24) | (kh << 8), (kh >> 24) | (vl << 8),
+                               (vl >> 24) | (vh << 8), vh >> 24};
+        or_bytes(W, (int64_t)pos - (int64_t)b0, c, 17);
     }
     __syncthreads();
     const uint32_t bytes = (uint32_t)(b1 - b0);
+    const uint8_t* S = reinterpret_cast<const uint8_t*>(W);
     uint8_t* dst = out + b0;
     if (((uintptr_t)dst & 15) == 0) {
         const uint32_t nv = bytes / 16;
         for (uint32_t i = threadIdx.x; i < nv; i += kLogBlock)
-            st_stream(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(S)[i]);
+            st_stream(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(W)[i]);
         for (uint32_t i = nv * 16 + threadIdx.x; i < bytes; i += kLogBlock) dst[i] = S[i];
     } else {
         for (uint32_t i = threadIdx.x; i < bytes; i += kLogBlock) dst[i] = S[i];
