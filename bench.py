@@ -112,6 +112,10 @@ def parse():
     ap.add_argument("--kv-capacity", type=int, default=0,
                     help="apply: engine key capacity (0 = --apply-keys; the table gets >= 2x slots, load <= 1/2)")
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
+    ap.add_argument("--fused-totals", action="store_true",
+                    help="step: the totals from the step kernels (mpx_group_step_totals_dev) "
+                         "instead of their own launch after the group step (A/B: the fast "
+                         "kernel's per-group atomics cost about what the launch saves)")
     ap.add_argument("--apply-path", default="auto",
                     choices=["auto", "small", "sorted", "partitioned"],
                     help="apply: mpx_config.apply_path (auto = by call size)")
@@ -392,10 +396,15 @@ def step_bench(a, rk):
             eng.stream_wait_event(comp, ev_comm[buf])
         if timed:
             eng.event_record(ev_k[i][0], comp)
-        eng.group_step_dev(steps[buf], comp)
+        # the group step, then its totals (decided, executed instances, executed commands)
+        if a.fused_totals:
+            eng.group_step_totals_dev(steps[buf], d["tot"][buf].ptr, comp)
+        else:
+            eng.group_step_dev(steps[buf], comp)
         if timed:
             eng.event_record(ev_k[i][1], comp)
-        eng.step_totals_dev(steps[buf], d["tot"][buf].ptr, comp)
+        if not a.fused_totals:
+            eng.step_totals_dev(steps[buf], d["tot"][buf].ptr, comp)
         eng.event_record(ev_done[buf], comp)
         eng.stream_wait_event(comm, ev_done[buf])
         eng.step_allreduce_oop_dev(d["wms"][buf].ptr, d["wmr"][buf].ptr, G_total,

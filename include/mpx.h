@@ -358,6 +358,11 @@ int mpx_group_step_dev(mpx_engine* eng, const mpx_group_batch* b, void* stream);
 #define MPX_STEP_TOTALS 3
 int mpx_step_totals_dev(mpx_engine* eng, const mpx_group_batch* b, int64_t* d_totals,
                         void* stream);
+/* mpx_group_step_dev and mpx_step_totals_dev in one: the step kernels accumulate the totals
+ * as they finish each group and write d_totals[0..2] (same values) at their end, so a step is
+ * two kernel launches instead of three (b->n_decided optional here).                       */
+int mpx_group_step_totals_dev(mpx_engine* eng, const mpx_group_batch* b, int64_t* d_totals,
+                              void* stream);
 
 /* ---- multi-GPU: the one collective (RCCL over xGMI) -------------------------------------
  * Each rank owns a block of groups; non-owned entries must hold -1. After the call every

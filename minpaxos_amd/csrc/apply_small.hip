@@ -1,26 +1,25 @@
-// apply_small.hip — mpx_apply for replica-sized calls (at most 8192 commands) in ONE launch.
+// apply_small.hip — mpx_apply for replica-sized calls (at most 8192 commands) in TWO launches.
 //
 // Reference: executeCommands (src/bareminpaxos/bareminpaxos.go:1066-1098) drains one committed
 // batch (MAX_BATCH = 5000 commands, :22) and runs (*state.Command).Execute (src/state/state.go:
 // 77-103) on each in log order; conf_prev[i] = state.Conflict (state.go:53-60) of command i with
 // the previous command on the same key in the call. The replica shim calls mpx_apply once per
 // drained batch, so the call's cost is its latency, not its bandwidth: the multi-launch
-// pipelines (about ten dependent launches, ~60 us) are replaced by one 1024-thread workgroup
-// that keeps the call in LDS:
-//   1. commands -> registers (8 per thread, wave w holds positions [512w, 512w + 512));
-//      PUTs find or claim their slot in the engine's table (kvtab.hpp, 64-bit CAS), then the
-//      other commands look theirs up. A command whose key has no slot (never PUT, absent) is
-//      final already: Execute returns NIL (0) and, as no PUT of its key precedes it, it
-//      conflicts with nothing. Every command's default result goes out now: PUT its value, GET
-//      the table value at call start (present ? value : 0), the rest 0.
-//   2. each slot gets a dense group id (LDS open-addressing table, id = table index < 16383);
-//      (id, position) pairs are sorted by id, stably, with two 7-bit LSD passes (wave-level
-//      bit-sliced ballot matching ranks each wave's 64 lanes, per-wave digit counts, one
-//      2048-entry scan) - positions stay in log order within a group.
-//   3. over the sorted groups: the previous command on the key is the left neighbour (conf),
-//      the last PUT before a command a segmented exclusive max-scan of PUT positions (GET
-//      results), and each group's last PUT is committed to the table (value, present bit,
-//      n_present).
+// pipelines (about ten dependent launches, ~60 us) are replaced by
+//   1. k_small_probe, a thread per command over many CUs (the call's scattered table accesses
+//      spread over their memory pipelines): PUTs find or claim their slot in the engine's table
+//      (kvtab.hpp, 64-bit CAS), the other commands look theirs up; every command's default
+//      result goes out (PUT its value, GET the table value at call start, the rest NIL); slot /
+//      resume position and state word per command into the table's probe scratch.
+//   2. k_apply_small, one 1024-thread workgroup that keeps the call in LDS: the lookups that met
+//      a free slot probe again (a PUT of the call may have claimed it); a command whose key has
+//      no slot is final (NIL, no conflict). Each slot gets a dense group id (LDS open
+//      addressing); a command alone on its key in the call is final too but for a PUT's commit;
+//      the (id, position) pairs of shared keys are sorted by id, stably, with two 7-bit LSD
+//      passes (bit-sliced ballot ranks, per-wave digit counts, one 2048-entry scan), and over
+//      the sorted groups the previous command on the key is the left neighbour (conf), the last
+//      PUT before a command a segmented exclusive max-scan of PUT positions (GET results), and
+//      each group's last PUT is committed to the table (value, present bit, n_present).
 // The call epoch is neither read nor advanced: conflicts never reach across calls (orc_apply),
 // and the tags other pipelines compare stay older than their next epoch.
 #include "common.hpp"
@@ -104,6 +103,65 @@ __device__ __forceinline__ uint32_t block_excl_sum(SmallLds& S, uint32_t v) {
 }
 }  // namespace
 
+// ---- 1. probe: one command per thread, spread over many CUs ---------------------------------
+// A PUT finds or claims its key's slot (linear probe in the key's bucket, 64-bit CAS,
+// kvtab.hpp); another command stops at its key or at the first free slot (a PUT of the same call
+// may claim the key there later: the resolve kernel probes those again from the position
+// recorded here). Every command's default result goes out now: PUT its value, GET the value at
+// call start (present ? value : NIL), the rest NIL; a slot's state word is kept for the commits.
+// probe[p] = slot | kMissBit (resume position) | kNoSlot; probe[kSmMax + p] = state word.
+constexpr uint32_t kMissBit = 0x80000000u;
+constexpr int kProbeBlock = 256;
+__global__ __launch_bounds__(kProbeBlock) void k_small_probe(KvTable t, const uint8_t* __restrict__ op,
+                                                       const int64_t* __restrict__ key,
+                                                       const int64_t* __restrict__ val, uint32_t m,
+                                                       int64_t* __restrict__ ret, uint32_t* err) {
+    const uint32_t p = blockIdx.x * kProbeBlock + threadIdx.x;
+    if (p >= m) return;
+    const uint8_t o = op[p];
+    const int64_t k = key[p];
+    const bool put = o == MPX_OP_PUT;
+    if (put) ret[p] = val[p];  // a PUT returns its value
+    uint32_t slot = kNoSlot;
+    if (k == kSentinel) {
+        slot = (uint32_t)t.cap;  // the sentinel key lives in the side slot
+    } else {
+        const uint64_t h = hash64((uint64_t)k);
+        const uint32_t base = bucket_of(h, t.lgnb) << kLgSB;
+        uint32_t sp = home_of(h);
+        for (int step = 0; step < kSB; ++step, sp = (sp + 1) & (kSB - 1)) {
+            unsigned long long* a = reinterpret_cast<unsigned long long*>(t.keys + base + sp);
+            unsigned long long cur = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cur == (unsigned long long)kSentinel) {
+                if (!put) {  // not in the table (yet)
+                    slot = kMissBit | (base + sp);
+                    break;
+                }
+                cur = atomicCAS(a, (unsigned long long)kSentinel, (unsigned long long)k);
+                if (cur == (unsigned long long)kSentinel) {
+                    slot = base + sp;  // claimed
+                    break;
+                }
+            }
+            if ((int64_t)cur == k) {
+                slot = base + sp;
+                break;
+            }
+        }
+        if (slot == kNoSlot) raise_err(err, kErrKvFull);  // a full bucket (never for a lookup)
+    }
+    uint32_t st = 0;
+    if (!(slot & kMissBit)) {  // (kNoSlot has the bit too)
+        st = t.state[slot];
+        if (!put) ret[p] = (o == MPX_OP_GET && (st & kPresent)) ? t.vals[slot] : 0;
+    } else if (!put) {
+        ret[p] = 0;  // absent at call start: NIL (a PUT of this call cannot precede a miss)
+    }
+    t.probe[p] = slot;
+    t.probe[kSmMax + p] = st;
+}
+
+// ---- 2.-3. resolve: one 1024-thread workgroup --------------------------------------------
 __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* __restrict__ op,
                                                       const int64_t* __restrict__ key,
                                                       const int64_t* __restrict__ val, uint32_t m,
@@ -112,143 +170,68 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
     __shared__ SmallLds S;
 #if MPX_SMALL_STAMP
     unsigned long long _sm_prev = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long _sm_rt0 = _sm_prev, _sm_clk0 = __builtin_amdgcn_s_memtime();
 #endif
     const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
     const uint64_t below = lanes_below(l);
     for (int i = tid; i < kSmHash; i += kSmT) S.tab[i] = 0;
     if (tid == 0) S.n_new = 0;
 
-    // ---- 1. commands, slots, default results --------------------------------------------
-    // the keys wait in LDS (the sort buffers' space, free until step 2), not in registers
-    int64_t* const kl = reinterpret_cast<int64_t*>(&S.buf[0][0]);
     uint8_t o8[kSmPer];
-    uint32_t slot[kSmPer];  // kNoSlot: none (the table has fewer than 2^31 - 1 slots)
+    uint32_t slot[kSmPer];     // kNoSlot: none (the table has fewer than 2^31 - 1 slots)
     uint32_t slot_st[kSmPer];  // the slot's state word after the call (present set)
-    int64_t vr[kSmPer];     // values (a lone PUT commits its own in step 2)
+    int64_t vr[kSmPer];        // values (a lone PUT commits its own)
+    bool pres[kSmPer];
     const uint32_t p0 = (uint32_t)(w * (kSmPer * kWave) + l);  // position of k: p0 + 64 k
     {
-        int64_t kr[kSmPer];  // every load in flight before the first use
+        uint32_t st[kSmPer];
+        int64_t kk[kSmPer];  // (keys for the probes to redo: loaded with the rest, one round trip)
 #pragma unroll
-        for (int k = 0; k < kSmPer; ++k) {
+        for (int k = 0; k < kSmPer; ++k) {  // every load in flight before the first use
             const uint32_t p = p0 + k * kWave;
             const bool v = p < m;
             o8[k] = v ? op[p] : (uint8_t)MPX_OP_NONE;
-            kr[k] = v ? key[p] : 0;
             vr[k] = v ? val[p] : 0;
-            slot[k] = kNoSlot;
+            kk[k] = v ? key[p] : 0;
+            slot[k] = v ? t.probe[p] : kNoSlot;
+            st[k] = v ? t.probe[kSmMax + p] : 0u;
         }
+        SM_STAMP(0);
+        // the probes that met a free slot, again now that every claim of the call is in (the
+        // slots before the recorded position hold other keys for good); a key found now was
+        // claimed by this call: not present at call start, state word 0
+        bool miss[kSmPer], again = false;
 #pragma unroll
         for (int k = 0; k < kSmPer; ++k) {
-            const uint32_t p = p0 + k * kWave;
-            if (p >= m) continue;
-            kl[p] = kr[k];
-            if (o8[k] == MPX_OP_PUT) ret[p] = vr[k];  // a PUT returns its value
+            miss[k] = slot[k] != kNoSlot && (slot[k] & kMissBit);
+            again |= miss[k];
         }
-    }
-    SM_STAMP(0);
-    // Every command probes its key at once (one step of the bucket's linear probe per round,
-    // all of a thread's probes in flight together): a PUT claims the first free slot (64-bit
-    // CAS, kv_insert), another command stops at its key or at a free slot; those that saw a
-    // free slot probe again once every claim is in (a PUT of the same call may have taken it).
-    bool miss[kSmPer];
-    {
-        uint32_t base[kSmPer], s[kSmPer];
-        bool act[kSmPer];
-#pragma unroll
-        for (int k = 0; k < kSmPer; ++k) {
-            const uint32_t p = p0 + k * kWave;
-            act[k] = p < m;
-            miss[k] = false;
-            const int64_t kk = act[k] ? kl[p] : 0;
-            if (act[k] && kk == kSentinel) {  // the sentinel key lives in the side slot
-                slot[k] = (uint32_t)t.cap;
-                act[k] = false;
-            }
-            const uint64_t h = hash64((uint64_t)kk);
-            base[k] = bucket_of(h, t.lgnb) << kLgSB;
-            s[k] = home_of(h);
-        }
-        for (int step = 0; step < kSB; ++step) {
-            unsigned long long cur[kSmPer];
-#pragma unroll
-            for (int k = 0; k < kSmPer; ++k)
-                cur[k] = act[k] ? __hip_atomic_load(reinterpret_cast<unsigned long long*>(
-                                                         t.keys + base[k] + s[k]),
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                : 0ull;
-#pragma unroll
-            for (int k = 0; k < kSmPer; ++k)
-                if (act[k] && o8[k] == MPX_OP_PUT && cur[k] == (unsigned long long)kSentinel)
-                    cur[k] = atomicCAS(reinterpret_cast<unsigned long long*>(t.keys + base[k] + s[k]),
-                                       (unsigned long long)kSentinel,
-                                       (unsigned long long)kl[p0 + k * kWave]);
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < kSmPer; ++k) {
-                if (!act[k]) continue;
-                const bool free_ = cur[k] == (unsigned long long)kSentinel;
-                if ((int64_t)cur[k] == kl[p0 + k * kWave] || (free_ && o8[k] == MPX_OP_PUT)) {
-                    slot[k] = base[k] + s[k];  // the key's slot, or claimed
-                    act[k] = false;
-                } else if (free_) {
-                    miss[k] = true;  // not in the table yet: again after the claims
-                    act[k] = false;
-                } else {
-                    s[k] = (s[k] + 1) & (kSB - 1);
-                    any = true;
-                }
-            }
-            if (!__ballot(any)) break;
-        }
-#pragma unroll
-        for (int k = 0; k < kSmPer; ++k)
-            if (act[k]) raise_err(err, kErrKvFull);  // a full bucket (never for a lookup)
-        SM_STAMP(1);
-        __syncthreads();  // every claim is in the table
-        // misses: from the free slot they saw (the slots before it hold other keys for good)
-        bool again = false;
-#pragma unroll
-        for (int k = 0; k < kSmPer; ++k) again |= miss[k];
         for (int step = 0; step < kSB && __ballot(again); ++step) {
             again = false;
 #pragma unroll
             for (int k = 0; k < kSmPer; ++k) {
                 if (!miss[k]) continue;
+                const uint32_t pos = slot[k] & ~kMissBit;
                 const unsigned long long c = __hip_atomic_load(
-                    reinterpret_cast<unsigned long long*>(t.keys + base[k] + s[k]),
-                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((int64_t)c == kl[p0 + k * kWave]) {
-                    slot[k] = base[k] + s[k];
+                    reinterpret_cast<unsigned long long*>(t.keys + pos), __ATOMIC_RELAXED,
+                    __HIP_MEMORY_SCOPE_AGENT);
+                if ((int64_t)c == kk[k]) {
+                    slot[k] = pos;
                     miss[k] = false;
                 } else if (c == (unsigned long long)kSentinel) {
-                    miss[k] = false;  // absent, and no PUT of this call: no slot
+                    slot[k] = kNoSlot;  // absent, and no PUT of this call: no slot
+                    miss[k] = false;
                 } else {
-                    s[k] = (s[k] + 1) & (kSB - 1);
+                    slot[k] = kMissBit | ((pos & ~(uint32_t)(kSB - 1)) | ((pos + 1) & (kSB - 1)));
                     again = true;
                 }
             }
         }
-    }
-    SM_STAMP(2);
-    // default results of the other commands: GET -> the value at call start, the rest NIL;
-    // the GETs that follow a PUT of their key in this call are rewritten in step 3
-    // (the state word of every slot, so the commits know which keys become present: one plain
-    // store each, no atomic; only this call's workgroup touches the table while it runs)
-    bool pres[kSmPer];
-    {
-        uint32_t st[kSmPer];
-        int64_t tv[kSmPer];
-#pragma unroll
-        for (int k = 0; k < kSmPer; ++k) {
-            const bool h = p0 + k * kWave < m && slot[k] != kNoSlot;
-            st[k] = h ? t.state[slot[k]] : 0u;
-            tv[k] = h && o8[k] == MPX_OP_GET ? t.vals[slot[k]] : 0;
-        }
+        SM_STAMP(1);
 #pragma unroll
         for (int k = 0; k < kSmPer; ++k) {
             const uint32_t p = p0 + k * kWave;
             pres[k] = (st[k] & kPresent) != 0;
-            if (p < m && o8[k] != MPX_OP_PUT) ret[p] = pres[k] ? tv[k] : 0;
             if (p >= m) continue;
             if (conf && slot[k] == kNoSlot) conf[p] = 0;  // nothing precedes it on a PUT-less key
             S.op[p] = (uint8_t)(o8[k] | (pres[k] ? kOpPresent : 0));  // op + present at call start
@@ -257,6 +240,7 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
             slot_st[k] = st[k];
         }
     }
+    SM_STAMP(2);
     SM_STAMP(3);
     // ---- 2. group ids, lone commands, the stable sort by id ----------------------------------
     // Each slot gets a dense id (LDS open addressing: tab[id] = slot + 1, bit 31 set once a
@@ -264,7 +248,7 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
     // common case of a replica batch over a large key space - is final after step 1 but for
     // its commit (a PUT's value and present bit); only the commands of shared keys are sorted
     // and scanned, compacted in log order.
-    __syncthreads();  // tab cleared; the keys in the sort buffers are dead
+    __syncthreads();  // tab cleared
     uint32_t id[kSmPer];
 #pragma unroll
     for (int k = 0; k < kSmPer; ++k) {
@@ -327,6 +311,28 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
     SM_STAMP(4);
     // the shared commands' (id, position) pairs, stably by id: two 7-bit LSD passes; entry j of
     // a pass is held by thread (j / 512) * 64 + j % 64, like the positions above
+#ifndef MPX_SMALL_RANK
+#define MPX_SMALL_RANK 1
+#endif
+    if (MPX_SMALL_RANK && m2 <= (uint32_t)kSmT) {
+        // few shared commands (a batch over a large key space): each entry's rank is the count
+        // of smaller entries (id << 13 | position is unique, so the order is stable), one pass
+        // of broadcast LDS reads instead of the two radix passes' dozen barriers
+        __syncthreads();  // every shared command's entry is in buf[0]
+        const uint32_t e = (uint32_t)tid < m2 ? S.buf[0][tid] : 0u;
+        uint32_t r = 0;
+        if ((uint32_t)tid < m2) {
+            const uint4* b4 = reinterpret_cast<const uint4*>(S.buf[0]);
+            const uint32_t n4 = m2 / 4;
+            for (uint32_t i = 0; i < n4; ++i) {
+                const uint4 q = b4[i];
+                r += (q.x < e) + (q.y < e) + (q.z < e) + (q.w < e);
+            }
+            for (uint32_t i = n4 * 4; i < m2; ++i) r += S.buf[0][i] < e;
+        }
+        __syncthreads();
+        if ((uint32_t)tid < m2) S.buf[0][r] = e;
+    } else
     for (int pass = 0; pass < 2; ++pass) {
         const uint32_t* src = S.buf[pass];
         uint32_t* dst = S.buf[pass ^ 1];
@@ -469,6 +475,12 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
     __syncthreads();
     if (tid == 0 && S.n_new) atomicAdd(t.n_present, (unsigned long long)S.n_new);
     SM_STAMP(6);
+#if MPX_SMALL_STAMP
+    if (threadIdx.x == 0) {  // shader clock ticks and 100 MHz ticks of the whole kernel
+        atomicAdd(&mpx_small_stamp[8], __builtin_amdgcn_s_memtime() - _sm_clk0);
+        atomicAdd(&mpx_small_stamp[9], __builtin_amdgcn_s_memrealtime() - _sm_rt0);
+    }
+#endif
 }
 
 #if MPX_SMALL_STAMP
@@ -489,6 +501,8 @@ hipError_t launch_apply_small(KvTable& t, const uint8_t* op, const int64_t* key,
                               hipStream_t stream) {
     if (!m) return hipSuccess;
     if (m > (uint64_t)kSmMax || t.cap >= 0x7FFFFFFEull) return hipErrorInvalidValue;
+    k_small_probe<<<(unsigned)((m + kProbeBlock - 1) / kProbeBlock), kProbeBlock, 0, stream>>>(
+        t, op, key, val, (uint32_t)m, ret, err);
     k_apply_small<<<1, kSmT, 0, stream>>>(t, op, key, val, (uint32_t)m, ret, conf, err);
     return hipGetLastError();
 }

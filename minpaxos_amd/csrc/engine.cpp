@@ -155,6 +155,7 @@ void free_kv(mpx::KvTable& t) {
     if (t.state) (void)hipFree(t.state);
     if (t.n_present) (void)hipFree(t.n_present);
     if (t.epoch) (void)hipFree(t.epoch);
+    if (t.probe) (void)hipFree(t.probe);
     t = mpx::KvTable{};
 }
 
@@ -172,7 +173,8 @@ int ensure_kv(mpx_engine* e) {
         hipMalloc(&t.vals, (cap + 1) * 8) != hipSuccess ||
         hipMalloc(&t.state, (cap + 1) * 4) != hipSuccess ||
         hipMalloc(&t.n_present, sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&t.epoch, 2 * sizeof(uint32_t)) != hipSuccess) {
+        hipMalloc(&t.epoch, 2 * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&t.probe, 2 * MPX_APPLY_SMALL_MAX * sizeof(uint32_t)) != hipSuccess) {
         (void)hipGetLastError();
         free_kv(t);
         return fail(e, MPX_E_NOMEM, "KV table allocation failed");
@@ -624,7 +626,9 @@ int mpx_conflict_batch_dev(mpx_engine* e, const uint8_t* d_op, const int64_t* d_
 }
 
 // ---- fused group step -------------------------------------------------------------------------
-int mpx_group_step_dev(mpx_engine* e, const mpx_group_batch* b, void* stream) {
+namespace {
+// the device-pointer group step; d_totals (optional) gets the step totals from the same kernels
+int group_step_dev(mpx_engine* e, const mpx_group_batch* b, int64_t* d_totals, void* stream) {
     if (!e) return MPX_E_INVAL;
     if (!b) return fail(e, MPX_E_INVAL, "null or invalid argument");
     if (b->n_groups && (!b->recs || !b->grp_rec_off || !b->st_in || !b->st_out ||
@@ -638,9 +642,21 @@ int mpx_group_step_dev(mpx_engine* e, const mpx_group_batch* b, void* stream) {
     if ((uint64_t)b->n_groups * sizeof(uint32_t) > e->worklist.cap)
         return fail(e, MPX_E_INVAL, "n_groups exceeds mpx_config.max_groups");
     HIPCHK(e, mpx::launch_group_step(e->cfg.mode, e->cfg.n_replicas, e->cfg.kv_per_group, b,
-                                     (uint32_t*)e->worklist.p, e->d_wcount, e->d_err,
+                                     (uint32_t*)e->worklist.p, e->d_wcount, d_totals, e->d_err,
                                      pick(e, stream)));
     return MPX_OK;
+}
+}  // namespace
+
+int mpx_group_step_dev(mpx_engine* e, const mpx_group_batch* b, void* stream) {
+    return group_step_dev(e, b, nullptr, stream);
+}
+
+int mpx_group_step_totals_dev(mpx_engine* e, const mpx_group_batch* b, int64_t* d_totals,
+                              void* stream) {
+    if (!e) return MPX_E_INVAL;
+    if (!d_totals) return fail(e, MPX_E_INVAL, "null d_totals");
+    return group_step_dev(e, b, d_totals, stream);
 }
 
 int mpx_step_totals_dev(mpx_engine* e, const mpx_group_batch* b, int64_t* d_totals,
@@ -732,7 +748,7 @@ int mpx_group_step(mpx_engine* e, const mpx_group_batch* hb) {
     if (ipg > 8192) return fail(e, MPX_E_UNSUPPORTED, "more than 8192 instances per group");
     GROW(e, e->worklist, G * sizeof(uint32_t));
     HIPCHK(e, mpx::launch_group_step(e->cfg.mode, N, (uint32_t)K, &db, (uint32_t*)e->worklist.p,
-                                     e->d_wcount, e->d_err, e->stream));
+                                     e->d_wcount, nullptr, e->d_err, e->stream));
     CK(d2h(e, hb->st_out, d + o_st, ni * 16));
     CK(d2h(e, hb->committed_out, d + o_co, G * 4));
     CK(d2h(e, hb->executed_out, d + o_eo, G * 4));

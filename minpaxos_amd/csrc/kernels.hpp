@@ -53,14 +53,19 @@ hipError_t launch_conflict_batch(const uint8_t* op, const int64_t* key, const ui
 
 // fused per-group step: tally + executeCommands against per-group compact KV tables.
 // worklist: n_groups u32 + wcount (device) for groups the fast kernel hands on.
+// totals (optional, device): the step's d_totals[0..2] computed inside the same two kernels
+// (per-group partials into kTotSlots accumulators of the control words, folded by the general
+// kernel's last workgroup), so a step needs no k_step_totals launch.
 hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
                              const mpx_group_batch* b, uint32_t* worklist, uint32_t* wcount,
-                             uint32_t* err, hipStream_t stream);
+                             int64_t* totals, uint32_t* err, hipStream_t stream);
 // d_totals[0..2] = decided instances, executed instances, executed commands of the batch
 // step control words (engine-owned, zeroed once): [0] work-list count, [1] its ticket, [4..9]
-// the totals' 64-bit accumulators, [10] their ticket. Both kernels that consume a count reset
-// it in their last workgroup, so a step launches no memset.
-constexpr int kStepCtlWords = 16;
+// the totals' 64-bit accumulators, [10] their ticket, [16..) the fused totals' partials
+// (kTotSlots x 3 u64, by group % kTotSlots). Every kernel that consumes a count or a partial
+// resets it in its last workgroup, so a step launches no memset.
+constexpr int kTotSlots = 64;
+constexpr int kStepCtlWords = 16 + kTotSlots * 3 * 2;
 hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, uint32_t* ctl,
                               hipStream_t stream);
 
@@ -74,6 +79,8 @@ struct KvTable {
     unsigned long long* n_present;  // device counter
     uint32_t* epoch;     // device: [0] call epoch of mpx_apply (1 .. kKvEpochMax-1), [1] k_epoch_next's
                          // completion counter (0 between calls)
+    uint32_t* probe;     // device, 2 x MPX_APPLY_SMALL_MAX: the replica-batch apply's probe
+                         // results (slot or resume position per command, its state word)
 };
 
 constexpr uint32_t kKvEpochMax = 1u << 30;  // = kvtab.hpp kEpochMax (state bits 2..31)

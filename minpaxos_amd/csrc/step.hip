@@ -375,7 +375,8 @@ __device__ __forceinline__ int fast_slot(FastLds<Cfg>& S, unsigned long long key
 template <int MODE, class Cfg>
 __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int32_t nrep,
                                                          uint32_t kvpg, uint32_t* worklist,
-                                                         uint32_t* wcount, uint32_t* err) {
+                                                         uint32_t* wcount,
+                                                         unsigned long long* tacc, uint32_t* err) {
     MPX_FAST_CONSTS
     __shared__ FastLds<Cfg> S;
     STAMP_DECL
@@ -824,6 +825,17 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
         b.executed_out[g] = stop > lo ? (int32_t)(stop - 1) : ex_in;
         b.kv_cnt_out[g] = total < kvpg ? total : kvpg;
         if (b.n_decided) b.n_decided[g] = S.ndec;
+        if (tacc) {  // the step totals' partials (no-return atomics: the next kernel reads them)
+            unsigned long long* a = tacc + (g % kTotSlots) * 3;
+            const unsigned long long xi = stop > lo ? (unsigned long long)(stop - lo) : 0ull;
+            if (S.ndec) __hip_atomic_fetch_add(a, (unsigned long long)S.ndec, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+            if (xi) {
+                __hip_atomic_fetch_add(a + 1, xi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(a + 2, (unsigned long long)(x1 - x0), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
     }
     ebits &= 0x7FFFFFFFu;
     if (ebits) raise_err(err, ebits);
@@ -856,7 +868,7 @@ struct GenLds {
 
 template <int MODE>
 __device__ void group_general(GenLds& S, const mpx_group_batch& b, uint32_t g, int32_t nrep,
-                             uint32_t kvpg, uint32_t* err) {
+                             uint32_t kvpg, unsigned long long* tacc, uint32_t* err) {
     const int t = threadIdx.x, l = lane_id(), w = t / kWave;
     const int32_t half = nrep >> 1;
     const uint64_t ipg = b.ipg;
@@ -899,7 +911,7 @@ __device__ void group_general(GenLds& S, const mpx_group_batch& b, uint32_t g, i
     if (b.decided)
         for (uint64_t i = t; i < ipg; i += kStepBlock)
             b.decided[gi0 + i] = (S.dec_bits[i >> 5] >> (i & 31)) & 1u;
-    if (b.n_decided) {  // popcount of the decided bitmap (bits past ipg stay 0)
+    if (b.n_decided || tacc) {  // popcount of the decided bitmap (bits past ipg stay 0)
         uint32_t c = 0;
         for (uint64_t i = t; i < (ipg + 31) / 32; i += kStepBlock) c += __popc(S.dec_bits[i]);
         if (c) atomicAdd(&S.ndec, c);
@@ -960,6 +972,15 @@ __device__ void group_general(GenLds& S, const mpx_group_batch& b, uint32_t g, i
     if (t == 0) {
         b.executed_out[g] = stop > lo ? (int32_t)(stop - 1) : ex_in;
         if (b.n_decided) b.n_decided[g] = S.ndec;
+        if (tacc) {  // partials, performed before the workgroup takes its ticket
+            unsigned long long* a = tacc + (g % kTotSlots) * 3;
+            if (S.ndec) atomic_add_done(a, (unsigned long long)S.ndec);
+            if (stop > lo) {
+                atomic_add_done(a + 1, (unsigned long long)(stop - lo));
+                atomic_add_done(a + 2, (unsigned long long)(b.cmd_off[gi0 + stop] -
+                                                            b.cmd_off[gi0 + lo]));
+            }
+        }
     }
 
     const Dict D{S.dkey, S.dval, S.dfirst, S.cnt, S.hslot, S.dpresent, S.dseen, &S.dn,
@@ -1042,17 +1063,30 @@ template <int MODE>
 __global__ __launch_bounds__(kStepBlock) void k_group_general(mpx_group_batch b, int32_t nrep,
                                                               uint32_t kvpg,
                                                               const uint32_t* worklist,
-                                                              uint32_t* wcount, uint32_t* err) {
+                                                              uint32_t* wcount,
+                                                              unsigned long long* tacc,
+                                                              int64_t* totals, uint32_t* err) {
     __shared__ GenLds S;
     const uint32_t n = *wcount;
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        group_general<MODE>(S, b, worklist[i], nrep, kvpg, err);
+        group_general<MODE>(S, b, worklist[i], nrep, kvpg, tacc, err);
         __syncthreads();
     }
-    // the last workgroup to finish (every one has read the count) zeroes it for the next step
-    if (threadIdx.x == 0 && atomicAdd(wcount + 1, 1u) == gridDim.x - 1) {
-        wcount[0] = 0;
-        wcount[1] = 0;
+    // the last workgroup to finish (every one has read the count and performed its partials)
+    // zeroes the count for the next step and folds the totals' partials
+    if (threadIdx.x == 0) {
+        const uint32_t k = __hip_atomic_fetch_add(wcount + 1, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        if (k == gridDim.x - 1) {
+            wcount[0] = 0;
+            wcount[1] = 0;
+            if (tacc) {
+                unsigned long long s[3] = {0ull, 0ull, 0ull};
+                for (int q = 0; q < kTotSlots; ++q)
+                    for (int i = 0; i < 3; ++i) s[i] += atomic_take(tacc + q * 3 + i);
+                for (int i = 0; i < 3; ++i) totals[i] = (int64_t)s[i];
+            }
+        }
     }
 }
 
@@ -1065,9 +1099,9 @@ __global__ void k_fill_worklist(uint32_t* worklist, uint32_t* wcount, uint32_t n
 namespace {
 template <int MODE, class Cfg>
 void launch_fast(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t* worklist,
-                 uint32_t* wcount, uint32_t* err, hipStream_t stream) {
+                 uint32_t* wcount, unsigned long long* tacc, uint32_t* err, hipStream_t stream) {
     k_group_fast<MODE, Cfg><<<b->n_groups, Cfg::kFT, 0, stream>>>(*b, nrep, kvpg, worklist, wcount,
-                                                                   err);
+                                                                   tacc, err);
 }
 // the smallest fast-path variant the batch's shape fits (0 = none: every group is general)
 int fast_variant(int32_t nrep, uint32_t ipg, uint32_t kvpg) {
@@ -1080,32 +1114,36 @@ int fast_variant(int32_t nrep, uint32_t ipg, uint32_t kvpg) {
 }
 template <int MODE>
 void launch_step(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t* worklist,
-                 uint32_t* wcount, uint32_t* err, hipStream_t stream) {
+                 uint32_t* wcount, int64_t* totals, uint32_t* err, hipStream_t stream) {
+    unsigned long long* tacc =
+        totals ? reinterpret_cast<unsigned long long*>(wcount + 16) : nullptr;
     switch (fast_variant(nrep, b->ipg, kvpg)) {
-    case 1: launch_fast<MODE, FastBase>(b, nrep, kvpg, worklist, wcount, err, stream); break;
-    case 2: launch_fast<MODE, FastRecs>(b, nrep, kvpg, worklist, wcount, err, stream); break;
-    case 3: launch_fast<MODE, FastKeys>(b, nrep, kvpg, worklist, wcount, err, stream); break;
-    case 4: launch_fast<MODE, FastWide>(b, nrep, kvpg, worklist, wcount, err, stream); break;
+    case 1: launch_fast<MODE, FastBase>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
+    case 2: launch_fast<MODE, FastRecs>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
+    case 3: launch_fast<MODE, FastKeys>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
+    case 4: launch_fast<MODE, FastWide>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
     default:
         k_fill_worklist<<<(b->n_groups + 255) / 256, 256, 0, stream>>>(worklist, wcount,
                                                                        b->n_groups);
     }
     const unsigned gen_grid = b->n_groups < 256 ? b->n_groups : 256;  // one per CU (LDS)
-    k_group_general<MODE><<<gen_grid, kStepBlock, 0, stream>>>(*b, nrep, kvpg, worklist, wcount,
-                                                               err);
+    k_group_general<MODE><<<gen_grid ? gen_grid : 1, kStepBlock, 0, stream>>>(
+        *b, nrep, kvpg, worklist, wcount, tacc, totals, err);
 }
 }  // namespace
 
 hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
                              const mpx_group_batch* b, uint32_t* worklist, uint32_t* wcount,
-                             uint32_t* err, hipStream_t stream) {
-    if (!b->n_groups) return hipSuccess;
+                             int64_t* totals, uint32_t* err, hipStream_t stream) {
+    if (!b->n_groups)
+        return totals ? hipMemsetAsync(totals, 0, 3 * sizeof(int64_t), stream) : hipSuccess;
     if (kv_per_group > (uint32_t)kDCap) return hipErrorInvalidValue;
     if (b->ipg > (uint32_t)kMaxIpgBits) return hipErrorInvalidValue;
     if (mode == MPX_MODE_MIN)
-        launch_step<MPX_MODE_MIN>(b, nrep, kv_per_group, worklist, wcount, err, stream);
+        launch_step<MPX_MODE_MIN>(b, nrep, kv_per_group, worklist, wcount, totals, err, stream);
     else
-        launch_step<MPX_MODE_CLASSIC>(b, nrep, kv_per_group, worklist, wcount, err, stream);
+        launch_step<MPX_MODE_CLASSIC>(b, nrep, kv_per_group, worklist, wcount, totals, err,
+                                      stream);
     return hipGetLastError();
 }
 

@@ -270,6 +270,11 @@ class Engine:
     def group_step_dev(self, gb, stream=None):
         self._check(self.lib.mpx_group_step_dev(self.h, C.byref(gb), stream), "mpx_group_step_dev")
 
+    def group_step_totals_dev(self, gb, d_totals, stream=None):
+        """mpx_group_step_totals_dev: the group step with its totals from the same kernels"""
+        self._check(self.lib.mpx_group_step_totals_dev(self.h, C.byref(gb), d_totals, stream),
+                    "mpx_group_step_totals_dev")
+
     def step_totals_dev(self, gb, d_totals, stream=None):
         """d_totals[0..2] = decided instances, executed instances, executed commands"""
         self._check(self.lib.mpx_step_totals_dev(self.h, C.byref(gb), d_totals, stream),

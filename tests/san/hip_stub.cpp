@@ -239,14 +239,23 @@ hipError_t launch_conflict_batch(const uint8_t*, const int64_t*, const uint64_t*
                                  uint8_t*, hipStream_t) { return hipSuccess; }
 #if MPX_STUB_ORACLE
 // the group step through the oracle; its error codes become the kernels' error-word bits
+hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, uint32_t*, hipStream_t);
 hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group, const mpx_group_batch* b,
-                             uint32_t*, uint32_t*, uint32_t* err, hipStream_t) {
-    const int rc = orc_group_step(nrep, mode, b, kv_per_group);
+                             uint32_t*, uint32_t* ctl, int64_t* totals, uint32_t* err,
+                             hipStream_t s) {
+    // the fused form needs the per-group decided counts the oracle writes to n_decided
+    std::vector<uint32_t> nd;
+    mpx_group_batch bb = *b;
+    if (totals && !bb.n_decided) {
+        nd.resize(b->n_groups);
+        bb.n_decided = nd.data();
+    }
+    const int rc = orc_group_step(nrep, mode, &bb, kv_per_group);
     if (rc == MPX_E_NIL_INSTANCE) *err |= kErrNil;
     else if (rc == MPX_E_BAD_ID) *err |= kErrBadId;
     else if (rc == MPX_E_KV_FULL) *err |= kErrKvFull;
     else if (rc) *err |= kErrInval;
-    return hipSuccess;
+    return totals ? launch_step_totals(&bb, totals, ctl, s) : hipSuccess;
 }
 // k_step_totals (step.hip) over host memory
 hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, uint32_t*, hipStream_t) {
@@ -268,7 +277,7 @@ hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, uint32_
 }
 #else
 hipError_t launch_group_step(int, int32_t, uint32_t, const mpx_group_batch*, uint32_t*, uint32_t*,
-                             uint32_t*, hipStream_t) { return hipSuccess; }
+                             int64_t*, uint32_t*, hipStream_t) { return hipSuccess; }
 hipError_t launch_step_totals(const mpx_group_batch*, int64_t*, uint32_t*, hipStream_t) { return hipSuccess; }
 #endif
 uint64_t apply_chunk_commands(uint64_t c, uint64_t m) { return c ? c : m; }

@@ -9,6 +9,7 @@ import pytest
 import gen_cases
 import kat_cases
 from oracle_lib import Oracle, OracleError
+from minpaxos_amd import _lib
 from minpaxos_amd import records as R
 from minpaxos_amd import synth
 from minpaxos_amd.engine import MpxError
@@ -296,6 +297,26 @@ def test_apply_small_calls(mk_engine, path):
         wk, wv = o.kv_export()
         assert np.array_equal(gk, wk) and np.array_equal(gv, wv), m
         assert e.kv_size() == len(wk)
+    # wide key spaces: almost every command alone on its key (the sort sees a few dozen shared
+    # ones), and one call where exactly 1024 / 1025 commands share keys (the rank / radix switch)
+    for m, kr, seed in ((8192, 1 << 40, 95), (5000, 1 << 20, 96)):
+        op, key, val = synth.commands(m, kr, 0.5, "uniform", seed=seed)
+        gr, gc = e.apply(op, key, val)
+        wr, wc = o.apply(op, key, val)
+        assert np.array_equal(gr, wr) and np.array_equal(gc, wc), m
+    for n_sh in (1024, 1025):
+        op, key, val = synth.commands(6000, 1 << 40, 0.5, "uniform", seed=n_sh)
+        op[:] = R.OP_PUT  # every command gets a slot: exactly n_sh are shared
+        key = key + (1 << 41)  # fresh, distinct
+        key[:n_sh // 2] = key[n_sh // 2:n_sh // 2 * 2]  # n_sh // 2 pairs share a key ...
+        if n_sh % 2:
+            key[n_sh - 1] = key[0]  # ... and one triple
+        gr, gc = e.apply(op, key, val)
+        wr, wc = o.apply(op, key, val)
+        assert np.array_equal(gr, wr) and np.array_equal(gc, wc), n_sh
+    gk, gv = e.kv_export()
+    wk, wv = o.kv_export()
+    assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
     # the device-pointer form, one MAX_BATCH call
     from minpaxos_amd.devbuf import Arena
     op, key, val = synth.commands(5000, 1 << 12, 0.5, "uniform", seed=92)
@@ -564,3 +585,71 @@ def test_group_step_variants(mk_engine, shape, mode):
     except OracleError:
         return
     _cmp_group(e.group_step(b2, want["kv_cnt"], want["kv_key"], want["kv_val"]), want2, G, K)
+
+
+def _dev_group_batch(ar, b, N, K, with_nd):
+    """the device-pointer mpx_group_batch of a host batch dict (empty input tables)"""
+    G, ipg, m = b["n_groups"], b["ipg"], len(b["op"])
+    d = dict(recs=ar.put(b["recs"]), off=ar.put(b["grp_rec_off"]), st_in=ar.put(b["st_in"]),
+             st_out=ar.put(b["st_in"]), ci=ar.put(b["committed_in"]),
+             co=ar.empty(G, np.int32), ei=ar.put(b["executed_in"]), eo=ar.empty(G, np.int32),
+             pi=ar.put(b["peer_in"]), po=ar.empty(G * N, np.int32), op=ar.put(b["op"]),
+             key=ar.put(b["key"]), val=ar.put(b["val"]), coff=ar.put(b["cmd_off"]),
+             hc=ar.put(b["has_cmds"]) if b.get("has_cmds") is not None else None,
+             ret=ar.full(m, np.int64, 0), conf=ar.full(m, np.uint8, 0),
+             kc0=ar.full(G, np.uint32, 0), kk0=ar.full(G * K, np.int64, 0),
+             kv0=ar.full(G * K, np.int64, 0), kc1=ar.full(G, np.uint32, 0),
+             kk1=ar.full(G * K, np.int64, 0), kv1=ar.full(G * K, np.int64, 0),
+             nd=ar.full(G, np.uint32, 0) if with_nd else None)
+    p = lambda x: x.ptr if x is not None else None  # noqa: E731
+    gb = _lib.MpxGroupBatch(
+        G, ipg, p(d["recs"]), p(d["off"]), p(d["st_in"]), p(d["st_out"]), p(d["ci"]), p(d["co"]),
+        p(d["ei"]), p(d["eo"]), p(d["pi"]), p(d["po"]), p(d["op"]), p(d["key"]), p(d["val"]),
+        p(d["coff"]), p(d["hc"]), p(d["ret"]), p(d["conf"]), p(d["kc0"]), p(d["kk0"]),
+        p(d["kv0"]), p(d["kc1"]), p(d["kk1"]), p(d["kv1"]), None, p(d["nd"]))
+    return gb, d
+
+
+def _want_totals(b, want):
+    """decided instances, executed instances, executed commands of one step (oracle outputs)"""
+    G, ipg = b["n_groups"], b["ipg"]
+    coff = b["cmd_off"].astype(np.int64)
+    xi = xc = 0
+    for g in range(G):
+        lo, eo = max(int(b["executed_in"][g]) + 1, 0), int(want["executed_out"][g])
+        if lo <= eo < ipg:
+            xi += eo - lo + 1
+            xc += int(coff[g * ipg + eo + 1] - coff[g * ipg + lo])
+    return [int(want["decided"].sum()), xi, xc]
+
+
+@pytest.mark.parametrize("kind", ["fast", "general"])
+def test_group_step_fused_totals(mk_engine, kind):
+    """mpx_group_step_totals_dev: the step totals accumulated by the step kernels (fast-path
+    groups with no-return atomics, work-list groups in the general kernel, folded by its last
+    workgroup) equal the oracle's and mpx_step_totals_dev's, with and without n_decided, over
+    repeated steps (the partials reset themselves) and after a plain mpx_group_step_dev"""
+    from minpaxos_amd.devbuf import Arena
+    if kind == "fast":
+        N, K = 5, 256
+        b = synth.group_batch(300, 256, N, 4, 256, seed=77)
+    else:  # > 1024 commands per group: every group goes through the work list
+        N, K = 3, 1024
+        b = synth.group_batch(64, 128, N, 9, 800, seed=78)
+    b.setdefault("has_cmds", None)
+    e, o = mk_engine(N, R.MODE_MIN, kv_per_group=K), Oracle(N, R.MODE_MIN, kv_per_group=K)
+    want = _want_totals(b, o.group_step(b))
+    with Arena(e) as ar:
+        for with_nd in (True, False):
+            gb, d = _dev_group_batch(ar, b, N, K, with_nd)
+            tot = ar.full(3, np.int64, 0x55)
+            e.group_step_dev(gb, e.stream)  # leaves no partials behind
+            for _ in range(3):
+                e.group_step_totals_dev(gb, tot.ptr, e.stream)
+                e.stream_synchronize(e.stream)
+                assert ar.get(tot).tolist() == want
+            if with_nd:
+                tot2 = ar.full(3, np.int64, 0x55)
+                e.step_totals_dev(gb, tot2.ptr, e.stream)
+                e.stream_synchronize(e.stream)
+                assert ar.get(tot2).tolist() == want

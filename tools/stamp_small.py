@@ -10,7 +10,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-PHASES = ["load", "PUT claim", "lookup", "defaults", "ids+lone", "radix x2", "groups+commit"]
+PHASES = ["load", "re-probe", "flags", "-", "ids+lone", "radix x2", "groups+commit"]
 
 
 def main():
@@ -41,6 +41,8 @@ def main():
         tot += us
         print(f"{name:14s} {us:8.2f} us")
     print(f"{'total':14s} {tot:8.2f} us")
+    if buf[9]:
+        print(f"shader clock during the resolve kernel: {buf[8] / (buf[9] / 100.0) / 1e3:.2f} GHz")
 
 
 if __name__ == "__main__":
