@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define MPX_ABI_VERSION 3
+#define MPX_ABI_VERSION 4  /* 4: + mpx_group_step_totals_dev */
 
 /* ---- error codes ---------------------------------------------------------------------- */
 #define MPX_OK 0

@@ -672,7 +672,12 @@ hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const
 // instances have at most kSmall commands (MAX_BATCH-sized instances are rare) and tests all
 // |b1| x |b2| products in registers. The wave then takes its larger pairs one at a time, lanes
 // striding over the products with an early exit on the first hit.
-constexpr int kSmall = 8;
+// (4: the products of two 4-command instances in registers take 16 key registers, not 32, and
+// the kernel runs at higher occupancy; pairs with more commands take the wave path)
+#ifndef MPX_CONF_SMALL
+#define MPX_CONF_SMALL 4
+#endif
+constexpr int kSmall = MPX_CONF_SMALL;
 constexpr int kConfBlock = 256;
 constexpr int kStage = 2560;
 

@@ -114,7 +114,10 @@ __global__ void k_fan_empty(uint64_t* client_off, uint32_t n_clients) {
 constexpr uint32_t kFanMaxClients = 1024;
 constexpr int kFanThreads = 512;
 constexpr int kFanWaves = kFanThreads / kWave;        // 8
-constexpr int kFanPer = 8;                            // replies per lane per tile
+#ifndef MPX_FAN_PER
+#define MPX_FAN_PER 8
+#endif
+constexpr int kFanPer = MPX_FAN_PER;                  // replies per lane per tile
 constexpr int kFanSeg = kFanPer * kWave;              // 512 replies per wave segment
 constexpr int kFanTile = kFanSeg * kFanWaves;         // 4096 replies per tile
 constexpr uint32_t kFanMaxSlices = 1024;              // workgroups (client-major histogram columns)

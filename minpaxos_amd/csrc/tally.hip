@@ -25,8 +25,16 @@ namespace mpx {
 // replies are written 0 in the gap pass.
 // Control words (engine-owned, zero between calls): [0] ticket, [1..1+N) MIN keys / [1] CLASSIC
 // "some instance committed", [2] CLASSIC ~first_bad.
+#ifndef MPX_TALLY_WPE
+#define MPX_TALLY_WPE 0
+#endif
+#if MPX_TALLY_WPE
+#define MPX_TALLY_ATTR __attribute__((amdgpu_waves_per_eu(MPX_TALLY_WPE, MPX_TALLY_WPE)))
+#else
+#define MPX_TALLY_ATTR
+#endif
 template <int MODE>
-__global__ __launch_bounds__(kTileBlock) void k_accept_tile(
+__global__ MPX_TALLY_ATTR __launch_bounds__(kTileBlock) void k_accept_tile(
     const mpx_accept_reply* __restrict__ recs, uint64_t n, const mpx_inst_state* __restrict__ st_in,
     mpx_inst_state* __restrict__ st_out, uint64_t n_inst, int32_t base, int32_t half, int32_t nrep,
     int32_t* __restrict__ scalars, uint32_t* __restrict__ ctl, uint8_t* __restrict__ decided,
