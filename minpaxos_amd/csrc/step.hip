@@ -269,7 +269,10 @@ struct FastCfg {
     // the table's start values in LDS (GETs of keys present at the start read them there);
     // the 1024-key variant reads them from the input table instead: its 8 KB would hold the
     // workgroup at 3 per CU (41.7 KB), without them 4 fit (33.5 KB)
-    static constexpr bool kFDvalLds = TB_ <= 512;
+#ifndef MPX_DVAL_LDS_MAX
+#define MPX_DVAL_LDS_MAX 512
+#endif
+    static constexpr bool kFDvalLds = TB_ <= MPX_DVAL_LDS_MAX;
     static_assert(kFCmds % kFT == 0 && kFRecs % kFT == 0, "whole items per thread");
     static_assert(kFCmds / 32 <= kWave, "the new-key bitmap is scanned by one wave");
     static_assert(kWaveCmds < 2047, "kTabLp holds 1 + a wave-relative command index");
