@@ -10,7 +10,7 @@
 //   MPX_LOG_DURABLE  recordInstanceMetadata (bareminpaxos.go:164-174: Ballot u32, Status u32,
 //                    instNo u32) followed by recordCommands (:177-188: Command.Marshal each; a
 //                    nil slice writes nothing), one record per stable-store append.
-// Pipeline: k_log_sizes (bytes per record) -> rocPRIM inclusive scan (record offsets) ->
+// Pipeline: rocPRIM inclusive scan of the record sizes (computed from cmd_off as it reads them) ->
 // k_log_block_first (the record holding each 8 KB output block's first byte) -> k_log_emit:
 // per block, the overlapping records' headers and commands are written into an LDS image of the
 // block (one thread per header, one per command, so the command loads are coalesced) and the
@@ -39,10 +39,10 @@ constexpr int kLogMaxRecs = kLogBlockBytes / kLogMinRec + 2;
 // commands overlapping one window: at most a whole 17 bytes each, plus a partial one per end
 constexpr int kLogMaxCmds = kLogBlockBytes / 17 + 3;
 
-__device__ __forceinline__ uint64_t zigzag(int64_t x) {  // binary.PutVarint's mapping
+__host__ __device__ __forceinline__ uint64_t zigzag(int64_t x) {  // binary.PutVarint's mapping
     return x < 0 ? ~((uint64_t)x << 1) : (uint64_t)x << 1;
 }
-__device__ __forceinline__ uint32_t uvarint_len(uint64_t u) {
+__host__ __device__ __forceinline__ uint32_t uvarint_len(uint64_t u) {
     uint32_t l = 1;
     while (u >= 0x80) {
         u >>= 7;
@@ -54,19 +54,23 @@ __device__ __forceinline__ uint32_t uvarint_byte(uint64_t u, uint32_t k) {
     u >>= 7 * k;
     return (uint32_t)(u & 0x7F) | (u >= 0x80 ? 0x80u : 0u);
 }
-__device__ __forceinline__ uint32_t hdr_bytes(int format, uint64_t ncmd) {
+__host__ __device__ __forceinline__ uint32_t hdr_bytes(int format, uint64_t ncmd) {
     return format == MPX_LOG_CATCHUP ? 8u + uvarint_len(zigzag((int64_t)ncmd)) : 12u;
 }
 }  // namespace
 
-__global__ __launch_bounds__(256) void k_log_sizes(int format, const uint64_t* __restrict__ cmd_off,
-                                                   uint64_t n, uint64_t* __restrict__ sizes) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+// bytes of record i, read by the offsets scan straight from cmd_off (no sizes array: one pass
+// and one launch less than a sizes kernel + a scan of its output)
+struct RecBytes {
+    int format;
+    const uint64_t* cmd_off;
+    __host__ __device__ uint64_t operator()(uint64_t i) const {
         const uint64_t nc = cmd_off[i + 1] - cmd_off[i];
-        sizes[i] = hdr_bytes(format, nc) + 17 * nc;
+        return hdr_bytes(format, nc) + 17 * nc;
     }
-}
+};
+using RecBytesIt =
+    rocprim::transform_iterator<rocprim::counting_iterator<uint64_t>, RecBytes, uint64_t>;
 
 __global__ void k_log_zero(uint64_t* rec_off) { rec_off[0] = 0; }
 
@@ -205,10 +209,11 @@ uint64_t blocks_for(uint64_t n, uint64_t m) {
 
 uint64_t logenc_work_bytes(uint64_t n, uint64_t m) {
     size_t tmp = 0;
-    (void)rocprim::inclusive_scan(nullptr, tmp, (uint64_t*)nullptr, (uint64_t*)nullptr,
-                                  (size_t)(n ? n : 1), rocprim::plus<uint64_t>());
+    const RecBytesIt it(rocprim::counting_iterator<uint64_t>(0), RecBytes{0, nullptr});
+    (void)rocprim::inclusive_scan(nullptr, tmp, it, (uint64_t*)nullptr, (size_t)(n ? n : 1),
+                                  rocprim::plus<uint64_t>());
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
-    return al((n ? n : 1) * 8) + al(tmp) + al(blocks_for(n, m) * 8);
+    return al(tmp) + al(blocks_for(n, m) * 8);
 }
 
 hipError_t launch_encode_log(int format, const mpx_log_rec* recs, uint64_t n,
@@ -221,13 +226,12 @@ hipError_t launch_encode_log(int format, const mpx_log_rec* recs, uint64_t n,
     if (n == 0) return hipGetLastError();
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
     const uint64_t blocks = blocks_for(n, m);
-    uint64_t* sizes = (uint64_t*)work;
-    uint64_t* blk_first = (uint64_t*)((char*)work + al(n * 8));
+    uint64_t* blk_first = (uint64_t*)work;
     void* tmp = (char*)blk_first + al(blocks * 8);
-    size_t tmp_bytes = work_bytes - al(n * 8) - al(blocks * 8);
+    size_t tmp_bytes = work_bytes - al(blocks * 8);
     const uint64_t g = (n + 255) / 256;
     const unsigned gg = (unsigned)(g > 8192 ? 8192 : g);
-    k_log_sizes<<<gg, 256, 0, stream>>>(format, cmd_off, n, sizes);
+    const RecBytesIt sizes(rocprim::counting_iterator<uint64_t>(0), RecBytes{format, cmd_off});
     hipError_t r = rocprim::inclusive_scan(tmp, tmp_bytes, sizes, rec_off + 1, (size_t)n,
                                            rocprim::plus<uint64_t>(), stream);
     if (r != hipSuccess) return r;
