@@ -619,9 +619,40 @@ __device__ __forceinline__ void stage_tile(const SParams& P, uint64_t t0, uint8_
     }
 }
 
+// the tile's bytes for stage_tile, loaded into registers (kStageVec 16-byte pieces per lane)
+constexpr int kStageVec = ((kTB + kE) / 16 + kTL - 1) / kTL;
+__device__ __forceinline__ void load_tile_regs(const SParams& P, uint64_t t0, uint4 (&v)[kStageVec]) {
+#pragma unroll
+    for (int k = 0; k < kStageVec; ++k) {
+        const int i = threadIdx.x + k * kTL;
+        const uint64_t a = t0 + (uint64_t)i * 16;
+        if (i >= (kTB + kE) / 16) {
+            v[k] = make_uint4(0, 0, 0, 0);
+        } else if (a + 16 <= P.len) {
+            v[k] = *reinterpret_cast<const uint4*>(P.buf + a);
+        } else {
+            uint32_t q[4] = {0, 0, 0, 0};
+            for (int b = 0; b < 16; ++b)
+                if (a + b < P.len) q[b >> 2] |= (uint32_t)P.buf[a + b] << (8 * (b & 3));
+            v[k] = make_uint4(q[0], q[1], q[2], q[3]);
+        }
+    }
+}
+
+#ifndef MPX_SD_COUNT_UNION
+#define MPX_SD_COUNT_UNION 1
+#endif
 __global__ __launch_bounds__(kTL) void k_sd_count(SParams P, Work W) {
+#if MPX_SD_COUNT_UNION
+    // the chunk maps are dead once the chunk entries are known: the tile's bytes (loaded into
+    // registers meanwhile) take their LDS, so a workgroup needs 16.5 KB instead of 24.5 KB
+    __shared__ __attribute__((aligned(16))) uint8_t U[kTB + kE];
+    uint8_t* const B = U;
+    uint8_t(*const X)[kE] = reinterpret_cast<uint8_t(*)[kE]>(U);
+#else
     __shared__ __attribute__((aligned(16))) uint8_t B[kTB + kE];
     __shared__ __attribute__((aligned(16))) uint8_t X[kTL][kE];
+#endif
     __shared__ uint8_t G[kTL / 8][kE];
     __shared__ uint8_t GE[kTL / 8];
     __shared__ uint8_t En[kTL];
@@ -634,10 +665,24 @@ __global__ __launch_bounds__(kTL) void k_sd_count(SParams P, Work W) {
         return;
     }
     const uint64_t t0 = (uint64_t)tile * kTB;
+#if MPX_SD_COUNT_UNION
+    uint4 tv[kStageVec];
+    load_tile_regs(P, t0, tv);
+    load_chunk_maps(W, tile, X);
+    __syncthreads();
+    chunk_entries(ent, X, G, GE, En);  // (ends with a barrier: X is dead)
+#pragma unroll
+    for (int k = 0; k < kStageVec; ++k) {
+        const int i = l + k * kTL;
+        if (i < (kTB + kE) / 16) reinterpret_cast<uint4*>(B)[i] = tv[k];
+    }
+    __syncthreads();
+#else
     stage_tile(P, t0, B);
     load_chunk_maps(W, tile, X);
     __syncthreads();
     chunk_entries(ent, X, G, GE, En);
+#endif
     const uint64_t c0 = t0 + (uint64_t)l * kC;
     const Bytes by{P.buf, B, t0, t0 + kTB + kE < P.len ? t0 + kTB + kE : P.len};
     uint32_t cnt[4] = {0, 0, 0, 0};
