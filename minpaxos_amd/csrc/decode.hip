@@ -365,16 +365,29 @@ __global__ __launch_bounds__(kTileLanes) void k_dec_emit(
     const uint8_t* __restrict__ buf, uint64_t len, const GEntry* __restrict__ tres,
     const ulonglong2* __restrict__ xmap, mpx_accept_reply* __restrict__ ar_out, uint64_t ar_cap,
     mpx_peer_frame* __restrict__ oth_out, uint64_t oth_cap) {
-    __shared__ uint8_t X[2 * kTileLanes - 1][kXPad];
+#ifndef MPX_DEC_EMIT_UNION
+#define MPX_DEC_EMIT_UNION 1
+#endif
     __shared__ uint8_t E[2 * kTileLanes - 1];  // entry per tree node (kXStop = dead)
+#if MPX_DEC_EMIT_UNION
+    // the exit-map tree is dead once every chunk has its entry: the tile's bytes (loaded into
+    // registers meanwhile) take its LDS, 16.7 KB per workgroup instead of 21.8 KB
+    constexpr int kVec = ((kTileBytes + 32) / 16 + kTileLanes - 1) / kTileLanes;
+    static_assert((2 * kTileLanes - 1) * kXPad <= kTileBytes + 32, "the tree fits the tile image");
     __shared__ __attribute__((aligned(16))) uint8_t B[kTileBytes + 32];
+    uint8_t(*const X)[kXPad] = reinterpret_cast<uint8_t(*)[kXPad]>(B);
+#else
+    __shared__ uint8_t X[2 * kTileLanes - 1][kXPad];
+    __shared__ __attribute__((aligned(16))) uint8_t B[kTileBytes + 32];
+#endif
     __shared__ uint32_t wsum[kTileLanes / kWave];
     const GEntry r = tres[blockIdx.x];
     if (r.pos == kDead) return;  // uniform per block
     const uint64_t t0 = (uint64_t)blockIdx.x * kTileBytes;
     const int l = threadIdx.x;
-    // stage the tile (+32 bytes of the next) in LDS
-    for (int i = l; i < (kTileBytes + 32) / 16; i += kTileLanes) {
+    // stage the tile (+32 bytes of the next) in LDS (with the union: into registers now, into
+    // LDS after the down-sweep)
+    auto tile_vec = [&](int i) {
         const uint64_t a = t0 + (uint64_t)i * 16;
         uint4 v;
         if (a + 16 <= len) {
@@ -385,8 +398,19 @@ __global__ __launch_bounds__(kTileLanes) void k_dec_emit(
                 if (a + b < len) q[b >> 2] |= (uint32_t)buf[a + b] << (8 * (b & 3));
             v = make_uint4(q[0], q[1], q[2], q[3]);
         }
-        *reinterpret_cast<uint4*>(&B[i * 16]) = v;
+        return v;
+    };
+#if MPX_DEC_EMIT_UNION
+    uint4 tv[kVec];
+#pragma unroll
+    for (int k = 0; k < kVec; ++k) {
+        const int i = l + k * kTileLanes;
+        tv[k] = i < (kTileBytes + 32) / 16 ? tile_vec(i) : make_uint4(0, 0, 0, 0);
     }
+#else
+    for (int i = l; i < (kTileBytes + 32) / 16; i += kTileLanes)
+        *reinterpret_cast<uint4*>(&B[i * 16]) = tile_vec(i);
+#endif
     {
         const ulonglong2 m = xmap[(uint64_t)blockIdx.x * kTileLanes + l];
 #pragma unroll
@@ -417,6 +441,15 @@ __global__ __launch_bounds__(kTileLanes) void k_dec_emit(
         __syncthreads();
     }
     const uint32_t e = E[l];
+#if MPX_DEC_EMIT_UNION
+    __syncthreads();  // every lane has read its tree nodes: the tile's bytes take the tree's LDS
+#pragma unroll
+    for (int k = 0; k < kVec; ++k) {
+        const int i = l + k * kTileLanes;
+        if (i < (kTileBytes + 32) / 16) *reinterpret_cast<uint4*>(&B[i * 16]) = tv[k];
+    }
+    __syncthreads();
+#endif
     // walk 1: frames starting in this chunk on the true chain
     const uint32_t base = (uint32_t)l * kChunk;  // chunk start within the tile
     const uint64_t tl = len - t0;               // bytes of the buffer from the tile start
