@@ -302,14 +302,16 @@ constexpr uint32_t kTabLp = 0x07FFu;
     (void)kFT; (void)kFRecs; (void)kFIpg; (void)kFCmds; (void)kFTab; (void)kFH; \
     (void)kFPer; (void)kFRecPer; (void)kFTabPer; (void)kFWaves; (void)kWaveCmds;
 
-template <class Cfg>
+template <class Cfg, int MODE>
 struct FastLds {
     static constexpr int kFRecs = Cfg::kFRecs, kFIpg = Cfg::kFIpg, kFCmds = Cfg::kFCmds;
     static constexpr int kFTab = Cfg::kFTab, kFH = Cfg::kFH, kFWaves = Cfg::kFWaves;
     union {
         struct {                 // until the tally: the group's replies (SoA) + reply ranges
             int32_t inst[kFRecs];
-            int32_t bal[kFRecs];
+            // reply ballots: CLASSIC only (MIN's handleAcceptReply ignores them; without them
+            // the N <= 9 variant's MIN workgroup fits 6 per CU instead of 5)
+            int32_t bal[MODE == MPX_MODE_CLASSIC ? kFRecs : 1];
             uint8_t idok[kFRecs];    // (id code << 1) | ok, id code kIdBad = outside [0, N)
             uint16_t rstart[kFIpg];
             uint16_t rend[kFIpg];
@@ -359,8 +361,8 @@ __device__ __forceinline__ uint32_t fhash(int64_t k) {
 // slot of key in the group's table, claiming a free slot if the key is absent (*fresh = 1);
 // -1 when the table is full. Linear probing; the CAS returns the slot's key, so a probe that
 // meets the key (inserted earlier or concurrently by another lane) ends there too.
-template <class Cfg>
-__device__ __forceinline__ int fast_slot(FastLds<Cfg>& S, unsigned long long key, uint32_t h,
+template <class Cfg, class Lds>
+__device__ __forceinline__ int fast_slot(Lds& S, unsigned long long key, uint32_t h,
                                          int& fresh) {
     constexpr int kFH = Cfg::kFH;
     uint32_t i = h & (kFH - 1);
@@ -381,7 +383,7 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
                                                          uint32_t* wcount,
                                                          unsigned long long* tacc, uint32_t* err) {
     MPX_FAST_CONSTS
-    __shared__ FastLds<Cfg> S;
+    __shared__ FastLds<Cfg, MODE> S;
     STAMP_DECL
     const uint32_t g = blockIdx.x;
     const int t = threadIdx.x, l = lane_id();
@@ -451,7 +453,7 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
         const uint32_t p = t + k * kFT;
         const uint32_t idc = (rr[k].z >= 0 && rr[k].z < nrep) ? (uint32_t)rr[k].z : kIdBad;
         S.u.a.inst[p] = rr[k].x;
-        S.u.a.bal[p] = rr[k].y;
+        if (MODE == MPX_MODE_CLASSIC) S.u.a.bal[p] = rr[k].y;
         S.u.a.idok[p] = (uint8_t)((idc << 1) | ((rr[k].w & 0xff) == 1 ? 1u : 0u));
     }
     // command keys and opcodes: issued now, they arrive during the tally (the replies' registers
@@ -498,7 +500,7 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
             int fresh = 0;
             const int sl = (unsigned long long)tk[k] == kFreeKey
                                ? -1
-                               : fast_slot(S, (unsigned long long)tk[k], fhash<Cfg::kFHB>(tk[k]),
+                               : fast_slot<Cfg>(S, (unsigned long long)tk[k], fhash<Cfg::kFHB>(tk[k]),
                                            fresh);
             ebits |= sl < 0 ? kOverflow : 0u;
             tslot[k] = sl < 0 ? 0 : sl;
@@ -666,7 +668,7 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
 #else
         if (act && key != kFreeKey) {
             int fresh = 0;
-            kd = fast_slot(S, key, fhash<Cfg::kFHB>(ck[k]), fresh);
+            kd = fast_slot<Cfg>(S, key, fhash<Cfg::kFHB>(ck[k]), fresh);
         }
 #endif
         ebits |= (act && kd < 0) ? kOverflow : 0u;  // table full, or the key INT64_MIN
