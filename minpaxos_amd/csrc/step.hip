@@ -276,12 +276,15 @@ struct FastCfg {
     static_assert(kFCmds % kFT == 0 && kFRecs % kFT == 0, "whole items per thread");
     static_assert(kFCmds / 32 <= kWave, "the new-key bitmap is scanned by one wave");
     static_assert(kWaveCmds < 2047, "kTabLp holds 1 + a wave-relative command index");
-    static_assert(kFH % (2 * kFT) == 0 && (kFH * 2) % (kWave * 16) == 0, "init strides");
+    static_assert(kFH % kFT == 0 && (kFH * 2) % (kWave * 16) == 0, "init strides");
 };
 using FastBase = FastCfg<256, 1024, 1024, 256, 9>;   // config 5: N <= 5, keys per group <= 256
 using FastRecs = FastCfg<256, 2048, 1024, 256, 9>;   // N <= 9
 using FastKeys = FastCfg<256, 1024, 1024, 1024, 10>; // group tables of up to 1024 keys
 using FastWide = FastCfg<512, 2048, 2048, 512, 10>;  // 512 instances per group
+// 512 instances per group with tables of up to 256 keys: a 512-slot hash halves the per-wave
+// slot tables, 3 workgroups per CU instead of 2
+using FastWide256 = FastCfg<512, 2048, 2048, 256, 9>;
 constexpr uint16_t kNone16 = 0xFFFF;
 constexpr uint8_t kIdBad = 31;
 constexpr unsigned long long kFreeKey = 0x8000000000000000ull;  // INT64_MIN marks a free slot
@@ -434,9 +437,8 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
     // LDS initialisation (regions outside the reply image)
 #pragma unroll
     for (int k = 0; k < kFH / kFT; ++k) S.hkey[t + k * kFT] = kFreeKey;
-#pragma unroll
-    for (int k = 0; k < kFH / (2 * kFT); ++k)
-        reinterpret_cast<uint32_t*>(S.tabidx)[t + k * kFT] = 0xFFFFFFFFu;  // kNone16 pairs
+    for (int i = t; i < kFH / 2; i += kFT)
+        reinterpret_cast<uint32_t*>(S.tabidx)[i] = 0xFFFFFFFFu;  // kNone16 pairs
     if (t < kFCmds / 32) S.newbits[t] = 0u;
     S.u.a.rstart[t] = kNone16;
     S.coff[t] = (uint16_t)(own ? co - c_lo : ncmd);
@@ -1114,6 +1116,7 @@ int fast_variant(int32_t nrep, uint32_t ipg, uint32_t kvpg) {
     if (ipg <= 256 && recs <= 1024 && kvpg <= 256) return 1;
     if (ipg <= 256 && recs <= 2048 && kvpg <= 256) return 2;
     if (ipg <= 256 && recs <= 1024 && kvpg <= 1024) return 3;
+    if (ipg <= 512 && recs <= 2048 && kvpg <= 256) return 5;
     if (ipg <= 512 && recs <= 2048 && kvpg <= 512) return 4;
     return 0;
 }
@@ -1127,6 +1130,7 @@ void launch_step(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t
     case 2: launch_fast<MODE, FastRecs>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
     case 3: launch_fast<MODE, FastKeys>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
     case 4: launch_fast<MODE, FastWide>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
+    case 5: launch_fast<MODE, FastWide256>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
     default:
         k_fill_worklist<<<(b->n_groups + 255) / 256, 256, 0, stream>>>(worklist, wcount,
                                                                        b->n_groups);

@@ -564,6 +564,8 @@ def test_group_step_ragged(mk_engine):
     dict(N=9, ipg=256, K=256, keys=200, B=3),      # FastRecs, 8 replies per instance
     dict(N=5, ipg=256, K=1024, keys=1024, B=4),    # FastKeys (tables of up to 1024 keys)
     dict(N=5, ipg=512, K=512, keys=256, B=4),      # FastWide (512 instances per group)
+    dict(N=5, ipg=512, K=256, keys=256, B=4),      # FastWide256 (512 instances, 256-key tables)
+    dict(N=3, ipg=400, K=256, keys=240, B=5),      # FastWide256, partial space, fuller tables
     dict(N=5, ipg=384, K=512, keys=400, B=5),      # FastWide with a partial instance space
     dict(N=3, ipg=128, K=1024, keys=5000, B=9),    # FastKeys -> general (1152 commands)
 ], ids=lambda d: "N{N}_ipg{ipg}_K{K}_keys{keys}_B{B}".format(**d))
