@@ -632,8 +632,12 @@ int mpx_runtime_info(char* buf, size_t cap);
  * mpx_debug_kv_set_epoch: set the KV table's call epoch (1 <= epoch < 2^30) without touching
  * its slots, so a test can drive calls across the epoch wrap on a table whose slots carry
  * older tags. mpx_debug_kv_state: copy the table's per-slot state words (bit 0 present, bit 1
- * last command of the tagged call was a PUT, bits 2.. the tag); *n = slots (cap + 1).       */
+ * last command of the tagged call was a PUT, bits 2.. the tag); *n = slots (cap + 1).
+ * mpx_debug_kv_set_small_tag: set the tag of the last replica-batch call (0 <= tag < 2^19 - 1;
+ * the next call uses tag + 1, and the call with tag 2^19 - 1 clears the per-slot list heads and
+ * restarts the tags at 1), so a test can drive calls across the tag wrap.                                                       */
 int mpx_debug_kv_set_epoch(mpx_engine* eng, uint32_t epoch);
+int mpx_debug_kv_set_small_tag(mpx_engine* eng, uint32_t tag);
 int mpx_debug_kv_state(mpx_engine* eng, uint32_t* state, size_t cap, size_t* n);
 
 #ifdef __cplusplus

@@ -101,6 +101,7 @@ SIGNATURES = {
     "mpx_event_elapsed_ms": (C.c_int, [_p, _p, _p, C.POINTER(C.c_float)]),
     "mpx_runtime_info": (C.c_int, [C.c_char_p, _sz]),
     "mpx_debug_kv_set_epoch": (C.c_int, [_p, C.c_uint32]),
+    "mpx_debug_kv_set_small_tag": (C.c_int, [_p, C.c_uint32]),
     "mpx_debug_kv_state": (C.c_int, [_p, _p, _sz, C.POINTER(_sz)]),
 }
 

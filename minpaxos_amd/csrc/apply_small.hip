@@ -1,25 +1,32 @@
-// apply_small.hip — mpx_apply for replica-sized calls (at most 8192 commands) in TWO launches.
+// apply_small.hip — mpx_apply for replica-sized calls (at most 8192 commands).
 //
 // Reference: executeCommands (src/bareminpaxos/bareminpaxos.go:1066-1098) drains one committed
 // batch (MAX_BATCH = 5000 commands, :22) and runs (*state.Command).Execute (src/state/state.go:
 // 77-103) on each in log order; conf_prev[i] = state.Conflict (state.go:53-60) of command i with
 // the previous command on the same key in the call. The replica shim calls mpx_apply once per
-// drained batch, so the call's cost is its latency, not its bandwidth: the multi-launch
-// pipelines (about ten dependent launches, ~60 us) are replaced by
-//   1. k_small_probe, a thread per command over many CUs (the call's scattered table accesses
-//      spread over their memory pipelines): PUTs find or claim their slot in the engine's table
-//      (kvtab.hpp, 64-bit CAS), the other commands look theirs up; every command's default
-//      result goes out (PUT its value, GET the table value at call start, the rest NIL); slot /
-//      resume position and state word per command into the table's probe scratch.
-//   2. k_apply_small, one 1024-thread workgroup that keeps the call in LDS: the lookups that met
-//      a free slot probe again (a PUT of the call may have claimed it); a command whose key has
-//      no slot is final (NIL, no conflict). Each slot gets a dense group id (LDS open
-//      addressing); a command alone on its key in the call is final too but for a PUT's commit;
-//      the (id, position) pairs of shared keys are sorted by id, stably, with two 7-bit LSD
-//      passes (bit-sliced ballot ranks, per-wave digit counts, one 2048-entry scan), and over
-//      the sorted groups the previous command on the key is the left neighbour (conf), the last
-//      PUT before a command a segmented exclusive max-scan of PUT positions (GET results), and
-//      each group's last PUT is committed to the table (value, present bit, n_present).
+// drained batch, so the call's cost is its latency, not its bandwidth. Four launches, the first
+// three a thread per command over many CUs (the call's scattered table accesses spread over
+// their memory pipelines):
+//   1. k_small_probe: PUTs find or claim their slot in the engine's table (kvtab.hpp, 64-bit
+//      CAS), the other commands look theirs up; every command's default result goes out (PUT its
+//      value, GET the table value at call start, the rest NIL); a command with a slot pushes its
+//      position onto the slot's command list (one atomicExch on a per-slot head word tagged with
+//      the call, the previous head and the command's PUT bit into its link word).
+//   2. k_small_reprobe: the lookups that met a free slot probe again from there (a PUT of the
+//      call may have claimed it since) and join the list; a key with no slot is final (NIL, no
+//      conflict).
+//   3. k_small_walk: each command walks its slot's list (every command of the call on its key,
+//      in no particular order): the nearest earlier command gives conf, the nearest earlier PUT a
+//      GET's result, and the PUT with no later PUT commits the key's value (and present bit).
+//      Lists of a replica batch over a large key space hold one or two commands; a walk longer
+//      than kWalkMax marks the command LONG instead.
+//   4. k_apply_small, one 1024-thread workgroup, returns at once unless a command is LONG; then it
+//      resolves the LONG commands (all of every long list) in LDS: each slot gets a dense group id
+//      (LDS open addressing), the (id, position) pairs are sorted by id, stably (a counting rank
+//      for up to 1024 entries, else two 7-bit LSD passes with bit-sliced ballot ranks and one
+//      2048-entry scan), and over the sorted groups the previous command on the key is the left
+//      neighbour (conf), the last PUT before a command a segmented exclusive max-scan of PUT
+//      positions (GET results), and each group's last PUT is committed.
 // The call epoch is neither read nor advanced: conflicts never reach across calls (orc_apply),
 // and the tags other pipelines compare stay older than their next epoch.
 #include "common.hpp"
@@ -64,6 +71,16 @@ constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 constexpr uint32_t kShared = 0x80000000u;  // tab: a second command joined the slot
 constexpr uint8_t kOpPresent = 0x80;       // LDS op byte: the key was present at call start
 static_assert(kSmMax == MPX_APPLY_SMALL_MAX, "small apply capacity");
+// command lists (steps 1-3): lhead[slot] = tag << 13 | position of the last command pushed;
+// probe[kLinkOff + p] = the position pushed before p (kLinkEnd: none) | kLinkPut if p is a PUT
+constexpr uint32_t kLinkEnd = 0xFFFFu;
+constexpr uint32_t kLinkPut = 1u << 16;
+constexpr uint32_t kLongBit = 0x80000000u;  // probe[p] after the walk: p's list is long
+constexpr int kWalkMax = 16;                // longest list a walk resolves
+constexpr uint32_t kLinkOff = 2 * kSmMax;
+constexpr uint32_t kCtlOff = kSmallCtl;     // probe[kCtlOff]: LONG commands, [+1]: last call's tag
+static_assert(kCtlOff == 3 * kSmMax && kCtlOff + 2 <= kSmallScratchWords, "small apply scratch");
+static_assert(kSmMax <= (1 << kPosBits) && (kSmallTagMax << kPosBits) == 0, "tagged list head");
 
 struct SmallLds {
     uint32_t tab[kSmHash];          // group id -> slot + 1 (0 = free)            64 KB
@@ -106,18 +123,29 @@ __device__ __forceinline__ uint32_t block_excl_sum(SmallLds& S, uint32_t v) {
 // ---- 1. probe: one command per thread, spread over many CUs ---------------------------------
 // A PUT finds or claims its key's slot (linear probe in the key's bucket, 64-bit CAS,
 // kvtab.hpp); another command stops at its key or at the first free slot (a PUT of the same call
-// may claim the key there later: the resolve kernel probes those again from the position
-// recorded here). Every command's default result goes out now: PUT its value, GET the value at
-// call start (present ? value : NIL), the rest NIL; a slot's state word is kept for the commits.
+// may claim the key there later: k_small_reprobe probes those again from the position recorded
+// here). Every command's default result goes out now: PUT its value, GET the value at call start
+// (present ? value : NIL), the rest NIL; a slot's state word is kept for the commits.
 // probe[p] = slot | kMissBit (resume position) | kNoSlot; probe[kSmMax + p] = state word.
 constexpr uint32_t kMissBit = 0x80000000u;
 constexpr int kProbeBlock = 256;
+
+// push command p onto its slot's list of this call
+__device__ __forceinline__ uint32_t call_tag(const KvTable& t) { return t.probe[kCtlOff + 1] + 1u; }
+__device__ __forceinline__ void list_push(const KvTable& t, uint32_t tag, uint32_t slot, uint32_t p,
+                                          bool put) {
+    const uint32_t old = atomicExch(&t.lhead[slot], (tag << kPosBits) | p);
+    const uint32_t nx = (old >> kPosBits) == tag ? (old & kPosMask) : kLinkEnd;
+    t.probe[kLinkOff + p] = nx | (put ? kLinkPut : 0u);
+}
+
 __global__ __launch_bounds__(kProbeBlock) void k_small_probe(KvTable t, const uint8_t* __restrict__ op,
                                                        const int64_t* __restrict__ key,
                                                        const int64_t* __restrict__ val, uint32_t m,
                                                        int64_t* __restrict__ ret, uint32_t* err) {
     const uint32_t p = blockIdx.x * kProbeBlock + threadIdx.x;
     if (p >= m) return;
+    const uint32_t tag = call_tag(t);
     const uint8_t o = op[p];
     const int64_t k = key[p];
     const bool put = o == MPX_OP_PUT;
@@ -152,6 +180,7 @@ __global__ __launch_bounds__(kProbeBlock) void k_small_probe(KvTable t, const ui
     }
     uint32_t st = 0;
     if (!(slot & kMissBit)) {  // (kNoSlot has the bit too)
+        list_push(t, tag, slot, p, put);
         st = t.state[slot];
         if (!put) ret[p] = (o == MPX_OP_GET && (st & kPresent)) ? t.vals[slot] : 0;
     } else if (!put) {
@@ -161,7 +190,115 @@ __global__ __launch_bounds__(kProbeBlock) void k_small_probe(KvTable t, const ui
     t.probe[kSmMax + p] = st;
 }
 
-// ---- 2.-3. resolve: one 1024-thread workgroup --------------------------------------------
+// ---- 2. the lookups that met a free slot, again now that every claim of the call is in --------
+// (the slots before the recorded position hold other keys for good); a key found now was claimed
+// by this call: not present at call start, state word 0 (as recorded)
+__global__ __launch_bounds__(kProbeBlock) void k_small_reprobe(KvTable t,
+                                                         const int64_t* __restrict__ key,
+                                                         uint32_t m) {
+    const uint32_t p = blockIdx.x * kProbeBlock + threadIdx.x;
+    if (p >= m) return;
+    const uint32_t s = t.probe[p];
+    if (s == kNoSlot || !(s & kMissBit)) return;
+    const int64_t k = key[p];
+    uint32_t pos = s & ~kMissBit, slot = kNoSlot;
+    for (int step = 0; step < kSB; ++step) {
+        const unsigned long long c = __hip_atomic_load(
+            reinterpret_cast<unsigned long long*>(t.keys + pos), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+        if ((int64_t)c == k) {
+            slot = pos;
+            break;
+        }
+        if (c == (unsigned long long)kSentinel) break;  // absent, and no PUT of this call
+        pos = (pos & ~(uint32_t)(kSB - 1)) | ((pos + 1) & (kSB - 1));
+    }
+    if (slot != kNoSlot) list_push(t, call_tag(t), slot, p, false);  // (a miss is never a PUT)
+    t.probe[p] = slot;
+}
+
+// ---- 3. the list walks ----------------------------------------------------------------------
+// Command p's list holds every command of the call on its key. The nearest earlier one decides
+// conf (state.Conflict: either is a PUT), the nearest earlier PUT a GET's result, and the PUT
+// with no later PUT is the key's value after the call. A list longer than kWalkMax is left to
+// k_apply_small (its commands marked LONG, counted in probe[kCtlOff]).
+__global__ __launch_bounds__(kProbeBlock) void k_small_walk(KvTable t, const uint8_t* __restrict__ op,
+                                                      const int64_t* __restrict__ val, uint32_t m,
+                                                      int64_t* __restrict__ ret,
+                                                      uint8_t* __restrict__ conf) {
+    const uint32_t p = blockIdx.x * kProbeBlock + threadIdx.x;
+    const bool v = p < m;
+    const uint32_t slot = v ? t.probe[p] : kNoSlot;
+    const uint8_t o = v ? op[p] : (uint8_t)MPX_OP_NONE;
+    bool fresh = false, lng = false;  // a key made present / a long list
+    if (slot != kNoSlot) {
+        const uint32_t mine = t.probe[kLinkOff + p];
+        const uint32_t st = t.probe[kSmMax + p];
+        uint32_t q = t.lhead[slot] & kPosMask;  // (tagged with this call: p is on the list)
+        int32_t prev = -1, last_put = -1;
+        bool prev_put = false, later_put = false;
+        int n = 0;
+        for (; q != kLinkEnd; ++n) {
+            if (n == kWalkMax) {
+                lng = true;
+                break;
+            }
+            const uint32_t w = q == p ? mine : t.probe[kLinkOff + q];
+            const bool put_q = (w & kLinkPut) != 0;
+            if (q < p) {
+                if ((int32_t)q > prev) {
+                    prev = (int32_t)q;
+                    prev_put = put_q;
+                }
+                if (put_q && (int32_t)q > last_put) last_put = (int32_t)q;
+            } else if (q > p) {
+                later_put |= put_q;
+            }
+            q = w & kLinkEnd;
+        }
+        if (lng) {
+            t.probe[p] = slot | kLongBit;
+        } else {
+            const bool put = (mine & kLinkPut) != 0;
+            if (conf) conf[p] = (prev >= 0 && (put || prev_put)) ? 1 : 0;
+            if (put) {
+                if (!later_put) {  // the key's value after the call
+                    t.vals[slot] = val[p];
+                    if (!(st & kPresent)) {
+                        t.state[slot] = st | kPresent;
+                        fresh = true;
+                    }
+                }
+            } else if (o == MPX_OP_GET && last_put >= 0) {
+                ret[p] = val[last_put];  // the last PUT before it (other ops return NIL)
+            }
+        }
+    } else if (v && conf) {
+        conf[p] = 0;  // nothing precedes it on a PUT-less key
+    }
+    const uint64_t bf = __ballot(fresh), bl = __ballot(lng);
+    if (lane_id() == 0) {
+        if (bf) atomicAdd(t.n_present, (unsigned long long)popc(bf));
+        if (bl) atomicAdd(&t.probe[kCtlOff], (uint32_t)popc(bl));
+    }
+}
+
+// ---- 4. the LONG lists: one 1024-thread workgroup -------------------------------------------
+// The call's last kernel also closes it: the LONG count back to 0 and the next call's tag; after
+// the call with the last tag every list head is cleared and the tags restart at 1 (once per
+// 2^19 - 1 calls: one workgroup's pass over the heads). All threads call it.
+__device__ __forceinline__ void end_of_call(const KvTable& t, uint32_t tag) {
+    __syncthreads();  // every thread has read the control words
+    const bool wrap = tag + 1u >= kSmallTagMax;
+    if (wrap) {
+        for (uint64_t i = threadIdx.x; i <= t.cap; i += blockDim.x) t.lhead[i] = 0u;
+    }
+    if (threadIdx.x == 0) {
+        t.probe[kCtlOff] = 0u;
+        t.probe[kCtlOff + 1] = wrap ? 0u : tag;
+    }
+}
+
 __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* __restrict__ op,
                                                       const int64_t* __restrict__ key,
                                                       const int64_t* __restrict__ val, uint32_t m,
@@ -174,66 +311,39 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
 #endif
     const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
     const uint64_t below = lanes_below(l);
+    const uint32_t n_long = t.probe[kCtlOff], tag = call_tag(t);
+    if (n_long == 0) {  // every list was walked (the common case)
+        end_of_call(t, tag);
+        return;
+    }
     for (int i = tid; i < kSmHash; i += kSmT) S.tab[i] = 0;
     if (tid == 0) S.n_new = 0;
 
     uint8_t o8[kSmPer];
-    uint32_t slot[kSmPer];     // kNoSlot: none (the table has fewer than 2^31 - 1 slots)
+    uint32_t slot[kSmPer];     // kNoSlot: finished by k_small_walk (or no slot at all)
     uint32_t slot_st[kSmPer];  // the slot's state word after the call (present set)
     int64_t vr[kSmPer];        // values (a lone PUT commits its own)
     bool pres[kSmPer];
     const uint32_t p0 = (uint32_t)(w * (kSmPer * kWave) + l);  // position of k: p0 + 64 k
     {
         uint32_t st[kSmPer];
-        int64_t kk[kSmPer];  // (keys for the probes to redo: loaded with the rest, one round trip)
 #pragma unroll
         for (int k = 0; k < kSmPer; ++k) {  // every load in flight before the first use
             const uint32_t p = p0 + k * kWave;
             const bool v = p < m;
             o8[k] = v ? op[p] : (uint8_t)MPX_OP_NONE;
             vr[k] = v ? val[p] : 0;
-            kk[k] = v ? key[p] : 0;
-            slot[k] = v ? t.probe[p] : kNoSlot;
+            const uint32_t s = v ? t.probe[p] : kNoSlot;
+            slot[k] = s != kNoSlot && (s & kLongBit) ? s & ~kLongBit : kNoSlot;
             st[k] = v ? t.probe[kSmMax + p] : 0u;
         }
         SM_STAMP(0);
-        // the probes that met a free slot, again now that every claim of the call is in (the
-        // slots before the recorded position hold other keys for good); a key found now was
-        // claimed by this call: not present at call start, state word 0
-        bool miss[kSmPer], again = false;
-#pragma unroll
-        for (int k = 0; k < kSmPer; ++k) {
-            miss[k] = slot[k] != kNoSlot && (slot[k] & kMissBit);
-            again |= miss[k];
-        }
-        for (int step = 0; step < kSB && __ballot(again); ++step) {
-            again = false;
-#pragma unroll
-            for (int k = 0; k < kSmPer; ++k) {
-                if (!miss[k]) continue;
-                const uint32_t pos = slot[k] & ~kMissBit;
-                const unsigned long long c = __hip_atomic_load(
-                    reinterpret_cast<unsigned long long*>(t.keys + pos), __ATOMIC_RELAXED,
-                    __HIP_MEMORY_SCOPE_AGENT);
-                if ((int64_t)c == kk[k]) {
-                    slot[k] = pos;
-                    miss[k] = false;
-                } else if (c == (unsigned long long)kSentinel) {
-                    slot[k] = kNoSlot;  // absent, and no PUT of this call: no slot
-                    miss[k] = false;
-                } else {
-                    slot[k] = kMissBit | ((pos & ~(uint32_t)(kSB - 1)) | ((pos + 1) & (kSB - 1)));
-                    again = true;
-                }
-            }
-        }
         SM_STAMP(1);
 #pragma unroll
         for (int k = 0; k < kSmPer; ++k) {
             const uint32_t p = p0 + k * kWave;
             pres[k] = (st[k] & kPresent) != 0;
             if (p >= m) continue;
-            if (conf && slot[k] == kNoSlot) conf[p] = 0;  // nothing precedes it on a PUT-less key
             S.op[p] = (uint8_t)(o8[k] | (pres[k] ? kOpPresent : 0));  // op + present at call start
             pres[k] = pres[k] || slot[k] == kNoSlot;
             if (!pres[k]) st[k] |= kPresent;
@@ -242,12 +352,11 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
     }
     SM_STAMP(2);
     SM_STAMP(3);
-    // ---- 2. group ids, lone commands, the stable sort by id ----------------------------------
+    // ---- 4a. group ids, the stable sort by id ------------------------------------------------
     // Each slot gets a dense id (LDS open addressing: tab[id] = slot + 1, bit 31 set once a
-    // second command of the call joins the slot). A command alone on its key in the call - the
-    // common case of a replica batch over a large key space - is final after step 1 but for
-    // its commit (a PUT's value and present bit); only the commands of shared keys are sorted
-    // and scanned, compacted in log order.
+    // second command of the call joins the slot). A command alone on its key would be final but
+    // for its commit (a PUT's value and present bit; a LONG command never is); the commands of
+    // shared keys are sorted and scanned, compacted in log order.
     __syncthreads();  // tab cleared
     uint32_t id[kSmPer];
 #pragma unroll
@@ -375,7 +484,7 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
         __syncthreads();
     }
     SM_STAMP(5);
-    // ---- 3. per group, in log order ----------------------------------------------------------
+    // ---- 4b. per group, in log order ---------------------------------------------------------
     // thread tid takes sorted entries q = 8 tid + j (blocked, two 16-byte LDS reads); groups of
     // kNoId (no slot) come last. The default results' stores are complete before any rewrite.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -474,6 +583,7 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
     if (n_new) atomicAdd(&S.n_new, n_new);
     __syncthreads();
     if (tid == 0 && S.n_new) atomicAdd(t.n_present, (unsigned long long)S.n_new);
+    end_of_call(t, tag);
     SM_STAMP(6);
 #if MPX_SMALL_STAMP
     if (threadIdx.x == 0) {  // shader clock ticks and 100 MHz ticks of the whole kernel
@@ -501,8 +611,10 @@ hipError_t launch_apply_small(KvTable& t, const uint8_t* op, const int64_t* key,
                               hipStream_t stream) {
     if (!m) return hipSuccess;
     if (m > (uint64_t)kSmMax || t.cap >= 0x7FFFFFFEull) return hipErrorInvalidValue;
-    k_small_probe<<<(unsigned)((m + kProbeBlock - 1) / kProbeBlock), kProbeBlock, 0, stream>>>(
-        t, op, key, val, (uint32_t)m, ret, err);
+    const unsigned g = (unsigned)((m + kProbeBlock - 1) / kProbeBlock);
+    k_small_probe<<<g, kProbeBlock, 0, stream>>>(t, op, key, val, (uint32_t)m, ret, err);
+    k_small_reprobe<<<g, kProbeBlock, 0, stream>>>(t, key, (uint32_t)m);
+    k_small_walk<<<g, kProbeBlock, 0, stream>>>(t, op, val, (uint32_t)m, ret, conf);
     k_apply_small<<<1, kSmT, 0, stream>>>(t, op, key, val, (uint32_t)m, ret, conf, err);
     return hipGetLastError();
 }

@@ -156,6 +156,7 @@ void free_kv(mpx::KvTable& t) {
     if (t.n_present) (void)hipFree(t.n_present);
     if (t.epoch) (void)hipFree(t.epoch);
     if (t.probe) (void)hipFree(t.probe);
+    if (t.lhead) (void)hipFree(t.lhead);
     t = mpx::KvTable{};
 }
 
@@ -174,12 +175,16 @@ int ensure_kv(mpx_engine* e) {
         hipMalloc(&t.state, (cap + 1) * 4) != hipSuccess ||
         hipMalloc(&t.n_present, sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&t.epoch, 2 * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&t.probe, 2 * MPX_APPLY_SMALL_MAX * sizeof(uint32_t)) != hipSuccess) {
+        hipMalloc(&t.probe, mpx::kSmallScratchWords * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&t.lhead, (cap + 1) * 4) != hipSuccess) {
         (void)hipGetLastError();
         free_kv(t);
         return fail(e, MPX_E_NOMEM, "KV table allocation failed");
     }
-    const hipError_t r0 = hipMemsetAsync(t.epoch, 0, 2 * sizeof(uint32_t), e->stream);
+    hipError_t r0 = hipMemsetAsync(t.epoch, 0, 2 * sizeof(uint32_t), e->stream);
+    if (r0 == hipSuccess)
+        r0 = hipMemsetAsync(t.probe, 0, mpx::kSmallScratchWords * sizeof(uint32_t), e->stream);
+    if (r0 == hipSuccess) r0 = hipMemsetAsync(t.lhead, 0, (cap + 1) * 4, e->stream);
     const hipError_t r1 = r0 == hipSuccess ? mpx::launch_kv_clear(t, e->stream) : r0;
     if (r1 != hipSuccess) {
         (void)hipGetLastError();
@@ -1198,6 +1203,16 @@ int mpx_debug_kv_set_epoch(mpx_engine* e, uint32_t epoch) {
     CK(begin(e));
     CK(ensure_kv(e));
     HIPCHK(e, hipMemcpyAsync(e->kv.epoch, &epoch, sizeof epoch, hipMemcpyHostToDevice, e->stream));
+    return finish(e);
+}
+
+int mpx_debug_kv_set_small_tag(mpx_engine* e, uint32_t tag) {
+    if (!e) return MPX_E_INVAL;
+    if (tag >= mpx::kSmallTagMax - 1) return fail(e, MPX_E_INVAL, "tag must lie in [0, 2^19 - 1)");
+    CK(begin(e));
+    CK(ensure_kv(e));
+    HIPCHK(e, hipMemcpyAsync(e->kv.probe + mpx::kSmallCtl + 1, &tag, sizeof tag,
+                             hipMemcpyHostToDevice, e->stream));
     return finish(e);
 }
 

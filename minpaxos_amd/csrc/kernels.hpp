@@ -79,9 +79,17 @@ struct KvTable {
     unsigned long long* n_present;  // device counter
     uint32_t* epoch;     // device: [0] call epoch of mpx_apply (1 .. kKvEpochMax-1), [1] k_epoch_next's
                          // completion counter (0 between calls)
-    uint32_t* probe;     // device, 2 x MPX_APPLY_SMALL_MAX: the replica-batch apply's probe
-                         // results (slot or resume position per command, its state word)
+    uint32_t* probe;     // device, kSmallScratchWords: the replica-batch apply's per-command
+                         // slot, state word and list link, and its control words (zeroed once)
+    uint32_t* lhead;     // device, [cap + 1]: per slot, the head of the replica-batch call's
+                         // command list, tagged with the call (zeroed once and at each tag wrap)
 };
+// probe scratch: 3 x MPX_APPLY_SMALL_MAX per-command words, then the control words:
+// [kSmallCtl] LONG commands of the call, [kSmallCtl + 1] the tag of the last call (device-side,
+// so a captured graph's replays take fresh tags)
+constexpr uint32_t kSmallCtl = 3 * MPX_APPLY_SMALL_MAX;
+constexpr uint32_t kSmallScratchWords = kSmallCtl + 64;
+constexpr uint32_t kSmallTagMax = 1u << 19;  // 19 tag bits above the 13 position bits
 
 constexpr uint32_t kKvEpochMax = 1u << 30;  // = kvtab.hpp kEpochMax (state bits 2..31)
 
@@ -107,13 +115,13 @@ hipError_t launch_epoch_next(KvTable& t, uint32_t* n_miss, hipStream_t stream);
 uint64_t apply_reserve_bytes(const KvTable& t, const ApplyOpts& o, uint64_t max_m);
 // the partitioned pipeline (apply_fast.hip): tables of at most 1024 bins of 16 buckets
 bool apply_fast_ok(const KvTable& t);
-// the call runs the one-launch kernel (apply_small.hip): no scratch, inputs read once
+// the call runs the replica-batch kernels (apply_small.hip): no pipeline scratch
 bool apply_is_one_launch(const ApplyOpts& o, uint64_t m);
 uint64_t apply_fast_work_bytes(const KvTable& t, uint64_t c);
 hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
                              uint64_t m, int64_t* ret, uint8_t* conf, uint64_t C, ApplyWork& w,
                              uint32_t hot_min, uint32_t* err, hipStream_t stream);
-// one-launch apply of at most MPX_APPLY_SMALL_MAX commands (apply_small.hip), no scratch
+// replica-batch apply of at most MPX_APPLY_SMALL_MAX commands (apply_small.hip, four launches)
 hipError_t launch_apply_small(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
                               uint64_t m, int64_t* ret, uint8_t* conf, uint32_t* err,
                               hipStream_t stream);

@@ -177,6 +177,10 @@ class Engine:
         """TEST-ONLY: the KV table's call epoch, its slots untouched (mpx_debug_kv_set_epoch)"""
         self._check(self.lib.mpx_debug_kv_set_epoch(self.h, epoch), "mpx_debug_kv_set_epoch")
 
+    def debug_kv_set_small_tag(self, tag):
+        """TEST-ONLY: the tag of the last replica-batch call (mpx_debug_kv_set_small_tag)"""
+        self._check(self.lib.mpx_debug_kv_set_small_tag(self.h, tag), "mpx_debug_kv_set_small_tag")
+
     def debug_kv_state(self):
         """TEST-ONLY: the KV table's per-slot state words (uint32, cap + 1 of them)"""
         n = C.c_size_t(0)

@@ -458,6 +458,42 @@ def test_apply_epoch_wrap(mk_engine, path):
         e.debug_kv_set_epoch(1 << 30)  # outside [1, 2^30)
 
 
+def test_apply_small_lists_and_tag_wrap(mk_engine):
+    """replica-sized calls resolve each key's commands by walking the key's list of the call
+    (apply_small.hip steps 1-3) and leave lists longer than 16 to the one-workgroup sort: calls
+    whose key ranges put 1 .. ~100 commands on a key mix both in one call. The list heads are
+    tagged with the call (19 bits); at the wrap the heads are cleared: calls on key set A at tags
+    1..3, the tag moved to three calls before the wrap (mpx_debug_kv_set_small_tag), two calls on
+    a disjoint set B, then calls on A at the wrapped tags 1..3 - without the clear A's heads would
+    still carry tags 1..3 and link stale positions. Every call and the table bit-exact."""
+    e = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 16, apply_path=R.APPLY_SMALL)
+    o = Oracle(5, R.MODE_MIN)
+
+    def call(m, kr, lo, seed):
+        op, key, val = synth.commands(m, kr, 0.5, "uniform", seed=seed, other_ops=0.1)
+        key = key + lo
+        gr, gc = e.apply(op, key, val)
+        wr, wc = o.apply(op, key, val)
+        assert np.array_equal(gr, wr), (m, kr, np.nonzero(gr != wr)[0][:5])
+        assert np.array_equal(gc, wc), (m, kr, np.nonzero(gc != wc)[0][:5])
+
+    for i, kr in enumerate((20000, 2000, 600, 300, 250, 40, 1)):
+        call(5000, kr, 1, 300 + i)
+    for i in range(3):
+        call(3000, 500, 10_000_000, 310 + i)          # key set A
+    e.debug_kv_set_small_tag((1 << 19) - 3)
+    for i in range(2):
+        call(3000, 500, 20_000_000, 320 + i)          # key set B, tags 2^19-2, 2^19-1
+    for i in range(3):
+        call(3000, 500, 10_000_000, 330 + i)          # A again at the wrapped tags 1..3
+    gk, gv = e.kv_export()
+    wk, wv = o.kv_export()
+    assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
+    assert e.kv_size() == len(wk)
+    with pytest.raises(MpxError):
+        e.debug_kv_set_small_tag(1 << 19)
+
+
 @pytest.mark.parametrize("cap_lg", [22, 23, 25, 26])
 def test_apply_large_table(mk_engine, cap_lg):
     """tables past the partition's 1024 bins: kv_capacity 2^22 / 2^23 / 2^25 keys (2^23..2^26

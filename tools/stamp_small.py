@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Per-phase time of the one-launch small apply (diagnostic build, -DMPX_SMALL_STAMP=1):
+"""Per-phase time of the replica-batch apply's one-workgroup kernel for LONG lists (k_apply_small,
+diagnostic build -DMPX_SMALL_STAMP=1); it does work only when a call puts more than 16 commands
+on a key (e.g. --keys 64), else every phase reads 0:
   make -C minpaxos_amd variant_of FILE=apply_small NAME=sstamp DEFS=-DMPX_SMALL_STAMP=1
-  python tools/stamp_small.py minpaxos_amd/ab/libmpx_sstamp.so [--commands 5000]
+  python tools/stamp_small.py minpaxos_amd/ab/libmpx_sstamp.so [--commands 5000] [--keys 64]
 """
 import argparse
 import ctypes as C
@@ -10,7 +12,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-PHASES = ["load", "re-probe", "flags", "-", "ids+lone", "radix x2", "groups+commit"]
+PHASES = ["load", "-", "flags", "-", "ids", "rank / radix", "groups+commit"]
 
 
 def main():
