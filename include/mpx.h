@@ -50,6 +50,11 @@
  *     engine's stream) and are asynchronous; they never allocate or synchronise, so they can be
  *     captured into a hipGraph.
  *   - a handle is not re-entrant; use one handle per replica event loop / per GPU.
+ *   - the tally (mpx_accept_tally_dev), CLASSIC prepare (mpx_prepare_select_dev), apply
+ *     (mpx_apply_dev) and group-step kernels keep control words in the handle between calls
+ *     (tickets, maxima, the replica-batch list tags), each reset by the call's last workgroup:
+ *     all *_dev calls on one handle must be issued in ONE stream order (one stream, or streams
+ *     ordered by events) — two such calls in flight at once corrupt every later call.
  *   - where the reference would panic (nil instance, peer id outside peerCommits), the engine
  *     returns MPX_E_NIL_INSTANCE / MPX_E_BAD_ID and the outputs are unspecified.
  */

@@ -176,7 +176,9 @@ __global__ __launch_bounds__(kProbeBlock) void k_small_probe(KvTable t, const ui
                 break;
             }
         }
-        if (slot == kNoSlot) raise_err(err, kErrKvFull);  // a full bucket (never for a lookup)
+        // a PUT that finds its bucket full fails the call; a lookup that walks a full bucket
+        // without its key is absent (NIL, no table change), as on the other pipelines
+        if (slot == kNoSlot && put) raise_err(err, kErrKvFull);
     }
     uint32_t st = 0;
     if (!(slot & kMissBit)) {  // (kNoSlot has the bit too)
@@ -321,8 +323,6 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
 
     uint8_t o8[kSmPer];
     uint32_t slot[kSmPer];     // kNoSlot: finished by k_small_walk (or no slot at all)
-    uint32_t slot_st[kSmPer];  // the slot's state word after the call (present set)
-    int64_t vr[kSmPer];        // values (a lone PUT commits its own)
     bool pres[kSmPer];
     const uint32_t p0 = (uint32_t)(w * (kSmPer * kWave) + l);  // position of k: p0 + 64 k
     {
@@ -332,7 +332,6 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
             const uint32_t p = p0 + k * kWave;
             const bool v = p < m;
             o8[k] = v ? op[p] : (uint8_t)MPX_OP_NONE;
-            vr[k] = v ? val[p] : 0;
             const uint32_t s = v ? t.probe[p] : kNoSlot;
             slot[k] = s != kNoSlot && (s & kLongBit) ? s & ~kLongBit : kNoSlot;
             st[k] = v ? t.probe[kSmMax + p] : 0u;
@@ -345,18 +344,14 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
             pres[k] = (st[k] & kPresent) != 0;
             if (p >= m) continue;
             S.op[p] = (uint8_t)(o8[k] | (pres[k] ? kOpPresent : 0));  // op + present at call start
-            pres[k] = pres[k] || slot[k] == kNoSlot;
-            if (!pres[k]) st[k] |= kPresent;
-            slot_st[k] = st[k];
         }
     }
     SM_STAMP(2);
     SM_STAMP(3);
     // ---- 4a. group ids, the stable sort by id ------------------------------------------------
     // Each slot gets a dense id (LDS open addressing: tab[id] = slot + 1, bit 31 set once a
-    // second command of the call joins the slot). A command alone on its key would be final but
-    // for its commit (a PUT's value and present bit; a LONG command never is); the commands of
-    // shared keys are sorted and scanned, compacted in log order.
+    // second command of the call joins the slot); the LONG commands are sorted and scanned,
+    // compacted in log order.
     __syncthreads();  // tab cleared
     uint32_t id[kSmPer];
 #pragma unroll
@@ -379,8 +374,8 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
         id[k] = h;
     }
     __syncthreads();
-    // lone commands: conf 0 (nothing before them on the key in this call), a PUT commits;
-    // shared ones get their rank in log order (wave w holds positions [512 w, 512 w + 512),
+    // every command here is LONG, i.e. on a list of more than kWalkMax commands, so none is alone
+    // on its key: each gets its rank in log order (wave w holds positions [512 w, 512 w + 512),
     // round k of it the 64 positions 512 w + 64 k + lane)
     uint32_t m2, rank[kSmPer];
     bool shared[kSmPer];
@@ -389,20 +384,10 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
         uint32_t before = 0;
 #pragma unroll
         for (int k = 0; k < kSmPer; ++k) {
-            const uint32_t p = p0 + k * kWave;
-            shared[k] = id[k] != kNoId && (S.tab[id[k]] & kShared);
+            shared[k] = id[k] != kNoId;
             const uint64_t b = __ballot(shared[k]);
             rank[k] = before + (uint32_t)popc(b & below);
             before += (uint32_t)popc(b);
-            const bool lone = id[k] != kNoId && !shared[k];
-            if (lone && conf) conf[p] = 0;
-            if (lone && o8[k] == MPX_OP_PUT) {
-                t.vals[slot[k]] = vr[k];
-                if (!pres[k]) {
-                    t.state[slot[k]] = slot_st[k];
-                    ++n_new;
-                }
-            }
         }
         if (l == 0) S.wsum[w] = before;
         __syncthreads();

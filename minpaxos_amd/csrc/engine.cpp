@@ -1211,6 +1211,9 @@ int mpx_debug_kv_set_small_tag(mpx_engine* e, uint32_t tag) {
     if (tag >= mpx::kSmallTagMax - 1) return fail(e, MPX_E_INVAL, "tag must lie in [0, 2^19 - 1)");
     CK(begin(e));
     CK(ensure_kv(e));
+    // the heads carry the tags of earlier calls: a tag moved backwards would let a later call
+    // follow one of them, so every head is cleared with the move (as at the wrap)
+    HIPCHK(e, hipMemsetAsync(e->kv.lhead, 0, (e->kv.cap + 1) * 4, e->stream));
     HIPCHK(e, hipMemcpyAsync(e->kv.probe + mpx::kSmallCtl + 1, &tag, sizeof tag,
                              hipMemcpyHostToDevice, e->stream));
     return finish(e);

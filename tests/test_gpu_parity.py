@@ -376,7 +376,60 @@ def test_apply_paths(mk_engine, hot_min, path):
         assert e.kv_size() == len(wk)
 
 
-@pytest.mark.parametrize("path", [R.APPLY_PARTITIONED, R.APPLY_SORTED])
+def _bucket_keys(lgnb, bucket, n, start=1):
+    """n keys whose hash (kvtab.hpp hash64) puts them in `bucket` of a table of 2^lgnb buckets"""
+    M = np.uint64(0xFFFFFFFFFFFFFFFF)
+    x = np.arange(start, start + 64 * n * (1 << lgnb), dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        h = x ^ (x >> np.uint64(30))
+        h = (h * np.uint64(0xBF58476D1CE4E5B9)) & M
+        h ^= h >> np.uint64(27)
+        h = (h * np.uint64(0x94D049BB133111EB)) & M
+        h ^= h >> np.uint64(31)
+    sel = x[(h >> np.uint64(64 - lgnb)) == np.uint64(bucket)]
+    assert len(sel) >= n
+    return sel[:n].astype(np.int64)
+
+
+@pytest.mark.parametrize("path", [R.APPLY_SMALL, R.APPLY_PARTITIONED, R.APPLY_SORTED])
+def test_apply_full_bucket_lookups(mk_engine, path):
+    """a bucket filled exactly (256 PUT keys in one of the 4 buckets of a 1024-slot table):
+    GETs and other ops of keys absent from that full bucket return NIL and leave the table
+    unchanged, on every pipeline (mpx.h: only keys PUT at some point occupy the table); a PUT of
+    a new key in the full bucket is MPX_E_KV_FULL"""
+    e = mk_engine(5, R.MODE_MIN, kv_capacity=512, apply_path=path)  # 1024 slots, 4 buckets
+    o = Oracle(5, R.MODE_MIN)
+    full = _bucket_keys(2, 1, 256 + 64)
+    fill, absent = full[:256], full[256:]
+    op = np.full(256, R.OP_PUT, np.uint8)
+    gr, gc = e.apply(op, fill, fill * 7)
+    wr, wc = o.apply(op, fill, fill * 7)
+    assert np.array_equal(gr, wr) and np.array_equal(gc, wc)
+    rng = np.random.default_rng(17 + path)
+    other = _bucket_keys(2, 2, 100, start=1 << 30)
+    key = np.concatenate([absent, absent[:10], fill[:50], other])
+    op = np.concatenate([np.full(74, R.OP_GET, np.uint8), np.full(50, R.OP_GET, np.uint8),
+                         np.full(100, R.OP_PUT, np.uint8)])
+    op[rng.random(len(op)) < 0.1] = R.OP_DELETE
+    op[:len(absent) + 10] = np.where(op[:len(absent) + 10] == R.OP_PUT, R.OP_GET,
+                                     op[:len(absent) + 10])
+    perm = rng.permutation(len(key))
+    key, op = key[perm], op[perm]
+    val = np.arange(len(key), dtype=np.int64) + 1000
+    gr, gc = e.apply(op, key, val)
+    wr, wc = o.apply(op, key, val)
+    assert np.array_equal(gr, wr), np.nonzero(gr != wr)[0][:5]
+    assert np.array_equal(gc, wc)
+    gk, gv = e.kv_export()
+    wk, wv = o.kv_export()
+    assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
+    assert e.kv_size() == len(wk)
+    with pytest.raises(MpxError) as ei:
+        e.apply(np.array([R.OP_PUT], np.uint8), absent[:1], np.array([5], np.int64))
+    assert ei.value.code == R.E_KV_FULL
+
+
+@pytest.mark.parametrize("path", [R.APPLY_SMALL, R.APPLY_PARTITIONED, R.APPLY_SORTED])
 def test_apply_bucket_full(mk_engine, path):
     """more distinct PUT keys than a table of 4 buckets x 256 slots holds: MPX_E_KV_FULL (the
     oracle's Go map never fills; the engine's capacity is documented in mpx.h); a call that fits
