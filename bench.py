@@ -123,6 +123,11 @@ def parse():
                          "watermark vector stays 2 x G_total through the engine's all-reduce "
                          "(one rank: RCCL's copy); a proxy for the per-rank cost of strong / weak "
                          "scaling, not a multi-GPU measurement")
+    ap.add_argument("--graph", action="store_true",
+                    help="step: after the timed loop, capture the step sequence (group step, "
+                         "totals, the RCCL group on the second stream, the double-buffer "
+                         "event waits) into hipGraphs of up to 64 steps (mpx_graph_*) and time "
+                         "their replay; value / ms_per_step then come from the replay")
     ap.add_argument("--apply-path", default="auto",
                     choices=["auto", "small", "sorted", "partitioned"],
                     help="apply: mpx_config.apply_path (auto = by call size)")
@@ -435,9 +440,47 @@ def step_bench(a, rk):
     t1 = time.perf_counter()
     elapsed = rk.max(t1 - t0)
     kern_ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in ev_k[:a.steps]]
+    last = (a.steps - 1) & 1
+    graph_info = None
+    if a.graph:
+        # the same step sequence replayed from hipGraphs: a chunk of U steps is one capture on
+        # the compute stream (the second stream joins through ev_done and is joined back at
+        # the chunk's end); graph launches on one stream run one after another, so a chunk's
+        # first two steps need no wait on the previous chunk's collectives
+        U = min(a.steps, 64)
+        chunks = [U] * (a.steps // U) + ([a.steps % U] if a.steps % U else [])
+
+        def capture(n):
+            eng.graph_begin(comp)
+            for j in range(n):
+                step(j, False)
+            if comm != comp:
+                eng.stream_wait_event(comp, ev_comm[(n - 1) & 1])  # join the second stream
+                if n > 1:
+                    eng.stream_wait_event(comp, ev_comm[(n - 2) & 1])
+            return eng.graph_end(comp)
+        graphs = {n: capture(n) for n in set(chunks)}
+        for _ in range(max(a.warmup, 1)):
+            eng.graph_launch(graphs[U], comp)
+        eng.synchronize()
+        rk.barrier()
+        eng.synchronize()
+        t0 = time.perf_counter()
+        for n in chunks:
+            eng.graph_launch(graphs[n], comp)
+        eng.synchronize()
+        rk.barrier()
+        t1 = time.perf_counter()
+        elapsed_graph = rk.max(t1 - t0)
+        graph_info = {"steps_per_graph": U, "graph_launches": len(chunks),
+                      "ms_per_step_graph": elapsed_graph / a.steps * 1e3,
+                      "ms_per_step_no_graph": elapsed / a.steps * 1e3}
+        last = (chunks[-1] - 1) & 1
+        elapsed = elapsed_graph
+        for gx in graphs.values():
+            eng.graph_destroy(gx)
 
     # ---- outputs of the (identical) timed steps -------------------------------------------------
-    last = (a.steps - 1) & 1
     tot = ar.get(d["tot"][last])  # summed over ranks by the step's all-reduce
     n_decided, n_exec_inst, n_exec_cmds = (int(x) for x in tot)
     wm = ar.get(d["wmr"][last])
@@ -476,7 +519,7 @@ def step_bench(a, rk):
     res = {}
     if rank == 0:
         # parity: the first groups of the timed output against the oracle (test infra)
-        res["parity"] = parity_sample(b, d, ar, a, mode, N, K, G_total, g0)
+        res["parity"] = parity_sample(b, d, ar, a, mode, N, K, G_total, g0, last)
         if world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(b, a, mode, N, K)
 
@@ -535,7 +578,10 @@ def step_bench(a, rk):
             "instances_processed_per_s": G_total * ipg * a.steps / elapsed,
             "executed_instances_per_s": n_exec_inst * a.steps / elapsed,
             "executed_commands_per_s": n_exec_cmds * a.steps / elapsed,
-            "launches_in_process": 1 + a.warmup + a.steps,  # table fill + warm-up + timed
+            # table fill + warm-up + timed (+ the graph replays' warm-up and timed steps)
+            "launches_in_process": 1 + a.warmup + a.steps + (
+                max(a.warmup, 1) * graph_info["steps_per_graph"] + a.steps if graph_info else 0),
+            **({"graph": graph_info} if graph_info else {}),
             "watermark_allreduce_ok": wm_ok,
             **({"emulated_world": {
                 "ranks": emu, "groups_on_this_rank": G, "groups_total": G_total,
@@ -573,7 +619,7 @@ def _oracle_sub(b, g0, g1, ipg, N):
     return sub, (c0, c1)
 
 
-def parity_sample(b, d, ar, a, mode, N, K, G_total, g0):
+def parity_sample(b, d, ar, a, mode, N, K, G_total, g0, last):
     """every output of the first --parity-groups groups of the last timed step against the
     oracle: instance states, decided counts, watermarks (after the all-reduce), peerCommits,
     Execute results, conflicts and the group tables (count, keys, values)"""
@@ -586,7 +632,7 @@ def parity_sample(b, d, ar, a, mode, N, K, G_total, g0):
     # the timed steps started from the table the warm-up step produced
     w0 = o.group_step(sub)
     want = o.group_step(sub, w0["kv_cnt"], w0["kv_key"], w0["kv_val"])
-    wm = ar.get(d["wmr"][(a.steps - 1) & 1])
+    wm = ar.get(d["wmr"][last])
     kc = ar.get(d["kc1"], S).astype(np.uint32)
     kk = ar.get(d["kk1"], S * K)
     kv = ar.get(d["kv1"], S * K)

@@ -68,7 +68,7 @@
 extern "C" {
 #endif
 
-#define MPX_ABI_VERSION 4  /* 4: + mpx_group_step_totals_dev */
+#define MPX_ABI_VERSION 5  /* 4: + mpx_group_step_totals_dev; 5: + mpx_graph_* */
 
 /* ---- error codes ---------------------------------------------------------------------- */
 #define MPX_OK 0
@@ -209,14 +209,15 @@ typedef struct mpx_config {
      * gives identical results; they move time and scratch only.                            */
     uint64_t apply_chunk;   /* commands per pipeline chunk (bounds the scratch of one call:
                                34 B / command partitioned, 48 B sorted); 0 = 1<<26          */
-    uint32_t apply_path;    /* MPX_APPLY_AUTO: by call size (single-launch kernel up to
-                               MPX_APPLY_SMALL_MAX commands, the sort-based pipeline below
-                               apply_fast_min, the partitioned one from there, sort-based
-                               again for tables past 2^26 slots); or force one of
-                               MPX_APPLY_SMALL / _SORTED / _PARTITIONED (SMALL and
-                               PARTITIONED where the call / table allow, else AUTO's pick)  */
-    uint32_t apply_fast_min;  /* AUTO: calls of at least this many commands run
-                                 partitioned; 0 = 16384 (the measured crossover)            */
+    uint32_t apply_path;    /* MPX_APPLY_AUTO: by call size (the replica-batch kernels up to
+                               MPX_APPLY_SMALL_MAX commands, the partitioned pipeline past
+                               it - the sort-based one only between MPX_APPLY_SMALL_MAX and
+                               a raised apply_fast_min, or for tables past 2^30 slots); or
+                               force one of MPX_APPLY_SMALL / _SORTED / _PARTITIONED (SMALL
+                               and PARTITIONED where the call / table allow, else AUTO's
+                               pick)                                                        */
+    uint32_t apply_fast_min;  /* AUTO: calls of at least this many commands (and more than
+                                 MPX_APPLY_SMALL_MAX) run partitioned; 0 = 16384            */
     uint32_t apply_hot_min;   /* partitioned: samples (of 64K) that make a key hot and keep
                                  its commands in place; 0 = 5; MPX_APPLY_NO_HOT = none      */
     uint32_t reserved;        /* 0                                                          */
@@ -227,7 +228,7 @@ typedef struct mpx_config {
 #define MPX_APPLY_PARTITIONED 2
 #define MPX_APPLY_SMALL 3
 #define MPX_APPLY_NO_HOT 0xFFFFFFFFu
-#define MPX_APPLY_SMALL_MAX 8192
+#define MPX_APPLY_SMALL_MAX 16384
 
 typedef struct mpx_engine mpx_engine;
 
@@ -628,6 +629,21 @@ int mpx_stream_wait_event(mpx_engine* eng, void* stream, void* event);
 /* milliseconds between two recorded (and completed) timing events                          */
 int mpx_event_elapsed_ms(mpx_engine* eng, void* ev_start, void* ev_end, float* ms);
 
+/* ---- hipGraph capture of *_dev sequences (ABI 5) -----------------------------------------
+ * mpx_graph_begin puts `stream` into capture (relaxed mode): every *_dev call, copy, memset,
+ * event record and stream wait issued on it - and on other streams that join it through an
+ * event it records - until mpx_graph_end is recorded into a graph, not run. Every stream that
+ * joined must be joined back (an event recorded on it, waited on by `stream`) before the end.
+ * mpx_graph_end ends the capture and instantiates the graph (*exec_out); mpx_graph_launch
+ * replays it on a stream as one submission; mpx_graph_destroy frees it. Captured calls keep
+ * the argument values (pointers, sizes) they were issued with. Used by bench.py to replay the
+ * whole per-step sequence of the sharded engine (group step, step totals, the RCCL group on a
+ * second stream) with one host call per step group.                                         */
+int mpx_graph_begin(mpx_engine* eng, void* stream);
+int mpx_graph_end(mpx_engine* eng, void* stream, void** exec_out);
+int mpx_graph_launch(mpx_engine* eng, void* exec, void* stream);
+int mpx_graph_destroy(mpx_engine* eng, void* exec);
+
 /* the HIP and RCCL runtimes this library is bound to, as one JSON object (NUL-terminated,
  * truncated to cap): {"hip_runtime": v, "hip_driver": v, "rccl": v, "hip_path": "...",
  * "rccl_path": "..."}. Returns the full length (excluding the NUL) or a negative error.    */
@@ -638,8 +654,8 @@ int mpx_runtime_info(char* buf, size_t cap);
  * its slots, so a test can drive calls across the epoch wrap on a table whose slots carry
  * older tags. mpx_debug_kv_state: copy the table's per-slot state words (bit 0 present, bit 1
  * last command of the tagged call was a PUT, bits 2.. the tag); *n = slots (cap + 1).
- * mpx_debug_kv_set_small_tag: set the tag of the last replica-batch call (0 <= tag < 2^19 - 1;
- * the next call uses tag + 1, and the call with tag 2^19 - 1 clears the per-slot list heads and
+ * mpx_debug_kv_set_small_tag: set the tag of the last replica-batch call (0 <= tag < 2^18 - 1;
+ * the next call uses tag + 1, and the call with tag 2^18 - 1 clears the per-slot list heads and
  * restarts the tags at 1), so a test can drive calls across the tag wrap.                                                       */
 int mpx_debug_kv_set_epoch(mpx_engine* eng, uint32_t epoch);
 int mpx_debug_kv_set_small_tag(mpx_engine* eng, uint32_t tag);

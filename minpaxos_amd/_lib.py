@@ -97,6 +97,10 @@ SIGNATURES = {
     "mpx_event_create": (C.c_int, [_p, C.c_int, C.POINTER(_p)]),
     "mpx_event_destroy": (C.c_int, [_p, _p]),
     "mpx_event_record": (C.c_int, [_p, _p, _p]),
+    "mpx_graph_begin": (C.c_int, [_p, _p]),
+    "mpx_graph_end": (C.c_int, [_p, _p, C.POINTER(C.c_void_p)]),
+    "mpx_graph_launch": (C.c_int, [_p, _p, _p]),
+    "mpx_graph_destroy": (C.c_int, [_p, _p]),
     "mpx_stream_wait_event": (C.c_int, [_p, _p, _p]),
     "mpx_event_elapsed_ms": (C.c_int, [_p, _p, _p, C.POINTER(C.c_float)]),
     "mpx_runtime_info": (C.c_int, [C.c_char_p, _sz]),

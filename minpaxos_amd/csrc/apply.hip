@@ -25,8 +25,8 @@
 //   3. radix sort on the slot bits - stable, so log order within a slot; the op class rides in
 //                         the key's low bits
 //   4-5. segmented inclusive max-scan by slot of (q if PUT else -1) -> last PUT at or before q
-//                         in its slot; keys and values are transform iterators over the sorted
-//                         keys, so nothing but the scan's output is materialised
+//                         in its slot; its items are computed from the sorted keys as the scan
+//                         reads them, so nothing but the scan's output is materialised
 //   6. k_apply_finish     a 32-bit result code per command (conf bit + where its ret comes
 //                         from); a slot's first command in the chunk takes its predecessor
 //                         from the table's per-slot state word (epoch-tagged)
@@ -40,14 +40,15 @@
 // results travel back by a second radix sort instead; what stays random is one table probe per
 // command (2), one per PUT (1) and one value gather per GET (8), all reads. Chunks only bound
 // the scratch memory.
-// Steps 3, 5 and 7 use rocPRIM device primitives (stable LSD radix sort, look-back scan_by_key).
+// Steps 3, 5 and 7 use the engine's own device primitives (radix.hpp: stable LSD radix sort;
+// scan.hpp: the segmented max-scan as a scan of (slot, position) pairs).
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
-#include <rocprim/rocprim.hpp>
-
 #include "kvtab.hpp"
+#include "radix.hpp"
+#include "scan.hpp"
 
 namespace mpx {
 
@@ -311,20 +312,32 @@ __device__ __forceinline__ uint32_t sk_index(uint64_t k) { return (uint32_t)k >>
 __device__ __forceinline__ uint32_t sk_class(uint64_t k) { return (uint32_t)k & 3u; }
 
 // the segmented max-scan reads its keys (slots) and values (own position if PUT, else -1)
-// straight from the sorted keys: no materialised slot / position arrays
+// straight from the sorted keys: no materialised slot / position arrays. Its items are
+// (slot, value) pairs; combining an earlier a with a later b keeps b's slot and takes the max
+// only within one slot (associative over slot-sorted items, scan.hpp's contract)
 __device__ __forceinline__ uint32_t sk_slot(uint64_t k) { return (uint32_t)(k >> 32); }
-struct SlotOf {
-    __host__ __device__ uint32_t operator()(uint64_t k) const { return (uint32_t)(k >> 32); }
+struct SlotPos {
+    uint32_t slot;
+    int32_t pos;
 };
-struct PutPos {
-    const uint64_t* skey;
-    __host__ __device__ int32_t operator()(uint32_t q) const {
-        return ((uint32_t)skey[q] & 3u) == kClsPut ? (int32_t)q : -1;
+struct SegMax {
+    __device__ __forceinline__ SlotPos operator()(SlotPos a, SlotPos b) const {
+        return SlotPos{b.slot, a.slot == b.slot && a.pos > b.pos ? a.pos : b.pos};
     }
 };
-using SlotIter = rocprim::transform_iterator<const uint64_t*, SlotOf, uint32_t>;
-using PutPosIter =
-    rocprim::transform_iterator<rocprim::counting_iterator<uint32_t>, PutPos, int32_t>;
+struct PutPosIn {
+    const uint64_t* skey;
+    __device__ __forceinline__ SlotPos operator()(uint64_t q) const {
+        const uint64_t k = skey[q];
+        return SlotPos{sk_slot(k), ((uint32_t)k & 3u) == kClsPut ? (int32_t)q : -1};
+    }
+};
+struct LastPutOut {  // lps[q] = the last PUT at or before q in its slot (inclusive)
+    int32_t* lps;
+    __device__ __forceinline__ void operator()(uint64_t q, SlotPos ex, SlotPos x) const {
+        lps[q] = SegMax{}(ex, x).pos;
+    }
+};
 
 // per sorted position q: the command's chunk index and a 32-bit result code
 //   bit 31 conf | bits 29-30 kind | bits 0-28 payload
@@ -489,31 +502,14 @@ __global__ __launch_bounds__(256) void k_apply_commit(KvTable t, const uint64_t*
 }
 
 namespace {
-hipError_t sort_slot_keys(void* tmp, size_t& tb, uint64_t* in, uint64_t* out, size_t n,
-                          unsigned b0, unsigned b1, hipStream_t st) {
-    return rocprim::radix_sort_keys(tmp, tb, in, out, n, b0, b1, st);
-}
-
-hipError_t sort_back_pairs(void* tmp, size_t& tb, uint32_t* ki, uint32_t* ko, uint32_t* vi,
-                           uint32_t* vo, size_t n, unsigned b0, unsigned b1, hipStream_t st) {
-    return rocprim::radix_sort_pairs(tmp, tb, ki, ko, vi, vo, n, b0, b1, st);
-}
-
 struct WorkLayout {
     uint64_t skey_a, skey_b, lps, jkey, code, jkey_b, code_b, n_miss, tmp, tmp_bytes, total;
 };
 WorkLayout layout(uint64_t m) {
-    size_t sort_tmp = 0, scan_tmp = 0, back_tmp = 0;
-    (void)sort_slot_keys(nullptr, sort_tmp, nullptr, nullptr, (size_t)m, 32u, 64u, 0);
-    (void)rocprim::inclusive_scan_by_key(nullptr, scan_tmp, SlotIter(nullptr, SlotOf()),
-                                         PutPosIter(rocprim::counting_iterator<uint32_t>(0),
-                                                    PutPos{nullptr}),
-                                         (int32_t*)nullptr, (size_t)m,
-                                         rocprim::maximum<int32_t>(),
-                                         rocprim::equal_to<uint32_t>());
-    (void)sort_back_pairs(nullptr, back_tmp, nullptr, nullptr, nullptr, nullptr, (size_t)m, 0u,
-                          32u, 0);
-    size_t t = sort_tmp > scan_tmp ? sort_tmp : scan_tmp;
+    const uint64_t sort_tmp = radix_scratch_bytes<uint64_t, RsNoValue>(m);
+    const uint64_t scan_tmp = scan_scratch_bytes<SlotPos>(m);
+    const uint64_t back_tmp = radix_scratch_bytes<uint32_t, uint32_t>(m);
+    uint64_t t = sort_tmp > scan_tmp ? sort_tmp : scan_tmp;
     t = t > back_tmp ? t : back_tmp;
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
     WorkLayout w;
@@ -633,25 +629,18 @@ hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const
         const unsigned g = grid_for(n);
         if (!one)
             k_kv_lookup<<<g, 256, 0, stream>>>(t, op + c0, key + c0, n, skey_a);
-        size_t tmp_bytes = L.tmp_bytes;
-        hipError_t r = sort_slot_keys(tmp, tmp_bytes, skey_a, skey_b, (size_t)n, 32u,
-                                      32u + slot_bits, stream);
+        hipError_t r = radix_sort<uint64_t, RsNoValue>(skey_a, skey_b, nullptr, nullptr, n, 32u,
+                                                       32u + slot_bits, tmp, L.tmp_bytes, stream);
         if (r != hipSuccess) return r;
-        tmp_bytes = L.tmp_bytes;
-        r = rocprim::inclusive_scan_by_key(tmp, tmp_bytes, SlotIter(skey_b, SlotOf()),
-                                           PutPosIter(rocprim::counting_iterator<uint32_t>(0),
-                                                      PutPos{skey_b}),
-                                           lps, (size_t)n,
-                                           rocprim::maximum<int32_t>(),
-                                           rocprim::equal_to<uint32_t>(), stream);
+        r = device_scan(PutPosIn{skey_b}, LastPutOut{lps}, n, SegMax{},
+                        SlotPos{0xFFFFFFFFu, -1}, (SlotPos*)tmp, stream);
         if (r != hipSuccess) return r;
         k_apply_finish<<<g, 256, 0, stream>>>(t, skey_b, lps, n, jkey, code);
-        tmp_bytes = L.tmp_bytes;
         const unsigned jb = bits_for(n);
         const uint32_t *jk = jkey, *cd = code;  // one emit group: LDS placement alone suffices
         if (jb > (unsigned)kEmitBits) {
-            r = sort_back_pairs(tmp, tmp_bytes, jkey, jkey_b, code, code_b, (size_t)n,
-                                (unsigned)kEmitBits, jb, stream);
+            r = radix_sort<uint32_t, uint32_t>(jkey, jkey_b, code, code_b, n, (unsigned)kEmitBits,
+                                               jb, tmp, L.tmp_bytes, stream);
             if (r != hipSuccess) return r;
             jk = jkey_b;
             cd = code_b;

@@ -68,7 +68,10 @@ constexpr int kLgHMax = 7;
 constexpr int kHotTab = 512;       // LDS hash of the hot keys (load <= 1/8: probes stay short)
 constexpr int kLgMaxBins = 10;
 constexpr int kMaxBins = 1 << kLgMaxBins;  // partition bins (super-bins past it)
-constexpr int kLgMaxSub = 4;   // bins per super-bin, at most (tables to 2^10 x 2^4 x 4096 slots)
+// bins per super-bin, at most: tables to 2^10 x 2^8 x 4096 = 2^30 slots (the resolve workgroup
+// streams its super-bin's records once per bin, so the cost grows with the table past 2^26 slots;
+// the sort-based pipeline's result codes stop at 2^29 slots)
+constexpr int kLgMaxSub = 8;
 // buckets per bin = waves of the resolve workgroup (MPX_RS_LGBPB: 3 = 8-wave workgroups of half
 // the LDS, two per CU; 4 = 16 waves, one per CU)
 #ifndef MPX_RS_LGBPB

@@ -1,12 +1,12 @@
-// apply_small.hip — mpx_apply for replica-sized calls (at most 8192 commands).
+// apply_small.hip — mpx_apply for replica-sized calls (at most 16384 commands: up to three
+// drained MAX_BATCH batches).
 //
 // Reference: executeCommands (src/bareminpaxos/bareminpaxos.go:1066-1098) drains one committed
 // batch (MAX_BATCH = 5000 commands, :22) and runs (*state.Command).Execute (src/state/state.go:
 // 77-103) on each in log order; conf_prev[i] = state.Conflict (state.go:53-60) of command i with
 // the previous command on the same key in the call. The replica shim calls mpx_apply once per
-// drained batch, so the call's cost is its latency, not its bandwidth. Four launches, the first
-// three a thread per command over many CUs (the call's scattered table accesses spread over
-// their memory pipelines):
+// drained batch, so the call's cost is its latency, not its bandwidth. Three launches, a thread
+// per command (the call's scattered table accesses spread over many CUs' memory pipelines):
 //   1. k_small_probe: PUTs find or claim their slot in the engine's table (kvtab.hpp, 64-bit
 //      CAS), the other commands look theirs up; every command's default result goes out (PUT its
 //      value, GET the table value at call start, the rest NIL); a command with a slot pushes its
@@ -20,7 +20,7 @@
 //      GET's result, and the PUT with no later PUT commits the key's value (and present bit).
 //      Lists of a replica batch over a large key space hold one or two commands; a walk longer
 //      than kWalkMax marks the command LONG instead.
-//   4. k_apply_small, one 1024-thread workgroup, returns at once unless a command is LONG; then it
+//   4. the walk kernel's last workgroup returns at once unless a command is LONG; then it
 //      resolves the LONG commands (all of every long list) in LDS: each slot gets a dense group id
 //      (LDS open addressing), the (id, position) pairs are sorted by id, stably (a counting rank
 //      for up to 1024 entries, else two 7-bit LSD passes with bit-sliced ballot ranks and one
@@ -59,19 +59,21 @@ __device__ unsigned long long mpx_small_stamp[16];
 namespace {
 constexpr int kSmT = 1024;                 // threads of the workgroup
 constexpr int kSmWaves = kSmT / kWave;     // 16
-constexpr int kSmPer = 8;                  // commands per thread
-constexpr int kSmMax = kSmT * kSmPer;      // 8192 = MPX_APPLY_SMALL_MAX
-constexpr int kSmHash = 16384;             // LDS id table
+constexpr int kSmPer = 16;                 // commands per thread
+constexpr int kSmMax = kSmT * kSmPer;      // 16384 = MPX_APPLY_SMALL_MAX
+// LDS id table of the LONG slots: a LONG list holds more than kWalkMax commands, so a call has
+// at most kSmMax / (kWalkMax + 1) = 963 LONG slots (load <= 0.47)
+constexpr int kSmHash = 2048;
 constexpr uint32_t kNoId = kSmHash - 1;    // reserved: commands without a slot sort last
-constexpr int kPosBits = 13;
+constexpr int kPosBits = 14;
 constexpr uint32_t kPosMask = (1u << kPosBits) - 1;
-constexpr int kDigit = 7;                  // radix digit bits (2 passes cover the 14-bit id)
+constexpr int kDigit = 6;                  // radix digit bits (2 passes cover the 11-bit id)
 constexpr int kDigits = 1 << kDigit;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 constexpr uint32_t kShared = 0x80000000u;  // tab: a second command joined the slot
 constexpr uint8_t kOpPresent = 0x80;       // LDS op byte: the key was present at call start
 static_assert(kSmMax == MPX_APPLY_SMALL_MAX, "small apply capacity");
-// command lists (steps 1-3): lhead[slot] = tag << 13 | position of the last command pushed;
+// command lists (steps 1-3): lhead[slot] = tag << 14 | position of the last command pushed;
 // probe[kLinkOff + p] = the position pushed before p (kLinkEnd: none) | kLinkPut if p is a PUT
 constexpr uint32_t kLinkEnd = 0xFFFFu;
 constexpr uint32_t kLinkPut = 1u << 16;
@@ -79,14 +81,14 @@ constexpr uint32_t kLongBit = 0x80000000u;  // probe[p] after the walk: p's list
 constexpr int kWalkMax = 16;                // longest list a walk resolves
 constexpr uint32_t kLinkOff = 2 * kSmMax;
 constexpr uint32_t kCtlOff = kSmallCtl;     // probe[kCtlOff]: LONG commands, [+1]: last call's tag
-static_assert(kCtlOff == 3 * kSmMax && kCtlOff + 2 <= kSmallScratchWords, "small apply scratch");
+static_assert(kCtlOff == 3 * kSmMax && kCtlOff + 3 <= kSmallScratchWords, "small apply scratch");
 static_assert(kSmMax <= (1 << kPosBits) && (kSmallTagMax << kPosBits) == 0, "tagged list head");
 
 struct SmallLds {
-    uint32_t tab[kSmHash];          // group id -> slot + 1 (0 = free)            64 KB
-    uint32_t buf[2][kSmMax];        // (id << 13 | position), radix ping-pong      64 KB
-    uint32_t cnt[kSmWaves][kDigits];  // per wave and digit: counts, then offsets  8 KB
-    uint8_t op[kSmMax];             // op by position                              8 KB
+    uint32_t tab[kSmHash];          // group id -> slot + 1 (0 = free)             8 KB
+    uint32_t buf[2][kSmMax];        // (id << 14 | position), radix ping-pong     128 KB
+    uint32_t cnt[kSmWaves][kDigits];  // per wave and digit: counts, then offsets  4 KB
+    uint8_t op[kSmMax];             // op by position                              16 KB
     uint32_t wsum[kSmWaves];        // block scan: wave totals
     int32_t wv[kSmWaves];           // segmented scan: wave values
     uint32_t wf[kSmWaves];          //                 and head flags
@@ -178,7 +180,9 @@ __global__ __launch_bounds__(kProbeBlock) void k_small_probe(KvTable t, const ui
         }
         // a PUT that finds its bucket full fails the call; a lookup that walks a full bucket
         // without its key is absent (NIL, no table change), as on the other pipelines
-        if (slot == kNoSlot && put) raise_err(err, kErrKvFull);
+        // (a plain read-modify-write: err may live in host memory, where device atomics are not
+        // available; the threads of this kernel only ever add the same bit)
+        if (slot == kNoSlot && put && err) *(volatile uint32_t*)err |= kErrKvFull;
     }
     uint32_t st = 0;
     if (!(slot & kMissBit)) {  // (kNoSlot has the bit too)
@@ -222,17 +226,18 @@ __global__ __launch_bounds__(kProbeBlock) void k_small_reprobe(KvTable t,
 // ---- 3. the list walks ----------------------------------------------------------------------
 // Command p's list holds every command of the call on its key. The nearest earlier one decides
 // conf (state.Conflict: either is a PUT), the nearest earlier PUT a GET's result, and the PUT
-// with no later PUT is the key's value after the call. A list longer than kWalkMax is left to
-// k_apply_small (its commands marked LONG, counted in probe[kCtlOff]).
-__global__ __launch_bounds__(kProbeBlock) void k_small_walk(KvTable t, const uint8_t* __restrict__ op,
-                                                      const int64_t* __restrict__ val, uint32_t m,
-                                                      int64_t* __restrict__ ret,
-                                                      uint8_t* __restrict__ conf) {
-    const uint32_t p = blockIdx.x * kProbeBlock + threadIdx.x;
+// with no later PUT is the key's value after the call. A list longer than kWalkMax is left to the
+// LONG phase (its commands marked LONG, counted in probe[kCtlOff]). Returns the commands it made
+// present / marked LONG through fresh / lng.
+__device__ __forceinline__ void walk_one(const KvTable& t, const uint8_t* __restrict__ op,
+                                         const int64_t* __restrict__ val, uint32_t m, uint32_t p,
+                                         int64_t* __restrict__ ret, uint8_t* __restrict__ conf,
+                                         bool& fresh, bool& lng) {
     const bool v = p < m;
     const uint32_t slot = v ? t.probe[p] : kNoSlot;
     const uint8_t o = v ? op[p] : (uint8_t)MPX_OP_NONE;
-    bool fresh = false, lng = false;  // a key made present / a long list
+    fresh = false;
+    lng = false;
     if (slot != kNoSlot) {
         const uint32_t mine = t.probe[kLinkOff + p];
         const uint32_t st = t.probe[kSmMax + p];
@@ -259,7 +264,10 @@ __global__ __launch_bounds__(kProbeBlock) void k_small_walk(KvTable t, const uin
             q = w & kLinkEnd;
         }
         if (lng) {
-            t.probe[p] = slot | kLongBit;
+            // read by the grid's last workgroup (the LONG phase), maybe on another XCD: stored
+            // at the device's coherence point
+            __hip_atomic_store(&t.probe[p], slot | kLongBit, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         } else {
             const bool put = (mine & kLinkPut) != 0;
             if (conf) conf[p] = (prev >= 0 && (put || prev_put)) ? 1 : 0;
@@ -278,17 +286,12 @@ __global__ __launch_bounds__(kProbeBlock) void k_small_walk(KvTable t, const uin
     } else if (v && conf) {
         conf[p] = 0;  // nothing precedes it on a PUT-less key
     }
-    const uint64_t bf = __ballot(fresh), bl = __ballot(lng);
-    if (lane_id() == 0) {
-        if (bf) atomicAdd(t.n_present, (unsigned long long)popc(bf));
-        if (bl) atomicAdd(&t.probe[kCtlOff], (uint32_t)popc(bl));
-    }
 }
 
-// ---- 4. the LONG lists: one 1024-thread workgroup -------------------------------------------
-// The call's last kernel also closes it: the LONG count back to 0 and the next call's tag; after
-// the call with the last tag every list head is cleared and the tags restart at 1 (once per
-// 2^19 - 1 calls: one workgroup's pass over the heads). All threads call it.
+// ---- 4. the LONG lists: the walk kernel's last workgroup ----------------------------------------
+// The call's last workgroup also closes it: the LONG count and the ticket back to 0 and the next
+// call's tag; after the call with the last tag every list head is cleared and the tags restart at
+// 1 (once per 2^18 - 1 calls: one workgroup's pass over the heads). All threads call it.
 __device__ __forceinline__ void end_of_call(const KvTable& t, uint32_t tag) {
     __syncthreads();  // every thread has read the control words
     const bool wrap = tag + 1u >= kSmallTagMax;
@@ -296,24 +299,39 @@ __device__ __forceinline__ void end_of_call(const KvTable& t, uint32_t tag) {
         for (uint64_t i = threadIdx.x; i <= t.cap; i += blockDim.x) t.lhead[i] = 0u;
     }
     if (threadIdx.x == 0) {
-        t.probe[kCtlOff] = 0u;
+        (void)atomic_take(&t.probe[kCtlOff]);
         t.probe[kCtlOff + 1] = wrap ? 0u : tag;
     }
 }
 
-__global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* __restrict__ op,
-                                                      const int64_t* __restrict__ key,
-                                                      const int64_t* __restrict__ val, uint32_t m,
-                                                      int64_t* __restrict__ ret,
-                                                      uint8_t* __restrict__ conf, uint32_t* err) {
+// The walks (a thread per command, kSmT per workgroup: a replica batch takes a few CUs; the
+// workgroups carry the LONG phase's LDS, so one runs per CU), then the LONG phase in the grid's
+// last workgroup: its LONG marks and counts reach the device's coherence point (agent-scope atomic
+// stores, awaited atomic adds) before its ticket, and the last workgroup reads them the same way.
+__global__ __launch_bounds__(kSmT) void k_small_walk(KvTable t, const uint8_t* __restrict__ op,
+                                                     const int64_t* __restrict__ val, uint32_t m,
+                                                     int64_t* __restrict__ ret,
+                                                     uint8_t* __restrict__ conf) {
     __shared__ SmallLds S;
+    {
+        bool fresh, lng;
+        walk_one(t, op, val, m, blockIdx.x * kSmT + threadIdx.x, ret, conf, fresh, lng);
+        const uint64_t bf = __ballot(fresh), bl = __ballot(lng);
+        if (lane_id() == 0) {
+            if (bf) atomicAdd(t.n_present, (unsigned long long)popc(bf));
+            if (bl) atomic_add_done(&t.probe[kCtlOff], (uint32_t)popc(bl));
+        }
+    }
+    if (!last_workgroup(&t.probe[kCtlOff + 2])) return;
 #if MPX_SMALL_STAMP
     unsigned long long _sm_prev = __builtin_amdgcn_s_memrealtime();
     const unsigned long long _sm_rt0 = _sm_prev, _sm_clk0 = __builtin_amdgcn_s_memtime();
 #endif
     const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
     const uint64_t below = lanes_below(l);
-    const uint32_t n_long = t.probe[kCtlOff], tag = call_tag(t);
+    const uint32_t n_long = __hip_atomic_load(&t.probe[kCtlOff], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t tag = call_tag(t);
     if (n_long == 0) {  // every list was walked (the common case)
         end_of_call(t, tag);
         return;
@@ -332,7 +350,9 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
             const uint32_t p = p0 + k * kWave;
             const bool v = p < m;
             o8[k] = v ? op[p] : (uint8_t)MPX_OP_NONE;
-            const uint32_t s = v ? t.probe[p] : kNoSlot;
+            const uint32_t s = v ? __hip_atomic_load(&t.probe[p], __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)
+                                 : kNoSlot;
             slot[k] = s != kNoSlot && (s & kLongBit) ? s & ~kLongBit : kNoSlot;
             st[k] = v ? t.probe[kSmMax + p] : 0u;
         }
@@ -410,7 +430,7 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
 #endif
     if (MPX_SMALL_RANK && m2 <= (uint32_t)kSmT) {
         // few shared commands (a batch over a large key space): each entry's rank is the count
-        // of smaller entries (id << 13 | position is unique, so the order is stable), one pass
+        // of smaller entries (id << 14 | position is unique, so the order is stable), one pass
         // of broadcast LDS reads instead of the two radix passes' dozen barriers
         __syncthreads();  // every shared command's entry is in buf[0]
         const uint32_t e = (uint32_t)tid < m2 ? S.buf[0][tid] : 0u;
@@ -454,13 +474,13 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
                 S.cnt[w][d] = run + (uint32_t)popc(peers);
         }
         __syncthreads();
-        // offsets: exclusive scan of the counts in (digit, wave) order, two entries per thread
+        // offsets: exclusive scan of the counts in (digit, wave) order, one entry per thread
+        static_assert(kDigits * kSmWaves == kSmT, "one (digit, wave) count per thread");
         {
-            const uint32_t d = (uint32_t)tid >> 3, w0 = ((uint32_t)tid & 7) * 2;
-            const uint32_t a = S.cnt[w0][d], b = S.cnt[w0 + 1][d];
-            const uint32_t ex = block_excl_sum(S, a + b);
+            const uint32_t d = (uint32_t)tid / kSmWaves, w0 = (uint32_t)tid % kSmWaves;
+            const uint32_t a = S.cnt[w0][d];
+            const uint32_t ex = block_excl_sum(S, a);
             S.cnt[w0][d] = ex;
-            S.cnt[w0 + 1][d] = ex + a;
         }
         __syncthreads();
 #pragma unroll
@@ -477,11 +497,13 @@ __global__ __launch_bounds__(kSmT) void k_apply_small(KvTable t, const uint8_t* 
     const uint32_t* srt = S.buf[0];
     const uint32_t q0 = (uint32_t)tid * kSmPer;
     uint32_t e[kSmPer];
-    {
-        const uint4 a = reinterpret_cast<const uint4*>(srt)[2 * tid];
-        const uint4 b = reinterpret_cast<const uint4*>(srt)[2 * tid + 1];
-        e[0] = a.x; e[1] = a.y; e[2] = a.z; e[3] = a.w;
-        e[4] = b.x; e[5] = b.y; e[6] = b.z; e[7] = b.w;
+#pragma unroll
+    for (int v = 0; v < kSmPer / 4; ++v) {
+        const uint4 a = reinterpret_cast<const uint4*>(srt)[(kSmPer / 4) * tid + v];
+        e[4 * v] = a.x;
+        e[4 * v + 1] = a.y;
+        e[4 * v + 2] = a.z;
+        e[4 * v + 3] = a.w;
     }
     const uint32_t e_prev = q0 > 0 && q0 - 1 < m2 ? srt[q0 - 1] : 0xFFFFFFFFu;
     const uint32_t e_next = q0 + kSmPer < m2 ? srt[q0 + kSmPer] : 0xFFFFFFFFu;
@@ -599,8 +621,8 @@ hipError_t launch_apply_small(KvTable& t, const uint8_t* op, const int64_t* key,
     const unsigned g = (unsigned)((m + kProbeBlock - 1) / kProbeBlock);
     k_small_probe<<<g, kProbeBlock, 0, stream>>>(t, op, key, val, (uint32_t)m, ret, err);
     k_small_reprobe<<<g, kProbeBlock, 0, stream>>>(t, key, (uint32_t)m);
-    k_small_walk<<<g, kProbeBlock, 0, stream>>>(t, op, val, (uint32_t)m, ret, conf);
-    k_apply_small<<<1, kSmT, 0, stream>>>(t, op, key, val, (uint32_t)m, ret, conf, err);
+    k_small_walk<<<(unsigned)((m + kSmT - 1) / kSmT), kSmT, 0, stream>>>(t, op, val, (uint32_t)m,
+                                                                         ret, conf);
     return hipGetLastError();
 }
 

@@ -120,6 +120,10 @@ __device__ __forceinline__ void atomic_add_done(unsigned long long* p, unsigned 
         __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::"v"(old) : "memory");
 }
+__device__ __forceinline__ void atomic_add_done(uint32_t* p, uint32_t v) {
+    const uint32_t old = __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::"v"(old) : "memory");
+}
 __device__ __forceinline__ uint32_t atomic_take(uint32_t* p) {  // read and reset to 0
     return __hip_atomic_exchange(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -460,12 +460,15 @@ int mpx_apply(mpx_engine* e, const uint8_t* op, const int64_t* key, const int64_
     if (!e) return MPX_E_INVAL;
     if (m && (!op || !key || !val || !ret)) return fail(e, MPX_E_INVAL, "null argument");
     if (m >= (1ull << 31)) return fail(e, MPX_E_UNSUPPORTED, "more than 2^31-1 commands per call");
-    CK(begin(e));
-    CK(ensure_kv(e));
     if (mpx::apply_is_one_launch(e->apply, m)) {
-        // one drained executeCommands batch: the commands go into pinned host memory the kernel
-        // reads over the link, the results come back the same way; a CPU copy on each side
-        const size_t a16 = (m + 15) & ~(size_t)15, need = a16 * 2 + m * 24;
+        // one drained executeCommands batch: the commands go into pinned host memory the kernels
+        // read over the link, the results and the call's error word come back the same way (no
+        // DMA, no memset, no copy of the error word: the host clears and reads it in place); a
+        // CPU copy on each side
+        HIPCHK(e, hipSetDevice(e->device));
+        CK(ensure_kv(e));
+        constexpr size_t kHdr = 64;  // the error word, alone in its cache line
+        const size_t a16 = (m + 15) & ~(size_t)15, need = kHdr + a16 * 2 + m * 24;
         if (e->pin_cap < need) {
             if (e->pin) (void)hipHostFree(e->pin);
             e->pin = nullptr;
@@ -476,28 +479,33 @@ int mpx_apply(mpx_engine* e, const uint8_t* op, const int64_t* key, const int64_
             e->pin = (uint8_t*)hp;
             e->pin_cap = need;
         }
-        uint8_t* h_op = e->pin;
-        int64_t* h_key = (int64_t*)(e->pin + a16);
+        volatile uint32_t* h_err = (volatile uint32_t*)e->pin;
+        uint8_t* h_op = e->pin + kHdr;
+        int64_t* h_key = (int64_t*)(h_op + a16);
         int64_t* h_val = h_key + m;
         int64_t* h_ret = h_val + m;
         uint8_t* h_conf = (uint8_t*)(h_ret + m);
+        *h_err = 0u;
         std::memcpy(h_op, op, m);
         std::memcpy(h_key, key, m * 8);
         std::memcpy(h_val, val, m * 8);
         void* dp = nullptr;
         HIPCHK(e, hipHostGetDevicePointer(&dp, e->pin, 0));
-        uint8_t* d0 = (uint8_t*)dp;
+        uint8_t* d0 = (uint8_t*)dp + kHdr;
         mpx::ApplyWork w{nullptr, 0};
         HIPCHK(e, mpx::launch_apply(e->kv, d0, (const int64_t*)(d0 + a16),
                                     (const int64_t*)(d0 + a16) + m, m,
                                     (int64_t*)(d0 + a16) + 2 * m,
                                     conf_prev ? d0 + a16 + m * 24 : nullptr, e->apply, w,
-                                    e->d_err, e->stream));
-        const int rc = finish(e);
+                                    (uint32_t*)dp, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        const uint32_t werr = *h_err;
         std::memcpy(ret, h_ret, m * 8);
         if (conf_prev) std::memcpy(conf_prev, h_conf, m);
-        return rc;
+        return check_errword(e, werr);
     }
+    CK(begin(e));
+    CK(ensure_kv(e));
     GROW(e, e->b[7], m);
     GROW(e, e->b[8], m * 8);
     GROW(e, e->b[9], m * 8);
@@ -1208,7 +1216,7 @@ int mpx_debug_kv_set_epoch(mpx_engine* e, uint32_t epoch) {
 
 int mpx_debug_kv_set_small_tag(mpx_engine* e, uint32_t tag) {
     if (!e) return MPX_E_INVAL;
-    if (tag >= mpx::kSmallTagMax - 1) return fail(e, MPX_E_INVAL, "tag must lie in [0, 2^19 - 1)");
+    if (tag >= mpx::kSmallTagMax - 1) return fail(e, MPX_E_INVAL, "tag must lie in [0, 2^18 - 1)");
     CK(begin(e));
     CK(ensure_kv(e));
     // the heads carry the tags of earlier calls: a tag moved backwards would let a later call
@@ -1333,6 +1341,42 @@ int mpx_event_elapsed_ms(mpx_engine* e, void* ev0, void* ev1, float* ms) {
     if (!e) return MPX_E_INVAL;
     if (!ev0 || !ev1 || !ms) return fail(e, MPX_E_INVAL, "null or invalid argument");
     HIPCHK(e, hipEventElapsedTime(ms, (hipEvent_t)ev0, (hipEvent_t)ev1));
+    return MPX_OK;
+}
+
+// ---- hipGraph capture ----------------------------------------------------------------------------
+int mpx_graph_begin(mpx_engine* e, void* s) {
+    if (!e) return MPX_E_INVAL;
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamBeginCapture(pick(e, s), hipStreamCaptureModeRelaxed));
+    return MPX_OK;
+}
+
+int mpx_graph_end(mpx_engine* e, void* s, void** exec_out) {
+    if (!e) return MPX_E_INVAL;
+    if (!exec_out) return fail(e, MPX_E_INVAL, "null exec_out");
+    *exec_out = nullptr;
+    hipGraph_t g = nullptr;
+    HIPCHK(e, hipStreamEndCapture(pick(e, s), &g));
+    hipGraphExec_t x = nullptr;
+    const hipError_t r = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (r != hipSuccess) return hip_fail(e, "hipGraphInstantiate", r);
+    *exec_out = (void*)x;
+    return MPX_OK;
+}
+
+int mpx_graph_launch(mpx_engine* e, void* exec, void* s) {
+    if (!e) return MPX_E_INVAL;
+    if (!exec) return fail(e, MPX_E_INVAL, "null graph");
+    HIPCHK(e, hipGraphLaunch((hipGraphExec_t)exec, pick(e, s)));
+    return MPX_OK;
+}
+
+int mpx_graph_destroy(mpx_engine* e, void* exec) {
+    if (!e) return MPX_E_INVAL;
+    if (!exec) return fail(e, MPX_E_INVAL, "null graph");
+    HIPCHK(e, hipGraphExecDestroy((hipGraphExec_t)exec));
     return MPX_OK;
 }
 

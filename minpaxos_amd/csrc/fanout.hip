@@ -22,16 +22,16 @@
 //                  copies every client's run of the image to its place in that client's output
 //                  run with dword stores (head and tail bytes of a run with byte stores).
 // HBM: the replies are read twice (count, scatter) and the output written once, coalesced in
-// runs; nothing is gathered at random. More connections: a rocPRIM radix sort of the client id
-// with the reply index as payload, then each block gathers 256 replies, assembles their
+// runs; nothing is gathered at random. More connections: a radix sort (radix.hpp) of the client
+// id with the reply index as payload, then each block gathers 256 replies, assembles their
 // encodings in LDS and stores the 6400-byte run with 16-byte vector stores.
 // client_off[c] = byte offset of client c's run; client_off[n_clients] = 25 n.
 #include <cstring>
 
-#include <rocprim/rocprim.hpp>
-
 #include "common.hpp"
 #include "kernels.hpp"
+#include "radix.hpp"
+#include "scan.hpp"
 
 namespace mpx {
 
@@ -46,10 +46,27 @@ unsigned bits_for_clients(uint32_t c) {  // bits to represent every client id < 
 }
 }  // namespace
 
-struct ClientOf {
-    __host__ __device__ uint32_t operator()(const mpx_reply_rec& r) const { return r.client; }
+// the radix sort's input: client id and reply index of every reply
+__global__ __launch_bounds__(256) void k_fan_keys(const mpx_reply_rec* __restrict__ recs, uint64_t n,
+                                                 uint32_t* __restrict__ keys,
+                                                 uint32_t* __restrict__ idx) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = recs[i].client;
+    idx[i] = (uint32_t)i;
+}
+
+// exclusive scan of the client-major histogram: the first output record of every (client, slice)
+struct HistIn {
+    const uint32_t* h;
+    __device__ __forceinline__ uint32_t operator()(uint64_t i) const { return h[i]; }
 };
-using ClientKeys = rocprim::transform_iterator<const mpx_reply_rec*, ClientOf, uint32_t>;
+struct FirstOut {
+    uint32_t* first;
+    __device__ __forceinline__ void operator()(uint64_t i, uint32_t ex, uint32_t) const {
+        first[i] = ex;
+    }
+};
 
 template <bool kAligned>
 __global__ __launch_bounds__(kFanBlock) void k_fan_encode(
@@ -386,18 +403,11 @@ __global__ __launch_bounds__(kFanThreads) void k_fan_scatter(
 }
 
 uint64_t fanout_work_bytes(uint64_t n) {
-    size_t tmp = 0;
     const uint64_t m = n ? n : 1;
-    (void)rocprim::radix_sort_pairs(nullptr, tmp, ClientKeys(nullptr, ClientOf()),
-                                    (uint32_t*)nullptr, rocprim::counting_iterator<uint32_t>(0),
-                                    (uint32_t*)nullptr, (size_t)m, 0u, 32u);
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
-    const uint64_t radix = 2 * al(m * 4) + al(tmp);
+    const uint64_t radix = 4 * al(m * 4) + al(radix_scratch_bytes<uint32_t, uint32_t>(m));
     const uint64_t h = (uint64_t)kFanMaxClients * fan_plan(m).slices;
-    size_t stmp = 0;
-    (void)rocprim::exclusive_scan(nullptr, stmp, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
-                                  (size_t)h, rocprim::plus<uint32_t>());
-    const uint64_t counting = 2 * al(h * 4) + al(stmp);
+    const uint64_t counting = 2 * al(h * 4) + al(scan_scratch_bytes<uint32_t>(h));
     return radix > counting ? radix : counting;
 }
 
@@ -418,12 +428,11 @@ hipError_t launch_encode_replies(const mpx_reply_rec* recs, uint64_t n, uint32_t
         const uint64_t h = (uint64_t)n_clients * p.slices;
         uint32_t* hist = (uint32_t*)w;
         uint32_t* first = (uint32_t*)(w + al(h * 4));
-        void* tmp = w + 2 * al(h * 4);
-        size_t tmp_bytes = work_bytes - 2 * al(h * 4);
+        uint32_t* tmp = (uint32_t*)(w + 2 * al(h * 4));
         k_fan_count<<<p.slices, kFanThreads, 0, stream>>>(recs, n, p.per_slice, n_clients,
                                                           p.slices, hist, err);
-        hipError_t r = rocprim::exclusive_scan(tmp, tmp_bytes, hist, first, 0u, (size_t)h,
-                                               rocprim::plus<uint32_t>(), stream);
+        const hipError_t r = device_scan(HistIn{hist}, FirstOut{first}, h, ScanSum32{}, 0u, tmp,
+                                         stream);
         if (r != hipSuccess) return r;
         k_fan_scatter<<<p.slices, kFanThreads, 0, stream>>>(recs, n, p.per_slice, n_clients,
                                                             p.slices, first, ok, leader, out,
@@ -432,12 +441,13 @@ hipError_t launch_encode_replies(const mpx_reply_rec* recs, uint64_t n, uint32_t
     }
     uint32_t* skeys = (uint32_t*)w;
     uint32_t* perm = (uint32_t*)(w + al(n * 4));
-    void* tmp = w + 2 * al(n * 4);
-    size_t tmp_bytes = work_bytes - 2 * al(n * 4);
-    // keys read straight from the records (no separate key pass)
-    hipError_t r = rocprim::radix_sort_pairs(tmp, tmp_bytes, ClientKeys(recs, ClientOf()), skeys,
-                                             rocprim::counting_iterator<uint32_t>(0), perm,
-                                             (size_t)n, 0u, bits_for_clients(n_clients), stream);
+    uint32_t* keys_in = (uint32_t*)(w + 2 * al(n * 4));
+    uint32_t* idx_in = (uint32_t*)(w + 3 * al(n * 4));
+    void* tmp = w + 4 * al(n * 4);
+    const uint64_t tmp_bytes = work_bytes - 4 * al(n * 4);
+    k_fan_keys<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(recs, n, keys_in, idx_in);
+    const hipError_t r = radix_sort(keys_in, skeys, idx_in, perm, n, 0u,
+                                    bits_for_clients(n_clients), tmp, tmp_bytes, stream);
     if (r != hipSuccess) return r;
     const unsigned blocks = (unsigned)((n + kFanBlock - 1) / kFanBlock);
     if (((uintptr_t)out & 15) == 0)

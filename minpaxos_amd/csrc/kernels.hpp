@@ -86,10 +86,10 @@ struct KvTable {
 };
 // probe scratch: 3 x MPX_APPLY_SMALL_MAX per-command words, then the control words:
 // [kSmallCtl] LONG commands of the call, [kSmallCtl + 1] the tag of the last call (device-side,
-// so a captured graph's replays take fresh tags)
+// so a captured graph's replays take fresh tags), [kSmallCtl + 2] the walk kernel's ticket
 constexpr uint32_t kSmallCtl = 3 * MPX_APPLY_SMALL_MAX;
 constexpr uint32_t kSmallScratchWords = kSmallCtl + 64;
-constexpr uint32_t kSmallTagMax = 1u << 19;  // 19 tag bits above the 13 position bits
+constexpr uint32_t kSmallTagMax = 1u << 18;  // 18 tag bits above the 14 position bits
 
 constexpr uint32_t kKvEpochMax = 1u << 30;  // = kvtab.hpp kEpochMax (state bits 2..31)
 
@@ -121,7 +121,9 @@ uint64_t apply_fast_work_bytes(const KvTable& t, uint64_t c);
 hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
                              uint64_t m, int64_t* ret, uint8_t* conf, uint64_t C, ApplyWork& w,
                              uint32_t hot_min, uint32_t* err, hipStream_t stream);
-// replica-batch apply of at most MPX_APPLY_SMALL_MAX commands (apply_small.hip, four launches)
+// replica-batch apply of at most MPX_APPLY_SMALL_MAX commands (apply_small.hip, three launches).
+// err may be a host-mapped word (the host-pointer form): the kernels raise into it with plain
+// stores (every bit they raise is kErrKvFull), never atomics
 hipError_t launch_apply_small(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
                               uint64_t m, int64_t* ret, uint8_t* conf, uint32_t* err,
                               hipStream_t stream);

@@ -10,17 +10,17 @@
 //   MPX_LOG_DURABLE  recordInstanceMetadata (bareminpaxos.go:164-174: Ballot u32, Status u32,
 //                    instNo u32) followed by recordCommands (:177-188: Command.Marshal each; a
 //                    nil slice writes nothing), one record per stable-store append.
-// Pipeline: rocPRIM inclusive scan of the record sizes (computed from cmd_off as it reads them) ->
-// k_log_block_first (the record holding each 8 KB output block's first byte) -> k_log_emit:
+// Pipeline: a scan of the record sizes (scan.hpp, computed from cmd_off as it reads them; its
+// last pass also writes, per 8 KB output block, the record holding the block's first byte) ->
+// k_log_emit:
 // per block, the overlapping records' headers and commands are written into an LDS image of the
 // block (one thread per header, one per command, so the command loads are coalesced) and the
 // image goes out as 16-byte vector stores (no partial lines except at the run's two ends).
 #include <cstring>
 
-#include <rocprim/rocprim.hpp>
-
 #include "common.hpp"
 #include "kernels.hpp"
+#include "scan.hpp"
 
 namespace mpx {
 
@@ -64,29 +64,28 @@ __host__ __device__ __forceinline__ uint32_t hdr_bytes(int format, uint64_t ncmd
 struct RecBytes {
     int format;
     const uint64_t* cmd_off;
-    __host__ __device__ uint64_t operator()(uint64_t i) const {
+    __device__ __forceinline__ uint64_t operator()(uint64_t i) const {
         const uint64_t nc = cmd_off[i + 1] - cmd_off[i];
         return hdr_bytes(format, nc) + 17 * nc;
     }
 };
-using RecBytesIt =
-    rocprim::transform_iterator<rocprim::counting_iterator<uint64_t>, RecBytes, uint64_t>;
-
-__global__ void k_log_zero(uint64_t* rec_off) { rec_off[0] = 0; }
-
-// blk_first[b] = the record holding output byte b * kLogBlockBytes (a block start falls inside
-// exactly one record), so no emit block has to binary-search the offsets in global memory
-__global__ __launch_bounds__(256) void k_log_block_first(const uint64_t* __restrict__ rec_off,
-                                                         uint64_t n, uint32_t n_blocks,
-                                                         uint64_t* __restrict__ blk_first) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t s = rec_off[i], e = rec_off[i + 1];
+// the scan's output: rec_off[i + 1] = end of record i, and blk_first[b] = the record holding
+// output byte b * kLogBlockBytes (a block start falls inside exactly one record), so no emit
+// block has to binary-search the offsets in global memory
+struct RecOffOut {
+    uint64_t* rec_off;
+    uint64_t* blk_first;
+    uint32_t n_blocks;
+    __device__ __forceinline__ void operator()(uint64_t i, uint64_t s, uint64_t bytes) const {
+        const uint64_t e = s + bytes;
+        rec_off[i + 1] = e;
         for (uint64_t b = (s + kLogBlockBytes - 1) / kLogBlockBytes;
              b * kLogBlockBytes < e && b < n_blocks; ++b)
             blk_first[b] = i;
     }
-}
+};
+
+__global__ void k_log_zero(uint64_t* rec_off) { rec_off[0] = 0; }
 
 // OR the n bytes of w (little-endian dwords, bytes past n zero) into the zeroed LDS window W at
 // byte offset s (may be negative: the part before the window is dropped, as is anything past
@@ -208,12 +207,8 @@ uint64_t blocks_for(uint64_t n, uint64_t m) {
 }  // namespace
 
 uint64_t logenc_work_bytes(uint64_t n, uint64_t m) {
-    size_t tmp = 0;
-    const RecBytesIt it(rocprim::counting_iterator<uint64_t>(0), RecBytes{0, nullptr});
-    (void)rocprim::inclusive_scan(nullptr, tmp, it, (uint64_t*)nullptr, (size_t)(n ? n : 1),
-                                  rocprim::plus<uint64_t>());
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
-    return al(tmp) + al(blocks_for(n, m) * 8);
+    return al(scan_scratch_bytes<uint64_t>(n ? n : 1)) + al(blocks_for(n, m) * 8);
 }
 
 hipError_t launch_encode_log(int format, const mpx_log_rec* recs, uint64_t n,
@@ -227,15 +222,11 @@ hipError_t launch_encode_log(int format, const mpx_log_rec* recs, uint64_t n,
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
     const uint64_t blocks = blocks_for(n, m);
     uint64_t* blk_first = (uint64_t*)work;
-    void* tmp = (char*)blk_first + al(blocks * 8);
-    size_t tmp_bytes = work_bytes - al(blocks * 8);
-    const uint64_t g = (n + 255) / 256;
-    const unsigned gg = (unsigned)(g > 8192 ? 8192 : g);
-    const RecBytesIt sizes(rocprim::counting_iterator<uint64_t>(0), RecBytes{format, cmd_off});
-    hipError_t r = rocprim::inclusive_scan(tmp, tmp_bytes, sizes, rec_off + 1, (size_t)n,
-                                           rocprim::plus<uint64_t>(), stream);
+    uint64_t* tmp = (uint64_t*)((char*)blk_first + al(blocks * 8));
+    const hipError_t r = device_scan(RecBytes{format, cmd_off},
+                                     RecOffOut{rec_off, blk_first, (uint32_t)blocks}, n,
+                                     ScanSum64{}, (uint64_t)0, tmp, stream);
     if (r != hipSuccess) return r;
-    k_log_block_first<<<gg, 256, 0, stream>>>(rec_off, n, (uint32_t)blocks, blk_first);
     // grid from the largest possible output (the exact size is only known on the device)
     k_log_emit<<<(unsigned)blocks, kLogBlock, 0, stream>>>(format, recs, cmd_off, op, key, val, n,
                                                           rec_off, blk_first, (uint32_t)blocks,

@@ -503,6 +503,21 @@ class Engine:
     def stream_wait_event(self, stream, ev):
         self._check(self.lib.mpx_stream_wait_event(self.h, stream, ev), "mpx_stream_wait_event")
 
+    def graph_begin(self, stream=None):
+        """capture every call issued on `stream` (and streams joined to it) into a graph"""
+        self._check(self.lib.mpx_graph_begin(self.h, stream), "mpx_graph_begin")
+
+    def graph_end(self, stream=None):
+        x = C.c_void_p()
+        self._check(self.lib.mpx_graph_end(self.h, stream, C.byref(x)), "mpx_graph_end")
+        return x.value
+
+    def graph_launch(self, graph, stream=None):
+        self._check(self.lib.mpx_graph_launch(self.h, graph, stream), "mpx_graph_launch")
+
+    def graph_destroy(self, graph):
+        self._check(self.lib.mpx_graph_destroy(self.h, graph), "mpx_graph_destroy")
+
     def event_elapsed_ms(self, ev0, ev1):
         ms = C.c_float(0.0)
         self._check(self.lib.mpx_event_elapsed_ms(self.h, ev0, ev1, C.byref(ms)),

@@ -100,4 +100,4 @@ assert PREPARE_EFFECT.itemsize == 8
 # mpx_config.apply_path / apply_hot_min (include/mpx.h)
 APPLY_AUTO, APPLY_SORTED, APPLY_PARTITIONED, APPLY_SMALL = 0, 1, 2, 3
 APPLY_NO_HOT = 0xFFFFFFFF
-APPLY_SMALL_MAX = 8192
+APPLY_SMALL_MAX = 16384

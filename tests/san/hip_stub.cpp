@@ -143,6 +143,15 @@ hipError_t hipEventElapsedTime(float* ms, hipEvent_t a, hipEvent_t b) {
     *ms = (float)((*reinterpret_cast<double*>(b) - *reinterpret_cast<double*>(a)) * 1e3);
     return hipSuccess;
 }
+// graph capture: the stub runs every call at once, so it has nothing to record
+hipError_t hipStreamBeginCapture(hipStream_t, hipStreamCaptureMode) { return hipErrorNotSupported; }
+hipError_t hipStreamEndCapture(hipStream_t, hipGraph_t*) { return hipErrorNotSupported; }
+hipError_t hipGraphInstantiate(hipGraphExec_t*, hipGraph_t, hipGraphNode_t*, char*, size_t) {
+    return hipErrorNotSupported;
+}
+hipError_t hipGraphDestroy(hipGraph_t) { return hipErrorNotSupported; }
+hipError_t hipGraphLaunch(hipGraphExec_t, hipStream_t) { return hipErrorNotSupported; }
+hipError_t hipGraphExecDestroy(hipGraphExec_t) { return hipErrorNotSupported; }
 hipError_t hipRuntimeGetVersion(int* v) { *v = 1; return hipSuccess; }
 hipError_t hipDriverGetVersion(int* v) { *v = 1; return hipSuccess; }
 

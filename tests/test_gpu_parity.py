@@ -277,13 +277,15 @@ def test_apply_chunked(mk_engine, chunk):
 def test_apply_small_calls(mk_engine, path):
     """replica-sized calls (one drained executeCommands batch, MAX_BATCH = 5000 commands,
     bareminpaxos.go:22,1071-1089): sizes around the wave (64), the workgroup (1024) and the
-    small kernel's limit (8192), mixed ops, the special keys, a hot key, GETs of absent keys
+    small kernels' limit (16384: up to three drained MAX_BATCH batches), mixed ops, the
+    special keys, a hot key, GETs of absent keys
     before their first PUT, and one table carried through all calls; every call's results,
     the table and its size bit-exact. AUTO and SMALL run the one-launch kernel (apply_small.hip)
     here, SORTED the multi-launch pipeline"""
     rng = np.random.default_rng(91 + path)
-    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 14, apply_path=path), Oracle(5, R.MODE_MIN)
-    sizes = [1, 2, 63, 64, 65, 1000, 1023, 1024, 1025, 4095, 5000, 8191, 8192]
+    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 16, apply_path=path), Oracle(5, R.MODE_MIN)
+    sizes = [1, 2, 63, 64, 65, 1000, 1023, 1024, 1025, 4095, 5000, 8191, 8192, 8193, 9000,
+             12000, 16383, 16384]
     for i, m in enumerate(sizes):
         op, key, val = gen_cases.commands_mixed(rng, m, 50 + 37 * i)
         key = np.where(key > 0, key + (i % 3) * 1_000_003, key)  # fresh keys every third call
@@ -299,7 +301,7 @@ def test_apply_small_calls(mk_engine, path):
         assert e.kv_size() == len(wk)
     # wide key spaces: almost every command alone on its key (the sort sees a few dozen shared
     # ones), and one call where exactly 1024 / 1025 commands share keys (the rank / radix switch)
-    for m, kr, seed in ((8192, 1 << 40, 95), (5000, 1 << 20, 96)):
+    for m, kr, seed in ((8192, 1 << 40, 95), (5000, 1 << 20, 96), (16384, 1 << 20, 97)):
         op, key, val = synth.commands(m, kr, 0.5, "uniform", seed=seed)
         gr, gc = e.apply(op, key, val)
         wr, wc = o.apply(op, key, val)
@@ -448,15 +450,16 @@ def test_apply_bucket_full(mk_engine, path):
 
 
 def test_apply_size_dispatch(mk_engine):
-    """with apply_path AUTO the call size picks the pipeline (apply_fast_min, here 10000
-    commands): calls on both sides of the switch carry one table, bit-exact. The
+    """with apply_path AUTO the call size picks the pipeline: the replica-batch kernels up to
+    16384 commands, the sort-based pipeline below apply_fast_min (here 20000), the partitioned
+    one from there: calls on both sides of both switches carry one table, bit-exact. The
     device-pointer entry point reserved for the largest call also runs the smaller calls, which
-    take the other pipeline with its own scratch layout (mpx_apply_reserve covers both)"""
+    take the other pipelines with their own scratch layouts (mpx_apply_reserve covers all)"""
     from minpaxos_amd.devbuf import Arena
     rng = np.random.default_rng(57)
-    e = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 16, apply_fast_min=10000)
+    e = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 16, apply_fast_min=20000)
     o = Oracle(5, R.MODE_MIN)
-    sizes = [40000, 9999, 10000, 37, 25000, 1]
+    sizes = [40000, 19999, 20000, 37, 16384, 16385, 25000, 1]
     e.apply_reserve(max(sizes))
     with Arena(e) as ar:
         for i, m in enumerate(sizes):
@@ -515,7 +518,7 @@ def test_apply_small_lists_and_tag_wrap(mk_engine):
     """replica-sized calls resolve each key's commands by walking the key's list of the call
     (apply_small.hip steps 1-3) and leave lists longer than 16 to the one-workgroup sort: calls
     whose key ranges put 1 .. ~100 commands on a key mix both in one call. The list heads are
-    tagged with the call (19 bits); at the wrap the heads are cleared: calls on key set A at tags
+    tagged with the call (18 bits); at the wrap the heads are cleared: calls on key set A at tags
     1..3, the tag moved to three calls before the wrap (mpx_debug_kv_set_small_tag), two calls on
     a disjoint set B, then calls on A at the wrapped tags 1..3 - without the clear A's heads would
     still carry tags 1..3 and link stale positions. Every call and the table bit-exact."""
@@ -534,9 +537,9 @@ def test_apply_small_lists_and_tag_wrap(mk_engine):
         call(5000, kr, 1, 300 + i)
     for i in range(3):
         call(3000, 500, 10_000_000, 310 + i)          # key set A
-    e.debug_kv_set_small_tag((1 << 19) - 3)
+    e.debug_kv_set_small_tag((1 << 18) - 3)
     for i in range(2):
-        call(3000, 500, 20_000_000, 320 + i)          # key set B, tags 2^19-2, 2^19-1
+        call(3000, 500, 20_000_000, 320 + i)          # key set B, tags 2^18-2, 2^18-1
     for i in range(3):
         call(3000, 500, 10_000_000, 330 + i)          # A again at the wrapped tags 1..3
     gk, gv = e.kv_export()
@@ -544,16 +547,17 @@ def test_apply_small_lists_and_tag_wrap(mk_engine):
     assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
     assert e.kv_size() == len(wk)
     with pytest.raises(MpxError):
-        e.debug_kv_set_small_tag(1 << 19)
+        e.debug_kv_set_small_tag(1 << 18)
 
 
 @pytest.mark.parametrize("cap_lg", [22, 23, 25, 26])
 def test_apply_large_table(mk_engine, cap_lg):
-    """tables past the partition's 1024 bins: kv_capacity 2^22 / 2^23 / 2^25 keys (2^23..2^26
-    slots) split the log into 1024 super-bins of 2 / 4 / 16 bins, which the resolve workgroup
-    takes one after another (partitioned pipeline forced); 2^26 keys is past the 16-bin limit and
-    takes the sort-based pipeline. Every call and the final table bit-exact, across calls, with
-    GETs of new keys before their first PUT (the two-pass bins) and a zipf call (hot keys)"""
+    """tables past the partition's 1024 bins: kv_capacity 2^22 / 2^23 / 2^25 / 2^26 keys
+    (2^23..2^27 slots) split the log into 1024 super-bins of 2 / 4 / 16 / 32 bins, which the
+    resolve workgroup takes one after another (partitioned pipeline forced for the smaller
+    tables, AUTO's pick - the same pipeline - for 2^27 slots). Every call and the final table
+    bit-exact, across calls, with GETs of new keys before their first PUT (the two-pass bins)
+    and a zipf call (hot keys)"""
     rng = np.random.default_rng(41 + cap_lg)
     path = R.APPLY_PARTITIONED if cap_lg < 26 else R.APPLY_AUTO
     e = mk_engine(5, R.MODE_MIN, kv_capacity=1 << cap_lg, apply_path=path)
