@@ -731,15 +731,31 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
 // ---- per-bin resolve ------------------------------------------------------------------------------
 constexpr int kRH = 3;             // records per thread per resolve batch
 constexpr int kRT = kRTT * kRH;    // records per batch (3072 at 16 buckets per bin)
+// MPX_RS_FP: the lookups read a one-byte fingerprint per slot (0 = empty, else 0x80 | 7 hash bits
+// that neither the bucket nor the home slot uses) 8 slots at a time - a bucket's 256 fingerprints
+// are one 64-bank row of LDS, so a wave's window reads never conflict - and the 8-byte key only
+// where a fingerprint matches, instead of 8 keys (64 random LDS bytes) per probe step
+#ifndef MPX_RS_FP
+#define MPX_RS_FP 1
+#endif
+// MPX_RS_META: the ranking pass, which hashes every record for its bucket, stages the hash's
+// low 16 bits beside it, so the bucket rounds compute no hash (a 64-bit multiply chain per record)
+#ifndef MPX_RS_META
+#define MPX_RS_META 1
+#endif
 struct ResolveLds {
     int64_t tk[kMaxBPB * kSB];
     int64_t tv[kMaxBPB * kSB];
+    uint8_t fp[kMaxBPB * kSB];
     uint8_t ts[kMaxBPB * kSB];
     uint8_t W[kRTW][kSB];
     unsigned long long PM[kRTW][kWave];
     int4 skv[kRT];                    // the batch's records in bucket order (log order inside)
     uint8_t sop[kRT];
     uint16_t sidx[kRT];               // their index in the batch
+#if MPX_RS_META
+    uint16_t shh[kRT];                // the low 16 bits of their key hash (home slot, fingerprint)
+#endif
     uint32_t cw[kRH * kRTW][kMaxBPB];  // per (half, wave): records per bucket -> exclusive prefix
     uint32_t bcnt[kMaxBPB], bst[kMaxBPB];
     uint32_t flags;
@@ -750,6 +766,13 @@ struct ResolveLds {
 
 __device__ __forceinline__ int64_t kv_lo_hi(int lo, int hi) {
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__device__ __forceinline__ uint8_t key_fp(uint64_t h) { return (uint8_t)(0x80u | ((h >> 8) & 0x7Fu)); }
+// bit 7 of byte j set iff byte j of x is zero (exact: no carry crosses a byte)
+__device__ __forceinline__ uint64_t zero_bytes(uint64_t x) {
+    constexpr uint64_t lo7 = 0x7F7F7F7F7F7F7F7Full;
+    return ~(((x & lo7) + lo7) | x | lo7);
 }
 
 // bucket b of the bin (wave b): its cnt records of this batch, in log order, 64 per round.
@@ -786,7 +809,43 @@ __device__ __forceinline__ RoundA resolve_stage_a(ResolveLds& S, int b, uint32_t
     // lookup in the bucket, MPX_RS_PROBE (8) slots per step (1 / 2 / 4 measured slower): the worst probe length among the wave's 64 lanes
     // sets the number of dependent LDS reads
     int s = -1;
-    uint32_t p = home_of(hash64((uint64_t)k));
+#if MPX_RS_META
+    const uint64_t hk = S.shh[x];  // (only the bits below 16 are used here)
+#else
+    const uint64_t hk = hash64((uint64_t)k);
+#endif
+    uint32_t p = home_of(hk);
+#if MPX_RS_FP
+    const uint8_t myfp = key_fp(hk);
+    if (a.live) {
+        const uint64_t* F = reinterpret_cast<const uint64_t*>(S.fp + b * kSB);
+        const uint64_t rep = 0x0101010101010101ull * myfp;
+        for (int step = 0; step < kSB / 8; ++step) {
+            // fingerprints of slots p .. p+7 (wrapping inside the bucket): two aligned words
+            const uint32_t wi = p >> 3, sh = (p & 7u) * 8u;
+            const uint64_t w0 = F[wi], w1 = F[(wi + 1) & (kSB / 8 - 1)];
+            const uint64_t win = sh ? (w0 >> sh) | (w1 << (64u - sh)) : w0;
+            const uint64_t emp = zero_bytes(win);
+            const int stop = emp ? (__ffsll((long long)emp) - 1) >> 3 : 8;
+            uint64_t cand = zero_bytes(win ^ rep);
+            if (stop < 8) cand &= (1ull << (8 * stop)) - 1ull;
+            while (cand) {
+                const uint32_t q = (p + (uint32_t)((__ffsll((long long)cand) - 1) >> 3)) & (kSB - 1);
+                if (T[q] == k) {
+                    s = (int)q;
+                    break;
+                }
+                cand &= cand - 1ull;
+            }
+            if (s >= 0) break;
+            if (stop < 8) {
+                p = (p + (uint32_t)stop) & (kSB - 1);  // the first empty slot: an insert starts here
+                break;
+            }
+            p = (p + 8) & (kSB - 1);
+        }
+    }
+#else
     if (a.live) {
 #ifndef MPX_RS_PROBE
 #define MPX_RS_PROBE 8
@@ -813,6 +872,7 @@ __device__ __forceinline__ RoundA resolve_stage_a(ResolveLds& S, int b, uint32_t
             p = (p + kPS) & (kSB - 1);
         }
     }
+#endif
     if (a.live && s < 0 && a.isput) {  // a key new to the table: claim a slot
         if (mode == 0) atomicOr(&S.flags, kFNewPut);
         for (int probe = 0; probe < kSB; ++probe) {
@@ -822,6 +882,7 @@ __device__ __forceinline__ RoundA resolve_stage_a(ResolveLds& S, int b, uint32_t
             if (cur == (unsigned long long)kSentinel) {
                 s = (int)p;
                 TS[p] |= kSNew;
+                S.fp[b * kSB + p] = key_fp(hk);
                 break;
             }
             if ((int64_t)cur == k) {
@@ -923,7 +984,9 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
     };
     auto load_tables = [&]() {
         for (uint32_t i = tid; i < nslot; i += kRTT) {
-            S.tk[i] = t.keys[gbase + i];
+            const int64_t tkey = t.keys[gbase + i];
+            S.tk[i] = tkey;
+            S.fp[i] = tkey == kSentinel ? (uint8_t)0 : key_fp(hash64((uint64_t)tkey));
             S.tv[i] = t.vals[gbase + i];
             const uint32_t x = t.state[gbase + i];
             const uint8_t pres = (uint8_t)(x & kPresent);
@@ -959,6 +1022,7 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
                                   (unsigned long long)kSentinel, (unsigned long long)k);
                     if (cur == (unsigned long long)kSentinel) {
                         S.ts[b * kSB + p] |= kSNew;
+                        S.fp[b * kSB + p] = key_fp(h);
                         done = true;
                     } else if ((int64_t)cur == k) {
                         done = true;
@@ -994,10 +1058,16 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
         for (uint32_t base = r0; base < r1; base += kRT) {
             uint32_t bl[kRH], rk[kRH];
             bool live[kRH];
+#if MPX_RS_META
+            uint16_t hlo[kRH];
+#endif
 #pragma unroll
             for (int hh = 0; hh < kRH; ++hh) {
                 const uint32_t i = hh * kRTT + tid;
                 const uint64_t h = hash64((uint64_t)kv_lo_hi(kv[hh].x, kv[hh].y));
+#if MPX_RS_META
+                hlo[hh] = (uint16_t)h;
+#endif
                 live[hh] = base + i < r1 && member(h);
                 bl[hh] = bucket_of(h, g.lgnb) & (bpb - 1);
                 rk[hh] = 0;
@@ -1055,6 +1125,9 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
                         S.skv[x] = kv[hh];
                         S.sop[x] = (uint8_t)o[hh];
                         S.sidx[x] = (uint16_t)(hh * kRTT + tid);
+#if MPX_RS_META
+                        S.shh[x] = hlo[hh];
+#endif
                     }
                 }
             }

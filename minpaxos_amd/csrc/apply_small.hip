@@ -81,7 +81,7 @@ constexpr uint32_t kLongBit = 0x80000000u;  // probe[p] after the walk: p's list
 constexpr int kWalkMax = 16;                // longest list a walk resolves
 constexpr uint32_t kLinkOff = 2 * kSmMax;
 constexpr uint32_t kCtlOff = kSmallCtl;     // probe[kCtlOff]: LONG commands, [+1]: last call's tag
-static_assert(kCtlOff == 3 * kSmMax && kCtlOff + 3 <= kSmallScratchWords, "small apply scratch");
+static_assert(kCtlOff == 3 * kSmMax && kCtlOff + 3 <= kSmallKeyOff, "small apply scratch");
 static_assert(kSmMax <= (1 << kPosBits) && (kSmallTagMax << kPosBits) == 0, "tagged list head");
 
 struct SmallLds {
@@ -144,14 +144,20 @@ __device__ __forceinline__ void list_push(const KvTable& t, uint32_t tag, uint32
 __global__ __launch_bounds__(kProbeBlock) void k_small_probe(KvTable t, const uint8_t* __restrict__ op,
                                                        const int64_t* __restrict__ key,
                                                        const int64_t* __restrict__ val, uint32_t m,
-                                                       int64_t* __restrict__ ret, uint32_t* err) {
+                                                       int64_t* __restrict__ ret, uint32_t* err,
+                                                       bool host_out) {
     const uint32_t p = blockIdx.x * kProbeBlock + threadIdx.x;
     if (p >= m) return;
     const uint32_t tag = call_tag(t);
     const uint8_t o = op[p];
     const int64_t k = key[p];
+    const int64_t v = val[p];
+    // the later kernels read the commands from here (device memory)
+    reinterpret_cast<int64_t*>(t.probe + kSmallKeyOff)[p] = k;
+    reinterpret_cast<int64_t*>(t.probe + kSmallValOff)[p] = v;
+    reinterpret_cast<uint8_t*>(t.probe + kSmallOpOff)[p] = o;
     const bool put = o == MPX_OP_PUT;
-    if (put) ret[p] = val[p];  // a PUT returns its value
+    if (put) ret[p] = v;  // a PUT returns its value
     uint32_t slot = kNoSlot;
     if (k == kSentinel) {
         slot = (uint32_t)t.cap;  // the sentinel key lives in the side slot
@@ -194,6 +200,9 @@ __global__ __launch_bounds__(kProbeBlock) void k_small_probe(KvTable t, const ui
     }
     t.probe[p] = slot;
     t.probe[kSmMax + p] = st;
+    // host-mapped results: performed at system scope before the kernel ends, so the walk kernel's
+    // completion flag (stored after its own results) can never overtake them
+    if (host_out) __threadfence_system();
 }
 
 // ---- 2. the lookups that met a free slot, again now that every claim of the call is in --------
@@ -292,6 +301,14 @@ __device__ __forceinline__ void walk_one(const KvTable& t, const uint8_t* __rest
 // The call's last workgroup also closes it: the LONG count and the ticket back to 0 and the next
 // call's tag; after the call with the last tag every list head is cleared and the tags restart at
 // 1 (once per 2^18 - 1 calls: one workgroup's pass over the heads). All threads call it.
+// the host form's completion flag: every result of the call is visible to the host before it
+__device__ __forceinline__ void signal_done(uint32_t* done, uint32_t seq) {
+    if (!done) return;
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ void end_of_call(const KvTable& t, uint32_t tag) {
     __syncthreads();  // every thread has read the control words
     const bool wrap = tag + 1u >= kSmallTagMax;
@@ -311,7 +328,8 @@ __device__ __forceinline__ void end_of_call(const KvTable& t, uint32_t tag) {
 __global__ __launch_bounds__(kSmT) void k_small_walk(KvTable t, const uint8_t* __restrict__ op,
                                                      const int64_t* __restrict__ val, uint32_t m,
                                                      int64_t* __restrict__ ret,
-                                                     uint8_t* __restrict__ conf) {
+                                                     uint8_t* __restrict__ conf, uint32_t* done,
+                                                     uint32_t seq) {
     __shared__ SmallLds S;
     {
         bool fresh, lng;
@@ -322,6 +340,7 @@ __global__ __launch_bounds__(kSmT) void k_small_walk(KvTable t, const uint8_t* _
             if (bl) atomic_add_done(&t.probe[kCtlOff], (uint32_t)popc(bl));
         }
     }
+    if (done) __threadfence_system();  // this workgroup's host-mapped results, before its ticket
     if (!last_workgroup(&t.probe[kCtlOff + 2])) return;
 #if MPX_SMALL_STAMP
     unsigned long long _sm_prev = __builtin_amdgcn_s_memrealtime();
@@ -334,6 +353,7 @@ __global__ __launch_bounds__(kSmT) void k_small_walk(KvTable t, const uint8_t* _
     const uint32_t tag = call_tag(t);
     if (n_long == 0) {  // every list was walked (the common case)
         end_of_call(t, tag);
+        signal_done(done, seq);
         return;
     }
     for (int i = tid; i < kSmHash; i += kSmT) S.tab[i] = 0;
@@ -591,6 +611,7 @@ __global__ __launch_bounds__(kSmT) void k_small_walk(KvTable t, const uint8_t* _
     __syncthreads();
     if (tid == 0 && S.n_new) atomicAdd(t.n_present, (unsigned long long)S.n_new);
     end_of_call(t, tag);
+    signal_done(done, seq);
     SM_STAMP(6);
 #if MPX_SMALL_STAMP
     if (threadIdx.x == 0) {  // shader clock ticks and 100 MHz ticks of the whole kernel
@@ -615,14 +636,18 @@ extern "C" int mpx_debug_small_stamps(unsigned long long* out16, int reset) {
 
 hipError_t launch_apply_small(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
                               uint64_t m, int64_t* ret, uint8_t* conf, uint32_t* err,
-                              hipStream_t stream) {
+                              hipStream_t stream, uint32_t* done, uint32_t seq) {
     if (!m) return hipSuccess;
     if (m > (uint64_t)kSmMax || t.cap >= 0x7FFFFFFEull) return hipErrorInvalidValue;
     const unsigned g = (unsigned)((m + kProbeBlock - 1) / kProbeBlock);
-    k_small_probe<<<g, kProbeBlock, 0, stream>>>(t, op, key, val, (uint32_t)m, ret, err);
-    k_small_reprobe<<<g, kProbeBlock, 0, stream>>>(t, key, (uint32_t)m);
-    k_small_walk<<<(unsigned)((m + kSmT - 1) / kSmT), kSmT, 0, stream>>>(t, op, val, (uint32_t)m,
-                                                                         ret, conf);
+    const int64_t* d_key = reinterpret_cast<const int64_t*>(t.probe + kSmallKeyOff);
+    const int64_t* d_val = reinterpret_cast<const int64_t*>(t.probe + kSmallValOff);
+    const uint8_t* d_op = reinterpret_cast<const uint8_t*>(t.probe + kSmallOpOff);
+    k_small_probe<<<g, kProbeBlock, 0, stream>>>(t, op, key, val, (uint32_t)m, ret, err,
+                                                 done != nullptr);
+    k_small_reprobe<<<g, kProbeBlock, 0, stream>>>(t, d_key, (uint32_t)m);
+    k_small_walk<<<(unsigned)((m + kSmT - 1) / kSmT), kSmT, 0, stream>>>(
+        t, d_op, d_val, (uint32_t)m, ret, conf, done, seq);
     return hipGetLastError();
 }
 

@@ -60,6 +60,7 @@ struct mpx_engine {
     // commands from and writes the results to (no DMA copies on the call's path)
     uint8_t* pin = nullptr;
     size_t pin_cap = 0;
+    uint32_t small_seq = 0;  // the host form's completion flag value of the last call
     // group-step work list (groups the fast kernel hands to the general kernel) + its count
     DevBuf worklist;
     uint32_t* d_wcount = nullptr;
@@ -467,7 +468,7 @@ int mpx_apply(mpx_engine* e, const uint8_t* op, const int64_t* key, const int64_
         // CPU copy on each side
         HIPCHK(e, hipSetDevice(e->device));
         CK(ensure_kv(e));
-        constexpr size_t kHdr = 64;  // the error word, alone in its cache line
+        constexpr size_t kHdr = 128;  // the error word and the completion flag, a line each
         const size_t a16 = (m + 15) & ~(size_t)15, need = kHdr + a16 * 2 + m * 24;
         if (e->pin_cap < need) {
             if (e->pin) (void)hipHostFree(e->pin);
@@ -480,6 +481,7 @@ int mpx_apply(mpx_engine* e, const uint8_t* op, const int64_t* key, const int64_
             e->pin_cap = need;
         }
         volatile uint32_t* h_err = (volatile uint32_t*)e->pin;
+        volatile uint32_t* h_done = (volatile uint32_t*)(e->pin + 64);
         uint8_t* h_op = e->pin + kHdr;
         int64_t* h_key = (int64_t*)(h_op + a16);
         int64_t* h_val = h_key + m;
@@ -492,13 +494,30 @@ int mpx_apply(mpx_engine* e, const uint8_t* op, const int64_t* key, const int64_
         void* dp = nullptr;
         HIPCHK(e, hipHostGetDevicePointer(&dp, e->pin, 0));
         uint8_t* d0 = (uint8_t*)dp + kHdr;
-        mpx::ApplyWork w{nullptr, 0};
-        HIPCHK(e, mpx::launch_apply(e->kv, d0, (const int64_t*)(d0 + a16),
-                                    (const int64_t*)(d0 + a16) + m, m,
-                                    (int64_t*)(d0 + a16) + 2 * m,
-                                    conf_prev ? d0 + a16 + m * 24 : nullptr, e->apply, w,
-                                    (uint32_t*)dp, e->stream));
-        HIPCHK(e, hipStreamSynchronize(e->stream));
+        uint32_t seq = ++e->small_seq;
+        if (!seq) seq = e->small_seq = 1;  // 0 never marks a finished call
+        HIPCHK(e, mpx::launch_apply_small(e->kv, d0, (const int64_t*)(d0 + a16),
+                                          (const int64_t*)(d0 + a16) + m, m,
+                                          (int64_t*)(d0 + a16) + 2 * m,
+                                          conf_prev ? d0 + a16 + m * 24 : nullptr,
+                                          (uint32_t*)dp, e->stream,
+                                          (uint32_t*)((uint8_t*)dp + 64), seq));
+        // the last workgroup stores seq once every result is visible here: poll it (a stream
+        // wait adds the runtime's wake-up latency to a ~13 us call); the stream is queried now
+        // and then, so a failed launch or a faulted kernel ends the wait with its error
+        for (uint64_t it = 1; *h_done != seq; ++it) {
+            if ((it & 1023) == 0) {
+                const hipError_t q = hipStreamQuery(e->stream);
+                if (q == hipSuccess) {
+                    if (*h_done == seq) break;
+                    return fail(e, MPX_E_HIP, "mpx_apply: the call ended without its completion flag");
+                }
+                if (q != hipErrorNotReady) return hip_fail(e, "mpx_apply", q);
+            }
+#if defined(__x86_64__)
+            __builtin_ia32_pause();
+#endif
+        }
         const uint32_t werr = *h_err;
         std::memcpy(ret, h_ret, m * 8);
         if (conf_prev) std::memcpy(conf_prev, h_conf, m);

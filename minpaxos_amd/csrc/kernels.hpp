@@ -88,7 +88,12 @@ struct KvTable {
 // [kSmallCtl] LONG commands of the call, [kSmallCtl + 1] the tag of the last call (device-side,
 // so a captured graph's replays take fresh tags), [kSmallCtl + 2] the walk kernel's ticket
 constexpr uint32_t kSmallCtl = 3 * MPX_APPLY_SMALL_MAX;
-constexpr uint32_t kSmallScratchWords = kSmallCtl + 64;
+// then the call's commands as the probe kernel read them (key, val: 2 words each; op: bytes), so
+// the later kernels read device memory, not the host form's pinned staging across the link
+constexpr uint32_t kSmallKeyOff = kSmallCtl + 64;
+constexpr uint32_t kSmallValOff = kSmallKeyOff + 2 * MPX_APPLY_SMALL_MAX;
+constexpr uint32_t kSmallOpOff = kSmallValOff + 2 * MPX_APPLY_SMALL_MAX;
+constexpr uint32_t kSmallScratchWords = kSmallOpOff + MPX_APPLY_SMALL_MAX / 4;
 constexpr uint32_t kSmallTagMax = 1u << 18;  // 18 tag bits above the 14 position bits
 
 constexpr uint32_t kKvEpochMax = 1u << 30;  // = kvtab.hpp kEpochMax (state bits 2..31)
@@ -123,10 +128,12 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
                              uint32_t hot_min, uint32_t* err, hipStream_t stream);
 // replica-batch apply of at most MPX_APPLY_SMALL_MAX commands (apply_small.hip, three launches).
 // err may be a host-mapped word (the host-pointer form): the kernels raise into it with plain
-// stores (every bit they raise is kErrKvFull), never atomics
+// stores (every bit they raise is kErrKvFull), never atomics. done (optional, host-mapped): the
+// last workgroup stores seq there once every result of the call is visible to the host, so the
+// host form can poll it instead of waiting on the stream
 hipError_t launch_apply_small(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
                               uint64_t m, int64_t* ret, uint8_t* conf, uint32_t* err,
-                              hipStream_t stream);
+                              hipStream_t stream, uint32_t* done = nullptr, uint32_t seq = 0);
 hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
                         uint64_t m, int64_t* ret, uint8_t* conf, const ApplyOpts& o, ApplyWork& w,
                         uint32_t* err, hipStream_t stream);

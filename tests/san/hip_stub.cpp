@@ -112,6 +112,7 @@ hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned int) {
 }
 hipError_t hipStreamDestroy(hipStream_t s) { free(s); return hipSuccess; }
 hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipStreamQuery(hipStream_t) { return hipSuccess; }
 hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned int) { return hipSuccess; }
 hipError_t hipDeviceSynchronize(void) { return hipSuccess; }
 hipError_t hipMalloc(void** p, size_t n) { *p = calloc(1, n ? n : 1); return *p ? hipSuccess : hipErrorOutOfMemory; }
@@ -298,6 +299,13 @@ uint64_t apply_work_bytes(const KvTable&, const ApplyOpts&, uint64_t m) { return
 uint64_t apply_reserve_bytes(const KvTable&, const ApplyOpts&, uint64_t m) { return 48 * m + 256; }
 hipError_t launch_apply(KvTable&, const uint8_t*, const int64_t*, const int64_t*, uint64_t,
                         int64_t*, uint8_t*, const ApplyOpts&, ApplyWork&, uint32_t*, hipStream_t) { return hipSuccess; }
+// the replica-batch form: nothing to compute on the stub, but the call completes (its flag)
+hipError_t launch_apply_small(KvTable&, const uint8_t*, const int64_t*, const int64_t*, uint64_t,
+                              int64_t*, uint8_t*, uint32_t*, hipStream_t, uint32_t* done,
+                              uint32_t seq) {
+    if (done) *done = seq;
+    return hipSuccess;
+}
 hipError_t launch_kv_clear(KvTable&, hipStream_t) { return hipSuccess; }
 hipError_t launch_kv_import(KvTable&, const int64_t*, const int64_t*, uint64_t, uint32_t*,
                             hipStream_t) { return hipSuccess; }
