@@ -934,6 +934,22 @@ def kernel_bench(a, rk):
             host_call = {"median_us": float(np.median(hc)) * 1e6,
                          "min_us": float(np.min(hc)) * 1e6, "calls": len(hc),
                          "form": "mpx_apply (host pointers, synchronous)"}
+            if M <= R.APPLY_SMALL_MAX and a.apply_path in ("auto", "small"):
+                # the zero-copy form (mpx_apply_buffers / mpx_apply_staged): the shim builds the
+                # drained batch straight in the engine's pinned arrays, so only the call is timed
+                io = eng.apply_buffers(M)
+                io["op"][:M], io["key"][:M], io["val"][:M] = op, key, val
+                hs = []
+                for _ in range(max(20, 4 * a.steps)):
+                    t0 = time.perf_counter()
+                    eng.apply_staged(M)
+                    hs.append(time.perf_counter() - t0)
+                parity["staged_form_bit_exact"] = bool(np.array_equal(io["ret"][:M], w_ret)
+                                                       and np.array_equal(io["conf"][:M], w_conf))
+                host_call["staged"] = {"median_us": float(np.median(hs)) * 1e6,
+                                       "min_us": float(np.min(hs)) * 1e6, "calls": len(hs),
+                                       "form": "mpx_apply_staged (engine-pinned arrays, "
+                                               "synchronous)"}
         ret = np.zeros(M, np.int64)
         k0, v0 = np.ascontiguousarray(wk), np.ascontiguousarray(wv)
         secs, reps = _cpu_loop(lambda: lib.orc_bench_apply(

@@ -68,7 +68,7 @@
 extern "C" {
 #endif
 
-#define MPX_ABI_VERSION 5  /* 4: + mpx_group_step_totals_dev; 5: + mpx_graph_* */
+#define MPX_ABI_VERSION 5  /* 4: + mpx_group_step_totals_dev; 5: + mpx_graph_*, mpx_apply_buffers / _staged */
 
 /* ---- error codes ---------------------------------------------------------------------- */
 #define MPX_OK 0
@@ -293,6 +293,24 @@ int mpx_apply_reserve(mpx_engine* eng, size_t max_cmds);
 int mpx_apply_dev(mpx_engine* eng, const uint8_t* d_op, const int64_t* d_key,
                   const int64_t* d_val, size_t m, int64_t* d_ret, uint8_t* d_conf_prev,
                   void* stream);
+/* ---- replica-batch apply without copies (the cgo shim's form, ABI 5) -------------------
+ * mpx_apply_buffers: the engine's pinned, GPU-mapped command and result arrays for calls of up
+ * to max_m (<= MPX_APPLY_SMALL_MAX) commands; the caller writes a drained executeCommands batch
+ * straight into io->op / key / val and calls mpx_apply_staged(eng, m): the results of
+ * mpx_apply(eng, io->op, io->key, io->val, m, io->ret, io->conf) land in io->ret / io->conf,
+ * read and written by the kernels across the link, with no copy on either side. The arrays stay
+ * valid until the next mpx_apply_buffers that grows them or mpx_close; needs apply_path AUTO or
+ * SMALL. Synchronous, like mpx_apply.                                                       */
+typedef struct mpx_apply_io {
+    uint8_t* op;
+    int64_t* key;
+    int64_t* val;
+    int64_t* ret;
+    uint8_t* conf;
+    uint64_t cap;  /* commands the arrays hold                                               */
+} mpx_apply_io;
+int mpx_apply_buffers(mpx_engine* eng, size_t max_m, mpx_apply_io* io);
+int mpx_apply_staged(mpx_engine* eng, size_t m);
 /* table access: number of present keys; export (any order) / import / clear               */
 int mpx_kv_size(mpx_engine* eng, size_t* n);
 int mpx_kv_export(mpx_engine* eng, int64_t* keys, int64_t* vals, size_t cap, size_t* n);

@@ -37,6 +37,11 @@ class MpxDecodeOut(C.Structure):
                 ("var_cap", _sz), ("other", _p), ("other_cap", _sz)]
 
 
+class MpxApplyIo(C.Structure):
+    _fields_ = [("op", _p), ("key", _p), ("val", _p), ("ret", _p), ("conf", _p),
+                ("cap", C.c_uint64)]
+
+
 # name -> (restype, argtypes); every symbol of include/mpx.h
 SIGNATURES = {
     "mpx_abi_version": (C.c_int, []),
@@ -97,6 +102,8 @@ SIGNATURES = {
     "mpx_event_create": (C.c_int, [_p, C.c_int, C.POINTER(_p)]),
     "mpx_event_destroy": (C.c_int, [_p, _p]),
     "mpx_event_record": (C.c_int, [_p, _p, _p]),
+    "mpx_apply_buffers": (C.c_int, [_p, _sz, C.POINTER(MpxApplyIo)]),
+    "mpx_apply_staged": (C.c_int, [_p, _sz]),
     "mpx_graph_begin": (C.c_int, [_p, _p]),
     "mpx_graph_end": (C.c_int, [_p, _p, C.POINTER(C.c_void_p)]),
     "mpx_graph_launch": (C.c_int, [_p, _p, _p]),

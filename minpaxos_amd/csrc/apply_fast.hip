@@ -79,8 +79,19 @@ constexpr int kLgMaxSub = 8;
 #endif
 constexpr int kLgMaxBPB = MPX_RS_LGBPB;
 constexpr int kMaxBPB = 1 << kLgMaxBPB;
-constexpr int kRTT = kMaxBPB * kWave;  // threads of the resolve workgroup
-constexpr int kRTW = kMaxBPB;
+// resolve workgroups per bin (MPX_RS_SPLIT): 1 = one 16-wave workgroup per bin (one per CU, its
+// LDS); 2 = two 8-wave workgroups, each resolving 8 of the bin's 16 buckets from the same record
+// stream (half the LDS each: two per CU, one waits at a barrier while the other works)
+#ifndef MPX_RS_SPLIT
+#define MPX_RS_SPLIT 1
+#endif
+constexpr int kRSplit = MPX_RS_SPLIT;
+constexpr int kLgRSplit = kRSplit == 4 ? 2 : (kRSplit == 2 ? 1 : 0);
+static_assert((1 << kLgRSplit) == kRSplit && kRSplit <= kMaxBPB, "resolve split");
+constexpr int kLgRBPW = kLgMaxBPB - kLgRSplit;
+constexpr int kRBPW = 1 << kLgRBPW;    // buckets (= waves) of a resolve workgroup
+constexpr int kRTT = kRBPW * kWave;    // threads of the resolve workgroup
+constexpr int kRTW = kRBPW;
 constexpr int kLgSamples = 16;
 constexpr uint32_t kSamples = 1u << kLgSamples;  // (k_ap_sample divides by a shift)
 constexpr uint32_t kHotIdx = 0x8000u;  // ipos: hot command (| hot index), else image index
@@ -731,33 +742,17 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
 // ---- per-bin resolve ------------------------------------------------------------------------------
 constexpr int kRH = 3;             // records per thread per resolve batch
 constexpr int kRT = kRTT * kRH;    // records per batch (3072 at 16 buckets per bin)
-// MPX_RS_FP: the lookups read a one-byte fingerprint per slot (0 = empty, else 0x80 | 7 hash bits
-// that neither the bucket nor the home slot uses) 8 slots at a time - a bucket's 256 fingerprints
-// are one 64-bank row of LDS, so a wave's window reads never conflict - and the 8-byte key only
-// where a fingerprint matches, instead of 8 keys (64 random LDS bytes) per probe step
-#ifndef MPX_RS_FP
-#define MPX_RS_FP 1
-#endif
-// MPX_RS_META: the ranking pass, which hashes every record for its bucket, stages the hash's
-// low 16 bits beside it, so the bucket rounds compute no hash (a 64-bit multiply chain per record)
-#ifndef MPX_RS_META
-#define MPX_RS_META 1
-#endif
 struct ResolveLds {
-    int64_t tk[kMaxBPB * kSB];
-    int64_t tv[kMaxBPB * kSB];
-    uint8_t fp[kMaxBPB * kSB];
-    uint8_t ts[kMaxBPB * kSB];
+    int64_t tk[kRBPW * kSB];
+    int64_t tv[kRBPW * kSB];
+    uint8_t ts[kRBPW * kSB];
     uint8_t W[kRTW][kSB];
     unsigned long long PM[kRTW][kWave];
     int4 skv[kRT];                    // the batch's records in bucket order (log order inside)
     uint8_t sop[kRT];
     uint16_t sidx[kRT];               // their index in the batch
-#if MPX_RS_META
-    uint16_t shh[kRT];                // the low 16 bits of their key hash (home slot, fingerprint)
-#endif
-    uint32_t cw[kRH * kRTW][kMaxBPB];  // per (half, wave): records per bucket -> exclusive prefix
-    uint32_t bcnt[kMaxBPB], bst[kMaxBPB];
+    uint32_t cw[kRH * kRTW][kRBPW];  // per (third, wave): records per bucket -> exclusive prefix
+    uint32_t bcnt[kRBPW], bst[kRBPW];
     uint32_t flags;
 #if MPX_RS_STAMP
     unsigned long long ph[8], rb[kRTW];
@@ -768,12 +763,6 @@ __device__ __forceinline__ int64_t kv_lo_hi(int lo, int hi) {
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
-__device__ __forceinline__ uint8_t key_fp(uint64_t h) { return (uint8_t)(0x80u | ((h >> 8) & 0x7Fu)); }
-// bit 7 of byte j set iff byte j of x is zero (exact: no carry crosses a byte)
-__device__ __forceinline__ uint64_t zero_bytes(uint64_t x) {
-    constexpr uint64_t lo7 = 0x7F7F7F7F7F7F7F7Full;
-    return ~(((x & lo7) + lo7) | x | lo7);
-}
 
 // bucket b of the bin (wave b): its cnt records of this batch, in log order, 64 per round.
 // A round is two stages: A = the slot lookup (claiming slots for new keys) and the peer masks;
@@ -809,43 +798,7 @@ __device__ __forceinline__ RoundA resolve_stage_a(ResolveLds& S, int b, uint32_t
     // lookup in the bucket, MPX_RS_PROBE (8) slots per step (1 / 2 / 4 measured slower): the worst probe length among the wave's 64 lanes
     // sets the number of dependent LDS reads
     int s = -1;
-#if MPX_RS_META
-    const uint64_t hk = S.shh[x];  // (only the bits below 16 are used here)
-#else
-    const uint64_t hk = hash64((uint64_t)k);
-#endif
-    uint32_t p = home_of(hk);
-#if MPX_RS_FP
-    const uint8_t myfp = key_fp(hk);
-    if (a.live) {
-        const uint64_t* F = reinterpret_cast<const uint64_t*>(S.fp + b * kSB);
-        const uint64_t rep = 0x0101010101010101ull * myfp;
-        for (int step = 0; step < kSB / 8; ++step) {
-            // fingerprints of slots p .. p+7 (wrapping inside the bucket): two aligned words
-            const uint32_t wi = p >> 3, sh = (p & 7u) * 8u;
-            const uint64_t w0 = F[wi], w1 = F[(wi + 1) & (kSB / 8 - 1)];
-            const uint64_t win = sh ? (w0 >> sh) | (w1 << (64u - sh)) : w0;
-            const uint64_t emp = zero_bytes(win);
-            const int stop = emp ? (__ffsll((long long)emp) - 1) >> 3 : 8;
-            uint64_t cand = zero_bytes(win ^ rep);
-            if (stop < 8) cand &= (1ull << (8 * stop)) - 1ull;
-            while (cand) {
-                const uint32_t q = (p + (uint32_t)((__ffsll((long long)cand) - 1) >> 3)) & (kSB - 1);
-                if (T[q] == k) {
-                    s = (int)q;
-                    break;
-                }
-                cand &= cand - 1ull;
-            }
-            if (s >= 0) break;
-            if (stop < 8) {
-                p = (p + (uint32_t)stop) & (kSB - 1);  // the first empty slot: an insert starts here
-                break;
-            }
-            p = (p + 8) & (kSB - 1);
-        }
-    }
-#else
+    uint32_t p = home_of(hash64((uint64_t)k));
     if (a.live) {
 #ifndef MPX_RS_PROBE
 #define MPX_RS_PROBE 8
@@ -872,7 +825,6 @@ __device__ __forceinline__ RoundA resolve_stage_a(ResolveLds& S, int b, uint32_t
             p = (p + kPS) & (kSB - 1);
         }
     }
-#endif
     if (a.live && s < 0 && a.isput) {  // a key new to the table: claim a slot
         if (mode == 0) atomicOr(&S.flags, kFNewPut);
         for (int probe = 0; probe < kSB; ++probe) {
@@ -882,7 +834,6 @@ __device__ __forceinline__ RoundA resolve_stage_a(ResolveLds& S, int b, uint32_t
             if (cur == (unsigned long long)kSentinel) {
                 s = (int)p;
                 TS[p] |= kSNew;
-                S.fp[b * kSB + p] = key_fp(hk);
                 break;
             }
             if ((int64_t)cur == k) {
@@ -969,24 +920,45 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
                                                     uint32_t* err) {
     __shared__ ResolveLds S;
     const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
-    const uint32_t bpb = 1u << g.lgbpb, nslot = bpb * kSB;
+    const uint32_t bpb = 1u << g.lgbpb;
+    // this workgroup's (super-)bin and its part of the bin's buckets: the parts of one bin run on
+    // one XCD (workgroup x runs on XCD x % 8), dispatched together, so the second stream of the
+    // bin's records is an L2 hit
+    uint32_t bin = blockIdx.x, part = 0;
+    if (kRSplit > 1) {
+        if ((g.nbin & 7u) == 0) {
+            bin = (blockIdx.x >> (3 + kLgRSplit)) * 8u + (blockIdx.x & 7u);
+            part = (blockIdx.x >> 3) & (kRSplit - 1);
+        } else {
+            bin = blockIdx.x >> kLgRSplit;
+            part = blockIdx.x & (kRSplit - 1);
+        }
+    }
+    const uint32_t b_lo = part * kRBPW;
+    if (b_lo >= bpb) return;  // a table of fewer buckets per bin than the workgroups cover
+    const uint32_t nb = bpb - b_lo < (uint32_t)kRBPW ? bpb - b_lo : (uint32_t)kRBPW;
+    const int lgnbw = (int)(g.lgbpb < (uint32_t)kLgRBPW ? g.lgbpb : (uint32_t)kLgRBPW);
+    const uint32_t nslot = nb * kSB;
     const uint32_t nsub = 1u << g.lgsub;
     const uint32_t ep = t.epoch[0];
-    const uint32_t r0 = bin_start[blockIdx.x], r1 = bin_start[blockIdx.x + 1];
+    const uint32_t r0 = bin_start[bin], r1 = bin_start[bin + 1];
     if (r0 == r1) return;  // no records: nothing read, nothing touched (small calls, hot-heavy chunks)
     const unsigned long long below = (1ull << l) - 1ull;
+    // a record's bucket among this workgroup's (meaningful where member() holds)
+    auto local_bucket = [&](uint64_t h) {
+        return ((bucket_of(h, g.lgnb) & (bpb - 1)) - b_lo) & (uint32_t)(kRBPW - 1);
+    };
     for (uint32_t sub = 0; sub < nsub; ++sub) {
-    // bin (blockIdx.x << lgsub) | sub: its records are those of the super-bin's log whose bucket
-    // falls in it (every pass streams the super-bin's records)
-    const uint64_t gbase = (((uint64_t)blockIdx.x << g.lgsub) | sub) * nslot;
+    // bin (bin << lgsub) | sub: its records are those of the super-bin's log whose bucket falls
+    // in it (every pass streams the super-bin's records), of those the ones in this part
+    const uint64_t gbase = ((((uint64_t)bin << g.lgsub) | sub) * bpb + b_lo) * kSB;
     auto member = [&](uint64_t h) {
-        return ((bucket_of(h, g.lgnb) >> g.lgbpb) & (nsub - 1)) == sub;
+        const uint32_t bk = bucket_of(h, g.lgnb);
+        return ((bk >> g.lgbpb) & (nsub - 1)) == sub && ((bk & (bpb - 1)) - b_lo) < nb;
     };
     auto load_tables = [&]() {
         for (uint32_t i = tid; i < nslot; i += kRTT) {
-            const int64_t tkey = t.keys[gbase + i];
-            S.tk[i] = tkey;
-            S.fp[i] = tkey == kSentinel ? (uint8_t)0 : key_fp(hash64((uint64_t)tkey));
+            S.tk[i] = t.keys[gbase + i];
             S.tv[i] = t.vals[gbase + i];
             const uint32_t x = t.state[gbase + i];
             const uint8_t pres = (uint8_t)(x & kPresent);
@@ -1012,7 +984,7 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
                 const int64_t k = kv_lo_hi(kv.x, kv.y);
                 const uint64_t h = hash64((uint64_t)k);
                 if (!member(h)) continue;
-                const uint32_t b = bucket_of(h, g.lgnb) & (bpb - 1);
+                const uint32_t b = local_bucket(h);
                 int64_t* T = S.tk + b * kSB;
                 uint32_t p = home_of(h);
                 bool done = false;
@@ -1022,7 +994,6 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
                                   (unsigned long long)kSentinel, (unsigned long long)k);
                     if (cur == (unsigned long long)kSentinel) {
                         S.ts[b * kSB + p] |= kSNew;
-                        S.fp[b * kSB + p] = key_fp(h);
                         done = true;
                     } else if ((int64_t)cur == k) {
                         done = true;
@@ -1034,7 +1005,7 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
             __syncthreads();
         }
         // the next batch is loaded while this one is resolved
-        for (int i = tid; i < kRH * kRTW * kMaxBPB; i += kRTT) (&S.cw[0][0])[i] = 0u;
+        for (int i = tid; i < kRH * kRTW * kRBPW; i += kRTT) (&S.cw[0][0])[i] = 0u;
         __syncthreads();
         // (ops held as 32-bit values: packed into one register as bytes, the compiler waits for the
         // prefetch at the loop back-edge)
@@ -1058,21 +1029,15 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
         for (uint32_t base = r0; base < r1; base += kRT) {
             uint32_t bl[kRH], rk[kRH];
             bool live[kRH];
-#if MPX_RS_META
-            uint16_t hlo[kRH];
-#endif
 #pragma unroll
             for (int hh = 0; hh < kRH; ++hh) {
                 const uint32_t i = hh * kRTT + tid;
                 const uint64_t h = hash64((uint64_t)kv_lo_hi(kv[hh].x, kv[hh].y));
-#if MPX_RS_META
-                hlo[hh] = (uint16_t)h;
-#endif
                 live[hh] = base + i < r1 && member(h);
-                bl[hh] = bucket_of(h, g.lgnb) & (bpb - 1);
+                bl[hh] = local_bucket(h);
                 rk[hh] = 0;
                 if (MPX_RS_ABL & 4) continue;
-                const unsigned long long m = match_bits(bl[hh], (int)g.lgbpb, live[hh]);
+                const unsigned long long m = match_bits(bl[hh], lgnbw, live[hh]);
                 rk[hh] = (uint32_t)__popcll(m & below);
                 if (live[hh] && (m >> l) == 1ull)  // the last lane of its bucket: the count
                     S.cw[hh * kRTW + w][bl[hh]] = (uint32_t)__popcll(m);
@@ -1083,14 +1048,14 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
             // every wave computes the prefixes its own records need (lane b: bucket b), so no wave
             // waits for another between the ranking and the staging
             {
-                const uint32_t b = (uint32_t)l & (kMaxBPB - 1);
+                const uint32_t b = (uint32_t)l & (kRBPW - 1);
                 // per half: the records of this wave's earlier groups, and of all groups
                 uint32_t pre[kRH], all[kRH];
 #pragma unroll
                 for (int hh = 0; hh < kRH; ++hh) {
                     uint32_t c[kRTW];
 #pragma unroll
-                    for (int v = 0; v < kRTW; ++v) c[v] = b < bpb ? S.cw[hh * kRTW + v][b] : 0u;
+                    for (int v = 0; v < kRTW; ++v) c[v] = b < nb ? S.cw[hh * kRTW + v][b] : 0u;
                     pre[hh] = 0;
                     all[hh] = 0;
 #pragma unroll
@@ -1105,14 +1070,14 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
                     pre[hh] += tot;
                     tot += all[hh];
                 }
-                uint32_t sc = tot;  // inclusive scan over the buckets (each 16-lane segment)
+                uint32_t sc = tot;  // inclusive scan over the buckets (each kRBPW-lane segment)
 #pragma unroll
-                for (int d = 1; d < kMaxBPB; d <<= 1) {
+                for (int d = 1; d < kRBPW; d <<= 1) {
                     const uint32_t y = __shfl_up(sc, d);
-                    if ((l & (kMaxBPB - 1)) >= d) sc += y;
+                    if ((l & (kRBPW - 1)) >= d) sc += y;
                 }
                 const uint32_t st = sc - tot;
-                if (w == 0 && l < kMaxBPB && b < bpb) {
+                if (w == 0 && l < kRBPW && b < nb) {
                     S.bcnt[b] = tot;
                     S.bst[b] = st;
                 }
@@ -1125,9 +1090,6 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
                         S.skv[x] = kv[hh];
                         S.sop[x] = (uint8_t)o[hh];
                         S.sidx[x] = (uint16_t)(hh * kRTT + tid);
-#if MPX_RS_META
-                        S.shh[x] = hlo[hh];
-#endif
                     }
                 }
             }
@@ -1142,11 +1104,11 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
             RS_STAMP(2);
             __syncthreads();
             RS_STAMP(3);
-            for (int i = tid; i < kRH * kRTW * kMaxBPB; i += kRTT) (&S.cw[0][0])[i] = 0u;
+            for (int i = tid; i < kRH * kRTW * kRBPW; i += kRTT) (&S.cw[0][0])[i] = 0u;
 #if MPX_RS_STAMP
             const unsigned long long rb0 = clock64();
 #endif
-            if (!(MPX_RS_ABL & 1) && (uint32_t)w < bpb)
+            if (!(MPX_RS_ABL & 1) && (uint32_t)w < nb)
                 resolve_bucket(S, w, S.bcnt[w], S.bst[w], mode, base, r_ret, r_conf, err);
 #if MPX_RS_STAMP
             if (l == 0) S.rb[w] += clock64() - rb0;
@@ -1459,7 +1421,7 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
         k_ap_scan_rows<<<g.ng, 256, 0, stream>>>(g, rows, part, bin_start, hot);
         k_ap_scatter<<<kScatterGrid, kTT, 0, stream>>>(g, op + c0, key + c0, val + c0, n, rows, hot,
                                                   rec_kv, rec_op, ipos, cpos, tcold);
-        k_ap_resolve<<<g.nbin, kRTT, 0, stream>>>(g, t, bin_start, rec_kv, rec_op, r_ret, r_conf,
+        k_ap_resolve<<<g.nbin * kRSplit, kRTT, 0, stream>>>(g, t, bin_start, rec_kv, rec_op, r_ret, r_conf,
                                                  hot, err);
         k_ap_hot_commit<<<1, kHMax, 0, stream>>>(t, val + c0, hot, err);
         k_ap_emit<<<g.tiles, kTT, 0, stream>>>(g, op + c0, val + c0, n, ipos, cpos, tcold, r_ret,

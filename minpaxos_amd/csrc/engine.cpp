@@ -24,6 +24,37 @@ struct DevBuf {
     size_t cap = 0;
 };
 
+// pinned, GPU-mapped staging of a replica-batch apply: [error word | completion flag] (a cache
+// line each), then op (cap rounded to 16), key, val, ret (cap each) and conf
+struct PinIo {
+    uint8_t* p = nullptr;
+    size_t cap = 0;  // commands
+};
+constexpr size_t kPinHdr = 128;
+struct PinView {
+    volatile uint32_t* err;
+    volatile uint32_t* done;
+    uint8_t* op;
+    int64_t* key;
+    int64_t* val;
+    int64_t* ret;
+    uint8_t* conf;
+};
+PinView pin_view_at(uint8_t* base, size_t cap) {
+    const size_t a16 = (cap + 15) & ~(size_t)15;
+    PinView v;
+    v.err = (volatile uint32_t*)base;
+    v.done = (volatile uint32_t*)(base + 64);
+    v.op = base + kPinHdr;
+    v.key = (int64_t*)(v.op + a16);
+    v.val = v.key + cap;
+    v.ret = v.val + cap;
+    v.conf = (uint8_t*)(v.ret + cap);
+    return v;
+}
+PinView pin_view(const PinIo& p) { return pin_view_at(p.p, p.cap); }
+size_t pin_bytes(size_t cap) { return kPinHdr + ((cap + 15) & ~(size_t)15) + cap * 25; }
+
 }  // namespace
 
 struct mpx_engine {
@@ -58,8 +89,8 @@ struct mpx_engine {
     mpx::ApplyOpts apply{};  // mpx_config.apply_* (fixed for the handle's life)
     // replica-sized mpx_apply calls: pinned, GPU-mapped staging the one-launch kernel reads the
     // commands from and writes the results to (no DMA copies on the call's path)
-    uint8_t* pin = nullptr;
-    size_t pin_cap = 0;
+    PinIo pin_io;       // mpx_apply's (copies in and out)
+    PinIo pin_staged;   // mpx_apply_buffers / mpx_apply_staged's (the caller fills it)
     uint32_t small_seq = 0;  // the host form's completion flag value of the last call
     // group-step work list (groups the fast kernel hands to the general kernel) + its count
     DevBuf worklist;
@@ -197,6 +228,54 @@ int ensure_kv(mpx_engine* e) {
     return MPX_OK;
 }
 
+int pin_grow(mpx_engine* e, PinIo& p, size_t m) {
+    if (p.cap >= m && p.p) return MPX_OK;
+    if (p.p) (void)hipHostFree(p.p);
+    p.p = nullptr;
+    p.cap = 0;
+    const size_t cap = m < 1024 ? 1024 : m;
+    void* hp = nullptr;
+    if (hipHostMalloc(&hp, pin_bytes(cap), hipHostMallocDefault) != hipSuccess || !hp) {
+        (void)hipGetLastError();
+        return fail(e, MPX_E_NOMEM, "pinned staging for the replica-batch apply");
+    }
+    p.p = (uint8_t*)hp;
+    p.cap = cap;
+    return MPX_OK;
+}
+
+// the replica-batch kernels on m commands in pinned staging p, results back in it; returns once
+// the kernels' completion flag is set (the last workgroup stores it after every result is
+// visible to the host): polling it avoids the runtime's stream-wait wake-up latency on a ~13 us
+// call; the stream is queried now and then, so a failed launch or a faulted kernel ends the
+// wait with its error
+int run_pinned(mpx_engine* e, const PinIo& p, size_t m, bool want_conf) {
+    const PinView v = pin_view(p);
+    *v.err = 0u;
+    void* dp = nullptr;
+    HIPCHK(e, hipHostGetDevicePointer(&dp, p.p, 0));
+    const PinView d = pin_view_at((uint8_t*)dp, p.cap);
+    uint32_t seq = ++e->small_seq;
+    if (!seq) seq = e->small_seq = 1;  // 0 never marks a finished call
+    HIPCHK(e, mpx::launch_apply_small(e->kv, d.op, d.key, d.val, m, d.ret,
+                                      want_conf ? d.conf : nullptr, (uint32_t*)d.err, e->stream,
+                                      (uint32_t*)d.done, seq));
+    for (uint64_t it = 1; *v.done != seq; ++it) {
+        if ((it & 1023) == 0) {
+            const hipError_t q = hipStreamQuery(e->stream);
+            if (q == hipSuccess) {
+                if (*v.done == seq) break;
+                return fail(e, MPX_E_HIP, "mpx_apply: the call ended without its completion flag");
+            }
+            if (q != hipErrorNotReady) return hip_fail(e, "mpx_apply", q);
+        }
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+    }
+    return check_errword(e, *v.err);
+}
+
 }  // namespace
 
 extern "C" {
@@ -267,7 +346,8 @@ int mpx_close(mpx_engine* e) {
     for (auto& x : e->b)
         if (x.p) (void)hipFree(x.p);
     if (e->apply_work.p) (void)hipFree(e->apply_work.p);
-    if (e->pin) (void)hipHostFree(e->pin);
+    if (e->pin_io.p) (void)hipHostFree(e->pin_io.p);
+    if (e->pin_staged.p) (void)hipHostFree(e->pin_staged.p);
     for (auto& x : e->dec)
         if (x.p) (void)hipFree(x.p);
     if (e->decode_work.p) (void)hipFree(e->decode_work.p);
@@ -465,63 +545,18 @@ int mpx_apply(mpx_engine* e, const uint8_t* op, const int64_t* key, const int64_
         // one drained executeCommands batch: the commands go into pinned host memory the kernels
         // read over the link, the results and the call's error word come back the same way (no
         // DMA, no memset, no copy of the error word: the host clears and reads it in place); a
-        // CPU copy on each side
+        // CPU copy on each side (mpx_apply_staged: none)
         HIPCHK(e, hipSetDevice(e->device));
         CK(ensure_kv(e));
-        constexpr size_t kHdr = 128;  // the error word and the completion flag, a line each
-        const size_t a16 = (m + 15) & ~(size_t)15, need = kHdr + a16 * 2 + m * 24;
-        if (e->pin_cap < need) {
-            if (e->pin) (void)hipHostFree(e->pin);
-            e->pin = nullptr;
-            e->pin_cap = 0;
-            void* hp = nullptr;
-            if (hipHostMalloc(&hp, need, hipHostMallocDefault) != hipSuccess || !hp)
-                return fail(e, MPX_E_NOMEM, "pinned staging for mpx_apply");
-            e->pin = (uint8_t*)hp;
-            e->pin_cap = need;
-        }
-        volatile uint32_t* h_err = (volatile uint32_t*)e->pin;
-        volatile uint32_t* h_done = (volatile uint32_t*)(e->pin + 64);
-        uint8_t* h_op = e->pin + kHdr;
-        int64_t* h_key = (int64_t*)(h_op + a16);
-        int64_t* h_val = h_key + m;
-        int64_t* h_ret = h_val + m;
-        uint8_t* h_conf = (uint8_t*)(h_ret + m);
-        *h_err = 0u;
-        std::memcpy(h_op, op, m);
-        std::memcpy(h_key, key, m * 8);
-        std::memcpy(h_val, val, m * 8);
-        void* dp = nullptr;
-        HIPCHK(e, hipHostGetDevicePointer(&dp, e->pin, 0));
-        uint8_t* d0 = (uint8_t*)dp + kHdr;
-        uint32_t seq = ++e->small_seq;
-        if (!seq) seq = e->small_seq = 1;  // 0 never marks a finished call
-        HIPCHK(e, mpx::launch_apply_small(e->kv, d0, (const int64_t*)(d0 + a16),
-                                          (const int64_t*)(d0 + a16) + m, m,
-                                          (int64_t*)(d0 + a16) + 2 * m,
-                                          conf_prev ? d0 + a16 + m * 24 : nullptr,
-                                          (uint32_t*)dp, e->stream,
-                                          (uint32_t*)((uint8_t*)dp + 64), seq));
-        // the last workgroup stores seq once every result is visible here: poll it (a stream
-        // wait adds the runtime's wake-up latency to a ~13 us call); the stream is queried now
-        // and then, so a failed launch or a faulted kernel ends the wait with its error
-        for (uint64_t it = 1; *h_done != seq; ++it) {
-            if ((it & 1023) == 0) {
-                const hipError_t q = hipStreamQuery(e->stream);
-                if (q == hipSuccess) {
-                    if (*h_done == seq) break;
-                    return fail(e, MPX_E_HIP, "mpx_apply: the call ended without its completion flag");
-                }
-                if (q != hipErrorNotReady) return hip_fail(e, "mpx_apply", q);
-            }
-#if defined(__x86_64__)
-            __builtin_ia32_pause();
-#endif
-        }
-        const uint32_t werr = *h_err;
-        std::memcpy(ret, h_ret, m * 8);
-        if (conf_prev) std::memcpy(conf_prev, h_conf, m);
-        return check_errword(e, werr);
+        CK(pin_grow(e, e->pin_io, m));
+        const PinView v = pin_view(e->pin_io);
+        std::memcpy(v.op, op, m);
+        std::memcpy(v.key, key, m * 8);
+        std::memcpy(v.val, val, m * 8);
+        const int rc = run_pinned(e, e->pin_io, m, conf_prev != nullptr);
+        std::memcpy(ret, v.ret, m * 8);
+        if (conf_prev) std::memcpy(conf_prev, v.conf, m);
+        return rc;
     }
     CK(begin(e));
     CK(ensure_kv(e));
@@ -542,6 +577,38 @@ int mpx_apply(mpx_engine* e, const uint8_t* op, const int64_t* key, const int64_
     CK(d2h(e, ret, e->b[10].p, m * 8));
     if (conf_prev) CK(d2h(e, conf_prev, d_conf, m));
     return finish(e);
+}
+
+int mpx_apply_buffers(mpx_engine* e, size_t max_m, mpx_apply_io* io) {
+    if (!e) return MPX_E_INVAL;
+    if (!io) return fail(e, MPX_E_INVAL, "null io");
+    if (!max_m || max_m > MPX_APPLY_SMALL_MAX)
+        return fail(e, MPX_E_INVAL, "max_m must lie in [1, MPX_APPLY_SMALL_MAX]");
+    if (!mpx::apply_is_one_launch(e->apply, max_m))
+        return fail(e, MPX_E_INVAL, "the staged apply needs apply_path AUTO or SMALL");
+    HIPCHK(e, hipSetDevice(e->device));
+    CK(ensure_kv(e));
+    if (e->pin_staged.cap < max_m) {
+        HIPCHK(e, hipStreamSynchronize(e->stream));  // (no call may still use the old buffers)
+        CK(pin_grow(e, e->pin_staged, max_m));
+    }
+    const PinView v = pin_view(e->pin_staged);
+    io->op = v.op;
+    io->key = v.key;
+    io->val = v.val;
+    io->ret = v.ret;
+    io->conf = v.conf;
+    io->cap = e->pin_staged.cap;
+    return MPX_OK;
+}
+
+int mpx_apply_staged(mpx_engine* e, size_t m) {
+    if (!e) return MPX_E_INVAL;
+    if (!m) return MPX_OK;
+    if (!e->pin_staged.p || m > e->pin_staged.cap)
+        return fail(e, MPX_E_INVAL, "m exceeds the buffers of mpx_apply_buffers");
+    HIPCHK(e, hipSetDevice(e->device));
+    return run_pinned(e, e->pin_staged, m, true);
 }
 
 int mpx_apply_reserve(mpx_engine* e, size_t max_cmds) {

@@ -42,13 +42,26 @@ __global__ __launch_bounds__(kTileBlock) void k_prepare_tile(
     const int4* r4 = reinterpret_cast<const int4*>(recs);
     const int4* s4 = reinterpret_cast<const int4*>(st_in);
     int4* o4 = reinterpret_cast<int4*>(st_out);
-    tile_walk(S, r4, n, err, [&](uint32_t a, uint32_t cnt, uint64_t after, uint64_t oend, bool own,
-                                 int64_t nxt, bool first) {
+    int64_t spec_idx = -1;  // the state loaded ahead for round 0 (tile_walk's pre)
+    int4 specA = make_int4(0, 0, 0, 0), specB = make_int4(0, 0, 0, 0);
+    auto pre = [&](int32_t inst0) {
+        spec_idx = (int64_t)inst0 - base + t;
+        if (spec_idx >= 0 && (uint64_t)spec_idx < n_inst) {
+            specA = ld_stream(s4 + 2 * spec_idx);
+            specB = ld_stream(s4 + 2 * spec_idx + 1);
+        }
+    };
+    tile_walk(S, r4, n, err, pre, [&](uint32_t a, uint32_t cnt, uint64_t after, uint64_t oend,
+                                      bool own, int64_t nxt, bool first) {
         const int32_t inst = own ? S.rec[a].x : 0;
         const int64_t idx = (int64_t)inst - base;
         const bool inwin = own && idx >= 0 && (uint64_t)idx < n_inst;
-        int4 A = inwin ? ld_stream(s4 + 2 * idx) : make_int4(0, MPX_STATUS_NIL, 0, 0);      // ballot status oks nacks
-        int4 B = inwin ? ld_stream(s4 + 2 * idx + 1) : make_int4(0, 0, 0, 0);              // mx value_id flags pad
+        const bool hit = idx == spec_idx;
+        spec_idx = -1;  // (later rounds of the tile load their own)
+        int4 A = inwin ? (hit ? specA : ld_stream(s4 + 2 * idx))
+                       : make_int4(0, MPX_STATUS_NIL, 0, 0);  // ballot status oks nacks
+        int4 B = inwin ? (hit ? specB : ld_stream(s4 + 2 * idx + 1))
+                       : make_int4(0, 0, 0, 0);  // mx value_id flags pad
         const bool live_inst = inwin && A.y != MPX_STATUS_NIL;
         ebits |= (own && !live_inst) ? kErrNil : 0u;
         // per-call event flags describe this call (the head record clears them)

@@ -49,13 +49,21 @@ __global__ MPX_TALLY_ATTR __launch_bounds__(kTileBlock) void k_accept_tile(
     const int64_t j0 = MODE == MPX_MODE_CLASSIC ? (int64_t)scalars[0] + 1 - base : 0;
     uint32_t fb_key = 0;  // ~(first non-committed instance >= j0) seen by this lane, 0 = none
     const int4* r4 = reinterpret_cast<const int4*>(recs);
-    tile_walk(S, r4, n, err, [&](uint32_t a, uint32_t cnt, uint64_t after, uint64_t oend, bool own,
-                                 int64_t nxt, bool first) {
+    const int4* s4 = reinterpret_cast<const int4*>(st_in);
+    int64_t spec_idx = -1;  // the state loaded ahead for round 0 (tile_walk's pre)
+    int4 spec = make_int4(0, 0, 0, 0);
+    auto pre = [&](int32_t inst0) {
+        spec_idx = (int64_t)inst0 - base + t;
+        if (spec_idx >= 0 && (uint64_t)spec_idx < n_inst) spec = ld_stream(s4 + spec_idx);
+    };
+    tile_walk(S, r4, n, err, pre, [&](uint32_t a, uint32_t cnt, uint64_t after, uint64_t oend,
+                                      bool own, int64_t nxt, bool first) {
         const int32_t inst = own ? S.rec[a].x : 0;
         const int64_t idx = (int64_t)inst - base;
         const bool inwin = own && idx >= 0 && (uint64_t)idx < n_inst;
-        int4 st = inwin ? ld_stream(reinterpret_cast<const int4*>(st_in) + idx)
+        int4 st = inwin ? (idx == spec_idx ? spec : ld_stream(s4 + idx))
                         : make_int4(MPX_STATUS_NIL, 0, 0, 0);
+        spec_idx = -1;  // (later rounds of the tile load their own)
         const bool nil = st.x == MPX_STATUS_NIL;
         ebits |= (own && !inwin) ? kErrNil : 0u;  // outside instanceSpace
         if (MODE == MPX_MODE_CLASSIC) ebits |= (own && nil) ? kErrNil : 0u;  // paxos.go:634

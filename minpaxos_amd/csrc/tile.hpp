@@ -47,9 +47,13 @@ __device__ __forceinline__ int4 tile_load(const int4* __restrict__ recs, uint64_
 // (tile_gaps). Every lane of the workgroup calls `body` the same number of times per tile
 // (rounds of 256 instances; lanes without an instance in a round get count = 0), so `body` may
 // use wave-level ballots. `err` receives kErrOrder when instances are not ascending.
-template <typename Body>
+// pre(inst0), called by every thread as soon as a tile is in LDS (inst0 = the instance of its
+// first record), lets the caller issue the loads of the per-instance state its lanes will most
+// likely own in round 0 (instance inst0 + lane, when the tile's instances are dense) while the
+// tile's heads are found: the state load is otherwise a dependent round trip after two barriers.
+template <typename Pre, typename Body>
 __device__ __forceinline__ void tile_walk(TileLds& S, const int4* __restrict__ recs, uint64_t n,
-                                          uint32_t* err, Body&& body) {
+                                          uint32_t* err, Pre&& pre, Body&& body) {
     const int t = threadIdx.x, l = lane_id(), w = t / kWave;
     const uint64_t n_tiles = (n + kTileRecs - 1) / kTileRecs;
     const unsigned long long below = (1ull << l) - 1ull;
@@ -75,6 +79,7 @@ __device__ __forceinline__ void tile_walk(TileLds& S, const int4* __restrict__ r
             cur[k] = Tn < n_tiles ? tile_load(recs, n, Tn * kTileRecs + t + k * kTileBlock)
                                   : make_int4(0, 0, 0, 0);
         __syncthreads();
+        pre(S.rec[0].x);
         bool head[kTilePer];
 #pragma unroll
         for (int k = 0; k < kTilePer; ++k) {

@@ -162,6 +162,22 @@ class Engine:
         self._check(rc, "mpx_prepare_select_min_dev")
 
     # ---- A5 / A6 ----------------------------------------------------------------------------
+    def apply_buffers(self, max_m):
+        """mpx_apply_buffers: numpy views of the engine's pinned op / key / val / ret / conf
+        arrays (valid until they grow or the engine closes) for mpx_apply_staged"""
+        io = _lib.MpxApplyIo()
+        self._check(self.lib.mpx_apply_buffers(self.h, max_m, C.byref(io)), "mpx_apply_buffers")
+
+        def view(ptr, ct, dt):
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), shape=(io.cap,)).view(dt)
+        return {"op": view(io.op, C.c_uint8, np.uint8), "key": view(io.key, C.c_int64, np.int64),
+                "val": view(io.val, C.c_int64, np.int64), "ret": view(io.ret, C.c_int64, np.int64),
+                "conf": view(io.conf, C.c_uint8, np.uint8), "cap": int(io.cap)}
+
+    def apply_staged(self, m):
+        """mpx_apply_staged: apply the first m commands of the apply_buffers arrays"""
+        self._check(self.lib.mpx_apply_staged(self.h, m), "mpx_apply_staged")
+
     def apply(self, op, key, val, want_conf=True):
         op = _c(op, np.uint8)
         key = _c(key, np.int64)

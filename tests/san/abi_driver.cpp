@@ -84,6 +84,13 @@ int main() {
     FAILS(e, mpx_apply(e, op.data(), nullptr, val.data(), m, ret.data(), nullptr), MPX_E_INVAL);
     FAILS(e, mpx_apply_dev(e, op.data(), key.data(), val.data(), 1u << 20, ret.data(), nullptr, nullptr), MPX_E_INVAL);
     CHECK(mpx_apply_reserve(e, m) == MPX_OK);
+    mpx_apply_io aio{};
+    CHECK(mpx_apply_buffers(e, m, &aio) == MPX_OK && aio.cap >= m && aio.op && aio.conf);
+    for (size_t i = 0; i < m; ++i) aio.op[i] = op[i], aio.key[i] = key[i], aio.val[i] = val[i];
+    CHECK(mpx_apply_staged(e, m) == MPX_OK);
+    FAILS(e, mpx_apply_staged(e, aio.cap + 1), MPX_E_INVAL);
+    FAILS(e, mpx_apply_buffers(e, 0, &aio), MPX_E_INVAL);
+    FAILS(e, mpx_apply_buffers(e, MPX_APPLY_SMALL_MAX + 1, &aio), MPX_E_INVAL);
     size_t nk = 9;
     CHECK(mpx_kv_size(e, &nk) == MPX_OK);
     int64_t kk[4], kv[4];

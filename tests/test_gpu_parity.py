@@ -332,6 +332,31 @@ def test_apply_small_calls(mk_engine, path):
         assert np.array_equal(ar.get(d_ret), wr) and np.array_equal(ar.get(d_conf), wc)
 
 
+def test_apply_staged(mk_engine):
+    """the zero-copy replica-batch form (mpx_apply_buffers + mpx_apply_staged): batches written
+    straight into the engine's pinned arrays, mixed with host-pointer calls on the same table,
+    every call and the final table bit-exact; sizes past the arrays are rejected"""
+    rng = np.random.default_rng(94)
+    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 16), Oracle(5, R.MODE_MIN)
+    io = e.apply_buffers(6000)
+    assert io["cap"] >= 6000
+    for i, m in enumerate([5000, 1, 6000, 4096, 333]):
+        op, key, val = gen_cases.commands_mixed(rng, m, 700 + 13 * i)
+        if i % 2:
+            gr, gc = e.apply(op, key, val)
+        else:
+            io["op"][:m], io["key"][:m], io["val"][:m] = op, key, val
+            e.apply_staged(m)
+            gr, gc = io["ret"][:m].copy(), io["conf"][:m].copy()
+        wr, wc = o.apply(op, key, val)
+        assert np.array_equal(gr, wr) and np.array_equal(gc, wc), m
+    gk, gv = e.kv_export()
+    wk, wv = o.kv_export()
+    assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
+    with pytest.raises(MpxError):
+        e.apply_staged(io["cap"] + 1)
+
+
 def test_apply_small_then_pipelines(mk_engine):
     """the one-launch kernel neither reads nor advances the call epoch: calls on it between
     calls of the partitioned and sorted pipelines (which tag slots with the epoch) leave
