@@ -113,10 +113,10 @@ def parse():
     ap.add_argument("--kv-capacity", type=int, default=0,
                     help="apply: engine key capacity (0 = --apply-keys; the table gets >= 2x slots, load <= 1/2)")
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
-    ap.add_argument("--fused-totals", action="store_true",
-                    help="step: the totals from the step kernels (mpx_group_step_totals_dev) "
-                         "instead of their own launch after the group step (A/B: the fast "
-                         "kernel's per-group atomics cost about what the launch saves)")
+    ap.add_argument("--separate-totals", action="store_true",
+                    help="step: the totals by their own launch after the group step "
+                         "(mpx_step_totals_dev) instead of the step's work-list kernel "
+                         "(mpx_group_step_totals_dev, the default: two launches per step)")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="step: one process measures the share of ONE rank of a P-rank job (P = "
                          "this value): it owns groups [0, G_total/P) of the job's G_total, the "
@@ -413,13 +413,13 @@ def step_bench(a, rk):
         if timed:
             eng.event_record(ev_k[i][0], comp)
         # the group step, then its totals (decided, executed instances, executed commands)
-        if a.fused_totals:
+        if not a.separate_totals:
             eng.group_step_totals_dev(steps[buf], d["tot"][buf].ptr, comp)
         else:
             eng.group_step_dev(steps[buf], comp)
         if timed:
             eng.event_record(ev_k[i][1], comp)
-        if not a.fused_totals:
+        if a.separate_totals:
             eng.step_totals_dev(steps[buf], d["tot"][buf].ptr, comp)
         eng.event_record(ev_done[buf], comp)
         eng.stream_wait_event(comm, ev_done[buf])

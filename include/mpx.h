@@ -382,9 +382,9 @@ int mpx_group_step_dev(mpx_engine* eng, const mpx_group_batch* b, void* stream);
 #define MPX_STEP_TOTALS 3
 int mpx_step_totals_dev(mpx_engine* eng, const mpx_group_batch* b, int64_t* d_totals,
                         void* stream);
-/* mpx_group_step_dev and mpx_step_totals_dev in one: the step kernels accumulate the totals
- * as they finish each group and write d_totals[0..2] (same values) at their end, so a step is
- * two kernel launches instead of three (b->n_decided optional here).                       */
+/* mpx_group_step_dev and mpx_step_totals_dev in one (b->n_decided required): the second
+ * kernel of the step (the work-list kernel) also reduces the groups' outputs to d_totals[0..2]
+ * (same values), so a step is two kernel launches instead of three.                       */
 int mpx_group_step_totals_dev(mpx_engine* eng, const mpx_group_batch* b, int64_t* d_totals,
                               void* stream);
 

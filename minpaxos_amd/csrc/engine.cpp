@@ -755,6 +755,8 @@ int mpx_group_step_totals_dev(mpx_engine* e, const mpx_group_batch* b, int64_t* 
                               void* stream) {
     if (!e) return MPX_E_INVAL;
     if (!d_totals) return fail(e, MPX_E_INVAL, "null d_totals");
+    if (b && b->n_groups && !b->n_decided)
+        return fail(e, MPX_E_INVAL, "mpx_group_step_totals_dev needs n_decided");
     return group_step_dev(e, b, d_totals, stream);
 }
 

@@ -832,17 +832,6 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
         b.executed_out[g] = stop > lo ? (int32_t)(stop - 1) : ex_in;
         b.kv_cnt_out[g] = total < kvpg ? total : kvpg;
         if (b.n_decided) b.n_decided[g] = S.ndec;
-        if (tacc) {  // the step totals' partials (no-return atomics: the next kernel reads them)
-            unsigned long long* a = tacc + (g % kTotSlots) * 3;
-            const unsigned long long xi = stop > lo ? (unsigned long long)(stop - lo) : 0ull;
-            if (S.ndec) __hip_atomic_fetch_add(a, (unsigned long long)S.ndec, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-            if (xi) {
-                __hip_atomic_fetch_add(a + 1, xi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_fetch_add(a + 2, (unsigned long long)(x1 - x0), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
     }
     ebits &= 0x7FFFFFFFu;
     if (ebits) raise_err(err, ebits);
@@ -918,7 +907,7 @@ __device__ void group_general(GenLds& S, const mpx_group_batch& b, uint32_t g, i
     if (b.decided)
         for (uint64_t i = t; i < ipg; i += kStepBlock)
             b.decided[gi0 + i] = (S.dec_bits[i >> 5] >> (i & 31)) & 1u;
-    if (b.n_decided || tacc) {  // popcount of the decided bitmap (bits past ipg stay 0)
+    if (b.n_decided) {  // popcount of the decided bitmap (bits past ipg stay 0)
         uint32_t c = 0;
         for (uint64_t i = t; i < (ipg + 31) / 32; i += kStepBlock) c += __popc(S.dec_bits[i]);
         if (c) atomicAdd(&S.ndec, c);
@@ -979,15 +968,6 @@ __device__ void group_general(GenLds& S, const mpx_group_batch& b, uint32_t g, i
     if (t == 0) {
         b.executed_out[g] = stop > lo ? (int32_t)(stop - 1) : ex_in;
         if (b.n_decided) b.n_decided[g] = S.ndec;
-        if (tacc) {  // partials, performed before the workgroup takes its ticket
-            unsigned long long* a = tacc + (g % kTotSlots) * 3;
-            if (S.ndec) atomic_add_done(a, (unsigned long long)S.ndec);
-            if (stop > lo) {
-                atomic_add_done(a + 1, (unsigned long long)(stop - lo));
-                atomic_add_done(a + 2, (unsigned long long)(b.cmd_off[gi0 + stop] -
-                                                            b.cmd_off[gi0 + lo]));
-            }
-        }
     }
 
     const Dict D{S.dkey, S.dval, S.dfirst, S.cnt, S.hslot, S.dpresent, S.dseen, &S.dn,
@@ -1066,34 +1046,133 @@ __device__ void group_general(GenLds& S, const mpx_group_batch& b, uint32_t g, i
     if (t == 0) b.kv_cnt_out[g] = S.scal[0] < kvpg ? S.scal[0] : kvpg;
 }
 
+// the step totals of group g from its outputs: decided instances, executed instances (the
+// executeCommands iterations), executed commands
+__device__ __forceinline__ void group_totals(const mpx_group_batch& b, uint32_t g,
+                                             unsigned long long& d, unsigned long long& xi,
+                                             unsigned long long& xc) {
+    d = b.n_decided[g];
+    const int64_t ei = b.executed_in[g], eo = b.executed_out[g];
+    const int64_t lo = ei + 1 < 0 ? 0 : ei + 1;
+    xi = xc = 0;
+    if (eo >= lo && eo < (int64_t)b.ipg) {
+        const uint64_t gi0 = (uint64_t)g * b.ipg;
+        xi = (unsigned long long)(eo - lo + 1);
+        xc = b.cmd_off[gi0 + eo + 1] - b.cmd_off[gi0 + lo];
+    }
+}
+
+// (d, xi, xc) summed over the workgroup, valid in thread 0
+__device__ __forceinline__ void block_sum3(unsigned long long& d, unsigned long long& xi,
+                                           unsigned long long& xc) {
+    __shared__ unsigned long long red3[3][kStepBlock / kWave];
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) {
+        d += __shfl_xor(d, k);
+        xi += __shfl_xor(xi, k);
+        xc += __shfl_xor(xc, k);
+    }
+    const int w = threadIdx.x / kWave;
+    if (lane_id() == 0) {
+        red3[0][w] = d;
+        red3[1][w] = xi;
+        red3[2][w] = xc;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        d = xi = xc = 0;
+        for (int k = 0; k < kStepBlock / kWave; ++k) {
+            d += red3[0][k];
+            xi += red3[1][k];
+            xc += red3[2][k];
+        }
+    }
+    __syncthreads();
+}
+
+// Groups per totals workgroup when the work list is empty (the common case)
+constexpr uint32_t kTotGroupsPerWg = 2048;
+
+// The work list, and (totals != nullptr) the step totals, so a step with totals is two launches.
+// Empty work list (the common case): no workgroup touches a control word but the first
+// ceil(G / kTotGroupsPerWg), which reduce the totals of their slice of groups from the fast
+// kernel's outputs (a previous kernel), add them with awaited atomics and take a ticket; the
+// last writes the totals and zeroes the accumulators. Otherwise the workgroups with list entries
+// run them, release their outputs (agent-scope fence) and take a ticket among themselves; the
+// last zeroes the list count and, for the totals, acquires and reduces every group itself (a
+// step with spilled groups is rare; its totals need every group's final outputs).
 template <int MODE>
 __global__ __launch_bounds__(kStepBlock) void k_group_general(mpx_group_batch b, int32_t nrep,
                                                               uint32_t kvpg,
                                                               const uint32_t* worklist,
                                                               uint32_t* wcount,
-                                                              unsigned long long* tacc,
                                                               int64_t* totals, uint32_t* err) {
     __shared__ GenLds S;
+    __shared__ bool last;
+    unsigned long long* acc = reinterpret_cast<unsigned long long*>(wcount + 4);
     const uint32_t n = *wcount;
+    if (n == 0) {
+        if (!totals) return;
+        const uint32_t tw = (b.n_groups + kTotGroupsPerWg - 1) / kTotGroupsPerWg;
+        if (blockIdx.x >= tw) return;
+        unsigned long long d = 0, xi = 0, xc = 0;
+        const uint32_t g1 = b.n_groups < (blockIdx.x + 1) * kTotGroupsPerWg
+                                ? b.n_groups
+                                : (blockIdx.x + 1) * kTotGroupsPerWg;
+        for (uint32_t g = blockIdx.x * kTotGroupsPerWg + threadIdx.x; g < g1; g += kStepBlock) {
+            unsigned long long a0, a1, a2;
+            group_totals(b, g, a0, a1, a2);
+            d += a0;
+            xi += a1;
+            xc += a2;
+        }
+        block_sum3(d, xi, xc);
+        if (threadIdx.x == 0) {
+            if (d) atomic_add_done(acc, d);
+            if (xi) atomic_add_done(acc + 1, xi);
+            if (xc) atomic_add_done(acc + 2, xc);
+            const uint32_t k = __hip_atomic_fetch_add(wcount + 10, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            if (k == tw - 1) {
+                (void)atomic_take(wcount + 10);
+                for (int q = 0; q < 3; ++q) totals[q] = (int64_t)atomic_take(acc + q);
+            }
+        }
+        return;
+    }
+    const uint32_t workers = n < gridDim.x ? n : gridDim.x;
+    if (blockIdx.x >= workers) return;
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        group_general<MODE>(S, b, worklist[i], nrep, kvpg, tacc, err);
+        group_general<MODE>(S, b, worklist[i], nrep, kvpg, nullptr, err);
         __syncthreads();
     }
-    // the last workgroup to finish (every one has read the count and performed its partials)
-    // zeroes the count for the next step and folds the totals' partials
+    if (totals) __threadfence();  // this workgroup's group outputs, before its ticket
+    __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t k = __hip_atomic_fetch_add(wcount + 1, 1u, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
-        if (k == gridDim.x - 1) {
+        last = k == workers - 1;
+        if (last) {
             wcount[0] = 0;
             wcount[1] = 0;
-            if (tacc) {
-                unsigned long long s[3] = {0ull, 0ull, 0ull};
-                for (int q = 0; q < kTotSlots; ++q)
-                    for (int i = 0; i < 3; ++i) s[i] += atomic_take(tacc + q * 3 + i);
-                for (int i = 0; i < 3; ++i) totals[i] = (int64_t)s[i];
-            }
         }
+    }
+    __syncthreads();
+    if (!last || !totals) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    unsigned long long d = 0, xi = 0, xc = 0;
+    for (uint32_t g = threadIdx.x; g < b.n_groups; g += kStepBlock) {
+        unsigned long long a0, a1, a2;
+        group_totals(b, g, a0, a1, a2);
+        d += a0;
+        xi += a1;
+        xc += a2;
+    }
+    block_sum3(d, xi, xc);
+    if (threadIdx.x == 0) {
+        totals[0] = (int64_t)d;
+        totals[1] = (int64_t)xi;
+        totals[2] = (int64_t)xc;
     }
 }
 
@@ -1123,8 +1202,7 @@ int fast_variant(int32_t nrep, uint32_t ipg, uint32_t kvpg) {
 template <int MODE>
 void launch_step(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t* worklist,
                  uint32_t* wcount, int64_t* totals, uint32_t* err, hipStream_t stream) {
-    unsigned long long* tacc =
-        totals ? reinterpret_cast<unsigned long long*>(wcount + 16) : nullptr;
+    unsigned long long* const tacc = nullptr;  // (the totals come from the general kernel)
     switch (fast_variant(nrep, b->ipg, kvpg)) {
     case 1: launch_fast<MODE, FastBase>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
     case 2: launch_fast<MODE, FastRecs>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
@@ -1137,7 +1215,7 @@ void launch_step(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t
     }
     const unsigned gen_grid = b->n_groups < 256 ? b->n_groups : 256;  // one per CU (LDS)
     k_group_general<MODE><<<gen_grid ? gen_grid : 1, kStepBlock, 0, stream>>>(
-        *b, nrep, kvpg, worklist, wcount, tacc, totals, err);
+        *b, nrep, kvpg, worklist, wcount, totals, err);
 }
 }  // namespace
 
@@ -1165,16 +1243,7 @@ __global__ __launch_bounds__(256) void k_step_totals(mpx_group_batch b, unsigned
     __shared__ unsigned long long red[3][kStepBlock / kWave];
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long d = 0, xi = 0, xc = 0;
-    if (g < b.n_groups) {
-        d = b.n_decided[g];
-        const int64_t ei = b.executed_in[g], eo = b.executed_out[g];
-        const int64_t lo = ei + 1 < 0 ? 0 : ei + 1;
-        if (eo >= lo && eo < (int64_t)b.ipg) {
-            const uint64_t gi0 = (uint64_t)g * b.ipg;
-            xi = (unsigned long long)(eo - lo + 1);
-            xc = b.cmd_off[gi0 + eo + 1] - b.cmd_off[gi0 + lo];
-        }
-    }
+    if (g < b.n_groups) group_totals(b, g, d, xi, xc);
 #pragma unroll
     for (int k = 32; k >= 1; k >>= 1) {
         d += __shfl_xor(d, k);

@@ -745,10 +745,11 @@ def _want_totals(b, want):
 
 @pytest.mark.parametrize("kind", ["fast", "general"])
 def test_group_step_fused_totals(mk_engine, kind):
-    """mpx_group_step_totals_dev: the step totals accumulated by the step kernels (fast-path
-    groups with no-return atomics, work-list groups in the general kernel, folded by its last
-    workgroup) equal the oracle's and mpx_step_totals_dev's, with and without n_decided, over
-    repeated steps (the partials reset themselves) and after a plain mpx_group_step_dev"""
+    """mpx_group_step_totals_dev: the step totals reduced by the step's second kernel (an empty
+    work list: slices of the fast kernel's outputs; a full one: its last workgroup over every
+    group) equal the oracle's and mpx_step_totals_dev's over repeated steps (the accumulators
+    and tickets reset themselves) and after a plain mpx_group_step_dev; without n_decided the
+    call is rejected"""
     from minpaxos_amd.devbuf import Arena
     if kind == "fast":
         N, K = 5, 256
@@ -764,6 +765,10 @@ def test_group_step_fused_totals(mk_engine, kind):
             gb, d = _dev_group_batch(ar, b, N, K, with_nd)
             tot = ar.full(3, np.int64, 0x55)
             e.group_step_dev(gb, e.stream)  # leaves no partials behind
+            if not with_nd:
+                with pytest.raises(MpxError):
+                    e.group_step_totals_dev(gb, tot.ptr, e.stream)
+                continue
             for _ in range(3):
                 e.group_step_totals_dev(gb, tot.ptr, e.stream)
                 e.stream_synchronize(e.stream)
