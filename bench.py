@@ -242,25 +242,41 @@ def instr_for(key, path=""):
 
 
 def issue_roofline(kernel, key, kern_ms, hbm, path=""):
-    """the roofline object of a row bound by instruction issue: VALU (and LDS) wave-instructions
-    per launch from the counter database / the call's kernel time, against the issue peaks; the
-    HBM figures stay beside it under "hbm". The bound is whichever fraction is higher; without a
-    counter pass it stays "valu" (measured bound) with achieved null."""
+    """the roofline object of a row not bound by HBM bandwidth: VALU and LDS wave-instructions
+    per launch (counter database) against the issue peaks, and the SQ wave-cycle split (parked
+    at s_waitcnt / barriers, issue-stalled, issuing: MI355X_MICROARCH.md, the three are disjoint
+    and sum to SQ_WAVE_CYCLES). bound = "valu" / "lds" when that issue fraction is at least 0.5,
+    else "latency" when the waves are parked for most of their cycles (the HBM figures then carry
+    the row: achieved / peak / frac are its HBM numbers), else "issue-stall". Without a counter
+    pass the bound stays "valu"  with achieved null."""
     ins = instr_for(key, path) or {}
     t = kern_ms * 1e-3
     valu, lds = ins.get("SQ_INSTS_VALU"), ins.get("SQ_INSTS_LDS")
     fv = valu / t / 1e9 / PEAK_VALU_GIPS if valu else None
     fl = lds / t / 1e9 / PEAK_LDS_GIPS if lds else None
+    wc = ins.get("SQ_WAVE_CYCLES")
+    waits = {k: ins[k] / wc for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")
+             if wc and k in ins}
     use_lds = fl is not None and (fv is None or fl > fv)
-    return {"bound": "lds" if use_lds else "valu", "kernel": kernel,
-            "achieved": (lds if use_lds else valu) / t / 1e9 if (valu or lds) else None,
-            "peak": PEAK_LDS_GIPS if use_lds else PEAK_VALU_GIPS, "unit": "G wave-instr/s",
-            "frac": fl if use_lds else fv, "valu_frac": fv, "lds_frac": fl,
-            "valu_instr_per_launch": valu, "lds_instr_per_launch": lds,
-            "instr_note": "SQ_INSTS_VALU / SQ_INSTS_LDS rocprofv3 passes (tools/pmc_collect.py "
-                          "--instr) of this exact configuration" if ins else
-                          "no instruction-counter pass for this exact configuration",
-            "hbm": hbm}
+    top = max(x for x in (fv, fl, 0.0) if x is not None)
+    out = {"kernel": kernel, "valu_frac": fv, "lds_frac": fl,
+           "valu_instr_per_launch": valu, "lds_instr_per_launch": lds,
+           "wave_cycle_split": waits or None,
+           "instr_note": "SQ_INSTS_VALU / SQ_INSTS_LDS and SQ_WAVE_CYCLES / SQ_WAIT_ANY / "
+                         "SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY rocprofv3 passes "
+                         "(tools/pmc_collect.py --instr) of this exact configuration" if ins else
+                         "no instruction-counter pass for this exact configuration",
+           "hbm": hbm}
+    if top >= 0.5 or not waits:
+        out.update({"bound": "lds" if use_lds else "valu",
+                    "achieved": (lds if use_lds else valu) / t / 1e9 if (valu or lds) else None,
+                    "peak": PEAK_LDS_GIPS if use_lds else PEAK_VALU_GIPS,
+                    "unit": "G wave-instr/s", "frac": fl if use_lds else fv})
+    else:
+        out.update({"bound": "latency" if waits.get("SQ_WAIT_ANY", 0) >= 0.5 else "issue-stall",
+                    "achieved": hbm["achieved"], "peak": hbm["peak"], "unit": hbm["unit"],
+                    "frac": hbm["frac"]})
+    return out
 
 
 def launch_ranks(n):

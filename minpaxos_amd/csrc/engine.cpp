@@ -257,9 +257,16 @@ int run_pinned(mpx_engine* e, const PinIo& p, size_t m, bool want_conf) {
     const PinView d = pin_view_at((uint8_t*)dp, p.cap);
     uint32_t seq = ++e->small_seq;
     if (!seq) seq = e->small_seq = 1;  // 0 never marks a finished call
+#ifndef MPX_SMALL_POLL
+#define MPX_SMALL_POLL 1  // A/B builds: 0 = wait on the stream (no completion flag, no fences)
+#endif
     HIPCHK(e, mpx::launch_apply_small(e->kv, d.op, d.key, d.val, m, d.ret,
                                       want_conf ? d.conf : nullptr, (uint32_t*)d.err, e->stream,
-                                      (uint32_t*)d.done, seq));
+                                      MPX_SMALL_POLL ? (uint32_t*)d.done : nullptr, seq));
+    if (!MPX_SMALL_POLL) {
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        return check_errword(e, *v.err);
+    }
     for (uint64_t it = 1; *v.done != seq; ++it) {
         if ((it & 1023) == 0) {
             const hipError_t q = hipStreamQuery(e->stream);

@@ -1090,8 +1090,10 @@ __device__ __forceinline__ void block_sum3(unsigned long long& d, unsigned long 
     __syncthreads();
 }
 
-// Groups per totals workgroup when the work list is empty (the common case)
-constexpr uint32_t kTotGroupsPerWg = 2048;
+// Groups per thread and per workgroup of the totals when the work list is empty (the common
+// case): a thread's groups have their loads issued together (two dependent rounds in all)
+constexpr uint32_t kTotPer = 4;
+constexpr uint32_t kTotGroupsPerWg = kStepBlock * kTotPer;
 
 // The work list, and (totals != nullptr) the step totals, so a step with totals is two launches.
 // Empty work list (the common case): no workgroup touches a control word but the first
@@ -1116,15 +1118,31 @@ __global__ __launch_bounds__(kStepBlock) void k_group_general(mpx_group_batch b,
         const uint32_t tw = (b.n_groups + kTotGroupsPerWg - 1) / kTotGroupsPerWg;
         if (blockIdx.x >= tw) return;
         unsigned long long d = 0, xi = 0, xc = 0;
-        const uint32_t g1 = b.n_groups < (blockIdx.x + 1) * kTotGroupsPerWg
-                                ? b.n_groups
-                                : (blockIdx.x + 1) * kTotGroupsPerWg;
-        for (uint32_t g = blockIdx.x * kTotGroupsPerWg + threadIdx.x; g < g1; g += kStepBlock) {
-            unsigned long long a0, a1, a2;
-            group_totals(b, g, a0, a1, a2);
-            d += a0;
-            xi += a1;
-            xc += a2;
+        {
+            uint32_t nd[kTotPer];
+            int32_t ei[kTotPer], eo[kTotPer];
+            uint64_t c0[kTotPer], c1[kTotPer];
+#pragma unroll
+            for (uint32_t k = 0; k < kTotPer; ++k) {  // round 1: the group's outputs
+                const uint32_t g = blockIdx.x * kTotGroupsPerWg + k * kStepBlock + threadIdx.x;
+                const bool v = g < b.n_groups;
+                nd[k] = v ? b.n_decided[g] : 0u;
+                ei[k] = v ? b.executed_in[g] : 0;
+                eo[k] = v ? b.executed_out[g] : -1;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kTotPer; ++k) {  // round 2: the executed command range
+                const uint32_t g = blockIdx.x * kTotGroupsPerWg + k * kStepBlock + threadIdx.x;
+                const int64_t lo = ei[k] + 1 < 0 ? 0 : (int64_t)ei[k] + 1;
+                const bool x = g < b.n_groups && eo[k] >= lo && eo[k] < (int32_t)b.ipg;
+                const uint64_t gi0 = (uint64_t)g * b.ipg;
+                c0[k] = x ? b.cmd_off[gi0 + lo] : 0;
+                c1[k] = x ? b.cmd_off[gi0 + eo[k] + 1] : 0;
+                d += nd[k];
+                xi += x ? (unsigned long long)(eo[k] - lo + 1) : 0ull;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kTotPer; ++k) xc += c1[k] - c0[k];
         }
         block_sum3(d, xi, xc);
         if (threadIdx.x == 0) {

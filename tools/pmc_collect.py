@@ -34,7 +34,9 @@ def bench_line(args, extra=()):
 
 
 def pmc_pass(args, counter, d, steps):
-    cmd = ["timeout", "-s", "KILL", "300", "rocprofv3", "--pmc", counter, "--output-format", "csv",
+    # counter: one name, or a comma group collected in one pass (within one pass's limits)
+    cmd = ["timeout", "-s", "KILL", "300", "rocprofv3", "--pmc", *counter.split(","),
+           "--output-format", "csv",
            "-d", d, "-o", "pmc", "--", sys.executable, os.path.join(ROOT, "bench.py"),
            *args.split(), "--no-cpu-baseline", "--steps", str(steps), "--warmup", "1"]
     r = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT)
@@ -47,10 +49,12 @@ def pmc_pass(args, counter, d, steps):
     raise SystemExit(f"no counter csv under {d}")
 
 
-def per_kernel(path, pats):
+def per_kernel(path, pats, counter=None):
     vals = {}
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
+        if counter and r["Counter_Name"] != counter:
+            continue
         if any(p in name for p in pats):
             vals.setdefault(name, []).append(float(r["Counter_Value"]))
     return vals
@@ -62,9 +66,10 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pmc", "traffic.json"))
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--instr", default="",
-                    help="comma list of SQ instruction counters (e.g. SQ_INSTS_VALU,SQ_INSTS_LDS) "
-                         "to add to the entries instead of the FETCH/WRITE passes: per launch, "
-                         "summed over the call's kernels, one --pmc pass each")
+                    help="SQ counters (e.g. SQ_INSTS_VALU,SQ_INSTS_LDS) to add to the entries "
+                         "instead of the FETCH/WRITE passes: per launch, summed over the call's "
+                         "kernels; ',' separates passes, '+' joins counters into one pass "
+                         "(e.g. SQ_WAVE_CYCLES+SQ_WAIT_ANY+SQ_WAIT_INST_ANY)")
     a = ap.parse_args()
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     db = {"entries": []}
@@ -81,12 +86,15 @@ def main():
             ent = old[0] if old else {"key": key, "kernels": pats, "bytes_per_launch": None,
                                       "alg_bytes_per_launch": rf["alg_bytes_per_launch"]}
             ins = ent.setdefault("instr", {})
-            for c in a.instr.split(","):
-                vals = per_kernel(pmc_pass(args, c, os.path.join(d, c), a.steps), pats)
-                tot = 0.0
-                for name, v in vals.items():
-                    tot += statistics.median(v) * max(1, round(len(v) / launches))
-                ins[c] = tot
+            for grp in a.instr.split(","):
+                names = grp.split("+")
+                path = pmc_pass(args, ",".join(names), os.path.join(d, names[0]), a.steps)
+                for c in names:
+                    vals = per_kernel(path, pats, c)
+                    tot = 0.0
+                    for name, v in vals.items():
+                        tot += statistics.median(v) * max(1, round(len(v) / launches))
+                    ins[c] = tot
             ent["instr_source"] = (f"rocprofv3 --pmc passes ({a.instr}) of bench.py {args} "
                                    f"(tools/pmc_collect.py --instr)")
             db["entries"] = [e for e in db["entries"] if e["key"] != key] + [ent]
