@@ -245,10 +245,9 @@ int pin_grow(mpx_engine* e, PinIo& p, size_t m) {
 }
 
 // the replica-batch kernels on m commands in pinned staging p, results back in it; returns once
-// the kernels' completion flag is set (the last workgroup stores it after every result is
-// visible to the host): polling it avoids the runtime's stream-wait wake-up latency on a ~13 us
-// call; the stream is queried now and then, so a failed launch or a faulted kernel ends the
-// wait with its error
+// the stream is done (MPX_SMALL_POLL builds: once the kernels' completion flag is set - the last
+// workgroup stores it after every result is visible to the host - the stream queried now and
+// then, so a failed launch or a faulted kernel ends the wait with its error)
 int run_pinned(mpx_engine* e, const PinIo& p, size_t m, bool want_conf) {
     const PinView v = pin_view(p);
     *v.err = 0u;
@@ -257,8 +256,13 @@ int run_pinned(mpx_engine* e, const PinIo& p, size_t m, bool want_conf) {
     const PinView d = pin_view_at((uint8_t*)dp, p.cap);
     uint32_t seq = ++e->small_seq;
     if (!seq) seq = e->small_seq = 1;  // 0 never marks a finished call
+// MPX_SMALL_POLL=1 (A/B builds): the kernels store a completion flag into the pinned staging
+// after a system-scope release of every result and the host polls it instead of waiting on the
+// stream; same-box A/B (profiles/r04/replica): 40.6-45.0 vs 32.0-37.9 us per 5000-command host
+// call, 30.6-32.7 vs 22.9-23.0 us staged - the per-thread system fences cost more than the
+// stream wait's wake-up, so the default waits on the stream
 #ifndef MPX_SMALL_POLL
-#define MPX_SMALL_POLL 1  // A/B builds: 0 = wait on the stream (no completion flag, no fences)
+#define MPX_SMALL_POLL 0
 #endif
     HIPCHK(e, mpx::launch_apply_small(e->kv, d.op, d.key, d.val, m, d.ret,
                                       want_conf ? d.conf : nullptr, (uint32_t*)d.err, e->stream,
