@@ -66,7 +66,7 @@ from minpaxos_amd import _lib  # noqa: E402
 from minpaxos_amd import records as R  # noqa: E402
 from minpaxos_amd import shard, synth  # noqa: E402
 from minpaxos_amd.devbuf import D2D, Arena, DevArray  # noqa: E402
-from minpaxos_amd.engine import Engine  # noqa: E402
+from minpaxos_amd.engine import Engine, MpxError  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -123,11 +123,13 @@ def parse():
                          "watermark vector stays 2 x G_total through the engine's all-reduce "
                          "(one rank: RCCL's copy); a proxy for the per-rank cost of strong / weak "
                          "scaling, not a multi-GPU measurement")
-    ap.add_argument("--graph", action="store_true",
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="step: after the timed loop, capture the step sequence (group step, "
                          "totals, the RCCL group on the second stream, the double-buffer "
                          "event waits) into hipGraphs of up to 64 steps (mpx_graph_*) and time "
-                         "their replay; value / ms_per_step then come from the replay")
+                         "their replay; value / ms_per_step then come from the replay. auto = "
+                         "on in one process (a one-rank communicator, validated on the GPU "
+                         "box), off across processes (RCCL capture across ranks unvalidated)")
     ap.add_argument("--apply-path", default="auto",
                     choices=["auto", "small", "sorted", "partitioned"],
                     help="apply: mpx_config.apply_path (auto = by call size)")
@@ -196,7 +198,7 @@ def host_cores():
     return max(1, min(n, 16))
 
 
-TRAFFIC_DB = os.path.join(ROOT, "profiles", "traffic_r03.json")
+TRAFFIC_DB = os.path.join(ROOT, "profiles", "traffic_r04.json")
 ISSUE_BOUND = ("decode", "stream", "fanout")
 
 
@@ -257,13 +259,20 @@ def issue_roofline(kernel, key, kern_ms, hbm, path=""):
     wc = ins.get("SQ_WAVE_CYCLES")
     waits = {k: ins[k] / wc for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")
              if wc and k in ins}
+    # mean resident waves per CU over the call's kernels: SQ_WAVE_CYCLES counts quad-cycles
+    # summed over every wave, GRBM_GUI_ACTIVE the busy cycles summed over the 8 XCDs
+    # (MI355X_MICROARCH.md), so waves / CU = 4 x WAVE_CYCLES / (GRBM / 8 x 256 CUs)
+    grbm = ins.get("GRBM_GUI_ACTIVE")
+    if wc and grbm:
+        waits["mean_waves_per_cu"] = wc * 4.0 / (grbm / 8.0 * 256)
     use_lds = fl is not None and (fv is None or fl > fv)
     top = max(x for x in (fv, fl, 0.0) if x is not None)
     out = {"kernel": kernel, "valu_frac": fv, "lds_frac": fl,
            "valu_instr_per_launch": valu, "lds_instr_per_launch": lds,
            "wave_cycle_split": waits or None,
            "instr_note": "SQ_INSTS_VALU / SQ_INSTS_LDS and SQ_WAVE_CYCLES / SQ_WAIT_ANY / "
-                         "SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY rocprofv3 passes "
+                         "SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY (+ GRBM_GUI_ACTIVE for the mean "
+                         "resident waves per CU) rocprofv3 passes "
                          "(tools/pmc_collect.py --instr) of this exact configuration" if ins else
                          "no instruction-counter pass for this exact configuration",
            "hbm": hbm}
@@ -458,7 +467,8 @@ def step_bench(a, rk):
     kern_ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in ev_k[:a.steps]]
     last = (a.steps - 1) & 1
     graph_info = None
-    if a.graph:
+    use_graph = a.graph == "on" or (a.graph == "auto" and world == 1)
+    if use_graph:
         # the same step sequence replayed from hipGraphs: a chunk of U steps is one capture on
         # the compute stream (the second stream joins through ev_done and is joined back at
         # the chunk's end); graph launches on one stream run one after another, so a chunk's
@@ -475,7 +485,14 @@ def step_bench(a, rk):
                 if n > 1:
                     eng.stream_wait_event(comp, ev_comm[(n - 2) & 1])
             return eng.graph_end(comp)
-        graphs = {n: capture(n) for n in set(chunks)}
+        try:
+            graphs = {n: capture(n) for n in set(chunks)}
+        except MpxError as e:  # "auto" on a library without stream capture (the CPU stub)
+            if a.graph == "on":
+                raise
+            graph_info = {"used": False, "unavailable": str(e)[:160]}
+            use_graph = False
+    if use_graph:
         for _ in range(max(a.warmup, 1)):
             eng.graph_launch(graphs[U], comp)
         eng.synchronize()
@@ -488,7 +505,7 @@ def step_bench(a, rk):
         rk.barrier()
         t1 = time.perf_counter()
         elapsed_graph = rk.max(t1 - t0)
-        graph_info = {"steps_per_graph": U, "graph_launches": len(chunks),
+        graph_info = {"used": True, "steps_per_graph": U, "graph_launches": len(chunks),
                       "ms_per_step_graph": elapsed_graph / a.steps * 1e3,
                       "ms_per_step_no_graph": elapsed / a.steps * 1e3}
         last = (chunks[-1] - 1) & 1
@@ -596,8 +613,8 @@ def step_bench(a, rk):
             "executed_commands_per_s": n_exec_cmds * a.steps / elapsed,
             # table fill + warm-up + timed (+ the graph replays' warm-up and timed steps)
             "launches_in_process": 1 + a.warmup + a.steps + (
-                max(a.warmup, 1) * graph_info["steps_per_graph"] + a.steps if graph_info else 0),
-            **({"graph": graph_info} if graph_info else {}),
+                max(a.warmup, 1) * graph_info["steps_per_graph"] + a.steps if use_graph else 0),
+            "graph": graph_info or {"used": False},
             "watermark_allreduce_ok": wm_ok,
             **({"emulated_world": {
                 "ranks": emu, "groups_on_this_rank": G, "groups_total": G_total,

@@ -12,12 +12,12 @@ run() {
   [ $rc = 0 ] || exit $rc
 }
 for P in ${PS:-1 2 4 8}; do
-  run p${P} --emulate-world $P --steps ${STEPS:-40} --warmup 3 --no-cpu-baseline ${XARGS:-}
-  run p${P}_graph --emulate-world $P --graph --steps ${STEPS:-40} --warmup 3 --no-cpu-baseline ${XARGS:-}
+  run p${P} --emulate-world $P --graph off --steps ${STEPS:-40} --warmup 3 --no-cpu-baseline ${XARGS:-}
+  run p${P}_graph --emulate-world $P --graph on --steps ${STEPS:-40} --warmup 3 --no-cpu-baseline ${XARGS:-}
 done
 if [ "${PROF:-1}" = "1" ]; then
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_p8 -o trace -- python3 bench.py --emulate-world 8 --steps 40 --warmup 3 --no-cpu-baseline > $OUT/trace_p8.log 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_p8 -o trace -- python3 bench.py --emulate-world 8 --graph off --steps 40 --warmup 3 --no-cpu-baseline > $OUT/trace_p8.log 2>&1
   rc=$?; echo "trace_p8 rc=$rc"; [ $rc = 0 ] || exit $rc
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_p8g -o trace -- python3 bench.py --emulate-world 8 --graph --steps 40 --warmup 3 --no-cpu-baseline > $OUT/trace_p8g.log 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_p8g -o trace -- python3 bench.py --emulate-world 8 --graph on --steps 40 --warmup 3 --no-cpu-baseline > $OUT/trace_p8g.log 2>&1
   rc=$?; echo "trace_p8g rc=$rc"; [ $rc = 0 ] || exit $rc
 fi
