@@ -213,13 +213,15 @@ __device__ __forceinline__ uint32_t lut_len(uint64_t lut, uint32_t code) {
     return (((uint32_t)(lut >> ((i & 7u) * 8u)) & 0xFFu) & in) | (1u & ~in);
 }
 
+#ifndef MPX_SD_VARLDS
+#define MPX_SD_VARLDS 0
+#endif
 // Phase 1 (variable-length messages only): the bounded parse of every variable-message code of
 // the lane's chunk (bytes through L2), D[p] = its length if it lands no further than `lim`,
 // else 0 (terminal); the DP reads it back at p before writing D[p].
-__device__ __noinline__ void var_lengths(const uint8_t* g, uint64_t len, uint64_t c0,
+__device__ __noinline__ void var_lengths(const Bytes by, uint64_t len, uint64_t c0,
                                          uint64_t lim, int proto, uint64_t m_lo, uint64_t m_hi,
                                          uint8_t* D) {
-    const Bytes by{g, nullptr, 0, 0};
     for (int h = 0; h < 2; ++h) {
         uint64_t m = h ? m_hi : m_lo;
         while (m) {
@@ -296,6 +298,11 @@ __global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
     // own row, hit 64 different banks (a 128-byte stride put every lane on two banks)
     __shared__ __attribute__((aligned(16))) uint8_t D[kTL][kDRow];
     __shared__ uint8_t G[kTL / 8][kE];
+#if MPX_SD_VARLDS
+    // the tile's bytes (+ the next kE + 16) for the variable-message parses, which otherwise
+    // read global memory byte by byte on a dependent chain
+    __shared__ __attribute__((aligned(16))) uint8_t Bt[kTB + kE + 16];
+#endif
     const int l = threadIdx.x;
     const uint64_t t0 = (uint64_t)blockIdx.x * kTB;
     const uint64_t c0 = t0 + (uint64_t)l * kC;
@@ -322,6 +329,31 @@ __global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
         }
     }
     const uint64_t lut = P.proto == MPX_MODE_MIN ? kLutMin : kLutClassic;
+#if MPX_SD_VARLDS
+    // each lane's own chunk from its registers; the tail (kE + 16 bytes past the tile) by lanes
+    // 0..4
+#pragma unroll
+    for (int i = 0; i < kC / 16; ++i)
+        reinterpret_cast<uint4*>(Bt + l * kC)[i] =
+            make_uint4(wd[4 * i], wd[4 * i + 1], wd[4 * i + 2], wd[4 * i + 3]);
+    if (l < (kE + 16) / 16) {
+        const uint64_t a = t0 + kTB + 16 * (uint64_t)l;
+        uint32_t q[4] = {0, 0, 0, 0};
+        if (a + 16 <= P.len) {
+            const uint4 v = *reinterpret_cast<const uint4*>(P.buf + a);
+            q[0] = v.x; q[1] = v.y; q[2] = v.z; q[3] = v.w;
+        } else {
+            for (int b = 0; b < 16; ++b)
+                if (a + b < P.len) q[b >> 2] |= (uint32_t)P.buf[a + b] << (8 * (b & 3));
+        }
+        reinterpret_cast<uint4*>(Bt + kTB)[l] = make_uint4(q[0], q[1], q[2], q[3]);
+    }
+    __syncthreads();
+    const uint64_t bhi = t0 + kTB + kE + 16 < P.len ? t0 + kTB + kE + 16 : P.len;
+    const Bytes vby{P.buf, Bt, t0, bhi};
+#else
+    const Bytes vby{P.buf, nullptr, 0, 0};
+#endif
     if (!P.legacy) {
         uint64_t m_lo = 0, m_hi = 0;  // positions of variable-message codes
 #pragma unroll
@@ -331,7 +363,7 @@ __global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
             if (p < 64) m_lo |= bit; else m_hi |= bit;
         }
         if (m_lo | m_hi)
-            var_lengths(P.buf, P.len, c0, c0 + kC + kE - 1, P.proto, m_lo, m_hi, D[l]);
+            var_lengths(vby, P.len, c0, c0 + kC + kE - 1, P.proto, m_lo, m_hi, D[l]);
     }
     if (c0 + kC + 17 + kE > P.len)
         chunk_dp<true>(wd, c0, P.len, lut, P.legacy != 0, D[l]);
@@ -773,10 +805,19 @@ __global__ __launch_bounds__(kScanT) void k_sd_scan(Work W, uint32_t n_tiles) {
     if (t == 0) *W.ticket = 0;
 }
 
+#ifndef MPX_SD_EMIT_STAGE
+#define MPX_SD_EMIT_STAGE 0
+#endif
+// AcceptReplies of a tile staged in LDS (every MIN tile fits: frames of 14 bytes starting in
+// 16 KB); a tile with more (CLASSIC's 10-byte frames) stores them directly
+constexpr int kStageAR = (kTB + 13) / 14 + 1;
 __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint32_t n_tiles,
                                                  mpx_stream_result* res) {
     __shared__ __attribute__((aligned(16))) uint8_t B[kTB + kE + 16];  // + lds_le32's 2nd dword
     __shared__ uint32_t wsum[kTL / kWave][4];
+#if MPX_SD_EMIT_STAGE
+    __shared__ uint4 R[kStageAR];
+#endif
     const int l = threadIdx.x;
     const uint32_t tile = blockIdx.x;
     const uint8_t ent = W.tent[tile];
@@ -833,9 +874,12 @@ __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint
         res->n_var = base[2] + tp[2] + tot[2];
         res->n_other = base[3] + tp[3] + tot[3];
     }
-    if (e == kDeadE) return;
+#if MPX_SD_EMIT_STAGE
+    const bool staged = tot[0] <= (uint32_t)kStageAR;  // uniform over the workgroup
+    const uint64_t ar0 = base[0] + tp[0];              // the tile's first AcceptReply
+#endif
     // walk 2: the records
-    for (uint64_t a = c0 + e; a < c0 + kC;) {
+    for (uint64_t a = c0 + e; e != kDeadE && a < c0 + kC;) {
         const uint32_t code = B[a - t0];
         uint32_t fl = lut_len(lut, code);
         const bool at_stop = a == stop;
@@ -895,8 +939,22 @@ __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint
             ++idx[2];
             if (at_stop) break;
         } else if (code == MPX_PEER_ACCEPT_REPLY) {
+#ifdef MPX_SD_NOSTORE  // diagnostic build: the walk without its AcceptReply stores
+            if (idx[0] == ~0ull) {
+#else
             if (idx[0] < O.ar_cap) {  // a complete fixed frame: inside the LDS window
+#endif
                 const uint32_t o = (uint32_t)(a - t0);
+#if MPX_SD_EMIT_STAGE
+                const uint4 r = make_uint4((uint32_t)lds_le32(B, o + 1), (uint32_t)lds_le32(B, o + 6),
+                                           P.proto == MPX_MODE_MIN ? (uint32_t)lds_le32(B, o + 10)
+                                                                   : 0xFFFFFFFFu,
+                                           (uint32_t)B[o + 5]);
+                if (staged)
+                    R[idx[0] - ar0] = r;
+                else
+                    reinterpret_cast<uint4*>(O.ar)[idx[0]] = r;
+#else
                 mpx_accept_reply r;
                 r.instance = lds_le32(B, o + 1);
                 r.ok = B[o + 5];
@@ -904,6 +962,7 @@ __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint
                 r.id = P.proto == MPX_MODE_MIN ? lds_le32(B, o + 10) : -1;
                 r.pad[0] = r.pad[1] = r.pad[2] = 0;
                 O.ar[idx[0]] = r;
+#endif
             }
             ++idx[0];
         } else {
@@ -918,6 +977,13 @@ __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint
         }
         a += fl;
     }
+#if MPX_SD_EMIT_STAGE
+    if (staged) {  // the tile's AcceptReplies, one coalesced run
+        __syncthreads();
+        const uint64_t n = ar0 + tot[0] < O.ar_cap ? tot[0] : (ar0 < O.ar_cap ? O.ar_cap - ar0 : 0);
+        for (uint32_t i = l; i < n; i += kTL) reinterpret_cast<uint4*>(O.ar)[ar0 + i] = R[i];
+    }
+#endif
 }
 
 // an empty call ([start, len) holds no byte): END, counts unchanged

@@ -18,8 +18,15 @@
 
 namespace mpx {
 
-constexpr int kTileRecs = 1024;
-constexpr int kTileBlock = 256;
+#ifndef MPX_TILE_RECS  // A/B builds (make variant_of): other tile shapes
+#define MPX_TILE_RECS 1024
+#endif
+#ifndef MPX_TILE_BLOCK
+#define MPX_TILE_BLOCK 256
+#endif
+constexpr int kTileRecs = MPX_TILE_RECS;
+constexpr int kTileBlock = MPX_TILE_BLOCK;
+static_assert(kTileRecs % kTileBlock == 0 && kTileRecs < 65536, "tile shape");
 constexpr int kTilePer = kTileRecs / kTileBlock;
 constexpr int kTileWaves = kTileBlock / kWave;
 
