@@ -135,6 +135,9 @@ def parse():
                     help="apply: mpx_config.apply_path (auto = by call size)")
     ap.add_argument("--replay-dups", action="store_true",
                     help="replay: instNo drawn with repeats (last record wins) instead of a permutation")
+    ap.add_argument("--replay-atomic", action="store_true",
+                    help="replay: no mpx_replay_durable_reserve, so one device atomic per record "
+                         "(the A/B of the binned slot maximum)")
     return ap.parse_args()
 
 
@@ -1119,6 +1122,8 @@ def kernel_bench(a, rk):
         d_val = ar.empty(I, np.int64)
         d_last = ar.full(I, np.int32, 0xFF)
         d_sc = put(np.array([0, -1], np.int32))
+        if not a.replay_atomic:
+            eng.replay_durable_reserve(L, I)  # the binned slot maximum's scratch
         t_gen = time.time() - t_gen
         # every output is idempotent under repetition (slots and watermarks are maxima)
         wall, ms = _timed(eng, a.steps, a.warmup,
@@ -1130,7 +1135,7 @@ def kernel_bench(a, rk):
         alg = L + I * (16 + 1 + 8 + 8) + I * 4
         units, unit = I, "records/s"
         kernel = "k_replay_durable"
-        kernel_pat = ["k_replay_durable"]
+        kernel_pat = ["k_replay_durable", "k_rb_", "k_scan_"]
         bit_exact = bool(np.array_equal(get(d_recs), w[0]) and np.array_equal(get(d_op), w[1])
                          and np.array_equal(get(d_key), w[2]) and np.array_equal(get(d_val), w[3])
                          and np.array_equal(get(d_last), w[4])
@@ -1265,7 +1270,8 @@ def kernel_bench(a, rk):
                            "prep_cmds": a.prep_cmds},
         "fanout": lambda: {"commands": a.commands, "clients": a.clients},
         "log": lambda: {"instances": a.instances, "log_format": a.log_format},
-        "replay": lambda: {"instances": a.instances, "replay_dups": bool(a.replay_dups)},
+        "replay": lambda: {"instances": a.instances, "replay_dups": bool(a.replay_dups),
+                           **({"replay_atomic": True} if a.replay_atomic else {})},
     }[a.workload]())
     traffic, tnote = traffic_for(tkey, alg, a.traffic_json)
     rl = {"bound": "hbm", "kernel": kernel, "achieved": achieved,

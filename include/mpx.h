@@ -68,7 +68,8 @@
 extern "C" {
 #endif
 
-#define MPX_ABI_VERSION 5  /* 4: + mpx_group_step_totals_dev; 5: + mpx_graph_*, mpx_apply_buffers / _staged */
+#define MPX_ABI_VERSION 6  /* 4: + mpx_group_step_totals_dev; 5: + mpx_graph_*, mpx_apply_buffers / _staged;
+                              6: + mpx_replay_durable_reserve */
 
 /* ---- error codes ---------------------------------------------------------------------- */
 #define MPX_OK 0
@@ -619,7 +620,12 @@ int mpx_encode_log_dev(mpx_engine* eng, int format, const mpx_log_rec* d_recs, s
 int mpx_replay_durable(mpx_engine* eng, const uint8_t* log, size_t len, int32_t inst_cap,
                        int32_t rec_base, mpx_log_rec* recs, uint8_t* op, int64_t* key,
                        int64_t* val, int32_t* last_rec, int32_t* scalars);
-/* device form: d_log 16-byte aligned; d_last_rec[inst_cap] and d_scalars[2] in/out          */
+/* device form: d_log 16-byte aligned; d_last_rec[inst_cap] and d_scalars[2] in/out.
+ * The slot maxima are binned in LDS (no device atomic per record) when the engine holds the
+ * scratch for the call: mpx_replay_durable_reserve(max_len, inst_cap) once beforehand (the dev
+ * entry never allocates; instance spaces up to 2^25 slots); without it the call takes one
+ * device-scope atomicMax per record. Same results either way.                              */
+int mpx_replay_durable_reserve(mpx_engine* eng, size_t max_len, int32_t inst_cap);
 int mpx_replay_durable_dev(mpx_engine* eng, const uint8_t* d_log, size_t len, int32_t inst_cap,
                            int32_t rec_base, mpx_log_rec* d_recs, uint8_t* d_op,
                            int64_t* d_key, int64_t* d_val, int32_t* d_last_rec,

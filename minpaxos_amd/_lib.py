@@ -88,6 +88,7 @@ SIGNATURES = {
     "mpx_encode_log_dev": (C.c_int, [_p, C.c_int, _p, _sz, _p, _p, _p, _p, _sz, _p, _p, _p]),
     "mpx_replay_durable": (C.c_int, [_p, _p, _sz, _i32, _i32, _p, _p, _p, _p, _p, _p]),
     "mpx_replay_durable_dev": (C.c_int, [_p, _p, _sz, _i32, _i32, _p, _p, _p, _p, _p, _p, _p]),
+    "mpx_replay_durable_reserve": (C.c_int, [_p, _sz, _i32]),
     "mpx_step_totals_dev": (C.c_int, [_p, C.POINTER(MpxGroupBatch), _p, _p]),
     "mpx_group_step_totals_dev": (C.c_int, [_p, C.POINTER(MpxGroupBatch), _p, _p]),
     "mpx_step_allreduce_dev": (C.c_int, [_p, _p, _sz, _p, _sz, _p]),

@@ -86,6 +86,7 @@ struct mpx_engine {
     DevBuf log_work;
     // durable-log replay staging: log bytes, records, op, key, val, last_rec, scalars
     DevBuf rp[7];
+    DevBuf replay_work;  // the binned slot maximum (mpx_replay_durable_reserve)
     mpx::ApplyOpts apply{};  // mpx_config.apply_* (fixed for the handle's life)
     // replica-sized mpx_apply calls: pinned, GPU-mapped staging the one-launch kernel reads the
     // commands from and writes the results to (no DMA copies on the call's path)
@@ -373,6 +374,7 @@ int mpx_close(mpx_engine* e) {
     if (e->log_work.p) (void)hipFree(e->log_work.p);
     for (auto& x : e->rp)
         if (x.p) (void)hipFree(x.p);
+    if (e->replay_work.p) (void)hipFree(e->replay_work.p);
     if (e->worklist.p) (void)hipFree(e->worklist.p);
     if (e->d_wcount) (void)hipFree(e->d_wcount);
     if (e->kv_ready) free_kv(e->kv);
@@ -1262,8 +1264,18 @@ int mpx_replay_durable_dev(mpx_engine* e, const uint8_t* d_log, size_t len, int3
     if ((uintptr_t)d_log % 16)
         return fail(e, MPX_E_INVAL, "d_log must be 16-byte aligned (the tiles load 16 B vectors)");
     HIPCHK(e, mpx::launch_replay_durable(d_log, n, inst_cap, rec_base, d_recs, d_op, d_key, d_val,
-                                         d_last_rec, d_scalars, e->d_err, pick(e, stream)));
+                                         d_last_rec, d_scalars, e->d_err, e->replay_work.p,
+                                         e->replay_work.cap, pick(e, stream)));
     return MPX_OK;
+}
+
+int mpx_replay_durable_reserve(mpx_engine* e, size_t max_len, int32_t inst_cap) {
+    if (!e) return MPX_E_INVAL;
+    if (inst_cap < 0) return fail(e, MPX_E_INVAL, "inst_cap must be >= 0");
+    const size_t n = max_len / MPX_DURABLE_REC_BYTES;
+    CK(begin(e));
+    GROW(e, e->replay_work, mpx::replay_work_bytes(n, inst_cap));
+    return finish(e);
 }
 
 int mpx_replay_durable(mpx_engine* e, const uint8_t* log, size_t len, int32_t inst_cap,
@@ -1282,6 +1294,7 @@ int mpx_replay_durable(mpx_engine* e, const uint8_t* log, size_t len, int32_t in
     GROW(e, e->rp[4], n * 8);
     GROW(e, e->rp[5], (size_t)inst_cap * 4);
     GROW(e, e->rp[6], 2 * sizeof(int32_t));
+    GROW(e, e->replay_work, mpx::replay_work_bytes(n, inst_cap));
     CK(h2d(e, e->rp[0].p, log, len));
     CK(h2d(e, e->rp[5].p, last_rec, (size_t)inst_cap * 4));
     CK(h2d(e, e->rp[6].p, scalars, 2 * sizeof(int32_t)));

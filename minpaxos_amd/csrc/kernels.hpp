@@ -187,6 +187,9 @@ hipError_t launch_encode_log(int format, const mpx_log_rec* recs, uint64_t n,
 hipError_t launch_replay_durable(const uint8_t* log, uint64_t n, int32_t inst_cap,
                                  int32_t rec_base, mpx_log_rec* recs, uint8_t* op, int64_t* key, int64_t* val,
                                  int32_t* last_rec, int32_t* scalars, uint32_t* err,
-                                 hipStream_t stream);
+                                 void* work, uint64_t work_bytes, hipStream_t stream);
+// scratch of the binned slot maximum for n records over inst_cap slots (0: the call takes the
+// per-record atomic form, which needs none)
+uint64_t replay_work_bytes(uint64_t n, int32_t inst_cap);
 
 }  // namespace mpx

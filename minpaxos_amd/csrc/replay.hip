@@ -9,7 +9,21 @@
 //   instanceSpace[instNo] = {ballot, status, {0,0,0,nil}, [command]}               (:153-157)
 // The two watermarks are running maxima, so they are order-free; the last record naming an
 // instance wins its slot, so the slot keeps the HIGHEST record index.
-// The slot maximum without a device-scope atomic per record (MPX_REPLAY_ATOMIC=0, default):
+// The slot maximum, binned (the default when the engine holds the call's scratch,
+// replay_work_bytes; instance spaces up to kRbMaxCap slots): 2^24 random device-scope atomics
+// are request-bound on this chip (0.45 ms of the 0.69 ms call, round 3), so the slots are
+// maximised in LDS instead:
+//   k_replay_durable  writes pair[i] = (rec_base + i) << 32 | instNo, coalesced (8 B / record)
+//   k_rb_count        a workgroup per chunk of kRbChunk pairs: LDS histogram of the bins
+//                     (kRbSlots instance slots each) into hist[bin][chunk], bin-major
+//   scan              scan.hpp over the bins x chunks counts (+1: the total)
+//   k_rb_scatter      the chunk's pairs to their bins' runs (LDS cursors; order inside a bin
+//                     is free, a maximum does not depend on it)
+//   k_rb_max          a workgroup per bin: the bin's slice of last_rec into LDS, one LDS
+//                     atomicMax per pair, the slice written back
+// 8 B x 4 of pair traffic per record + the slots read and written once, all coalesced.
+// Without the scratch (or past kRbMaxCap slots), one atomicMax per record:
+// The slot maximum without a device-scope atomic per record (MPX_REPLAY_ATOMIC=0, A/B):
 //   pass 1 (k_replay_durable) raises a slot with a plain load + store when its record index is
 //          higher: racing records of one instance may leave a lower index, never a value below
 //          the slot's value at call start (memory holds it when the kernel begins);
@@ -26,6 +40,7 @@
 // 29 B in + 33 B out + one 4-byte slot update per record (+ pass 2's 16-byte re-read).
 #include "common.hpp"
 #include "kernels.hpp"
+#include "scan.hpp"
 
 namespace mpx {
 
@@ -39,6 +54,7 @@ constexpr uint64_t kReplayGrid = 256 * 8;  // 256 CUs x 8 workgroups
 #define MPX_REPLAY_ATOMIC 1
 #endif
 static_assert(kTileBytes % 16 == 0, "tile must be a whole number of 16-byte vectors");
+constexpr int kVecPer = (kTileVec + kReplayBlock - 1) / kReplayBlock;  // vectors per thread
 
 __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
 #pragma unroll
@@ -49,34 +65,57 @@ __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
     return v;
 }
 
+constexpr int kRbLg = 13;
+constexpr uint32_t kRbSlots = 1u << kRbLg;      // instance slots per bin (32 KB of LDS)
+constexpr uint32_t kRbMaxBins = 4096;           // the count / scatter LDS tables (16 KB)
+constexpr int64_t kRbMaxCap = (int64_t)kRbSlots * kRbMaxBins;  // 2^25 slots
+constexpr int kRbT = 1024;
+constexpr uint64_t kRbChunk = 64 * kRbT;        // pairs per count / scatter workgroup
+constexpr uint64_t kRbNone = ~0ull;             // an instNo outside [0, inst_cap): no slot
+
+// pairs: null = the atomic form
 __global__ __launch_bounds__(kReplayBlock) void k_replay_durable(
     const uint8_t* __restrict__ log, uint64_t n, int32_t inst_cap, int32_t rec_base,
     mpx_log_rec* __restrict__ recs,
     uint8_t* __restrict__ op, int64_t* __restrict__ key, int64_t* __restrict__ val,
-    int32_t* __restrict__ last_rec, int32_t* __restrict__ scalars, uint32_t* __restrict__ err) {
+    int32_t* __restrict__ last_rec, int32_t* __restrict__ scalars, uint32_t* __restrict__ err,
+    uint64_t* __restrict__ pairs) {
     __shared__ uint4 tile[kTileVec + 1];  // +1: the last lane's 9th dword reads past the tile
     __shared__ int32_t red[2][kReplayBlock / kWave];
     const int t = threadIdx.x;
     int32_t ballot = INT32_MIN, committed = INT32_MIN;
     const uint64_t n_tiles = (n + kReplayBlock - 1) / kReplayBlock;
-    for (uint64_t tl = blockIdx.x; tl < n_tiles; tl += gridDim.x) {
+    // the tile's 16-byte vectors: whole ones inside its records, the ragged tail byte by byte
+    auto load_tile = [&](uint64_t tl, uint4 (&v)[kVecPer]) {
         const uint64_t r0 = tl * kReplayBlock;
         const uint64_t nrec = n - r0 < (uint64_t)kReplayBlock ? n - r0 : (uint64_t)kReplayBlock;
         const uint64_t tile_bytes = nrec * kRecBytes;
         const uint8_t* src = log + r0 * kRecBytes;
-        // stage: whole 16-byte vectors inside the tile's records, the ragged tail byte by byte
         const uint64_t nvec = tile_bytes / 16;
-        __syncthreads();  // the previous tile's readers are done with the LDS image
-        for (int v = t; v < kTileVec; v += kReplayBlock) {
-            if ((uint64_t)v < nvec) {
-                tile[v] = ld_stream(reinterpret_cast<const uint4*>(src) + v);
-            } else if ((uint64_t)v * 16 < tile_bytes) {
+#pragma unroll
+        for (int k = 0; k < kVecPer; ++k) {
+            const int vi = t + k * kReplayBlock;
+            v[k] = make_uint4(0, 0, 0, 0);
+            if ((uint64_t)vi < nvec) {
+                v[k] = ld_stream(reinterpret_cast<const uint4*>(src) + vi);
+            } else if (vi < kTileVec && (uint64_t)vi * 16 < tile_bytes) {
                 uint8_t b[16] = {};
-                for (uint64_t k = (uint64_t)v * 16; k < tile_bytes; ++k)
-                    b[k - (uint64_t)v * 16] = src[k];
-                tile[v] = *reinterpret_cast<const uint4*>(b);
+                for (uint64_t q = (uint64_t)vi * 16; q < tile_bytes; ++q) b[q - (uint64_t)vi * 16] = src[q];
+                v[k] = *reinterpret_cast<const uint4*>(b);
             }
         }
+    };
+    uint4 cur[kVecPer];
+    if (blockIdx.x < n_tiles) load_tile(blockIdx.x, cur);
+    for (uint64_t tl = blockIdx.x; tl < n_tiles; tl += gridDim.x) {
+        const uint64_t r0 = tl * kReplayBlock;
+        const uint64_t nrec = n - r0 < (uint64_t)kReplayBlock ? n - r0 : (uint64_t)kReplayBlock;
+        __syncthreads();  // the previous tile's readers are done with the LDS image
+#pragma unroll
+        for (int k = 0; k < kVecPer; ++k)
+            if (t + k * kReplayBlock < kTileVec) tile[t + k * kReplayBlock] = cur[k];
+        // the workgroup's next tile: in flight while this one is cut into records
+        if (tl + gridDim.x < n_tiles) load_tile(tl + gridDim.x, cur);
         __syncthreads();
         if ((uint64_t)t < nrec) {
             // the record as 8 realigned dwords from 9 aligned LDS dword reads (not 29 byte reads)
@@ -108,8 +147,15 @@ __global__ __launch_bounds__(kReplayBlock) void k_replay_durable(
             ballot = b > ballot ? b : ballot;
             if (st == MPX_COMMITTED && inst > committed) committed = inst;
             // instanceSpace[instNo] panics outside the array (Go index check)
-            if (inst < 0 || inst >= inst_cap)
+            const bool bad = inst < 0 || inst >= inst_cap;
+            if (pairs)
+                st_stream(pairs + i, bad ? kRbNone
+                                         : ((uint64_t)(uint32_t)(rec_base + (int32_t)i) << 32) |
+                                               (uint32_t)inst);
+            if (bad)
                 raise_err(err, kErrNil);
+            else if (pairs)
+                ;
             else if (MPX_REPLAY_ATOMIC)
                 atomicMax(last_rec + inst, rec_base + (int32_t)i);
             else if (last_rec[inst] < rec_base + (int32_t)i)
@@ -147,18 +193,133 @@ __global__ __launch_bounds__(256) void k_replay_fix(const mpx_log_rec* __restric
         if (last_rec[inst] < me) atomicMax(last_rec + inst, me);
     }
 }
+// ---- the binned slot maximum --------------------------------------------------------------
+__global__ __launch_bounds__(kRbT) void k_rb_count(const uint64_t* __restrict__ pairs, uint64_t n,
+                                                  uint32_t bins, uint32_t chunks,
+                                                  uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[kRbMaxBins];
+    for (uint32_t b = threadIdx.x; b < bins; b += kRbT) h[b] = 0;
+    __syncthreads();
+    const uint64_t c0 = (uint64_t)blockIdx.x * kRbChunk;
+#pragma unroll 8
+    for (uint64_t k = threadIdx.x; k < kRbChunk; k += kRbT) {
+        const uint64_t i = c0 + k;
+        if (i >= n) break;
+        const uint64_t p = ld_stream(pairs + i);
+        if (p != kRbNone) atomicAdd(&h[(uint32_t)p >> kRbLg], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < bins; b += kRbT) hist[(uint64_t)b * chunks + blockIdx.x] = h[b];
+}
+
+__global__ __launch_bounds__(kRbT) void k_rb_scatter(const uint64_t* __restrict__ pairs, uint64_t n,
+                                                    uint32_t bins, uint32_t chunks,
+                                                    const uint32_t* __restrict__ offs,
+                                                    uint64_t* __restrict__ binned) {
+    __shared__ uint32_t cur[kRbMaxBins];
+    for (uint32_t b = threadIdx.x; b < bins; b += kRbT)
+        cur[b] = offs[(uint64_t)b * chunks + blockIdx.x];
+    __syncthreads();
+    const uint64_t c0 = (uint64_t)blockIdx.x * kRbChunk;
+#pragma unroll 8
+    for (uint64_t k = threadIdx.x; k < kRbChunk; k += kRbT) {
+        const uint64_t i = c0 + k;
+        if (i >= n) break;
+        const uint64_t p = ld_stream(pairs + i);
+        if (p != kRbNone) binned[atomicAdd(&cur[(uint32_t)p >> kRbLg], 1u)] = p;
+    }
+}
+
+__global__ __launch_bounds__(kRbT) void k_rb_max(const uint64_t* __restrict__ binned,
+                                                uint32_t chunks, const uint32_t* __restrict__ offs,
+                                                int32_t inst_cap, int32_t* __restrict__ last_rec) {
+    __shared__ int32_t sl[kRbSlots];
+    const uint32_t b = blockIdx.x;
+    const uint64_t s0 = (uint64_t)b * kRbSlots;
+    const uint32_t ns = (uint64_t)inst_cap - s0 < kRbSlots ? (uint32_t)((uint64_t)inst_cap - s0)
+                                                            : kRbSlots;
+    for (uint32_t j = threadIdx.x; j < ns; j += kRbT) sl[j] = last_rec[s0 + j];
+    // the bin's run: from its first chunk's offset to the next bin's (the total after the last)
+    const uint64_t lo = offs[(uint64_t)b * chunks], hi = offs[(uint64_t)(b + 1) * chunks];
+    __syncthreads();
+#pragma unroll 4
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += kRbT) {
+        const uint64_t p = ld_stream(binned + i);
+        atomicMax(&sl[(uint32_t)p & (kRbSlots - 1)], (int32_t)(p >> 32));
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < ns; j += kRbT) last_rec[s0 + j] = sl[j];
+}
+
+// the scan of hist: bins x chunks counts, then one zero item whose prefix is the total
+struct RbHistIn {
+    const uint32_t* h;
+    uint64_t n;
+    __device__ __forceinline__ uint32_t operator()(uint64_t i) const { return i < n ? h[i] : 0u; }
+};
+struct RbHistOut {
+    uint32_t* o;
+    __device__ __forceinline__ void operator()(uint64_t i, uint32_t ex, uint32_t) const { o[i] = ex; }
+};
+
+struct RbLayout {
+    uint64_t pairs, binned, hist, offs, scan, total;
+};
+RbLayout rb_layout(uint64_t n, int32_t inst_cap) {
+    auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+    const uint64_t chunks = (n + kRbChunk - 1) / kRbChunk;
+    const uint64_t bins = ((uint64_t)inst_cap + kRbSlots - 1) / kRbSlots;
+    const uint64_t h = bins * chunks + 1;
+    RbLayout L{};
+    uint64_t o = 0;
+    L.pairs = o; o += al(n * 8);
+    L.binned = o; o += al(n * 8);
+    L.hist = o; o += al(h * 4);
+    L.offs = o; o += al(h * 4);
+    L.scan = o; o += al(scan_scratch_bytes<uint32_t>(h));
+    L.total = o;
+    return L;
+}
+bool rb_eligible(uint64_t n, int32_t inst_cap) {
+    return n > 0 && inst_cap > 0 && (int64_t)inst_cap <= kRbMaxCap && n < (1ull << 32);
+}
 }  // namespace
+
+uint64_t replay_work_bytes(uint64_t n, int32_t inst_cap) {
+    return rb_eligible(n, inst_cap) ? rb_layout(n, inst_cap).total : 0;
+}
 
 hipError_t launch_replay_durable(const uint8_t* log, uint64_t n, int32_t inst_cap,
                                  int32_t rec_base, mpx_log_rec* recs, uint8_t* op, int64_t* key, int64_t* val,
                                  int32_t* last_rec, int32_t* scalars, uint32_t* err,
-                                 hipStream_t stream) {
+                                 void* work, uint64_t work_bytes, hipStream_t stream) {
     if (!n) return hipSuccess;
+    const bool binned = rb_eligible(n, inst_cap) && work &&
+                        work_bytes >= rb_layout(n, inst_cap).total;
+    const RbLayout L = binned ? rb_layout(n, inst_cap) : RbLayout{};
+    char* w = (char*)work;
+    uint64_t* pairs = binned ? (uint64_t*)(w + L.pairs) : nullptr;
     // a few workgroups per CU walk the tiles (grid-stride), so the watermark atomics stay few
     const uint64_t tiles = (n + kReplayBlock - 1) / kReplayBlock;
     const uint64_t grid = tiles < kReplayGrid ? tiles : kReplayGrid;
     hipLaunchKernelGGL(k_replay_durable, dim3((unsigned)grid), dim3(kReplayBlock), 0, stream, log,
-                       n, inst_cap, rec_base, recs, op, key, val, last_rec, scalars, err);
+                       n, inst_cap, rec_base, recs, op, key, val, last_rec, scalars, err, pairs);
+    if (binned) {
+        const uint32_t chunks = (uint32_t)((n + kRbChunk - 1) / kRbChunk);
+        const uint32_t bins = (uint32_t)(((uint64_t)inst_cap + kRbSlots - 1) / kRbSlots);
+        const uint64_t h = (uint64_t)bins * chunks;
+        uint32_t* hist = (uint32_t*)(w + L.hist);
+        uint32_t* offs = (uint32_t*)(w + L.offs);
+        k_rb_count<<<chunks, kRbT, 0, stream>>>(pairs, n, bins, chunks, hist);
+        const hipError_t r = device_scan(RbHistIn{hist, h}, RbHistOut{offs}, h + 1, ScanSum32{},
+                                         0u, (uint32_t*)(w + L.scan), stream);
+        if (r != hipSuccess) return r;
+        k_rb_scatter<<<chunks, kRbT, 0, stream>>>(pairs, n, bins, chunks, offs,
+                                                  (uint64_t*)(w + L.binned));
+        k_rb_max<<<bins, kRbT, 0, stream>>>((const uint64_t*)(w + L.binned), chunks, offs,
+                                            inst_cap, last_rec);
+        return hipGetLastError();
+    }
     if (!MPX_REPLAY_ATOMIC) {
         const uint64_t g = (n + 255) / 256;
         hipLaunchKernelGGL(k_replay_fix, dim3((unsigned)(g < 8192 ? g : 8192)), dim3(256), 0,

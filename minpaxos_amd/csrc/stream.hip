@@ -213,9 +213,6 @@ __device__ __forceinline__ uint32_t lut_len(uint64_t lut, uint32_t code) {
     return (((uint32_t)(lut >> ((i & 7u) * 8u)) & 0xFFu) & in) | (1u & ~in);
 }
 
-#ifndef MPX_SD_VARLDS
-#define MPX_SD_VARLDS 0
-#endif
 // Phase 1 (variable-length messages only): the bounded parse of every variable-message code of
 // the lane's chunk (bytes through L2), D[p] = its length if it lands no further than `lim`,
 // else 0 (terminal); the DP reads it back at p before writing D[p].
@@ -298,11 +295,6 @@ __global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
     // own row, hit 64 different banks (a 128-byte stride put every lane on two banks)
     __shared__ __attribute__((aligned(16))) uint8_t D[kTL][kDRow];
     __shared__ uint8_t G[kTL / 8][kE];
-#if MPX_SD_VARLDS
-    // the tile's bytes (+ the next kE + 16) for the variable-message parses, which otherwise
-    // read global memory byte by byte on a dependent chain
-    __shared__ __attribute__((aligned(16))) uint8_t Bt[kTB + kE + 16];
-#endif
     const int l = threadIdx.x;
     const uint64_t t0 = (uint64_t)blockIdx.x * kTB;
     const uint64_t c0 = t0 + (uint64_t)l * kC;
@@ -329,31 +321,7 @@ __global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
         }
     }
     const uint64_t lut = P.proto == MPX_MODE_MIN ? kLutMin : kLutClassic;
-#if MPX_SD_VARLDS
-    // each lane's own chunk from its registers; the tail (kE + 16 bytes past the tile) by lanes
-    // 0..4
-#pragma unroll
-    for (int i = 0; i < kC / 16; ++i)
-        reinterpret_cast<uint4*>(Bt + l * kC)[i] =
-            make_uint4(wd[4 * i], wd[4 * i + 1], wd[4 * i + 2], wd[4 * i + 3]);
-    if (l < (kE + 16) / 16) {
-        const uint64_t a = t0 + kTB + 16 * (uint64_t)l;
-        uint32_t q[4] = {0, 0, 0, 0};
-        if (a + 16 <= P.len) {
-            const uint4 v = *reinterpret_cast<const uint4*>(P.buf + a);
-            q[0] = v.x; q[1] = v.y; q[2] = v.z; q[3] = v.w;
-        } else {
-            for (int b = 0; b < 16; ++b)
-                if (a + b < P.len) q[b >> 2] |= (uint32_t)P.buf[a + b] << (8 * (b & 3));
-        }
-        reinterpret_cast<uint4*>(Bt + kTB)[l] = make_uint4(q[0], q[1], q[2], q[3]);
-    }
-    __syncthreads();
-    const uint64_t bhi = t0 + kTB + kE + 16 < P.len ? t0 + kTB + kE + 16 : P.len;
-    const Bytes vby{P.buf, Bt, t0, bhi};
-#else
     const Bytes vby{P.buf, nullptr, 0, 0};
-#endif
     if (!P.legacy) {
         uint64_t m_lo = 0, m_hi = 0;  // positions of variable-message codes
 #pragma unroll
@@ -805,19 +773,20 @@ __global__ __launch_bounds__(kScanT) void k_sd_scan(Work W, uint32_t n_tiles) {
     if (t == 0) *W.ticket = 0;
 }
 
-#ifndef MPX_SD_EMIT_STAGE
-#define MPX_SD_EMIT_STAGE 0
+#ifndef MPX_SD_EMIT_REG
+#define MPX_SD_EMIT_REG 1
 #endif
-// AcceptReplies of a tile staged in LDS (every MIN tile fits: frames of 14 bytes starting in
-// 16 KB); a tile with more (CLASSIC's 10-byte frames) stores them directly
-constexpr int kStageAR = (kTB + 13) / 14 + 1;
+// frames whose AcceptReplies a lane keeps in registers for the staged stores (a 128-byte chunk
+// starts at most 10 MIN AcceptReply frames; 13 would cost a wave per SIMD of occupancy, so a
+// tile with a longer chunk - CLASSIC's 10-byte frames back to back - stores directly), and the
+// tile's records per LDS pass
+constexpr int kRegAR = 10;
+constexpr uint32_t kRegCap = 1024;
 __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint32_t n_tiles,
                                                  mpx_stream_result* res) {
     __shared__ __attribute__((aligned(16))) uint8_t B[kTB + kE + 16];  // + lds_le32's 2nd dword
     __shared__ uint32_t wsum[kTL / kWave][4];
-#if MPX_SD_EMIT_STAGE
-    __shared__ uint4 R[kStageAR];
-#endif
+    static_assert((kTB + kE + 16) / 16 >= kRegCap, "a pass of staged records fits the tile image");
     const int l = threadIdx.x;
     const uint32_t tile = blockIdx.x;
     const uint8_t ent = W.tent[tile];
@@ -874,16 +843,18 @@ __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint
         res->n_var = base[2] + tp[2] + tot[2];
         res->n_other = base[3] + tp[3] + tot[3];
     }
-#if MPX_SD_EMIT_STAGE
-    const bool staged = tot[0] <= (uint32_t)kStageAR;  // uniform over the workgroup
-    const uint64_t ar0 = base[0] + tp[0];              // the tile's first AcceptReply
-#endif
-    // walk 2: the records
-    for (uint64_t a = c0 + e; e != kDeadE && a < c0 + kC;) {
+    const uint64_t ar0 = base[0] + tp[0];  // the tile's first AcceptReply
+    // walk 2, one frame at a: an AcceptReply comes back in rec (is_ar), every other record is
+    // stored here; live = false after the chunk's last frame
+    auto frame = [&](uint64_t& a, bool& live, bool& is_ar, uint4& rec) {
+        is_ar = false;
         const uint32_t code = B[a - t0];
         uint32_t fl = lut_len(lut, code);
         const bool at_stop = a == stop;
-        if (at_stop && !long_stop) break;
+        if (at_stop && !long_stop) {
+            live = false;
+            return;
+        }
         if (fl == 0) {
             VarInfo f;
             if (at_stop) {
@@ -891,14 +862,6 @@ __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint
                             (uint32_t)W.stop[6], (uint32_t)W.stop[7]};
             } else {
                 f = parse_var(by, P.len, ~0ull, a, P.proto).f;
-#ifdef MPX_DEBUG_STREAM
-                {
-                    const VarRes d = parse_var(Bytes{P.buf, nullptr, 0, 0}, P.len, ~0ull, a, P.proto);
-                    printf("var@%lu code %u: lds-by len %u n %u co %u m %u lo %u | global st %d len %u n %u co %u m %u lo %u | B[a-t0]=%u g=%u\n",
-                           (unsigned long)a, code, f.len, f.n_cmds, f.cmds_off, f.n_log, f.log_off, d.st, d.f.len,
-                           d.f.n_cmds, d.f.cmds_off, d.f.n_log, d.f.log_off, (unsigned)B[a - t0], (unsigned)P.buf[a]);
-                }
-#endif
             }
             fl = f.len;
             if (code == MPX_PEER_PREPARE_REPLY) {
@@ -937,34 +900,17 @@ __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint
                 O.var[idx[2]] = v;
             }
             ++idx[2];
-            if (at_stop) break;
-        } else if (code == MPX_PEER_ACCEPT_REPLY) {
-#ifdef MPX_SD_NOSTORE  // diagnostic build: the walk without its AcceptReply stores
-            if (idx[0] == ~0ull) {
-#else
-            if (idx[0] < O.ar_cap) {  // a complete fixed frame: inside the LDS window
-#endif
-                const uint32_t o = (uint32_t)(a - t0);
-#if MPX_SD_EMIT_STAGE
-                const uint4 r = make_uint4((uint32_t)lds_le32(B, o + 1), (uint32_t)lds_le32(B, o + 6),
-                                           P.proto == MPX_MODE_MIN ? (uint32_t)lds_le32(B, o + 10)
-                                                                   : 0xFFFFFFFFu,
-                                           (uint32_t)B[o + 5]);
-                if (staged)
-                    R[idx[0] - ar0] = r;
-                else
-                    reinterpret_cast<uint4*>(O.ar)[idx[0]] = r;
-#else
-                mpx_accept_reply r;
-                r.instance = lds_le32(B, o + 1);
-                r.ok = B[o + 5];
-                r.ballot = lds_le32(B, o + 6);
-                r.id = P.proto == MPX_MODE_MIN ? lds_le32(B, o + 10) : -1;
-                r.pad[0] = r.pad[1] = r.pad[2] = 0;
-                O.ar[idx[0]] = r;
-#endif
+            if (at_stop) {
+                live = false;
+                return;
             }
-            ++idx[0];
+        } else if (code == MPX_PEER_ACCEPT_REPLY) {
+            // a complete fixed frame, inside the LDS window: Instance, OK, Ballot, Id
+            const uint32_t o = (uint32_t)(a - t0);
+            rec = make_uint4((uint32_t)lds_le32(B, o + 1), (uint32_t)lds_le32(B, o + 6),
+                             P.proto == MPX_MODE_MIN ? (uint32_t)lds_le32(B, o + 10) : 0xFFFFFFFFu,
+                             (uint32_t)B[o + 5]);
+            is_ar = true;
         } else {
             if (idx[3] < O.oth_cap) {
                 mpx_peer_frame f;
@@ -976,12 +922,63 @@ __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint
             ++idx[3];
         }
         a += fl;
+        live = a < c0 + kC;
+    };
+    uint4* const ar4 = reinterpret_cast<uint4*>(O.ar);  // mpx_accept_reply as 4 dwords
+    uint64_t a = c0 + e;
+    bool live = e != kDeadE;
+    bool is_ar;
+    uint4 rec;
+#if MPX_SD_EMIT_REG
+    // the lane's first kRegAR frames with their AcceptReplies held in registers ...
+    uint4 rr[kRegAR];
+    uint32_t rl[kRegAR];  // tile-local index, ~0 = none
+#pragma clang loop unroll(full)
+    for (int it = 0; it < kRegAR; ++it) {
+        rl[it] = ~0u;
+        if (live) {
+            frame(a, live, is_ar, rec);
+            if (is_ar) {
+                rr[it] = rec;
+                rl[it] = idx[0] < O.ar_cap ? (uint32_t)(idx[0] - ar0) : ~0u;
+                ++idx[0];
+            }
+        }
     }
-#if MPX_SD_EMIT_STAGE
-    if (staged) {  // the tile's AcceptReplies, one coalesced run
+    if (__syncthreads_or(live)) {  // a chunk with more frames: every record stored directly
+#pragma unroll
+        for (int it = 0; it < kRegAR; ++it)
+            if (rl[it] != ~0u) ar4[ar0 + rl[it]] = rr[it];
+        while (live) {
+            frame(a, live, is_ar, rec);
+            if (is_ar) {
+                if (idx[0] < O.ar_cap) ar4[idx[0]] = rec;
+                ++idx[0];
+            }
+        }
+        return;
+    }
+    // ... then through LDS (the tile image is dead: every lane has left its walk) in passes of
+    // kRegCap, so the tile's AcceptReplies leave as one coalesced run instead of a 16-byte store
+    // per lane and frame 150 bytes apart
+    uint4* const R = reinterpret_cast<uint4*>(B);
+    for (uint32_t ph = 0; ph < tot[0]; ph += kRegCap) {
+#pragma unroll
+        for (int it = 0; it < kRegAR; ++it)
+            if (rl[it] - ph < kRegCap) R[rl[it] - ph] = rr[it];
         __syncthreads();
-        const uint64_t n = ar0 + tot[0] < O.ar_cap ? tot[0] : (ar0 < O.ar_cap ? O.ar_cap - ar0 : 0);
-        for (uint32_t i = l; i < n; i += kTL) reinterpret_cast<uint4*>(O.ar)[ar0 + i] = R[i];
+        const uint32_t hi = tot[0] - ph < kRegCap ? tot[0] : ph + kRegCap;
+        for (uint32_t i = ph + (uint32_t)l; i < hi; i += kTL)
+            if (ar0 + i < O.ar_cap) ar4[ar0 + i] = R[i - ph];
+        __syncthreads();
+    }
+#else
+    while (live) {
+        frame(a, live, is_ar, rec);
+        if (is_ar) {
+            if (idx[0] < O.ar_cap) ar4[idx[0]] = rec;
+            ++idx[0];
+        }
     }
 #endif
 }

@@ -430,6 +430,12 @@ class Engine:
                     "mpx_replay_durable")
         return recs, op, key, val, last, int(sc[0]), int(sc[1])
 
+    def replay_durable_reserve(self, max_len, inst_cap):
+        """scratch for the binned slot maximum of replay_durable_dev calls up to max_len bytes
+        over inst_cap slots (without it the device form takes one atomic per record)"""
+        self._check(self.lib.mpx_replay_durable_reserve(self.h, max_len, inst_cap),
+                    "mpx_replay_durable_reserve")
+
     def replay_durable_dev(self, d_log, nbytes, inst_cap, d_recs, d_op, d_key, d_val, d_last,
                            d_scalars, stream=None, rec_base=0):
         self._check(self.lib.mpx_replay_durable_dev(self.h, d_log, nbytes, inst_cap, rec_base,

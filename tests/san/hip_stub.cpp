@@ -328,5 +328,6 @@ hipError_t launch_encode_log(int, const mpx_log_rec*, uint64_t, const uint64_t*,
                              uint64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_replay_durable(const uint8_t*, uint64_t, int32_t, int32_t, mpx_log_rec*,
                                  uint8_t*, int64_t*, int64_t*, int32_t*, int32_t*, uint32_t*,
-                                 hipStream_t) { return hipSuccess; }
+                                 void*, uint64_t, hipStream_t) { return hipSuccess; }
+uint64_t replay_work_bytes(uint64_t n, int32_t) { return 16 * n + 256; }
 }  // namespace mpx

@@ -189,3 +189,49 @@ def test_replay_chunked(mk_engine):
             assert np.array_equal(got[4], want[4]) and got[5:] == want[5:]
             last, db, cu = got[4], got[5], got[6]
         assert np.array_equal(last, whole[4]) and (db, cu) == tuple(whole[5:])
+
+
+@pytest.mark.gpu
+def test_replay_dev_binned_and_atomic(mk_engine):
+    """mpx_replay_durable_dev with the reserved scratch (the binned slot maximum: pairs, bin
+    counts, scan, scatter, one LDS slice per 8192 slots) and without it (one device atomicMax per
+    record): the same slots as the oracle - ragged last bins, every record in one bin, heavy
+    repeats, a space past the binned limit (2^25 slots: the atomic form), rec_base offsets"""
+    e, o = mk_engine(5, R.MODE_MIN), Oracle()
+    cases = [(100003, 50000, 0), (70001, 3 * 8192 + 5, 17), (1 << 18, 1000, 5),
+             (4099, 8192, 0), (1000, (1 << 25) + 1, 3)]
+    with Arena(e) as hip:
+        for n, cap, base in cases:
+            log = durable_log(n, cap, n ^ cap, dup=True)
+            # slots from earlier chunks: below this call's rec_base (chunks replay in file order)
+            last0 = np.random.default_rng(n).integers(-1, max(base, 0) + 0, cap).astype(np.int32) \
+                if base else np.full(cap, -1, np.int32)
+            want = o.replay_durable(log, cap, 7, -1, rec_base=base, last_rec=last0)
+            for reserve in (True, False):
+                if reserve:
+                    e.replay_durable_reserve(len(log), cap)
+                d_log = hip.put(log)
+                d = [hip.put(np.zeros_like(w)) for w in want[:4]]
+                d_last = hip.put(last0)
+                d_sc = hip.put(np.array([7, -1], np.int32))
+                e.replay_durable_dev(d_log.ptr, len(log), cap, *[x.ptr for x in d], d_last.ptr,
+                                     d_sc.ptr, rec_base=base)
+                e.synchronize()
+                for x, w in zip(d, want[:4]):
+                    assert np.array_equal(hip.get(x), w), (n, cap, reserve)
+                assert np.array_equal(hip.get(d_last), want[4]), (n, cap, reserve)
+                assert hip.get(d_sc).tolist() == [want[5], want[6]], (n, cap, reserve)
+        # an instNo outside the space through the binned form: E_NIL_INSTANCE
+        from minpaxos_amd.engine import MpxError
+        log = durable_log(5000, 600, 99)  # instNos in [0, 300)
+        e.replay_durable_reserve(len(log), 100)
+        d_log = hip.put(log)
+        want = o.replay_durable(log, 600)
+        d = [hip.put(np.zeros_like(w)) for w in want[:4]]
+        d_last = hip.put(np.full(100, -1, np.int32))
+        d_sc = hip.put(np.array([0, -1], np.int32))
+        with pytest.raises(MpxError) as ei:
+            e.replay_durable_dev(d_log.ptr, len(log), 100, *[x.ptr for x in d], d_last.ptr,
+                                 d_sc.ptr)
+            e.synchronize()
+        assert ei.value.code == R.E_NIL_INSTANCE
