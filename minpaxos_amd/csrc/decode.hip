@@ -361,6 +361,18 @@ __global__ __launch_bounds__(256) void k_dec_tile_entries(const GEntry* __restri
 // The tile's bytes are staged in LDS; the true chain is walked per chunk twice (count, then
 // emit at the offsets of a block-wide exclusive scan of the counts).
 constexpr int kXPad = 20;  // bytes per exit map in LDS (17 used)
+#ifndef MPX_DEC_EMIT_REG
+#define MPX_DEC_EMIT_REG 1
+#endif
+constexpr int kDecRegAR = 10;          // a 128-byte chunk starts at most 10 AcceptReply frames
+constexpr uint32_t kDecRegCap = 1024;  // staged records per LDS pass (the tile image's space)
+// 4 bytes at LDS byte offset o from two aligned dword reads (o + 8 inside the buffer)
+__device__ __forceinline__ int32_t lds_le32(const uint8_t* B, uint32_t o) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(B) + (o >> 2);
+    const uint32_t sh = o & 3u;
+    const uint64_t x = ((uint64_t)w[1] << 32) | w[0];
+    return (int32_t)(uint32_t)(x >> (8 * sh));
+}
 __global__ __launch_bounds__(kTileLanes) void k_dec_emit(
     const uint8_t* __restrict__ buf, uint64_t len, const GEntry* __restrict__ tres,
     const ulonglong2* __restrict__ xmap, mpx_accept_reply* __restrict__ ar_out, uint64_t ar_cap,
@@ -475,26 +487,21 @@ __global__ __launch_bounds__(kTileLanes) void k_dec_emit(
     __syncthreads();
     uint32_t pre = inc - v;
     for (int w2 = 0; w2 < l / kWave; ++w2) pre += wsum[w2];
-    if (e == kXStop) return;
     uint64_t ar_i = r.ar + (pre & 0xFFFFu), oth_i = r.oth + (pre >> 16);
-    // walk 2: emit
-    for (uint32_t p = base + e; p < base + kChunk;) {
+    // walk 2, one frame at p: an AcceptReply comes back in rec (is_ar), any other frame is stored
+    // here; live = false after the chunk's last frame
+    auto frame = [&](uint32_t& p, bool& live, bool& is_ar, uint4& rec) {
+        is_ar = false;
         const uint32_t code = B[p];
         const uint32_t fl = frame_len(code);
-        if ((uint64_t)p >= tl || fl == 0 || (uint64_t)p + fl > tl) break;
-        if (code == MPX_PEER_ACCEPT_REPLY) {
-            const uint8_t* b = B + p + 1;  // Instance, OK, Ballot, Id (little endian)
-            mpx_accept_reply rec;
-            rec.instance = (int32_t)((uint32_t)b[0] | ((uint32_t)b[1] << 8) |
-                                     ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24));
-            rec.ok = b[4];
-            rec.ballot = (int32_t)((uint32_t)b[5] | ((uint32_t)b[6] << 8) |
-                                   ((uint32_t)b[7] << 16) | ((uint32_t)b[8] << 24));
-            rec.id = (int32_t)((uint32_t)b[9] | ((uint32_t)b[10] << 8) |
-                               ((uint32_t)b[11] << 16) | ((uint32_t)b[12] << 24));
-            rec.pad[0] = rec.pad[1] = rec.pad[2] = 0;
-            if (ar_i < ar_cap) ar_out[ar_i] = rec;
-            ++ar_i;
+        if ((uint64_t)p >= tl || fl == 0 || (uint64_t)p + fl > tl) {
+            live = false;
+            return;
+        }
+        if (code == MPX_PEER_ACCEPT_REPLY) {  // Instance, OK, Ballot, Id (little endian)
+            rec = make_uint4((uint32_t)lds_le32(B, p + 1), (uint32_t)lds_le32(B, p + 6),
+                             (uint32_t)lds_le32(B, p + 10), (uint32_t)B[p + 5]);
+            is_ar = true;
         } else {
             if (oth_i < oth_cap) {
                 mpx_peer_frame f;
@@ -506,7 +513,66 @@ __global__ __launch_bounds__(kTileLanes) void k_dec_emit(
             ++oth_i;
         }
         p += fl;
+        live = p < base + kChunk;
+    };
+    uint4* const ar4 = reinterpret_cast<uint4*>(ar_out);  // mpx_accept_reply as 4 dwords
+    uint32_t p = base + e;
+    bool live = e != kXStop;
+    bool is_ar;
+    uint4 rec;
+#if MPX_DEC_EMIT_REG
+    // the first kDecRegAR frames with their AcceptReplies in registers, then (the tile image dead)
+    // through LDS, so the tile's AcceptReplies leave as coalesced runs (stream.hip k_sd_emit)
+    uint32_t tot_ar = 0;
+    for (int w2 = 0; w2 < kTileLanes / kWave; ++w2) tot_ar += wsum[w2] & 0xFFFFu;
+    const uint64_t ar0 = r.ar;
+    uint4 rr[kDecRegAR];
+    uint32_t rl[kDecRegAR];  // tile-local index, ~0 = none
+#pragma clang loop unroll(full)
+    for (int it = 0; it < kDecRegAR; ++it) {
+        rl[it] = ~0u;
+        if (live) {
+            frame(p, live, is_ar, rec);
+            if (is_ar) {
+                rr[it] = rec;
+                rl[it] = ar_i < ar_cap ? (uint32_t)(ar_i - ar0) : ~0u;
+                ++ar_i;
+            }
+        }
     }
+    if (__syncthreads_or(live)) {  // a chunk with more frames: every record stored directly
+#pragma unroll
+        for (int it = 0; it < kDecRegAR; ++it)
+            if (rl[it] != ~0u) ar4[ar0 + rl[it]] = rr[it];
+        while (live) {
+            frame(p, live, is_ar, rec);
+            if (is_ar) {
+                if (ar_i < ar_cap) ar4[ar_i] = rec;
+                ++ar_i;
+            }
+        }
+        return;
+    }
+    uint4* const R = reinterpret_cast<uint4*>(B);
+    for (uint32_t ph = 0; ph < tot_ar; ph += kDecRegCap) {
+#pragma unroll
+        for (int it = 0; it < kDecRegAR; ++it)
+            if (rl[it] - ph < kDecRegCap) R[rl[it] - ph] = rr[it];
+        __syncthreads();
+        const uint32_t hi = tot_ar - ph < kDecRegCap ? tot_ar : ph + kDecRegCap;
+        for (uint32_t i = ph + (uint32_t)l; i < hi; i += kTileLanes)
+            if (ar0 + i < ar_cap) ar4[ar0 + i] = R[i - ph];
+        __syncthreads();
+    }
+#else
+    while (live) {
+        frame(p, live, is_ar, rec);
+        if (is_ar) {
+            if (ar_i < ar_cap) ar4[ar_i] = rec;
+            ++ar_i;
+        }
+    }
+#endif
 }
 
 __global__ void k_dec_empty(mpx_decode_result* res) {
