@@ -15,10 +15,10 @@
 // maximised in LDS instead:
 //   k_replay_durable  writes pair[i] = (rec_base + i) << 32 | instNo, coalesced (8 B / record)
 //   k_rb_count        a workgroup per chunk of kRbChunk pairs: LDS histogram of the bins
-//                     (kRbSlots instance slots each) into hist[bin][chunk], bin-major
+//                     (kRbSlots = 32768 instance slots each) into hist[bin][chunk], bin-major
 //   scan              scan.hpp over the bins x chunks counts (+1: the total)
-//   k_rb_scatter      the chunk's pairs to their bins' runs (LDS cursors; order inside a bin
-//                     is free, a maximum does not depend on it)
+//   k_rb_scatter      the chunk's pairs sorted by bin in LDS, then stored as the bins' runs
+//                     (order inside a bin is free: a maximum does not depend on it)
 //   k_rb_max          a workgroup per bin: the bin's slice of last_rec into LDS, one LDS
 //                     atomicMax per pair, the slice written back
 // 8 B x 4 of pair traffic per record + the slots read and written once, all coalesced.
@@ -65,12 +65,13 @@ __device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
     return v;
 }
 
-constexpr int kRbLg = 13;
-constexpr uint32_t kRbSlots = 1u << kRbLg;      // instance slots per bin (32 KB of LDS)
-constexpr uint32_t kRbMaxBins = 4096;           // the count / scatter LDS tables (16 KB)
+constexpr int kRbLg = 15;
+constexpr uint32_t kRbSlots = 1u << kRbLg;      // instance slots per bin (128 KB of LDS)
+constexpr uint32_t kRbMaxBins = 1024;           // the count / scatter LDS tables (4 KB)
 constexpr int64_t kRbMaxCap = (int64_t)kRbSlots * kRbMaxBins;  // 2^25 slots
 constexpr int kRbT = 1024;
-constexpr uint64_t kRbChunk = 64 * kRbT;        // pairs per count / scatter workgroup
+constexpr int kRbPer = 16;
+constexpr uint64_t kRbChunk = kRbPer * kRbT;    // pairs per count / scatter workgroup (128 KB)
 constexpr uint64_t kRbNone = ~0ull;             // an instNo outside [0, inst_cap): no slot
 
 // pairs: null = the atomic form
@@ -212,21 +213,61 @@ __global__ __launch_bounds__(kRbT) void k_rb_count(const uint64_t* __restrict__ 
     for (uint32_t b = threadIdx.x; b < bins; b += kRbT) hist[(uint64_t)b * chunks + blockIdx.x] = h[b];
 }
 
+// the chunk's pairs sorted by bin in LDS first (ranks from LDS counters, a block scan of the
+// counts), then stored in that order: consecutive lanes write consecutive positions of a bin's
+// run (~32 pairs per bin and chunk at 2^24 slots) instead of 64 random 8-byte stores per wave
+// instruction (0.30 -> see DESIGN §5)
 __global__ __launch_bounds__(kRbT) void k_rb_scatter(const uint64_t* __restrict__ pairs, uint64_t n,
                                                     uint32_t bins, uint32_t chunks,
                                                     const uint32_t* __restrict__ offs,
                                                     uint64_t* __restrict__ binned) {
-    __shared__ uint32_t cur[kRbMaxBins];
-    for (uint32_t b = threadIdx.x; b < bins; b += kRbT)
-        cur[b] = offs[(uint64_t)b * chunks + blockIdx.x];
+    __shared__ uint64_t sp[kRbChunk];
+    __shared__ uint32_t cnt[kRbMaxBins];  // counts, then the bins' starts in sp
+    __shared__ uint32_t gof[kRbMaxBins];  // the bins' first output position for this chunk
+    __shared__ uint32_t wtot[kRbT / kWave];
+    const int t = threadIdx.x, l = lane_id(), w = t / kWave;
+    for (uint32_t b = t; b < bins; b += kRbT) {
+        cnt[b] = 0;
+        gof[b] = offs[(uint64_t)b * chunks + blockIdx.x];
+    }
     __syncthreads();
     const uint64_t c0 = (uint64_t)blockIdx.x * kRbChunk;
-#pragma unroll 8
-    for (uint64_t k = threadIdx.x; k < kRbChunk; k += kRbT) {
-        const uint64_t i = c0 + k;
-        if (i >= n) break;
-        const uint64_t p = ld_stream(pairs + i);
-        if (p != kRbNone) binned[atomicAdd(&cur[(uint32_t)p >> kRbLg], 1u)] = p;
+    uint64_t p[kRbPer];
+    uint32_t rk[kRbPer];
+#pragma unroll
+    for (int k = 0; k < kRbPer; ++k) {
+        const uint64_t i = c0 + (uint64_t)(t + k * kRbT);
+        p[k] = i < n ? ld_stream(pairs + i) : kRbNone;
+    }
+#pragma unroll
+    for (int k = 0; k < kRbPer; ++k)
+        rk[k] = p[k] != kRbNone ? atomicAdd(&cnt[(uint32_t)p[k] >> kRbLg], 1u) : 0u;
+    __syncthreads();
+    // exclusive scan of the counts, one bin per thread (bins <= kRbT)
+    const uint32_t c = (uint32_t)t < bins ? cnt[t] : 0u;
+    uint32_t x = c;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (l >= d) x += y;
+    }
+    if (l == kWave - 1) wtot[w] = x;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (int v = 0; v < kRbT / kWave; ++v) {
+        before += v < w ? wtot[v] : 0u;
+        total += wtot[v];
+    }
+    if ((uint32_t)t < bins) cnt[t] = before + x - c;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kRbPer; ++k)
+        if (p[k] != kRbNone) sp[cnt[(uint32_t)p[k] >> kRbLg] + rk[k]] = p[k];
+    __syncthreads();
+    for (uint32_t i = t; i < total; i += kRbT) {
+        const uint64_t q = sp[i];
+        const uint32_t b = (uint32_t)q >> kRbLg;
+        binned[gof[b] + (i - cnt[b])] = q;
     }
 }
 
