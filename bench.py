@@ -251,8 +251,9 @@ def issue_roofline(kernel, key, kern_ms, hbm, path=""):
     per launch (counter database) against the issue peaks, and the SQ wave-cycle split (parked
     at s_waitcnt / barriers, issue-stalled, issuing: MI355X_MICROARCH.md, the three are disjoint
     and sum to SQ_WAVE_CYCLES). bound = "valu" / "lds" when that issue fraction is at least 0.5,
-    else "latency" when the waves are parked for most of their cycles (the HBM figures then carry
-    the row: achieved / peak / frac are its HBM numbers), else "issue-stall". Without a counter
+    else "latency" when parked is the largest of the three shares, "issue-stall" when issue
+    stalls are, else "issue (mixed)" (the HBM figures then carry the row: achieved / peak / frac
+    are its HBM numbers). Without a counter
     pass the bound stays "valu"  with achieved null."""
     ins = instr_for(key, path) or {}
     t = kern_ms * 1e-3
@@ -285,7 +286,10 @@ def issue_roofline(kernel, key, kern_ms, hbm, path=""):
                     "peak": PEAK_LDS_GIPS if use_lds else PEAK_VALU_GIPS,
                     "unit": "G wave-instr/s", "frac": fl if use_lds else fv})
     else:
-        out.update({"bound": "latency" if waits.get("SQ_WAIT_ANY", 0) >= 0.5 else "issue-stall",
+        wa, wi, ac = (waits.get(k, 0.0) for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+                                                   "SQ_ACTIVE_INST_ANY"))
+        out.update({"bound": "latency" if wa >= max(wi, ac) else
+                    "issue-stall" if wi >= ac else "issue (mixed)",
                     "achieved": hbm["achieved"], "peak": hbm["peak"], "unit": hbm["unit"],
                     "frac": hbm["frac"]})
     return out

@@ -9,6 +9,9 @@ import os
 import shutil
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from design_table import bound_label  # noqa: E402
+
 
 def main(src: str, dst: str) -> None:
     os.makedirs(dst, exist_ok=True)
@@ -33,14 +36,12 @@ def main(src: str, dst: str) -> None:
         rf, cb = d.get("roofline") or {}, d.get("cpu_baseline") or {}
         par = d.get("parity", {})
         hbm = rf.get("hbm") or rf  # issue-bound rows keep their HBM figures under "hbm"
-        bound = rf.get("bound", "hbm")
-        issue = ("%.3f of %s issue" % (rf["frac"], bound)) if bound != "hbm" and rf.get("frac") \
-            else ("%s (no counter pass)" % bound if bound != "hbm" else "-")
+        issue = bound_label(rf)
         cpu = ("%.3g (%s core)" % (cb["value"], cb.get("cores", "?"))) if cb.get("value") else "-"
         rows.append("| %s | %s | %.3g %s | %.3f | %.0f | %.3f | %s | %s | %s |" % (
             name, d["config"]["workload"], d["value"], d["unit"], d["ms_per_step"],
             hbm.get("achieved") or 0.0, hbm.get("frac") or 0.0, issue, cpu, par.get("bit_exact")))
-    print("| workload | shape | value | ms / launch | GB/s | frac of 8 TB/s | issue bound | CPU port | bit-exact |")
+    print("| workload | shape | value | ms / launch | GB/s | frac of 8 TB/s | bound (SQ counters) | CPU port | bit-exact |")
     print("|---|---|---|---|---|---|---|---|---|")
     print("\n".join(rows))
 
