@@ -103,7 +103,7 @@ __global__ __launch_bounds__(kTileBlock) void k_prepare_tile(
             const int4 r = S.rec[j < cnt ? a + j : 0];
             if (j < cnt && live_inst) step(r);
         }
-        for (uint64_t q = after; live_inst && q < oend; ++q) step(r4[q]);
+        for (uint64_t q = after; live_inst && q < oend; ++q) step(over_rec(S, r4, after, q));
         if (inwin && live_inst) {
             B.z = (int32_t)fl;
             st_stream(o4 + 2 * idx, A);

@@ -108,7 +108,7 @@ __global__ MPX_TALLY_ATTR __launch_bounds__(kTileBlock) void k_accept_tile(
             step(r, (j < cnt && inwin) ? 1 : 0);
         }
         // the overhang of the tile's last instance (one lane per tile)
-        for (uint64_t q = after; inwin && q < oend; ++q) step(r4[q], 1);
+        for (uint64_t q = after; inwin && q < oend; ++q) step(over_rec(S, r4, after, q), 1);
         if (inwin) {
             st_stream(reinterpret_cast<int4*>(st_out) + idx, st);
             if (decided) st_stream(decided + idx, (uint8_t)(deci ? 1 : 0));

@@ -34,12 +34,19 @@ struct TileLds {
     int4 rec[kTileRecs];                 // the tile's records
     uint16_t hpos[kTileRecs + 1];        // positions of the owned instances' first records
     uint32_t wcnt[kTilePer * kTileWaves];  // heads per (register k, wave), then their offsets
+    int4 ovr[kWave];                     // the records after the tile: the overhang's start
     uint32_t nh;                         // owned instances in the tile
     uint64_t oend;                       // end of the last owned instance's overhang
     int64_t onext;                       // instance of the record at oend (kNoNext: none)
 };
 
 constexpr int64_t kNoNext = INT64_MAX;  // no record follows the instance in the log
+
+// record q of the tile's last instance's overhang [after, oend): the first kWave from LDS
+__device__ __forceinline__ int4 over_rec(const TileLds& S, const int4* __restrict__ recs,
+                                         uint64_t after, uint64_t q) {
+    return q - after < (uint64_t)kWave ? S.ovr[q - after] : recs[q];
+}
 
 __device__ __forceinline__ int4 tile_load(const int4* __restrict__ recs, uint64_t n, uint64_t p) {
     return p < n ? ld_stream(recs + p) : make_int4(0, 0, 0, 0);
@@ -123,9 +130,13 @@ __device__ __forceinline__ void tile_walk(TileLds& S, const int4* __restrict__ r
             int64_t onext = after < n ? (int64_t)after_inst : kNoNext;
             if (after < n && cnt && after_inst == S.rec[cnt - 1].x) {
                 const int32_t inst = after_inst;
-                for (uint64_t q = after + 1;; q += kWave) {
+                // whole records, so the first 64 of the overhang reach its lane through LDS
+                // instead of one dependent global load per record (over_rec)
+                for (uint64_t q = after;; q += kWave) {
                     const uint64_t p = q + l;
-                    const int32_t pi = p < n ? recs[p].x : 0;
+                    const int4 rr = p < n ? recs[p] : make_int4(0, 0, 0, 0);
+                    if (q == after) S.ovr[l] = rr;
+                    const int32_t pi = rr.x;
                     const bool stop = p >= n || pi != inst;
                     const unsigned long long m = __ballot(stop);
                     if (m) {
