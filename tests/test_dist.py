@@ -213,3 +213,21 @@ def test_bench_launcher_rank_failure_exits_nonzero(stub_lib):
                "--no-cpu-baseline", devices=1, timeout=180)
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+@pytest.mark.parametrize("P,g_total", [(2, 64), (3, 37)])
+def test_bench_emulate_world(stub_lib, P, g_total):
+    """`--emulate-world P`: one process runs rank 0's share of a P-rank job (groups
+    [0, ceil(g_total / P)) under the launcher's block split) with the full watermark vector
+    through the engine's all-reduce; the owned range must hold the oracle's watermarks and every
+    foreign entry must stay -1 (watermark_allreduce_ok), and the line names the emulation"""
+    r = _bench(stub_lib, "--emulate-world", str(P), "--groups-total", str(g_total), "--steps", "2",
+               "--warmup", "1", "--no-cpu-baseline", devices=1)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    import json
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    emu = line["emulated_world"]
+    assert emu["ranks"] == P and emu["groups_total"] == g_total
+    assert 0 < emu["groups_on_this_rank"] < g_total
+    assert line["watermark_allreduce_ok"] and line["parity"]["bit_exact"], line["parity"]
+    assert "EMULATED" in line["config"]["workload"]

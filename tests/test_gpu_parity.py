@@ -778,3 +778,52 @@ def test_group_step_fused_totals(mk_engine, kind):
                 e.step_totals_dev(gb, tot2.ptr, e.stream)
                 e.stream_synchronize(e.stream)
                 assert ar.get(tot2).tolist() == want
+
+
+@pytest.mark.gpu
+def test_group_step_graph_replay(mk_engine):
+    """mpx_graph_begin / _end / _launch: a group step (+ its totals) captured on a stream and
+    replayed from the graph three times gives the oracle's outputs and totals every time (the
+    captured kernels' control words reset themselves, so replays are independent); what
+    bench.py's one-process line replays"""
+    from minpaxos_amd.devbuf import Arena
+    N, K = 5, 256
+    b = synth.group_batch(300, 256, N, 4, 256, seed=91)
+    b.setdefault("has_cmds", None)
+    e, o = mk_engine(N, R.MODE_MIN, kv_per_group=K), Oracle(N, R.MODE_MIN, kv_per_group=K)
+    want = o.group_step(b)
+    want_tot = _want_totals(b, want)
+    # the commands the step executes (the rest keep whatever ret / conf held)
+    G, ipg = b["n_groups"], b["ipg"]
+    coff = b["cmd_off"].astype(np.int64)
+    ex = np.zeros(len(b["op"]), bool)
+    for g in range(G):
+        lo, eo = max(int(b["executed_in"][g]) + 1, 0), int(want["executed_out"][g])
+        if lo <= eo < ipg:
+            ex[coff[g * ipg + lo]:coff[g * ipg + eo + 1]] = True
+    assert ex.any()
+    s = e.stream_create()
+    with Arena(e) as ar:
+        gb, d = _dev_group_batch(ar, b, N, K, True)
+        tot = ar.full(3, np.int64, 0x55)
+        e.graph_begin(s)
+        e.group_step_totals_dev(gb, tot.ptr, s)
+        g = e.graph_end(s)
+        try:
+            for _ in range(3):
+                for x in ("co", "eo", "ret", "conf"):  # poison what the replay must rewrite
+                    e.memset(d[x].ptr, 0x77, d[x].nbytes, s)
+                e.graph_launch(g, s)
+                e.stream_synchronize(s)
+                assert ar.get(tot).tolist() == want_tot
+                assert np.array_equal(ar.get(d["co"]), want["committed_out"])
+                assert np.array_equal(ar.get(d["eo"]), want["executed_out"])
+                ret, conf = ar.get(d["ret"]), ar.get(d["conf"])
+                assert np.array_equal(ret[ex], want["ret"][ex])
+                assert np.array_equal(conf[ex], want["conf_prev"][ex])
+                assert (ret[~ex] == 0x7777777777777777).all() and (conf[~ex] == 0x77).all()
+                assert np.array_equal(ar.get(d["st_out"]).view(np.int32),
+                                      want["st_out"].view(np.int32))
+        finally:
+            e.graph_destroy(g)
+            e.stream_destroy(s)
