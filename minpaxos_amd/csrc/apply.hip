@@ -321,6 +321,7 @@ struct SlotPos {
     int32_t pos;
 };
 struct SegMax {
+    static constexpr bool kCommutes = false;  // segmented: order matters
     __device__ __forceinline__ SlotPos operator()(SlotPos a, SlotPos b) const {
         return SlotPos{b.slot, a.slot == b.slot && a.pos > b.pos ? a.pos : b.pos};
     }

@@ -64,13 +64,25 @@ __global__ __launch_bounds__(kScT) void k_scan_reduce(In in, uint64_t n, T* __re
     __shared__ T ws[kScWaves];
     const int l = lane_id(), w = threadIdx.x / kWave;
     const uint64_t w0 = (uint64_t)blockIdx.x * kScTile + (uint64_t)w * kScWaveItems;
-    T acc = id;
+    // every round's item loaded before the first is combined (a loop that loaded round r + 1
+    // only after combining round r waited for 16 dependent loads per wave), then combined in
+    // index order (op need not be commutative)
+    T xs[kScRounds];
+#pragma unroll
     for (int r = 0; r < kScRounds; ++r) {
-        const uint64_t i0 = w0 + (uint64_t)r * kWave;
-        if (i0 >= n) break;  // uniform over the wave
-        const uint64_t i = i0 + l;
-        const T v = wave_incl_scan(i < n ? in(i) : id, op);
-        acc = op(acc, shfl_any(v, kWave - 1));
+        const uint64_t i = w0 + (uint64_t)r * kWave + l;
+        xs[r] = i < n ? in(i) : id;
+    }
+    T acc = id;
+    if constexpr (Op::kCommutes) {  // a sum: each lane folds its rounds, then one wave reduction
+#pragma unroll
+        for (int r = 0; r < kScRounds; ++r) acc = op(acc, xs[r]);
+#pragma unroll
+        for (int d = kWave / 2; d >= 1; d >>= 1) acc = op(acc, shfl_any(acc, l ^ d));
+    } else {
+#pragma unroll
+        for (int r = 0; r < kScRounds; ++r)
+            acc = op(acc, shfl_any(wave_incl_scan(xs[r], op), kWave - 1));
     }
     if (l == 0) ws[w] = acc;
     __syncthreads();
@@ -137,6 +149,52 @@ __global__ __launch_bounds__(kScT) void k_scan_tiles(In in, uint64_t n, const T*
     }
 }
 
+// k_scan_tiles for a commutative op (sums): each wave's 1024 items go through LDS so that a lane
+// holds 16 CONSECUTIVE items, scans them serially, and one wave scan of the lane totals replaces
+// a wave scan per round (16 x 6 shuffle steps, of 64-bit values for the log offsets); the
+// prefixes go back through LDS so the loads and the out() stores stay coalesced
+template <typename T, typename Op, typename In, typename Out>
+__global__ __launch_bounds__(kScT) void k_scan_tiles_c(In in, uint64_t n, const T* __restrict__ tot,
+                                                      Op op, T id, Out out) {
+    constexpr int kPad = kScWaveItems + kScWaveItems / kScRounds;  // one pad slot per 16 items
+    __shared__ T tx[kScWaves][kPad];
+    __shared__ T ws[kScWaves];
+    const int l = lane_id(), w = threadIdx.x / kWave;
+    const uint64_t w0 = (uint64_t)blockIdx.x * kScTile + (uint64_t)w * kScWaveItems;
+    auto at = [](int j) { return j + j / kScRounds; };  // item j of the wave's run -> LDS slot
+    T xs[kScRounds];
+#pragma unroll
+    for (int r = 0; r < kScRounds; ++r) {
+        const uint64_t i = w0 + (uint64_t)r * kWave + l;
+        xs[r] = i < n ? in(i) : id;
+        tx[w][at(r * kWave + l)] = xs[r];
+    }
+    __syncthreads();
+    T pre[kScRounds];  // exclusive prefixes of the lane's 16 consecutive items
+    T run = id;
+#pragma unroll
+    for (int j = 0; j < kScRounds; ++j) {
+        pre[j] = run;
+        run = op(run, tx[w][at(l * kScRounds + j)]);
+    }
+    const T incl = wave_incl_scan(run, op);
+    const T up = shfl_up_any(incl, 1);  // every lane takes part in the shuffle
+    const T lane_ex = l ? up : id;
+    if (l == kWave - 1) ws[w] = incl;
+    __syncthreads();
+    T carry = tot[blockIdx.x];
+    for (int x = 0; x < w; ++x) carry = op(carry, ws[x]);
+    carry = op(carry, lane_ex);
+#pragma unroll
+    for (int j = 0; j < kScRounds; ++j) tx[w][at(l * kScRounds + j)] = op(carry, pre[j]);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kScRounds; ++r) {
+        const uint64_t i = w0 + (uint64_t)r * kWave + l;
+        if (i < n) out(i, tx[w][at(r * kWave + l)], xs[r]);
+    }
+}
+
 // scratch: one T per tile
 template <typename T>
 __host__ __forceinline__ uint64_t scan_scratch_bytes(uint64_t n) {
@@ -150,14 +208,23 @@ hipError_t device_scan(In in, Out out, uint64_t n, Op op, T id, T* scratch, hipS
     if (tiles >= (1ull << 31)) return hipErrorInvalidValue;
     k_scan_reduce<T, Op, In><<<(unsigned)tiles, kScT, 0, stream>>>(in, n, scratch, op, id);
     k_scan_totals<T, Op><<<1, kScTotT, 0, stream>>>(scratch, tiles, op, id);
-    k_scan_tiles<T, Op, In, Out><<<(unsigned)tiles, kScT, 0, stream>>>(in, n, scratch, op, id, out);
+    if constexpr (Op::kCommutes)
+        k_scan_tiles_c<T, Op, In, Out><<<(unsigned)tiles, kScT, 0, stream>>>(in, n, scratch, op, id,
+                                                                             out);
+    else
+        k_scan_tiles<T, Op, In, Out><<<(unsigned)tiles, kScT, 0, stream>>>(in, n, scratch, op, id,
+                                                                           out);
     return hipGetLastError();
 }
 
+// an op's kCommutes lets the tile reduction fold in any order (sums); order-sensitive ops (the
+// segmented max-scan) combine in index order
 struct ScanSum64 {
+    static constexpr bool kCommutes = true;
     __device__ __forceinline__ uint64_t operator()(uint64_t a, uint64_t b) const { return a + b; }
 };
 struct ScanSum32 {
+    static constexpr bool kCommutes = true;
     __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; }
 };
 
