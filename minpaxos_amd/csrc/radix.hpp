@@ -14,6 +14,8 @@
 // The passes alternate between the output and a scratch buffer so the last one writes the
 // output (the input is only read).
 #pragma once
+#include <type_traits>
+
 #include "common.hpp"
 #include "scan.hpp"
 
@@ -25,6 +27,9 @@ constexpr int kRsRounds = 16;
 constexpr int kRsWaveItems = kWave * kRsRounds;    // 1024
 constexpr int kRsTile = kRsWaveItems * kRsWaves;   // 4096
 constexpr int kRsDigits = 256;
+#ifndef MPX_RS_LDS  // the scatter's tile digit-sorted in LDS before the stores (A/B: 0)
+#define MPX_RS_LDS 1
+#endif
 
 struct RsNoValue {};
 
@@ -60,6 +65,12 @@ __global__ __launch_bounds__(kRsT) void k_rs_scatter(const K* __restrict__ kin, 
     constexpr bool kVals = !__is_same(V, RsNoValue);
     __shared__ uint32_t cnt[kRsWaves][kRsDigits];
     __shared__ uint32_t base[kRsDigits];
+#if MPX_RS_LDS
+    __shared__ uint32_t tst[kRsDigits];  // the digits' first positions in the sorted tile
+    __shared__ uint32_t wtot[kRsWaves];
+    __shared__ K sk[kRsTile];
+    __shared__ typename std::conditional<kVals, V, char>::type sv[kVals ? kRsTile : 1];
+#endif
     const int t = threadIdx.x, l = lane_id(), w = t / kWave;
     const uint64_t below = lanes_below(l);
 #pragma unroll
@@ -92,6 +103,7 @@ __global__ __launch_bounds__(kRsT) void k_rs_scatter(const K* __restrict__ kin, 
         if (live && !(peers >> l >> 1)) cnt[w][d] = run + (uint32_t)popc(peers);  // last lane
     }
     __syncthreads();
+    uint32_t tot_d;  // this thread's digit: its count in the tile
     {  // per digit: the earlier waves' counts
         uint32_t p = 0;
 #pragma unroll
@@ -100,7 +112,47 @@ __global__ __launch_bounds__(kRsT) void k_rs_scatter(const K* __restrict__ kin, 
             cnt[x][t] = p;
             p += c;
         }
+        tot_d = p;
     }
+#if MPX_RS_LDS
+    // the tile digit-sorted in LDS first, then stored in that order: consecutive threads write
+    // consecutive positions of a digit's run (a tile holds ~16 elements per digit) instead of
+    // each wave instruction landing in up to 64 runs
+    {  // the digits' starts in the tile (block exclusive scan of the 256 counts)
+        uint32_t x = tot_d;
+#pragma unroll
+        for (int d2 = 1; d2 < kWave; d2 <<= 1) {
+            const uint32_t y = __shfl_up(x, d2);
+            if (l >= d2) x += y;
+        }
+        if (l == kWave - 1) wtot[w] = x;
+        __syncthreads();
+        uint32_t before = 0;
+#pragma unroll
+        for (int x2 = 0; x2 < kRsWaves; ++x2) before += x2 < w ? wtot[x2] : 0u;
+        tst[t] = before + x - tot_d;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRsRounds; ++r) {
+        const uint64_t i = w0 + (uint64_t)r * kWave + l;
+        if (i >= n) continue;
+        const uint32_t d = rs_digit(k[r], sh, mask);
+        const uint32_t pos = tst[d] + cnt[w][d] + rk[r];
+        sk[pos] = k[r];
+        if constexpr (kVals) sv[pos] = v[r];
+    }
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * kRsTile;
+    const uint32_t tn = (uint32_t)(n - t0 < (uint64_t)kRsTile ? n - t0 : (uint64_t)kRsTile);
+    for (uint32_t i = t; i < tn; i += kRsT) {
+        const K kk = sk[i];
+        const uint32_t d = rs_digit(kk, sh, mask);
+        const uint64_t dst = (uint64_t)base[d] + (i - tst[d]);
+        kout[dst] = kk;
+        if constexpr (kVals) vout[dst] = sv[i];
+    }
+#else
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kRsRounds; ++r) {
@@ -111,6 +163,7 @@ __global__ __launch_bounds__(kRsT) void k_rs_scatter(const K* __restrict__ kin, 
         kout[dst] = k[r];
         if constexpr (kVals) vout[dst] = v[r];
     }
+#endif
 }
 
 struct RsHistIn {
