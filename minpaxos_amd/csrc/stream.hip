@@ -275,6 +275,38 @@ __device__ __forceinline__ void chunk_dp(const uint32_t (&wd)[kC / 4], uint64_t 
     }
 }
 
+// The same DP reading each landing's value straight from the lane's LDS row (D[p + L]) instead
+// of selecting it from a 64-register window: a position costs ~12 VALU ops, an LDS read of its
+// landing (and of its length for a variable message) and the write of D[p], instead of ~45 VALU
+// ops of which six compare-selects each wait on a VCC hazard; the chain through LDS is hidden
+// by the other waves of the CU (stream 2.14 -> 2.02 ms MIN, 2.03 -> 1.87 CLASSIC; 0 = the
+// register window, A/B).
+#ifndef MPX_SD_DP_LDS
+#define MPX_SD_DP_LDS 1
+#endif
+template <bool kEdge>
+__device__ __forceinline__ void chunk_dp_lds(const uint32_t (&wd)[kC / 4], uint64_t c0,
+                                             uint64_t len, uint64_t lut, bool legacy, uint8_t* D) {
+#pragma unroll
+    for (int p = kC - 1; p >= 0; --p) {
+        const uint32_t code = (wd[p >> 2] >> ((p & 3) * 8)) & 0xFFu;
+        const uint32_t fl = lut_len(lut, code);
+        const uint32_t term = (uint32_t)kE + (uint32_t)p;
+        uint32_t L = fl;
+        if (fl == 0) L = legacy ? 0u : (uint32_t)D[p];  // a variable message's parsed length
+        const uint32_t q = (uint32_t)p + L;
+        const uint32_t dq = D[q < (uint32_t)kC ? q : 0];
+        uint32_t v = L == 0 ? term
+                     : q < (uint32_t)kC ? dq
+                     : q < (uint32_t)(kC + kE) ? q - (uint32_t)kC : term;
+        if (kEdge) {
+            const uint64_t a = c0 + (uint64_t)p;
+            if (a >= len || a + L > len) v = term;
+        }
+        D[p] = (uint8_t)v;
+    }
+}
+
 // 16 groups of 8 chunks: G[g][e] = where entry e of chunk 8g leaves chunk 8g+7 (kTerm: a
 // terminal on the way); X[c][e] are chunk maps with terminals as kTerm or >= kE
 __device__ __forceinline__ void chunk_groups(const uint8_t* X, int xstride, uint8_t (*G)[kE]) {
@@ -333,10 +365,17 @@ __global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
         if (m_lo | m_hi)
             var_lengths(vby, P.len, c0, c0 + kC + kE - 1, P.proto, m_lo, m_hi, D[l]);
     }
+#if MPX_SD_DP_LDS
+    if (c0 + kC + 17 + kE > P.len)
+        chunk_dp_lds<true>(wd, c0, P.len, lut, P.legacy != 0, D[l]);
+    else
+        chunk_dp_lds<false>(wd, c0, P.len, lut, P.legacy != 0, D[l]);
+#else
     if (c0 + kC + 17 + kE > P.len)
         chunk_dp<true>(wd, c0, P.len, lut, P.legacy != 0, D[l]);
     else
         chunk_dp<false>(wd, c0, P.len, lut, P.legacy != 0, D[l]);
+#endif
     {  // this chunk's map (64 bytes) for the emit pass and the walk
         const uint32_t* src = reinterpret_cast<const uint32_t*>(D[l]);
         uint4* dst = reinterpret_cast<uint4*>(W.cmap + ((uint64_t)blockIdx.x * kTL + l) * kE);
