@@ -394,13 +394,21 @@ __global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
     }
 }
 
+// n bytes (a multiple of 16; both ends 16-byte aligned) from global memory into LDS, 16 per load
+// (the maps were staged a byte per load: 256 dependent-issue loads per thread)
+__device__ __forceinline__ void stage16(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                        uint32_t n) {
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    const uint4* g = reinterpret_cast<const uint4*>(src);
+    for (uint32_t i = threadIdx.x; i < n / 16; i += blockDim.x) d[i] = g[i];
+}
+
 // ---- pass B1: group maps (lane e walks entry e over the group's tile maps) --------------------
 __global__ __launch_bounds__(kE) void k_sd_group_maps(Work W, uint32_t n_tiles) {
-    __shared__ uint8_t S[kGT][kE];
+    __shared__ __attribute__((aligned(16))) uint8_t S[kGT][kE];
     const uint32_t g = blockIdx.x, first = g * kGT;
     const uint32_t nt = min((uint32_t)kGT, n_tiles - first);
-    for (uint32_t i = threadIdx.x; i < nt * kE; i += blockDim.x)
-        (&S[0][0])[i] = W.tmap[(uint64_t)first * kE + i];
+    stage16(&S[0][0], W.tmap + (uint64_t)first * kE, nt * kE);
     __syncthreads();
     uint8_t e = (uint8_t)threadIdx.x;
     for (uint32_t t = 0; t < nt && e != kTerm; ++t) e = S[t][e];
@@ -412,7 +420,7 @@ __global__ __launch_bounds__(kE) void k_sd_group_maps(Work W, uint32_t n_tiles) 
 // to the terminal tile, chunk and byte, classifies the frame there and writes the result.
 __global__ __launch_bounds__(64) void k_sd_walk(SParams P, Work W, uint32_t n_tiles,
                                                  uint32_t n_groups, mpx_stream_result* res) {
-    __shared__ uint8_t S[kGT][kE];
+    __shared__ __attribute__((aligned(16))) uint8_t S[kGT][kE];
     __shared__ uint32_t st[3];  // entry, terminal group (n_groups = none), its entry
     const int t = threadIdx.x;
     if (t == 0) {
@@ -432,8 +440,7 @@ __global__ __launch_bounds__(64) void k_sd_walk(SParams P, Work W, uint32_t n_ti
             for (uint32_t g = t; g < nb; g += blockDim.x) W.gent[b0 + g] = kDeadE;
             continue;
         }
-        for (uint32_t i = t; i < nb * kE; i += blockDim.x)
-            (&S[0][0])[i] = W.gmap[(uint64_t)b0 * kE + i];
+        stage16(&S[0][0], W.gmap + (uint64_t)b0 * kE, nb * kE);
         __syncthreads();
         if (t == 0) {
             uint32_t e = st[0], stop = st[1];
@@ -461,8 +468,7 @@ __global__ __launch_bounds__(64) void k_sd_walk(SParams P, Work W, uint32_t n_ti
     uint32_t e = st[2];
     // terminal tile within group gs
     const uint32_t first = gs * kGT, nt = min((uint32_t)kGT, n_tiles - first);
-    for (uint32_t i = t; i < nt * kE; i += blockDim.x)
-        (&S[0][0])[i] = W.tmap[(uint64_t)first * kE + i];
+    stage16(&S[0][0], W.tmap + (uint64_t)first * kE, nt * kE);
     __syncthreads();
     if (t == 0) {
         uint32_t ts = first;
@@ -535,7 +541,7 @@ __global__ __launch_bounds__(64) void k_sd_walk(SParams P, Work W, uint32_t n_ti
 
 // ---- pass B3: tile entries inside each group ---------------------------------------------------
 __global__ __launch_bounds__(kE) void k_sd_tile_entries(Work W, uint32_t n_tiles) {
-    __shared__ uint8_t S[kGT][kE];
+    __shared__ __attribute__((aligned(16))) uint8_t S[kGT][kE];
     const uint32_t g = blockIdx.x, first = g * kGT;
     const uint32_t nt = min((uint32_t)kGT, n_tiles - first);
     const uint8_t r = W.gent[g];
@@ -543,8 +549,7 @@ __global__ __launch_bounds__(kE) void k_sd_tile_entries(Work W, uint32_t n_tiles
         for (uint32_t t = threadIdx.x; t < nt; t += blockDim.x) W.tent[first + t] = kDeadE;
         return;
     }
-    for (uint32_t i = threadIdx.x; i < nt * kE; i += blockDim.x)
-        (&S[0][0])[i] = W.tmap[(uint64_t)first * kE + i];
+    stage16(&S[0][0], W.tmap + (uint64_t)first * kE, nt * kE);
     __syncthreads();
     if (threadIdx.x == 0) {
         uint8_t e = r;
