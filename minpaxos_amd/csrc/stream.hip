@@ -214,8 +214,7 @@ __device__ __forceinline__ uint32_t lut_len(uint64_t lut, uint32_t code) {
 }
 
 // Phase 1 (variable-length messages only): the bounded parse of every variable-message code of
-// the lane's chunk (bytes through L2), D[p] = its length if it lands no further than `lim`,
-// else 0 (terminal); the DP reads it back at p before writing D[p].
+// the lane's chunk (bytes through L2); D[p] = its landing in the DP's byte encoding (dp_enc).
 __device__ __noinline__ void var_lengths(const Bytes by, uint64_t len, uint64_t c0,
                                          uint64_t lim, int proto, uint64_t m_lo, uint64_t m_hi,
                                          uint8_t* D) {
@@ -225,86 +224,76 @@ __device__ __noinline__ void var_lengths(const Bytes by, uint64_t len, uint64_t 
             const int p = __ffsll((long long)m) - 1 + 64 * h;
             m &= m - 1;
             const VarRes r = parse_var(by, len, lim, c0 + (uint64_t)p, proto);
-            D[p] = r.st == kOk ? (uint8_t)r.f.len : (uint8_t)0;  // len <= kC + kE
+            const uint32_t q = (uint32_t)p + r.f.len;  // len <= kC + kE - 1 - p (the limit)
+            D[p] = (uint8_t)(r.st == kOk && q < (uint32_t)(kC + kE) ? q : 0xFFu);
         }
     }
 }
 
-// Phase 2: the backward DP over the chunk's positions in registers: w[k] = D[p + 1 + k] (the
-// window of the next kE positions; past the chunk it holds the exit offsets 0..kE-1). A fixed
-// frame takes its successor's value from the window at a compile-time offset; a variable one
-// reads its length and its landing's value from the LDS mirror D (only when some lane of the
-// wave has a variable-message code at p). kEdge: the chunk runs into the end of the buffer.
-template <bool kEdge>
-__device__ __forceinline__ void chunk_dp(const uint32_t (&wd)[kC / 4], uint64_t c0, uint64_t len,
-                                         uint64_t lut, bool legacy, uint8_t* D) {
-    uint32_t w[kE];
-#pragma unroll
-    for (int k = 0; k < kE; ++k) w[k] = (uint32_t)k;  // D[kC + k] = exit offset k
-#pragma unroll
-    for (int p = kC - 1; p >= 0; --p) {
-        const uint32_t code = (wd[p >> 2] >> ((p & 3) * 8)) & 0xFFu;
-        const uint32_t fl = lut_len(lut, code);
-        const uint32_t term = (uint32_t)kE + (uint32_t)p;
-        // fixed lengths 1, 9, 10, 13, 14, 17
-        uint32_t v = (w[0] & (0u - (uint32_t)(fl == 1))) | (w[8] & (0u - (uint32_t)(fl == 9))) |
-                     (w[9] & (0u - (uint32_t)(fl == 10))) | (w[12] & (0u - (uint32_t)(fl == 13))) |
-                     (w[13] & (0u - (uint32_t)(fl == 14))) | (w[16] & (0u - (uint32_t)(fl == 17)));
-        const bool var = fl == 0;
-        uint32_t L = fl;
-        if (__ballot(var && !legacy)) {  // wave-uniform: the slow operands only when needed
-            L = var ? (uint32_t)D[p] : fl;
-            const uint32_t q = (uint32_t)p + L;
-            const uint32_t dq = D[q < (uint32_t)kC ? q : 0];
-            const uint32_t vv = L == 0 ? term
-                                : q < (uint32_t)kC ? dq
-                                : q < (uint32_t)(kC + kE) ? q - (uint32_t)kC : term;
-            v = var ? vv : v;
-        } else if (var) {
-            v = term;  // legacy: stop at variable-length messages
-            L = 0;
-        }
-        if (kEdge) {
-            const uint64_t a = c0 + (uint64_t)p;
-            if (a >= len || a + L > len) v = term;
-        }
-        D[p] = (uint8_t)v;
-#pragma unroll
-        for (int k = kE - 1; k > 0; --k) w[k] = w[k - 1];
-        w[0] = v;
-    }
+// The DP's byte per position p (dp_enc): the landing q = p + length of the frame at p, which
+// is < kC for a landing inside the chunk (its value is D[q]), in [kC, kC + kE) for an exit (bit 7
+// set, bit 6 clear: exit q - kC), and 0xFF for a terminal at p (value kE + p).
+//
+// Phase 2a: the landings of the fixed-length frames, four positions per dword of chunk bytes.
+// v_perm_b32 looks the four codes up in an 8-byte table of length - 1 (0x7F for a variable
+// message) indexed by code - MPX_PEER_BEACON; every other code selects 0x00 or 0xFF, cleared to
+// 0 (a 1-byte frame); the positions are added bytewise (no carries: <= 0x7F + 128). Returns the
+// dword of landings; *var gets the variable-message positions as 4 bits.
+__device__ __forceinline__ uint32_t dp_landings(uint32_t w, uint32_t lut_lo, uint32_t lut_hi,
+                                                uint32_t pos4, uint32_t* var) {
+    const uint32_t h = w & 0x80808080u;
+    const uint32_t sel = (((w | 0x80808080u) - 0x06060606u) ^ 0x80808080u) | h;  // code - 6
+    const uint32_t y = __builtin_amdgcn_perm(lut_hi, lut_lo, sel);
+    const uint32_t hb = y & 0x80808080u;
+    const uint32_t y2 = y & ~(hb | (hb - (hb >> 7)));  // 0xFF bytes (out of the table) -> 0
+    const uint32_t z = y2 ^ 0x7F7F7F7Fu;                // zero bytes = variable messages
+    const uint32_t t = ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z | 0x7F7F7F7Fu);
+    *var = (((t >> 7) * 0x204081u) >> 21) & 0xFu;
+    return y2 + pos4;
+}
+static_assert(MPX_PEER_BEACON == 6, "dp_landings indexes the table by code - 6");
+
+// the byte mask of the 4 variable-message bits of a dword
+__device__ __forceinline__ uint32_t var_bytes(uint32_t nib) {
+    return ((nib * 0x204081u) & 0x01010101u) * 0xFFu;
 }
 
-// The same DP reading each landing's value straight from the lane's LDS row (D[p + L]) instead
-// of selecting it from a 64-register window: a position costs ~12 VALU ops, an LDS read of its
-// landing (and of its length for a variable message) and the write of D[p], instead of ~45 VALU
-// ops of which six compare-selects each wait on a VCC hazard; the chain through LDS is hidden
-// by the other waves of the CU (stream 2.14 -> 2.02 ms MIN, 2.03 -> 1.87 CLASSIC; 0 = the
-// register window, A/B).
-#ifndef MPX_SD_DP_LDS
-#define MPX_SD_DP_LDS 1
-#endif
-template <bool kEdge>
-__device__ __forceinline__ void chunk_dp_lds(const uint32_t (&wd)[kC / 4], uint64_t c0,
-                                             uint64_t len, uint64_t lut, bool legacy, uint8_t* D) {
-#pragma unroll
-    for (int p = kC - 1; p >= 0; --p) {
-        const uint32_t code = (wd[p >> 2] >> ((p & 3) * 8)) & 0xFFu;
-        const uint32_t fl = lut_len(lut, code);
-        const uint32_t term = (uint32_t)kE + (uint32_t)p;
-        uint32_t L = fl;
-        if (fl == 0) L = legacy ? 0u : (uint32_t)D[p];  // a variable message's parsed length
-        const uint32_t q = (uint32_t)p + L;
-        const uint32_t dq = D[q < (uint32_t)kC ? q : 0];
-        uint32_t v = L == 0 ? term
-                     : q < (uint32_t)kC ? dq
-                     : q < (uint32_t)(kC + kE) ? q - (uint32_t)kC : term;
-        if (kEdge) {
-            const uint64_t a = c0 + (uint64_t)p;
-            if (a >= len || a + L > len) v = term;
-        }
-        D[p] = (uint8_t)v;
+// the table of dp_landings for a protocol (kLutMin / kLutClassic: lengths by code - 6)
+__host__ __device__ constexpr uint64_t dp_table(uint64_t lut) {
+    uint64_t e = 0;
+    for (int i = 0; i < 8; ++i) {
+        const uint64_t fl = (lut >> (8 * i)) & 0xFFu;
+        e |= (fl ? fl - 1 : 0x7Fu) << (8 * i);
     }
+    return e;
+}
+
+// Phase 2b: the backward DP over the chunk's positions, in the lane's LDS row, with every
+// position a pointer: a position whose value is final (an exit or a terminal, bit 7 of its
+// landing byte) gets that value written to its own row byte first and points at itself, the
+// finals made four at a time (bytewise masks from bits 7 and 6). A position is then a byte
+// extract, the LDS read of its landing's value (already final: landings lie ahead) and the LDS
+// write of its own: ~3 VALU ops. Round 3's 64-register window compiled to ~45 VALU ops per
+// position and round 4's LDS form with a per-position length lookup and selects to ~25 (the
+// DP is issue-bound at 4 cycles per wave64 VALU op); the same DP with bit-mask selects in
+// place of the self-pointers (~11 ops) measured 2 % slower (stream 1.90 -> 1.65 / 1.62 ms
+// MIN, 1.62 -> 1.44 / 1.41 CLASSIC, profiles/r04/stream/ab_dp_self.txt).
+__device__ __forceinline__ void chunk_dp_self(uint32_t (&pw)[kC / 4], uint8_t* D) {
+    uint32_t* row = reinterpret_cast<uint32_t*>(D);
+#pragma unroll
+    for (int i = 0; i < kC / 4; ++i) {
+        const uint32_t x = pw[i];
+        const uint32_t f = x & 0x80808080u;
+        const uint32_t fmask = f | (f - (f >> 7));                  // finals
+        const uint32_t t = (x & (f >> 1)) & 0x40404040u;            // terminals
+        const uint32_t tmask = (t << 1) | ((t << 1) - (t >> 6));
+        const uint32_t self = (uint32_t)(4 * i) * 0x01010101u + 0x03020100u;
+        const uint32_t term = self + 0x40404040u;  // kE + p
+        row[i] = (x & 0x3F3F3F3Fu & ~tmask) | (term & tmask);
+        pw[i] = (x & ~fmask) | (self & fmask);
+    }
+#pragma unroll
+    for (int p = kC - 1; p >= 0; --p) D[p] = D[(pw[p >> 2] >> ((p & 3) * 8)) & 0xFFu];
 }
 
 // 16 groups of 8 chunks: G[g][e] = where entry e of chunk 8g leaves chunk 8g+7 (kTerm: a
@@ -352,30 +341,37 @@ __global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
             wd[i] = x;
         }
     }
-    const uint64_t lut = P.proto == MPX_MODE_MIN ? kLutMin : kLutClassic;
-    const Bytes vby{P.buf, nullptr, 0, 0};
-    if (!P.legacy) {
-        uint64_t m_lo = 0, m_hi = 0;  // positions of variable-message codes
+    const uint64_t tab = P.proto == MPX_MODE_MIN ? dp_table(kLutMin) : dp_table(kLutClassic);
+    const uint32_t tab_lo = (uint32_t)tab, tab_hi = (uint32_t)(tab >> 32);
+    uint64_t m_lo = 0, m_hi = 0;  // positions of variable-message codes
+#pragma unroll
+    for (int i = 0; i < kC / 4; ++i) {
+        uint32_t nib;
+        const uint32_t pos4 = (uint32_t)(4 * i + 1) * 0x01010101u + 0x03020100u;
+        wd[i] = dp_landings(wd[i], tab_lo, tab_hi, pos4, &nib);
+        if (P.legacy) wd[i] |= var_bytes(nib);  // stop at variable-length messages: terminal
+        if (i < 16) m_lo |= (uint64_t)nib << (4 * i); else m_hi |= (uint64_t)nib << (4 * (i - 16));
+    }
+    if (!P.legacy && (m_lo | m_hi)) {
+        const Bytes vby{P.buf, nullptr, 0, 0};
+        var_lengths(vby, P.len, c0, c0 + kC + kE - 1, P.proto, m_lo, m_hi, D[l]);
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(D[l]);
+#pragma unroll
+        for (int i = 0; i < kC / 4; ++i) {
+            const uint32_t nib = (uint32_t)((i < 16 ? m_lo >> (4 * i) : m_hi >> (4 * (i - 16))) & 0xFu);
+            const uint32_t vm = var_bytes(nib);
+            wd[i] = (wd[i] & ~vm) | (row[i] & vm);
+        }
+    }
+    if (c0 + kC + 17 + kE > P.len) {  // the end of the buffer: terminals (rare, per position)
 #pragma unroll
         for (int p = 0; p < kC; ++p) {
-            const uint32_t code = (wd[p >> 2] >> ((p & 3) * 8)) & 0xFFu;
-            const uint64_t bit = (uint64_t)(lut_len(lut, code) == 0) << (p & 63);
-            if (p < 64) m_lo |= bit; else m_hi |= bit;
+            const uint32_t sh = (p & 3) * 8, x = (wd[p >> 2] >> sh) & 0xFFu;
+            const uint64_t a = c0 + (uint64_t)p;
+            if (a >= P.len || (x < 0xC0u && a + (x - (uint32_t)p) > P.len)) wd[p >> 2] |= 0xFFu << sh;
         }
-        if (m_lo | m_hi)
-            var_lengths(vby, P.len, c0, c0 + kC + kE - 1, P.proto, m_lo, m_hi, D[l]);
     }
-#if MPX_SD_DP_LDS
-    if (c0 + kC + 17 + kE > P.len)
-        chunk_dp_lds<true>(wd, c0, P.len, lut, P.legacy != 0, D[l]);
-    else
-        chunk_dp_lds<false>(wd, c0, P.len, lut, P.legacy != 0, D[l]);
-#else
-    if (c0 + kC + 17 + kE > P.len)
-        chunk_dp<true>(wd, c0, P.len, lut, P.legacy != 0, D[l]);
-    else
-        chunk_dp<false>(wd, c0, P.len, lut, P.legacy != 0, D[l]);
-#endif
+    chunk_dp_self(wd, D[l]);
     {  // this chunk's map (64 bytes) for the emit pass and the walk
         const uint32_t* src = reinterpret_cast<const uint32_t*>(D[l]);
         uint4* dst = reinterpret_cast<uint4*>(W.cmap + ((uint64_t)blockIdx.x * kTL + l) * kE);
