@@ -297,17 +297,28 @@ __device__ __forceinline__ void chunk_dp_self(uint32_t (&pw)[kC / 4], uint8_t* D
 }
 
 // 16 groups of 8 chunks: G[g][e] = where entry e of chunk 8g leaves chunk 8g+7 (kTerm: a
-// terminal on the way); X[c][e] are chunk maps with terminals as kTerm or >= kE
+// terminal on the way); X[c][e] are chunk maps with terminals as kTerm or >= kE. A thread
+// follows its 8 (group, entry) chains one chunk at a time, so 8 LDS reads are in flight per
+// step instead of one chain of 64 dependent reads (branch-free: a terminal reads entry 0's
+// byte and stays terminal).
 __device__ __forceinline__ void chunk_groups(const uint8_t* X, int xstride, uint8_t (*G)[kE]) {
-    for (int t = threadIdx.x; t < (kTL / 8) * kE; t += kTL) {
-        const int g = t / kE;
-        uint32_t x = (uint32_t)(t % kE);
+    constexpr int kTasks = (kTL / 8) * kE / kTL;
+    static_assert((kTL / 8) * kE % kTL == 0, "whole tasks per thread");
+    uint32_t x[kTasks];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const uint32_t y = x < (uint32_t)kE ? X[(8 * g + c) * xstride + x] : kTerm;
-            x = y < (uint32_t)kE ? y : kTerm;
+    for (int j = 0; j < kTasks; ++j) x[j] = (uint32_t)((threadIdx.x + j * kTL) % kE);
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int j = 0; j < kTasks; ++j) {
+            const int g = (threadIdx.x + j * kTL) / kE;
+            const uint32_t y = X[(8 * g + c) * xstride + (x[j] & (uint32_t)(kE - 1))];
+            x[j] = (x[j] | y) >= (uint32_t)kE ? (uint32_t)kTerm : y;
         }
-        G[g][t % kE] = (uint8_t)x;
+#pragma unroll
+    for (int j = 0; j < kTasks; ++j) {
+        const int t = threadIdx.x + j * kTL;
+        G[t / kE][t % kE] = (uint8_t)x[j];
     }
 }
 
@@ -382,11 +393,21 @@ __global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
     __syncthreads();
     chunk_groups(&D[0][0], kDRow, G);
     __syncthreads();
-    if (l < kE) {  // the tile map: entry l through the 16 group maps
-        uint32_t x = (uint32_t)l;
+    {  // the tile map: the first and second 8 group maps composed by two halves of the
+       // workgroup side by side, then entry l through both
+        static_assert(kTL == 2 * kE && kTL / 8 == 16, "two halves of 8 group maps");
+        const int h = l / kE, e = l % kE;
+        uint32_t x = (uint32_t)e;
 #pragma unroll
-        for (int g = 0; g < kTL / 8; ++g) x = x == kTerm ? kTerm : G[g][x];
-        W.tmap[(uint64_t)blockIdx.x * kE + l] = (uint8_t)x;
+        for (int g = 0; g < 8; ++g) x = x >= (uint32_t)kE ? (uint32_t)kTerm : G[8 * h + g][x & (kE - 1)];
+        __syncthreads();
+        G[h][e] = (uint8_t)x;  // (rows 0 and 1 were read by this thread's half only before)
+        __syncthreads();
+        if (l < kE) {
+            const uint32_t y = G[0][l];
+            W.tmap[(uint64_t)blockIdx.x * kE + l] =
+                (uint8_t)(y >= (uint32_t)kE ? (uint32_t)kTerm : G[1][y]);
+        }
     }
 }
 

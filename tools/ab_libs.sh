@@ -16,7 +16,7 @@ for rep in 1 2; do
       MPX_LIB=$path timeout -k 10 300 python bench.py $args --no-cpu-baseline > $OUT/$name.json 2> $OUT/$name.err
       rc=$?
       [ $rc = 0 ] || { echo "$name rc=$rc"; tail -5 $OUT/$name.err; exit $rc; }
-      python3 -c "import json,sys; d=json.loads(open('$OUT/$name.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$name', '%.4f ms' % r['kernel_ms_avg'], 'step %.4f ms' % d['ms_per_step'], 'frac %.3f' % r['frac'], 'exact', d['parity']['bit_exact'])"
+      python3 -c "import json,sys; d=json.loads(open('$OUT/$name.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$name', '%.4f ms' % r['kernel_ms_avg'], 'step %.4f ms' % d['ms_per_step'], 'frac %s' % (r['frac'] if r['frac'] is None else round(r['frac'], 3)), 'exact', d['parity']['bit_exact'])"
     done
   done
 done
