@@ -420,16 +420,34 @@ __device__ __forceinline__ void stage16(uint8_t* __restrict__ dst, const uint8_t
     for (uint32_t i = threadIdx.x; i < n / 16; i += blockDim.x) d[i] = g[i];
 }
 
-// ---- pass B1: group maps (lane e walks entry e over the group's tile maps) --------------------
-__global__ __launch_bounds__(kE) void k_sd_group_maps(Work W, uint32_t n_tiles) {
+// ---- pass B1: group maps --------------------------------------------------------------------
+// The group's 256 tile maps in kParts parts of 32: thread (q, e) follows entry e through part
+// q (8 chains of 32 dependent LDS reads side by side instead of one of 256), then entry e runs
+// through the 8 part maps.
+constexpr int kParts = 8;
+constexpr int kPartTiles = kGT / kParts;
+__device__ __forceinline__ void part_maps(const uint8_t (*S)[kE], uint32_t nt, uint8_t (*Q)[kE]) {
+    const uint32_t q = threadIdx.x / kE, e = threadIdx.x % kE;
+    const uint32_t t0 = q * kPartTiles, t1 = min(t0 + (uint32_t)kPartTiles, nt);
+    uint32_t x = e;
+    for (uint32_t t = t0; t < t1; ++t) x = x >= (uint32_t)kE ? (uint32_t)kTerm : S[t][x];
+    Q[q][e] = (uint8_t)x;
+}
+__global__ __launch_bounds__(kParts * kE) void k_sd_group_maps(Work W, uint32_t n_tiles) {
     __shared__ __attribute__((aligned(16))) uint8_t S[kGT][kE];
+    __shared__ uint8_t Q[kParts][kE];
     const uint32_t g = blockIdx.x, first = g * kGT;
     const uint32_t nt = min((uint32_t)kGT, n_tiles - first);
     stage16(&S[0][0], W.tmap + (uint64_t)first * kE, nt * kE);
     __syncthreads();
-    uint8_t e = (uint8_t)threadIdx.x;
-    for (uint32_t t = 0; t < nt && e != kTerm; ++t) e = S[t][e];
-    W.gmap[(uint64_t)g * kE + threadIdx.x] = e;
+    part_maps(S, nt, Q);
+    __syncthreads();
+    if (threadIdx.x < kE) {
+        uint32_t x = threadIdx.x;
+#pragma unroll
+        for (int q = 0; q < kParts; ++q) x = x >= (uint32_t)kE ? (uint32_t)kTerm : Q[q][x];
+        W.gmap[(uint64_t)g * kE + threadIdx.x] = (uint8_t)x;
+    }
 }
 
 // ---- pass B2: the true chain over the group maps, then the exact stop ------------------------
@@ -557,8 +575,10 @@ __global__ __launch_bounds__(64) void k_sd_walk(SParams P, Work W, uint32_t n_ti
 }
 
 // ---- pass B3: tile entries inside each group ---------------------------------------------------
-__global__ __launch_bounds__(kE) void k_sd_tile_entries(Work W, uint32_t n_tiles) {
+__global__ __launch_bounds__(kParts * kE) void k_sd_tile_entries(Work W, uint32_t n_tiles) {
     __shared__ __attribute__((aligned(16))) uint8_t S[kGT][kE];
+    __shared__ uint8_t Q[kParts][kE];
+    __shared__ uint8_t E[kParts];
     const uint32_t g = blockIdx.x, first = g * kGT;
     const uint32_t nt = min((uint32_t)kGT, n_tiles - first);
     const uint8_t r = W.gent[g];
@@ -568,11 +588,22 @@ __global__ __launch_bounds__(kE) void k_sd_tile_entries(Work W, uint32_t n_tiles
     }
     stage16(&S[0][0], W.tmap + (uint64_t)first * kE, nt * kE);
     __syncthreads();
+    part_maps(S, nt, Q);  // (as in k_sd_group_maps: the parts' maps, then the parts' entries)
+    __syncthreads();
     if (threadIdx.x == 0) {
-        uint8_t e = r;
-        for (uint32_t t = 0; t < nt; ++t) {
-            W.tent[first + t] = e;
-            e = e == kDeadE ? kDeadE : S[t][e];  // kTerm == kDeadE: the tiles after are dead
+        uint32_t x = r;
+        for (int q = 0; q < kParts; ++q) {
+            E[q] = (uint8_t)x;
+            x = x >= (uint32_t)kE ? (uint32_t)kDeadE : Q[q][x];  // kTerm == kDeadE
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < kParts) {  // part q's tiles from its entry
+        const uint32_t q = threadIdx.x, t0 = q * kPartTiles, t1 = min(t0 + (uint32_t)kPartTiles, nt);
+        uint32_t e = E[q];
+        for (uint32_t t = t0; t < t1; ++t) {
+            W.tent[first + t] = (uint8_t)e;
+            e = e >= (uint32_t)kE ? (uint32_t)kDeadE : S[t][e];  // the tiles after are dead
         }
     }
 }
@@ -1107,9 +1138,9 @@ hipError_t launch_decode_stream(int proto, int legacy, const uint8_t* buf, uint6
     Outs O{outs.ar, outs.ar_cap, outs.prep, outs.prep_cap, outs.var, outs.var_cap, outs.oth,
            outs.oth_cap};
     k_sd_tile_maps<<<tiles, kTL, 0, stream>>>(P, W);
-    k_sd_group_maps<<<groups, kE, 0, stream>>>(W, tiles);
+    k_sd_group_maps<<<groups, kParts * kE, 0, stream>>>(W, tiles);
     k_sd_walk<<<1, 64, 0, stream>>>(P, W, tiles, groups, res);
-    k_sd_tile_entries<<<groups, kE, 0, stream>>>(W, tiles);
+    k_sd_tile_entries<<<groups, kParts * kE, 0, stream>>>(W, tiles);
     k_sd_count<<<tiles, kTL, 0, stream>>>(P, W);
     k_sd_scan<<<(tiles + kScanT - 1) / kScanT, kScanT, 0, stream>>>(W, tiles);
     k_sd_emit<<<tiles, kTL, 0, stream>>>(P, W, O, tiles, res);
