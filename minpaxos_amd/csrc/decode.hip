@@ -244,28 +244,88 @@ __global__ __launch_bounds__(kTileLanes) void k_dec_tile_maps(const uint8_t* __r
     }
 }
 
-// ---- pass B1: group maps (a group = 256 consecutive tiles; lane e walks entry e) -------------
+// The map walks of passes B1-B3 follow 256 maps in kDParts parts of 32 side by side: thread
+// (q, e) takes entry e through part q (8 x 17 chains of 32 dependent LDS reads instead of 17 of
+// 256), one thread chains the 8 part maps from the run's entry, and 8 threads then walk their
+// parts from their part's entry where every map's entry is wanted (gres, tres).
+constexpr int kDParts = 8;
+constexpr uint32_t kDPer = kGroupTiles / kDParts;
+__device__ __forceinline__ void dec_part_maps(const GEntry (*S)[kEntries], uint32_t n,
+                                              GEntry (*Q)[kEntries]) {
+    const uint32_t t = threadIdx.x;
+    if (t < (uint32_t)(kDParts * kEntries)) {
+        const uint32_t q = t / kEntries, e = t % kEntries;
+        const uint32_t t0 = q * kDPer, t1 = min(t0 + kDPer, n);
+        GEntry a{e, 0, 0};
+        for (uint32_t k = t0; k < t1 && !(a.pos & kGStop); ++k) {
+            const GEntry y = S[k][a.pos];
+            a = GEntry{y.pos, a.ar + y.ar, a.oth + y.oth};
+        }
+        Q[q][e] = a;
+    }
+}
+// thread 0: the parts' entries from the run's entry r (pos kDead: past the stop); returns the
+// state after the run ({pos, ar, oth} with pos = kGStop | stop position once stopped)
+__device__ __forceinline__ GEntry dec_part_entries(const GEntry (*Q)[kEntries], GEntry r, GEntry* PE) {
+    for (int q = 0; q < kDParts; ++q) {
+        PE[q] = (r.pos & kGStop) ? GEntry{kDead, r.ar, r.oth} : r;
+        if (!(r.pos & kGStop)) {
+            const GEntry y = Q[q][r.pos];
+            r = GEntry{y.pos, r.ar + y.ar, r.oth + y.oth};
+        }
+    }
+    return r;
+}
+// threads q < kDParts: part q's maps from its entry, out[k] = {entry, ar, oth before map k}
+// (kDead entries past the stop)
+__device__ __forceinline__ void dec_part_walk(const GEntry (*S)[kEntries], uint32_t n,
+                                              const GEntry* PE, GEntry* out, bool keep_counts) {
+    const uint32_t q = threadIdx.x;
+    if (q >= (uint32_t)kDParts) return;
+    const uint32_t t0 = q * kDPer, t1 = min(t0 + kDPer, n);
+    uint32_t e = PE[q].pos, ar = PE[q].ar, oth = PE[q].oth;
+    bool dead = e == kDead;
+    for (uint32_t k = t0; k < t1; ++k) {
+        if (dead) {
+            out[k] = keep_counts ? GEntry{kDead, ar, oth} : GEntry{kDead, 0, 0};
+            continue;
+        }
+        out[k] = GEntry{e, ar, oth};
+        const GEntry x = S[k][e];
+        ar += x.ar;
+        oth += x.oth;
+        if (x.pos & kGStop) dead = true;
+        else e = x.pos;
+    }
+}
+
+// ---- pass B1: group maps (a group = 256 consecutive tiles) ----------------------------------
 __global__ __launch_bounds__(256) void k_dec_group_maps(const GEntry* __restrict__ tmap,
                                                         uint32_t n_tiles,
                                                         GEntry* __restrict__ gmap) {
     __shared__ GEntry S[kGroupTiles][kEntries];
+    __shared__ GEntry Q[kDParts][kEntries];
     const uint32_t g = blockIdx.x, first = g * kGroupTiles;
     const uint32_t nt = min((uint32_t)kGroupTiles, n_tiles - first);
     for (uint32_t i = threadIdx.x; i < nt * kEntries; i += blockDim.x)
         (&S[0][0])[i] = tmap[(uint64_t)first * kEntries + i];
     __syncthreads();
+    dec_part_maps(S, nt, Q);
+    __syncthreads();
     if (threadIdx.x < kEntries) {
-        GEntry a = S[0][threadIdx.x];
-        for (uint32_t t = 1; t < nt && !(a.pos & kGStop); ++t) {
-            const GEntry y = S[t][a.pos];
-            a = GEntry{y.pos, a.ar + y.ar, a.oth + y.oth};
-        }
+        GEntry a{threadIdx.x, 0, 0};
+#pragma unroll
+        for (int q = 0; q < kDParts; ++q)
+            if (!(a.pos & kGStop)) {
+                const GEntry y = Q[q][a.pos];
+                a = GEntry{y.pos, a.ar + y.ar, a.oth + y.oth};
+            }
         gmap[(uint64_t)g * kEntries + threadIdx.x] = a;
     }
 }
 
 // ---- pass B2: the true chain through the group maps from entry 0 (one block; the maps are
-// staged in LDS 256 groups at a time and thread 0 walks them) ----------------------------------
+// staged in LDS 256 groups at a time, followed in parts) --------------------------------------
 // gres[g] = {entry of group g (kDead past the stop), AcceptReplies before it, others before it}
 __global__ __launch_bounds__(256) void k_dec_walk(const GEntry* __restrict__ gmap,
                                                   uint32_t n_groups, uint64_t len,
@@ -273,46 +333,29 @@ __global__ __launch_bounds__(256) void k_dec_walk(const GEntry* __restrict__ gma
                                                   GEntry* __restrict__ gres,
                                                   mpx_decode_result* __restrict__ res) {
     __shared__ GEntry S[kGroupTiles][kEntries];
-    __shared__ uint32_t st[4];  // e, ar, oth, stop (kDead = not yet)
-    if (threadIdx.x == 0) {
-        st[0] = 0;
-        st[1] = 0;
-        st[2] = 0;
-        st[3] = kDead;
-    }
+    __shared__ GEntry Q[kDParts][kEntries];
+    __shared__ GEntry PE[kDParts];
+    __shared__ GEntry cur;  // the chain's state before the batch: {entry | kGStop stop, ar, oth}
+    if (threadIdx.x == 0) cur = GEntry{0, 0, 0};
     for (uint32_t b0 = 0; b0 < n_groups; b0 += kGroupTiles) {
         const uint32_t nb = min((uint32_t)kGroupTiles, n_groups - b0);
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < nb * kEntries; i += blockDim.x)
             (&S[0][0])[i] = gmap[(uint64_t)b0 * kEntries + i];
         __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t e = st[0], ar = st[1], oth = st[2], stop = st[3];
-            for (uint32_t g = 0; g < nb; ++g) {
-                if (stop != kDead) {
-                    gres[b0 + g] = GEntry{kDead, ar, oth};
-                    continue;
-                }
-                gres[b0 + g] = GEntry{e, ar, oth};
-                const GEntry x = S[g][e];
-                ar += x.ar;
-                oth += x.oth;
-                if (x.pos & kGStop) stop = x.pos & ~kGStop;
-                else e = x.pos;
-            }
-            st[0] = e;
-            st[1] = ar;
-            st[2] = oth;
-            st[3] = stop;
-        }
+        dec_part_maps(S, nb, Q);
+        __syncthreads();
+        if (threadIdx.x == 0) cur = dec_part_entries(Q, cur, PE);
+        __syncthreads();
+        dec_part_walk(S, nb, PE, gres + b0, true);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         // the chain always stops inside the last tile at the latest (position len)
-        const uint64_t stop = st[3] == kDead ? len : st[3];
+        const uint64_t stop = (cur.pos & kGStop) ? (uint64_t)(cur.pos & ~kGStop) : len;
         res->consumed = stop;
-        res->n_accept_replies = st[1];
-        res->n_other = st[2];
+        res->n_accept_replies = cur.ar;
+        res->n_other = cur.oth;
         int32_t why = MPX_DECODE_END, code = -1;
         if (stop < len) {
             code = buf[stop];
@@ -323,12 +366,14 @@ __global__ __launch_bounds__(256) void k_dec_walk(const GEntry* __restrict__ gma
     }
 }
 
-// ---- pass B3: tile entries inside each group (thread 0 walks the group's tile maps) ---------
+// ---- pass B3: tile entries inside each group (the group's tile maps followed in parts) -------
 __global__ __launch_bounds__(256) void k_dec_tile_entries(const GEntry* __restrict__ tmap,
                                                           uint32_t n_tiles,
                                                           const GEntry* __restrict__ gres,
                                                           GEntry* __restrict__ tres) {
     __shared__ GEntry S[kGroupTiles][kEntries];
+    __shared__ GEntry Q[kDParts][kEntries];
+    __shared__ GEntry PE[kDParts];
     const uint32_t g = blockIdx.x, first = g * kGroupTiles;
     const uint32_t nt = min((uint32_t)kGroupTiles, n_tiles - first);
     const GEntry r = gres[g];
@@ -339,22 +384,11 @@ __global__ __launch_bounds__(256) void k_dec_tile_entries(const GEntry* __restri
     for (uint32_t i = threadIdx.x; i < nt * kEntries; i += blockDim.x)
         (&S[0][0])[i] = tmap[(uint64_t)first * kEntries + i];
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t e = r.pos, ar = r.ar, oth = r.oth;
-        bool dead = false;
-        for (uint32_t t = 0; t < nt; ++t) {
-            if (dead) {
-                tres[first + t] = GEntry{kDead, 0, 0};
-                continue;
-            }
-            tres[first + t] = GEntry{e, ar, oth};
-            const GEntry x = S[t][e];
-            ar += x.ar;
-            oth += x.oth;
-            if (x.pos & kGStop) dead = true;
-            else e = x.pos;
-        }
-    }
+    dec_part_maps(S, nt, Q);
+    __syncthreads();
+    if (threadIdx.x == 0) dec_part_entries(Q, r, PE);
+    __syncthreads();
+    dec_part_walk(S, nt, PE, tres + first, false);
 }
 
 // ---- pass C: chunk entries (tree over the stored exit maps) and record emission -------------
