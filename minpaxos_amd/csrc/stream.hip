@@ -451,12 +451,45 @@ __global__ __launch_bounds__(kParts * kE) void k_sd_group_maps(Work W, uint32_t 
 }
 
 // ---- pass B2: the true chain over the group maps, then the exact stop ------------------------
-// One block: thread 0 walks (maps staged in LDS by the block). At the terminal group it descends
-// to the terminal tile, chunk and byte, classifies the frame there and writes the result.
-__global__ __launch_bounds__(64) void k_sd_walk(SParams P, Work W, uint32_t n_tiles,
-                                                 uint32_t n_groups, mpx_stream_result* res) {
+// One block of kParts x 64 threads. The group maps are staged 256 at a time and followed in
+// parts (part_maps; one thread chains the 8 part maps, 8 threads walk their parts writing the
+// group entries); at the terminal group the block descends the same way to the terminal tile
+// and chunk, then thread 0 classifies the frame at the terminal byte and writes the result.
+// The run's first map at which the chain from entry e0 reaches a terminal: part maps, the parts
+// chained by thread 0, then thread 0 walks the terminal part. S[k][e] >= kE is a terminal (kTerm
+// in tile / group maps, kE + byte in chunk maps). Thread 0 gets (map index, entry into it,
+// the terminal value); every chain reaches one (at the latest the end of the buffer).
+__device__ __forceinline__ void first_terminal(const uint8_t (*S)[kE], uint32_t n, uint32_t e0,
+                                               uint8_t (*Q)[kE], uint32_t* k_out,
+                                               uint32_t* e_out, uint32_t* v_out) {
+    part_maps(S, n, Q);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t e = e0, q = 0;
+        for (; q < (uint32_t)kParts - 1; ++q) {
+            const uint32_t x = Q[q][e];
+            if (x >= (uint32_t)kE) break;
+            e = x;
+        }
+        const uint32_t t1 = min((q + 1) * (uint32_t)kPartTiles, n);
+        uint32_t k = q * kPartTiles, v = kTerm;
+        for (; k < t1; ++k) {
+            v = S[k][e];
+            if (v >= (uint32_t)kE) break;
+            e = v;
+        }
+        *k_out = k;
+        *e_out = e;
+        *v_out = v;
+    }
+}
+__global__ __launch_bounds__(kParts * kE) void k_sd_walk(SParams P, Work W, uint32_t n_tiles,
+                                                         uint32_t n_groups, mpx_stream_result* res) {
     __shared__ __attribute__((aligned(16))) uint8_t S[kGT][kE];
+    __shared__ uint8_t Q[kParts][kE];
+    __shared__ uint8_t PE[kParts];
     __shared__ uint32_t st[3];  // entry, terminal group (n_groups = none), its entry
+    __shared__ uint32_t fk[3];  // first_terminal's result
     const int t = threadIdx.x;
     if (t == 0) {
         st[0] = P.entry0;
@@ -477,65 +510,52 @@ __global__ __launch_bounds__(64) void k_sd_walk(SParams P, Work W, uint32_t n_ti
         }
         stage16(&S[0][0], W.gmap + (uint64_t)b0 * kE, nb * kE);
         __syncthreads();
-        if (t == 0) {
-            uint32_t e = st[0], stop = st[1];
-            for (uint32_t g = 0; g < nb; ++g) {
-                if (stop != n_groups) {
-                    W.gent[b0 + g] = kDeadE;
-                    continue;
-                }
-                W.gent[b0 + g] = (uint8_t)e;
-                const uint8_t x = S[g][e];
-                if (x == kTerm) {
-                    stop = b0 + g;
-                    st[2] = e;
-                } else {
-                    e = x;
-                }
+        part_maps(S, nb, Q);
+        __syncthreads();
+        if (t == 0) {  // the parts' entries (kDeadE after the part that reaches the terminal)
+            uint32_t e = st[0];
+            for (int q = 0; q < kParts; ++q) {
+                PE[q] = (uint8_t)e;
+                e = e >= (uint32_t)kE ? (uint32_t)kDeadE : Q[q][e];
             }
-            st[0] = e;
-            st[1] = stop;
+            st[0] = e;  // the next batch's entry (unused once a terminal is found)
+        }
+        __syncthreads();
+        if (t < kParts) {  // part t's group entries; the part with the terminal records it
+            const uint32_t g0 = t * kPartTiles, g1 = min(g0 + (uint32_t)kPartTiles, nb);
+            uint32_t e = PE[t];
+            for (uint32_t g = g0; g < g1; ++g) {
+                W.gent[b0 + g] = (uint8_t)e;
+                if (e >= (uint32_t)kE) continue;
+                const uint32_t x = S[g][e];
+                if (x >= (uint32_t)kE) {
+                    st[1] = b0 + g;
+                    st[2] = e;
+                }
+                e = x >= (uint32_t)kE ? (uint32_t)kDeadE : x;
+            }
         }
     }
     __syncthreads();
-    // the terminal: every chain ends in one (at the latest the end of the buffer)
+    // the terminal tile within group gs
     const uint32_t gs = st[1];
-    uint32_t e = st[2];
-    // terminal tile within group gs
     const uint32_t first = gs * kGT, nt = min((uint32_t)kGT, n_tiles - first);
     stage16(&S[0][0], W.tmap + (uint64_t)first * kE, nt * kE);
     __syncthreads();
-    if (t == 0) {
-        uint32_t ts = first;
-        for (uint32_t k = 0; k < nt; ++k) {
-            const uint8_t x = S[k][e];
-            if (x == kTerm) {
-                ts = first + k;
-                break;
-            }
-            e = x;
-        }
-        st[0] = ts;
-        st[2] = e;
-    }
+    first_terminal(S, nt, st[2], Q, &fk[0], &fk[1], &fk[2]);
     __syncthreads();
-    // terminal chunk within the tile (its 128 chunk maps, 8 KB, over S)
-    const uint32_t ts = st[0];
+    const uint32_t ts = first + fk[0];
+    const uint32_t te = fk[1];
+    __syncthreads();
+    // the terminal chunk within the tile (its 128 chunk maps, 8 KB, over S)
     for (uint32_t i = t; i < (uint32_t)kTL * kE / 16; i += blockDim.x)
         reinterpret_cast<uint4*>(&S[0][0])[i] =
             reinterpret_cast<const uint4*>(W.cmap + (uint64_t)ts * kTL * kE)[i];
     __syncthreads();
+    first_terminal(S, kTL, te, Q, &fk[0], &fk[1], &fk[2]);
+    __syncthreads();
     if (t == 0) {
-        e = st[2];
-        uint32_t cs = 0, v = 0;
-        for (uint32_t c = 0; c < (uint32_t)kTL; ++c) {
-            v = S[c][e];
-            if (v >= (uint32_t)kE) {
-                cs = c;
-                break;
-            }
-            e = v;
-        }
+        const uint32_t cs = fk[0], v = fk[2];
         const uint64_t s = (uint64_t)ts * kTB + (uint64_t)cs * kC + (v - kE);  // terminal byte
         int32_t why, code = -1;
         uint64_t next = s;
@@ -1139,7 +1159,7 @@ hipError_t launch_decode_stream(int proto, int legacy, const uint8_t* buf, uint6
            outs.oth_cap};
     k_sd_tile_maps<<<tiles, kTL, 0, stream>>>(P, W);
     k_sd_group_maps<<<groups, kParts * kE, 0, stream>>>(W, tiles);
-    k_sd_walk<<<1, 64, 0, stream>>>(P, W, tiles, groups, res);
+    k_sd_walk<<<1, kParts * kE, 0, stream>>>(P, W, tiles, groups, res);
     k_sd_tile_entries<<<groups, kParts * kE, 0, stream>>>(W, tiles);
     k_sd_count<<<tiles, kTL, 0, stream>>>(P, W);
     k_sd_scan<<<(tiles + kScanT - 1) / kScanT, kScanT, 0, stream>>>(W, tiles);
