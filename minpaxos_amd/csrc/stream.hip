@@ -734,6 +734,20 @@ __device__ __forceinline__ void stage_tile(const SParams& P, uint64_t t0, uint8_
 // the tile's bytes for stage_tile, loaded into registers (kStageVec 16-byte pieces per lane)
 constexpr int kStageVec = ((kTB + kE) / 16 + kTL - 1) / kTL;
 __device__ __forceinline__ void load_tile_regs(const SParams& P, uint64_t t0, uint4 (&v)[kStageVec]) {
+    if (t0 + (uint64_t)kStageVec * kTL * 16 <= P.len) {
+        // interior tile (block-uniform): one basic block of loads, all in flight together (with
+        // the edge checks below per load, the compiler waited out each load at the branch join);
+        // only the last vector is partial: its lanes past the window load nothing
+        const uint4* src = reinterpret_cast<const uint4*>(P.buf + t0);
+        const int l = threadIdx.x;
+        __builtin_assume(l < kTL);
+#pragma unroll
+        for (int k = 0; k < kStageVec - 1; ++k) v[k] = src[l + k * kTL];
+        constexpr int kLast = (kTB + kE) / 16 - (kStageVec - 1) * kTL;
+        v[kStageVec - 1] = make_uint4(0, 0, 0, 0);
+        if (l < kLast) v[kStageVec - 1] = src[l + (kStageVec - 1) * kTL];
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < kStageVec; ++k) {
         const int i = threadIdx.x + k * kTL;
@@ -904,7 +918,22 @@ __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint
     const uint8_t ent = W.tent[tile];
     if (ent == kDeadE) return;  // every tile after the stop tile, never one before it
     const uint64_t t0 = (uint64_t)tile * kTB;
-    stage_tile(P, t0, B);
+    // the tile's bytes. MIN wire: all of a lane's 16-byte loads issued before the first LDS
+    // store (the load-store loop of stage_tile waits out each load in turn, 9 round trips per
+    // lane): emit 574 -> 447 us. CLASSIC's 10-byte AcceptReply frames overflow the register
+    // staging (kRegAR) and take the direct-store path, which ran 678 -> 727 us with the loads
+    // batched (profiles/r04/stream/ab_tile_loads.txt), so it keeps the loop.
+    if (P.proto == MPX_MODE_MIN) {
+        uint4 tv[kStageVec];
+        load_tile_regs(P, t0, tv);
+#pragma unroll
+        for (int k = 0; k < kStageVec; ++k) {
+            const int i = l + k * kTL;
+            if (i < (kTB + kE) / 16) reinterpret_cast<uint4*>(B)[i] = tv[k];
+        }
+    } else {
+        stage_tile(P, t0, B);
+    }
     const uint2 ci = W.cinfo[(uint64_t)tile * kTL + l];  // entry and counts (k_sd_count)
     __syncthreads();
     const uint32_t e = ci.x;
