@@ -677,8 +677,15 @@ __device__ __forceinline__ void chunk_entries(uint32_t ent, uint8_t (*X)[kE], ui
 }
 
 __device__ __forceinline__ void load_chunk_maps(const Work& W, uint32_t tile, uint8_t (*X)[kE]) {
+    // the 8 KB of chunk maps: a lane's four loads in flight together, then the LDS stores
     const uint4* src = reinterpret_cast<const uint4*>(W.cmap + (uint64_t)tile * kTL * kE);
-    for (int i = threadIdx.x; i < kTL * kE / 16; i += kTL) reinterpret_cast<uint4*>(&X[0][0])[i] = src[i];
+    constexpr int kN = kTL * kE / 16 / kTL;
+    static_assert(kTL * kE / 16 % kTL == 0, "whole vectors per lane");
+    uint4 v[kN];
+#pragma unroll
+    for (int k = 0; k < kN; ++k) v[k] = src[threadIdx.x + k * kTL];
+#pragma unroll
+    for (int k = 0; k < kN; ++k) reinterpret_cast<uint4*>(&X[0][0])[threadIdx.x + k * kTL] = v[k];
 }
 
 // frames of the lane's chunk on the true chain, by kind: AcceptReplies, PrepareReplies, variable
@@ -737,15 +744,13 @@ __device__ __forceinline__ void load_tile_regs(const SParams& P, uint64_t t0, ui
     if (t0 + (uint64_t)kStageVec * kTL * 16 <= P.len) {
         // interior tile (block-uniform): one basic block of loads, all in flight together (with
         // the edge checks below per load, the compiler waited out each load at the branch join);
-        // only the last vector is partial: its lanes past the window load nothing
+        // only the last vector is partial: its lanes past the window reload the window's last
+        // vector (no branch, whose join would wait for every load; the stores skip them)
         const uint4* src = reinterpret_cast<const uint4*>(P.buf + t0);
         const int l = threadIdx.x;
         __builtin_assume(l < kTL);
 #pragma unroll
-        for (int k = 0; k < kStageVec - 1; ++k) v[k] = src[l + k * kTL];
-        constexpr int kLast = (kTB + kE) / 16 - (kStageVec - 1) * kTL;
-        v[kStageVec - 1] = make_uint4(0, 0, 0, 0);
-        if (l < kLast) v[kStageVec - 1] = src[l + (kStageVec - 1) * kTL];
+        for (int k = 0; k < kStageVec; ++k) v[k] = src[min(l + k * kTL, (kTB + kE) / 16 - 1)];
         return;
     }
 #pragma unroll
@@ -792,9 +797,16 @@ __global__ __launch_bounds__(kTL) void k_sd_count(SParams P, Work W) {
     }
     const uint64_t t0 = (uint64_t)tile * kTB;
 #if MPX_SD_COUNT_UNION
+    // the chunk maps' loads first (needed first), then the tile's, all in flight together
+    constexpr int kCm = kTL * kE / 16 / kTL;
+    uint4 cm[kCm];
+    const uint4* csrc = reinterpret_cast<const uint4*>(W.cmap + (uint64_t)tile * kTL * kE);
+#pragma unroll
+    for (int k = 0; k < kCm; ++k) cm[k] = csrc[l + k * kTL];
     uint4 tv[kStageVec];
     load_tile_regs(P, t0, tv);
-    load_chunk_maps(W, tile, X);
+#pragma unroll
+    for (int k = 0; k < kCm; ++k) reinterpret_cast<uint4*>(&X[0][0])[l + k * kTL] = cm[k];
     __syncthreads();
     chunk_entries(ent, X, G, GE, En);  // (ends with a barrier: X is dead)
 #pragma unroll
