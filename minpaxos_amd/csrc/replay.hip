@@ -202,13 +202,17 @@ __global__ __launch_bounds__(kRbT) void k_rb_count(const uint64_t* __restrict__ 
     for (uint32_t b = threadIdx.x; b < bins; b += kRbT) h[b] = 0;
     __syncthreads();
     const uint64_t c0 = (uint64_t)blockIdx.x * kRbChunk;
-#pragma unroll 8
-    for (uint64_t k = threadIdx.x; k < kRbChunk; k += kRbT) {
-        const uint64_t i = c0 + k;
-        if (i >= n) break;
-        const uint64_t p = ld_stream(pairs + i);
-        if (p != kRbNone) atomicAdd(&h[(uint32_t)p >> kRbLg], 1u);
+    // all of a thread's loads in flight before its first LDS atomic (an early-exit loop waited
+    // out each load in turn)
+    uint64_t p[kRbPer];
+#pragma unroll
+    for (int k = 0; k < kRbPer; ++k) {
+        const uint64_t i = c0 + (uint64_t)(threadIdx.x + k * kRbT);
+        p[k] = i < n ? ld_stream(pairs + i) : kRbNone;
     }
+#pragma unroll
+    for (int k = 0; k < kRbPer; ++k)
+        if (p[k] != kRbNone) atomicAdd(&h[(uint32_t)p[k] >> kRbLg], 1u);
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < bins; b += kRbT) hist[(uint64_t)b * chunks + blockIdx.x] = h[b];
 }
@@ -279,14 +283,36 @@ __global__ __launch_bounds__(kRbT) void k_rb_max(const uint64_t* __restrict__ bi
     const uint64_t s0 = (uint64_t)b * kRbSlots;
     const uint32_t ns = (uint64_t)inst_cap - s0 < kRbSlots ? (uint32_t)((uint64_t)inst_cap - s0)
                                                             : kRbSlots;
-    for (uint32_t j = threadIdx.x; j < ns; j += kRbT) sl[j] = last_rec[s0 + j];
+    // the slice's current values, then the bin's pairs, kB loads in flight per thread at a time
+    // (load-use loops waited out each load in turn)
+    constexpr int kB = 8;
+    static_assert(kRbSlots % (kB * kRbT) == 0, "whole batches of slots");
+    for (uint32_t j0 = 0; j0 < ns; j0 += kB * kRbT) {
+        int32_t v[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            const uint32_t j = j0 + threadIdx.x + k * kRbT;
+            v[k] = j < ns ? last_rec[s0 + j] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            const uint32_t j = j0 + threadIdx.x + k * kRbT;
+            if (j < ns) sl[j] = v[k];
+        }
+    }
     // the bin's run: from its first chunk's offset to the next bin's (the total after the last)
     const uint64_t lo = offs[(uint64_t)b * chunks], hi = offs[(uint64_t)(b + 1) * chunks];
     __syncthreads();
-#pragma unroll 4
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += kRbT) {
-        const uint64_t p = ld_stream(binned + i);
-        atomicMax(&sl[(uint32_t)p & (kRbSlots - 1)], (int32_t)(p >> 32));
+    for (uint64_t i0 = lo; i0 < hi; i0 += (uint64_t)kB * kRbT) {
+        uint64_t p[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            const uint64_t i = i0 + threadIdx.x + (uint64_t)k * kRbT;
+            p[k] = i < hi ? ld_stream(binned + i) : kRbNone;
+        }
+#pragma unroll
+        for (int k = 0; k < kB; ++k)
+            if (p[k] != kRbNone) atomicMax(&sl[(uint32_t)p[k] & (kRbSlots - 1)], (int32_t)(p[k] >> 32));
     }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < ns; j += kRbT) last_rec[s0 + j] = sl[j];
