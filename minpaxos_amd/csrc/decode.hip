@@ -448,10 +448,19 @@ __global__ __launch_bounds__(kTileLanes) void k_dec_emit(
     };
 #if MPX_DEC_EMIT_UNION
     uint4 tv[kVec];
+    if (t0 + (uint64_t)kVec * kTileLanes * 16 <= len) {
+        // interior tile (block-uniform): every load in flight together, no per-load branch
+        // (whose join waited out each load in turn); lanes past the window reload its last
+        // vector, which the stores below skip
+        const uint4* src = reinterpret_cast<const uint4*>(buf + t0);
 #pragma unroll
-    for (int k = 0; k < kVec; ++k) {
-        const int i = l + k * kTileLanes;
-        tv[k] = i < (kTileBytes + 32) / 16 ? tile_vec(i) : make_uint4(0, 0, 0, 0);
+        for (int k = 0; k < kVec; ++k) tv[k] = src[min(l + k * kTileLanes, (kTileBytes + 32) / 16 - 1)];
+    } else {
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            const int i = l + k * kTileLanes;
+            tv[k] = i < (kTileBytes + 32) / 16 ? tile_vec(i) : make_uint4(0, 0, 0, 0);
+        }
     }
 #else
     for (int i = l; i < (kTileBytes + 32) / 16; i += kTileLanes)
