@@ -68,8 +68,8 @@
 extern "C" {
 #endif
 
-#define MPX_ABI_VERSION 6  /* 4: + mpx_group_step_totals_dev; 5: + mpx_graph_*, mpx_apply_buffers / _staged;
-                              6: + mpx_replay_durable_reserve */
+#define MPX_ABI_VERSION 7  /* 4: + mpx_group_step_totals_dev; 5: + mpx_graph_*, mpx_apply_buffers / _staged;
+                              6: + mpx_replay_durable_reserve; 7: + mpx_group_step_events */
 
 /* ---- error codes ---------------------------------------------------------------------- */
 #define MPX_OK 0
@@ -388,6 +388,11 @@ int mpx_step_totals_dev(mpx_engine* eng, const mpx_group_batch* b, int64_t* d_to
  * (same values), so a step is two kernel launches instead of three.                       */
 int mpx_group_step_totals_dev(mpx_engine* eng, const mpx_group_batch* b, int64_t* d_totals,
                               void* stream);
+/* timing hook (ABI 7): every later group step of the handle records ev_fast_start right before
+ * and ev_fast_end right after the launch of its first kernel (the per-group fast kernel, or the
+ * work-list fill), on the call's stream, so the pair brackets that kernel alone (the work-list
+ * kernel that follows is outside). Both NULL turns it off. Events from mpx_event_create.    */
+int mpx_group_step_events(mpx_engine* eng, void* ev_fast_start, void* ev_fast_end);
 
 /* ---- multi-GPU: the one collective (RCCL over xGMI) -------------------------------------
  * Each rank owns a block of groups; non-owned entries must hold -1. After the call every

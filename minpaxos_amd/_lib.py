@@ -101,6 +101,7 @@ SIGNATURES = {
     "mpx_stream_destroy": (C.c_int, [_p, _p]),
     "mpx_stream_synchronize": (C.c_int, [_p, _p]),
     "mpx_event_create": (C.c_int, [_p, C.c_int, C.POINTER(_p)]),
+    "mpx_group_step_events": (C.c_int, [_p, _p, _p]),
     "mpx_event_destroy": (C.c_int, [_p, _p]),
     "mpx_event_record": (C.c_int, [_p, _p, _p]),
     "mpx_apply_buffers": (C.c_int, [_p, _sz, C.POINTER(MpxApplyIo)]),
@@ -134,7 +135,10 @@ def load():
             f"{LIB_PATH} is not built; run `make -C minpaxos_amd` (hipcc, gfx950)")
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        # an A/B run against an older build (MPX_LIB) may lack the newer entry points
+        fn = getattr(lib, name) if not os.environ.get("MPX_LIB") else getattr(lib, name, None)
+        if fn is None:
+            continue
         fn.restype = res
         fn.argtypes = args
     _lib = lib

@@ -586,6 +586,12 @@ __global__ __launch_bounds__(256) void k_ap_scan_rows(ApGeo g, uint32_t* __restr
 }
 
 // ---- partition ----------------------------------------------------------------------------------
+// MPX_EMIT_CPOS=1 (A/B builds): the scatter stores each image position's partition slot (4 B per
+// command) for the emit; the default has the emit derive them from the scanned rows (the tile's
+// run start per bin, and the next tile's as its end)
+#ifndef MPX_EMIT_CPOS
+#define MPX_EMIT_CPOS 0
+#endif
 struct ScatterLds {
     HotLds hl;
     uint32_t roff[kMaxBins];    // this tile's run start per bin (partition position)
@@ -725,7 +731,8 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
             const uint32_t dst = S.roff[b] + (i - S.lstart[b]);
             if (!(MPX_SC_ABL & 32)) rec_kv[dst] = S.img[i];
             if (!(MPX_SC_ABL & 8)) rec_op[dst] = S.iop[i];
-            if (!(MPX_SC_ABL & 16)) cpos[(uint64_t)tile * kTL + i] = dst;  // image order: emit gathers run by run
+            if (MPX_EMIT_CPOS && !(MPX_SC_ABL & 16))
+                cpos[(uint64_t)tile * kTL + i] = dst;  // image order: emit gathers run by run
         }
         for (int i = tid; i < kTW * kMaxBins / 2; i += kTT) cw32[i] = 0u;  // next tile's counts
         __syncthreads();
@@ -1146,6 +1153,567 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
     }
 }
 
+// ---- per-bin resolve, list form (the default; MPX_RS_LIST=0 builds the bucket rounds above) ----
+// One workgroup per bin, every record of a batch at once instead of 64 per wave and round:
+//   P1  each record finds its slot in the bin's LDS table (a command on a key the table does not
+//       hold claims a slot for it, PUT or not: a GET before the first PUT of a new key must still
+//       be that PUT's predecessor) and pushes itself onto the slot's list of the batch (one LDS
+//       exchange on a head word tagged with the batch; its link keeps the previous head)
+//   P2  each record walks its slot's list (every record of the batch on its key, in push order):
+//       the highest index below its own is its predecessor (state.Conflict), the highest PUT
+//       below it its GET's source, none above it makes it the slot's last; the slot's state at
+//       batch start covers what the batch does not. Results are stored in partition order
+//       (coalesced). The slot's last record keeps the slot's new state
+//   P3  the last records write the new states (after a barrier: P2 read the old ones)
+// A slot claimed by commands that never PUT (a "phantom": the key stays absent) is removed at
+// write-back and the bucket's new keys are placed again, so the table stays a linear-probing
+// table of the present keys. A bucket that runs out of slots re-runs the bin in the two-pass form
+// (every PUT key inserted first; other commands on absent keys then have no PUT in the call and
+// resolve to 0 without a slot).
+#ifndef MPX_RS_LIST
+#define MPX_RS_LIST 1
+#endif
+#ifndef MPX_RL_PER
+#define MPX_RL_PER 3
+#endif
+// result stores: plain (default: the emit reads them back soon, through L2) or nontemporal
+#ifndef MPX_RL_NT
+#define MPX_RL_NT 0
+#endif
+// diagnostic build: wave 0's clock per phase of k_ap_resolve_list, printed by bin 0
+#ifndef MPX_RL_STAMP
+#define MPX_RL_STAMP 0
+#endif
+#if MPX_RL_STAMP
+#define RL_STAMP(k)                                              \
+    do {                                                         \
+        const unsigned long long _c = clock64();                 \
+        if (tid == 0) S.rph[k] += _c - rl_c0;                    \
+        rl_c0 = _c;                                              \
+    } while (0)
+#else
+#define RL_STAMP(k) do {} while (0)
+#endif
+constexpr int kLT = 1024;                 // threads of the list-resolve workgroup
+constexpr int kLW = kLT / kWave;
+constexpr int kLPer = MPX_RL_PER;         // records per thread and batch
+constexpr int kLB = kLT * kLPer;          // records per batch
+constexpr int kLSlots = kMaxBPB * kSB;    // table slots of a bin
+constexpr uint32_t kLIdx = 13;            // bits of 1 + a batch index
+constexpr uint32_t kLIdxMask = (1u << kLIdx) - 1u;
+constexpr uint32_t kLTagMax = (1u << (32 - kLIdx)) - 1u;
+constexpr uint32_t kFOverflow = 4u;
+static_assert(kLB < (1 << kLIdx) && kLB <= 0x7FFF, "links hold 1 + a batch index below the PUT bit");
+
+// A slot with more than kLHeavyMin records in a batch (a warm key: walking its list would cost
+// O(count^2)) is HEAVY: its records set their bits in a bitmap over the batch (and a bitmap of
+// its PUTs), one wave scans each bitmap's words for the last set bit at or before every word, and
+// a record's predecessor / last PUT before it is then a masked word plus one prefix entry. At most
+// kLHeavy heavy slots per batch (more walk their lists).
+constexpr uint32_t kLHeavyMin = 16;
+constexpr int kLHeavy = 8;
+constexpr int kLWords = kLB / 32;
+static_assert(kLB % 32 == 0 && kLWords <= 2 * kWave, "a wave scans a heavy bitmap, two words a lane");
+
+struct ListLds {
+    int64_t tk[kLSlots];
+    int64_t tv[kLSlots];
+    uint32_t head[kLSlots];  // per slot: (batch tag << kLIdx) | (1 + the last record pushed)
+    uint32_t cnt[2][kLSlots / 2];  // per batch parity, two 16-bit slot counts a word
+    uint8_t ts[kLSlots];
+    uint16_t link[kLB];      // per record: (PUT << 15) | (1 + the record pushed before it)
+    int64_t bval[kLB];       // per record: its value (read for PUTs)
+    uint32_t hb[kLHeavy][kLWords];  // heavy slots: the batch's records on it, bit per record
+    uint32_t hp[kLHeavy][kLWords];  //   ... its PUTs
+    int32_t la[kLHeavy][kLWords];   //   the last record at or before each word (-1: none)
+    int32_t lp[kLHeavy][kLWords];   //   the last PUT at or before each word
+    uint32_t hslot[kLHeavy];
+    uint32_t nheavy[2];
+    uint32_t flags;
+#if MPX_RL_STAMP
+    unsigned long long rph[8];
+#endif
+};
+
+__global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
+                                                         const uint32_t* __restrict__ bin_start,
+                                                         const int4* __restrict__ rec_kv,
+                                                         const uint8_t* __restrict__ rec_op,
+                                                         int64_t* __restrict__ r_ret,
+                                                         uint8_t* __restrict__ r_conf, ApHot* hot,
+                                                         uint32_t* err) {
+    __shared__ ListLds S;
+    const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
+    const uint32_t bpb = 1u << g.lgbpb;
+    const uint32_t bin = blockIdx.x;
+    const uint32_t nslot = bpb * kSB;
+    const uint32_t nsub = 1u << g.lgsub;
+    const uint32_t ep = t.epoch[0];
+    const uint32_t r0 = bin_start[bin], r1 = bin_start[bin + 1];
+    if (r0 == r1) return;  // no records: nothing read, nothing touched
+    for (uint32_t sub = 0; sub < nsub; ++sub) {
+        const uint64_t gbase = ((((uint64_t)bin << g.lgsub) | sub) * bpb) * kSB;
+        auto member = [&](uint64_t h) {
+            return ((bucket_of(h, g.lgnb) >> g.lgbpb) & (nsub - 1)) == sub;
+        };
+        bool rerun = false;
+        for (int mode = 0; mode < 2; ++mode) {
+            if (mode == 1 && !rerun) break;
+            __syncthreads();  // the previous pass is done with the LDS
+            for (uint32_t i = tid; i < nslot; i += kLT) {
+                S.tk[i] = t.keys[gbase + i];
+                S.tv[i] = t.vals[gbase + i];
+                const uint32_t x = t.state[gbase + i];
+                const uint8_t pres = (uint8_t)(x & kPresent);
+                S.ts[i] = (uint8_t)(pres | (pres ? kSWasPresent : 0) |
+                                    ((x >> 2) == ep ? (kSTouched | (x & kLastPut)) : 0u));
+                S.head[i] = 0u;
+            }
+            for (uint32_t i = tid; i < (uint32_t)kLSlots; i += kLT) (&S.cnt[0][0])[i] = 0u;
+            for (uint32_t i = tid; i < (uint32_t)(kLHeavy * kLWords); i += kLT) {
+                (&S.hb[0][0])[i] = 0u;
+                (&S.hp[0][0])[i] = 0u;
+            }
+            if (tid == 0) {
+                S.flags = 0;
+                S.nheavy[0] = S.nheavy[1] = 0;
+            }
+            __syncthreads();
+            if (mode == 1) {  // two-pass form: every PUT key of the bin first
+                if (tid == 0) atomicAdd(&hot->restarts, 1u);
+                for (uint32_t q = r0 + tid; q < r1; q += kLT) {
+                    if (rec_op[q] != MPX_OP_PUT) continue;
+                    const int4 kv = rec_kv[q];
+                    const int64_t k = kv_lo_hi(kv.x, kv.y);
+                    const uint64_t h = hash64((uint64_t)k);
+                    if (!member(h)) continue;
+                    const uint32_t bb = (bucket_of(h, g.lgnb) & (bpb - 1)) * kSB;
+                    uint32_t p = home_of(h);
+                    bool done = false;
+                    for (int probe = 0; probe < kSB && !done; ++probe) {
+                        const unsigned long long cur =
+                            atomicCAS(reinterpret_cast<unsigned long long*>(&S.tk[bb + p]),
+                                      (unsigned long long)kSentinel, (unsigned long long)k);
+                        if (cur == (unsigned long long)kSentinel) {
+                            S.ts[bb + p] |= kSNew;
+                            done = true;
+                        } else if ((int64_t)cur == k) {
+                            done = true;
+                        }
+                        p = (p + 1) & (kSB - 1);
+                    }
+                    if (!done) raise_err(err, kErrKvFull);
+                }
+                __syncthreads();
+            }
+            int4 kv[kLPer];
+            uint32_t o[kLPer];
+#pragma unroll
+            for (int hh = 0; hh < kLPer; ++hh) {
+                const uint32_t q = r0 + hh * kLT + tid;
+                kv[hh] = rec_kv[q < r1 ? q : r1 - 1];
+                o[hh] = rec_op[q < r1 ? q : r1 - 1];
+            }
+            uint32_t tag = 0;
+#if MPX_RL_STAMP
+            if (tid < 8) S.rph[tid] = 0;
+            unsigned long long rl_c0 = clock64();
+#endif
+            for (uint32_t base = r0; base < r1; base += kLB) {
+                if (++tag == kLTagMax) {  // (after 2^19 batches) heads of old tags would match
+                    for (uint32_t i = tid; i < nslot; i += kLT) S.head[i] = 0u;
+                    __syncthreads();
+                    tag = 1;
+                }
+                const uint32_t par = tag & 1u;
+                // ---- P1: slot, push ----
+                // (the thread's records side by side: the common path is straight-line code, so
+                // their LDS round trips overlap; a probe past 4 slots and a claim run after)
+                int sl[kLPer];
+                int64_t v[kLPer], k[kLPer];
+                uint32_t cl[kLPer];  // bit 0 a record of this pass, bit 1 PUT, bit 2 GET
+                uint32_t bbs[kLPer], ps[kLPer];
+                int64_t c[kLPer][4];
+#pragma unroll
+                for (int hh = 0; hh < kLPer; ++hh) {
+                    const uint32_t i = hh * kLT + tid;
+                    k[hh] = kv_lo_hi(kv[hh].x, kv[hh].y);
+                    v[hh] = kv_lo_hi(kv[hh].z, kv[hh].w);
+                    const uint64_t h = hash64((uint64_t)k[hh]);
+                    const bool live = base + i < r1 && member(h);
+                    cl[hh] = (live ? 1u : 0u) | (o[hh] == MPX_OP_PUT ? 2u : 0u) |
+                             (o[hh] == MPX_OP_GET ? 4u : 0u);
+                    bbs[hh] = (bucket_of(h, g.lgnb) & (bpb - 1)) * kSB;
+                    ps[hh] = home_of(h);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) c[hh][u] = S.tk[bbs[hh] + ((ps[hh] + u) & (kSB - 1))];
+                }
+                // first probe step; -1: look further (no hit and no free slot among the 4), -2:
+                // absent (p = the first free slot)
+#pragma unroll
+                for (int hh = 0; hh < kLPer; ++hh) {
+                    int hit = -1, stop = -1;
+#pragma unroll
+                    for (int u = 3; u >= 0; --u) {
+                        if (c[hh][u] == k[hh]) hit = u;
+                        if (c[hh][u] == kSentinel) stop = u;
+                    }
+                    int s = -1;
+                    if (hit >= 0 && (stop < 0 || hit < stop)) s = (int)((ps[hh] + hit) & (kSB - 1));
+                    else if (stop >= 0) {
+                        s = -2;
+                        ps[hh] = (ps[hh] + stop) & (kSB - 1);
+                    } else {
+                        ps[hh] = (ps[hh] + 4) & (kSB - 1);
+                    }
+                    sl[hh] = (cl[hh] & 1u) ? s : -3;  // -3: not a record of this pass
+                }
+#pragma unroll
+                for (int hh = 0; hh < kLPer; ++hh) {
+                    if (sl[hh] != -1) continue;  // rare: a long probe
+                    const uint32_t bb = bbs[hh];
+                    uint32_t p = ps[hh];
+                    int s = -2;
+                    for (int step = 1; step < kSB / 4; ++step) {
+                        int64_t cc[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) cc[u] = S.tk[bb + ((p + u) & (kSB - 1))];
+                        int hit = -1, stop = -1;
+#pragma unroll
+                        for (int u = 3; u >= 0; --u) {
+                            if (cc[u] == k[hh]) hit = u;
+                            if (cc[u] == kSentinel) stop = u;
+                        }
+                        if (hit >= 0 && (stop < 0 || hit < stop)) {
+                            s = (int)((p + hit) & (kSB - 1));
+                            break;
+                        }
+                        if (stop >= 0) {
+                            p = (p + stop) & (kSB - 1);
+                            break;
+                        }
+                        p = (p + 4) & (kSB - 1);
+                    }
+                    ps[hh] = p;
+                    sl[hh] = s;
+                }
+#pragma unroll
+                for (int hh = 0; hh < kLPer; ++hh) {
+                    if (sl[hh] != -2) continue;  // absent: claim a slot (any op in the one-pass form)
+                    const bool isput = (cl[hh] & 2u) != 0;
+                    int s = -1;
+                    if (mode == 0 || isput) {
+                        const uint32_t bb = bbs[hh];
+                        uint32_t p = ps[hh];
+                        for (int probe = 0; probe < kSB; ++probe) {
+                            const unsigned long long cur =
+                                atomicCAS(reinterpret_cast<unsigned long long*>(&S.tk[bb + p]),
+                                          (unsigned long long)kSentinel, (unsigned long long)k[hh]);
+                            if (cur == (unsigned long long)kSentinel) {
+                                s = (int)p;
+                                S.ts[bb + p] |= kSNew;
+                                break;
+                            }
+                            if ((int64_t)cur == k[hh]) {
+                                s = (int)p;
+                                break;
+                            }
+                            p = (p + 1) & (kSB - 1);
+                        }
+                        if (s < 0) {
+                            if (mode == 0) atomicOr(&S.flags, kFOverflow);
+                            else raise_err(err, kErrKvFull);
+                        }
+                    }
+                    sl[hh] = s;
+                }
+                uint32_t olds[kLPer];
+#pragma unroll
+                for (int hh = 0; hh < kLPer; ++hh) {
+                    const uint32_t i = hh * kLT + tid;
+                    sl[hh] = sl[hh] >= 0 ? (int)(bbs[hh] + (uint32_t)sl[hh]) : -1;
+                    olds[hh] = sl[hh] >= 0 ? atomicExch(&S.head[sl[hh]], (tag << kLIdx) | (i + 1u)) : 0u;
+                }
+                uint32_t cnts[kLPer];
+#pragma unroll
+                for (int hh = 0; hh < kLPer; ++hh) {
+                    const uint32_t i = hh * kLT + tid;
+                    cnts[hh] = 0;
+                    if (sl[hh] < 0) continue;
+                    const uint32_t x = (uint32_t)sl[hh];
+                    const bool isput = (cl[hh] & 2u) != 0;
+                    const uint32_t pv = (olds[hh] >> kLIdx) == tag ? (olds[hh] & kLIdxMask) : 0u;
+                    S.link[i] = (uint16_t)((isput ? 0x8000u : 0u) | pv);
+                    if (isput) S.bval[i] = v[hh];
+                    const uint32_t sh = 16u * (x & 1u);
+                    cnts[hh] = (atomicAdd(&S.cnt[par][x >> 1], 1u << sh) >> sh) & 0xFFFFu;
+                }
+#pragma unroll
+                for (int hh = 0; hh < kLPer; ++hh) {
+                    if (sl[hh] >= 0 && cnts[hh] == kLHeavyMin) {  // the slot turns heavy
+                        const uint32_t hx = atomicAdd(&S.nheavy[par], 1u);
+                        if (hx < (uint32_t)kLHeavy) S.hslot[hx] = (uint32_t)sl[hh];
+                    }
+                }
+                // the next batch's records load while this one resolves
+#pragma unroll
+                for (int hh = 0; hh < kLPer; ++hh) {  // (clamped, not guarded: no branch)
+                    const uint32_t q = base + kLB + hh * kLT + tid;
+                    kv[hh] = rec_kv[q < r1 ? q : r1 - 1];
+                    o[hh] = rec_op[q < r1 ? q : r1 - 1];
+                }
+                RL_STAMP(0);
+                __syncthreads();
+                RL_STAMP(1);
+                // ---- heavy slots: bitmaps, then their prefix maxima (uniform branch) ----
+                const uint32_t nh0 = S.nheavy[par];
+                const uint32_t nh = nh0 < (uint32_t)kLHeavy ? nh0 : (uint32_t)kLHeavy;
+                // (cl bits 4..7: 1 + the heavy index of the record's slot, 0: walk its list)
+#pragma unroll
+                for (int hh = 0; hh < kLPer; ++hh) {
+                    if (!nh || sl[hh] < 0) continue;
+                    const uint32_t x = (uint32_t)sl[hh];
+                    const uint32_t c = (S.cnt[par][x >> 1] >> (16u * (x & 1u))) & 0xFFFFu;
+                    if (c <= kLHeavyMin) continue;
+                    int hx = -1;
+                    for (uint32_t q = 0; q < nh; ++q)
+                        if (S.hslot[q] == x) hx = (int)q;
+                    if (hx >= 0) {
+                        const uint32_t i = hh * kLT + tid;
+                        cl[hh] |= (uint32_t)(hx + 1) << 4;
+                        atomicOr(&S.hb[hx][i >> 5], 1u << (i & 31));
+                        if (cl[hh] & 2u) atomicOr(&S.hp[hx][i >> 5], 1u << (i & 31));
+                    }
+                }
+                if (nh) {
+                    __syncthreads();
+                    if ((uint32_t)w < nh) {  // wave w: heavy slot w's prefix maxima over the words
+                        int a0 = -1, a1 = -1, p0 = -1, p1 = -1;
+                        {
+                            const uint32_t b0 = S.hb[w][l], q0 = S.hp[w][l];
+                            a0 = b0 ? l * 32 + hi_bit(b0) : -1;
+                            p0 = q0 ? l * 32 + hi_bit(q0) : -1;
+                        }
+                        if (l + kWave < kLWords) {
+                            const uint32_t b1 = S.hb[w][l + kWave], q1 = S.hp[w][l + kWave];
+                            a1 = b1 ? (l + kWave) * 32 + hi_bit(b1) : -1;
+                            p1 = q1 ? (l + kWave) * 32 + hi_bit(q1) : -1;
+                        }
+#pragma unroll
+                        for (int d = 1; d < kWave; d <<= 1) {
+                            const int ya0 = __shfl_up(a0, d), yp0 = __shfl_up(p0, d);
+                            const int ya1 = __shfl_up(a1, d), yp1 = __shfl_up(p1, d);
+                            if (l >= d) {
+                                a0 = a0 > ya0 ? a0 : ya0;
+                                p0 = p0 > yp0 ? p0 : yp0;
+                                a1 = a1 > ya1 ? a1 : ya1;
+                                p1 = p1 > yp1 ? p1 : yp1;
+                            }
+                        }
+                        const int ta = __shfl(a0, kWave - 1), tp = __shfl(p0, kWave - 1);
+                        S.la[w][l] = a0;
+                        S.lp[w][l] = p0;
+                        if (l + kWave < kLWords) {
+                            S.la[w][l + kWave] = a1 > ta ? a1 : ta;
+                            S.lp[w][l + kWave] = p1 > tp ? p1 : tp;
+                        }
+                    }
+                    __syncthreads();
+                }
+                RL_STAMP(2);
+                // ---- P2: walk, results ----
+                // (the thread's lists walked side by side: one round issues the next link of
+                // each, so a round trip serves all three)
+                uint32_t j1[kLPer];
+                uint32_t stt[kLPer];
+                int64_t tabv[kLPer];
+                int prev[kLPer], lastput[kLPer];
+                uint32_t fl[kLPer];  // bit 0 the predecessor is a PUT, bit 1 a later record
+#pragma unroll
+                for (int hh = 0; hh < kLPer; ++hh) {
+                    const int x = sl[hh] >= 0 ? sl[hh] : 0;
+                    j1[hh] = sl[hh] >= 0 && !(cl[hh] >> 4) ? (S.head[x] & kLIdxMask) : 0u;
+                    stt[hh] = S.ts[x];
+                    tabv[hh] = S.tv[x];
+                    prev[hh] = lastput[hh] = -1;
+                    fl[hh] = 0;
+                }
+#pragma unroll
+                for (int hh = 0; hh < kLPer; ++hh) {
+                    if (!(cl[hh] >> 4)) continue;  // heavy: the bitmaps
+                    const uint32_t i = hh * kLT + tid;
+                    const int hx = (int)(cl[hh] >> 4) - 1;
+                    const uint32_t wd = i >> 5, mk = (1u << (i & 31)) - 1u;
+                    const uint32_t ba = S.hb[hx][wd] & mk, bp = S.hp[hx][wd] & mk;
+                    prev[hh] = ba ? (int)(wd * 32 + hi_bit(ba)) : (wd ? S.la[hx][wd - 1] : -1);
+                    lastput[hh] = bp ? (int)(wd * 32 + hi_bit(bp)) : (wd ? S.lp[hx][wd - 1] : -1);
+                    fl[hh] = (prev[hh] >= 0 && prev[hh] == lastput[hh] ? 1u : 0u) |
+                             (S.la[hx][kLWords - 1] > (int)i ? 2u : 0u);
+                }
+                for (;;) {
+                    uint32_t any = 0;
+#pragma unroll
+                    for (int hh = 0; hh < kLPer; ++hh) any |= j1[hh];
+                    if (!any) break;
+                    uint32_t lk[kLPer];
+#pragma unroll
+                    for (int hh = 0; hh < kLPer; ++hh) lk[hh] = S.link[j1[hh] ? j1[hh] - 1u : 0u];
+#pragma unroll
+                    for (int hh = 0; hh < kLPer; ++hh) {
+                        if (!j1[hh]) continue;
+                        const uint32_t i = hh * kLT + tid;
+                        const uint32_t j = j1[hh] - 1u;
+                        const bool pj = (lk[hh] >> 15) != 0;
+                        if (j < i) {
+                            if ((int)j > prev[hh]) {
+                                prev[hh] = (int)j;
+                                fl[hh] = (fl[hh] & ~1u) | (pj ? 1u : 0u);
+                            }
+                            if (pj && (int)j > lastput[hh]) lastput[hh] = (int)j;
+                        } else if (j > i) {
+                            fl[hh] |= 2u;
+                        }
+                        j1[hh] = lk[hh] & 0x7FFFu;
+                    }
+                }
+                int64_t lpv[kLPer];
+#pragma unroll
+                for (int hh = 0; hh < kLPer; ++hh) lpv[hh] = S.bval[lastput[hh] >= 0 ? lastput[hh] : 0];
+                uint32_t nst = 0;  // byte hh: the new state of record hh's slot (0: not its last)
+                int64_t nval[kLPer];
+#pragma unroll
+                for (int hh = 0; hh < kLPer; ++hh) {
+                    const uint32_t i = hh * kLT + tid;
+                    nval[hh] = 0;
+                    const bool isput = (cl[hh] & 2u) != 0, isget = (cl[hh] & 4u) != 0;
+                    int64_t ret = 0;
+                    bool conf = false;
+                    if (sl[hh] >= 0) {
+                        const uint32_t st0 = stt[hh];
+                        const bool hl = lastput[hh] >= 0;
+                        const bool hasprev = prev[hh] >= 0 || (st0 & kSTouched) != 0;
+                        const bool pput = prev[hh] >= 0 ? (fl[hh] & 1u) != 0 : (st0 & kSLastPut) != 0;
+                        ret = isput ? v[hh]
+                                    : (isget ? (hl ? lpv[hh] : ((st0 & kSPresent) ? tabv[hh] : 0)) : 0);
+                        conf = hasprev && (pput || isput);
+                        if (!(fl[hh] & 2u)) {  // the slot's last record of the batch: its new state
+                            uint32_t ns = (st0 & (kSPresent | kSValDirty | kSNew | kSWasPresent)) |
+                                          kSTouched | (isput ? kSLastPut : 0);
+                            if (isput || hl) ns |= kSPresent | kSValDirty;
+                            nst |= ns << (8 * hh);
+                            nval[hh] = isput ? v[hh] : (hl ? lpv[hh] : tabv[hh]);
+                        }
+                    }
+                    // (a record of this pass without a slot: the two-pass form's key that is
+                    // absent and never PUT in the call - NIL, no conflict)
+                    if ((cl[hh] & 1u) && !(MPX_RS_ABL & 2)) {
+#if MPX_RL_NT
+                        st_stream(r_ret + base + i, ret);
+                        st_stream(r_conf + base + i, (uint8_t)(conf ? 1 : 0));
+#else
+                        r_ret[base + i] = ret;
+                        r_conf[base + i] = conf ? 1 : 0;
+#endif
+                    }
+                }
+                RL_STAMP(3);
+                __syncthreads();
+                RL_STAMP(4);
+                // ---- P3: the slots' new states; this parity's counters and bitmaps cleared (its
+                // next batch comes after the next batch's first barrier) ----
+#pragma unroll
+                for (int hh = 0; hh < kLPer; ++hh) {
+                    const uint8_t ns = (uint8_t)(nst >> (8 * hh));
+                    if (ns) {  // (a last record's state has kSTouched)
+                        S.ts[sl[hh]] = ns;
+                        if (ns & kSValDirty) S.tv[sl[hh]] = nval[hh];
+                    }
+                    if (sl[hh] >= 0) S.cnt[par][(uint32_t)sl[hh] >> 1] = 0u;
+                }
+                if (nh && (uint32_t)w < nh) {
+                    S.hb[w][l] = 0u;
+                    S.hp[w][l] = 0u;
+                    if (l + kWave < kLWords) {
+                        S.hb[w][l + kWave] = 0u;
+                        S.hp[w][l + kWave] = 0u;
+                    }
+                }
+                if (tid == 0) S.nheavy[par] = 0u;
+                RL_STAMP(5);
+            }
+            __syncthreads();
+#if MPX_RL_STAMP
+            if (bin == 0 && sub == 0 && tid == 0)
+                printf("RL_STAMP bin0 mode %d recs %u batches %u: P1 %llu bar1 %llu heavy %llu P2 %llu bar2 %llu P3 %llu\n",
+                       mode, r1 - r0, tag, S.rph[0], S.rph[1], S.rph[2], S.rph[3], S.rph[4], S.rph[5]);
+#endif
+            if (mode == 0) rerun = (S.flags & kFOverflow) != 0;
+        }
+        // ---- phantoms out: a bucket holding slots whose keys never became present has them
+        // removed and its new keys placed again (existing keys never move: every slot of their
+        // probe chains was occupied before this call). Wave w takes bucket w.
+        for (uint32_t b = (uint32_t)w; b < bpb; b += kLW) {
+            int64_t* T = S.tk + b * kSB;
+            int64_t* V = S.tv + b * kSB;
+            uint8_t* TS = S.ts + b * kSB;
+            uint8_t sv[kSB / kWave];
+            bool ph = false;
+#pragma unroll
+            for (int u = 0; u < kSB / kWave; ++u) {
+                sv[u] = TS[l + u * kWave];
+                ph |= (sv[u] & kSNew) && !(sv[u] & kSPresent);
+            }
+            if (!__ballot(ph)) continue;
+            int64_t kk[kSB / kWave], vv[kSB / kWave];
+#pragma unroll
+            for (int u = 0; u < kSB / kWave; ++u) {
+                kk[u] = T[l + u * kWave];
+                vv[u] = V[l + u * kWave];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#pragma unroll
+            for (int u = 0; u < kSB / kWave; ++u) {
+                if (sv[u] & kSNew) {
+                    T[l + u * kWave] = kSentinel;
+                    TS[l + u * kWave] = 0;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#pragma unroll
+            for (int u = 0; u < kSB / kWave; ++u) {
+                if ((sv[u] & kSNew) && (sv[u] & kSPresent)) {
+                    uint32_t p = home_of(hash64((uint64_t)kk[u]));
+                    for (int probe = 0; probe < kSB; ++probe) {
+                        const unsigned long long cur =
+                            atomicCAS(reinterpret_cast<unsigned long long*>(&T[p]),
+                                      (unsigned long long)kSentinel, (unsigned long long)kk[u]);
+                        if (cur == (unsigned long long)kSentinel) {
+                            V[p] = vv[u];
+                            TS[p] = sv[u];
+                            break;
+                        }
+                        p = (p + 1) & (kSB - 1);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // write back the touched slots; count the keys that became present
+        uint32_t added = 0;
+        for (uint32_t i = tid; i < nslot; i += kLT) {
+            const uint8_t s = S.ts[i];
+            if (s & kSNew) t.keys[gbase + i] = S.tk[i];
+            if (s & kSValDirty) t.vals[gbase + i] = S.tv[i];
+            if (s & kSTouched) t.state[gbase + i] = (ep << 2) | (s & (kPresent | kLastPut));
+            added += ((s & kSPresent) && !(s & kSWasPresent)) ? 1u : 0u;
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) added += __shfl_xor(added, d);
+        if (l == 0 && added) atomicAdd(t.n_present, (unsigned long long)added);
+        __syncthreads();  // the next sub-bin reloads the LDS table
+    }
+}
+
 // ---- hot keys: final state ----------------------------------------------------------------------
 __global__ void k_ap_hot_commit(KvTable t, const int64_t* __restrict__ val, const ApHot* hot,
                                 uint32_t* err) {
@@ -1174,8 +1742,11 @@ struct EmitLds {
     uint2 inc[kHMax];      // over the earlier tiles
     int64_t hval[kHMax];
     uint32_t hfl[kHMax];
-    int64_t iret[kTL];     // the tile's cold results in image order (bin runs)
+    int64_t iret[kTL];     // the tile's cold results in image order (bin runs); first the
+                           // image's run marks (MPX_EMIT_CPOS=0)
     uint8_t iconf[kTL];
+    unsigned long long bmax[kTPer * kTW], bpre[kTPer * kTW];  // run marks: per 64-block maxima
+    uint32_t wsum[kTW];
 };
 
 __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restrict__ op,
@@ -1186,6 +1757,7 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
                                                  const int64_t* __restrict__ r_ret,
                                                  const uint8_t* __restrict__ r_conf,
                                                  const uint32_t* __restrict__ rows,
+                                                 const uint32_t* __restrict__ bin_start,
                                                  const ApHot* __restrict__ hot,
                                                  int64_t* __restrict__ ret,
                                                  uint8_t* __restrict__ conf) {
@@ -1211,6 +1783,7 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
     }
     // the cold results, lanes over the tile image: consecutive lanes read consecutive positions of
     // one bin run (the gather in command order touched one line per lane)
+#if MPX_EMIT_CPOS
     {
         const uint32_t nc = tcold[tile];
         const uint32_t* cp = cpos + (uint64_t)tile * kTL;
@@ -1237,6 +1810,87 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
             }
         }
     }
+#else
+    {
+        // the tile's run of bin b starts at partition position rows[tile][b] and ends at the next
+        // tile's start (the bin's end after the last tile); its image start is the exclusive
+        // scan of the run lengths over the bins. An image position's run is the last run start
+        // at or before it: a max-scan of marks (1 + bin) << 40 | (run start - image start + 4096)
+        unsigned long long* M = reinterpret_cast<unsigned long long*>(S.iret);
+        uint32_t rof = 0, cnt = 0;
+        if ((uint32_t)tid < g.nbin) {
+            rof = rows[(uint64_t)tile * g.rowlen + tid];
+            const uint32_t nx = tile + 1 < g.tiles ? rows[(uint64_t)(tile + 1) * g.rowlen + tid]
+                                                   : bin_start[tid + 1];
+            cnt = nx - rof;
+        }
+#pragma unroll
+        for (int u = 0; u < kTPer; ++u) M[tid + u * kTT] = 0ull;
+        uint32_t x = cnt;
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d);
+            if (l >= d) x += y;
+        }
+        if (l == kWave - 1) S.wsum[w] = x;
+        __syncthreads();
+        uint32_t wb = 0, nc = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < kTW; ++w2) {
+            const uint32_t ws = S.wsum[w2];
+            wb += w2 < w ? ws : 0u;
+            nc += ws;
+        }
+        const uint32_t lst = wb + x - cnt;
+        if (cnt)
+            M[lst] = ((unsigned long long)(tid + 1) << 40) | (unsigned long long)(rof - lst + 4096u);
+        __syncthreads();
+        unsigned long long mk[kTPer];
+#pragma unroll
+        for (int u = 0; u < kTPer; ++u) {
+            unsigned long long m = M[tid + u * kTT];
+#pragma unroll
+            for (int d = 1; d < kWave; d <<= 1) {
+                const unsigned long long y = (unsigned long long)__shfl_up((long long)m, d);
+                if (l >= d) m = m > y ? m : y;
+            }
+            mk[u] = m;
+            if (l == kWave - 1) S.bmax[u * kTW + w] = m;  // 64-blocks in image order
+        }
+        __syncthreads();
+        if (w == 0) {
+            unsigned long long m = S.bmax[l];
+#pragma unroll
+            for (int d = 1; d < kWave; d <<= 1) {
+                const unsigned long long y = (unsigned long long)__shfl_up((long long)m, d);
+                if (l >= d) m = m > y ? m : y;
+            }
+            const unsigned long long ex = (unsigned long long)__shfl_up((long long)m, 1);
+            S.bpre[l] = l ? ex : 0ull;
+        }
+        __syncthreads();
+        int64_t xr[kTPer];
+        uint8_t c[kTPer];
+#pragma unroll
+        for (int u = 0; u < kTPer; ++u) {
+            const uint32_t i = tid + u * kTT;
+            const unsigned long long pb = S.bpre[u * kTW + w];
+            const unsigned long long m = mk[u] > pb ? mk[u] : pb;
+            const uint32_t q = (uint32_t)(m & ((1ull << 40) - 1ull)) - 4096u + i;
+            xr[u] = i < nc ? r_ret[q] : 0;
+            c[u] = i < nc ? r_conf[q] : 0;
+        }
+        __syncthreads();  // every mark is read before the results overwrite them
+#pragma unroll
+        for (int u = 0; u < kTPer; ++u) {
+            const uint32_t i = tid + u * kTT;
+            if (i < nc) {
+                S.iret[i] = xr[u];
+                S.iconf[i] = c[u];
+            }
+        }
+    }
+#endif
 #pragma unroll
     for (int r = 0; r < kTPer; ++r) {
         const uint32_t j = jw + r * kWave + l;
@@ -1421,11 +2075,15 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
         k_ap_scan_rows<<<g.ng, 256, 0, stream>>>(g, rows, part, bin_start, hot);
         k_ap_scatter<<<kScatterGrid, kTT, 0, stream>>>(g, op + c0, key + c0, val + c0, n, rows, hot,
                                                   rec_kv, rec_op, ipos, cpos, tcold);
-        k_ap_resolve<<<g.nbin * kRSplit, kRTT, 0, stream>>>(g, t, bin_start, rec_kv, rec_op, r_ret, r_conf,
-                                                 hot, err);
+        if (MPX_RS_LIST)
+            k_ap_resolve_list<<<g.nbin, kLT, 0, stream>>>(g, t, bin_start, rec_kv, rec_op, r_ret,
+                                                          r_conf, hot, err);
+        else
+            k_ap_resolve<<<g.nbin * kRSplit, kRTT, 0, stream>>>(g, t, bin_start, rec_kv, rec_op,
+                                                                r_ret, r_conf, hot, err);
         k_ap_hot_commit<<<1, kHMax, 0, stream>>>(t, val + c0, hot, err);
         k_ap_emit<<<g.tiles, kTT, 0, stream>>>(g, op + c0, val + c0, n, ipos, cpos, tcold, r_ret,
-                                               r_conf, rows,
+                                               r_conf, rows, bin_start,
                                                hot, ret + c0, conf ? conf + c0 : nullptr);
     }
     return hipGetLastError();

@@ -96,6 +96,7 @@ struct mpx_engine {
     // group-step work list (groups the fast kernel hands to the general kernel) + its count
     DevBuf worklist;
     uint32_t* d_wcount = nullptr;
+    hipEvent_t ev_fast0 = nullptr, ev_fast1 = nullptr;  // mpx_group_step_events
     // RCCL
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -755,7 +756,7 @@ int group_step_dev(mpx_engine* e, const mpx_group_batch* b, int64_t* d_totals, v
         return fail(e, MPX_E_INVAL, "n_groups exceeds mpx_config.max_groups");
     HIPCHK(e, mpx::launch_group_step(e->cfg.mode, e->cfg.n_replicas, e->cfg.kv_per_group, b,
                                      (uint32_t*)e->worklist.p, e->d_wcount, d_totals, e->d_err,
-                                     pick(e, stream)));
+                                     pick(e, stream), e->ev_fast0, e->ev_fast1));
     return MPX_OK;
 }
 }  // namespace
@@ -771,6 +772,14 @@ int mpx_group_step_totals_dev(mpx_engine* e, const mpx_group_batch* b, int64_t* 
     if (b && b->n_groups && !b->n_decided)
         return fail(e, MPX_E_INVAL, "mpx_group_step_totals_dev needs n_decided");
     return group_step_dev(e, b, d_totals, stream);
+}
+
+int mpx_group_step_events(mpx_engine* e, void* ev_fast_start, void* ev_fast_end) {
+    if (!e) return MPX_E_INVAL;
+    if (!ev_fast_start != !ev_fast_end) return fail(e, MPX_E_INVAL, "give both events or neither");
+    e->ev_fast0 = (hipEvent_t)ev_fast_start;
+    e->ev_fast1 = (hipEvent_t)ev_fast_end;
+    return MPX_OK;
 }
 
 int mpx_step_totals_dev(mpx_engine* e, const mpx_group_batch* b, int64_t* d_totals,
@@ -862,7 +871,7 @@ int mpx_group_step(mpx_engine* e, const mpx_group_batch* hb) {
     if (ipg > 8192) return fail(e, MPX_E_UNSUPPORTED, "more than 8192 instances per group");
     GROW(e, e->worklist, G * sizeof(uint32_t));
     HIPCHK(e, mpx::launch_group_step(e->cfg.mode, N, (uint32_t)K, &db, (uint32_t*)e->worklist.p,
-                                     e->d_wcount, nullptr, e->d_err, e->stream));
+                                     e->d_wcount, nullptr, e->d_err, e->stream, nullptr, nullptr));
     CK(d2h(e, hb->st_out, d + o_st, ni * 16));
     CK(d2h(e, hb->committed_out, d + o_co, G * 4));
     CK(d2h(e, hb->executed_out, d + o_eo, G * 4));

@@ -54,11 +54,15 @@ hipError_t launch_conflict_batch(const uint8_t* op, const int64_t* key, const ui
 // fused per-group step: tally + executeCommands against per-group compact KV tables.
 // worklist: n_groups u32 + wcount (device) for groups the fast kernel hands on.
 // totals (optional, device): the step's d_totals[0..2] computed inside the same two kernels
-// (per-group partials into kTotSlots accumulators of the control words, folded by the general
-// kernel's last workgroup), so a step needs no k_step_totals launch.
+// (per-group partials into kTotSlots accumulators of the control words, added by the kernel
+// that finishes the group, folded by the general kernel), so a step needs no k_step_totals
+// launch.
+// ev_fast0 / ev_fast1 (optional): recorded on `stream` right before and after the fast kernel's
+// launch (mpx_group_step_events), so a timer can bracket that kernel alone.
 hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
                              const mpx_group_batch* b, uint32_t* worklist, uint32_t* wcount,
-                             int64_t* totals, uint32_t* err, hipStream_t stream);
+                             int64_t* totals, uint32_t* err, hipStream_t stream,
+                             hipEvent_t ev_fast0, hipEvent_t ev_fast1);
 // d_totals[0..2] = decided instances, executed instances, executed commands of the batch
 // step control words (engine-owned, zeroed once): [0] work-list count, [1] its ticket, [4..9]
 // the totals' 64-bit accumulators, [10] their ticket, [16..) the fused totals' partials

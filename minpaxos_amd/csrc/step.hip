@@ -833,6 +833,15 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
         b.kv_cnt_out[g] = total < kvpg ? total : kvpg;
         if (b.n_decided) b.n_decided[g] = S.ndec;
     }
+    // the step totals: this group's decided instances, executed instances and executed commands
+    // into partial slot g % kTotSlots (no-return atomics: nothing waits for them here; the
+    // general kernel, a later launch, folds the slots)
+    if (tacc && t < 3) {
+        const uint32_t v = t == 0 ? S.ndec : (stop > lo ? (t == 1 ? (uint32_t)(stop - lo) : x1 - x0) : 0u);
+        if (v)
+            (void)__hip_atomic_fetch_add(tacc + (g & (kTotSlots - 1)) * 3 + t, (unsigned long long)v,
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     ebits &= 0x7FFFFFFFu;
     if (ebits) raise_err(err, ebits);
     STAMP(6);
@@ -969,6 +978,15 @@ __device__ void group_general(GenLds& S, const mpx_group_batch& b, uint32_t g, i
         b.executed_out[g] = stop > lo ? (int32_t)(stop - 1) : ex_in;
         if (b.n_decided) b.n_decided[g] = S.ndec;
     }
+    if (tacc && t == 0) {  // this group's step totals (performed before the caller's ticket)
+        unsigned long long* p = tacc + (g & (kTotSlots - 1)) * 3;
+        if (S.ndec) atomic_add_done(p, (unsigned long long)S.ndec);
+        if (stop > lo) {
+            atomic_add_done(p + 1, (unsigned long long)(stop - lo));
+            const uint64_t xc = b.cmd_off[gi0 + stop] - b.cmd_off[gi0 + lo];
+            if (xc) atomic_add_done(p + 2, (unsigned long long)xc);
+        }
+    }
 
     const Dict D{S.dkey, S.dval, S.dfirst, S.cnt, S.hslot, S.dpresent, S.dseen, &S.dn,
                  (uint32_t)kDCap, (uint32_t)kHCap};
@@ -1062,47 +1080,14 @@ __device__ __forceinline__ void group_totals(const mpx_group_batch& b, uint32_t 
     }
 }
 
-// (d, xi, xc) summed over the workgroup, valid in thread 0
-__device__ __forceinline__ void block_sum3(unsigned long long& d, unsigned long long& xi,
-                                           unsigned long long& xc) {
-    __shared__ unsigned long long red3[3][kStepBlock / kWave];
-#pragma unroll
-    for (int k = 32; k >= 1; k >>= 1) {
-        d += __shfl_xor(d, k);
-        xi += __shfl_xor(xi, k);
-        xc += __shfl_xor(xc, k);
-    }
-    const int w = threadIdx.x / kWave;
-    if (lane_id() == 0) {
-        red3[0][w] = d;
-        red3[1][w] = xi;
-        red3[2][w] = xc;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        d = xi = xc = 0;
-        for (int k = 0; k < kStepBlock / kWave; ++k) {
-            d += red3[0][k];
-            xi += red3[1][k];
-            xc += red3[2][k];
-        }
-    }
-    __syncthreads();
-}
-
-// Groups per thread and per workgroup of the totals when the work list is empty (the common
-// case): a thread's groups have their loads issued together (two dependent rounds in all)
-constexpr uint32_t kTotPer = 4;
-constexpr uint32_t kTotGroupsPerWg = kStepBlock * kTotPer;
-
-// The work list, and (totals != nullptr) the step totals, so a step with totals is two launches.
-// Empty work list (the common case): no workgroup touches a control word but the first
-// ceil(G / kTotGroupsPerWg), which reduce the totals of their slice of groups from the fast
-// kernel's outputs (a previous kernel), add them with awaited atomics and take a ticket; the
-// last writes the totals and zeroes the accumulators. Otherwise the workgroups with list entries
-// run them, release their outputs (agent-scope fence) and take a ticket among themselves; the
-// last zeroes the list count and, for the totals, acquires and reduces every group itself (a
-// step with spilled groups is rare; its totals need every group's final outputs).
+// The work list, and (totals != nullptr) the step's totals, so a step is two launches. The fast
+// kernel (the previous launch) added every group it kept into the kTotSlots partial slots of the
+// control words with no-return atomics; the groups on the list add theirs here. Empty work list
+// (the common case): workgroup 0 alone folds the slots (atomic exchanges: read and reset), writes
+// the totals and returns; every other workgroup returns at once, whatever it reads. Otherwise
+// the first `workers` workgroups run the list (workgroup 0 among them: it has read the count
+// before any reset), add their groups' totals with awaited atomics and take a ticket; the last
+// zeroes the list count and its ticket and folds the slots.
 template <int MODE>
 __global__ __launch_bounds__(kStepBlock) void k_group_general(mpx_group_batch b, int32_t nrep,
                                                               uint32_t kvpg,
@@ -1111,60 +1096,30 @@ __global__ __launch_bounds__(kStepBlock) void k_group_general(mpx_group_batch b,
                                                               int64_t* totals, uint32_t* err) {
     __shared__ GenLds S;
     __shared__ bool last;
-    unsigned long long* acc = reinterpret_cast<unsigned long long*>(wcount + 4);
+    __shared__ unsigned long long fold[3];
+    unsigned long long* part = reinterpret_cast<unsigned long long*>(wcount + 16);
+    auto fold_totals = [&]() {  // whole workgroup: the kTotSlots x 3 partials into totals[0..2]
+        if (threadIdx.x < 3) fold[threadIdx.x] = 0;
+        __syncthreads();
+        if (threadIdx.x < kTotSlots * 3) {
+            const unsigned long long v = atomic_take(part + threadIdx.x);
+            if (v) atomicAdd(&fold[threadIdx.x % 3], v);
+        }
+        __syncthreads();
+        if (threadIdx.x < 3) totals[threadIdx.x] = (int64_t)fold[threadIdx.x];
+    };
+    static_assert(kTotSlots * 3 <= kStepBlock, "one partial slot word per thread");
     const uint32_t n = *wcount;
     if (n == 0) {
-        if (!totals) return;
-        const uint32_t tw = (b.n_groups + kTotGroupsPerWg - 1) / kTotGroupsPerWg;
-        if (blockIdx.x >= tw) return;
-        unsigned long long d = 0, xi = 0, xc = 0;
-        {
-            uint32_t nd[kTotPer];
-            int32_t ei[kTotPer], eo[kTotPer];
-            uint64_t c0[kTotPer], c1[kTotPer];
-#pragma unroll
-            for (uint32_t k = 0; k < kTotPer; ++k) {  // round 1: the group's outputs
-                const uint32_t g = blockIdx.x * kTotGroupsPerWg + k * kStepBlock + threadIdx.x;
-                const bool v = g < b.n_groups;
-                nd[k] = v ? b.n_decided[g] : 0u;
-                ei[k] = v ? b.executed_in[g] : 0;
-                eo[k] = v ? b.executed_out[g] : -1;
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < kTotPer; ++k) {  // round 2: the executed command range
-                const uint32_t g = blockIdx.x * kTotGroupsPerWg + k * kStepBlock + threadIdx.x;
-                const int64_t lo = ei[k] + 1 < 0 ? 0 : (int64_t)ei[k] + 1;
-                const bool x = g < b.n_groups && eo[k] >= lo && eo[k] < (int32_t)b.ipg;
-                const uint64_t gi0 = (uint64_t)g * b.ipg;
-                c0[k] = x ? b.cmd_off[gi0 + lo] : 0;
-                c1[k] = x ? b.cmd_off[gi0 + eo[k] + 1] : 0;
-                d += nd[k];
-                xi += x ? (unsigned long long)(eo[k] - lo + 1) : 0ull;
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < kTotPer; ++k) xc += c1[k] - c0[k];
-        }
-        block_sum3(d, xi, xc);
-        if (threadIdx.x == 0) {
-            if (d) atomic_add_done(acc, d);
-            if (xi) atomic_add_done(acc + 1, xi);
-            if (xc) atomic_add_done(acc + 2, xc);
-            const uint32_t k = __hip_atomic_fetch_add(wcount + 10, 1u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-            if (k == tw - 1) {
-                (void)atomic_take(wcount + 10);
-                for (int q = 0; q < 3; ++q) totals[q] = (int64_t)atomic_take(acc + q);
-            }
-        }
+        if (totals && blockIdx.x == 0) fold_totals();
         return;
     }
     const uint32_t workers = n < gridDim.x ? n : gridDim.x;
     if (blockIdx.x >= workers) return;
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        group_general<MODE>(S, b, worklist[i], nrep, kvpg, nullptr, err);
+        group_general<MODE>(S, b, worklist[i], nrep, kvpg, totals ? part : nullptr, err);
         __syncthreads();
     }
-    if (totals) __threadfence();  // this workgroup's group outputs, before its ticket
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t k = __hip_atomic_fetch_add(wcount + 1, 1u, __ATOMIC_RELAXED,
@@ -1176,22 +1131,7 @@ __global__ __launch_bounds__(kStepBlock) void k_group_general(mpx_group_batch b,
         }
     }
     __syncthreads();
-    if (!last || !totals) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    unsigned long long d = 0, xi = 0, xc = 0;
-    for (uint32_t g = threadIdx.x; g < b.n_groups; g += kStepBlock) {
-        unsigned long long a0, a1, a2;
-        group_totals(b, g, a0, a1, a2);
-        d += a0;
-        xi += a1;
-        xc += a2;
-    }
-    block_sum3(d, xi, xc);
-    if (threadIdx.x == 0) {
-        totals[0] = (int64_t)d;
-        totals[1] = (int64_t)xi;
-        totals[2] = (int64_t)xc;
-    }
+    if (last && totals) fold_totals();
 }
 
 __global__ void k_fill_worklist(uint32_t* worklist, uint32_t* wcount, uint32_t n) {
@@ -1219,8 +1159,13 @@ int fast_variant(int32_t nrep, uint32_t ipg, uint32_t kvpg) {
 }
 template <int MODE>
 void launch_step(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t* worklist,
-                 uint32_t* wcount, int64_t* totals, uint32_t* err, hipStream_t stream) {
-    unsigned long long* const tacc = nullptr;  // (the totals come from the general kernel)
+                 uint32_t* wcount, int64_t* totals, uint32_t* err, hipStream_t stream,
+                 hipEvent_t ev0, hipEvent_t ev1) {
+    // the step totals' partial slots (control words [16..)): the fast kernel adds the groups it
+    // keeps, the general kernel the listed ones and folds them
+    unsigned long long* const tacc =
+        totals ? reinterpret_cast<unsigned long long*>(wcount + 16) : nullptr;
+    if (ev0) (void)hipEventRecord(ev0, stream);
     switch (fast_variant(nrep, b->ipg, kvpg)) {
     case 1: launch_fast<MODE, FastBase>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
     case 2: launch_fast<MODE, FastRecs>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
@@ -1231,6 +1176,7 @@ void launch_step(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t
         k_fill_worklist<<<(b->n_groups + 255) / 256, 256, 0, stream>>>(worklist, wcount,
                                                                        b->n_groups);
     }
+    if (ev1) (void)hipEventRecord(ev1, stream);
     const unsigned gen_grid = b->n_groups < 256 ? b->n_groups : 256;  // one per CU (LDS)
     k_group_general<MODE><<<gen_grid ? gen_grid : 1, kStepBlock, 0, stream>>>(
         *b, nrep, kvpg, worklist, wcount, totals, err);
@@ -1239,16 +1185,18 @@ void launch_step(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t
 
 hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
                              const mpx_group_batch* b, uint32_t* worklist, uint32_t* wcount,
-                             int64_t* totals, uint32_t* err, hipStream_t stream) {
+                             int64_t* totals, uint32_t* err, hipStream_t stream,
+                             hipEvent_t ev0, hipEvent_t ev1) {
     if (!b->n_groups)
         return totals ? hipMemsetAsync(totals, 0, 3 * sizeof(int64_t), stream) : hipSuccess;
     if (kv_per_group > (uint32_t)kDCap) return hipErrorInvalidValue;
     if (b->ipg > (uint32_t)kMaxIpgBits) return hipErrorInvalidValue;
     if (mode == MPX_MODE_MIN)
-        launch_step<MPX_MODE_MIN>(b, nrep, kv_per_group, worklist, wcount, totals, err, stream);
+        launch_step<MPX_MODE_MIN>(b, nrep, kv_per_group, worklist, wcount, totals, err, stream,
+                                  ev0, ev1);
     else
         launch_step<MPX_MODE_CLASSIC>(b, nrep, kv_per_group, worklist, wcount, totals, err,
-                                      stream);
+                                      stream, ev0, ev1);
     return hipGetLastError();
 }
 

@@ -516,6 +516,10 @@ class Engine:
                     "mpx_event_create")
         return ev.value
 
+    def group_step_events(self, ev0=None, ev1=None):
+        """record ev0 / ev1 around the fast kernel of every later group step (None: off)"""
+        self._check(self.lib.mpx_group_step_events(self.h, ev0, ev1), "mpx_group_step_events")
+
     def event_destroy(self, ev):
         self._check(self.lib.mpx_event_destroy(self.h, ev), "mpx_event_destroy")
 

@@ -252,7 +252,8 @@ hipError_t launch_conflict_batch(const uint8_t*, const int64_t*, const uint64_t*
 hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, uint32_t*, hipStream_t);
 hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group, const mpx_group_batch* b,
                              uint32_t*, uint32_t* ctl, int64_t* totals, uint32_t* err,
-                             hipStream_t s) {
+                             hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    if (ev0) hipEventRecord(ev0, s);
     // the fused form needs the per-group decided counts the oracle writes to n_decided
     std::vector<uint32_t> nd;
     mpx_group_batch bb = *b;
@@ -265,6 +266,7 @@ hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group, cons
     else if (rc == MPX_E_BAD_ID) *err |= kErrBadId;
     else if (rc == MPX_E_KV_FULL) *err |= kErrKvFull;
     else if (rc) *err |= kErrInval;
+    if (ev1) hipEventRecord(ev1, s);
     return totals ? launch_step_totals(&bb, totals, ctl, s) : hipSuccess;
 }
 // k_step_totals (step.hip) over host memory
@@ -287,7 +289,7 @@ hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, uint32_
 }
 #else
 hipError_t launch_group_step(int, int32_t, uint32_t, const mpx_group_batch*, uint32_t*, uint32_t*,
-                             int64_t*, uint32_t*, hipStream_t) { return hipSuccess; }
+                             int64_t*, uint32_t*, hipStream_t, hipEvent_t, hipEvent_t) { return hipSuccess; }
 hipError_t launch_step_totals(const mpx_group_batch*, int64_t*, uint32_t*, hipStream_t) { return hipSuccess; }
 #endif
 uint64_t apply_chunk_commands(uint64_t c, uint64_t m) { return c ? c : m; }

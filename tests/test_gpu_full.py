@@ -102,9 +102,12 @@ def _cmp_group(got, want, G, K):
     eq(got["kv_val"][mask], want["kv_val"][mask], "kv_val")
 
 
+# kv_per_group 256 is the bench's shape (bench.py --kv-per-group default): the FastBase variant
+# the headline times; 512 runs FastKeys (step.hip fast_variant)
+@pytest.mark.parametrize("K", [256, 512], ids=["K256_fastbase", "K512_fastkeys"])
 @pytest.mark.parametrize("mode", [R.MODE_MIN, R.MODE_CLASSIC], ids=["min", "classic"])
-def test_config5_group_step_full(mk_engine, mode):
-    G, ipg, K = 65536, 256, 512
+def test_config5_group_step_full(mk_engine, mode, K):
+    G, ipg = 65536, 256
     b = synth.group_batch(G, ipg, 5, 4, 256, seed=45)
     e, o = mk_engine(5, mode, kv_per_group=K), Oracle(5, mode, kv_per_group=K)
     got = e.group_step(b)
@@ -117,9 +120,11 @@ def test_config5_group_step_full(mk_engine, mode):
     assert int(want2["n_decided"].sum()) > 0.9 * G * ipg * 0.8  # p_ok 0.7 at N = 5: ~92 %
 
 
-def test_config5_n7_full(mk_engine):
-    """N = 7: 6 replies x 256 instances = 1536 records per group, beyond the fast path's image"""
-    G, ipg, K = 16384, 256, 512
+@pytest.mark.parametrize("K", [256, 512], ids=["K256_fastrecs", "K512_fastwide"])
+def test_config5_n7_full(mk_engine, K):
+    """N = 7: 6 replies x 256 instances = 1536 records per group, beyond FastBase's reply image:
+    FastRecs at kv_per_group 256 (the bench's step_n7 line), FastWide at 512"""
+    G, ipg = 65536, 256
     b = synth.group_batch(G, ipg, 7, 4, 256, seed=47)
     e, o = mk_engine(7, R.MODE_MIN, kv_per_group=K), Oracle(7, R.MODE_MIN, kv_per_group=K)
     _cmp_group(e.group_step(b), o.group_step(b), G, K)

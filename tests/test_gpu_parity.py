@@ -780,6 +780,27 @@ def test_group_step_fused_totals(mk_engine, kind):
                 assert ar.get(tot2).tolist() == want
 
 
+def test_group_step_totals_many_groups(mk_engine):
+    """the step totals of a batch of more groups than 256 workgroups x 1024 groups (ADVICE r4:
+    the old empty-list reduction covered only the first 262,144): 300,000 groups, three steps
+    in a row (the partial slots reset themselves), against the oracle's outputs"""
+    from minpaxos_amd.devbuf import Arena
+    N, K, G = 5, 256, 300000
+    b = synth.group_batch(G, 2, N, 2, 64, seed=79)
+    b.setdefault("has_cmds", None)
+    e = mk_engine(N, R.MODE_MIN, kv_per_group=K, max_groups=G)
+    o = Oracle(N, R.MODE_MIN, kv_per_group=K)
+    want = _want_totals(b, o.group_step(b))
+    assert want[0] > 0 and want[2] > 0
+    with Arena(e) as ar:
+        gb, d = _dev_group_batch(ar, b, N, K, True)
+        tot = ar.full(3, np.int64, 0x55)
+        for _ in range(3):
+            e.group_step_totals_dev(gb, tot.ptr, e.stream)
+            e.stream_synchronize(e.stream)
+            assert ar.get(tot).tolist() == want
+
+
 @pytest.mark.gpu
 def test_group_step_graph_replay(mk_engine):
     """mpx_graph_begin / _end / _launch: a group step (+ its totals) captured on a stream and

@@ -25,10 +25,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--mode", type=int, default=0)
+    ap.add_argument("--kv", type=int, default=512, help="kv_per_group (256: FastBase, the bench's)")
+    ap.add_argument("--totals", action="store_true",
+                    help="time mpx_group_step_totals_dev (the bench's step) instead of _dev")
     a = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
-    G, ipg, N, K = a.groups, 256, 5, 512
+    G, ipg, N, K = a.groups, 256, 5, a.kv
     b = synth.group_batch(G, ipg, N, 4, 256, seed=45)
 
     def dt(x):
@@ -46,7 +49,9 @@ def main():
              eo=torch.empty(G, dtype=torch.int32, device=dev),
              op=dt(b["op"]), key=dt(b["key"]), val=dt(b["val"]), coff=dt(b["cmd_off"]),
              ret=torch.zeros(m, dtype=torch.int64, device=dev),
-             conf=torch.zeros(m, dtype=torch.uint8, device=dev))
+             conf=torch.zeros(m, dtype=torch.uint8, device=dev),
+             nd=torch.zeros(G, dtype=torch.int32, device=dev),
+             tot=torch.zeros(3, dtype=torch.int64, device=dev))
     p = lambda t: t.data_ptr()  # noqa: E731
 
     def tables():  # each engine gets its own table buffers (its warm-up fills them)
@@ -60,14 +65,15 @@ def main():
                                   p(d["po"]), p(d["op"]), p(d["key"]), p(d["val"]), p(d["coff"]),
                                   None, p(d["ret"]), p(d["conf"]), p(tb["kc" + i]), p(tb["kk" + i]),
                                   p(tb["kv" + i]), p(tb["kc" + o]), p(tb["kk" + o]),
-                                  p(tb["kv" + o]), None)
+                                  p(tb["kv" + o]), None, p(d["nd"]) if a.totals else None)
 
     engines = []
     for path in a.libs:
         lib = C.CDLL(os.path.abspath(path))
         for name, (res, args) in _lib.SIGNATURES.items():
-            f = getattr(lib, name)
-            f.restype, f.argtypes = res, args
+            f = getattr(lib, name, None)  # (an older build lacks the newer entry points)
+            if f is not None:
+                f.restype, f.argtypes = res, args
         cfg = _lib.MpxConfig(N, a.mode, 0, K, 0, 0)
         h = C.c_void_p()
         assert lib.mpx_open(0, C.byref(cfg), C.byref(h)) == 0
@@ -86,12 +92,16 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(ts)
             for _ in range(a.iters):
-                lib.mpx_group_step_dev(h, C.byref(step), s)
+                if a.totals:
+                    lib.mpx_group_step_totals_dev(h, C.byref(step), C.c_void_p(p(d["tot"])), s)
+                else:
+                    lib.mpx_group_step_dev(h, C.byref(step), s)
             e1.record(ts)
             lib.mpx_synchronize(h)
             times[path].append(e0.elapsed_time(e1) / a.iters)
             if r == 0:
-                outs[path] = (d["ret"].sum().item(), d["co"].sum().item(), tb["kv1"].sum().item())
+                outs[path] = (d["ret"].sum().item(), d["co"].sum().item(), tb["kv1"].sum().item(),
+                              d["tot"].tolist() if a.totals else None)
     ref = None
     for path, ts in times.items():
         same = "" if ref is None else ("  outputs " + ("==" if outs[path] == ref else "DIFFER"))
