@@ -51,10 +51,15 @@
  *     captured into a hipGraph.
  *   - a handle is not re-entrant; use one handle per replica event loop / per GPU.
  *   - the tally (mpx_accept_tally_dev), CLASSIC prepare (mpx_prepare_select_dev), apply
- *     (mpx_apply_dev) and group-step kernels keep control words in the handle between calls
- *     (tickets, maxima, the replica-batch list tags), each reset by the call's last workgroup:
+ *     (mpx_apply_dev), group-step and durable-log replay (mpx_replay_durable_dev) kernels keep
+ *     control words or scratch in the handle between calls (tickets, maxima, the replica-batch
+ *     list tags, the replay's binned-maximum scratch), each reset by the call's last workgroup:
  *     all *_dev calls on one handle must be issued in ONE stream order (one stream, or streams
  *     ordered by events) — two such calls in flight at once corrupt every later call.
+ *   - a captured graph keeps the scratch pointers of the calls it captured: growing a handle's
+ *     scratch afterwards (a larger mpx_apply_reserve / mpx_replay_durable_reserve, or a host-
+ *     pointer mpx_apply / mpx_replay_durable call that needs more) frees the old buffers and
+ *     invalidates such graphs; reserve the largest size before capturing.
  *   - where the reference would panic (nil instance, peer id outside peerCommits), the engine
  *     returns MPX_E_NIL_INSTANCE / MPX_E_BAD_ID and the outputs are unspecified.
  */
@@ -213,7 +218,10 @@ typedef struct mpx_config {
     uint32_t apply_path;    /* MPX_APPLY_AUTO: by call size (the replica-batch kernels up to
                                MPX_APPLY_SMALL_MAX commands, the partitioned pipeline past
                                it - the sort-based one only between MPX_APPLY_SMALL_MAX and
-                               a raised apply_fast_min, or for tables past 2^30 slots); or
+                               a raised apply_fast_min); calls past MPX_APPLY_SMALL_MAX
+                               commands on tables past 2^30 slots are unsupported (the
+                               partitioned pipeline stops there, the sort-based one's result
+                               codes at 2^29 slots: the call fails); or
                                force one of MPX_APPLY_SMALL / _SORTED / _PARTITIONED (SMALL
                                and PARTITIONED where the call / table allow, else AUTO's
                                pick)                                                        */

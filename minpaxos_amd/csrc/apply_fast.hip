@@ -9,49 +9,48 @@
 //   conf[i] = Conflict(previous command on k in this call, command i)
 //   table   : k <- val of the last PUT on k in this call
 // Commands of different keys never interact, and the table (kvtab.hpp) is cut into 256-slot
-// buckets that each hold a closed set of keys. So the log is partitioned by bucket and every
-// bucket is resolved in LDS by one wave, against its own slice of the table, in log order:
+// buckets that each hold a closed set of keys. So the log is partitioned by bin (up to 16
+// buckets, at least 4 bins) and every bin is resolved in LDS by one workgroup, against its own
+// slice of the table, in log order:
 //   k_ap_sclear / k_ap_sample / k_ap_select  64K of the chunk's keys are sampled into a hash of
 //                 counts; the most frequent keys seen at least hot_min times (at most 127) are HOT:
 //                 they skip the partition and are resolved in log order by a per-key max-scan
-//                 (below), so a skewed key space cannot pile onto one wave. Index 0 is always the
+//                 (below), so a skewed key space cannot pile onto one bin. Index 0 is always the
 //                 key INT64_MIN (the table's sentinel, kept in a side slot).
-//   k_ap_count    per 4096-command log tile: commands per bin (16 buckets) of the cold keys, and
-//                 per hot key the last position of any command and of a PUT in the tile
+//   k_ap_count    per 4096-command log tile: commands per bin of the cold keys, and per hot key
+//                 the last position of any command and of a PUT in the tile
 //   scans         k_ap_scan_part / _top / _bins / _rows over the tile rows: bin offsets per tile
 //                 (sums), hot positions before each tile (maxima)
 //   k_ap_scatter  persistent (one workgroup per CU, XCD-contiguous tiles, the next tile
 //                 prefetched): a stable per-bin ranking (per-wave peer masks + wave prefix), the
 //                 tile's cold commands as a bin-sorted image in LDS, copied out as one contiguous
-//                 run per bin (16-byte key/value records + op bytes); per command its index in
-//                 the tile image (ipos, log order), per image position its partition slot (cpos)
-//   k_ap_resolve  one workgroup per bin: its 16 bucket tables in LDS (keys, values, state), the
-//                 bin's records streamed in log order 3072 at a time (the next batch prefetched),
-//                 staged in bucket order, each bucket's records resolved by its wave 64 at a time
-//                 (peer masks within the 64, the bucket table between rounds); results land at
-//                 the record's partition slot; touched slots written back once
+//                 run per bin of 16-byte records (the key's hash with the command's class in its
+//                 two top bits - bin bits the partition implies - and the value); per command its
+//                 index in the tile image (ipos, log order)
+//   k_ap_resolve_list  one workgroup per bin: its table slice in LDS (key hashes, values,
+//                 state), the bin's records streamed in log order 2048 at a time (the next batch
+//                 prefetched); every record of a batch at once finds its slot and joins its slot's
+//                 list of the batch, then walks the list (or, for a slot with many records, reads
+//                 two bitmaps) for its predecessor and last earlier PUT; results stored in
+//                 partition order; touched slots written back once
 //   k_ap_hot_commit  the hot keys' final value and state
 //   k_ap_emit     per tile, log order: the tile's cold results gathered run by run into an LDS
-//                 image (cpos), read back by ipos; a hot command's from the per-wave peer scan,
-//                 the earlier waves' tables and the tile's incoming positions; ret / conf stored
-//                 coalesced
+//                 image (each image position's run found by a binary search of the tile's run
+//                 starts, from the scanned rows), read back by ipos; a hot command's from the
+//                 per-wave peer scan, the earlier waves' tables and the tile's incoming
+//                 positions; ret / conf stored coalesced
 // Table traffic is one read and one write of each bin's slice per call instead of one random probe
-// per command. New keys: a bin whose records both PUT a key absent from the table and GET (or
-// run another op on) an absent key re-runs in two passes (insert every PUT key, then resolve), so
-// a GET before the first PUT of a new key still sees that later PUT as its successor. Calls of
-// several chunks insert every PUT key of the call first, as the fallback pipeline does.
+// per command. New keys: any command on a key the slice does not hold claims a slot for it (a GET
+// before the first PUT of a new key is still that PUT's predecessor); slots whose key never
+// became present are removed before the write-back (k_ap_resolve_list). Calls of several chunks
+// insert every PUT key of the call first, as the fallback pipeline does.
 #include "kvtab.hpp"
 
 namespace mpx {
 
-// diagnostic ablations of k_ap_resolve (variant builds only): 1 no bucket resolve, 2 no result
-// stores, 4 no batch ranking
+// diagnostic ablation of k_ap_resolve_list (variant builds only): 2 no result stores
 #ifndef MPX_RS_ABL
 #define MPX_RS_ABL 0
-#endif
-// diagnostic build: per-phase clock64() totals of k_ap_resolve printed by bin 0 (-DMPX_RS_STAMP=1)
-#ifndef MPX_RS_STAMP
-#define MPX_RS_STAMP 0
 #endif
 // diagnostic ablations of k_ap_scatter: 1 no partition writes, 2 no image either, 4 bin ranks
 // from ballots (match_bits) instead of the LDS peer masks
@@ -72,26 +71,9 @@ constexpr int kMaxBins = 1 << kLgMaxBins;  // partition bins (super-bins past it
 // streams its super-bin's records once per bin, so the cost grows with the table past 2^26 slots;
 // the sort-based pipeline's result codes stop at 2^29 slots)
 constexpr int kLgMaxSub = 8;
-// buckets per bin = waves of the resolve workgroup (MPX_RS_LGBPB: 3 = 8-wave workgroups of half
-// the LDS, two per CU; 4 = 16 waves, one per CU)
-#ifndef MPX_RS_LGBPB
-#define MPX_RS_LGBPB 4
-#endif
-constexpr int kLgMaxBPB = MPX_RS_LGBPB;
+// buckets per bin (the resolve workgroup's LDS table: 16 x 256 slots)
+constexpr int kLgMaxBPB = 4;
 constexpr int kMaxBPB = 1 << kLgMaxBPB;
-// resolve workgroups per bin (MPX_RS_SPLIT): 1 = one 16-wave workgroup per bin (one per CU, its
-// LDS); 2 = two 8-wave workgroups, each resolving 8 of the bin's 16 buckets from the same record
-// stream (half the LDS each: two per CU, one waits at a barrier while the other works)
-#ifndef MPX_RS_SPLIT
-#define MPX_RS_SPLIT 1
-#endif
-constexpr int kRSplit = MPX_RS_SPLIT;
-constexpr int kLgRSplit = kRSplit == 4 ? 2 : (kRSplit == 2 ? 1 : 0);
-static_assert((1 << kLgRSplit) == kRSplit && kRSplit <= kMaxBPB, "resolve split");
-constexpr int kLgRBPW = kLgMaxBPB - kLgRSplit;
-constexpr int kRBPW = 1 << kLgRBPW;    // buckets (= waves) of a resolve workgroup
-constexpr int kRTT = kRBPW * kWave;    // threads of the resolve workgroup
-constexpr int kRTW = kRBPW;
 constexpr int kLgSamples = 16;
 constexpr uint32_t kSamples = 1u << kLgSamples;  // (k_ap_sample divides by a shift)
 constexpr uint32_t kHotIdx = 0x8000u;  // ipos: hot command (| hot index), else image index
@@ -107,11 +89,9 @@ static_assert(kMaxBins <= kTT, "the bin scans take one bin per thread");
 static_assert(kSamples % (64 * 256) == 0, "k_ap_sample: whole samples per thread");
 static_assert((1 << 17) % (16 * kTT) == 0, "k_ap_select reads the sample table 16 counts per thread at a time");
 
-// LDS slot state of k_ap_resolve
+// LDS slot state of k_ap_resolve_list
 constexpr uint8_t kSPresent = 1, kSLastPut = 2, kSTouched = 4, kSValDirty = 8, kSNew = 16,
                   kSWasPresent = 32;
-// k_ap_resolve flags
-constexpr uint32_t kFAbsentOther = 1u, kFNewPut = 2u;
 
 struct ApHot {               // per chunk; written by k_ap_select (+ the scan's totals)
     int64_t key[kHMax];
@@ -128,11 +108,34 @@ struct ApHot {               // per chunk; written by k_ap_select (+ the scan's 
 // of 2^lgsub bins each; the resolve workgroup of a super-bin takes its bins one after another
 // (each pass streams the super-bin's records and resolves those of its bin)
 struct ApGeo {
-    uint32_t lgnb, lgbpb, lgsub, nbin, rowlen, tiles, ng, tpg;
+    uint32_t lgnb, lgbpb, lgsub, nbin, lgnbin, rowlen, tiles, ng, tpg;
 };
 
 __device__ __forceinline__ uint32_t bin_of(uint64_t h, const ApGeo& g) {
     return bucket_of(h, g.lgnb) >> (g.lgbpb + g.lgsub);
+}
+
+// buckets per bin: up to 16, and at least 4 bins (a table has at least 4 buckets): the top two
+// bits of a key's hash are then always bits of its bin
+__host__ __device__ inline uint32_t lgbpb_for(uint32_t lgnb) {
+    const uint32_t x = lgnb >= 2 ? lgnb - 2 : 0;
+    return x < (uint32_t)kLgMaxBPB ? x : (uint32_t)kLgMaxBPB;
+}
+
+// A partition record is 16 bytes: the key's hash (hash64 is a bijection) with its top two bits -
+// bin bits, which the partition itself implies - replaced by the command's class, then the value.
+// The resolve compares hashes (its LDS table holds the hashes of its keys) and recovers a key
+// only to write a new one to the table (unhash64).
+constexpr uint32_t kClsPut = 0, kClsGet = 1, kClsOther = 2;
+__device__ __forceinline__ uint32_t op_class(uint32_t op) {
+    return op == MPX_OP_PUT ? kClsPut : (op == MPX_OP_GET ? kClsGet : kClsOther);
+}
+__device__ __forceinline__ uint64_t rec_pack(uint64_t h, uint32_t cls) {
+    return (h & ~(3ull << 62)) | ((uint64_t)cls << 62);
+}
+// the hash of a record of bin `bin` (its top two bits restored from the bin)
+__device__ __forceinline__ uint64_t rec_hash(uint64_t x, uint32_t bin, const ApGeo& g) {
+    return (x & ~(3ull << 62)) | ((uint64_t)(bin >> (g.lgnbin - 2)) << 62);
 }
 
 typedef __attribute__((address_space(3))) volatile uint8_t lds_u8;
@@ -599,8 +602,7 @@ struct ScatterLds {
     uint16_t cw[kTW][kMaxBins]; // per-wave counts -> exclusive prefix over the waves
     uint8_t W[kTW][kMaxBins];
     unsigned long long PM[kTW][kWave];
-    int4 img[kTL];              // bin-sorted (key, val) of the tile's cold commands
-    uint8_t iop[kTL];
+    int4 img[kTL];              // bin-sorted records of the tile's cold commands
     uint16_t ibin[kTL];
     uint32_t wsum[kTW];
     uint32_t ncold;
@@ -611,8 +613,7 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
                                                     const int64_t* __restrict__ val, uint32_t n,
                                                     const uint32_t* __restrict__ rows,
                                                     const ApHot* __restrict__ hot,
-                                                    int4* __restrict__ rec_kv,
-                                                    uint8_t* __restrict__ rec_op,
+                                                    int4* __restrict__ rec_kv, uint32_t spare,
                                                     uint16_t* __restrict__ ipos,
                                                     uint32_t* __restrict__ cpos,
                                                     uint32_t* __restrict__ tcold) {
@@ -655,12 +656,14 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
         load(tile + tw.step, no, nk, nv);
         const uint32_t roff_nxt = load_roff(tile + tw.step);
         uint32_t bin[kTPer], rank[kTPer];
+        uint64_t hs[kTPer];  // the keys' hashes: the records carry them instead of the keys
         bool cold[kTPer];
 #pragma unroll
         for (int r = 0; r < kTPer; ++r) {
             const uint32_t j = j0 + r * kWave;
             const bool in = j < n;
             const uint64_t h = hash64((uint64_t)k[r]);
+            hs[r] = h;
             const int hh = in ? hot_find(S.hl, nh, k[r], h) : -1;
             if (in && hh >= 0) ipos[j] = (uint16_t)(kHotIdx | (uint32_t)hh);
             cold[r] = in && hh < 0;
@@ -717,22 +720,28 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
             const uint32_t b = bin[r];
             const uint32_t wr = S.cw[w][b] + rank[r];
             const uint32_t ip = S.lstart[b] + wr;
-            S.img[ip] = make_int4((int)(uint32_t)k[r], (int)(uint32_t)((uint64_t)k[r] >> 32),
+            const uint64_t x = rec_pack(hs[r], op_class(o[r]));
+            S.img[ip] = make_int4((int)(uint32_t)x, (int)(uint32_t)(x >> 32),
                                   (int)(uint32_t)v[r], (int)(uint32_t)((uint64_t)v[r] >> 32));
-            S.iop[ip] = (uint8_t)o[r];
             S.ibin[ip] = (uint16_t)b;
             ipos[j0 + r * kWave] = (uint16_t)ip;
         }
         __syncthreads();
-        const uint32_t nc = S.ncold;
+        const uint32_t nc = (MPX_SC_ABL & 3) ? 0u : S.ncold;
         if (tid == 0) tcold[tile] = nc;
-        for (uint32_t i = tid; i < ((MPX_SC_ABL & 3) ? 0u : nc); i += kTT) {
-            const uint32_t b = S.ibin[i];
-            const uint32_t dst = S.roff[b] + (i - S.lstart[b]);
-            if (!(MPX_SC_ABL & 32)) rec_kv[dst] = S.img[i];
-            if (!(MPX_SC_ABL & 8)) rec_op[dst] = S.iop[i];
+        // A fixed number of stores per thread (positions past the tile's cold commands store to
+        // the spare record past the chunk): the wait for the next tile's records, loaded before
+        // them, can then count them (with a variable count it waited for every store of the tile)
+#pragma unroll
+        for (int u = 0; u < kTPer; ++u) {
+            const uint32_t i = tid + u * kTT;
+            const bool live = i < nc;
+            const uint32_t ic = live ? i : 0u;
+            const uint32_t b = S.ibin[ic];
+            const uint32_t dst = live ? S.roff[b] + (i - S.lstart[b]) : spare;
+            if (!(MPX_SC_ABL & 32)) rec_kv[dst] = S.img[ic];
             if (MPX_EMIT_CPOS && !(MPX_SC_ABL & 16))
-                cpos[(uint64_t)tile * kTL + i] = dst;  // image order: emit gathers run by run
+                cpos[live ? (uint64_t)tile * kTL + i : (uint64_t)g.tiles * kTL] = dst;  // emit gathers run by run
         }
         for (int i = tid; i < kTW * kMaxBins / 2; i += kTT) cw32[i] = 0u;  // next tile's counts
         __syncthreads();
@@ -746,414 +755,11 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
     }
 }
 
-// ---- per-bin resolve ------------------------------------------------------------------------------
-constexpr int kRH = 3;             // records per thread per resolve batch
-constexpr int kRT = kRTT * kRH;    // records per batch (3072 at 16 buckets per bin)
-struct ResolveLds {
-    int64_t tk[kRBPW * kSB];
-    int64_t tv[kRBPW * kSB];
-    uint8_t ts[kRBPW * kSB];
-    uint8_t W[kRTW][kSB];
-    unsigned long long PM[kRTW][kWave];
-    int4 skv[kRT];                    // the batch's records in bucket order (log order inside)
-    uint8_t sop[kRT];
-    uint16_t sidx[kRT];               // their index in the batch
-    uint32_t cw[kRH * kRTW][kRBPW];  // per (third, wave): records per bucket -> exclusive prefix
-    uint32_t bcnt[kRBPW], bst[kRBPW];
-    uint32_t flags;
-#if MPX_RS_STAMP
-    unsigned long long ph[8], rb[kRTW];
-#endif
-};
-
 __device__ __forceinline__ int64_t kv_lo_hi(int lo, int hi) {
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
-
-// bucket b of the bin (wave b): its cnt records of this batch, in log order, 64 per round.
-// A round is two stages: A = the slot lookup (claiming slots for new keys) and the peer masks;
-// B = the slot state read, the results, the state update. (Issuing A of round r+1 before B of
-// round r, which it does not depend on, measured slower: the volatile peer-mask accesses keep
-// program order, so nothing overlapped and registers grew.)
-// (results go straight to the batch's partition positions: a batch covers 3072 consecutive ones,
-// so the scattered 8-byte stores of its waves meet in L2)
-struct RoundA {
-    unsigned long long peers, putm;
-    int64_t v;
-    uint32_t idx, sl;
-    bool live, act, isput, isget;
-};
-
-__device__ __forceinline__ RoundA resolve_stage_a(ResolveLds& S, int b, uint32_t cnt, uint32_t st0,
-                                                  uint32_t r, int mode, uint32_t* err) {
-    const int l = lane_id();
-    int64_t* T = S.tk + b * kSB;
-    uint8_t* TS = S.ts + b * kSB;
-    lds_u8* W = (lds_u8*)&S.W[b][0];
-    lds_u64* PM = (lds_u64*)&S.PM[b][0];
-    RoundA a;
-    a.live = r + l < cnt;
-    const uint32_t x = a.live ? st0 + r + l : 0u;
-    const int4 kv = S.skv[x];
-    a.idx = S.sidx[x];
-    const int64_t k = kv_lo_hi(kv.x, kv.y);
-    a.v = kv_lo_hi(kv.z, kv.w);
-    const uint8_t o = S.sop[x];
-    a.isput = o == MPX_OP_PUT;
-    a.isget = o == MPX_OP_GET;
-    // lookup in the bucket, MPX_RS_PROBE (8) slots per step (1 / 2 / 4 measured slower): the worst probe length among the wave's 64 lanes
-    // sets the number of dependent LDS reads
-    int s = -1;
-    uint32_t p = home_of(hash64((uint64_t)k));
-    if (a.live) {
-#ifndef MPX_RS_PROBE
-#define MPX_RS_PROBE 8
-#endif
-        constexpr int kPS = MPX_RS_PROBE;  // slots per probe step
-        for (int step = 0; step < kSB / kPS; ++step) {
-            int64_t c[kPS];
-#pragma unroll
-            for (int u = 0; u < kPS; ++u) c[u] = T[(p + u) & (kSB - 1)];
-            int hit = -1, stop = -1;
-#pragma unroll
-            for (int u = kPS - 1; u >= 0; --u) {
-                if (c[u] == k) hit = u;
-                if (c[u] == kSentinel) stop = u;
-            }
-            if (hit >= 0 && (stop < 0 || hit < stop)) {
-                s = (int)((p + hit) & (kSB - 1));
-                break;
-            }
-            if (stop >= 0) {
-                p = (p + stop) & (kSB - 1);  // the first empty slot: an insert starts here
-                break;
-            }
-            p = (p + kPS) & (kSB - 1);
-        }
-    }
-    if (a.live && s < 0 && a.isput) {  // a key new to the table: claim a slot
-        if (mode == 0) atomicOr(&S.flags, kFNewPut);
-        for (int probe = 0; probe < kSB; ++probe) {
-            const unsigned long long cur =
-                atomicCAS(reinterpret_cast<unsigned long long*>(&T[p]),
-                          (unsigned long long)kSentinel, (unsigned long long)k);
-            if (cur == (unsigned long long)kSentinel) {
-                s = (int)p;
-                TS[p] |= kSNew;
-                break;
-            }
-            if ((int64_t)cur == k) {
-                s = (int)p;
-                break;
-            }
-            p = (p + 1) & (kSB - 1);
-        }
-        if (s < 0) raise_err(err, kErrKvFull);
-    }
-    if (a.live && s < 0 && !a.isput && mode == 0) atomicOr(&S.flags, kFAbsentOther);
-    a.act = a.live && s >= 0;
-    a.sl = a.act ? (uint32_t)s : 0u;
-    a.peers = 0;
-    a.putm = 0;
-    if (__ballot(a.act)) {
-#ifndef MPX_RS_PEERS_LDS
-#define MPX_RS_PEERS_LDS 1
-#endif
-#if MPX_RS_PEERS_LDS
-        a.peers = wave_peers(W, PM, a.sl, a.act);
-#else
-        a.peers = match_bits(a.sl, kLgSB, a.act);
-#endif
-        a.putm = __ballot(a.act && a.isput);
-    }
-    return a;
-}
-
-__device__ __forceinline__ void resolve_stage_b(ResolveLds& S, int b, const RoundA& a,
-                                                uint32_t base, int64_t* __restrict__ r_ret,
-                                                uint8_t* __restrict__ r_conf) {
-    const int l = lane_id();
-    const unsigned long long below = (1ull << l) - 1ull;
-    int64_t* V = S.tv + b * kSB;
-    uint8_t* TS = S.ts + b * kSB;
-    int64_t ret = 0;
-    bool conf = false;
-    if (__ballot(a.act)) {
-        const uint32_t sl = a.sl;
-        const unsigned long long lp = a.peers & below, lput = lp & a.putm;
-        const unsigned long long allput = a.peers & a.putm;
-        const uint8_t stt = a.act ? TS[sl] : 0;
-        const bool hasprev = lp ? true : (stt & kSTouched) != 0;
-        const bool prevput = lp ? ((a.putm >> hi_bit(lp)) & 1ull) != 0 : (stt & kSLastPut) != 0;
-        const int64_t vget = shfl64(a.v, lput ? hi_bit(lput) : l);
-        const int64_t vlast = shfl64(a.v, allput ? hi_bit(allput) : l);
-        const int64_t tab = a.act ? V[sl] : 0;
-        ret = !a.act ? 0
-                     : a.isput ? a.v
-                               : (a.isget ? (lput ? vget : ((stt & kSPresent) ? tab : 0)) : 0);
-        conf = a.act && hasprev && (prevput || a.isput);
-        if (a.act && (a.peers >> l) == 1ull) {  // the round's last command on this slot
-            uint8_t ns = (uint8_t)((stt & (kSPresent | kSValDirty | kSNew | kSWasPresent)) |
-                                   kSTouched | (a.isput ? kSLastPut : 0));
-            if (allput) {
-                V[sl] = vlast;
-                ns |= kSPresent | kSValDirty;
-            }
-            TS[sl] = ns;
-        }
-    }
-    if (a.live && !(MPX_RS_ABL & 2)) {
-        r_ret[base + a.idx] = ret;
-        r_conf[base + a.idx] = conf ? 1 : 0;
-    }
-}
-
-__device__ __forceinline__ void resolve_bucket(ResolveLds& S, int b, uint32_t cnt, uint32_t st0,
-                                              int mode, uint32_t base, int64_t* __restrict__ r_ret,
-                                              uint8_t* __restrict__ r_conf, uint32_t* err) {
-    for (uint32_t r = 0; r < cnt; r += kWave) {
-        const RoundA a = resolve_stage_a(S, b, cnt, st0, r, mode, err);
-        resolve_stage_b(S, b, a, base, r_ret, r_conf);
-    }
-}
-
-__global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
-                                                    const uint32_t* __restrict__ bin_start,
-                                                    const int4* __restrict__ rec_kv,
-                                                    const uint8_t* __restrict__ rec_op,
-                                                    int64_t* __restrict__ r_ret,
-                                                    uint8_t* __restrict__ r_conf, ApHot* hot,
-                                                    uint32_t* err) {
-    __shared__ ResolveLds S;
-    const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
-    const uint32_t bpb = 1u << g.lgbpb;
-    // this workgroup's (super-)bin and its part of the bin's buckets: the parts of one bin run on
-    // one XCD (workgroup x runs on XCD x % 8), dispatched together, so the second stream of the
-    // bin's records is an L2 hit
-    uint32_t bin = blockIdx.x, part = 0;
-    if (kRSplit > 1) {
-        if ((g.nbin & 7u) == 0) {
-            bin = (blockIdx.x >> (3 + kLgRSplit)) * 8u + (blockIdx.x & 7u);
-            part = (blockIdx.x >> 3) & (kRSplit - 1);
-        } else {
-            bin = blockIdx.x >> kLgRSplit;
-            part = blockIdx.x & (kRSplit - 1);
-        }
-    }
-    const uint32_t b_lo = part * kRBPW;
-    if (b_lo >= bpb) return;  // a table of fewer buckets per bin than the workgroups cover
-    const uint32_t nb = bpb - b_lo < (uint32_t)kRBPW ? bpb - b_lo : (uint32_t)kRBPW;
-    const int lgnbw = (int)(g.lgbpb < (uint32_t)kLgRBPW ? g.lgbpb : (uint32_t)kLgRBPW);
-    const uint32_t nslot = nb * kSB;
-    const uint32_t nsub = 1u << g.lgsub;
-    const uint32_t ep = t.epoch[0];
-    const uint32_t r0 = bin_start[bin], r1 = bin_start[bin + 1];
-    if (r0 == r1) return;  // no records: nothing read, nothing touched (small calls, hot-heavy chunks)
-    const unsigned long long below = (1ull << l) - 1ull;
-    // a record's bucket among this workgroup's (meaningful where member() holds)
-    auto local_bucket = [&](uint64_t h) {
-        return ((bucket_of(h, g.lgnb) & (bpb - 1)) - b_lo) & (uint32_t)(kRBPW - 1);
-    };
-    for (uint32_t sub = 0; sub < nsub; ++sub) {
-    // bin (bin << lgsub) | sub: its records are those of the super-bin's log whose bucket falls
-    // in it (every pass streams the super-bin's records), of those the ones in this part
-    const uint64_t gbase = ((((uint64_t)bin << g.lgsub) | sub) * bpb + b_lo) * kSB;
-    auto member = [&](uint64_t h) {
-        const uint32_t bk = bucket_of(h, g.lgnb);
-        return ((bk >> g.lgbpb) & (nsub - 1)) == sub && ((bk & (bpb - 1)) - b_lo) < nb;
-    };
-    auto load_tables = [&]() {
-        for (uint32_t i = tid; i < nslot; i += kRTT) {
-            S.tk[i] = t.keys[gbase + i];
-            S.tv[i] = t.vals[gbase + i];
-            const uint32_t x = t.state[gbase + i];
-            const uint8_t pres = (uint8_t)(x & kPresent);
-            S.ts[i] = (uint8_t)(pres | (pres ? kSWasPresent : 0) |
-                                ((x >> 2) == ep ? (kSTouched | (x & kLastPut)) : 0u));
-        }
-    };
-    load_tables();
-    S.PM[w][l] = 0ull;
-    if (tid == 0) S.flags = 0;
-    __syncthreads();
-    for (int mode = 0; mode < 2; ++mode) {
-        if (mode == 1) {
-            // two-pass form: insert every PUT key of the bin, then resolve again from the start
-            if ((S.flags & (kFAbsentOther | kFNewPut)) != (kFAbsentOther | kFNewPut)) break;
-            __syncthreads();
-            load_tables();
-            if (tid == 0) atomicAdd(&hot->restarts, 1u);
-            __syncthreads();
-            for (uint32_t q = r0 + tid; q < r1; q += kRTT) {
-                if (rec_op[q] != MPX_OP_PUT) continue;
-                const int4 kv = rec_kv[q];
-                const int64_t k = kv_lo_hi(kv.x, kv.y);
-                const uint64_t h = hash64((uint64_t)k);
-                if (!member(h)) continue;
-                const uint32_t b = local_bucket(h);
-                int64_t* T = S.tk + b * kSB;
-                uint32_t p = home_of(h);
-                bool done = false;
-                for (int probe = 0; probe < kSB && !done; ++probe) {
-                    const unsigned long long cur =
-                        atomicCAS(reinterpret_cast<unsigned long long*>(&T[p]),
-                                  (unsigned long long)kSentinel, (unsigned long long)k);
-                    if (cur == (unsigned long long)kSentinel) {
-                        S.ts[b * kSB + p] |= kSNew;
-                        done = true;
-                    } else if ((int64_t)cur == k) {
-                        done = true;
-                    }
-                    p = (p + 1) & (kSB - 1);
-                }
-                if (!done) raise_err(err, kErrKvFull);
-            }
-            __syncthreads();
-        }
-        // the next batch is loaded while this one is resolved
-        for (int i = tid; i < kRH * kRTW * kRBPW; i += kRTT) (&S.cw[0][0])[i] = 0u;
-        __syncthreads();
-        // (ops held as 32-bit values: packed into one register as bytes, the compiler waits for the
-        // prefetch at the loop back-edge)
-        int4 kv[kRH];
-        uint32_t o[kRH];
-#pragma unroll
-        for (int hh = 0; hh < kRH; ++hh) {
-            const uint32_t q = r0 + hh * kRTT + tid;
-            kv[hh] = q < r1 ? rec_kv[q] : make_int4(0, 0, 0, 0);
-            o[hh] = q < r1 ? rec_op[q] : 0;
-        }
-#if MPX_RS_STAMP
-        if (tid < 8) S.ph[tid] = 0;
-        if (tid < kRTW) S.rb[tid] = 0;
-        __syncthreads();
-        unsigned long long c0 = clock64(), c1;
-#define RS_STAMP(i) do { c1 = clock64(); if (tid == 0) S.ph[i] += c1 - c0; c0 = c1; } while (0)
-#else
-#define RS_STAMP(i) do {} while (0)
-#endif
-        for (uint32_t base = r0; base < r1; base += kRT) {
-            uint32_t bl[kRH], rk[kRH];
-            bool live[kRH];
-#pragma unroll
-            for (int hh = 0; hh < kRH; ++hh) {
-                const uint32_t i = hh * kRTT + tid;
-                const uint64_t h = hash64((uint64_t)kv_lo_hi(kv[hh].x, kv[hh].y));
-                live[hh] = base + i < r1 && member(h);
-                bl[hh] = local_bucket(h);
-                rk[hh] = 0;
-                if (MPX_RS_ABL & 4) continue;
-                const unsigned long long m = match_bits(bl[hh], lgnbw, live[hh]);
-                rk[hh] = (uint32_t)__popcll(m & below);
-                if (live[hh] && (m >> l) == 1ull)  // the last lane of its bucket: the count
-                    S.cw[hh * kRTW + w][bl[hh]] = (uint32_t)__popcll(m);
-            }
-            RS_STAMP(0);
-            __syncthreads();
-            RS_STAMP(1);
-            // every wave computes the prefixes its own records need (lane b: bucket b), so no wave
-            // waits for another between the ranking and the staging
-            {
-                const uint32_t b = (uint32_t)l & (kRBPW - 1);
-                // per half: the records of this wave's earlier groups, and of all groups
-                uint32_t pre[kRH], all[kRH];
-#pragma unroll
-                for (int hh = 0; hh < kRH; ++hh) {
-                    uint32_t c[kRTW];
-#pragma unroll
-                    for (int v = 0; v < kRTW; ++v) c[v] = b < nb ? S.cw[hh * kRTW + v][b] : 0u;
-                    pre[hh] = 0;
-                    all[hh] = 0;
-#pragma unroll
-                    for (int v = 0; v < kRTW; ++v) {
-                        pre[hh] += v < w ? c[v] : 0u;
-                        all[hh] += c[v];
-                    }
-                }
-                uint32_t tot = 0;
-#pragma unroll
-                for (int hh = 0; hh < kRH; ++hh) {  // earlier halves come first in log order
-                    pre[hh] += tot;
-                    tot += all[hh];
-                }
-                uint32_t sc = tot;  // inclusive scan over the buckets (each kRBPW-lane segment)
-#pragma unroll
-                for (int d = 1; d < kRBPW; d <<= 1) {
-                    const uint32_t y = __shfl_up(sc, d);
-                    if ((l & (kRBPW - 1)) >= d) sc += y;
-                }
-                const uint32_t st = sc - tot;
-                if (w == 0 && l < kRBPW && b < nb) {
-                    S.bcnt[b] = tot;
-                    S.bst[b] = st;
-                }
-                // position of each record: bucket start + earlier groups + rank in its group
-#pragma unroll
-                for (int hh = 0; hh < kRH; ++hh) {
-                    const int bb = (int)bl[hh];
-                    const uint32_t x = (uint32_t)__shfl((int)(st + pre[hh]), bb) + rk[hh];
-                    if (live[hh]) {
-                        S.skv[x] = kv[hh];
-                        S.sop[x] = (uint8_t)o[hh];
-                        S.sidx[x] = (uint16_t)(hh * kRTT + tid);
-                    }
-                }
-            }
-            // the next batch's records load while this one resolves (issued only now: a wait for
-            // them must not be needed before this batch's records are in LDS)
-#pragma unroll
-            for (int hh = 0; hh < kRH; ++hh) {
-                const uint32_t q = base + kRT + hh * kRTT + tid;
-                kv[hh] = q < r1 ? rec_kv[q] : make_int4(0, 0, 0, 0);
-                o[hh] = q < r1 ? rec_op[q] : 0;
-            }
-            RS_STAMP(2);
-            __syncthreads();
-            RS_STAMP(3);
-            for (int i = tid; i < kRH * kRTW * kRBPW; i += kRTT) (&S.cw[0][0])[i] = 0u;
-#if MPX_RS_STAMP
-            const unsigned long long rb0 = clock64();
-#endif
-            if (!(MPX_RS_ABL & 1) && (uint32_t)w < nb)
-                resolve_bucket(S, w, S.bcnt[w], S.bst[w], mode, base, r_ret, r_conf, err);
-#if MPX_RS_STAMP
-            if (l == 0) S.rb[w] += clock64() - rb0;
-#endif
-            RS_STAMP(4);
-            __syncthreads();
-            RS_STAMP(5);
-        }
-        __syncthreads();
-    }
-#if MPX_RS_STAMP
-    if (blockIdx.x == 0 && sub == 0 && tid == 0) {
-        unsigned long long mx = 0, sm = 0;
-        for (int i = 0; i < kRTW; ++i) {
-            mx = S.rb[i] > mx ? S.rb[i] : mx;
-            sm += S.rb[i];
-        }
-        printf("RS_STAMP bin0 recs=%u rank=%llu bar1=%llu prefix+sorted=%llu bar2=%llu resolve(w0)=%llu bar3=%llu rb_max=%llu rb_mean=%llu\n",
-               r1 - r0, S.ph[0], S.ph[1], S.ph[2], S.ph[3], S.ph[4], S.ph[5], mx, sm / kRTW);
-    }
-#endif
-    // write back the touched slots; count the keys that became present
-    uint32_t added = 0;
-    for (uint32_t i = tid; i < nslot; i += kRTT) {
-        const uint8_t s = S.ts[i];
-        if (s & kSNew) t.keys[gbase + i] = S.tk[i];
-        if (s & kSValDirty) t.vals[gbase + i] = S.tv[i];
-        if (s & kSTouched) t.state[gbase + i] = (ep << 2) | (s & (kPresent | kLastPut));
-        added += ((s & kSPresent) && !(s & kSWasPresent)) ? 1u : 0u;
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) added += __shfl_xor(added, d);
-    if (l == 0 && added) atomicAdd(t.n_present, (unsigned long long)added);
-    __syncthreads();  // the next bin reloads the LDS tables
-    }
-}
-
-// ---- per-bin resolve, list form (the default; MPX_RS_LIST=0 builds the bucket rounds above) ----
+// ---- per-bin resolve -------------------------------------------------------------------------
 // One workgroup per bin, every record of a batch at once instead of 64 per wave and round:
 //   P1  each record finds its slot in the bin's LDS table (a command on a key the table does not
 //       hold claims a slot for it, PUT or not: a GET before the first PUT of a new key must still
@@ -1170,11 +776,8 @@ __global__ __launch_bounds__(kRTT) void k_ap_resolve(ApGeo g, KvTable t,
 // table of the present keys. A bucket that runs out of slots re-runs the bin in the two-pass form
 // (every PUT key inserted first; other commands on absent keys then have no PUT in the call and
 // resolve to 0 without a slot).
-#ifndef MPX_RS_LIST
-#define MPX_RS_LIST 1
-#endif
 #ifndef MPX_RL_PER
-#define MPX_RL_PER 3
+#define MPX_RL_PER 2
 #endif
 // result stores: plain (default: the emit reads them back soon, through L2) or nontemporal
 #ifndef MPX_RL_NT
@@ -1218,8 +821,10 @@ static_assert(kLB % 32 == 0 && kLWords <= 2 * kWave, "a wave scans a heavy bitma
 struct ListLds {
     int64_t tk[kLSlots];
     int64_t tv[kLSlots];
-    uint32_t head[kLSlots];  // per slot: (batch tag << kLIdx) | (1 + the last record pushed)
-    uint32_t cnt[2][kLSlots / 2];  // per batch parity, two 16-bit slot counts a word
+    // (one word past the slots: the target of the records without a slot, so the pushes and
+    // counts need no branch)
+    uint32_t head[kLSlots + 2];  // per slot: (batch tag << kLIdx) | (1 + the last record pushed)
+    uint32_t cnt[2][kLSlots / 2 + 1];  // per batch parity, two 16-bit slot counts a word
     uint8_t ts[kLSlots];
     uint16_t link[kLB];      // per record: (PUT << 15) | (1 + the record pushed before it)
     int64_t bval[kLB];       // per record: its value (read for PUTs)
@@ -1238,10 +843,9 @@ struct ListLds {
 __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                                                          const uint32_t* __restrict__ bin_start,
                                                          const int4* __restrict__ rec_kv,
-                                                         const uint8_t* __restrict__ rec_op,
                                                          int64_t* __restrict__ r_ret,
-                                                         uint8_t* __restrict__ r_conf, ApHot* hot,
-                                                         uint32_t* err) {
+                                                         uint8_t* __restrict__ r_conf, uint32_t spare,
+                                                         ApHot* hot, uint32_t* err) {
     __shared__ ListLds S;
     const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
     const uint32_t bpb = 1u << g.lgbpb;
@@ -1251,6 +855,9 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
     const uint32_t ep = t.epoch[0];
     const uint32_t r0 = bin_start[bin], r1 = bin_start[bin + 1];
     if (r0 == r1) return;  // no records: nothing read, nothing touched
+    // the LDS table holds hashes; a free slot holds the hash of INT64_MIN (the sentinel key,
+    // which never reaches a bin: it is always hot index 0)
+    const int64_t kHS = (int64_t)hash64((uint64_t)kSentinel);
     for (uint32_t sub = 0; sub < nsub; ++sub) {
         const uint64_t gbase = ((((uint64_t)bin << g.lgsub) | sub) * bpb) * kSB;
         auto member = [&](uint64_t h) {
@@ -1261,7 +868,8 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
             if (mode == 1 && !rerun) break;
             __syncthreads();  // the previous pass is done with the LDS
             for (uint32_t i = tid; i < nslot; i += kLT) {
-                S.tk[i] = t.keys[gbase + i];
+                const int64_t key = t.keys[gbase + i];
+                S.tk[i] = key == kSentinel ? kHS : (int64_t)hash64((uint64_t)key);
                 S.tv[i] = t.vals[gbase + i];
                 const uint32_t x = t.state[gbase + i];
                 const uint8_t pres = (uint8_t)(x & kPresent);
@@ -1269,7 +877,7 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                                     ((x >> 2) == ep ? (kSTouched | (x & kLastPut)) : 0u));
                 S.head[i] = 0u;
             }
-            for (uint32_t i = tid; i < (uint32_t)kLSlots; i += kLT) (&S.cnt[0][0])[i] = 0u;
+            for (uint32_t i = tid; i < (uint32_t)(2 * (kLSlots / 2 + 1)); i += kLT) (&S.cnt[0][0])[i] = 0u;
             for (uint32_t i = tid; i < (uint32_t)(kLHeavy * kLWords); i += kLT) {
                 (&S.hb[0][0])[i] = 0u;
                 (&S.hp[0][0])[i] = 0u;
@@ -1282,10 +890,11 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
             if (mode == 1) {  // two-pass form: every PUT key of the bin first
                 if (tid == 0) atomicAdd(&hot->restarts, 1u);
                 for (uint32_t q = r0 + tid; q < r1; q += kLT) {
-                    if (rec_op[q] != MPX_OP_PUT) continue;
                     const int4 kv = rec_kv[q];
-                    const int64_t k = kv_lo_hi(kv.x, kv.y);
-                    const uint64_t h = hash64((uint64_t)k);
+                    const uint64_t x = (uint64_t)kv_lo_hi(kv.x, kv.y);
+                    if ((uint32_t)(x >> 62) != kClsPut) continue;
+                    const uint64_t h = rec_hash(x, bin, g);
+                    const int64_t k = (int64_t)h;
                     if (!member(h)) continue;
                     const uint32_t bb = (bucket_of(h, g.lgnb) & (bpb - 1)) * kSB;
                     uint32_t p = home_of(h);
@@ -1293,8 +902,8 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                     for (int probe = 0; probe < kSB && !done; ++probe) {
                         const unsigned long long cur =
                             atomicCAS(reinterpret_cast<unsigned long long*>(&S.tk[bb + p]),
-                                      (unsigned long long)kSentinel, (unsigned long long)k);
-                        if (cur == (unsigned long long)kSentinel) {
+                                      (unsigned long long)kHS, (unsigned long long)k);
+                        if (cur == (unsigned long long)kHS) {
                             S.ts[bb + p] |= kSNew;
                             done = true;
                         } else if ((int64_t)cur == k) {
@@ -1307,12 +916,10 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                 __syncthreads();
             }
             int4 kv[kLPer];
-            uint32_t o[kLPer];
 #pragma unroll
             for (int hh = 0; hh < kLPer; ++hh) {
                 const uint32_t q = r0 + hh * kLT + tid;
                 kv[hh] = rec_kv[q < r1 ? q : r1 - 1];
-                o[hh] = rec_op[q < r1 ? q : r1 - 1];
             }
             uint32_t tag = 0;
 #if MPX_RL_STAMP
@@ -1337,12 +944,14 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
 #pragma unroll
                 for (int hh = 0; hh < kLPer; ++hh) {
                     const uint32_t i = hh * kLT + tid;
-                    k[hh] = kv_lo_hi(kv[hh].x, kv[hh].y);
+                    const uint64_t x = (uint64_t)kv_lo_hi(kv[hh].x, kv[hh].y);
+                    const uint32_t cls = (uint32_t)(x >> 62);
+                    const uint64_t h = rec_hash(x, bin, g);
+                    k[hh] = (int64_t)h;  // (the table is probed by hash)
                     v[hh] = kv_lo_hi(kv[hh].z, kv[hh].w);
-                    const uint64_t h = hash64((uint64_t)k[hh]);
                     const bool live = base + i < r1 && member(h);
-                    cl[hh] = (live ? 1u : 0u) | (o[hh] == MPX_OP_PUT ? 2u : 0u) |
-                             (o[hh] == MPX_OP_GET ? 4u : 0u);
+                    cl[hh] = (live ? 1u : 0u) | (cls == kClsPut ? 2u : 0u) |
+                             (cls == kClsGet ? 4u : 0u);
                     bbs[hh] = (bucket_of(h, g.lgnb) & (bpb - 1)) * kSB;
                     ps[hh] = home_of(h);
 #pragma unroll
@@ -1356,7 +965,7 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
 #pragma unroll
                     for (int u = 3; u >= 0; --u) {
                         if (c[hh][u] == k[hh]) hit = u;
-                        if (c[hh][u] == kSentinel) stop = u;
+                        if (c[hh][u] == kHS) stop = u;
                     }
                     int s = -1;
                     if (hit >= 0 && (stop < 0 || hit < stop)) s = (int)((ps[hh] + hit) & (kSB - 1));
@@ -1382,7 +991,7 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
 #pragma unroll
                         for (int u = 3; u >= 0; --u) {
                             if (cc[u] == k[hh]) hit = u;
-                            if (cc[u] == kSentinel) stop = u;
+                            if (cc[u] == kHS) stop = u;
                         }
                         if (hit >= 0 && (stop < 0 || hit < stop)) {
                             s = (int)((p + hit) & (kSB - 1));
@@ -1408,8 +1017,8 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                         for (int probe = 0; probe < kSB; ++probe) {
                             const unsigned long long cur =
                                 atomicCAS(reinterpret_cast<unsigned long long*>(&S.tk[bb + p]),
-                                          (unsigned long long)kSentinel, (unsigned long long)k[hh]);
-                            if (cur == (unsigned long long)kSentinel) {
+                                          (unsigned long long)kHS, (unsigned long long)k[hh]);
+                            if (cur == (unsigned long long)kHS) {
                                 s = (int)p;
                                 S.ts[bb + p] |= kSNew;
                                 break;
@@ -1427,24 +1036,24 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                     }
                     sl[hh] = s;
                 }
+                // (branch-free: a record without a slot pushes onto and counts in the spare word)
                 uint32_t olds[kLPer];
 #pragma unroll
                 for (int hh = 0; hh < kLPer; ++hh) {
                     const uint32_t i = hh * kLT + tid;
                     sl[hh] = sl[hh] >= 0 ? (int)(bbs[hh] + (uint32_t)sl[hh]) : -1;
-                    olds[hh] = sl[hh] >= 0 ? atomicExch(&S.head[sl[hh]], (tag << kLIdx) | (i + 1u)) : 0u;
+                    const uint32_t x = sl[hh] >= 0 ? (uint32_t)sl[hh] : (uint32_t)kLSlots;
+                    olds[hh] = atomicExch(&S.head[x], (tag << kLIdx) | (i + 1u));
                 }
                 uint32_t cnts[kLPer];
 #pragma unroll
                 for (int hh = 0; hh < kLPer; ++hh) {
                     const uint32_t i = hh * kLT + tid;
-                    cnts[hh] = 0;
-                    if (sl[hh] < 0) continue;
-                    const uint32_t x = (uint32_t)sl[hh];
+                    const uint32_t x = sl[hh] >= 0 ? (uint32_t)sl[hh] : (uint32_t)kLSlots;
                     const bool isput = (cl[hh] & 2u) != 0;
                     const uint32_t pv = (olds[hh] >> kLIdx) == tag ? (olds[hh] & kLIdxMask) : 0u;
                     S.link[i] = (uint16_t)((isput ? 0x8000u : 0u) | pv);
-                    if (isput) S.bval[i] = v[hh];
+                    S.bval[i] = v[hh];  // (read for PUTs only)
                     const uint32_t sh = 16u * (x & 1u);
                     cnts[hh] = (atomicAdd(&S.cnt[par][x >> 1], 1u << sh) >> sh) & 0xFFFFu;
                 }
@@ -1460,7 +1069,6 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                 for (int hh = 0; hh < kLPer; ++hh) {  // (clamped, not guarded: no branch)
                     const uint32_t q = base + kLB + hh * kLT + tid;
                     kv[hh] = rec_kv[q < r1 ? q : r1 - 1];
-                    o[hh] = rec_op[q < r1 ? q : r1 - 1];
                 }
                 RL_STAMP(0);
                 __syncthreads();
@@ -1532,7 +1140,8 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
 #pragma unroll
                 for (int hh = 0; hh < kLPer; ++hh) {
                     const int x = sl[hh] >= 0 ? sl[hh] : 0;
-                    j1[hh] = sl[hh] >= 0 && !(cl[hh] >> 4) ? (S.head[x] & kLIdxMask) : 0u;
+                    const uint32_t hw = S.head[x];  // (unconditional: no branch around the load)
+                    j1[hh] = sl[hh] >= 0 && !(cl[hh] >> 4) ? (hw & kLIdxMask) : 0u;
                     stt[hh] = S.ts[x];
                     tabv[hh] = S.tv[x];
                     prev[hh] = lastput[hh] = -1;
@@ -1606,13 +1215,17 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                     }
                     // (a record of this pass without a slot: the two-pass form's key that is
                     // absent and never PUT in the call - NIL, no conflict)
-                    if ((cl[hh] & 1u) && !(MPX_RS_ABL & 2)) {
+                    // (every record stores, those not of this pass to the spare slot past the chunk:
+                    // a fixed count, so the wait for the next batch, loaded before these stores,
+                    // does not wait for them)
+                    const uint32_t dst = (cl[hh] & 1u) ? base + i : spare;
+                    if (!(MPX_RS_ABL & 2)) {
 #if MPX_RL_NT
-                        st_stream(r_ret + base + i, ret);
-                        st_stream(r_conf + base + i, (uint8_t)(conf ? 1 : 0));
+                        st_stream(r_ret + dst, ret);
+                        st_stream(r_conf + dst, (uint8_t)(conf ? 1 : 0));
 #else
-                        r_ret[base + i] = ret;
-                        r_conf[base + i] = conf ? 1 : 0;
+                        r_ret[dst] = ret;
+                        r_conf[dst] = conf ? 1 : 0;
 #endif
                     }
                 }
@@ -1638,7 +1251,10 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                         S.hp[w][l + kWave] = 0u;
                     }
                 }
-                if (tid == 0) S.nheavy[par] = 0u;
+                if (tid == 0) {
+                    S.nheavy[par] = 0u;
+                    S.cnt[par][kLSlots / 2] = 0u;
+                }
                 RL_STAMP(5);
             }
             __syncthreads();
@@ -1674,7 +1290,7 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
 #pragma unroll
             for (int u = 0; u < kSB / kWave; ++u) {
                 if (sv[u] & kSNew) {
-                    T[l + u * kWave] = kSentinel;
+                    T[l + u * kWave] = kHS;
                     TS[l + u * kWave] = 0;
                 }
             }
@@ -1682,12 +1298,12 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
 #pragma unroll
             for (int u = 0; u < kSB / kWave; ++u) {
                 if ((sv[u] & kSNew) && (sv[u] & kSPresent)) {
-                    uint32_t p = home_of(hash64((uint64_t)kk[u]));
+                    uint32_t p = home_of((uint64_t)kk[u]);
                     for (int probe = 0; probe < kSB; ++probe) {
                         const unsigned long long cur =
                             atomicCAS(reinterpret_cast<unsigned long long*>(&T[p]),
-                                      (unsigned long long)kSentinel, (unsigned long long)kk[u]);
-                        if (cur == (unsigned long long)kSentinel) {
+                                      (unsigned long long)kHS, (unsigned long long)kk[u]);
+                        if (cur == (unsigned long long)kHS) {
                             V[p] = vv[u];
                             TS[p] = sv[u];
                             break;
@@ -1702,7 +1318,7 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
         uint32_t added = 0;
         for (uint32_t i = tid; i < nslot; i += kLT) {
             const uint8_t s = S.ts[i];
-            if (s & kSNew) t.keys[gbase + i] = S.tk[i];
+            if (s & kSNew) t.keys[gbase + i] = (int64_t)unhash64((uint64_t)S.tk[i]);
             if (s & kSValDirty) t.vals[gbase + i] = S.tv[i];
             if (s & kSTouched) t.state[gbase + i] = (ep << 2) | (s & (kPresent | kLastPut));
             added += ((s & kSPresent) && !(s & kSWasPresent)) ? 1u : 0u;
@@ -1745,7 +1361,8 @@ struct EmitLds {
     int64_t iret[kTL];     // the tile's cold results in image order (bin runs); first the
                            // image's run marks (MPX_EMIT_CPOS=0)
     uint8_t iconf[kTL];
-    unsigned long long bmax[kTPer * kTW], bpre[kTPer * kTW];  // run marks: per 64-block maxima
+    uint16_t lst[kMaxBins];  // per bin: image start of the tile's run (MPX_EMIT_CPOS=0)
+    uint32_t dof[kMaxBins];  //          partition start of the run - image start
     uint32_t wsum[kTW];
 };
 
@@ -1814,9 +1431,9 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
     {
         // the tile's run of bin b starts at partition position rows[tile][b] and ends at the next
         // tile's start (the bin's end after the last tile); its image start is the exclusive
-        // scan of the run lengths over the bins. An image position's run is the last run start
-        // at or before it: a max-scan of marks (1 + bin) << 40 | (run start - image start + 4096)
-        unsigned long long* M = reinterpret_cast<unsigned long long*>(S.iret);
+        // scan of the run lengths over the bins. An image position's run: a binary search of the
+        // runs' image starts (the last one at or before it; an empty run starts where the next
+        // one does, so the search never ends on one)
         uint32_t rof = 0, cnt = 0;
         if ((uint32_t)tid < g.nbin) {
             rof = rows[(uint64_t)tile * g.rowlen + tid];
@@ -1824,8 +1441,6 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
                                                    : bin_start[tid + 1];
             cnt = nx - rof;
         }
-#pragma unroll
-        for (int u = 0; u < kTPer; ++u) M[tid + u * kTT] = 0ull;
         uint32_t x = cnt;
 #pragma unroll
         for (int d = 1; d < kWave; d <<= 1) {
@@ -1841,46 +1456,37 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
             wb += w2 < w ? ws : 0u;
             nc += ws;
         }
-        const uint32_t lst = wb + x - cnt;
-        if (cnt)
-            M[lst] = ((unsigned long long)(tid + 1) << 40) | (unsigned long long)(rof - lst + 4096u);
-        __syncthreads();
-        unsigned long long mk[kTPer];
-#pragma unroll
-        for (int u = 0; u < kTPer; ++u) {
-            unsigned long long m = M[tid + u * kTT];
-#pragma unroll
-            for (int d = 1; d < kWave; d <<= 1) {
-                const unsigned long long y = (unsigned long long)__shfl_up((long long)m, d);
-                if (l >= d) m = m > y ? m : y;
-            }
-            mk[u] = m;
-            if (l == kWave - 1) S.bmax[u * kTW + w] = m;  // 64-blocks in image order
+        if ((uint32_t)tid < g.nbin) {
+            const uint32_t lst = wb + x - cnt;
+            S.lst[tid] = (uint16_t)lst;
+            S.dof[tid] = rof - lst;
         }
         __syncthreads();
-        if (w == 0) {
-            unsigned long long m = S.bmax[l];
+        uint32_t lo[kTPer];
 #pragma unroll
-            for (int d = 1; d < kWave; d <<= 1) {
-                const unsigned long long y = (unsigned long long)__shfl_up((long long)m, d);
-                if (l >= d) m = m > y ? m : y;
+        for (int u = 0; u < kTPer; ++u) lo[u] = 0;
+        // (the searches side by side; a wave whose positions are all past the tile's cold
+        // commands skips them: a skewed chunk's tiles have few)
+        const uint32_t nsearch = nc > (uint32_t)(tid - l) ? (nc - (uint32_t)(tid - l) + kTT - 1) / kTT : 0u;
+        for (uint32_t half = nsearch ? g.nbin >> 1 : 0u; half; half >>= 1) {
+#pragma unroll
+            for (int u = 0; u < kTPer; ++u) {
+                if ((uint32_t)u >= nsearch) continue;  // (wave-uniform)
+                const uint32_t i = tid + u * kTT;
+                lo[u] = S.lst[lo[u] + half] <= i ? lo[u] + half : lo[u];
             }
-            const unsigned long long ex = (unsigned long long)__shfl_up((long long)m, 1);
-            S.bpre[l] = l ? ex : 0ull;
         }
-        __syncthreads();
+        uint32_t q[kTPer];
+#pragma unroll
+        for (int u = 0; u < kTPer; ++u) q[u] = S.dof[lo[u]] + tid + u * kTT;
         int64_t xr[kTPer];
         uint8_t c[kTPer];
 #pragma unroll
         for (int u = 0; u < kTPer; ++u) {
             const uint32_t i = tid + u * kTT;
-            const unsigned long long pb = S.bpre[u * kTW + w];
-            const unsigned long long m = mk[u] > pb ? mk[u] : pb;
-            const uint32_t q = (uint32_t)(m & ((1ull << 40) - 1ull)) - 4096u + i;
-            xr[u] = i < nc ? r_ret[q] : 0;
-            c[u] = i < nc ? r_conf[q] : 0;
+            xr[u] = i < nc ? r_ret[q[u]] : 0;
+            c[u] = i < nc ? r_conf[q[u]] : 0;
         }
-        __syncthreads();  // every mark is read before the results overwrite them
 #pragma unroll
         for (int u = 0; u < kTPer; ++u) {
             const uint32_t i = tid + u * kTT;
@@ -1972,16 +1578,17 @@ emit_out:
 // ---- launcher ---------------------------------------------------------------------------------
 namespace {
 struct FastLayout {
-    uint64_t gk, gc, rows, part, ctot, bin_start, rec_kv, rec_op, ipos, cpos, tcold, r_ret, r_conf, hot, total;
+    uint64_t gk, gc, rows, part, ctot, bin_start, rec_kv, ipos, cpos, tcold, r_ret, r_conf, hot, total;
 };
 
 ApGeo geo_for(const KvTable& t, uint64_t n) {
     ApGeo g{};
     g.lgnb = t.lgnb;
-    g.lgbpb = t.lgnb < (uint32_t)kLgMaxBPB ? t.lgnb : (uint32_t)kLgMaxBPB;
+    g.lgbpb = lgbpb_for(t.lgnb);
     const uint32_t lgbins = t.lgnb - g.lgbpb;
     g.lgsub = lgbins > (uint32_t)kLgMaxBins ? lgbins - (uint32_t)kLgMaxBins : 0u;
-    g.nbin = 1u << (lgbins - g.lgsub);
+    g.lgnbin = lgbins - g.lgsub;
+    g.nbin = 1u << g.lgnbin;
     g.rowlen = g.nbin + 2 * kHMax;
     g.tiles = (uint32_t)((n + kTL - 1) / kTL);
     if (!g.tiles) g.tiles = 1;
@@ -2002,13 +1609,12 @@ FastLayout fast_layout(const KvTable& t, uint64_t c) {
     L.part = o; o += al((uint64_t)kScanGroups * g.rowlen * 4);
     L.ctot = o; o += al((uint64_t)g.nbin * 4);
     L.bin_start = o; o += al(((uint64_t)g.nbin + 1) * 4);
-    L.rec_kv = o; o += al(c * 16);
-    L.rec_op = o; o += al(c);
+    L.rec_kv = o; o += al((c + 1) * 16);  // (+ the spare record: see k_ap_scatter)
     L.ipos = o; o += al(c * 2);
-    L.cpos = o; o += al((uint64_t)g.tiles * kTL * 4);
+    L.cpos = o; o += al(((uint64_t)g.tiles * kTL + 1) * 4);
     L.tcold = o; o += al((uint64_t)g.tiles * 4);
-    L.r_ret = o; o += al(c * 8);
-    L.r_conf = o; o += al(c);
+    L.r_ret = o; o += al((c + 1) * 8);  // (+ the spare result: see k_ap_resolve_list)
+    L.r_conf = o; o += al(c + 1);
     L.hot = o; o += al(sizeof(ApHot));
     L.total = o;
     return L;
@@ -2016,8 +1622,7 @@ FastLayout fast_layout(const KvTable& t, uint64_t c) {
 }  // namespace
 
 bool apply_fast_ok(const KvTable& t) {
-    const uint32_t lgbpb = t.lgnb < (uint32_t)kLgMaxBPB ? t.lgnb : (uint32_t)kLgMaxBPB;
-    return t.lgnb - lgbpb <= (uint32_t)(kLgMaxBins + kLgMaxSub);
+    return t.lgnb >= 2 && t.lgnb - lgbpb_for(t.lgnb) <= (uint32_t)(kLgMaxBins + kLgMaxSub);
 }
 
 uint64_t apply_fast_work_bytes(const KvTable& t, uint64_t c) { return fast_layout(t, c).total; }
@@ -2044,7 +1649,6 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
     uint32_t* ctot = (uint32_t*)(b + L.ctot);
     uint32_t* bin_start = (uint32_t*)(b + L.bin_start);
     int4* rec_kv = (int4*)(b + L.rec_kv);
-    uint8_t* rec_op = (uint8_t*)(b + L.rec_op);
     uint16_t* ipos = (uint16_t*)(b + L.ipos);
     uint32_t* cpos = (uint32_t*)(b + L.cpos);
     uint32_t* tcold = (uint32_t*)(b + L.tcold);
@@ -2074,13 +1678,9 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
         k_ap_scan_bins<<<1, kTT, 0, stream>>>(g, ctot, bin_start);
         k_ap_scan_rows<<<g.ng, 256, 0, stream>>>(g, rows, part, bin_start, hot);
         k_ap_scatter<<<kScatterGrid, kTT, 0, stream>>>(g, op + c0, key + c0, val + c0, n, rows, hot,
-                                                  rec_kv, rec_op, ipos, cpos, tcold);
-        if (MPX_RS_LIST)
-            k_ap_resolve_list<<<g.nbin, kLT, 0, stream>>>(g, t, bin_start, rec_kv, rec_op, r_ret,
-                                                          r_conf, hot, err);
-        else
-            k_ap_resolve<<<g.nbin * kRSplit, kRTT, 0, stream>>>(g, t, bin_start, rec_kv, rec_op,
-                                                                r_ret, r_conf, hot, err);
+                                                  rec_kv, (uint32_t)C, ipos, cpos, tcold);
+        k_ap_resolve_list<<<g.nbin, kLT, 0, stream>>>(g, t, bin_start, rec_kv, r_ret, r_conf,
+                                                      (uint32_t)C, hot, err);
         k_ap_hot_commit<<<1, kHMax, 0, stream>>>(t, val + c0, hot, err);
         k_ap_emit<<<g.tiles, kTT, 0, stream>>>(g, op + c0, val + c0, n, ipos, cpos, tcold, r_ret,
                                                r_conf, rows, bin_start,

@@ -415,8 +415,8 @@ __global__ __launch_bounds__(kSmT) void k_small_walk(KvTable t, const uint8_t* _
     }
     __syncthreads();
     // every command here is LONG, i.e. on a list of more than kWalkMax commands, so none is alone
-    // on its key: each gets its rank in log order (wave w holds positions [512 w, 512 w + 512),
-    // round k of it the 64 positions 512 w + 64 k + lane)
+    // on its key: each gets its rank in log order (wave w holds positions [1024 w, 1024 w + 1024),
+    // round k of it the 64 positions 1024 w + 64 k + lane)
     uint32_t m2, rank[kSmPer];
     bool shared[kSmPer];
     uint32_t n_new = 0;

@@ -29,6 +29,17 @@ __device__ __forceinline__ uint64_t hash64(uint64_t x) {
     return x;
 }
 
+// the inverse of hash64 (every step of the finalizer is a bijection): the partitioned apply moves
+// keys as their hashes and recovers a key only where it writes one to the table
+__device__ __forceinline__ uint64_t unhash64(uint64_t x) {
+    x ^= (x >> 31) ^ (x >> 62);
+    x *= 0x319642B2D24D8EC3ull;  // 0x94D049BB133111EB^-1 mod 2^64
+    x ^= (x >> 27) ^ (x >> 54);
+    x *= 0x96DE1B173F119089ull;  // 0xBF58476D1CE4E5B9^-1 mod 2^64
+    x ^= (x >> 30) ^ (x >> 60);
+    return x;
+}
+
 __device__ __forceinline__ uint32_t bucket_of(uint64_t h, uint32_t lgnb) {
     return lgnb ? (uint32_t)(h >> (64 - lgnb)) : 0u;
 }
