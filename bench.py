@@ -438,28 +438,29 @@ def step_bench(a, rk):
             eng.memset(wb.at(lo), 0xFF, (hi - lo) * 4, comp)
     eng.synchronize()
 
-    def step(i, timed):
+    def step(i, timed, evs=None, cs=None):
+        cs = cs or comm  # the collective's stream
         buf = i & 1
         if i >= 2:  # buffers `buf` are free once the all-reduce of step i-2 has used them
             eng.stream_wait_event(comp, ev_comm[buf])
         # the timed steps' HIP events bracket the group kernel alone: the engine records them
         # right before and after its launch (mpx_group_step_events), the work-list kernel and
         # the totals are outside
-        eng.group_step_events(*(ev_k[i] if timed else (None, None)))
+        eng.group_step_events(*(evs or (ev_k[i] if timed else (None, None))))
         # the group step, then its totals (decided, executed instances, executed commands)
         if not a.separate_totals:
             eng.group_step_totals_dev(steps[buf], d["tot"][buf].ptr, comp)
         else:
             eng.group_step_dev(steps[buf], comp)
-        if timed:
+        if timed or evs:
             eng.group_step_events()
         if a.separate_totals:
             eng.step_totals_dev(steps[buf], d["tot"][buf].ptr, comp)
         eng.event_record(ev_done[buf], comp)
-        eng.stream_wait_event(comm, ev_done[buf])
+        eng.stream_wait_event(cs, ev_done[buf])
         eng.step_allreduce_oop_dev(d["wms"][buf].ptr, d["wmr"][buf].ptr, G_total,
-                                   d["tot"][buf].ptr, R_TOTALS, comm)
-        eng.event_record(ev_comm[buf], comm)
+                                   d["tot"][buf].ptr, R_TOTALS, cs)
+        eng.event_record(ev_comm[buf], cs)
 
     for i in range(a.warmup):
         step(i, False)
@@ -478,22 +479,25 @@ def step_bench(a, rk):
     graph_info = None
     use_graph = a.graph == "on" or (a.graph == "auto" and world == 1)
     if use_graph:
-        # the same step sequence replayed from hipGraphs: a chunk of U steps is one capture on
-        # the compute stream (the second stream joins through ev_done and is joined back at
-        # the chunk's end); graph launches on one stream run one after another, so a chunk's
-        # first two steps need no wait on the previous chunk's collectives
+        # the same step sequence replayed from hipGraphs, a chunk of U steps per capture. The
+        # graph runs the collective on the compute stream: a replayed graph executed the
+        # second stream's copy and its event edges between a step's kernels and the next step's
+        # anyway (profiles/r05/step), and one stream leaves out two cross-stream dependencies
+        # per step (--emulate-world 8: 0.113 -> 0.097 ms per step). The graph pass is one
+        # process: the one-rank all-reduce is RCCL's copy.
         U = min(a.steps, 64)
         chunks = [U] * (a.steps // U) + ([a.steps % U] if a.steps % U else [])
+        # a second U-step graph, the same steps with a HIP event pair around each group kernel
+        # (external event nodes, which cost a replay a few us per step, so the timed graphs have
+        # none): replayed once after the timed region, it gives the roofline's kernel times
+        ev_g = [(eng.event_create(), eng.event_create()) for _ in range(U)]
 
-        def capture(n):
+        def capture(n, evs=False):
             eng.graph_begin(comp)
             for j in range(n):
-                step(j, False)
-            if comm != comp:
-                eng.stream_wait_event(comp, ev_comm[(n - 1) & 1])  # join the second stream
-                if n > 1:
-                    eng.stream_wait_event(comp, ev_comm[(n - 2) & 1])
+                step(j, False, ev_g[j] if evs else None, cs=comp)
             return eng.graph_end(comp)
+        g_ev = None
         try:
             graphs = {n: capture(n) for n in set(chunks)}
         except MpxError as e:  # "auto" on a library without stream capture (the CPU stub)
@@ -501,6 +505,11 @@ def step_bench(a, rk):
                 raise
             graph_info = {"used": False, "unavailable": str(e)[:160]}
             use_graph = False
+        if use_graph:
+            try:
+                g_ev = capture(U, evs=True)
+            except MpxError:  # (a runtime without external event nodes: the enqueued pass's)
+                g_ev = None
     if use_graph:
         for _ in range(max(a.warmup, 1)):
             eng.graph_launch(graphs[U], comp)
@@ -515,9 +524,21 @@ def step_bench(a, rk):
         t1 = time.perf_counter()
         elapsed_graph = rk.max(t1 - t0)
         graph_info = {"used": True, "steps_per_graph": U, "graph_launches": len(chunks),
+                      "collective_stream": "compute (in the graph)",
                       "ms_per_step_graph": elapsed_graph / a.steps * 1e3,
-                      "ms_per_step_no_graph": elapsed / a.steps * 1e3}
-        last = (chunks[-1] - 1) & 1
+                      "ms_per_step_no_graph": elapsed / a.steps * 1e3,
+                      "kernel_ms_median_enqueued": float(np.median(kern_ms))}
+        if g_ev is not None:
+            for _ in range(3):  # (the first replays of a fresh graph run cold)
+                eng.graph_launch(g_ev, comp)
+            eng.synchronize()
+            kern_ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in ev_g]
+            graph_info["kernel_times"] = ("the third replay of the timed graph's steps with an "
+                                          "event pair around each group kernel")
+            eng.graph_destroy(g_ev)
+        else:
+            graph_info["kernel_times"] = "the enqueued pass's events"
+        last = ((U if g_ev is not None else chunks[-1]) - 1) & 1  # the last replayed step
         elapsed = elapsed_graph
         for gx in graphs.values():
             eng.graph_destroy(gx)
@@ -593,7 +614,7 @@ def step_bench(a, rk):
                 "collective": ("one RCCL group per step: out-of-place all-reduce(max) of 2 x "
                                "groups_total int32 watermarks + all-reduce(sum) of 3 int64 step "
                                "totals, "
-                               + ("on the compute stream" if a.no_overlap else
+                               + ("on the compute stream" if a.no_overlap or use_graph else
                                   "on a second stream overlapping the next step's kernel")),
             },
             "value_counts": "instances decided by the step (quorum crossings), all ranks",
@@ -612,10 +633,11 @@ def step_bench(a, rk):
                 "kernel_ms_min": float(np.min(kern_ms)),
                 "frac_at_median": alg / (kern_med_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                 "timing": ("HIP events recorded by the engine right before and after each "
-                           "k_group_fast launch (mpx_group_step_events) on the compute stream, in "
-                           "the enqueued (non-graph) timed pass; the work-list kernel and the "
-                           "collective are outside; achieved from their mean, the median beside "
-                           "it (SURVEY 8(d)); ms_per_step is the graph-replay pass"),
+                           "k_group_fast launch (mpx_group_step_events) on the compute stream - "
+                           "in the replayed hipGraph (external event nodes) when the line is the "
+                           "graph pass, as ms_per_step is, else in the enqueued pass; the "
+                           "work-list kernel and the collective are outside; achieved from their "
+                           "mean, the median beside it (SURVEY 8(d))"),
             },
             "decided_instances_per_step": n_decided,
             "executed_instances_per_step": n_exec_inst,

@@ -54,6 +54,13 @@ __device__ unsigned long long mpx_stamp_acc[16];
 #define MPX_ABLATE 0
 #endif
 
+// the fast kernel's per-chunk slot match: LDS peer masks (0) or ballots over the slot bits (1:
+// 4 KB less LDS, 7-8 workgroups per CU instead of 6, but 0.667 -> 0.755 ms per config-5 step
+// in a same-box A/B, tools/gpu_step_ab.sh: more resident groups contend for the memory system)
+#ifndef MPX_STEP_BALLOT
+#define MPX_STEP_BALLOT 0
+#endif
+
 constexpr int kStepBlock = 256;
 constexpr uint32_t kLock = 0xFFFFFFFFu;
 constexpr uint32_t kDead = 0xFFFFFFFEu;
@@ -325,10 +332,12 @@ struct FastLds {
             // command used the slot, whether the last one was a PUT, 1 + the last PUT relative
             // to the wave's first command (0 = none)
             uint16_t tab[kFWaves * kFH];
+#if !MPX_STEP_BALLOT
             // per wave, the chunk match: slot -> a lane of the chunk on that slot (the class),
             // class -> mask of the chunk's lanes on the slot
             uint8_t win[kFWaves * kFH];
             unsigned long long pmask[kFWaves * kWave];
+#endif
         } b;
     } u;
     unsigned long long hkey[kFH];  // slot -> key; kFreeKey = free
@@ -649,11 +658,13 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
     for (int k = 0; k < kFH * 2 / (kWave * 16); ++k)  // 16-byte stores clear the wave's table
         reinterpret_cast<uint4*>(T)[l + k * kWave] = make_uint4(0u, 0u, 0u, 0u);
     // volatile LDS pointers: every access below is a real ds_* instruction, in program order
+#if !MPX_STEP_BALLOT
     typedef __attribute__((address_space(3))) volatile uint8_t lds_u8;
     typedef __attribute__((address_space(3))) volatile unsigned long long lds_u64;
     lds_u8* W = (lds_u8*)(S.u.b.win + wv * kFH);
     lds_u64* PM = (lds_u64*)(S.u.b.pmask + wv * kWave);
     PM[l] = 0ull;
+#endif
     const unsigned long long lanebit = 1ull << l;
     const unsigned long long below = lanebit - 1ull;
     const uint32_t wfirst = (uint32_t)wv * kWaveCmds;  // the wave's first command
@@ -689,6 +700,18 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
         // matter: it only names the slot's class within the chunk); every lane ORs its bit into
         // its class's mask, reads the mask back, and clears it for the next chunk
         unsigned long long peers = 0;
+#if MPX_STEP_BALLOT
+        {  // one ballot per slot bit (no LDS scratch: 4 KB less per workgroup, 7 per CU)
+            unsigned long long m = livem;
+#pragma unroll
+            for (int i = 0; i < Cfg::kFHB; ++i) {
+                const bool bit = (sl >> i) & 1u;
+                const unsigned long long bm = __ballot(bit);
+                m &= bit ? bm : ~bm;
+            }
+            peers = live ? m : 0ull;
+        }
+#else
         if (live) {
             W[sl] = (uint8_t)l;
             const uint32_t cls = W[sl];
@@ -697,6 +720,7 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
             peers = PM[cls];
             PM[cls] = 0ull;
         }
+#endif
         const unsigned long long putm = __ballot(live && isput);
         const unsigned long long lp_m = peers & below;
         const unsigned long long lput_m = lp_m & putm;
@@ -1141,6 +1165,18 @@ __global__ void k_fill_worklist(uint32_t* worklist, uint32_t* wcount, uint32_t n
 }
 
 namespace {
+// a timing event on `stream`; while the stream is being captured into a graph, as an external
+// event-record node of the graph, so every replay records it (a plain record inside a capture
+// only orders the capture's streams)
+void record_timing_event(hipEvent_t ev, hipStream_t stream) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(stream, &cs);
+    if (cs == hipStreamCaptureStatusActive)
+        (void)hipEventRecordWithFlags(ev, stream, hipEventRecordExternal);
+    else
+        (void)hipEventRecord(ev, stream);
+}
+
 template <int MODE, class Cfg>
 void launch_fast(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t* worklist,
                  uint32_t* wcount, unsigned long long* tacc, uint32_t* err, hipStream_t stream) {
@@ -1165,7 +1201,7 @@ void launch_step(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t
     // keeps, the general kernel the listed ones and folds them
     unsigned long long* const tacc =
         totals ? reinterpret_cast<unsigned long long*>(wcount + 16) : nullptr;
-    if (ev0) (void)hipEventRecord(ev0, stream);
+    if (ev0) record_timing_event(ev0, stream);
     switch (fast_variant(nrep, b->ipg, kvpg)) {
     case 1: launch_fast<MODE, FastBase>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
     case 2: launch_fast<MODE, FastRecs>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
@@ -1176,7 +1212,7 @@ void launch_step(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t
         k_fill_worklist<<<(b->n_groups + 255) / 256, 256, 0, stream>>>(worklist, wcount,
                                                                        b->n_groups);
     }
-    if (ev1) (void)hipEventRecord(ev1, stream);
+    if (ev1) record_timing_event(ev1, stream);
     const unsigned gen_grid = b->n_groups < 256 ? b->n_groups : 256;  // one per CU (LDS)
     k_group_general<MODE><<<gen_grid ? gen_grid : 1, kStepBlock, 0, stream>>>(
         *b, nrep, kvpg, worklist, wcount, totals, err);
