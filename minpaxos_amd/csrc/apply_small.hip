@@ -131,6 +131,14 @@ __device__ __forceinline__ uint32_t block_excl_sum(SmallLds& S, uint32_t v) {
 // probe[p] = slot | kMissBit (resume position) | kNoSlot; probe[kSmMax + p] = state word.
 constexpr uint32_t kMissBit = 0x80000000u;
 constexpr int kProbeBlock = 256;
+// MPX_SMALL_FOLD=1 (A/B builds): the re-probe runs at the start of the walk kernel, its
+// workgroups then meet at a grid barrier (all of them are resident: at most 16, one per CU)
+// before the walks, so a call is two launches; 0 (the default): three launches. Same-box A/B
+// (5000 / 16000 commands, events): 14.0-14.2 / 14.4-14.5 us folded vs 13.7-13.9 / 14.0-14.1 us
+// - the grid barrier costs what the launch it saves does
+#ifndef MPX_SMALL_FOLD
+#define MPX_SMALL_FOLD 0
+#endif
 
 // push command p onto its slot's list of this call
 __device__ __forceinline__ uint32_t call_tag(const KvTable& t) { return t.probe[kCtlOff + 1] + 1u; }
@@ -138,24 +146,16 @@ __device__ __forceinline__ void list_push(const KvTable& t, uint32_t tag, uint32
                                           bool put) {
     const uint32_t old = atomicExch(&t.lhead[slot], (tag << kPosBits) | p);
     const uint32_t nx = (old >> kPosBits) == tag ? (old & kPosMask) : kLinkEnd;
-    t.probe[kLinkOff + p] = nx | (put ? kLinkPut : 0u);
+    // (at the device's coherence point: a re-probe's push is walked by other workgroups of the
+    // same kernel)
+    __hip_atomic_store(&t.probe[kLinkOff + p], nx | (put ? kLinkPut : 0u), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(kProbeBlock) void k_small_probe(KvTable t, const uint8_t* __restrict__ op,
-                                                       const int64_t* __restrict__ key,
-                                                       const int64_t* __restrict__ val, uint32_t m,
-                                                       int64_t* __restrict__ ret, uint32_t* err,
-                                                       bool host_out) {
-    const uint32_t p = blockIdx.x * kProbeBlock + threadIdx.x;
-    if (p >= m) return;
-    const uint32_t tag = call_tag(t);
-    const uint8_t o = op[p];
-    const int64_t k = key[p];
-    const int64_t v = val[p];
-    // the later kernels read the commands from here (device memory)
-    reinterpret_cast<int64_t*>(t.probe + kSmallKeyOff)[p] = k;
-    reinterpret_cast<int64_t*>(t.probe + kSmallValOff)[p] = v;
-    reinterpret_cast<uint8_t*>(t.probe + kSmallOpOff)[p] = o;
+// command p's probe (k_small_probe, and the one-launch form's first phase)
+__device__ __forceinline__ void probe_cmd(const KvTable& t, uint32_t tag, uint8_t o, int64_t k,
+                                          int64_t v, uint32_t p, int64_t* __restrict__ ret,
+                                          uint32_t* err) {
     const bool put = o == MPX_OP_PUT;
     if (put) ret[p] = v;  // a PUT returns its value
     uint32_t slot = kNoSlot;
@@ -192,14 +192,35 @@ __global__ __launch_bounds__(kProbeBlock) void k_small_probe(KvTable t, const ui
     }
     uint32_t st = 0;
     if (!(slot & kMissBit)) {  // (kNoSlot has the bit too)
-        list_push(t, tag, slot, p, put);
+        // the slot's state and value at call start are loaded before the push (they do not
+        // depend on it): one round trip for the three instead of three
         st = t.state[slot];
-        if (!put) ret[p] = (o == MPX_OP_GET && (st & kPresent)) ? t.vals[slot] : 0;
+        const int64_t v0 = t.vals[slot];
+        list_push(t, tag, slot, p, put);
+        if (!put) ret[p] = (o == MPX_OP_GET && (st & kPresent)) ? v0 : 0;
     } else if (!put) {
         ret[p] = 0;  // absent at call start: NIL (a PUT of this call cannot precede a miss)
     }
     t.probe[p] = slot;
     t.probe[kSmMax + p] = st;
+}
+
+__global__ __launch_bounds__(kProbeBlock) void k_small_probe(KvTable t, const uint8_t* __restrict__ op,
+                                                       const int64_t* __restrict__ key,
+                                                       const int64_t* __restrict__ val, uint32_t m,
+                                                       int64_t* __restrict__ ret, uint32_t* err,
+                                                       bool host_out) {
+    const uint32_t p = blockIdx.x * kProbeBlock + threadIdx.x;
+    if (p >= m) return;
+    const uint32_t tag = call_tag(t);
+    const uint8_t o = op[p];
+    const int64_t k = key[p];
+    const int64_t v = val[p];
+    // the later kernels read the commands from here (device memory)
+    reinterpret_cast<int64_t*>(t.probe + kSmallKeyOff)[p] = k;
+    reinterpret_cast<int64_t*>(t.probe + kSmallValOff)[p] = v;
+    reinterpret_cast<uint8_t*>(t.probe + kSmallOpOff)[p] = o;
+    probe_cmd(t, tag, o, k, v, p, ret, err);
     // host-mapped results: performed at system scope before the kernel ends, so the walk kernel's
     // completion flag (stored after its own results) can never overtake them
     if (host_out) __threadfence_system();
@@ -208,10 +229,8 @@ __global__ __launch_bounds__(kProbeBlock) void k_small_probe(KvTable t, const ui
 // ---- 2. the lookups that met a free slot, again now that every claim of the call is in --------
 // (the slots before the recorded position hold other keys for good); a key found now was claimed
 // by this call: not present at call start, state word 0 (as recorded)
-__global__ __launch_bounds__(kProbeBlock) void k_small_reprobe(KvTable t,
-                                                         const int64_t* __restrict__ key,
-                                                         uint32_t m) {
-    const uint32_t p = blockIdx.x * kProbeBlock + threadIdx.x;
+__device__ __forceinline__ void reprobe_one(const KvTable& t, const int64_t* __restrict__ key,
+                                            uint32_t m, uint32_t p) {
     if (p >= m) return;
     const uint32_t s = t.probe[p];
     if (s == kNoSlot || !(s & kMissBit)) return;
@@ -229,7 +248,36 @@ __global__ __launch_bounds__(kProbeBlock) void k_small_reprobe(KvTable t,
         pos = (pos & ~(uint32_t)(kSB - 1)) | ((pos + 1) & (kSB - 1));
     }
     if (slot != kNoSlot) list_push(t, call_tag(t), slot, p, false);  // (a miss is never a PUT)
-    t.probe[p] = slot;
+    // (read by the LONG phase, maybe in another workgroup of the same kernel)
+    __hip_atomic_store(&t.probe[p], slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kProbeBlock) void k_small_reprobe(KvTable t,
+                                                         const int64_t* __restrict__ key,
+                                                         uint32_t m) {
+    reprobe_one(t, key, m, blockIdx.x * kProbeBlock + threadIdx.x);
+}
+
+// every workgroup of the grid here before any goes on (all are resident: the walk grid is at most
+// kSmMax / kSmT = 16 one-per-CU workgroups). Each thread's agent-scope stores are performed before
+// its workgroup arrives. A bounded wait: past ~0.2 s the call fails (kErrInval) instead of hanging.
+constexpr uint32_t kGridCtr = kCtlOff + 3;  // the arrivals (reset by the call's last workgroup)
+__device__ __forceinline__ void grid_barrier(const KvTable& t, uint32_t* err) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t* ctr = &t.probe[kGridCtr];
+        (void)__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t spins = 0;
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins == (1u << 22)) {
+                if (err) *(volatile uint32_t*)err |= kErrInval;
+                break;
+            }
+        }
+    }
+    __syncthreads();
 }
 
 // ---- 3. the list walks ----------------------------------------------------------------------
@@ -243,14 +291,20 @@ __device__ __forceinline__ void walk_one(const KvTable& t, const uint8_t* __rest
                                          int64_t* __restrict__ ret, uint8_t* __restrict__ conf,
                                          bool& fresh, bool& lng) {
     const bool v = p < m;
-    const uint32_t slot = v ? t.probe[p] : kNoSlot;
-    const uint8_t o = v ? op[p] : (uint8_t)MPX_OP_NONE;
+    const uint32_t pc = v ? p : 0u;  // (every load issued at once, clamped, before any use)
+    const uint32_t slot0 = t.probe[pc];
+    const uint8_t o0 = op[pc];
+    const uint32_t mine = __hip_atomic_load(&t.probe[kLinkOff + pc], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t st = t.probe[kSmMax + pc];
+    const uint32_t slot = v ? slot0 : kNoSlot;
+    const uint8_t o = v ? o0 : (uint8_t)MPX_OP_NONE;
     fresh = false;
     lng = false;
     if (slot != kNoSlot) {
-        const uint32_t mine = t.probe[kLinkOff + p];
-        const uint32_t st = t.probe[kSmMax + p];
-        uint32_t q = t.lhead[slot] & kPosMask;  // (tagged with this call: p is on the list)
+        // (tagged with this call: p is on the list; agent scope: pushes of this kernel)
+        uint32_t q = __hip_atomic_load(&t.lhead[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
+                     kPosMask;
         int32_t prev = -1, last_put = -1;
         bool prev_put = false, later_put = false;
         int n = 0;
@@ -259,7 +313,9 @@ __device__ __forceinline__ void walk_one(const KvTable& t, const uint8_t* __rest
                 lng = true;
                 break;
             }
-            const uint32_t w = q == p ? mine : t.probe[kLinkOff + q];
+            const uint32_t w = q == p ? mine
+                                      : __hip_atomic_load(&t.probe[kLinkOff + q], __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
             const bool put_q = (w & kLinkPut) != 0;
             if (q < p) {
                 if ((int32_t)q > prev) {
@@ -317,6 +373,7 @@ __device__ __forceinline__ void end_of_call(const KvTable& t, uint32_t tag) {
     }
     if (threadIdx.x == 0) {
         (void)atomic_take(&t.probe[kCtlOff]);
+        (void)atomic_take(&t.probe[kGridCtr]);
         t.probe[kCtlOff + 1] = wrap ? 0u : tag;
     }
 }
@@ -325,37 +382,18 @@ __device__ __forceinline__ void end_of_call(const KvTable& t, uint32_t tag) {
 // workgroups carry the LONG phase's LDS, so one runs per CU), then the LONG phase in the grid's
 // last workgroup: its LONG marks and counts reach the device's coherence point (agent-scope atomic
 // stores, awaited atomic adds) before its ticket, and the last workgroup reads them the same way.
-__global__ __launch_bounds__(kSmT) void k_small_walk(KvTable t, const uint8_t* __restrict__ op,
-                                                     const int64_t* __restrict__ val, uint32_t m,
-                                                     int64_t* __restrict__ ret,
-                                                     uint8_t* __restrict__ conf, uint32_t* done,
-                                                     uint32_t seq) {
-    __shared__ SmallLds S;
-    {
-        bool fresh, lng;
-        walk_one(t, op, val, m, blockIdx.x * kSmT + threadIdx.x, ret, conf, fresh, lng);
-        const uint64_t bf = __ballot(fresh), bl = __ballot(lng);
-        if (lane_id() == 0) {
-            if (bf) atomicAdd(t.n_present, (unsigned long long)popc(bf));
-            if (bl) atomic_add_done(&t.probe[kCtlOff], (uint32_t)popc(bl));
-        }
-    }
-    if (done) __threadfence_system();  // this workgroup's host-mapped results, before its ticket
-    if (!last_workgroup(&t.probe[kCtlOff + 2])) return;
+// The LONG lists (commands marked LONG by the walks; own != nullptr: only the positions whose
+// bit is set, the calling workgroup's partition), resolved by the calling workgroup in LDS. All
+// threads call it.
+__device__ void long_lists(SmallLds& S, const KvTable& t, const uint8_t* __restrict__ op,
+                           const int64_t* __restrict__ val, uint32_t m, int64_t* __restrict__ ret,
+                           uint8_t* __restrict__ conf, const uint32_t* own) {
 #if MPX_SMALL_STAMP
     unsigned long long _sm_prev = __builtin_amdgcn_s_memrealtime();
     const unsigned long long _sm_rt0 = _sm_prev, _sm_clk0 = __builtin_amdgcn_s_memtime();
 #endif
     const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
     const uint64_t below = lanes_below(l);
-    const uint32_t n_long = __hip_atomic_load(&t.probe[kCtlOff], __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t tag = call_tag(t);
-    if (n_long == 0) {  // every list was walked (the common case)
-        end_of_call(t, tag);
-        signal_done(done, seq);
-        return;
-    }
     for (int i = tid; i < kSmHash; i += kSmT) S.tab[i] = 0;
     if (tid == 0) S.n_new = 0;
 
@@ -373,7 +411,9 @@ __global__ __launch_bounds__(kSmT) void k_small_walk(KvTable t, const uint8_t* _
             const uint32_t s = v ? __hip_atomic_load(&t.probe[p], __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT)
                                  : kNoSlot;
-            slot[k] = s != kNoSlot && (s & kLongBit) ? s & ~kLongBit : kNoSlot;
+            slot[k] = s != kNoSlot && (s & kLongBit) && (!own || ((own[p >> 5] >> (p & 31)) & 1u))
+                          ? s & ~kLongBit
+                          : kNoSlot;
             st[k] = v ? t.probe[kSmMax + p] : 0u;
         }
         SM_STAMP(0);
@@ -610,15 +650,330 @@ __global__ __launch_bounds__(kSmT) void k_small_walk(KvTable t, const uint8_t* _
     if (n_new) atomicAdd(&S.n_new, n_new);
     __syncthreads();
     if (tid == 0 && S.n_new) atomicAdd(t.n_present, (unsigned long long)S.n_new);
-    end_of_call(t, tag);
-    signal_done(done, seq);
     SM_STAMP(6);
 #if MPX_SMALL_STAMP
-    if (threadIdx.x == 0) {  // shader clock ticks and 100 MHz ticks of the whole kernel
+    if (threadIdx.x == 0) {  // shader clock ticks and 100 MHz ticks of the LONG phase
         atomicAdd(&mpx_small_stamp[8], __builtin_amdgcn_s_memtime() - _sm_clk0);
         atomicAdd(&mpx_small_stamp[9], __builtin_amdgcn_s_memrealtime() - _sm_rt0);
     }
 #endif
+}
+
+__global__ __launch_bounds__(kSmT) void k_small_walk(KvTable t, const uint8_t* __restrict__ op,
+                                                     const int64_t* __restrict__ val, uint32_t m,
+                                                     int64_t* __restrict__ ret,
+                                                     uint8_t* __restrict__ conf, uint32_t* done,
+                                                     uint32_t seq, const int64_t* __restrict__ key,
+                                                     uint32_t* err) {
+    __shared__ SmallLds S;
+    if (MPX_SMALL_FOLD) {  // the re-probes, then every push of the call is in
+        reprobe_one(t, key, m, blockIdx.x * kSmT + threadIdx.x);
+        grid_barrier(t, err);
+    }
+    {
+        bool fresh, lng;
+        walk_one(t, op, val, m, blockIdx.x * kSmT + threadIdx.x, ret, conf, fresh, lng);
+        const uint64_t bf = __ballot(fresh), bl = __ballot(lng);
+        if (lane_id() == 0) {
+            if (bf) atomicAdd(t.n_present, (unsigned long long)popc(bf));
+            if (bl) atomic_add_done(&t.probe[kCtlOff], (uint32_t)popc(bl));
+        }
+    }
+    if (done) __threadfence_system();  // this workgroup's host-mapped results, before its ticket
+    if (!last_workgroup(&t.probe[kCtlOff + 2])) return;
+    const uint32_t n_long = __hip_atomic_load(&t.probe[kCtlOff], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t tag = call_tag(t);
+    if (n_long) long_lists(S, t, op, val, m, ret, conf, nullptr);  // (else every list was walked)
+    end_of_call(t, tag);
+    signal_done(done, seq);
+}
+
+// ---- the one-launch form (device-resident commands: mpx_apply_dev) -----------------------------
+// Every workgroup reads every key and keeps the commands whose key hashes into its partition (the
+// high 32 bits of hash64 scaled to the grid). All commands on a key are then in one workgroup,
+// so steps 1-3 (probe, re-probe, walk) meet at workgroup barriers instead of kernel boundaries
+// and the LONG lists of a partition are resolved by its own workgroup: one launch per call. (On
+// MI355X an empty launch alone spans ~6 us between two events and each further one ~1.6 us,
+// tools/launch_floor.hip; the three-launch form above keeps the host forms, whose commands sit in
+// pinned host memory every workgroup would read over the link.) The grid's last workgroup
+// (ticket) closes the call. Table slots are shared between partitions only as probe positions in
+// a bucket: claims are device-scope CAS as in step 1, a key is probed and listed by one
+// workgroup only.
+#ifndef MPX_SMALL_PART
+#define MPX_SMALL_PART 1
+#endif
+#ifndef MPX_SMALL_PART_CMDS
+#define MPX_SMALL_PART_CMDS 256  // commands per partition (the grid: m / this, 1 .. kPartMax)
+#endif
+constexpr uint32_t kPartMax = 256;  // one workgroup per CU (the LONG phase's LDS); a power of 2
+#ifndef MPX_SMALL_FAST
+#define MPX_SMALL_FAST 1  // 0 (A/B builds): every partition takes steps 1-4
+#endif
+
+// every store of the workgroup performed (list pushes, links, slots, state words), then a barrier
+__device__ __forceinline__ void wg_barrier() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+// Partition hash (phase 0 of the one-launch form): the key's two halves folded, a Fibonacci
+// multiply, the top lgnp bits. Every workgroup hashes every key, so this stays one 32-bit
+// multiply (hash64's two 64-bit ones cost ~4 us of VALU per workgroup at 16384 commands).
+__device__ __forceinline__ uint32_t part_of(int64_t k, uint32_t lgnp) {
+    const uint32_t x = ((uint32_t)k ^ (uint32_t)((uint64_t)k >> 32)) * 0x9E3779B1u;
+    return lgnp ? x >> (32 - lgnp) : 0u;
+}
+
+// ---- the one-launch form's LDS resolve: a partition of at most kSmT commands, none of its keys
+// on more than kWalkMax of them (the common case; anything else takes steps 1-4 above) ----------
+// Command j of the partition is thread j. Its key goes into an LDS table of key hashes (hash64
+// is a bijection, so equal hashes are equal keys; the sentinel key has an entry of its own) and
+// gets a dense key id; the first thread to enter a key probes the engine's table for it once -
+// its slot, state word and value at call start in one round trip from the home slot, a claim
+// (64-bit CAS) when any command of the partition PUTs it - and every command then walks its
+// key's LDS list (at most kWalkMax entries) for the nearest earlier command (conf), the nearest
+// earlier PUT (a GET's result) and a later PUT (the last PUT commits). No list heads, links or
+// re-probes in device memory: about four dependent round trips per call instead of ~11.
+constexpr int kFTab = 2048;
+constexpr uint32_t kFSent = kFTab - 1;              // the sentinel key's entry
+constexpr uint64_t kHSent = 0x25c26ea579cea98aull;  // hash64(kSentinel): marks a free entry
+struct PartFastLds {
+    uint64_t th[kFTab];      // key hashes                                        16 KB
+    int64_t v0[kSmT];        // per key id: the value at call start                8 KB
+    int64_t cval[kSmT];      // per command: its value                             8 KB
+    uint32_t slot[kSmT];     // per key id: its table slot (kNoSlot: absent)       4 KB
+    uint32_t st[kSmT];       // per key id: its state word at call start           4 KB
+    uint32_t head[kSmT];     // per key id: its list of commands (command + 1)     4 KB
+    uint32_t cnt[kSmT];      // per key id: commands | PUTs << 16                  4 KB
+    uint16_t id_of[kFTab];   // table entry -> key id                              4 KB
+    uint16_t next[kSmT];     // per command: the next command on its key's list    2 KB
+    uint8_t op[kSmT];        // per command: its op                                1 KB
+    uint32_t nkeys, heavy;
+};
+static_assert(sizeof(PartFastLds) <= sizeof(uint32_t) * kSmMax, "overlays SmallLds::buf[0]");
+
+// All threads call it; false (before any store to the table) when some key of the partition
+// has more than kWalkMax commands. fresh: slots this thread made present.
+__device__ bool part_fast(PartFastLds& F, const KvTable& t, const uint8_t* __restrict__ op,
+                          const int64_t* __restrict__ key, const int64_t* __restrict__ val,
+                          const uint32_t* lst, uint32_t no, int64_t* __restrict__ ret,
+                          uint8_t* __restrict__ conf, uint32_t* err, uint32_t& fresh) {
+    const uint32_t j = threadIdx.x;
+    for (uint32_t i = j; i < (uint32_t)kFTab; i += kSmT) F.th[i] = kHSent;
+    F.cnt[j] = 0u;
+    F.head[j] = 0u;
+    if (j == 0) {
+        F.nkeys = 0u;
+        F.heavy = 0u;
+    }
+    const bool act = j < no;
+    const uint32_t p = act ? lst[j] : 0u;
+    const uint8_t o = op[p];  // (p = 0 for the idle threads: every load unconditional)
+    const int64_t k = key[p];
+    const int64_t v = val[p];
+    const bool put = act && o == MPX_OP_PUT;
+    __syncthreads();  // table and counters cleared
+    uint32_t e = 0;
+    bool lead = false;
+    uint64_t h = 0;
+    if (act) {
+        F.cval[j] = v;
+        F.op[j] = o;
+        if (k == kSentinel) {
+            e = kFSent;
+            lead = atomicCAS((unsigned long long*)&F.th[kFSent], (unsigned long long)kHSent, 0ull) ==
+                   (unsigned long long)kHSent;
+        } else {
+            h = hash64((uint64_t)k);
+            e = (uint32_t)(h >> 40) & (kFTab - 1);
+            for (;;) {
+                if (e == kFSent) e = 0;
+                const unsigned long long cur =
+                    atomicCAS((unsigned long long*)&F.th[e], (unsigned long long)kHSent,
+                              (unsigned long long)h);
+                if (cur == (unsigned long long)kHSent) {
+                    lead = true;
+                    break;
+                }
+                if (cur == (unsigned long long)h) break;
+                e = (e + 1) & (kFTab - 1);
+            }
+        }
+        if (lead) F.id_of[e] = (uint16_t)atomicAdd(&F.nkeys, 1u);
+    }
+    __syncthreads();  // every key has its id
+    uint32_t id = 0;
+    if (act) {
+        id = F.id_of[e];
+        const uint32_t c = atomicAdd(&F.cnt[id], 1u | (put ? 1u << 16 : 0u));
+        if ((c & 0xFFFFu) == (uint32_t)kWalkMax) F.heavy = 1u;  // the list passes kWalkMax
+        F.next[j] = (uint16_t)atomicExch(&F.head[id], j + 1u);
+    }
+    __syncthreads();  // counts and lists complete
+    if (F.heavy) return false;
+    if (lead) {  // the key's slot, state word and value at call start
+        const bool anyput = (F.cnt[id] >> 16) != 0u;
+        uint32_t slot = kNoSlot, st = 0u;
+        int64_t v0 = 0;
+        if (k == kSentinel) {
+            slot = (uint32_t)t.cap;  // the side slot
+            st = t.state[slot];
+            v0 = t.vals[slot];
+        } else {
+            const uint32_t base = bucket_of(h, t.lgnb) << kLgSB;
+            uint32_t sp = home_of(h);
+            for (int step = 0; step < kSB; ++step, sp = (sp + 1) & (kSB - 1)) {
+                unsigned long long* a = reinterpret_cast<unsigned long long*>(t.keys + base + sp);
+                unsigned long long cur =
+                    __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // (the slot's state and value in the same round trip: only this workgroup writes
+                // them during the call, a claimed free slot's included)
+                const uint32_t s1 = t.state[base + sp];
+                const int64_t v1 = t.vals[base + sp];
+                if (cur == (unsigned long long)kSentinel) {
+                    if (!anyput) break;  // absent, and no PUT of the call
+                    cur = atomicCAS(a, (unsigned long long)kSentinel, (unsigned long long)k);
+                    if (cur == (unsigned long long)kSentinel) {
+                        slot = base + sp;  // claimed
+                        st = s1;
+                        break;
+                    }
+                }
+                if ((int64_t)cur == k) {
+                    slot = base + sp;
+                    st = s1;
+                    v0 = v1;
+                    break;
+                }
+            }
+            if (slot == kNoSlot && anyput && err) *(volatile uint32_t*)err |= kErrKvFull;
+        }
+        F.slot[id] = slot;
+        F.st[id] = st;
+        F.v0[id] = v0;
+    }
+    __syncthreads();  // every key's slot
+    fresh = 0u;
+    if (act) {
+        const uint32_t slot = F.slot[id], st = F.st[id];
+        int32_t prev = -1, last_put = -1, lp_j = -1;
+        bool prev_put = false, later_put = false;
+        for (uint32_t q1 = F.head[id]; q1; q1 = F.next[q1 - 1]) {
+            const uint32_t q = q1 - 1u;
+            if (q == j) continue;
+            const int32_t pq = (int32_t)lst[q];
+            const bool put_q = F.op[q] == MPX_OP_PUT;
+            if (pq < (int32_t)p) {
+                if (pq > prev) {
+                    prev = pq;
+                    prev_put = put_q;
+                }
+                if (put_q && pq > last_put) {
+                    last_put = pq;
+                    lp_j = (int32_t)q;
+                }
+            } else {
+                later_put |= put_q;
+            }
+        }
+        int64_t r = 0;
+        if (put) r = v;
+        else if (o == MPX_OP_GET)
+            r = lp_j >= 0 ? F.cval[lp_j] : (slot != kNoSlot && (st & kPresent)) ? F.v0[id] : 0;
+        ret[p] = r;
+        if (conf) conf[p] = (prev >= 0 && (put || prev_put)) ? 1 : 0;
+        if (put && !later_put && slot != kNoSlot) {  // the key's value after the call
+            t.vals[slot] = v;
+            if (!(st & kPresent)) {
+                t.state[slot] = st | kPresent;
+                fresh = 1u;
+            }
+        }
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(kSmT) void k_small_part(KvTable t, const uint8_t* __restrict__ op,
+                                                     const int64_t* __restrict__ key,
+                                                     const int64_t* __restrict__ val, uint32_t m,
+                                                     int64_t* __restrict__ ret,
+                                                     uint8_t* __restrict__ conf, uint32_t* err) {
+    __shared__ SmallLds S;
+    __shared__ uint32_t own[kSmMax / 32];  // bit p: command p is in this partition
+    __shared__ uint32_t n_own, n_long, n_fresh;
+    const int tid = threadIdx.x, l = lane_id();
+    const uint64_t below = lanes_below(l);
+    const uint32_t me = blockIdx.x, lgnp = 31u - (uint32_t)__builtin_clz(gridDim.x);
+    const uint32_t tag = call_tag(t);
+    if (tid == 0) {
+        n_own = 0;
+        n_long = 0;
+        n_fresh = 0;
+    }
+    // ---- 0. the partition's positions: every key loaded at once (rounds of kSmT positions) ----
+    int64_t kk[kSmPer];
+#pragma unroll
+    for (int i = 0; i < kSmPer; ++i) {
+        const uint32_t p = (uint32_t)(i * kSmT + tid);
+        if ((uint32_t)(i * kSmT) < m) kk[i] = key[p < m ? p : m - 1];
+    }
+    __syncthreads();  // counters zeroed
+    uint32_t* lst = S.buf[1];  // this partition's positions, in no particular order
+#pragma unroll
+    for (int i = 0; i < kSmPer; ++i) {
+        if ((uint32_t)(i * kSmT) >= m) break;
+        const uint32_t p = (uint32_t)(i * kSmT + tid);
+        const bool mine = p < m && part_of(kk[i], lgnp) == me;
+        const uint64_t b = __ballot(mine);
+        if ((l & 31) == 0 && p < m) own[p >> 5] = (uint32_t)(b >> (l & 32));
+        if (b) {
+            uint32_t base = 0;
+            if (l == 0) base = atomicAdd(&n_own, (uint32_t)popc(b));
+            base = (uint32_t)__shfl((int)base, 0);
+            if (mine) lst[base + (uint32_t)popc(b & below)] = p;
+        }
+    }
+    __syncthreads();
+    const uint32_t no = n_own;
+    if (MPX_SMALL_FAST && no <= (uint32_t)kSmT) {
+        uint32_t fresh = 0;
+        if (part_fast(*reinterpret_cast<PartFastLds*>(S.buf[0]), t, op, key, val, lst, no, ret,
+                      conf, err, fresh)) {
+            const uint64_t bf = __ballot(fresh != 0u);
+            if (l == 0 && bf) atomicAdd(&n_fresh, (uint32_t)popc(bf));
+            __syncthreads();
+            if (tid == 0 && n_fresh) atomicAdd(t.n_present, (unsigned long long)n_fresh);
+            if (last_workgroup(&t.probe[kCtlOff + 2])) end_of_call(t, tag);
+            return;
+        }
+    }
+    // ---- 1. probes -----------------------------------------------------------------------------
+    for (uint32_t j = tid; j < no; j += kSmT) {
+        const uint32_t p = lst[j];
+        probe_cmd(t, tag, op[p], key[p], val[p], p, ret, err);
+    }
+    wg_barrier();
+    // ---- 2. the lookups that met a free slot -----------------------------------------------------
+    for (uint32_t j = tid; j < no; j += kSmT) reprobe_one(t, key, m, lst[j]);
+    wg_barrier();
+    // ---- 3. the walks --------------------------------------------------------------------------
+    {
+        uint32_t nf = 0, nl = 0;
+        for (uint32_t j = tid; j < no; j += kSmT) {
+            bool fresh, lng;
+            walk_one(t, op, val, m, lst[j], ret, conf, fresh, lng);
+            nf += fresh ? 1u : 0u;
+            nl += lng ? 1u : 0u;
+        }
+        if (nf) atomicAdd(&n_fresh, nf);
+        if (nl) atomicAdd(&n_long, nl);
+    }
+    wg_barrier();
+    if (tid == 0 && n_fresh) atomicAdd(t.n_present, (unsigned long long)n_fresh);
+    // ---- 4. this partition's LONG lists ----------------------------------------------------------
+    if (n_long) long_lists(S, t, op, val, m, ret, conf, own);
+    if (last_workgroup(&t.probe[kCtlOff + 2])) end_of_call(t, tag);
 }
 
 #if MPX_SMALL_STAMP
@@ -636,18 +991,25 @@ extern "C" int mpx_debug_small_stamps(unsigned long long* out16, int reset) {
 
 hipError_t launch_apply_small(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
                               uint64_t m, int64_t* ret, uint8_t* conf, uint32_t* err,
-                              hipStream_t stream, uint32_t* done, uint32_t seq) {
+                              hipStream_t stream, uint32_t* done, uint32_t seq, bool host_io) {
     if (!m) return hipSuccess;
     if (m > (uint64_t)kSmMax || t.cap >= 0x7FFFFFFEull) return hipErrorInvalidValue;
+    if (MPX_SMALL_PART && !host_io && !done) {
+        // a power of two of partitions, about MPX_SMALL_PART_CMDS commands each
+        unsigned np = 1;
+        while (np < kPartMax && (uint64_t)np * MPX_SMALL_PART_CMDS < m) np <<= 1;
+        k_small_part<<<np, kSmT, 0, stream>>>(t, op, key, val, (uint32_t)m, ret, conf, err);
+        return hipGetLastError();
+    }
     const unsigned g = (unsigned)((m + kProbeBlock - 1) / kProbeBlock);
     const int64_t* d_key = reinterpret_cast<const int64_t*>(t.probe + kSmallKeyOff);
     const int64_t* d_val = reinterpret_cast<const int64_t*>(t.probe + kSmallValOff);
     const uint8_t* d_op = reinterpret_cast<const uint8_t*>(t.probe + kSmallOpOff);
     k_small_probe<<<g, kProbeBlock, 0, stream>>>(t, op, key, val, (uint32_t)m, ret, err,
                                                  done != nullptr);
-    k_small_reprobe<<<g, kProbeBlock, 0, stream>>>(t, d_key, (uint32_t)m);
+    if (!MPX_SMALL_FOLD) k_small_reprobe<<<g, kProbeBlock, 0, stream>>>(t, d_key, (uint32_t)m);
     k_small_walk<<<(unsigned)((m + kSmT - 1) / kSmT), kSmT, 0, stream>>>(
-        t, d_op, d_val, (uint32_t)m, ret, conf, done, seq);
+        t, d_op, d_val, (uint32_t)m, ret, conf, done, seq, d_key, err);
     return hipGetLastError();
 }
 

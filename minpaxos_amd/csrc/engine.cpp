@@ -268,7 +268,8 @@ int run_pinned(mpx_engine* e, const PinIo& p, size_t m, bool want_conf) {
 #endif
     HIPCHK(e, mpx::launch_apply_small(e->kv, d.op, d.key, d.val, m, d.ret,
                                       want_conf ? d.conf : nullptr, (uint32_t*)d.err, e->stream,
-                                      MPX_SMALL_POLL ? (uint32_t*)d.done : nullptr, seq));
+                                      MPX_SMALL_POLL ? (uint32_t*)d.done : nullptr, seq,
+                                      /*host_io=*/true));
     if (!MPX_SMALL_POLL) {
         HIPCHK(e, hipStreamSynchronize(e->stream));
         return check_errword(e, *v.err);

@@ -137,7 +137,8 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
 // host form can poll it instead of waiting on the stream
 hipError_t launch_apply_small(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
                               uint64_t m, int64_t* ret, uint8_t* conf, uint32_t* err,
-                              hipStream_t stream, uint32_t* done = nullptr, uint32_t seq = 0);
+                              hipStream_t stream, uint32_t* done = nullptr, uint32_t seq = 0,
+                              bool host_io = false);
 hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const int64_t* val,
                         uint64_t m, int64_t* ret, uint8_t* conf, const ApplyOpts& o, ApplyWork& w,
                         uint32_t* err, hipStream_t stream);

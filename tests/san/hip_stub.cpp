@@ -304,7 +304,7 @@ hipError_t launch_apply(KvTable&, const uint8_t*, const int64_t*, const int64_t*
 // the replica-batch form: nothing to compute on the stub, but the call completes (its flag)
 hipError_t launch_apply_small(KvTable&, const uint8_t*, const int64_t*, const int64_t*, uint64_t,
                               int64_t*, uint8_t*, uint32_t*, hipStream_t, uint32_t* done,
-                              uint32_t seq) {
+                              uint32_t seq, bool) {
     if (done) *done = seq;
     return hipSuccess;
 }

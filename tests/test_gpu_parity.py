@@ -273,15 +273,35 @@ def test_apply_chunked(mk_engine, chunk):
         assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
 
 
-@pytest.mark.parametrize("path", [R.APPLY_SMALL, R.APPLY_AUTO, R.APPLY_SORTED])
-def test_apply_small_calls(mk_engine, path):
+def _apply_form(e, form, op, key, val):
+    """one apply call through the host-pointer form (the replica-batch kernels' three-launch
+    form over pinned host memory) or the device-pointer form (their one-launch form)"""
+    if form == "host":
+        return e.apply(op, key, val)
+    from minpaxos_amd.devbuf import Arena
+    m = len(op)
+    e.apply_reserve(m)
+    with Arena(e) as ar:
+        d_op, d_key, d_val = ar.put(op), ar.put(key), ar.put(val)
+        d_ret, d_conf = ar.empty(m, np.int64), ar.empty(m, np.uint8)
+        e.apply_dev(d_op.ptr, d_key.ptr, d_val.ptr, m, d_ret.ptr, d_conf.ptr, e.stream)
+        e.stream_synchronize(e.stream)
+        return ar.get(d_ret), ar.get(d_conf)
+
+
+@pytest.mark.parametrize("path,form", [(R.APPLY_SMALL, "host"), (R.APPLY_SMALL, "dev"),
+                                       (R.APPLY_AUTO, "host"), (R.APPLY_AUTO, "dev"),
+                                       (R.APPLY_SORTED, "host")])
+def test_apply_small_calls(mk_engine, path, form):
     """replica-sized calls (one drained executeCommands batch, MAX_BATCH = 5000 commands,
     bareminpaxos.go:22,1071-1089): sizes around the wave (64), the workgroup (1024) and the
     small kernels' limit (16384: up to three drained MAX_BATCH batches), mixed ops, the
     special keys, a hot key, GETs of absent keys
     before their first PUT, and one table carried through all calls; every call's results,
     the table and its size bit-exact. AUTO and SMALL run the one-launch kernel (apply_small.hip)
-    here, SORTED the multi-launch pipeline"""
+    here, SORTED the multi-launch pipeline; "dev" runs every call through mpx_apply_dev (the
+    replica-batch kernels' one-launch form: hash partitions, one workgroup each, up to 64 of
+    them at 16384 commands)"""
     rng = np.random.default_rng(91 + path)
     e, o = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 16, apply_path=path), Oracle(5, R.MODE_MIN)
     sizes = [1, 2, 63, 64, 65, 1000, 1023, 1024, 1025, 4095, 5000, 8191, 8192, 8193, 9000,
@@ -291,7 +311,7 @@ def test_apply_small_calls(mk_engine, path):
         key = np.where(key > 0, key + (i % 3) * 1_000_003, key)  # fresh keys every third call
         if i % 4 == 1:
             key[rng.random(m) < 0.5] = 424242  # a hot key
-        gr, gc = e.apply(op, key, val)
+        gr, gc = _apply_form(e, form, op, key, val)
         wr, wc = o.apply(op, key, val)
         assert np.array_equal(gr, wr), (m, np.nonzero(gr != wr)[0][:5])
         assert np.array_equal(gc, wc), (m, np.nonzero(gc != wc)[0][:5])
@@ -303,7 +323,7 @@ def test_apply_small_calls(mk_engine, path):
     # ones), and one call where exactly 1024 / 1025 commands share keys (the rank / radix switch)
     for m, kr, seed in ((8192, 1 << 40, 95), (5000, 1 << 20, 96), (16384, 1 << 20, 97)):
         op, key, val = synth.commands(m, kr, 0.5, "uniform", seed=seed)
-        gr, gc = e.apply(op, key, val)
+        gr, gc = _apply_form(e, form, op, key, val)
         wr, wc = o.apply(op, key, val)
         assert np.array_equal(gr, wr) and np.array_equal(gc, wc), m
     for n_sh in (1024, 1025):
@@ -313,7 +333,7 @@ def test_apply_small_calls(mk_engine, path):
         key[:n_sh // 2] = key[n_sh // 2:n_sh // 2 * 2]  # n_sh // 2 pairs share a key ...
         if n_sh % 2:
             key[n_sh - 1] = key[0]  # ... and one triple
-        gr, gc = e.apply(op, key, val)
+        gr, gc = _apply_form(e, form, op, key, val)
         wr, wc = o.apply(op, key, val)
         assert np.array_equal(gr, wr) and np.array_equal(gc, wc), n_sh
     gk, gv = e.kv_export()
@@ -418,8 +438,9 @@ def _bucket_keys(lgnb, bucket, n, start=1):
     return sel[:n].astype(np.int64)
 
 
-@pytest.mark.parametrize("path", [R.APPLY_SMALL, R.APPLY_PARTITIONED, R.APPLY_SORTED])
-def test_apply_full_bucket_lookups(mk_engine, path):
+@pytest.mark.parametrize("path,form", [(R.APPLY_SMALL, "host"), (R.APPLY_SMALL, "dev"),
+                                       (R.APPLY_PARTITIONED, "host"), (R.APPLY_SORTED, "host")])
+def test_apply_full_bucket_lookups(mk_engine, path, form):
     """a bucket filled exactly (256 PUT keys in one of the 4 buckets of a 1024-slot table):
     GETs and other ops of keys absent from that full bucket return NIL and leave the table
     unchanged, on every pipeline (mpx.h: only keys PUT at some point occupy the table); a PUT of
@@ -443,7 +464,7 @@ def test_apply_full_bucket_lookups(mk_engine, path):
     perm = rng.permutation(len(key))
     key, op = key[perm], op[perm]
     val = np.arange(len(key), dtype=np.int64) + 1000
-    gr, gc = e.apply(op, key, val)
+    gr, gc = _apply_form(e, form, op, key, val)
     wr, wc = o.apply(op, key, val)
     assert np.array_equal(gr, wr), np.nonzero(gr != wr)[0][:5]
     assert np.array_equal(gc, wc)
@@ -539,21 +560,23 @@ def test_apply_epoch_wrap(mk_engine, path):
         e.debug_kv_set_epoch(1 << 30)  # outside [1, 2^30)
 
 
-def test_apply_small_lists_and_tag_wrap(mk_engine):
+@pytest.mark.parametrize("form", ["host", "dev"])
+def test_apply_small_lists_and_tag_wrap(mk_engine, form):
     """replica-sized calls resolve each key's commands by walking the key's list of the call
     (apply_small.hip steps 1-3) and leave lists longer than 16 to the one-workgroup sort: calls
     whose key ranges put 1 .. ~100 commands on a key mix both in one call. The list heads are
     tagged with the call (18 bits); at the wrap the heads are cleared: calls on key set A at tags
     1..3, the tag moved to three calls before the wrap (mpx_debug_kv_set_small_tag), two calls on
     a disjoint set B, then calls on A at the wrapped tags 1..3 - without the clear A's heads would
-    still carry tags 1..3 and link stale positions. Every call and the table bit-exact."""
+    still carry tags 1..3 and link stale positions. Every call and the table bit-exact; "dev":
+    the one-launch form, whose partitions resolve their own LONG lists."""
     e = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 16, apply_path=R.APPLY_SMALL)
     o = Oracle(5, R.MODE_MIN)
 
     def call(m, kr, lo, seed):
         op, key, val = synth.commands(m, kr, 0.5, "uniform", seed=seed, other_ops=0.1)
         key = key + lo
-        gr, gc = e.apply(op, key, val)
+        gr, gc = _apply_form(e, form, op, key, val)
         wr, wc = o.apply(op, key, val)
         assert np.array_equal(gr, wr), (m, kr, np.nonzero(gr != wr)[0][:5])
         assert np.array_equal(gc, wc), (m, kr, np.nonzero(gc != wc)[0][:5])
@@ -573,6 +596,44 @@ def test_apply_small_lists_and_tag_wrap(mk_engine):
     assert e.kv_size() == len(wk)
     with pytest.raises(MpxError):
         e.debug_kv_set_small_tag(1 << 18)
+
+
+def _part_keys(n, lgnp, part, start):
+    """n distinct keys whose partition hash (apply_small.hip part_of) is `part` of 2^lgnp"""
+    x = np.arange(start, start + (n << lgnp) * 4, dtype=np.uint64)
+    f = ((x & np.uint64(0xFFFFFFFF)) ^ (x >> np.uint64(32))) * np.uint64(0x9E3779B1)
+    sel = x[((f & np.uint64(0xFFFFFFFF)) >> np.uint64(32 - lgnp)) == np.uint64(part)]
+    assert len(sel) >= n
+    return sel[:n].astype(np.int64)
+
+
+def test_apply_small_partition_skew(mk_engine):
+    """the one-launch form (mpx_apply_dev, at most 16384 commands) splits a call into 2^k hash
+    partitions, one workgroup each; a partition of at most 1024 commands whose keys each carry at
+    most 16 of them resolves in LDS, any other takes the list phases. Calls that put 2000-3000
+    commands on distinct keys into one partition (the list phases without LONG lists), a hot key
+    in the same partition (LONG lists), GETs of absent keys before and after their first PUT, the
+    sentinel key: every call and the table bit-exact"""
+    rng = np.random.default_rng(99)
+    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 16, apply_path=R.APPLY_SMALL), \
+        Oracle(5, R.MODE_MIN)
+    for i, (m, lgnp) in enumerate(((16384, 6), (5000, 5), (8000, 5))):
+        op, key, val = gen_cases.commands_mixed(rng, m, 400 + 100 * i)
+        skew = _part_keys(2000 + 500 * i, lgnp, 3 + i, start=10_000_000 * (i + 1))
+        at = rng.choice(m, size=len(skew), replace=False)
+        key[at] = skew
+        if i == 1:
+            key[at[:200]] = skew[0]  # a hot key inside the skewed partition
+        if i == 2:
+            key[rng.random(m) < 0.01] = np.iinfo(np.int64).min  # the sentinel key
+        gr, gc = _apply_form(e, "dev", op, key, val)
+        wr, wc = o.apply(op, key, val)
+        assert np.array_equal(gr, wr), (m, np.nonzero(gr != wr)[0][:5])
+        assert np.array_equal(gc, wc), (m, np.nonzero(gc != wc)[0][:5])
+        gk, gv = e.kv_export()
+        wk, wv = o.kv_export()
+        assert np.array_equal(gk, wk) and np.array_equal(gv, wv), m
+        assert e.kv_size() == len(wk)
 
 
 @pytest.mark.parametrize("cap_lg", [22, 23, 25, 26])
