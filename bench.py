@@ -66,7 +66,7 @@ from minpaxos_amd import _lib  # noqa: E402
 from minpaxos_amd import records as R  # noqa: E402
 from minpaxos_amd import shard, synth  # noqa: E402
 from minpaxos_amd.devbuf import D2D, Arena, DevArray  # noqa: E402
-from minpaxos_amd.engine import Engine, MpxError  # noqa: E402
+from minpaxos_amd.engine import Engine, MpxError, step_one_launch_fits  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -113,6 +113,11 @@ def parse():
     ap.add_argument("--kv-capacity", type=int, default=0,
                     help="apply: engine key capacity (0 = --apply-keys; the table gets >= 2x slots, load <= 1/2)")
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
+    ap.add_argument("--step-launches", type=int, default=2, choices=[1, 2],
+                    help="step: 1 = MPX_FLAG_STEP_ONE_LAUNCH (the fast kernel alone, totals "
+                         "folded by its last workgroup) where the shape fits a fast variant, "
+                         "2 = fast + work-list kernel (the default: 0.097 vs 0.103 ms per "
+                         "step at --emulate-world 8, DESIGN §9)")
     ap.add_argument("--separate-totals", action="store_true",
                     help="step: the totals by their own launch after the group step "
                          "(mpx_step_totals_dev) instead of the step's work-list kernel "
@@ -376,7 +381,9 @@ def step_bench(a, rk):
         G_total = a.groups_total
     g0, g1 = shard.block_range(G_total, P, rank)
     G = g1 - g0
-    eng = Engine(rk.local, n_replicas=N, mode=mode, kv_per_group=K, max_groups=max(G, 1))
+    one_launch = a.step_launches == 1 and step_one_launch_fits(N, ipg, K) and not a.separate_totals
+    eng = Engine(rk.local, n_replicas=N, mode=mode, kv_per_group=K, max_groups=max(G, 1),
+                 step_one_launch=one_launch)
     ar = Arena(eng)
 
     # ---- this rank's block of groups, generated from their global ids --------------------------
@@ -635,9 +642,13 @@ def step_bench(a, rk):
                 "timing": ("HIP events recorded by the engine right before and after each "
                            "k_group_fast launch (mpx_group_step_events) on the compute stream - "
                            "in the replayed hipGraph (external event nodes) when the line is the "
-                           "graph pass, as ms_per_step is, else in the enqueued pass; the "
-                           "work-list kernel and the collective are outside; achieved from their "
-                           "mean, the median beside it (SURVEY 8(d))"),
+                           "graph pass, as ms_per_step is, else in the enqueued pass; "
+                           + ("one launch per step: the kernel's last workgroup folds the step "
+                              "totals inside the bracket" if one_launch else
+                              "the work-list kernel (second launch) is outside")
+                           + "; the collective is outside; achieved from their mean, the median "
+                           "beside it (SURVEY 8(d))"),
+                "launches_per_step": 1 if one_launch else 2,
             },
             "decided_instances_per_step": n_decided,
             "executed_instances_per_step": n_exec_inst,

@@ -73,8 +73,9 @@
 extern "C" {
 #endif
 
-#define MPX_ABI_VERSION 7  /* 4: + mpx_group_step_totals_dev; 5: + mpx_graph_*, mpx_apply_buffers / _staged;
-                              6: + mpx_replay_durable_reserve; 7: + mpx_group_step_events */
+#define MPX_ABI_VERSION 8  /* 4: + mpx_group_step_totals_dev; 5: + mpx_graph_*, mpx_apply_buffers / _staged;
+                              6: + mpx_replay_durable_reserve; 7: + mpx_group_step_events;
+                              8: + MPX_FLAG_STEP_ONE_LAUNCH */
 
 /* ---- error codes ---------------------------------------------------------------------- */
 #define MPX_OK 0
@@ -209,7 +210,7 @@ typedef struct mpx_config {
                                0 = 512. Also picks the fused step's fast-path variant (256:
                                the config-5 kernel); a group whose call touches more than
                                2048 distinct keys fails with MPX_E_KV_FULL                  */
-    uint32_t flags;         /* reserved, 0                                                  */
+    uint32_t flags;         /* MPX_FLAG_* (0: none)                                         */
     uint64_t max_groups;    /* groups per mpx_group_step_dev call (work list); 0 = 1<<20    */
     /* mpx_apply tuning, fixed for the handle's life (0 = default everywhere). Every setting
      * gives identical results; they move time and scratch only.                            */
@@ -231,6 +232,21 @@ typedef struct mpx_config {
                                  its commands in place; 0 = 5; MPX_APPLY_NO_HOT = none      */
     uint32_t reserved;        /* 0                                                          */
 } mpx_config; /* 56 B */
+
+/* mpx_config.flags */
+#define MPX_FLAG_STEP_ONE_LAUNCH 1u /* every mpx_group_step[_totals]_dev is ONE kernel: the
+                               per-group fast kernel, which also reduces the step totals (its
+                               last workgroup), with no work-list kernel behind it. The shape
+                               must fit a fast variant (R = max(N-1,1) x ipg replies: ipg <= 256
+                               with R <= 1024 and kv_per_group <= 1024, or R <= 2048 and
+                               kv_per_group <= 256; ipg <= 512 with R <= 2048 and kv_per_group
+                               <= 512; else the call returns MPX_E_INVAL) and so must every
+                               group: at most R replies, 1024 commands (2048 at ipg > 256), distinct keys
+                               within the variant's LDS table - a group past them fails the step
+                               (MPX_E_INVAL at the next synchronising call, its outputs not
+                               written). For callers that bound their batches; the default
+                               two-launch step takes any group.                              */
+#define MPX_FLAG_KNOWN 1u
 
 #define MPX_APPLY_AUTO 0
 #define MPX_APPLY_SORTED 1

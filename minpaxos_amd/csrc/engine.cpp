@@ -314,7 +314,8 @@ int mpx_open(int device, const mpx_config* cfg, mpx_engine** out) {
     *out = nullptr;
     if (cfg->n_replicas < 1 || cfg->n_replicas > MPX_MAX_REPLICAS) return MPX_E_INVAL;
     if (cfg->mode != MPX_MODE_MIN && cfg->mode != MPX_MODE_CLASSIC) return MPX_E_INVAL;
-    if (cfg->apply_path > MPX_APPLY_SMALL || cfg->flags || cfg->reserved) return MPX_E_INVAL;
+    if (cfg->apply_path > MPX_APPLY_SMALL || (cfg->flags & ~MPX_FLAG_KNOWN) || cfg->reserved)
+        return MPX_E_INVAL;
     int c = 0;
     if (hipGetDeviceCount(&c) != hipSuccess || device < 0 || device >= c) {
         (void)hipGetLastError();
@@ -343,6 +344,8 @@ int mpx_open(int device, const mpx_config* cfg, mpx_engine** out) {
         hipMalloc(&e->d_wcount, mpx::kStepCtlWords * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(e->d_wcount, 0, mpx::kStepCtlWords * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&e->worklist.p, e->worklist.cap) != hipSuccess ||
+        // (one-launch steps keep their packed totals slots there, zero between steps)
+        hipMemset(e->worklist.p, 0, e->worklist.cap) != hipSuccess ||
         hipMemset(e->d_err, 0, sizeof(uint32_t)) != hipSuccess) {
         (void)hipGetLastError();
         mpx_close(e);
@@ -741,6 +744,12 @@ int mpx_conflict_batch_dev(mpx_engine* e, const uint8_t* d_op, const int64_t* d_
 
 // ---- fused group step -------------------------------------------------------------------------
 namespace {
+bool one_launch(const mpx_engine* e) { return (e->cfg.flags & MPX_FLAG_STEP_ONE_LAUNCH) != 0; }
+// one-launch steps: the packed totals slots (one u64 per 64 groups) live in the work list's
+// memory, which such a handle never uses as a list
+unsigned long long* pslots(const mpx_engine* e) {
+    return one_launch(e) ? reinterpret_cast<unsigned long long*>(e->worklist.p) : nullptr;
+}
 // the device-pointer group step; d_totals (optional) gets the step totals from the same kernels
 int group_step_dev(mpx_engine* e, const mpx_group_batch* b, int64_t* d_totals, void* stream) {
     if (!e) return MPX_E_INVAL;
@@ -755,9 +764,11 @@ int group_step_dev(mpx_engine* e, const mpx_group_batch* b, int64_t* d_totals, v
     if (b->ipg > 8192) return fail(e, MPX_E_UNSUPPORTED, "more than 8192 instances per group");
     if ((uint64_t)b->n_groups * sizeof(uint32_t) > e->worklist.cap)
         return fail(e, MPX_E_INVAL, "n_groups exceeds mpx_config.max_groups");
+    if (one_launch(e) && !mpx::step_one_launch_fits(e->cfg.n_replicas, b->ipg, e->cfg.kv_per_group))
+        return fail(e, MPX_E_INVAL, "MPX_FLAG_STEP_ONE_LAUNCH: the batch shape fits no fast variant");
     HIPCHK(e, mpx::launch_group_step(e->cfg.mode, e->cfg.n_replicas, e->cfg.kv_per_group, b,
                                      (uint32_t*)e->worklist.p, e->d_wcount, d_totals, e->d_err,
-                                     pick(e, stream), e->ev_fast0, e->ev_fast1));
+                                     pick(e, stream), e->ev_fast0, e->ev_fast1, pslots(e)));
     return MPX_OK;
 }
 }  // namespace
@@ -870,9 +881,15 @@ int mpx_group_step(mpx_engine* e, const mpx_group_batch* hb) {
     CK(h2d(e, d + o_kk, hb->kv_key_in, G * K * 8));
     CK(h2d(e, d + o_kvv, hb->kv_val_in, G * K * 8));
     if (ipg > 8192) return fail(e, MPX_E_UNSUPPORTED, "more than 8192 instances per group");
-    GROW(e, e->worklist, G * sizeof(uint32_t));
+    if (G * sizeof(uint32_t) > e->worklist.cap) {
+        GROW(e, e->worklist, G * sizeof(uint32_t));
+        HIPCHK(e, hipMemsetAsync(e->worklist.p, 0, e->worklist.cap, e->stream));  // (slots)
+    }
+    if (one_launch(e) && !mpx::step_one_launch_fits(N, (uint32_t)ipg, (uint32_t)K))
+        return fail(e, MPX_E_INVAL, "MPX_FLAG_STEP_ONE_LAUNCH: the batch shape fits no fast variant");
     HIPCHK(e, mpx::launch_group_step(e->cfg.mode, N, (uint32_t)K, &db, (uint32_t*)e->worklist.p,
-                                     e->d_wcount, nullptr, e->d_err, e->stream, nullptr, nullptr));
+                                     e->d_wcount, nullptr, e->d_err, e->stream, nullptr, nullptr,
+                                     pslots(e)));
     CK(d2h(e, hb->st_out, d + o_st, ni * 16));
     CK(d2h(e, hb->committed_out, d + o_co, G * 4));
     CK(d2h(e, hb->executed_out, d + o_eo, G * 4));

@@ -62,7 +62,12 @@ hipError_t launch_conflict_batch(const uint8_t* op, const int64_t* key, const ui
 hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
                              const mpx_group_batch* b, uint32_t* worklist, uint32_t* wcount,
                              int64_t* totals, uint32_t* err, hipStream_t stream,
-                             hipEvent_t ev_fast0, hipEvent_t ev_fast1);
+                             hipEvent_t ev_fast0, hipEvent_t ev_fast1,
+                             unsigned long long* pslots = nullptr);
+// one-launch steps (pslots: the engine's zeroed packed-totals slots, one u64 per 64 groups): the
+// fast kernel alone, which folds the totals in its last workgroup; the shape must fit a fast
+// variant (step_one_launch_fits) and a group that does not fit it fails the step
+bool step_one_launch_fits(int32_t nrep, uint32_t ipg, uint32_t kv_per_group);
 // d_totals[0..2] = decided instances, executed instances, executed commands of the batch
 // step control words (engine-owned, zeroed once): [0] work-list count, [1] its ticket, [4..9]
 // the totals' 64-bit accumulators, [10] their ticket, [16..) the fused totals' partials

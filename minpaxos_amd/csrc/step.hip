@@ -389,11 +389,81 @@ __device__ __forceinline__ int fast_slot(Lds& S, unsigned long long key, uint32_
     return -1;
 }
 
+// One-launch steps (mpx_config.flags MPX_FLAG_STEP_ONE_LAUNCH): no work-list kernel follows.
+// A group the fast kernel cannot take fails the step (kErrInval) instead of going on the list,
+// and with totals every group adds one packed word - arrival | decided << 7 | executed
+// instances << 23 | executed commands << 39 - into slot g % ceil(G / 64) of `pslots` (at most 64
+// groups of at most 512 instances and 2048 commands: no field overflows into the next). The grid's last
+// workgroup (dispatched last: every other one is resident or done) waits for every slot's
+// arrivals, sums and zeroes the slots and writes the totals: one kernel per step. Measured
+// (same box, graph replay, --emulate-world 8): 0.1026-0.1037 ms per step against 0.0967-0.0980
+// for the two-launch step - the fold's serial tail (the grid's last group, a round trip to the
+// slots, the zeroing stores) outlasts the work-list kernel's launch inside a graph (~2 us; the
+// fast kernel without any totals: 0.0945-0.0954; polling sleeps 2/16/64 change nothing), so
+// the flag is an option, not the default.
+constexpr uint32_t kPkGroups = 64;
+__device__ __forceinline__ unsigned long long pk_word(uint32_t d, uint32_t xi, uint32_t xc) {
+    return 1ull | ((unsigned long long)d << 7) | ((unsigned long long)xi << 23) |
+           ((unsigned long long)xc << 39);
+}
+// slot of group g: interleaved (g % nslots), so the groups running at the same time add into
+// different words; slot s then holds (G - 1 - s) / nslots + 1 <= 64 groups
+__device__ __forceinline__ uint32_t pk_slots(uint32_t n_groups) {
+    return (n_groups + kPkGroups - 1) / kPkGroups;
+}
+__device__ void fold_packed(unsigned long long* pslots, uint32_t n_groups, int64_t* totals,
+                            uint32_t* err) {
+    __shared__ unsigned long long fsum[3];
+    if (threadIdx.x < 3) fsum[threadIdx.x] = 0;
+    __syncthreads();
+    unsigned long long d = 0, xi = 0, xc = 0;
+    const uint32_t nslots = pk_slots(n_groups);
+    // slots a thread loads at once (one round trip for them); 2 keeps the fast kernel's VGPRs
+    // (8: 60 -> 90, one workgroup per CU fewer, the step 2-5 % slower)
+    constexpr int kBatch = 2;
+    for (uint32_t s0 = threadIdx.x; s0 < nslots; s0 += blockDim.x * kBatch) {
+        unsigned long long w[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            const uint32_t sl = s0 + k * blockDim.x;
+            w[k] = sl < nslots ? __hip_atomic_load(pslots + sl, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                               : 0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            const uint32_t sl = s0 + k * blockDim.x;
+            if (sl >= nslots) continue;
+            const uint32_t want = (n_groups - 1u - sl) / nslots + 1u;
+            uint32_t spins = 0;
+            while ((w[k] & 127ull) < want) {  // a group still running (the grid's tail)
+                __builtin_amdgcn_s_sleep(2);
+                w[k] = __hip_atomic_load(pslots + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (++spins == (1u << 22)) {  // never on a well-formed launch: fail, do not hang
+                    raise_err(err, kErrInval);
+                    break;
+                }
+            }
+            __hip_atomic_store(pslots + sl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            d += (w[k] >> 7) & 0xFFFFull;
+            xi += (w[k] >> 23) & 0xFFFFull;
+            xc += w[k] >> 39;
+        }
+    }
+    if (d) atomicAdd(&fsum[0], d);
+    if (xi) atomicAdd(&fsum[1], xi);
+    if (xc) atomicAdd(&fsum[2], xc);
+    __syncthreads();
+    if (threadIdx.x < 3) totals[threadIdx.x] = (int64_t)fsum[threadIdx.x];
+}
+
 template <int MODE, class Cfg>
 __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int32_t nrep,
                                                          uint32_t kvpg, uint32_t* worklist,
                                                          uint32_t* wcount,
-                                                         unsigned long long* tacc, uint32_t* err) {
+                                                         unsigned long long* tacc, uint32_t* err,
+                                                         unsigned long long* pslots,
+                                                         int64_t* totals) {
     MPX_FAST_CONSTS
     __shared__ FastLds<Cfg, MODE> S;
     STAMP_DECL
@@ -411,7 +481,16 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
     const uint32_t ncmd = c_hi - c_lo;
     if (r1 < r0 || c_hi < c_lo || nrec > (uint64_t)kFRecs || ncmd > (uint32_t)kFCmds ||
         kcnt > (uint32_t)kFTab || kcnt > kvpg) {
-        if (t == 0) worklist[atomicAdd(wcount, 1u)] = g;
+        if (pslots) {  // one-launch step: no work list behind this kernel
+            if (t == 0) {
+                raise_err(err, kErrInval);
+                if (totals) (void)__hip_atomic_fetch_add(pslots + g % pk_slots(gridDim.x), 1ull, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (totals && g == gridDim.x - 1) fold_packed(pslots, gridDim.x, totals, err);
+        } else if (t == 0) {
+            worklist[atomicAdd(wcount, 1u)] = g;
+        }
         return;
     }
     const int64_t lo = (int64_t)ex_in + 1 < 0 ? 0 : (int64_t)ex_in + 1;  // first instance to run
@@ -745,7 +824,16 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
     __syncthreads();  // B4
     STAMP(3);
     if (S.flags & 1u) {  // table overflow: the general kernel takes the group
-        if (t == 0) worklist[atomicAdd(wcount, 1u)] = g;
+        if (pslots) {  // (one-launch step: the step fails)
+            if (t == 0) {
+                raise_err(err, kErrInval);
+                if (totals) (void)__hip_atomic_fetch_add(pslots + g % pk_slots(gridDim.x), 1ull, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (totals && g == gridDim.x - 1) fold_packed(pslots, gridDim.x, totals, err);
+        } else if (t == 0) {
+            worklist[atomicAdd(wcount, 1u)] = g;
+        }
         return;
     }
     // the group stays here: the instance outputs can go now (st_out may alias st_in, so not
@@ -866,8 +954,14 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
             (void)__hip_atomic_fetch_add(tacc + (g & (kTotSlots - 1)) * 3 + t, (unsigned long long)v,
                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (pslots && totals && t == 0)  // one-launch step: the packed word (arrival included)
+        (void)__hip_atomic_fetch_add(pslots + g % pk_slots(gridDim.x),
+                                     pk_word(S.ndec, stop > lo ? (uint32_t)(stop - lo) : 0u,
+                                             stop > lo ? x1 - x0 : 0u),
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ebits &= 0x7FFFFFFFu;
     if (ebits) raise_err(err, ebits);
+    if (pslots && totals && g == gridDim.x - 1) fold_packed(pslots, gridDim.x, totals, err);
     STAMP(6);
 }
 
@@ -1179,9 +1273,10 @@ void record_timing_event(hipEvent_t ev, hipStream_t stream) {
 
 template <int MODE, class Cfg>
 void launch_fast(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t* worklist,
-                 uint32_t* wcount, unsigned long long* tacc, uint32_t* err, hipStream_t stream) {
+                 uint32_t* wcount, unsigned long long* tacc, uint32_t* err, hipStream_t stream,
+                 unsigned long long* pslots, int64_t* totals) {
     k_group_fast<MODE, Cfg><<<b->n_groups, Cfg::kFT, 0, stream>>>(*b, nrep, kvpg, worklist, wcount,
-                                                                   tacc, err);
+                                                                   tacc, err, pslots, totals);
 }
 // the smallest fast-path variant the batch's shape fits (0 = none: every group is general)
 int fast_variant(int32_t nrep, uint32_t ipg, uint32_t kvpg) {
@@ -1196,43 +1291,56 @@ int fast_variant(int32_t nrep, uint32_t ipg, uint32_t kvpg) {
 template <int MODE>
 void launch_step(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t* worklist,
                  uint32_t* wcount, int64_t* totals, uint32_t* err, hipStream_t stream,
-                 hipEvent_t ev0, hipEvent_t ev1) {
-    // the step totals' partial slots (control words [16..)): the fast kernel adds the groups it
-    // keeps, the general kernel the listed ones and folds them
+                 hipEvent_t ev0, hipEvent_t ev1, unsigned long long* pslots) {
+    // two-launch steps: the step totals' partial slots (control words [16..)), the fast kernel
+    // adds the groups it keeps, the general kernel the listed ones and folds them; one-launch
+    // steps (pslots): the fast kernel's packed slots and its last workgroup's fold
     unsigned long long* const tacc =
-        totals ? reinterpret_cast<unsigned long long*>(wcount + 16) : nullptr;
+        totals && !pslots ? reinterpret_cast<unsigned long long*>(wcount + 16) : nullptr;
+    int64_t* const ptot = pslots ? totals : nullptr;
     if (ev0) record_timing_event(ev0, stream);
     switch (fast_variant(nrep, b->ipg, kvpg)) {
-    case 1: launch_fast<MODE, FastBase>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
-    case 2: launch_fast<MODE, FastRecs>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
-    case 3: launch_fast<MODE, FastKeys>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
-    case 4: launch_fast<MODE, FastWide>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
-    case 5: launch_fast<MODE, FastWide256>(b, nrep, kvpg, worklist, wcount, tacc, err, stream); break;
+#define MPX_FAST_CASE(n, C)                                                                    \
+    case n:                                                                                    \
+        launch_fast<MODE, C>(b, nrep, kvpg, worklist, wcount, tacc, err, stream, pslots, ptot); \
+        break;
+    MPX_FAST_CASE(1, FastBase)
+    MPX_FAST_CASE(2, FastRecs)
+    MPX_FAST_CASE(3, FastKeys)
+    MPX_FAST_CASE(4, FastWide)
+    MPX_FAST_CASE(5, FastWide256)
+#undef MPX_FAST_CASE
     default:
         k_fill_worklist<<<(b->n_groups + 255) / 256, 256, 0, stream>>>(worklist, wcount,
                                                                        b->n_groups);
     }
     if (ev1) record_timing_event(ev1, stream);
+    if (pslots) return;  // (the host checked that a fast variant takes the shape)
     const unsigned gen_grid = b->n_groups < 256 ? b->n_groups : 256;  // one per CU (LDS)
     k_group_general<MODE><<<gen_grid ? gen_grid : 1, kStepBlock, 0, stream>>>(
         *b, nrep, kvpg, worklist, wcount, totals, err);
 }
 }  // namespace
 
+bool step_one_launch_fits(int32_t nrep, uint32_t ipg, uint32_t kv_per_group) {
+    return fast_variant(nrep, ipg, kv_per_group) != 0;
+}
+
 hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
                              const mpx_group_batch* b, uint32_t* worklist, uint32_t* wcount,
                              int64_t* totals, uint32_t* err, hipStream_t stream,
-                             hipEvent_t ev0, hipEvent_t ev1) {
+                             hipEvent_t ev0, hipEvent_t ev1, unsigned long long* pslots) {
     if (!b->n_groups)
         return totals ? hipMemsetAsync(totals, 0, 3 * sizeof(int64_t), stream) : hipSuccess;
     if (kv_per_group > (uint32_t)kDCap) return hipErrorInvalidValue;
     if (b->ipg > (uint32_t)kMaxIpgBits) return hipErrorInvalidValue;
+    if (pslots && !step_one_launch_fits(nrep, b->ipg, kv_per_group)) return hipErrorInvalidValue;
     if (mode == MPX_MODE_MIN)
         launch_step<MPX_MODE_MIN>(b, nrep, kv_per_group, worklist, wcount, totals, err, stream,
-                                  ev0, ev1);
+                                  ev0, ev1, pslots);
     else
         launch_step<MPX_MODE_CLASSIC>(b, nrep, kv_per_group, worklist, wcount, totals, err,
-                                      stream, ev0, ev1);
+                                      stream, ev0, ev1, pslots);
     return hipGetLastError();
 }
 

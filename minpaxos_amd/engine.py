@@ -47,20 +47,33 @@ def device_count():
     return c.value
 
 
+def step_one_launch_fits(n_replicas, ipg, kv_per_group):
+    """True when a fast group-step variant takes the batch shape, which MPX_FLAG_STEP_ONE_LAUNCH
+    requires (the variant choice of step.hip fast_variant / mpx.h)"""
+    recs = max(n_replicas - 1, 1) * ipg
+    K = kv_per_group or 512
+    return ((ipg <= 256 and recs <= 1024 and K <= 1024) or (ipg <= 256 and recs <= 2048 and K <= 256)
+            or (ipg <= 512 and recs <= 2048 and K <= 512))
+
+
 class Engine:
     def __init__(self, device=0, n_replicas=5, mode=R.MODE_MIN, kv_capacity=0, kv_per_group=0,
                  max_groups=0, apply_path=R.APPLY_AUTO, apply_fast_min=0, apply_hot_min=0,
-                 apply_chunk=0):
+                 apply_chunk=0, step_one_launch=False):
         """apply_* are the handle's mpx_apply settings (mpx_config): the pipeline choice
         (R.APPLY_AUTO / _SMALL / _SORTED / _PARTITIONED), AUTO's partitioned threshold, the hot
-        key sample threshold (R.APPLY_NO_HOT: none) and the chunk size; 0 = default"""
+        key sample threshold (R.APPLY_NO_HOT: none) and the chunk size; 0 = default.
+        step_one_launch: MPX_FLAG_STEP_ONE_LAUNCH (one kernel per group step; every group must
+        fit the fast kernel, see mpx.h)"""
         self.lib = _lib.load()
         if isinstance(mode, str):
             mode = {"min": R.MODE_MIN, "classic": R.MODE_CLASSIC}[mode.lower()]
         self.n_replicas = n_replicas
         self.mode = mode
         self.kv_per_group = kv_per_group or 512
-        cfg = _lib.MpxConfig(n_replicas, mode, kv_capacity, kv_per_group, 0, max_groups,
+        self.step_one_launch = bool(step_one_launch)
+        flags = R.FLAG_STEP_ONE_LAUNCH if step_one_launch else 0
+        cfg = _lib.MpxConfig(n_replicas, mode, kv_capacity, kv_per_group, flags, max_groups,
                              apply_chunk, apply_path, apply_fast_min, apply_hot_min, 0)
         h = C.c_void_p()
         rc = self.lib.mpx_open(device, C.byref(cfg), C.byref(h))

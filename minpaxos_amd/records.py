@@ -100,4 +100,5 @@ assert PREPARE_EFFECT.itemsize == 8
 # mpx_config.apply_path / apply_hot_min (include/mpx.h)
 APPLY_AUTO, APPLY_SORTED, APPLY_PARTITIONED, APPLY_SMALL = 0, 1, 2, 3
 APPLY_NO_HOT = 0xFFFFFFFF
+FLAG_STEP_ONE_LAUNCH = 1  # mpx_config.flags: one kernel per group step (mpx.h)
 APPLY_SMALL_MAX = 16384

@@ -248,11 +248,12 @@ hipError_t launch_prepare_min(const mpx_prepare_reply_min*, uint64_t, const uint
 hipError_t launch_conflict_batch(const uint8_t*, const int64_t*, const uint64_t*, uint64_t,
                                  uint8_t*, hipStream_t) { return hipSuccess; }
 #if MPX_STUB_ORACLE
+bool step_one_launch_fits(int32_t, uint32_t, uint32_t) { return true; }
 // the group step through the oracle; its error codes become the kernels' error-word bits
 hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, uint32_t*, hipStream_t);
 hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group, const mpx_group_batch* b,
                              uint32_t*, uint32_t* ctl, int64_t* totals, uint32_t* err,
-                             hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+                             hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, unsigned long long*) {
     if (ev0) hipEventRecord(ev0, s);
     // the fused form needs the per-group decided counts the oracle writes to n_decided
     std::vector<uint32_t> nd;
@@ -288,8 +289,10 @@ hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, uint32_
     return hipSuccess;
 }
 #else
+bool step_one_launch_fits(int32_t, uint32_t, uint32_t) { return true; }
 hipError_t launch_group_step(int, int32_t, uint32_t, const mpx_group_batch*, uint32_t*, uint32_t*,
-                             int64_t*, uint32_t*, hipStream_t, hipEvent_t, hipEvent_t) { return hipSuccess; }
+                             int64_t*, uint32_t*, hipStream_t, hipEvent_t, hipEvent_t,
+                             unsigned long long*) { return hipSuccess; }
 hipError_t launch_step_totals(const mpx_group_batch*, int64_t*, uint32_t*, hipStream_t) { return hipSuccess; }
 #endif
 uint64_t apply_chunk_commands(uint64_t c, uint64_t m) { return c ? c : m; }

@@ -32,7 +32,7 @@ def test_library_exports_every_header_symbol():
                          text=True, check=True).stdout
     exported = set(re.findall(r"\bT (mpx_[a-z0-9_]+)", out))
     assert set(header_functions()) <= exported
-    assert lib.mpx_abi_version() == 7
+    assert lib.mpx_abi_version() == 8
 
 
 def test_no_device_calls_fail_cleanly():

@@ -862,6 +862,81 @@ def test_group_step_totals_many_groups(mk_engine):
             assert ar.get(tot).tolist() == want
 
 
+@pytest.mark.parametrize("mode", [R.MODE_MIN, R.MODE_CLASSIC])
+@pytest.mark.parametrize("G", [1, 17, 300, 4099])
+def test_group_step_one_launch(mk_engine, mode, G):
+    """MPX_FLAG_STEP_ONE_LAUNCH: the group step is the fast kernel alone, its last workgroup
+    folding the packed totals (16 groups a slot; G not a multiple of 16 leaves a short last
+    slot). Outputs and totals equal the oracle's over repeated steps (the slots reset
+    themselves), also replayed from a captured graph; a shape no fast variant takes is rejected
+    at the call; a group past the fast kernel's capacity fails the step"""
+    from minpaxos_amd.devbuf import Arena
+    N, K = 5, 256
+    b = synth.group_batch(G, 256, N, 4, 256, seed=300 + G)
+    b.setdefault("has_cmds", None)
+    e = mk_engine(N, mode, kv_per_group=K, step_one_launch=True)
+    o = Oracle(N, mode, kv_per_group=K)
+    want = o.group_step(b)
+    want_tot = _want_totals(b, want)
+    with Arena(e) as ar:
+        gb, d = _dev_group_batch(ar, b, N, K, True)
+        tot = ar.full(3, np.int64, 0x55)
+        for _ in range(3):
+            e.group_step_totals_dev(gb, tot.ptr, e.stream)
+            e.synchronize()
+            assert ar.get(tot).tolist() == want_tot
+            assert np.array_equal(ar.get(d["co"]), want["committed_out"])
+            assert np.array_equal(ar.get(d["eo"]), want["executed_out"])
+            assert np.array_equal(ar.get(d["po"]), want["peer_out"].reshape(-1))
+            assert np.array_equal(ar.get(d["st_out"]).view(np.int32),
+                                  want["st_out"].view(np.int32))
+            assert np.array_equal(ar.get(d["nd"]), want["n_decided"])
+        e.group_step_dev(gb, e.stream)  # no totals: no slot is touched
+        e.synchronize()
+        s = e.stream_create()
+        e.graph_begin(s)
+        e.group_step_totals_dev(gb, tot.ptr, s)
+        g = e.graph_end(s)
+        try:
+            for _ in range(2):
+                e.memset(tot.ptr, 0x55, 24, s)
+                e.graph_launch(g, s)
+                e.stream_synchronize(s)
+                assert ar.get(tot).tolist() == want_tot
+        finally:
+            e.graph_destroy(g)
+            e.stream_destroy(s)
+    if G != 300:
+        return
+    # ipg 1024: no fast variant; rejected at the call
+    e2 = mk_engine(3, R.MODE_MIN, kv_per_group=K, step_one_launch=True)
+    b2 = synth.group_batch(4, 1024, 3, 2, 64, seed=5)
+    b2.setdefault("has_cmds", None)
+    with Arena(e2) as ar:
+        gb2, _ = _dev_group_batch(ar, b2, 3, K, True)
+        with pytest.raises(MpxError):
+            e2.group_step_dev(gb2, e2.stream)
+    # groups of more than 1024 commands (the work list's, on a two-launch handle): the step
+    # fails, and the next step on fitting groups runs clean (the slots were all taken)
+    e3 = mk_engine(3, R.MODE_MIN, kv_per_group=1024, step_one_launch=True)
+    b3 = synth.group_batch(64, 128, 3, 9, 800, seed=78)
+    b3.setdefault("has_cmds", None)
+    o3 = Oracle(3, R.MODE_MIN, kv_per_group=1024)
+    b4 = synth.group_batch(64, 128, 3, 2, 100, seed=79)
+    b4.setdefault("has_cmds", None)
+    want4 = _want_totals(b4, o3.group_step(b4))
+    with Arena(e3) as ar:
+        gb3, _ = _dev_group_batch(ar, b3, 3, 1024, True)
+        tot = ar.full(3, np.int64, 0)
+        e3.group_step_totals_dev(gb3, tot.ptr, e3.stream)
+        with pytest.raises(MpxError):
+            e3.synchronize()
+        gb4, _ = _dev_group_batch(ar, b4, 3, 1024, True)
+        e3.group_step_totals_dev(gb4, tot.ptr, e3.stream)
+        e3.synchronize()
+        assert ar.get(tot).tolist() == want4
+
+
 @pytest.mark.gpu
 def test_group_step_graph_replay(mk_engine):
     """mpx_graph_begin / _end / _launch: a group step (+ its totals) captured on a stream and
