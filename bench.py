@@ -206,7 +206,7 @@ def host_cores():
     return max(1, min(n, 16))
 
 
-TRAFFIC_DB = os.path.join(ROOT, "profiles", "traffic_r04.json")
+TRAFFIC_DB = os.path.join(ROOT, "profiles", "traffic_r05.json")
 ISSUE_BOUND = ("decode", "stream", "fanout")
 
 
@@ -542,6 +542,7 @@ def step_bench(a, rk):
             kern_ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in ev_g]
             graph_info["kernel_times"] = ("the third replay of the timed graph's steps with an "
                                           "event pair around each group kernel")
+            graph_info["evented_replay_steps"] = 3 * U
             eng.graph_destroy(g_ev)
         else:
             graph_info["kernel_times"] = "the enqueued pass's events"
@@ -658,7 +659,8 @@ def step_bench(a, rk):
             "executed_commands_per_s": n_exec_cmds * a.steps / elapsed,
             # table fill + warm-up + timed (+ the graph replays' warm-up and timed steps)
             "launches_in_process": 1 + a.warmup + a.steps + (
-                max(a.warmup, 1) * graph_info["steps_per_graph"] + a.steps if use_graph else 0),
+                max(a.warmup, 1) * graph_info["steps_per_graph"] + a.steps
+                + graph_info.get("evented_replay_steps", 0) if use_graph else 0),
             "graph": graph_info or {"used": False},
             "watermark_allreduce_ok": wm_ok,
             **({"emulated_world": {
@@ -989,6 +991,10 @@ def kernel_bench(a, rk):
         units, unit = M, "commands/s"
         kernel = "mpx_apply pipeline"
         kernel_pat = ["mpx::", "rocprim"]
+        if M <= R.APPLY_SMALL_MAX and a.apply_path in ("auto", "small"):
+            # the device-pointer call is one kernel (the host forms' three, timed below for
+            # host_call, are not part of the measured call)
+            kernel, kernel_pat = "k_small_part", ["k_small_part"]
         o = OL.Oracle(N, mode)
         o.apply(op, key, val)
         w_ret, w_conf = o.apply(op, key, val)
