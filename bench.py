@@ -113,6 +113,9 @@ def parse():
     ap.add_argument("--kv-capacity", type=int, default=0,
                     help="apply: engine key capacity (0 = --apply-keys; the table gets >= 2x slots, load <= 1/2)")
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
+    ap.add_argument("--kernel-events", default="separate", choices=["separate", "inline"],
+                    help="step, enqueued pass: HIP events around the group kernel in a separate "
+                         "pass after the timed steps (default) or inside the timed steps")
     ap.add_argument("--step-launches", type=int, default=2, choices=[1, 2],
                     help="step: 1 = MPX_FLAG_STEP_ONE_LAUNCH (the fast kernel alone, totals "
                          "folded by its last workgroup) where the shape fits a fast variant, "
@@ -476,13 +479,26 @@ def step_bench(a, rk):
     eng.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        step(i, True)
+        step(i, a.kernel_events == "inline")
     eng.synchronize()  # every stream of the device; raises if a kernel flagged an error
     rk.barrier()
     t1 = time.perf_counter()
     elapsed = rk.max(t1 - t0)
-    kern_ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in ev_k[:a.steps]]
-    last = (a.steps - 1) & 1
+    n_kev = 0
+    if a.kernel_events == "inline":
+        kern_ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in ev_k[:a.steps]]
+    else:
+        # the kernel times from a separate pass of the same steps right after the timed region:
+        # timing events between the kernels of every timed step cost the enqueued step ~17 us
+        # (a timestamp write on the compute stream per event; --emulate-world 8: 0.117-0.120 ms
+        # per step with them), so the timed steps carry none
+        n_kev = min(a.steps, n_ev, 64)
+        for j in range(n_kev):
+            step(a.steps + j, True, ev_k[j])
+        eng.synchronize()
+        rk.barrier()
+        kern_ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in ev_k[:n_kev]]
+    last = (a.steps + n_kev - 1) & 1
     graph_info = None
     use_graph = a.graph == "on" or (a.graph == "auto" and world == 1)
     if use_graph:
@@ -642,8 +658,9 @@ def step_bench(a, rk):
                 "frac_at_median": alg / (kern_med_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                 "timing": ("HIP events recorded by the engine right before and after each "
                            "k_group_fast launch (mpx_group_step_events) on the compute stream - "
-                           "in the replayed hipGraph (external event nodes) when the line is the "
-                           "graph pass, as ms_per_step is, else in the enqueued pass; "
+                           "in a replay of the timed hipGraph (external event nodes) when the "
+                           "line is the graph pass, as ms_per_step is, else in an enqueued pass "
+                           "of the same steps right after the timed region (--kernel-events); "
                            + ("one launch per step: the kernel's last workgroup folds the step "
                               "totals inside the bracket" if one_launch else
                               "the work-list kernel (second launch) is outside")
@@ -658,7 +675,7 @@ def step_bench(a, rk):
             "executed_instances_per_s": n_exec_inst * a.steps / elapsed,
             "executed_commands_per_s": n_exec_cmds * a.steps / elapsed,
             # table fill + warm-up + timed (+ the graph replays' warm-up and timed steps)
-            "launches_in_process": 1 + a.warmup + a.steps + (
+            "launches_in_process": 1 + a.warmup + a.steps + n_kev + (
                 max(a.warmup, 1) * graph_info["steps_per_graph"] + a.steps
                 + graph_info.get("evented_replay_steps", 0) if use_graph else 0),
             "graph": graph_info or {"used": False},
