@@ -1097,7 +1097,7 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                     __syncthreads();
                     if ((uint32_t)w < nh) {  // wave w: heavy slot w's prefix maxima over the words
                         int a0 = -1, a1 = -1, p0 = -1, p1 = -1;
-                        {
+                        if (l < kLWords) {  // (kLWords < 64 for batches under 2048 records)
                             const uint32_t b0 = S.hb[w][l], q0 = S.hp[w][l];
                             a0 = b0 ? l * 32 + hi_bit(b0) : -1;
                             p0 = q0 ? l * 32 + hi_bit(q0) : -1;
@@ -1119,8 +1119,10 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                             }
                         }
                         const int ta = __shfl(a0, kWave - 1), tp = __shfl(p0, kWave - 1);
-                        S.la[w][l] = a0;
-                        S.lp[w][l] = p0;
+                        if (l < kLWords) {
+                            S.la[w][l] = a0;
+                            S.lp[w][l] = p0;
+                        }
                         if (l + kWave < kLWords) {
                             S.la[w][l + kWave] = a1 > ta ? a1 : ta;
                             S.lp[w][l + kWave] = p1 > tp ? p1 : tp;
@@ -1244,8 +1246,10 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                     if (sl[hh] >= 0) S.cnt[par][(uint32_t)sl[hh] >> 1] = 0u;
                 }
                 if (nh && (uint32_t)w < nh) {
-                    S.hb[w][l] = 0u;
-                    S.hp[w][l] = 0u;
+                    if (l < kLWords) {
+                        S.hb[w][l] = 0u;
+                        S.hp[w][l] = 0u;
+                    }
                     if (l + kWave < kLWords) {
                         S.hb[w][l + kWave] = 0u;
                         S.hp[w][l + kWave] = 0u;

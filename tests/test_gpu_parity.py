@@ -613,7 +613,7 @@ def test_apply_small_partition_skew(mk_engine):
     most 16 of them resolves in LDS, any other takes the list phases. Calls that put 2000-3000
     commands on distinct keys into one partition (the list phases without LONG lists), a hot key
     in the same partition (LONG lists), GETs of absent keys before and after their first PUT, the
-    sentinel key: every call and the table bit-exact"""
+    sentinel key, calls whose every command is on one key: every call and the table bit-exact"""
     rng = np.random.default_rng(99)
     e, o = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 16, apply_path=R.APPLY_SMALL), \
         Oracle(5, R.MODE_MIN)
@@ -634,6 +634,18 @@ def test_apply_small_partition_skew(mk_engine):
         wk, wv = o.kv_export()
         assert np.array_equal(gk, wk) and np.array_equal(gv, wv), m
         assert e.kv_size() == len(wk)
+    # every command on one key (one partition, one LONG list of the whole call): a fresh key, the
+    # sentinel key, a key present in the table
+    for m, k in ((5000, 77_000_001), (16384, np.iinfo(np.int64).min), (3000, int(key[0]))):
+        op = rng.choice([R.OP_PUT, R.OP_GET, R.OP_DELETE], m, p=[0.4, 0.5, 0.1]).astype(np.uint8)
+        kk = np.full(m, k, np.int64)
+        vv = rng.integers(-(1 << 62), 1 << 62, m).astype(np.int64)
+        gr, gc = _apply_form(e, "dev", op, kk, vv)
+        wr, wc = o.apply(op, kk, vv)
+        assert np.array_equal(gr, wr) and np.array_equal(gc, wc), (m, k)
+    gk, gv = e.kv_export()
+    wk, wv = o.kv_export()
+    assert np.array_equal(gk, wk) and np.array_equal(gv, wv)
 
 
 @pytest.mark.parametrize("cap_lg", [22, 23, 25, 26])
