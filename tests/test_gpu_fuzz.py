@@ -1,0 +1,117 @@
+"""Randomised parity sweeps on the GPU: many seeded shapes per test, every result against the
+oracle (oracle/oracle.cpp through tests/oracle_lib.py). The fixed-shape tests elsewhere pin the
+cases the reference's handlers branch on; these draw the shape itself - call sizes, key ranges
+and distributions, table sizes, pipelines, fan-in, replica counts, group shapes - so a build
+parameter that only some shapes reach (a batch boundary, a heavy slot, a partition past its LDS
+capacity) meets them. Seeds are fixed: a failure names its seed and reproduces.
+
+References: Command.Execute / executeCommands (state.go:77-103, bareminpaxos.go:1066-1098),
+handleAcceptReply (bareminpaxos.go:1014-1064, paxos.go:631-673), the fused group step
+(bareminpaxos.go:1014-1098 per group)."""
+import numpy as np
+import pytest
+
+import gen_cases
+from oracle_lib import Oracle, OracleError
+from minpaxos_amd import records as R
+from minpaxos_amd import synth
+from test_gpu_parity import _apply_form, _cmp_group, eq_struct
+
+pytestmark = pytest.mark.gpu
+
+_PATHS = [R.APPLY_AUTO, R.APPLY_SMALL, R.APPLY_PARTITIONED, R.APPLY_SORTED]
+
+
+def _commands(rng, m, space, kind):
+    """m commands over `space` keys: uniform, zipf-like, one hot key mixed in, or the sentinel
+    and the extremes sprinkled in"""
+    op, key, val = gen_cases.commands_mixed(rng, m, space, neg_keys=kind == "special")
+    if kind == "zipf":
+        key = (rng.zipf(1.3, m) % space).astype(np.int64)
+    elif kind == "hot":
+        key[rng.random(m) < rng.uniform(0.05, 0.9)] = int(rng.integers(0, space))
+    return op, key, val
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_fuzz_apply(mk_engine, seed):
+    """apply: a random pipeline and table size, four calls of random size (replica-sized ones
+    through the host and the device-pointer forms), random key distributions; every call's
+    results and the final table bit-exact"""
+    rng = np.random.default_rng(5000 + seed)
+    path = _PATHS[seed % len(_PATHS)]
+    cap = 1 << int(rng.integers(12, 18))
+    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=cap, apply_path=path), Oracle(5, R.MODE_MIN)
+    for call in range(4):
+        small = path == R.APPLY_SMALL or rng.random() < 0.5
+        m = int(rng.integers(1, R.APPLY_SMALL_MAX + 1)) if small else int(rng.integers(1, 120000))
+        space = int(rng.integers(1, cap // 2 + 1))
+        kind = ["uniform", "zipf", "hot", "special"][int(rng.integers(0, 4))]
+        op, key, val = _commands(rng, m, space, kind)
+        form = "dev" if (m <= R.APPLY_SMALL_MAX and rng.random() < 0.5) else "host"
+        gr, gc = _apply_form(e, form, op, key, val)
+        wr, wc = o.apply(op, key, val)
+        tag = (seed, call, path, m, space, kind, form)
+        assert np.array_equal(gr, wr), (tag, np.nonzero(gr != wr)[0][:5])
+        assert np.array_equal(gc, wc), (tag, np.nonzero(gc != wc)[0][:5])
+    gk, gv = e.kv_export()
+    wk, wv = o.kv_export()
+    assert np.array_equal(gk, wk) and np.array_equal(gv, wv), seed
+    assert e.kv_size() == len(wk)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fuzz_accept_tally(mk_engine, seed):
+    """accept tally: random replica count, fan-in (with gaps and long instances), window base
+    and starting watermarks, both modes"""
+    rng = np.random.default_rng(6000 + seed)
+    n_rep = int(rng.integers(1, 10))
+    n_inst = int(rng.integers(1, 40000))
+    rec, st = gen_cases.ragged_accept(rng, n_inst, n_rep, max_r=int(rng.integers(1, 12)),
+                                      long_every=int(rng.integers(0, 3000)),
+                                      long_len=int(rng.integers(20, 400)),
+                                      base=int(rng.integers(0, 1000)))
+    base = int(rec["instance"][0]) if len(rec) else 0
+    for mode in (R.MODE_MIN, R.MODE_CLASSIC):
+        e, o = mk_engine(n_rep, mode), Oracle(n_rep, mode)
+        cu0 = int(rng.integers(-1, 50))
+        pc0 = rng.integers(-1, 10, n_rep).astype(np.int32)
+        got = e.accept_tally(rec, st, base, cu0, pc0)
+        want = o.accept_tally(rec, st, base, cu0, pc0)
+        eq_struct(got[0], want[0])
+        assert got[1] == want[1], (seed, mode, got[1], want[1])
+        assert np.array_equal(got[2], want[2]), (seed, mode)
+        assert np.array_equal(got[3], want[3]), (seed, mode)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fuzz_group_step(mk_engine, seed):
+    """the fused group step: random replica count, instances per group, commands per instance,
+    key range and table capacity (so every fast variant and the work list are drawn), two
+    chained steps, both modes"""
+    rng = np.random.default_rng(7000 + seed)
+    N = int(rng.integers(3, 10))
+    ipg = int(rng.choice([64, 128, 200, 256, 384, 512]))
+    K = int(rng.choice([64, 256, 512, 1024]))
+    B = int(rng.integers(1, 6))
+    keys = int(rng.integers(8, K + 1))
+    G = int(rng.integers(1, 200))
+    for mode in (R.MODE_MIN, R.MODE_CLASSIC):
+        b = synth.group_batch(G, ipg, N, B, keys, p_ok=float(rng.uniform(0.3, 0.95)),
+                              seed=int(rng.integers(0, 1 << 30)))
+        e, o = mk_engine(N, mode, kv_per_group=K), Oracle(N, mode, kv_per_group=K)
+        try:
+            want = o.group_step(b)
+        except OracleError:
+            continue  # a table past kv_per_group: the engine's MPX_E_KV_FULL, tested elsewhere
+        _cmp_group(e.group_step(b), want, G, K)
+        b2 = synth.group_batch(G, ipg, N, B, keys, seed=int(rng.integers(0, 1 << 30)))
+        b2["committed_in"] = want["committed_out"]
+        b2["executed_in"] = np.minimum(want["executed_out"], ipg // 2).astype(np.int32)
+        b2["peer_in"] = want["peer_out"]
+        try:
+            want2 = o.group_step(b2, want["kv_cnt"], want["kv_key"], want["kv_val"])
+        except OracleError:
+            continue
+        got2 = e.group_step(b2, want["kv_cnt"], want["kv_key"], want["kv_val"])
+        _cmp_group(got2, want2, G, K)
