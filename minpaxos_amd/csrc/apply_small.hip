@@ -704,7 +704,11 @@ __global__ __launch_bounds__(kSmT) void k_small_walk(KvTable t, const uint8_t* _
 #define MPX_SMALL_PART 1
 #endif
 #ifndef MPX_SMALL_PART_CMDS
-#define MPX_SMALL_PART_CMDS 256  // commands per partition (the grid: m / this, 1 .. kPartMax)
+// commands per partition (the grid: the power of two >= m / this, at most kPartMax). Same-box
+// A/B, 5000 / 16000 commands: 64 -> 9.9 / 14.2 us, 128 -> 9.3-9.6 / 13.1-13.3, 256 -> 9.7-10.0 /
+// 13.7, 512 -> 10.4-10.6 / 15.2 (more partitions: fewer commands each, but every workgroup
+// loads and hashes every key)
+#define MPX_SMALL_PART_CMDS 128
 #endif
 constexpr uint32_t kPartMax = 256;  // one workgroup per CU (the LONG phase's LDS); a power of 2
 #ifndef MPX_SMALL_FAST

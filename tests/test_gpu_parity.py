@@ -617,7 +617,14 @@ def test_apply_small_partition_skew(mk_engine):
     rng = np.random.default_rng(99)
     e, o = mk_engine(5, R.MODE_MIN, kv_capacity=1 << 16, apply_path=R.APPLY_SMALL), \
         Oracle(5, R.MODE_MIN)
-    for i, (m, lgnp) in enumerate(((16384, 6), (5000, 5), (8000, 5))):
+    def lg_parts(m, per=128, cap=256):  # apply_small.hip launch_apply_small (MPX_SMALL_PART_CMDS)
+        n = 1
+        while n < cap and n * per < m:
+            n <<= 1
+        return n.bit_length() - 1
+
+    for i, m in enumerate((16384, 5000, 8000)):
+        lgnp = lg_parts(m)
         op, key, val = gen_cases.commands_mixed(rng, m, 400 + 100 * i)
         skew = _part_keys(2000 + 500 * i, lgnp, 3 + i, start=10_000_000 * (i + 1))
         at = rng.choice(m, size=len(skew), replace=False)
