@@ -472,6 +472,7 @@ def step_bench(a, rk):
                                    d["tot"][buf].ptr, R_TOTALS, cs)
         eng.event_record(ev_comm[buf], cs)
 
+    use_graph = a.graph == "on" or (a.graph == "auto" and world == 1)
     for i in range(a.warmup):
         step(i, False)
     eng.synchronize()
@@ -480,6 +481,7 @@ def step_bench(a, rk):
     t0 = time.perf_counter()
     for i in range(a.steps):
         step(i, a.kernel_events == "inline")
+    t_enq = time.perf_counter() - t0  # host time to enqueue the timed steps
     eng.synchronize()  # every stream of the device; raises if a kernel flagged an error
     rk.barrier()
     t1 = time.perf_counter()
@@ -500,7 +502,6 @@ def step_bench(a, rk):
         kern_ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in ev_k[:n_kev]]
     last = (a.steps + n_kev - 1) & 1
     graph_info = None
-    use_graph = a.graph == "on" or (a.graph == "auto" and world == 1)
     if use_graph:
         # the same step sequence replayed from hipGraphs, a chunk of U steps per capture. The
         # graph runs the collective on the compute stream: a replayed graph executed the
@@ -668,6 +669,7 @@ def step_bench(a, rk):
                            "beside it (SURVEY 8(d))"),
                 "launches_per_step": 1 if one_launch else 2,
             },
+            "enqueue_ms_per_step": t_enq / max(a.steps, 1) * 1e3,  # the enqueued pass's host time
             "decided_instances_per_step": n_decided,
             "executed_instances_per_step": n_exec_inst,
             "executed_commands_per_step": n_exec_cmds,
