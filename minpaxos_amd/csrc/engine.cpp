@@ -1131,7 +1131,10 @@ int mpx_decode_stream(mpx_engine* e, const uint8_t* buf, size_t len, const mpx_d
         if (r.stop_reason == MPX_DECODE_LONG && r.next <= len) {
             start = r.next;
             window = 1u << 18;
-        } else if (r.stop_reason == MPX_DECODE_PARTIAL && end < len) {
+        } else if ((r.stop_reason == MPX_DECODE_PARTIAL || r.stop_reason == MPX_DECODE_END) &&
+                   end < len) {
+            // the window ended inside the buffer: a frame that runs past it (PARTIAL) or one
+            // that ends exactly at it (END) - both continue from there
             start = r.consumed;
             window = std::min<size_t>(window * 2, len);
         } else {

@@ -115,3 +115,49 @@ def test_fuzz_group_step(mk_engine, seed):
             continue
         got2 = e.group_step(b2, want["kv_cnt"], want["kv_key"], want["kv_val"])
         _cmp_group(got2, want2, G, K)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzz_stream_decode(mk_engine, seed):
+    """the full peer-stream decode (replicaListener + every Unmarshal): random frame mixes of
+    random length - up to several 4 MB tile groups - with variable frames of random size, cut
+    at random places, both wire formats"""
+    from minpaxos_amd import wire as W
+    rng = np.random.default_rng(8000 + seed)
+    for proto in (R.MODE_MIN, R.MODE_CLASSIC):
+        e, o = mk_engine(5, proto), Oracle(5, proto)
+        n = int(rng.integers(1, 12)) * int(10 ** rng.integers(1, 5))
+        b = W.random_stream(proto, rng, n, p_var=float(rng.uniform(0, 0.4)),
+                            p_big=float(rng.uniform(0, 0.03)), p_unknown=float(rng.uniform(0, 0.1)))
+        if seed % 3 == 0:  # a long AcceptReply run: past a tile group (4 MB)
+            recs, _ = synth.accept_replies(int(rng.integers(1 << 18, 1 << 19)), 5, 0.7,
+                                           seed=int(rng.integers(0, 1 << 30)))
+            b = b + bytes(W.leader_stream(proto, recs, prepare_every=int(rng.integers(1, 5000)),
+                                          n_cmds=int(rng.integers(0, 3)))) + b
+        for cut in (len(b), int(rng.integers(0, len(b) + 1))):
+            got, want = e.decode_stream(b[:cut]), o.decode_stream(b[:cut])
+            for g, w, name in zip(got[:4], want[:4], ("ar", "prep", "var", "other")):
+                assert len(g) == len(w) and g.tobytes() == w.tobytes(), (seed, proto, cut, name)
+            for f in ("consumed", "n_accept_replies", "n_prepare_replies", "n_var", "n_other",
+                      "stop_reason", "stop_code"):
+                assert int(got[4][f]) == int(want[4][f]), (seed, proto, cut, f)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzz_peer_decode(mk_engine, seed):
+    """the fixed-frame decoder: AcceptReplies with random mixes of the other fixed frames and
+    unknown codes, random lengths (a tile is ~1170 AcceptReplies, a group 256 tiles), cut at
+    random places"""
+    rng = np.random.default_rng(9000 + seed)
+    e, o = mk_engine(5, R.MODE_MIN), Oracle()
+    n = int(rng.integers(1, 1 << int(rng.integers(1, 20))))
+    recs, _ = synth.accept_replies(n, 5, 0.7, seed=int(rng.integers(0, 1 << 30)))
+    buf = synth.peer_stream(recs, seed=int(rng.integers(0, 1 << 30)),
+                            p_beacon=float(rng.uniform(0, 0.1)), p_prepare=float(rng.uniform(0, 0.05)),
+                            p_commit_short=float(rng.uniform(0, 0.05)),
+                            p_unknown=float(rng.uniform(0, 0.05)))
+    for cut in (len(buf), int(rng.integers(0, len(buf) + 1))):
+        ga, go, gr = e.decode_peer_stream(buf[:cut])
+        wa, wo, wr = o.decode_peer_stream(buf[:cut])
+        assert gr.tobytes() == wr.tobytes(), (seed, cut)
+        assert ga.tobytes() == wa.tobytes() and go.tobytes() == wo.tobytes(), (seed, cut)
