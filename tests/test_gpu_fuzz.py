@@ -161,3 +161,93 @@ def test_fuzz_peer_decode(mk_engine, seed):
         wa, wo, wr = o.decode_peer_stream(buf[:cut])
         assert gr.tobytes() == wr.tobytes(), (seed, cut)
         assert ga.tobytes() == wa.tobytes() and go.tobytes() == wo.tobytes(), (seed, cut)
+
+
+def _log_uniform(rng, lo, hi):
+    """an integer in [lo, hi], log-uniformly"""
+    return int(min(hi, max(lo, round(float(np.exp(rng.uniform(np.log(lo), np.log(hi))))))))
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_prepare(mk_engine, seed):
+    """CLASSIC prepare (random fan-in, gaps, long instances, window base, defaultBallot) and MIN
+    prepare (random groups and replies per group, peer commits)"""
+    rng = np.random.default_rng(10000 + seed)
+    n_rep = int(rng.integers(1, 10))
+    rec, st = gen_cases.ragged_prepare(rng, _log_uniform(rng, 1, 60000), n_rep,
+                                       max_r=int(rng.integers(1, 10)),
+                                       long_every=int(rng.integers(0, 2000)),
+                                       long_len=int(rng.integers(20, 300)), base=-int(rng.integers(0, 5)))
+    base = int(rec["instance"][0]) if len(rec) else 0
+    e, o = mk_engine(n_rep, R.MODE_CLASSIC), Oracle(n_rep, R.MODE_CLASSIC)
+    db = int(rng.integers(-1, 400))
+    got, want = e.prepare_select(rec, st, base, db), o.prepare_select(rec, st, base, db)
+    eq_struct(got[0], want[0])
+    assert got[1] == want[1] and np.array_equal(got[2], want[2]), seed
+    G = _log_uniform(rng, 1, 100000)
+    rec, off, gst = synth.prepare_replies_min(G, 5, seed=int(rng.integers(0, 1 << 30)),
+                                              replies_per_group=int(rng.integers(1, 10)))
+    e, o = mk_engine(5, R.MODE_MIN), Oracle(5, R.MODE_MIN)
+    pc = rng.integers(-1, 50, G * 5).astype(np.int32)
+    got, want = e.prepare_select_min(rec, off, gst, pc), o.prepare_select_min(rec, off, gst, pc)
+    eq_struct(got[0], want[0])
+    assert np.array_equal(got[1], want[1]), seed
+    eq_struct(got[2], want[2])
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_fanout(mk_engine, seed):
+    """client reply fan-out: random batch sizes, connection counts (the counting-sort and the
+    radix path), a hot connection, OK / leader fields"""
+    rng = np.random.default_rng(11000 + seed)
+    e, o = mk_engine(5, R.MODE_MIN), Oracle()
+    n = _log_uniform(rng, 1, 3_000_000)
+    c = _log_uniform(rng, 1, 70000)
+    rec = synth.replies(n, c, seed=int(rng.integers(0, 1 << 30)))
+    if seed % 2:
+        rec["client"][rng.random(n) < rng.uniform(0.1, 0.9)] = int(rng.integers(0, c))
+    ok, leader = int(rng.integers(0, 2)), int(rng.integers(0, 9))
+    got, want = e.encode_replies(rec, c, ok, leader), o.encode_replies(rec, c, ok, leader)
+    assert np.array_equal(got[1], want[1]), (seed, n, c)
+    assert got[0].tobytes() == want[0].tobytes(), (seed, n, c)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_logenc(mk_engine, seed):
+    """durable and catch-up log encoding: random instance counts and commands per instance
+    (ragged, empty instances, one very long instance)"""
+    rng = np.random.default_rng(12000 + seed)
+    e, o = mk_engine(5, R.MODE_MIN), Oracle()
+    n = _log_uniform(rng, 1, 200000)
+    recs, off, op, key, val = synth.log_records(n, int(rng.integers(1, 9)),
+                                                seed=int(rng.integers(0, 1 << 30)), ragged=True)
+    if seed % 3 == 0 and n > 2:  # one instance with many commands (multi-byte varint, big blocks)
+        big = np.array(off, np.int64)
+        extra = int(rng.integers(100, 3000))
+        big[n // 2:] += extra
+        op, key, val = synth.commands(int(big[-1]), 1 << 12, 0.5, "uniform",
+                                      seed=int(rng.integers(0, 1 << 30)))
+        off = big.astype(np.uint64)
+    for fmt in (R.LOG_CATCHUP, R.LOG_DURABLE):
+        got, want = e.encode_log(fmt, recs, off, op, key, val), o.encode_log(fmt, recs, off, op, key, val)
+        assert np.array_equal(got[1], want[1]), (seed, fmt, n)
+        assert got[0].tobytes() == want[0].tobytes(), (seed, fmt, n)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_replay(mk_engine, seed):
+    """durable-log replay: random record counts, instance spaces (dense, sparse, with repeats),
+    starting watermarks"""
+    from test_replay import durable_log
+    rng = np.random.default_rng(13000 + seed)
+    e, o = mk_engine(5, R.MODE_MIN), Oracle()
+    n = _log_uniform(rng, 1, 400000)
+    cap = _log_uniform(rng, max(1, n // 4), 2 * n + 1)
+    dup = bool(seed % 2) or cap < n
+    log = durable_log(n, cap, int(rng.integers(0, 1 << 30)), dup=dup)
+    db, cu = int(rng.integers(-1, 1000)), int(rng.integers(-1, 1 << 20))
+    got, want = e.replay_durable(log, cap, db, cu), o.replay_durable(log, cap, db, cu)
+    assert np.array_equal(got[0], want[0]), (seed, n, cap)
+    for g, w in zip(got[1:5], want[1:5]):
+        assert np.array_equal(g, w), (seed, n, cap)
+    assert got[5:] == want[5:], (seed, n, cap)
