@@ -251,3 +251,47 @@ def test_fuzz_replay(mk_engine, seed):
     for g, w in zip(got[1:5], want[1:5]):
         assert np.array_equal(g, w), (seed, n, cap)
     assert got[5:] == want[5:], (seed, n, cap)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_apply_sequence(mk_engine, seed):
+    """one table through a random sequence of every way to reach it: apply calls of every size
+    through the host, device-pointer and staged forms (so the replica-batch kernels, the
+    sort-based and the partitioned pipelines take turns on the same slots and call tags),
+    imports of present keys, clears, exports; bit-exact after every step"""
+    from minpaxos_amd.devbuf import Arena  # noqa: F401  (through _apply_form)
+    rng = np.random.default_rng(14000 + seed)
+    cap = 1 << int(rng.integers(13, 18))
+    e = mk_engine(5, R.MODE_MIN, kv_capacity=cap, apply_fast_min=int(rng.choice([0, 20000, 50000])))
+    o = Oracle(5, R.MODE_MIN)
+    io = e.apply_buffers(R.APPLY_SMALL_MAX)
+    space = int(rng.integers(16, cap // 3))
+    for stepno in range(14):
+        act = ["host", "dev", "staged", "host", "dev", "import", "clear"][int(rng.integers(0, 7))]
+        if act == "clear":
+            e.kv_clear()
+            o = Oracle(5, R.MODE_MIN)
+            continue
+        if act == "import":
+            n = int(rng.integers(0, space // 4 + 1))
+            keys = rng.choice(space * 4, n, replace=False).astype(np.int64) - space
+            vals = rng.integers(-(1 << 62), 1 << 62, n).astype(np.int64)
+            e.kv_import(keys, vals)
+            o.kv_import(keys, vals)
+        else:
+            m = (int(rng.integers(1, R.APPLY_SMALL_MAX + 1)) if act == "staged" or rng.random() < 0.6
+                 else int(rng.integers(R.APPLY_SMALL_MAX, 90000)))
+            op, key, val = _commands(rng, m, space, ["uniform", "zipf", "hot", "special"][int(rng.integers(0, 4))])
+            if act == "staged":
+                io["op"][:m], io["key"][:m], io["val"][:m] = op, key, val
+                e.apply_staged(m)
+                gr, gc = io["ret"][:m].copy(), io["conf"][:m].copy()
+            else:
+                gr, gc = _apply_form(e, act, op, key, val)
+            wr, wc = o.apply(op, key, val)
+            assert np.array_equal(gr, wr), (seed, stepno, act, m, np.nonzero(gr != wr)[0][:5])
+            assert np.array_equal(gc, wc), (seed, stepno, act, m, np.nonzero(gc != wc)[0][:5])
+        gk, gv = e.kv_export()
+        wk, wv = o.kv_export()
+        assert np.array_equal(gk, wk) and np.array_equal(gv, wv), (seed, stepno, act)
+        assert e.kv_size() == len(wk)
