@@ -41,7 +41,9 @@ def test_fuzz_apply(mk_engine, seed):
     rng = np.random.default_rng(5000 + seed)
     path = _PATHS[seed % len(_PATHS)]
     cap = 1 << int(rng.integers(12, 18))
-    e, o = mk_engine(5, R.MODE_MIN, kv_capacity=cap, apply_path=path), Oracle(5, R.MODE_MIN)
+    chunk = int(rng.choice([0, 0, 5000, 33333]))  # multi-chunk calls: every PUT key inserted first
+    e = mk_engine(5, R.MODE_MIN, kv_capacity=cap, apply_path=path, apply_chunk=chunk)
+    o = Oracle(5, R.MODE_MIN)
     for call in range(4):
         small = path == R.APPLY_SMALL or rng.random() < 0.5
         m = int(rng.integers(1, R.APPLY_SMALL_MAX + 1)) if small else int(rng.integers(1, 120000))
@@ -51,7 +53,7 @@ def test_fuzz_apply(mk_engine, seed):
         form = "dev" if (m <= R.APPLY_SMALL_MAX and rng.random() < 0.5) else "host"
         gr, gc = _apply_form(e, form, op, key, val)
         wr, wc = o.apply(op, key, val)
-        tag = (seed, call, path, m, space, kind, form)
+        tag = (seed, call, path, chunk, m, space, kind, form)
         assert np.array_equal(gr, wr), (tag, np.nonzero(gr != wr)[0][:5])
         assert np.array_equal(gc, wc), (tag, np.nonzero(gc != wc)[0][:5])
     gk, gv = e.kv_export()
@@ -295,3 +297,27 @@ def test_fuzz_apply_sequence(mk_engine, seed):
         wk, wv = o.kv_export()
         assert np.array_equal(gk, wk) and np.array_equal(gv, wv), (seed, stepno, act)
         assert e.kv_size() == len(wk)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_conflict_and_prefix(mk_engine, seed):
+    """ConflictBatch over every consecutive instance pair (random sizes, empty and very large
+    instances, key ranges) and updateCommittedUpTo over random status windows"""
+    import kat_cases
+    rng = np.random.default_rng(15000 + seed)
+    e, o = mk_engine(5, R.MODE_CLASSIC), Oracle(5, R.MODE_CLASSIC)
+    n_inst = _log_uniform(rng, 1, 200000)
+    sizes = rng.integers(0, int(rng.integers(1, 20)), n_inst)
+    if seed % 2:
+        sizes[rng.random(n_inst) < 0.002] = int(rng.integers(200, 3000))
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    op, key, _ = gen_cases.commands_mixed(rng, int(off[-1]), _log_uniform(rng, 1, 1 << 20),
+                                          neg_keys=bool(seed % 3 == 0))
+    assert np.array_equal(e.conflict_batch(op, key, off), o.conflict_batch(op, key, off)), seed
+    n = _log_uniform(rng, 1, 300000)
+    st = kat_cases.inst_states(n, R.COMMITTED)
+    bad = rng.integers(0, n, int(rng.integers(0, 6)))
+    st["status"][bad] = rng.choice([R.PREPARED, R.STATUS_NIL, R.ACCEPTED], len(bad))
+    base = int(rng.integers(-3, 3))
+    cu = int(rng.integers(base - 2, base + n))
+    assert e.committed_prefix(st, base, cu) == o.committed_prefix(st, base, cu), seed
