@@ -454,8 +454,13 @@ def step_bench(a, rk):
     clock_khz = eng.group_step_clock()
 
     def span_ms(n):
-        return [R.step_clock_ticks(w) / clock_khz
-                for w in ar.get(spans)[:SW * n].reshape(n, SW)]
+        # None: a step left its span unwritten (a shape no fast variant takes: the work-list
+        # kernel runs every group, and the events are the timer)
+        try:
+            return [R.step_clock_ticks(w) / clock_khz
+                    for w in ar.get(spans)[:SW * n].reshape(n, SW)]
+        except RuntimeError:
+            return None
 
     # watermark ranges other ranks own, [0, g0) and [g1, G_total) of both halves: -1 once
     for lo, hi in [(h + lo, h + hi) for h in (0, G_total) for lo, hi in ((0, g0), (g1, G_total))
@@ -527,7 +532,8 @@ def step_bench(a, rk):
         rk.barrier()
         ev_ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in ev_k[:n_kev]]
         clk_ms = span_ms(n_kev)
-    kern_ms = clk_ms if a.kernel_timer == "clock" else ev_ms
+    timer = a.kernel_timer if clk_ms is not None else "events"
+    kern_ms = clk_ms if timer == "clock" else ev_ms
     last = (a.steps + n_kev - 1) & 1
     graph_info = None
     if use_graph:
@@ -602,7 +608,8 @@ def step_bench(a, rk):
             "the third replay of the timed graph's steps with each fast kernel writing its clock "
             "span" + (" / with an event pair around each group kernel" if g_ev is not None else
                       " (events: the enqueued pass's)"))
-        kern_ms = clk_ms if a.kernel_timer == "clock" else ev_ms
+        timer = a.kernel_timer if clk_ms is not None else "events"
+        kern_ms = clk_ms if timer == "clock" else ev_ms
         last = (U - 1) & 1  # the last replayed step
         elapsed = elapsed_graph
         for gx in graphs.values():
@@ -697,15 +704,17 @@ def step_bench(a, rk):
                 "kernel_ms_avg": kern_avg_ms, "kernel_ms_median": kern_med_ms,
                 "kernel_ms_min": float(np.min(kern_ms)),
                 "frac_at_median": alg / (kern_med_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
-                "kernel_timer": a.kernel_timer,
-                "kernel_ms_median_clock": float(np.median(clk_ms)),
+                "kernel_timer": timer,
+                "kernel_ms_median_clock": float(np.median(clk_ms)) if clk_ms else None,
                 "kernel_ms_median_events": float(np.median(ev_ms)),
                 "clock_khz": clock_khz,
                 "timing": (("k_group_fast's own span on the device's constant-rate clock "
                             "(mpx_group_step_clock: the first workgroups' start to the last "
                             "workgroup's end, s_memrealtime; one atomic min per workgroup into "
                             "255 partial words)"
-                            if a.kernel_timer == "clock" else
+                            if timer == "clock" else
+                            ("(no fast variant takes this shape: no clock span) "
+                             if timer != a.kernel_timer else "") +
                             "HIP events recorded by the engine right before and after each "
                             "k_group_fast launch (mpx_group_step_events) on the compute stream")
                            + " - in a replay of the timed hipGraph's steps when the line is the "

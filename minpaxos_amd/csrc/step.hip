@@ -463,7 +463,11 @@ __device__ void fold_packed(unsigned long long* pslots, uint32_t n_groups, int64
 // as ~tick, to 255 partial words a 128-byte line apart, workgroup g to line 1 + g % 255: one
 // word for all workgroups (65536 at config 5) made the kernel 2.4x slower, its atomics
 // serialised at one address (profiles/r05/clock)
+#ifndef MPX_STEP_CLOCK  // 0: the hook compiled out (A/B builds: what it costs the kernel)
+#define MPX_STEP_CLOCK 1
+#endif
 __device__ __forceinline__ void span_mark(unsigned long long* span, bool end) {
+    if (!MPX_STEP_CLOCK) return;
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
     const uint32_t g = blockIdx.x;
     if (!end && g >= 8) return;
@@ -981,7 +985,7 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
     if (ebits) raise_err(err, ebits);
     if (pslots && totals && g == gridDim.x - 1) fold_packed(pslots, gridDim.x, totals, err);
     STAMP(6);
-    if (span) {  // the workgroup's end: after its last wave (span is uniform: the barrier is safe)
+    if (MPX_STEP_CLOCK && span) {  // the workgroup's end: after its last wave (span is uniform)
         __syncthreads();
         if (t == 0) span_mark(span, true);
     }
