@@ -116,12 +116,6 @@ def parse():
     ap.add_argument("--kernel-events", default="separate", choices=["separate", "inline"],
                     help="step, enqueued pass: HIP events around the group kernel in a separate "
                          "pass after the timed steps (default) or inside the timed steps")
-    ap.add_argument("--kernel-timer", default="clock", choices=["clock", "events"],
-                    help="step: the roofline's kernel times from the fast kernel's own span on "
-                         "the device clock (mpx_group_step_clock: first workgroup's start to "
-                         "last workgroup's end, the default) or from the HIP events recorded "
-                         "around its launch (mpx_group_step_events); the other's median is "
-                         "reported beside them")
     ap.add_argument("--step-launches", type=int, default=2, choices=[1, 2],
                     help="step: 1 = MPX_FLAG_STEP_ONE_LAUNCH (the fast kernel alone, totals "
                          "folded by its last workgroup) where the shape fits a fast variant, "
@@ -446,21 +440,6 @@ def step_bench(a, rk):
     ev_comm = [eng.event_create(False) for _ in range(2)]
     n_ev = max(a.steps, 1)
     ev_k = [(eng.event_create(), eng.event_create()) for _ in range(n_ev)]
-    # the fast kernel's clock spans (mpx_group_step_clock), MPX_STEP_CLOCK_WORDS u64 per timed
-    # step of a timing pass (start + ~end partials, by atomic min: a 0xFF fill readies them)
-    n_span = min(n_ev, 64)
-    SW = R.STEP_CLOCK_WORDS
-    spans = ar.full(SW * n_span, np.uint64, 0xFF)
-    clock_khz = eng.group_step_clock()
-
-    def span_ms(n):
-        # None: a step left its span unwritten (a shape no fast variant takes: the work-list
-        # kernel runs every group, and the events are the timer)
-        try:
-            return [R.step_clock_ticks(w) / clock_khz
-                    for w in ar.get(spans)[:SW * n].reshape(n, SW)]
-        except RuntimeError:
-            return None
 
     # watermark ranges other ranks own, [0, g0) and [g1, G_total) of both halves: -1 once
     for lo, hi in [(h + lo, h + hi) for h in (0, G_total) for lo, hi in ((0, g0), (g1, G_total))
@@ -469,27 +448,22 @@ def step_bench(a, rk):
             eng.memset(wb.at(lo), 0xFF, (hi - lo) * 4, comp)
     eng.synchronize()
 
-    def step(i, evs=None, cs=None, clk=None):
+    def step(i, timed, evs=None, cs=None):
         cs = cs or comm  # the collective's stream
         buf = i & 1
         if i >= 2:  # buffers `buf` are free once the all-reduce of step i-2 has used them
             eng.stream_wait_event(comp, ev_comm[buf])
-        # a timing step's HIP events bracket the group kernel alone: the engine records them
+        # the timed steps' HIP events bracket the group kernel alone: the engine records them
         # right before and after its launch (mpx_group_step_events), the work-list kernel and
-        # the totals are outside; its clock span (clk) is the fast kernel's own
-        if evs:
-            eng.group_step_events(*evs)
-        if clk:
-            eng.group_step_clock(clk)
+        # the totals are outside
+        eng.group_step_events(*(evs or (ev_k[i] if timed else (None, None))))
         # the group step, then its totals (decided, executed instances, executed commands)
         if not a.separate_totals:
             eng.group_step_totals_dev(steps[buf], d["tot"][buf].ptr, comp)
         else:
             eng.group_step_dev(steps[buf], comp)
-        if evs:
+        if timed or evs:
             eng.group_step_events()
-        if clk:
-            eng.group_step_clock()
         if a.separate_totals:
             eng.step_totals_dev(steps[buf], d["tot"][buf].ptr, comp)
         eng.event_record(ev_done[buf], comp)
@@ -500,40 +474,32 @@ def step_bench(a, rk):
 
     use_graph = a.graph == "on" or (a.graph == "auto" and world == 1)
     for i in range(a.warmup):
-        step(i)
+        step(i, False)
     eng.synchronize()
     rk.barrier()
     eng.synchronize()
     t0 = time.perf_counter()
-    inline = a.kernel_events == "inline"
     for i in range(a.steps):
-        step(i, ev_k[i] if inline else None,
-             clk=spans.at(SW * i) if inline and i < n_span else None)
+        step(i, a.kernel_events == "inline")
     t_enq = time.perf_counter() - t0  # host time to enqueue the timed steps
     eng.synchronize()  # every stream of the device; raises if a kernel flagged an error
     rk.barrier()
     t1 = time.perf_counter()
     elapsed = rk.max(t1 - t0)
     n_kev = 0
-    if inline:
-        ev_ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in ev_k[:a.steps]]
-        clk_ms = span_ms(min(a.steps, n_span))
+    if a.kernel_events == "inline":
+        kern_ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in ev_k[:a.steps]]
     else:
         # the kernel times from a separate pass of the same steps right after the timed region:
         # timing events between the kernels of every timed step cost the enqueued step ~17 us
         # (a timestamp write on the compute stream per event; --emulate-world 8: 0.117-0.120 ms
         # per step with them), so the timed steps carry none
-        # (both timers in this pass: the clock span is the kernel's own whatever surrounds it)
-        n_kev = min(a.steps, n_span)
-        eng.memset(spans.ptr, 0xFF, 8 * SW * n_kev, comp)
+        n_kev = min(a.steps, n_ev, 64)
         for j in range(n_kev):
-            step(a.steps + j, ev_k[j], clk=spans.at(SW * j))
+            step(a.steps + j, True, ev_k[j])
         eng.synchronize()
         rk.barrier()
-        ev_ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in ev_k[:n_kev]]
-        clk_ms = span_ms(n_kev)
-    timer = a.kernel_timer if clk_ms is not None else "events"
-    kern_ms = clk_ms if timer == "clock" else ev_ms
+        kern_ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in ev_k[:n_kev]]
     last = (a.steps + n_kev - 1) & 1
     graph_info = None
     if use_graph:
@@ -545,20 +511,17 @@ def step_bench(a, rk):
         # process: the one-rank all-reduce is RCCL's copy.
         U = min(a.steps, 64)
         chunks = [U] * (a.steps // U) + ([a.steps % U] if a.steps % U else [])
-        # two more U-step graphs for the roofline's kernel times, replayed after the timed region:
-        # the timed graph's steps with each fast kernel writing its clock span (the same nodes,
-        # one kernel argument apart), and with a HIP event pair around each group kernel
-        # (external event nodes, which cost a replay a few us per step and sit in the bracket, so
-        # neither the timed graphs nor the clock graph have them)
+        # a second U-step graph, the same steps with a HIP event pair around each group kernel
+        # (external event nodes, which cost a replay a few us per step, so the timed graphs have
+        # none): replayed once after the timed region, it gives the roofline's kernel times
         ev_g = [(eng.event_create(), eng.event_create()) for _ in range(U)]
 
-        def capture(n, evs=False, clk=False):
+        def capture(n, evs=False):
             eng.graph_begin(comp)
             for j in range(n):
-                step(j, ev_g[j] if evs else None, cs=comp,
-                     clk=spans.at(SW * j) if clk else None)
+                step(j, False, ev_g[j] if evs else None, cs=comp)
             return eng.graph_end(comp)
-        g_ev = g_clk = None
+        g_ev = None
         try:
             graphs = {n: capture(n) for n in set(chunks)}
         except MpxError as e:  # "auto" on a library without stream capture (the CPU stub)
@@ -567,7 +530,6 @@ def step_bench(a, rk):
             graph_info = {"used": False, "unavailable": str(e)[:160]}
             use_graph = False
         if use_graph:
-            g_clk = capture(U, clk=True)
             try:
                 g_ev = capture(U, evs=True)
             except MpxError:  # (a runtime without external event nodes: the enqueued pass's)
@@ -590,27 +552,18 @@ def step_bench(a, rk):
                       "ms_per_step_graph": elapsed_graph / a.steps * 1e3,
                       "ms_per_step_no_graph": elapsed / a.steps * 1e3,
                       "kernel_ms_median_enqueued": float(np.median(kern_ms))}
-        for _ in range(3):  # (the first replays of a fresh graph run cold; the third counts)
-            eng.memset(spans.ptr, 0xFF, 8 * SW * U, comp)
-            eng.graph_launch(g_clk, comp)
-        eng.synchronize()
-        clk_ms = span_ms(U)
-        eng.graph_destroy(g_clk)
-        graph_info["timing_replay_steps"] = 3 * U
         if g_ev is not None:
-            for _ in range(3):
+            for _ in range(3):  # (the first replays of a fresh graph run cold)
                 eng.graph_launch(g_ev, comp)
             eng.synchronize()
-            ev_ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in ev_g]
-            graph_info["timing_replay_steps"] += 3 * U
+            kern_ms = [eng.event_elapsed_ms(e0, e1) for e0, e1 in ev_g]
+            graph_info["kernel_times"] = ("the third replay of the timed graph's steps with an "
+                                          "event pair around each group kernel")
+            graph_info["evented_replay_steps"] = 3 * U
             eng.graph_destroy(g_ev)
-        graph_info["kernel_times"] = (
-            "the third replay of the timed graph's steps with each fast kernel writing its clock "
-            "span" + (" / with an event pair around each group kernel" if g_ev is not None else
-                      " (events: the enqueued pass's)"))
-        timer = a.kernel_timer if clk_ms is not None else "events"
-        kern_ms = clk_ms if timer == "clock" else ev_ms
-        last = (U - 1) & 1  # the last replayed step
+        else:
+            graph_info["kernel_times"] = "the enqueued pass's events"
+        last = ((U if g_ev is not None else chunks[-1]) - 1) & 1  # the last replayed step
         elapsed = elapsed_graph
         for gx in graphs.values():
             eng.graph_destroy(gx)
@@ -646,7 +599,14 @@ def step_bench(a, rk):
            + int(kc.sum()) * 16 * 2 + G * (4 * 4 + 2 * N * 4 + 4 * 2 + 8 * 2 + 4))
     kern_avg_ms = float(np.mean(kern_ms)) if kern_ms else float("nan")
     kern_med_ms = float(np.median(kern_ms)) if kern_ms else float("nan")
-    achieved_gbs = alg / (kern_avg_ms * 1e-3) / 1e9
+    # the kernel's time is bounded from above by its event bracket (the kernel plus the dispatch
+    # on either side and the event nodes' own cost) and by the step it is part of (the kernel
+    # plus the work-list kernel and the collective): achieved from the tighter bound, so the
+    # kernel is never credited with more time than the step took (the bracket came out 0.2 %
+    # above ms_per_step on one box)
+    step_ms = elapsed / max(a.steps, 1) * 1e3
+    kern_bound_ms = min(kern_avg_ms, step_ms)
+    achieved_gbs = alg / (kern_bound_ms * 1e-3) / 1e9
     tkey = {"workload": "step", "mode": a.mode, "groups": G, "ipg": ipg, "replicas": N,
             "cmds": B, "keys": a.keys, "kv_per_group": K}
     traffic, tnote = traffic_for(tkey, alg, a.traffic_json)
@@ -703,29 +663,19 @@ def step_bench(a, rk):
                              "alg_table_bytes of the total)"),
                 "kernel_ms_avg": kern_avg_ms, "kernel_ms_median": kern_med_ms,
                 "kernel_ms_min": float(np.min(kern_ms)),
-                "frac_at_median": alg / (kern_med_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
-                "kernel_timer": timer,
-                "kernel_ms_median_clock": float(np.median(clk_ms)) if clk_ms else None,
-                "kernel_ms_median_events": float(np.median(ev_ms)),
-                "clock_khz": clock_khz,
-                "timing": (("k_group_fast's own span on the device's constant-rate clock "
-                            "(mpx_group_step_clock: the first workgroups' start to the last "
-                            "workgroup's end, s_memrealtime; one atomic min per workgroup into "
-                            "255 partial words)"
-                            if timer == "clock" else
-                            ("(no fast variant takes this shape: no clock span) "
-                             if timer != a.kernel_timer else "") +
-                            "HIP events recorded by the engine right before and after each "
-                            "k_group_fast launch (mpx_group_step_events) on the compute stream")
-                           + " - in a replay of the timed hipGraph's steps when the line is the "
-                           "graph pass, as ms_per_step is, else in an enqueued pass of the same "
-                           "steps right after the timed region (--kernel-events); "
+                "kernel_ms_bound": kern_bound_ms,
+                "frac_at_median": alg / (min(kern_med_ms, step_ms) * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                "timing": ("HIP events recorded by the engine right before and after each "
+                           "k_group_fast launch (mpx_group_step_events) on the compute stream - "
+                           "in a replay of the timed hipGraph (external event nodes) when the "
+                           "line is the graph pass, as ms_per_step is, else in an enqueued pass "
+                           "of the same steps right after the timed region (--kernel-events); "
                            + ("one launch per step: the kernel's last workgroup folds the step "
-                              "totals inside the span" if one_launch else
+                              "totals inside the bracket" if one_launch else
                               "the work-list kernel (second launch) is outside")
-                           + "; the collective is outside; achieved from their mean, the median "
-                           "beside it, the other timer's median beside that (an event bracket "
-                           "also holds the dispatch around the kernel) (SURVEY 8(d))"),
+                           + "; the collective is outside; achieved from kernel_ms_bound = "
+                           "min(their mean, ms_per_step) - both bound the kernel's time from "
+                           "above - the median beside it (SURVEY 8(d))"),
                 "launches_per_step": 1 if one_launch else 2,
             },
             "enqueue_ms_per_step": t_enq / max(a.steps, 1) * 1e3,  # the enqueued pass's host time
@@ -738,7 +688,7 @@ def step_bench(a, rk):
             # table fill + warm-up + timed (+ the graph replays' warm-up and timed steps)
             "launches_in_process": 1 + a.warmup + a.steps + n_kev + (
                 max(a.warmup, 1) * graph_info["steps_per_graph"] + a.steps
-                + graph_info.get("timing_replay_steps", 0) if use_graph else 0),
+                + graph_info.get("evented_replay_steps", 0) if use_graph else 0),
             "graph": graph_info or {"used": False},
             "watermark_allreduce_ok": wm_ok,
             **({"emulated_world": {

@@ -73,9 +73,9 @@
 extern "C" {
 #endif
 
-#define MPX_ABI_VERSION 9  /* 4: + mpx_group_step_totals_dev; 5: + mpx_graph_*, mpx_apply_buffers / _staged;
+#define MPX_ABI_VERSION 8  /* 4: + mpx_group_step_totals_dev; 5: + mpx_graph_*, mpx_apply_buffers / _staged;
                               6: + mpx_replay_durable_reserve; 7: + mpx_group_step_events;
-                              8: + MPX_FLAG_STEP_ONE_LAUNCH; 9: + mpx_group_step_clock */
+                              8: + MPX_FLAG_STEP_ONE_LAUNCH */
 
 /* ---- error codes ---------------------------------------------------------------------- */
 #define MPX_OK 0
@@ -417,20 +417,6 @@ int mpx_group_step_totals_dev(mpx_engine* eng, const mpx_group_batch* b, int64_t
  * work-list fill), on the call's stream, so the pair brackets that kernel alone (the work-list
  * kernel that follows is outside). Both NULL turns it off. Events from mpx_event_create.    */
 int mpx_group_step_events(mpx_engine* eng, void* ev_fast_start, void* ev_fast_end);
-/* timing hook (ABI 9): the per-group fast kernel of every later group step of the handle writes
- * its own execution span on the device's constant-rate clock into span_dev (device memory,
- * MPX_STEP_CLOCK_WORDS uint64, 32 KiB): span_dev[0] = the start tick (min over the kernel's
- * first workgroups), span_dev[MPX_STEP_CLOCK_LINE * i] for i in 1..MPX_STEP_CLOCK_ENDS = the
- * bitwise NOT of the max end tick over a share of the workgroups; the kernel's end is the max
- * over those of the NOT. Every word is updated by atomic min, so fill the buffer with 0xFF
- * bytes before the step (a share with no workgroup keeps 0xFF.., NOT 0). ticks / clock_khz =
- * milliseconds. NULL turns it off; *clock_khz (may be NULL) receives the clock's rate. No
- * event or extra node is involved, so the hook can sit inside a replayed graph without
- * changing its other nodes. A step whose shape fits no fast variant writes nothing.        */
-#define MPX_STEP_CLOCK_LINE 16
-#define MPX_STEP_CLOCK_ENDS 255
-#define MPX_STEP_CLOCK_WORDS (MPX_STEP_CLOCK_LINE * (MPX_STEP_CLOCK_ENDS + 1))
-int mpx_group_step_clock(mpx_engine* eng, uint64_t* span_dev, int64_t* clock_khz);
 
 /* ---- multi-GPU: the one collective (RCCL over xGMI) -------------------------------------
  * Each rank owns a block of groups; non-owned entries must hold -1. After the call every

@@ -102,7 +102,6 @@ SIGNATURES = {
     "mpx_stream_synchronize": (C.c_int, [_p, _p]),
     "mpx_event_create": (C.c_int, [_p, C.c_int, C.POINTER(_p)]),
     "mpx_group_step_events": (C.c_int, [_p, _p, _p]),
-    "mpx_group_step_clock": (C.c_int, [_p, _p, C.POINTER(C.c_int64)]),
     "mpx_event_destroy": (C.c_int, [_p, _p]),
     "mpx_event_record": (C.c_int, [_p, _p, _p]),
     "mpx_apply_buffers": (C.c_int, [_p, _sz, C.POINTER(MpxApplyIo)]),

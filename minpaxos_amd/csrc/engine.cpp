@@ -97,7 +97,6 @@ struct mpx_engine {
     DevBuf worklist;
     uint32_t* d_wcount = nullptr;
     hipEvent_t ev_fast0 = nullptr, ev_fast1 = nullptr;  // mpx_group_step_events
-    uint64_t* span = nullptr;                            // mpx_group_step_clock
     // RCCL
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -769,8 +768,7 @@ int group_step_dev(mpx_engine* e, const mpx_group_batch* b, int64_t* d_totals, v
         return fail(e, MPX_E_INVAL, "MPX_FLAG_STEP_ONE_LAUNCH: the batch shape fits no fast variant");
     HIPCHK(e, mpx::launch_group_step(e->cfg.mode, e->cfg.n_replicas, e->cfg.kv_per_group, b,
                                      (uint32_t*)e->worklist.p, e->d_wcount, d_totals, e->d_err,
-                                     pick(e, stream), e->ev_fast0, e->ev_fast1, pslots(e),
-                                     reinterpret_cast<unsigned long long*>(e->span)));
+                                     pick(e, stream), e->ev_fast0, e->ev_fast1, pslots(e)));
     return MPX_OK;
 }
 }  // namespace
@@ -793,18 +791,6 @@ int mpx_group_step_events(mpx_engine* e, void* ev_fast_start, void* ev_fast_end)
     if (!ev_fast_start != !ev_fast_end) return fail(e, MPX_E_INVAL, "give both events or neither");
     e->ev_fast0 = (hipEvent_t)ev_fast_start;
     e->ev_fast1 = (hipEvent_t)ev_fast_end;
-    return MPX_OK;
-}
-
-int mpx_group_step_clock(mpx_engine* e, uint64_t* span_dev, int64_t* clock_khz) {
-    if (!e) return MPX_E_INVAL;
-    if (clock_khz) {
-        int khz = 0;
-        HIPCHK(e, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, e->device));
-        if (khz <= 0) return fail(e, MPX_E_UNSUPPORTED, "the device reports no constant-rate clock");
-        *clock_khz = khz;
-    }
-    e->span = span_dev;
     return MPX_OK;
 }
 

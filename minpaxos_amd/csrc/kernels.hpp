@@ -59,14 +59,11 @@ hipError_t launch_conflict_batch(const uint8_t* op, const int64_t* key, const ui
 // launch.
 // ev_fast0 / ev_fast1 (optional): recorded on `stream` right before and after the fast kernel's
 // launch (mpx_group_step_events), so a timer can bracket that kernel alone.
-// span (optional, device, MPX_STEP_CLOCK_WORDS u64 filled with 0xFF): the fast kernel's own start
-// / ~end ticks on the constant-rate clock (mpx_group_step_clock).
 hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
                              const mpx_group_batch* b, uint32_t* worklist, uint32_t* wcount,
                              int64_t* totals, uint32_t* err, hipStream_t stream,
                              hipEvent_t ev_fast0, hipEvent_t ev_fast1,
-                             unsigned long long* pslots = nullptr,
-                             unsigned long long* span = nullptr);
+                             unsigned long long* pslots = nullptr);
 // one-launch steps (pslots: the engine's zeroed packed-totals slots, one u64 per 64 groups): the
 // fast kernel alone, which folds the totals in its last workgroup; the shape must fit a fast
 // variant (step_one_launch_fits) and a group that does not fit it fails the step

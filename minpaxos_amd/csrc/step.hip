@@ -457,38 +457,18 @@ __device__ void fold_packed(unsigned long long* pslots, uint32_t n_groups, int64
     if (threadIdx.x < 3) totals[threadIdx.x] = (int64_t)fsum[threadIdx.x];
 }
 
-// mpx_group_step_clock: a workgroup's start (end = false) or end tick on the constant-rate clock,
-// by atomic min (so a 0xFF fill readies the words between steps). The start goes to word 0 from
-// the first workgroup of each XCD only (dispatch is in order: the kernel's first waves); the ends,
-// as ~tick, to 255 partial words a 128-byte line apart, workgroup g to line 1 + g % 255: one
-// word for all workgroups (65536 at config 5) made the kernel 2.4x slower, its atomics
-// serialised at one address (profiles/r05/clock)
-#ifndef MPX_STEP_CLOCK  // 0: the hook compiled out (A/B builds: what it costs the kernel)
-#define MPX_STEP_CLOCK 1
-#endif
-__device__ __forceinline__ void span_mark(unsigned long long* span, bool end) {
-    if (!MPX_STEP_CLOCK) return;
-    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-    const uint32_t g = blockIdx.x;
-    if (!end && g >= 8) return;
-    (void)__hip_atomic_fetch_min(span + (end ? MPX_STEP_CLOCK_LINE * (1 + g % MPX_STEP_CLOCK_ENDS) : 0),
-                                 end ? ~now : now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 template <int MODE, class Cfg>
 __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int32_t nrep,
                                                          uint32_t kvpg, uint32_t* worklist,
                                                          uint32_t* wcount,
                                                          unsigned long long* tacc, uint32_t* err,
                                                          unsigned long long* pslots,
-                                                         int64_t* totals,
-                                                         unsigned long long* span) {
+                                                         int64_t* totals) {
     MPX_FAST_CONSTS
     __shared__ FastLds<Cfg, MODE> S;
     STAMP_DECL
     const uint32_t g = blockIdx.x;
     const int t = threadIdx.x, l = lane_id();
-    if (span && t == 0) span_mark(span, false);
     const int32_t half = nrep >> 1;
     const uint32_t ipg = b.ipg;
     const uint64_t gi0 = (uint64_t)g * ipg;
@@ -511,7 +491,6 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
         } else if (t == 0) {
             worklist[atomicAdd(wcount, 1u)] = g;
         }
-        if (span && t == 0) span_mark(span, true);  // (this exit is uniform over the workgroup)
         return;
     }
     const int64_t lo = (int64_t)ex_in + 1 < 0 ? 0 : (int64_t)ex_in + 1;  // first instance to run
@@ -855,7 +834,6 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
         } else if (t == 0) {
             worklist[atomicAdd(wcount, 1u)] = g;
         }
-        if (span && t == 0) span_mark(span, true);  // (this exit is uniform over the workgroup)
         return;
     }
     // the group stays here: the instance outputs can go now (st_out may alias st_in, so not
@@ -985,10 +963,6 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
     if (ebits) raise_err(err, ebits);
     if (pslots && totals && g == gridDim.x - 1) fold_packed(pslots, gridDim.x, totals, err);
     STAMP(6);
-    if (MPX_STEP_CLOCK && span) {  // the workgroup's end: after its last wave (span is uniform)
-        __syncthreads();
-        if (t == 0) span_mark(span, true);
-    }
 }
 
 // ======================================= general path =========================================
@@ -1300,9 +1274,9 @@ void record_timing_event(hipEvent_t ev, hipStream_t stream) {
 template <int MODE, class Cfg>
 void launch_fast(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t* worklist,
                  uint32_t* wcount, unsigned long long* tacc, uint32_t* err, hipStream_t stream,
-                 unsigned long long* pslots, int64_t* totals, unsigned long long* span) {
+                 unsigned long long* pslots, int64_t* totals) {
     k_group_fast<MODE, Cfg><<<b->n_groups, Cfg::kFT, 0, stream>>>(*b, nrep, kvpg, worklist, wcount,
-                                                                   tacc, err, pslots, totals, span);
+                                                                   tacc, err, pslots, totals);
 }
 // the smallest fast-path variant the batch's shape fits (0 = none: every group is general)
 int fast_variant(int32_t nrep, uint32_t ipg, uint32_t kvpg) {
@@ -1317,8 +1291,7 @@ int fast_variant(int32_t nrep, uint32_t ipg, uint32_t kvpg) {
 template <int MODE>
 void launch_step(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t* worklist,
                  uint32_t* wcount, int64_t* totals, uint32_t* err, hipStream_t stream,
-                 hipEvent_t ev0, hipEvent_t ev1, unsigned long long* pslots,
-                 unsigned long long* span) {
+                 hipEvent_t ev0, hipEvent_t ev1, unsigned long long* pslots) {
     // two-launch steps: the step totals' partial slots (control words [16..)), the fast kernel
     // adds the groups it keeps, the general kernel the listed ones and folds them; one-launch
     // steps (pslots): the fast kernel's packed slots and its last workgroup's fold
@@ -1329,7 +1302,7 @@ void launch_step(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t
     switch (fast_variant(nrep, b->ipg, kvpg)) {
 #define MPX_FAST_CASE(n, C)                                                                    \
     case n:                                                                                    \
-        launch_fast<MODE, C>(b, nrep, kvpg, worklist, wcount, tacc, err, stream, pslots, ptot, span); \
+        launch_fast<MODE, C>(b, nrep, kvpg, worklist, wcount, tacc, err, stream, pslots, ptot); \
         break;
     MPX_FAST_CASE(1, FastBase)
     MPX_FAST_CASE(2, FastRecs)
@@ -1356,8 +1329,7 @@ bool step_one_launch_fits(int32_t nrep, uint32_t ipg, uint32_t kv_per_group) {
 hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
                              const mpx_group_batch* b, uint32_t* worklist, uint32_t* wcount,
                              int64_t* totals, uint32_t* err, hipStream_t stream,
-                             hipEvent_t ev0, hipEvent_t ev1, unsigned long long* pslots,
-                             unsigned long long* span) {
+                             hipEvent_t ev0, hipEvent_t ev1, unsigned long long* pslots) {
     if (!b->n_groups)
         return totals ? hipMemsetAsync(totals, 0, 3 * sizeof(int64_t), stream) : hipSuccess;
     if (kv_per_group > (uint32_t)kDCap) return hipErrorInvalidValue;
@@ -1365,10 +1337,10 @@ hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group,
     if (pslots && !step_one_launch_fits(nrep, b->ipg, kv_per_group)) return hipErrorInvalidValue;
     if (mode == MPX_MODE_MIN)
         launch_step<MPX_MODE_MIN>(b, nrep, kv_per_group, worklist, wcount, totals, err, stream,
-                                  ev0, ev1, pslots, span);
+                                  ev0, ev1, pslots);
     else
         launch_step<MPX_MODE_CLASSIC>(b, nrep, kv_per_group, worklist, wcount, totals, err,
-                                      stream, ev0, ev1, pslots, span);
+                                      stream, ev0, ev1, pslots);
     return hipGetLastError();
 }
 

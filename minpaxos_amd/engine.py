@@ -533,14 +533,6 @@ class Engine:
         """record ev0 / ev1 around the fast kernel of every later group step (None: off)"""
         self._check(self.lib.mpx_group_step_events(self.h, ev0, ev1), "mpx_group_step_events")
 
-    def group_step_clock(self, span_ptr=None):
-        """the fast kernel of every later group step writes its start / ~end ticks to the two
-        uint64 at device pointer span_ptr (None: off); returns the clock rate in kHz"""
-        khz = C.c_int64(0)
-        self._check(self.lib.mpx_group_step_clock(self.h, span_ptr, C.byref(khz)),
-                    "mpx_group_step_clock")
-        return khz.value
-
     def event_destroy(self, ev):
         self._check(self.lib.mpx_event_destroy(self.h, ev), "mpx_event_destroy")
 

@@ -101,24 +101,4 @@ assert PREPARE_EFFECT.itemsize == 8
 APPLY_AUTO, APPLY_SORTED, APPLY_PARTITIONED, APPLY_SMALL = 0, 1, 2, 3
 APPLY_NO_HOT = 0xFFFFFFFF
 FLAG_STEP_ONE_LAUNCH = 1  # mpx_config.flags: one kernel per group step (mpx.h)
-
-# mpx_group_step_clock's buffer (mpx.h): word 0 = the fast kernel's start tick, word
-# STEP_CLOCK_LINE * i (i = 1..STEP_CLOCK_ENDS) = ~(end tick) over a share of its workgroups
-STEP_CLOCK_LINE = 16
-STEP_CLOCK_ENDS = 255
-STEP_CLOCK_WORDS = STEP_CLOCK_LINE * (STEP_CLOCK_ENDS + 1)
-
-
-def step_clock_ticks(words):
-    """the fast kernel's span in clock ticks from one step's mpx_group_step_clock buffer (a
-    uint64 array of STEP_CLOCK_WORDS, 0xFF-filled before the step); raises if the kernel did
-    not write it"""
-    import numpy as np
-    w = np.asarray(words, dtype=np.uint64)
-    start = int(w[0])
-    ends = ~w[STEP_CLOCK_LINE::STEP_CLOCK_LINE][:STEP_CLOCK_ENDS]  # unwritten shares: 0
-    end = int(ends.max())
-    if start == (1 << 64) - 1 or end == 0 or end < start:
-        raise RuntimeError("the step's fast kernel left its clock span unwritten")
-    return end - start
 APPLY_SMALL_MAX = 16384

@@ -139,13 +139,6 @@ int main() {
     CHECK(mpx_step_totals_dev(e, &gb, tot, nullptr) == MPX_OK);
     gb.n_decided = nullptr;
     FAILS(e, mpx_step_totals_dev(e, &gb, tot, nullptr), MPX_E_INVAL);
-    // the clock hook: set, report the rate, clear
-    std::vector<uint64_t> span_buf(MPX_STEP_CLOCK_WORDS);
-    uint64_t* span = span_buf.data();
-    int64_t khz = 0;
-    CHECK(mpx_group_step_clock(nullptr, span, &khz) == MPX_E_INVAL);
-    CHECK(mpx_group_step_clock(e, span, &khz) == MPX_OK && khz > 0);
-    CHECK(mpx_group_step_clock(e, nullptr, nullptr) == MPX_OK);
 
     // collectives
     int32_t wm[4] = {1, 2, 3, 4};

@@ -23,7 +23,6 @@
 #include <time.h>
 #include <unistd.h>
 
-#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -107,13 +106,6 @@ int stub_devices() {
 extern "C" {
 hipError_t hipSetDevice(int d) { return d >= 0 && d < stub_devices() ? hipSuccess : hipErrorInvalidDevice; }
 hipError_t hipGetDeviceCount(int* c) { *c = stub_devices(); return hipSuccess; }
-// the constant-rate clock mpx_group_step_clock reports: 100 MHz, as on the GPU
-hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t a, int d) {
-    if (d < 0 || d >= stub_devices()) return hipErrorInvalidDevice;
-    if (a != hipDeviceAttributeWallClockRate) return hipErrorInvalidValue;
-    *v = 100000;
-    return hipSuccess;
-}
 hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned int) {
     *s = reinterpret_cast<hipStream_t>(malloc(8));
     return hipSuccess;
@@ -261,12 +253,8 @@ bool step_one_launch_fits(int32_t, uint32_t, uint32_t) { return true; }
 hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, uint32_t*, hipStream_t);
 hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group, const mpx_group_batch* b,
                              uint32_t*, uint32_t* ctl, int64_t* totals, uint32_t* err,
-                             hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, unsigned long long*,
-                             unsigned long long* span) {
+                             hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, unsigned long long*) {
     if (ev0) hipEventRecord(ev0, s);
-    // the kernel's clock span (100 MHz ticks), as the fast kernel's atomic mins leave it
-    auto tick = [] { return (unsigned long long)(now_s() * 1e8); };
-    if (span) span[0] = std::min(span[0], tick());
     // the fused form needs the per-group decided counts the oracle writes to n_decided
     std::vector<uint32_t> nd;
     mpx_group_batch bb = *b;
@@ -280,7 +268,6 @@ hipError_t launch_group_step(int mode, int32_t nrep, uint32_t kv_per_group, cons
     else if (rc == MPX_E_KV_FULL) *err |= kErrKvFull;
     else if (rc) *err |= kErrInval;
     if (ev1) hipEventRecord(ev1, s);
-    if (span) span[MPX_STEP_CLOCK_LINE] = std::min(span[MPX_STEP_CLOCK_LINE], ~tick());
     return totals ? launch_step_totals(&bb, totals, ctl, s) : hipSuccess;
 }
 // k_step_totals (step.hip) over host memory
@@ -305,7 +292,7 @@ hipError_t launch_step_totals(const mpx_group_batch* b, int64_t* totals, uint32_
 bool step_one_launch_fits(int32_t, uint32_t, uint32_t) { return true; }
 hipError_t launch_group_step(int, int32_t, uint32_t, const mpx_group_batch*, uint32_t*, uint32_t*,
                              int64_t*, uint32_t*, hipStream_t, hipEvent_t, hipEvent_t,
-                             unsigned long long*, unsigned long long*) { return hipSuccess; }
+                             unsigned long long*) { return hipSuccess; }
 hipError_t launch_step_totals(const mpx_group_batch*, int64_t*, uint32_t*, hipStream_t) { return hipSuccess; }
 #endif
 uint64_t apply_chunk_commands(uint64_t c, uint64_t m) { return c ? c : m; }

@@ -32,7 +32,7 @@ def test_library_exports_every_header_symbol():
                          text=True, check=True).stdout
     exported = set(re.findall(r"\bT (mpx_[a-z0-9_]+)", out))
     assert set(header_functions()) <= exported
-    assert lib.mpx_abi_version() == 9
+    assert lib.mpx_abi_version() == 8
 
 
 def test_no_device_calls_fail_cleanly():
@@ -109,22 +109,3 @@ def test_product_does_not_reference_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".hpp", "Makefile")):
                 assert "oracle" not in open(os.path.join(dp, f)).read().lower() or \
                     f == "__init__.py", f
-
-
-def test_step_clock_ticks():
-    """records.step_clock_ticks: the start word against the max over the ~end partials; a buffer
-    the kernel did not write raises"""
-    import numpy as np
-    import pytest
-    from minpaxos_amd import records as R
-    w = np.full(R.STEP_CLOCK_WORDS, np.uint64(2**64 - 1), dtype=np.uint64)
-    with pytest.raises(RuntimeError):
-        R.step_clock_ticks(w)
-    w[0] = 1000
-    w[R.STEP_CLOCK_LINE * 3] = ~np.uint64(1500)
-    w[R.STEP_CLOCK_LINE * 255] = ~np.uint64(1700)
-    w[R.STEP_CLOCK_LINE * 7 + 1] = 5  # not a partial word: ignored
-    assert R.step_clock_ticks(w) == 700
-    w[0] = 2000  # ends before the start
-    with pytest.raises(RuntimeError):
-        R.step_clock_ticks(w)

@@ -957,72 +957,6 @@ def test_group_step_one_launch(mk_engine, mode, G):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("one_launch", [False, True])
-def test_group_step_clock(mk_engine, one_launch):
-    """mpx_group_step_clock (what bench.py's roofline times): the fast kernel leaves its start
-    and end ticks in the buffer, the step's outputs stay the oracle's, a graph replay writes
-    the buffer each replay, the span sits inside an event bracket of the same step and costs
-    the kernel little (the same step without the hook, events around it), and the hook clears"""
-    from minpaxos_amd.devbuf import Arena
-    N, K, G = 5, 256, 8192
-    SW = R.STEP_CLOCK_WORDS
-    b = synth.group_batch(G, 256, N, 4, 256, seed=41)
-    b.setdefault("has_cmds", None)
-    e = mk_engine(N, R.MODE_MIN, kv_per_group=K, step_one_launch=one_launch)
-    want = Oracle(N, R.MODE_MIN, kv_per_group=K).group_step(b)
-    want_tot = _want_totals(b, want)
-    with Arena(e) as ar:
-        gb, d = _dev_group_batch(ar, b, N, K, True)
-        tot = ar.full(3, np.int64, 0)
-        span = ar.full(SW, np.uint64, 0xFF)
-        ev0, ev1 = e.event_create(), e.event_create()
-
-        def bracket(clock):
-            e.memset(span.ptr, 0xFF, 8 * SW, e.stream)
-            khz = e.group_step_clock(span.ptr if clock else None)
-            e.event_record(ev0, e.stream)
-            e.group_step_totals_dev(gb, tot.ptr, e.stream)
-            e.event_record(ev1, e.stream)
-            e.synchronize()
-            return khz, e.event_elapsed_ms(ev0, ev1)
-        for _ in range(2):
-            bracket(False)
-        _, plain = min(bracket(False) for _ in range(3))
-        khz, ev = min(bracket(True) for _ in range(3))
-        assert khz > 0
-        assert ar.get(tot).tolist() == want_tot
-        assert np.array_equal(ar.get(d["co"]), want["committed_out"])
-        assert np.array_equal(ar.get(d["st_out"]).view(np.int32), want["st_out"].view(np.int32))
-        ms = R.step_clock_ticks(ar.get(span)) / khz
-        assert 0 < ms <= ev + 0.01
-        assert ev <= plain * 1.1 + 0.01, (ev, plain)  # the hook's atomics cost the kernel little
-        s = e.stream_create()
-        e.graph_begin(s)
-        e.group_step_totals_dev(gb, tot.ptr, s)
-        g = e.graph_end(s)
-        try:
-            last = int(ar.get(span)[0])
-            for _ in range(2):
-                e.memset(span.ptr, 0xFF, 8 * SW, s)
-                e.graph_launch(g, s)
-                e.stream_synchronize(s)
-                w = ar.get(span)
-                assert int(w[0]) > last and 0 < R.step_clock_ticks(w) < khz * 1000
-                last = int(w[0])
-                assert ar.get(tot).tolist() == want_tot
-        finally:
-            e.graph_destroy(g)
-            e.stream_destroy(s)
-        e.group_step_clock()  # off: the buffer is left alone
-        e.memset(span.ptr, 0xFF, 8 * SW, e.stream)
-        e.group_step_dev(gb, e.stream)
-        e.synchronize()
-        assert (ar.get(span) == np.uint64(2**64 - 1)).all()
-        e.event_destroy(ev0)
-        e.event_destroy(ev1)
-
-
-@pytest.mark.gpu
 def test_group_step_graph_replay(mk_engine):
     """mpx_graph_begin / _end / _launch: a group step (+ its totals) captured on a stream and
     replayed from the graph three times gives the oracle's outputs and totals every time (the
