@@ -457,13 +457,21 @@ __device__ void fold_packed(unsigned long long* pslots, uint32_t n_groups, int64
     if (threadIdx.x < 3) totals[threadIdx.x] = (int64_t)fsum[threadIdx.x];
 }
 
-template <int MODE, class Cfg>
+// kOne: the one-launch step's instance (pslots / totals used); the two-launch step's instance has
+// them compiled out (pointers known null), so its code carries none of the fold's paths - code a
+// step never runs still costs the kernel through register allocation and scheduling (a dormant
+// timing hook cost 2.5-4 %)
+template <int MODE, class Cfg, bool kOne>
 __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int32_t nrep,
                                                          uint32_t kvpg, uint32_t* worklist,
                                                          uint32_t* wcount,
                                                          unsigned long long* tacc, uint32_t* err,
                                                          unsigned long long* pslots,
                                                          int64_t* totals) {
+    if constexpr (!kOne) {
+        pslots = nullptr;
+        totals = nullptr;
+    }
     MPX_FAST_CONSTS
     __shared__ FastLds<Cfg, MODE> S;
     STAMP_DECL
@@ -1275,8 +1283,12 @@ template <int MODE, class Cfg>
 void launch_fast(const mpx_group_batch* b, int32_t nrep, uint32_t kvpg, uint32_t* worklist,
                  uint32_t* wcount, unsigned long long* tacc, uint32_t* err, hipStream_t stream,
                  unsigned long long* pslots, int64_t* totals) {
-    k_group_fast<MODE, Cfg><<<b->n_groups, Cfg::kFT, 0, stream>>>(*b, nrep, kvpg, worklist, wcount,
-                                                                   tacc, err, pslots, totals);
+    if (pslots)
+        k_group_fast<MODE, Cfg, true><<<b->n_groups, Cfg::kFT, 0, stream>>>(
+            *b, nrep, kvpg, worklist, wcount, tacc, err, pslots, totals);
+    else
+        k_group_fast<MODE, Cfg, false><<<b->n_groups, Cfg::kFT, 0, stream>>>(
+            *b, nrep, kvpg, worklist, wcount, tacc, err, nullptr, nullptr);
 }
 // the smallest fast-path variant the batch's shape fits (0 = none: every group is general)
 int fast_variant(int32_t nrep, uint32_t ipg, uint32_t kvpg) {
