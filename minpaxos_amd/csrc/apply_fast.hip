@@ -595,6 +595,14 @@ __global__ __launch_bounds__(256) void k_ap_scan_rows(ApGeo g, uint32_t* __restr
 #ifndef MPX_EMIT_CPOS
 #define MPX_EMIT_CPOS 0
 #endif
+// MPX_SC_LAZYV=1: with hot keys in the chunk, a command's value is loaded only once the command is
+// known to be cold (after its hot-key probe, for the current tile), not prefetched for every
+// command: a skewed chunk's hot commands (~99 % under zipf) never need theirs in the scatter
+// (zipf 1.280 / 1.285 -> 1.256 / 1.246 ms per call, uniform unchanged - it has no hot keys and
+// keeps the prefetch; profiles/r05/apply/ab_lazyv_emit_persist.txt)
+#ifndef MPX_SC_LAZYV
+#define MPX_SC_LAZYV 1
+#endif
 struct ScatterLds {
     HotLds hl;
     uint32_t roff[kMaxBins];    // this tile's run start per bin (partition position)
@@ -629,6 +637,7 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
     // this tile's commands in registers; the next tile's are loaded while this one is ranked
     uint32_t o[kTPer];  // 32-bit: byte-packed ops make the compiler wait for the prefetch early
     int64_t k[kTPer], v[kTPer];
+    const bool lazy = MPX_SC_LAZYV && nh > 1;  // (uniform over the grid)
     auto load = [&](uint32_t tile, uint32_t* o_, int64_t* k_, int64_t* v_) {
 #pragma unroll
         for (int r = 0; r < kTPer; ++r) {
@@ -636,7 +645,7 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
             const bool in = tile < tw.end && j < n;
             o_[r] = in ? op[j] : 0;
             k_[r] = in ? key[j] : 0;
-            v_[r] = in ? val[j] : 0;
+            v_[r] = in && !lazy ? val[j] : 0;
         }
     };
     load(tw.tile, o, k, v);
@@ -667,6 +676,7 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
             const int hh = in ? hot_find(S.hl, nh, k[r], h) : -1;
             if (in && hh >= 0) ipos[j] = (uint16_t)(kHotIdx | (uint32_t)hh);
             cold[r] = in && hh < 0;
+            if (lazy && cold[r]) v[r] = val[j];  // (used after the scans below)
             bin[r] = cold[r] ? bin_of(h, g) : 0u;
             rank[r] = 0;
             if (!__ballot(cold[r])) continue;

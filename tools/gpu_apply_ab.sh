@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-apply_ab}; mkdir -p $OUT
 if [ -n "${PYTEST_K:-}" ]; then
-  timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_full.py tests/test_golden.py -m gpu -x -v --timeout 300 --timeout-method thread -k "$PYTEST_K" > $OUT/pytest.log 2>&1
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_full.py tests/test_golden.py tests/test_gpu_fuzz.py -m gpu -x -v --timeout 300 --timeout-method thread -k "$PYTEST_K" > $OUT/pytest.log 2>&1
   rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|error" $OUT/pytest.log | tail -3; [ $rc = 0 ] || exit $rc
 fi
 for d in ${DISTS:-uniform zipf}; do
