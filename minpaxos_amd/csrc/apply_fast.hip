@@ -32,7 +32,7 @@
 //                 prefetched); every record of a batch at once finds its slot and joins its slot's
 //                 list of the batch, then walks the list (or, for a slot with many records, reads
 //                 two bitmaps) for its predecessor and last earlier PUT; results stored in
-//                 partition order; touched slots written back once
+//                 partition order as 16-byte (ret, conf) records; touched slots written back once
 //   k_ap_hot_commit  the hot keys' final value and state
 //   k_ap_emit     per tile, log order: the tile's cold results gathered run by run into an LDS
 //                 image (each image position's run found by a binary search of the tile's run
@@ -793,6 +793,14 @@ __device__ __forceinline__ int64_t kv_lo_hi(int lo, int hi) {
 #ifndef MPX_RL_NT
 #define MPX_RL_NT 0
 #endif
+// MPX_RES16=1: a command's result travels from the resolve to the emit as ONE 16-byte record
+// (ret, conf) instead of an 8-byte ret and a separate conf byte: the emit's gather of the
+// tile's ~4-record runs is then one request per run instead of two, for 7 more bytes per
+// command written and read (uniform 2.09 -> 2.07 ms per call, zipf neutral;
+// profiles/r05/apply/ab_res16.txt)
+#ifndef MPX_RES16
+#define MPX_RES16 1
+#endif
 // diagnostic build: wave 0's clock per phase of k_ap_resolve_list, printed by bin 0
 #ifndef MPX_RL_STAMP
 #define MPX_RL_STAMP 0
@@ -1232,7 +1240,11 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                     // does not wait for them)
                     const uint32_t dst = (cl[hh] & 1u) ? base + i : spare;
                     if (!(MPX_RS_ABL & 2)) {
-#if MPX_RL_NT
+#if MPX_RES16
+                        reinterpret_cast<int4*>(r_ret)[dst] =
+                            make_int4((int)(uint32_t)ret, (int)(uint32_t)((uint64_t)ret >> 32),
+                                      conf ? 1 : 0, 0);
+#elif MPX_RL_NT
                         st_stream(r_ret + dst, ret);
                         st_stream(r_conf + dst, (uint8_t)(conf ? 1 : 0));
 #else
@@ -1429,8 +1441,14 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
 #pragma unroll
         for (int u = 0; u < kTPer; ++u) {
             const uint32_t i = tid + u * kTT;
+#if MPX_RES16
+            const int4 rr = i < nc ? reinterpret_cast<const int4*>(r_ret)[q[u]] : make_int4(0, 0, 0, 0);
+            x[u] = kv_lo_hi(rr.x, rr.y);
+            c[u] = (uint8_t)rr.z;
+#else
             x[u] = i < nc ? r_ret[q[u]] : 0;
             c[u] = i < nc ? r_conf[q[u]] : 0;
+#endif
         }
 #pragma unroll
         for (int u = 0; u < kTPer; ++u) {
@@ -1498,8 +1516,14 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
 #pragma unroll
         for (int u = 0; u < kTPer; ++u) {
             const uint32_t i = tid + u * kTT;
+#if MPX_RES16
+            const int4 rr = i < nc ? reinterpret_cast<const int4*>(r_ret)[q[u]] : make_int4(0, 0, 0, 0);
+            xr[u] = kv_lo_hi(rr.x, rr.y);
+            c[u] = (uint8_t)rr.z;
+#else
             xr[u] = i < nc ? r_ret[q[u]] : 0;
             c[u] = i < nc ? r_conf[q[u]] : 0;
+#endif
         }
 #pragma unroll
         for (int u = 0; u < kTPer; ++u) {
@@ -1627,8 +1651,8 @@ FastLayout fast_layout(const KvTable& t, uint64_t c) {
     L.ipos = o; o += al(c * 2);
     L.cpos = o; o += al(((uint64_t)g.tiles * kTL + 1) * 4);
     L.tcold = o; o += al((uint64_t)g.tiles * 4);
-    L.r_ret = o; o += al((c + 1) * 8);  // (+ the spare result: see k_ap_resolve_list)
-    L.r_conf = o; o += al(c + 1);
+    L.r_ret = o; o += al((c + 1) * (MPX_RES16 ? 16 : 8));  // (+ the spare result: see k_ap_resolve_list)
+    L.r_conf = o; o += MPX_RES16 ? 0 : al(c + 1);
     L.hot = o; o += al(sizeof(ApHot));
     L.total = o;
     return L;
