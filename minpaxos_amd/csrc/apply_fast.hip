@@ -32,7 +32,7 @@
 //                 prefetched); every record of a batch at once finds its slot and joins its slot's
 //                 list of the batch, then walks the list (or, for a slot with many records, reads
 //                 two bitmaps) for its predecessor and last earlier PUT; results stored in
-//                 partition order as 16-byte (ret, conf) records; touched slots written back once
+//                 partition order; touched slots written back once
 //   k_ap_hot_commit  the hot keys' final value and state
 //   k_ap_emit     per tile, log order: the tile's cold results gathered run by run into an LDS
 //                 image (each image position's run found by a binary search of the tile's run
@@ -797,9 +797,10 @@ __device__ __forceinline__ int64_t kv_lo_hi(int lo, int hi) {
 // (ret, conf) instead of an 8-byte ret and a separate conf byte: the emit's gather of the
 // tile's ~4-record runs is then one request per run instead of two, for 7 more bytes per
 // command written and read (uniform 2.09 -> 2.07 ms per call, zipf neutral;
-// profiles/r05/apply/ab_res16.txt)
+// profiles/r05/apply/ab_res16.txt). OFF by default: the padding costs 0.93 GB of HBM traffic
+// per uniform call (7.40 vs 6.47 GB, 4.16 x the algorithmic bytes instead of 3.64 x) for 1 %
 #ifndef MPX_RES16
-#define MPX_RES16 1
+#define MPX_RES16 0
 #endif
 // diagnostic build: wave 0's clock per phase of k_ap_resolve_list, printed by bin 0
 #ifndef MPX_RL_STAMP
