@@ -415,7 +415,9 @@ int mpx_group_step_totals_dev(mpx_engine* eng, const mpx_group_batch* b, int64_t
 /* timing hook (ABI 7): every later group step of the handle records ev_fast_start right before
  * and ev_fast_end right after the launch of its first kernel (the per-group fast kernel, or the
  * work-list fill), on the call's stream, so the pair brackets that kernel alone (the work-list
- * kernel that follows is outside). Both NULL turns it off. Events from mpx_event_create.    */
+ * kernel that follows is outside). Both NULL turns it off. Events from mpx_event_create;
+ * they must stay alive while registered - mpx_event_destroy of either one unregisters the
+ * pair (the hook is then off, as after NULL, NULL).                                           */
 int mpx_group_step_events(mpx_engine* eng, void* ev_fast_start, void* ev_fast_end);
 
 /* ---- multi-GPU: the one collective (RCCL over xGMI) -------------------------------------

@@ -52,11 +52,6 @@ namespace mpx {
 #ifndef MPX_RS_ABL
 #define MPX_RS_ABL 0
 #endif
-// diagnostic ablations of k_ap_scatter: 1 no partition writes, 2 no image either, 4 bin ranks
-// from ballots (match_bits) instead of the LDS peer masks
-#ifndef MPX_SC_ABL
-#define MPX_SC_ABL 0
-#endif
 
 constexpr int kTL = 4096;          // commands per log tile
 constexpr int kTT = 1024;          // threads of the tile and bin workgroups
@@ -387,81 +382,6 @@ __global__ __launch_bounds__(kTT) void k_ap_select(KvTable t, const int64_t* __r
     }
 }
 
-// ---- per-tile counts --------------------------------------------------------------------------
-// persistent (kCountGrid workgroups, XCD-contiguous tiles): the hot table is built once per
-// workgroup, and the next tile's keys load while this one is counted
-constexpr unsigned kCountGrid = 512;  // two 1024-thread workgroups per CU
-__global__ __launch_bounds__(kTT) void k_ap_count(ApGeo g, const uint8_t* __restrict__ op,
-                                                  const int64_t* __restrict__ key, uint32_t n,
-                                                  uint32_t* __restrict__ rows,
-                                                  const ApHot* __restrict__ hot) {
-    __shared__ HotLds hl;
-    __shared__ uint32_t hist[kMaxBins];
-    __shared__ uint32_t ha[kHMax], hp[kHMax];
-    const int tid = threadIdx.x;
-    const uint32_t nh = hot->n;
-    const TileWalk tw = tile_walk(g.tiles);
-    int64_t k[kTPer];
-    uint32_t o[kTPer];  // ops: loaded up front when hot keys exist, else only for INT64_MIN keys
-    auto load = [&](uint32_t tile) {
-        const uint32_t j0 = tile * (uint32_t)kTL;
-#pragma unroll
-        for (int u = 0; u < kTPer; ++u) {
-            const uint32_t j = j0 + u * kTT + tid;
-            const bool in = tile < tw.end && j < n;
-            k[u] = in ? key[j] : 0;
-            o[u] = in && nh > 1 ? op[j] : 0u;
-        }
-    };
-    load(tw.tile);  // in flight while the hot table is built (its key loads and barriers)
-    hot_build(hl, hot, nh);
-    const int l = lane_id();
-    for (uint32_t tile = tw.tile; tile < tw.end; tile += tw.step) {
-        for (uint32_t b = tid; b < g.nbin; b += kTT) hist[b] = 0;
-        if (tid < kHMax) {
-            ha[tid] = 0;
-            hp[tid] = 0;
-        }
-        __syncthreads();
-        const uint32_t j0 = tile * (uint32_t)kTL;
-        uint64_t h[kTPer];
-        int hh[kTPer];
-#pragma unroll
-        for (int u = 0; u < kTPer; ++u) {
-            const uint32_t j = j0 + u * kTT + tid;
-            h[u] = hash64((uint64_t)k[u]);
-            hh[u] = j < n ? hot_find(hl, nh, k[u], h[u]) : -1;
-        }
-        uint32_t oc[kTPer];
-#pragma unroll
-        for (int u = 0; u < kTPer; ++u) oc[u] = o[u];
-        load(tile + tw.step);  // the next tile's keys, while this one is counted
-#pragma unroll
-        for (int u = 0; u < kTPer; ++u) {
-            const uint32_t j = j0 + u * kTT + tid;
-            const bool in = j < n;
-            if (in && hh[u] < 0) atomicAdd(&hist[bin_of(h[u], g)], 1u);
-            const bool hotc = in && hh[u] >= 0;
-            if (!__ballot(hotc)) continue;
-            if (nh <= 1 && hotc) oc[u] = op[j];
-            // per hot key of the round: its last command and its last PUT, one LDS atomic each
-            const bool put = hotc && oc[u] == MPX_OP_PUT;
-            const unsigned long long peers = match_bits((uint32_t)hh[u], kLgHMax, hotc);
-            const unsigned long long puts = peers & __ballot(put);
-            if (hotc && hi_bit(peers) == l) atomicMax(&ha[hh[u]], j + 1);
-            if (put && hi_bit(puts) == l) atomicMax(&hp[hh[u]], j + 1);
-        }
-        __syncthreads();
-        uint32_t* row = rows + (uint64_t)tile * g.rowlen;
-        for (uint32_t b = tid; b < g.nbin; b += kTT) row[b] = hist[b];
-        if (tid < kHMax) {
-            row[g.nbin + 2 * tid] = ha[tid];
-            row[g.nbin + 2 * tid + 1] = hp[tid];
-        }
-        __syncthreads();
-    }
-}
-
 // ---- scan of the tile rows: columns < nbin exclusive sums, the rest exclusive maxima ----------
 __device__ __forceinline__ uint32_t col_op(bool sum, uint32_t a, uint32_t b) {
     return sum ? a + b : (a > b ? a : b);
@@ -589,12 +509,6 @@ __global__ __launch_bounds__(256) void k_ap_scan_rows(ApGeo g, uint32_t* __restr
 }
 
 // ---- partition ----------------------------------------------------------------------------------
-// MPX_EMIT_CPOS=1 (A/B builds): the scatter stores each image position's partition slot (4 B per
-// command) for the emit; the default has the emit derive them from the scanned rows (the tile's
-// run start per bin, and the next tile's as its end)
-#ifndef MPX_EMIT_CPOS
-#define MPX_EMIT_CPOS 0
-#endif
 // MPX_SC_LAZYV=1: with hot keys in the chunk, a command's value is loaded only once the command is
 // known to be cold (after its hot-key probe, for the current tile), not prefetched for every
 // command: a skewed chunk's hot commands (~99 % under zipf) never need theirs in the scatter
@@ -605,25 +519,31 @@ __global__ __launch_bounds__(256) void k_ap_scan_rows(ApGeo g, uint32_t* __restr
 #endif
 struct ScatterLds {
     HotLds hl;
-    uint32_t roff[kMaxBins];    // this tile's run start per bin (partition position)
     uint32_t lstart[kMaxBins];  // bin start inside the tile image
     uint16_t cw[kTW][kMaxBins]; // per-wave counts -> exclusive prefix over the waves
     uint8_t W[kTW][kMaxBins];
     unsigned long long PM[kTW][kWave];
     int4 img[kTL];              // bin-sorted records of the tile's cold commands
-    uint16_t ibin[kTL];
+    uint32_t ha[kHMax], hp[kHMax];  // per hot key: 1 + chunk position of its last command / PUT
     uint32_t wsum[kTW];
     uint32_t ncold;
 };
 
+// Per 4096-command log tile (persistent, one workgroup per CU, XCD-contiguous tiles, the next
+// tile's commands loaded while this one is ranked): the cold commands' stable ranks per bin
+// (per-wave LDS peer masks + per-wave counts, prefix over the waves), a bin-sorted image of their
+// 16-byte records in LDS, stored out WHOLE at the tile's own place (img[tile * kTL ...]: every
+// store coalesced), plus the tile's row: per bin its count (rows, scanned afterwards into the
+// runs' partition offsets) and its image start (lrow), per hot key its last command and last PUT
+// in the tile. Per command its image index (ipos, log order; hot: kHotIdx | hot index).
 __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __restrict__ op,
                                                     const int64_t* __restrict__ key,
                                                     const int64_t* __restrict__ val, uint32_t n,
-                                                    const uint32_t* __restrict__ rows,
+                                                    uint32_t* __restrict__ rows,
+                                                    uint16_t* __restrict__ lrow,
                                                     const ApHot* __restrict__ hot,
-                                                    int4* __restrict__ rec_kv, uint32_t spare,
+                                                    int4* __restrict__ img,
                                                     uint16_t* __restrict__ ipos,
-                                                    uint32_t* __restrict__ cpos,
                                                     uint32_t* __restrict__ tcold) {
     __shared__ ScatterLds S;
     const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
@@ -631,6 +551,7 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
     uint32_t* cw32 = reinterpret_cast<uint32_t*>(&S.cw[0][0]);
     for (int i = tid; i < kTW * kMaxBins / 2; i += kTT) cw32[i] = 0u;
     S.PM[w][l] = 0ull;
+    if (tid < kHMax) S.ha[tid] = S.hp[tid] = 0u;
     hot_build(S.hl, hot, nh);
     TileWalk tw = tile_walk(g.tiles);
     const uint32_t wofs = (uint32_t)w * (kWave * kTPer) + (uint32_t)l;
@@ -649,10 +570,6 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
         }
     };
     load(tw.tile, o, k, v);
-    auto load_roff = [&](uint32_t tile) {
-        return tile < tw.end && (uint32_t)tid < g.nbin ? rows[(uint64_t)tile * g.rowlen + tid] : 0u;
-    };
-    uint32_t roff_cur = load_roff(tw.tile);
     lds_u8* W = (lds_u8*)&S.W[w][0];
     lds_u64* PM = (lds_u64*)&S.PM[w][0];
     lds_u16* CW = (lds_u16*)&S.cw[w][0];
@@ -663,7 +580,6 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
         uint32_t no[kTPer];
         int64_t nk[kTPer], nv[kTPer];
         load(tile + tw.step, no, nk, nv);
-        const uint32_t roff_nxt = load_roff(tile + tw.step);
         uint32_t bin[kTPer], rank[kTPer];
         uint64_t hs[kTPer];  // the keys' hashes: the records carry them instead of the keys
         bool cold[kTPer];
@@ -674,15 +590,22 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
             const uint64_t h = hash64((uint64_t)k[r]);
             hs[r] = h;
             const int hh = in ? hot_find(S.hl, nh, k[r], h) : -1;
-            if (in && hh >= 0) ipos[j] = (uint16_t)(kHotIdx | (uint32_t)hh);
+            const bool hotc = in && hh >= 0;
+            if (hotc) ipos[j] = (uint16_t)(kHotIdx | (uint32_t)hh);
             cold[r] = in && hh < 0;
             if (lazy && cold[r]) v[r] = val[j];  // (used after the scans below)
+            if (__ballot(hotc)) {
+                // per hot key of the round: its last command and its last PUT, one LDS atomic each
+                const bool put = hotc && o[r] == MPX_OP_PUT;
+                const unsigned long long peers = match_bits((uint32_t)hh, kLgHMax, hotc);
+                const unsigned long long puts = peers & __ballot(put);
+                if (hotc && hi_bit(peers) == l) atomicMax(&S.ha[hh], j + 1);
+                if (put && hi_bit(puts) == l) atomicMax(&S.hp[hh], j + 1);
+            }
             bin[r] = cold[r] ? bin_of(h, g) : 0u;
             rank[r] = 0;
             if (!__ballot(cold[r])) continue;
-            const unsigned long long peers = (MPX_SC_ABL & 4)
-                                                 ? match_bits(bin[r], 31 - __clz((int)g.nbin), cold[r])
-                                                 : wave_peers(W, PM, bin[r], cold[r]);
+            const unsigned long long peers = wave_peers(W, PM, bin[r], cold[r]);
             if (cold[r]) {
                 const uint32_t base = CW[bin[r]];
                 rank[r] = base + (uint32_t)__popcll(peers & below);
@@ -691,6 +614,7 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
         }
         __syncthreads();
         // per bin: exclusive prefix over the waves, the tile's count per bin
+        uint32_t* row = rows + (uint64_t)tile * g.rowlen;
         for (uint32_t b = tid; b < g.nbin; b += kTT) {
             uint32_t x[kTW];  // all loads first: the stores below may alias them
 #pragma unroll
@@ -702,11 +626,16 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
                 s += x[w2];
             }
             S.lstart[b] = s;
+            row[b] = s;
+        }
+        if (tid < kHMax) {
+            row[g.nbin + 2 * tid] = S.ha[tid];
+            row[g.nbin + 2 * tid + 1] = S.hp[tid];
+            S.ha[tid] = S.hp[tid] = 0u;  // (read above by this thread only)
         }
         __syncthreads();
         {  // exclusive scan of the counts over the bins (nbin <= 1024: one per thread)
             const uint32_t c = (uint32_t)tid < g.nbin ? S.lstart[tid] : 0u;
-            const uint32_t ro = roff_cur;
             uint32_t x = c;
 #pragma unroll
             for (int d = 1; d < kWave; d <<= 1) {
@@ -719,39 +648,32 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
             for (int w2 = 0; w2 < w; ++w2) wb += S.wsum[w2];
             if ((uint32_t)tid < g.nbin) {
                 S.lstart[tid] = wb + x - c;
-                S.roff[tid] = ro;
+                lrow[(uint64_t)tile * g.nbin + tid] = (uint16_t)(wb + x - c);
             }
             if (tid == kTT - 1) S.ncold = wb + x;
         }
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < kTPer; ++r) {
-            if (!cold[r] || (MPX_SC_ABL & 2)) continue;
+            if (!cold[r]) continue;
             const uint32_t b = bin[r];
             const uint32_t wr = S.cw[w][b] + rank[r];
             const uint32_t ip = S.lstart[b] + wr;
             const uint64_t x = rec_pack(hs[r], op_class(o[r]));
             S.img[ip] = make_int4((int)(uint32_t)x, (int)(uint32_t)(x >> 32),
                                   (int)(uint32_t)v[r], (int)(uint32_t)((uint64_t)v[r] >> 32));
-            S.ibin[ip] = (uint16_t)b;
             ipos[j0 + r * kWave] = (uint16_t)ip;
         }
         __syncthreads();
-        const uint32_t nc = (MPX_SC_ABL & 3) ? 0u : S.ncold;
+        // the image out whole: a wave stores its 64 slots when any of them holds a record (the
+        // slots past the tile's cold commands are the tile's own, never read)
+        const uint32_t nc = S.ncold;
         if (tid == 0) tcold[tile] = nc;
-        // A fixed number of stores per thread (positions past the tile's cold commands store to
-        // the spare record past the chunk): the wait for the next tile's records, loaded before
-        // them, can then count them (with a variable count it waited for every store of the tile)
+        int4* dst = img + (uint64_t)tile * kTL;
 #pragma unroll
         for (int u = 0; u < kTPer; ++u) {
             const uint32_t i = tid + u * kTT;
-            const bool live = i < nc;
-            const uint32_t ic = live ? i : 0u;
-            const uint32_t b = S.ibin[ic];
-            const uint32_t dst = live ? S.roff[b] + (i - S.lstart[b]) : spare;
-            if (!(MPX_SC_ABL & 32)) rec_kv[dst] = S.img[ic];
-            if (MPX_EMIT_CPOS && !(MPX_SC_ABL & 16))
-                cpos[live ? (uint64_t)tile * kTL + i : (uint64_t)g.tiles * kTL] = dst;  // emit gathers run by run
+            if (i - (uint32_t)l < nc) dst[i] = S.img[i];
         }
         for (int i = tid; i < kTW * kMaxBins / 2; i += kTT) cw32[i] = 0u;  // next tile's counts
         __syncthreads();
@@ -761,7 +683,37 @@ __global__ __launch_bounds__(kTT) void k_ap_scatter(ApGeo g, const uint8_t* __re
             k[r] = nk[r];
             v[r] = nv[r];
         }
-        roff_cur = roff_nxt;
+    }
+}
+
+// The bin-major run table of the resolve: for bin b and tile t, run (t, b) = the tile's records of
+// bin b, at partition positions [roff(t, b), roff(t + 1, b)) (the scanned rows; the bin's end
+// after the last tile) and at image positions tile * kTL + lrow(t, b) + ...: runs[b][t] = {roff,
+// image start - roff} (so a partition position q of the run lives at img[q + .y], 32-bit wrap).
+// A transpose through LDS: 64 tiles x 64 bins per 256-thread workgroup.
+constexpr int kRunT = 64, kRunB = 64;
+__global__ __launch_bounds__(256) void k_ap_runs(ApGeo g, const uint32_t* __restrict__ rows,
+                                                 const uint16_t* __restrict__ lrow,
+                                                 uint2* __restrict__ runs) {
+    __shared__ uint2 T[kRunB][kRunT + 1];
+    const uint32_t t0 = blockIdx.x * kRunT, b0 = blockIdx.y * kRunB;
+    const int tid = threadIdx.x;
+    // read: 4 tiles x 64 bins per pass (lane = bin)
+    for (int u = tid; u < kRunT * kRunB; u += 256) {
+        const uint32_t tt = (uint32_t)u / kRunB, bb = (uint32_t)u % kRunB;
+        const uint32_t t = t0 + tt, b = b0 + bb;
+        if (t < g.tiles && b < g.nbin) {
+            const uint32_t ro = rows[(uint64_t)t * g.rowlen + b];
+            const uint32_t ls = lrow[(uint64_t)t * g.nbin + b];
+            T[bb][tt] = make_uint2(ro, t * (uint32_t)kTL + ls - ro);
+        }
+    }
+    __syncthreads();
+    // write: 4 bins x 64 tiles per pass (lane = tile)
+    for (int u = tid; u < kRunT * kRunB; u += 256) {
+        const uint32_t bb = (uint32_t)u / kRunT, tt = (uint32_t)u % kRunT;
+        const uint32_t t = t0 + tt, b = b0 + bb;
+        if (t < g.tiles && b < g.nbin) runs[(uint64_t)b * g.tiles + t] = T[bb][tt];
     }
 }
 
@@ -802,6 +754,13 @@ __device__ __forceinline__ int64_t kv_lo_hi(int lo, int hi) {
 #ifndef MPX_RES16
 #define MPX_RES16 0
 #endif
+// MPX_RES_IMG=1: the resolve stores each result at its record's IMAGE position (the tile's own
+// slots, the runs of the records' gather), so the emit reads its tile's results in one
+// contiguous run instead of gathering them run by run from partition order
+#ifndef MPX_RES_IMG
+#define MPX_RES_IMG 1
+#endif
+static_assert(!(MPX_RES_IMG && MPX_RES16), "one result layout");
 // diagnostic build: wave 0's clock per phase of k_ap_resolve_list, printed by bin 0
 #ifndef MPX_RL_STAMP
 #define MPX_RL_STAMP 0
@@ -825,6 +784,7 @@ constexpr uint32_t kLIdx = 13;            // bits of 1 + a batch index
 constexpr uint32_t kLIdxMask = (1u << kLIdx) - 1u;
 constexpr uint32_t kLTagMax = (1u << (32 - kLIdx)) - 1u;
 constexpr uint32_t kFOverflow = 4u;
+constexpr int kLWin = kLT;                // tiles of the run window (one per thread)
 static_assert(kLB < (1 << kLIdx) && kLB <= 0x7FFF, "links hold 1 + a batch index below the PUT bit");
 
 // A slot with more than kLHeavyMin records in a batch (a warm key: walking its list would cost
@@ -854,6 +814,12 @@ struct ListLds {
     uint32_t hslot[kLHeavy];
     uint32_t nheavy[2];
     uint32_t flags;
+    // the run window: tiles [wt0, wt0 + kLWin) of the bin's run table, their runs' partition
+    // starts (wr[kLWin]: the start of the run after the window, the bin's end past the last
+    // tile) and image offsets; per batch parity the image position of every record (P)
+    uint32_t wr[kLWin + 1];
+    uint32_t wd[kLWin];
+    uint32_t P[2][kLB];
 #if MPX_RL_STAMP
     unsigned long long rph[8];
 #endif
@@ -861,7 +827,8 @@ struct ListLds {
 
 __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                                                          const uint32_t* __restrict__ bin_start,
-                                                         const int4* __restrict__ rec_kv,
+                                                         const uint2* __restrict__ runs,
+                                                         const int4* __restrict__ img,
                                                          int64_t* __restrict__ r_ret,
                                                          uint8_t* __restrict__ r_conf, uint32_t spare,
                                                          ApHot* hot, uint32_t* err) {
@@ -877,6 +844,45 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
     // the LDS table holds hashes; a free slot holds the hash of INT64_MIN (the sentinel key,
     // which never reaches a bin: it is always hot index 0)
     const int64_t kHS = (int64_t)hash64((uint64_t)kSentinel);
+    // The bin's records in partition order are its runs (one per tile, bin-major run table):
+    // partition position q of run u lives at img[q + wd[u]]. A batch's image positions are
+    // written into P by the window's tiles (a run longer than 32 records of the batch by its
+    // wave); a batch past the window's last run moves the window on (workgroup-uniform).
+    const uint2* brun = runs + (uint64_t)bin * g.tiles;
+    uint32_t wt0 = 0;
+    auto load_win = [&](uint32_t t0) {  // (every thread; the caller's barrier publishes it)
+        wt0 = t0;
+        for (uint32_t u = tid; u <= (uint32_t)kLWin; u += kLT) {
+            const uint32_t tt = t0 + u;
+            const uint2 x = tt < g.tiles ? brun[tt] : make_uint2(r1, 0u);
+            S.wr[u] = x.x;
+            if (u < (uint32_t)kLWin) S.wd[u] = x.y;
+        }
+    };
+    auto expand = [&](uint32_t base, uint32_t* Pb) {  // every thread (barriers inside)
+        const uint32_t end = base + kLB < r1 ? base + kLB : r1;
+        for (;;) {
+            for (uint32_t u = tid; u < (uint32_t)kLWin; u += kLT) {
+                const uint32_t ra = S.wr[u], re = S.wr[u + 1], d = S.wd[u];
+                const uint32_t a = ra > base ? ra : base, e = re < end ? re : end;
+                const bool lng = e > a + 32;
+                if (!lng)
+                    for (uint32_t q = a; q < e; ++q) Pb[q - base] = q + d;
+                unsigned long long m = __ballot(lng);
+                while (m) {
+                    const int src = __ffsll((long long)m) - 1;
+                    m &= m - 1;
+                    const uint32_t A = (uint32_t)__shfl((int)a, src), E = (uint32_t)__shfl((int)e, src);
+                    const uint32_t D = (uint32_t)__shfl((int)d, src);
+                    for (uint32_t q = A + (uint32_t)l; q < E; q += kWave) Pb[q - base] = q + D;
+                }
+            }
+            if (S.wr[kLWin] >= end) break;
+            __syncthreads();  // the window is read
+            load_win(wt0 + kLWin);
+            __syncthreads();
+        }
+    };
     for (uint32_t sub = 0; sub < nsub; ++sub) {
         const uint64_t gbase = ((((uint64_t)bin << g.lgsub) | sub) * bpb) * kSB;
         auto member = [&](uint64_t h) {
@@ -908,8 +914,16 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
             __syncthreads();
             if (mode == 1) {  // two-pass form: every PUT key of the bin first
                 if (tid == 0) atomicAdd(&hot->restarts, 1u);
-                for (uint32_t q = r0 + tid; q < r1; q += kLT) {
-                    const int4 kv = rec_kv[q];
+                for (uint32_t q = 0, tt = tid, qe = 0, d = 0;; ++q) {  // thread: tiles tid + kLT k
+                    while (q >= qe && tt < g.tiles) {  // the next nonempty run of this thread
+                        const uint2 x = brun[tt];
+                        qe = tt + 1 < g.tiles ? brun[tt + 1].x : r1;
+                        q = x.x;
+                        d = x.y;
+                        tt += kLT;
+                    }
+                    if (q >= qe) break;
+                    const int4 kv = img[q + d];
                     const uint64_t x = (uint64_t)kv_lo_hi(kv.x, kv.y);
                     if ((uint32_t)(x >> 62) != kClsPut) continue;
                     const uint64_t h = rec_hash(x, bin, g);
@@ -934,11 +948,19 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                 }
                 __syncthreads();
             }
+            __syncthreads();  // (the pre-insert loop's window use is over)
+            load_win(0);
+            __syncthreads();
+            expand(r0, S.P[1]);
+            __syncthreads();
             int4 kv[kLPer];
+            {
+                const uint32_t nb1 = r1 - r0 < (uint32_t)kLB ? r1 - r0 : (uint32_t)kLB;
 #pragma unroll
-            for (int hh = 0; hh < kLPer; ++hh) {
-                const uint32_t q = r0 + hh * kLT + tid;
-                kv[hh] = rec_kv[q < r1 ? q : r1 - 1];
+                for (int hh = 0; hh < kLPer; ++hh) {
+                    const uint32_t i = hh * kLT + tid;
+                    kv[hh] = img[S.P[1][i < nb1 ? i : nb1 - 1]];
+                }
             }
             uint32_t tag = 0;
 #if MPX_RL_STAMP
@@ -1083,15 +1105,23 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                         if (hx < (uint32_t)kLHeavy) S.hslot[hx] = (uint32_t)sl[hh];
                     }
                 }
-                // the next batch's records load while this one resolves
-#pragma unroll
-                for (int hh = 0; hh < kLPer; ++hh) {  // (clamped, not guarded: no branch)
-                    const uint32_t q = base + kLB + hh * kLT + tid;
-                    kv[hh] = rec_kv[q < r1 ? q : r1 - 1];
-                }
+                // the next batch's image positions (batch parity par ^ 1: the one this batch
+                // was loaded through is read no more), then its records load while this one
+                // resolves
+                const bool more = base + kLB < r1;  // (uniform)
+                RL_STAMP(6);
+                if (more) expand(base + kLB, S.P[par ^ 1u]);
                 RL_STAMP(0);
                 __syncthreads();
                 RL_STAMP(1);
+                if (more) {
+                    const uint32_t nb1 = r1 - (base + kLB) < (uint32_t)kLB ? r1 - (base + kLB) : (uint32_t)kLB;
+#pragma unroll
+                    for (int hh = 0; hh < kLPer; ++hh) {  // (clamped, not guarded: no branch)
+                        const uint32_t i = hh * kLT + tid;
+                        kv[hh] = img[S.P[par ^ 1u][i < nb1 ? i : nb1 - 1]];
+                    }
+                }
                 // ---- heavy slots: bitmaps, then their prefix maxima (uniform branch) ----
                 const uint32_t nh0 = S.nheavy[par];
                 const uint32_t nh = nh0 < (uint32_t)kLHeavy ? nh0 : (uint32_t)kLHeavy;
@@ -1239,7 +1269,11 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                     // (every record stores, those not of this pass to the spare slot past the chunk:
                     // a fixed count, so the wait for the next batch, loaded before these stores,
                     // does not wait for them)
+#if MPX_RES_IMG
+                    const uint32_t dst = (cl[hh] & 1u) ? S.P[par][i] : spare;
+#else
                     const uint32_t dst = (cl[hh] & 1u) ? base + i : spare;
+#endif
                     if (!(MPX_RS_ABL & 2)) {
 #if MPX_RES16
                         reinterpret_cast<int4*>(r_ret)[dst] =
@@ -1287,8 +1321,8 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
             __syncthreads();
 #if MPX_RL_STAMP
             if (bin == 0 && sub == 0 && tid == 0)
-                printf("RL_STAMP bin0 mode %d recs %u batches %u: P1 %llu bar1 %llu heavy %llu P2 %llu bar2 %llu P3 %llu\n",
-                       mode, r1 - r0, tag, S.rph[0], S.rph[1], S.rph[2], S.rph[3], S.rph[4], S.rph[5]);
+                printf("RL_STAMP bin0 mode %d recs %u batches %u: P1 %llu expand %llu bar1 %llu heavy %llu P2 %llu bar2 %llu P3 %llu\n",
+                       mode, r1 - r0, tag, S.rph[6], S.rph[0], S.rph[1], S.rph[2], S.rph[3], S.rph[4], S.rph[5]);
 #endif
             if (mode == 0) rerun = (S.flags & kFOverflow) != 0;
         }
@@ -1385,10 +1419,9 @@ struct EmitLds {
     uint2 inc[kHMax];      // over the earlier tiles
     int64_t hval[kHMax];
     uint32_t hfl[kHMax];
-    int64_t iret[kTL];     // the tile's cold results in image order (bin runs); first the
-                           // image's run marks (MPX_EMIT_CPOS=0)
+    int64_t iret[kTL];     // the tile's cold results in image order (bin runs)
     uint8_t iconf[kTL];
-    uint16_t lst[kMaxBins];  // per bin: image start of the tile's run (MPX_EMIT_CPOS=0)
+    uint16_t lst[kMaxBins];  // per bin: image start of the tile's run
     uint32_t dof[kMaxBins];  //          partition start of the run - image start
     uint32_t wsum[kTW];
 };
@@ -1396,7 +1429,6 @@ struct EmitLds {
 __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restrict__ op,
                                                  const int64_t* __restrict__ val, uint32_t n,
                                                  const uint16_t* __restrict__ ipos,
-                                                 const uint32_t* __restrict__ cpos,
                                                  const uint32_t* __restrict__ tcold,
                                                  const int64_t* __restrict__ r_ret,
                                                  const uint8_t* __restrict__ r_conf,
@@ -1427,35 +1459,24 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
     }
     // the cold results, lanes over the tile image: consecutive lanes read consecutive positions of
     // one bin run (the gather in command order touched one line per lane)
-#if MPX_EMIT_CPOS
-    {
+#if MPX_RES_IMG
+    {  // the tile's results in image order are its own slots: one contiguous run
         const uint32_t nc = tcold[tile];
-        const uint32_t* cp = cpos + (uint64_t)tile * kTL;
-        uint32_t q[kTPer];
-#pragma unroll
-        for (int u = 0; u < kTPer; ++u) {
-            const uint32_t i = tid + u * kTT;
-            q[u] = i < nc ? cp[i] : 0u;
-        }
-        int64_t x[kTPer];
+        const uint64_t r0 = (uint64_t)tile * kTL;
+        int64_t xr[kTPer];
         uint8_t c[kTPer];
 #pragma unroll
         for (int u = 0; u < kTPer; ++u) {
             const uint32_t i = tid + u * kTT;
-#if MPX_RES16
-            const int4 rr = i < nc ? reinterpret_cast<const int4*>(r_ret)[q[u]] : make_int4(0, 0, 0, 0);
-            x[u] = kv_lo_hi(rr.x, rr.y);
-            c[u] = (uint8_t)rr.z;
-#else
-            x[u] = i < nc ? r_ret[q[u]] : 0;
-            c[u] = i < nc ? r_conf[q[u]] : 0;
-#endif
+            const bool any = i - (uint32_t)l < nc;  // (wave-uniform)
+            xr[u] = any ? r_ret[r0 + i] : 0;
+            c[u] = any ? r_conf[r0 + i] : 0;
         }
 #pragma unroll
         for (int u = 0; u < kTPer; ++u) {
             const uint32_t i = tid + u * kTT;
             if (i < nc) {
-                S.iret[i] = x[u];
+                S.iret[i] = xr[u];
                 S.iconf[i] = c[u];
             }
         }
@@ -1617,7 +1638,8 @@ emit_out:
 // ---- launcher ---------------------------------------------------------------------------------
 namespace {
 struct FastLayout {
-    uint64_t gk, gc, rows, part, ctot, bin_start, rec_kv, ipos, cpos, tcold, r_ret, r_conf, hot, total;
+    uint64_t gk, gc, rows, part, ctot, bin_start, img, lrow, runs, ipos, tcold, r_ret, r_conf, hot,
+        total;
 };
 
 ApGeo geo_for(const KvTable& t, uint64_t n) {
@@ -1648,12 +1670,15 @@ FastLayout fast_layout(const KvTable& t, uint64_t c) {
     L.part = o; o += al((uint64_t)kScanGroups * g.rowlen * 4);
     L.ctot = o; o += al((uint64_t)g.nbin * 4);
     L.bin_start = o; o += al(((uint64_t)g.nbin + 1) * 4);
-    L.rec_kv = o; o += al((c + 1) * 16);  // (+ the spare record: see k_ap_scatter)
+    L.img = o; o += al((uint64_t)g.tiles * kTL * 16);
+    L.lrow = o; o += al((uint64_t)g.tiles * g.nbin * 2);
+    L.runs = o; o += al((uint64_t)g.tiles * g.nbin * 8);
     L.ipos = o; o += al(c * 2);
-    L.cpos = o; o += al(((uint64_t)g.tiles * kTL + 1) * 4);
     L.tcold = o; o += al((uint64_t)g.tiles * 4);
-    L.r_ret = o; o += al((c + 1) * (MPX_RES16 ? 16 : 8));  // (+ the spare result: see k_ap_resolve_list)
-    L.r_conf = o; o += MPX_RES16 ? 0 : al(c + 1);
+    // results: at partition or image positions, + the spare result (see k_ap_resolve_list)
+    const uint64_t nres = (MPX_RES_IMG ? (uint64_t)g.tiles * kTL : c) + 1;
+    L.r_ret = o; o += al(nres * (MPX_RES16 ? 16 : 8));
+    L.r_conf = o; o += MPX_RES16 ? 0 : al(nres);
     L.hot = o; o += al(sizeof(ApHot));
     L.total = o;
     return L;
@@ -1687,9 +1712,10 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
     uint32_t* part = (uint32_t*)(b + L.part);
     uint32_t* ctot = (uint32_t*)(b + L.ctot);
     uint32_t* bin_start = (uint32_t*)(b + L.bin_start);
-    int4* rec_kv = (int4*)(b + L.rec_kv);
+    int4* img = (int4*)(b + L.img);
+    uint16_t* lrow = (uint16_t*)(b + L.lrow);
+    uint2* runs = (uint2*)(b + L.runs);
     uint16_t* ipos = (uint16_t*)(b + L.ipos);
-    uint32_t* cpos = (uint32_t*)(b + L.cpos);
     uint32_t* tcold = (uint32_t*)(b + L.tcold);
     int64_t* r_ret = (int64_t*)(b + L.r_ret);
     uint8_t* r_conf = (uint8_t*)(b + L.r_conf);
@@ -1711,19 +1737,20 @@ hipError_t launch_apply_fast(KvTable& t, const uint8_t* op, const int64_t* key, 
             k_ap_sample<<<kSampGrid, 256, 0, stream>>>(key + c0, n, hot_min, gk, gc, tab);
         }
         k_ap_select<<<1, kTT, 0, stream>>>(t, gk, gc, hot_min, tab, hot);
-        k_ap_count<<<kCountGrid, kTT, 0, stream>>>(g, op + c0, key + c0, n, rows, hot);
+        k_ap_scatter<<<kScatterGrid, kTT, 0, stream>>>(g, op + c0, key + c0, val + c0, n, rows,
+                                                       lrow, hot, img, ipos, tcold);
         k_ap_scan_part<<<g.ng, 256, 0, stream>>>(g, rows, part, hot);
         k_ap_scan_top<<<(g.rowlen + kTopCols - 1) / kTopCols, kTT, 0, stream>>>(g, part, ctot, hot);
         k_ap_scan_bins<<<1, kTT, 0, stream>>>(g, ctot, bin_start);
         k_ap_scan_rows<<<g.ng, 256, 0, stream>>>(g, rows, part, bin_start, hot);
-        k_ap_scatter<<<kScatterGrid, kTT, 0, stream>>>(g, op + c0, key + c0, val + c0, n, rows, hot,
-                                                  rec_kv, (uint32_t)C, ipos, cpos, tcold);
-        k_ap_resolve_list<<<g.nbin, kLT, 0, stream>>>(g, t, bin_start, rec_kv, r_ret, r_conf,
-                                                      (uint32_t)C, hot, err);
+        k_ap_runs<<<dim3((g.tiles + kRunT - 1) / kRunT, (g.nbin + kRunB - 1) / kRunB), 256, 0,
+                    stream>>>(g, rows, lrow, runs);
+        const uint32_t spare = MPX_RES_IMG ? g.tiles * (uint32_t)kTL : (uint32_t)C;
+        k_ap_resolve_list<<<g.nbin, kLT, 0, stream>>>(g, t, bin_start, runs, img, r_ret, r_conf,
+                                                      spare, hot, err);
         k_ap_hot_commit<<<1, kHMax, 0, stream>>>(t, val + c0, hot, err);
-        k_ap_emit<<<g.tiles, kTT, 0, stream>>>(g, op + c0, val + c0, n, ipos, cpos, tcold, r_ret,
-                                               r_conf, rows, bin_start,
-                                               hot, ret + c0, conf ? conf + c0 : nullptr);
+        k_ap_emit<<<g.tiles, kTT, 0, stream>>>(g, op + c0, val + c0, n, ipos, tcold, r_ret, r_conf, rows,
+                                               bin_start, hot, ret + c0, conf ? conf + c0 : nullptr);
     }
     return hipGetLastError();
 }

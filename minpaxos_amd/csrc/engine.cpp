@@ -1461,6 +1461,10 @@ int mpx_event_create(mpx_engine* e, int timing, void** out) {
 int mpx_event_destroy(mpx_engine* e, void* ev) {
     if (!e) return MPX_E_INVAL;
     if (!ev) return fail(e, MPX_E_INVAL, "null or invalid argument");
+    // a destroyed event never stays registered as the group step's timing hook: the pair is
+    // unregistered together (the hook records both or neither)
+    if ((hipEvent_t)ev == e->ev_fast0 || (hipEvent_t)ev == e->ev_fast1)
+        e->ev_fast0 = e->ev_fast1 = nullptr;
     HIPCHK(e, hipEventDestroy((hipEvent_t)ev));
     return MPX_OK;
 }

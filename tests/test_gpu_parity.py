@@ -692,6 +692,33 @@ def test_conflict_batch(mk_engine):
         assert np.array_equal(e.conflict_batch(op, key, off), o.conflict_batch(op, key, off))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("kshift,oshift", [(0, 0), (1, 3), (1, 15), (0, 7)])
+def test_conflict_batch_dev_misaligned(mk_engine, kshift, oshift):
+    """the device form with key / op pointers off their 16-byte alignment: the kernel stages
+    each workgroup's range by 16-byte vectors from the aligned address at or below it"""
+    from minpaxos_amd.devbuf import Arena
+    rng = np.random.default_rng(11 + kshift * 16 + oshift)
+    e, o = mk_engine(5, R.MODE_MIN), Oracle(5, R.MODE_MIN)
+    sizes = rng.integers(0, 9, 3000)
+    sizes[::700] = 40
+    sizes[5:9] = 0  # empty instances
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    m = int(off[-1])
+    op, key, _ = gen_cases.commands_mixed(rng, m, 300, neg_keys=True)
+    want = o.conflict_batch(op, key, off)
+    n_inst = len(off) - 1
+    with Arena(e) as ar:
+        d_key = ar.put(np.concatenate([np.zeros(kshift, np.int64), key]))
+        d_op = ar.put(np.concatenate([np.zeros(oshift, np.uint8), op]))
+        d_off = ar.put(off)
+        d_out = ar.full(n_inst, np.uint8, 0xEE)
+        e.conflict_batch_dev(d_op.at(oshift), d_key.at(kshift), d_off.ptr, n_inst, d_out.ptr)
+        e.stream_synchronize(None)
+        got = ar.get(d_out, n_inst - 1)
+    assert np.array_equal(got, want)
+
+
 # ---- fused group step (config 5 shape) ----------------------------------------------------------
 def _cmp_group(got, want, G, K):
     for f in ("committed_out", "executed_out", "peer_out", "ret", "conf_prev", "kv_cnt",
@@ -858,6 +885,31 @@ def test_group_step_fused_totals(mk_engine, kind):
                 e.step_totals_dev(gb, tot2.ptr, e.stream)
                 e.stream_synchronize(e.stream)
                 assert ar.get(tot2).tolist() == want
+
+
+def test_group_step_events_destroyed_unregister(mk_engine):
+    """destroying a registered timing event unregisters the pair, so later group
+    steps record nothing (no use of a destroyed event) and stay correct"""
+    from minpaxos_amd.devbuf import Arena
+    N, K = 5, 256
+    b = synth.group_batch(40, 256, N, 4, 256, seed=81)
+    b.setdefault("has_cmds", None)
+    e, o = mk_engine(N, R.MODE_MIN, kv_per_group=K), Oracle(N, R.MODE_MIN, kv_per_group=K)
+    want = _want_totals(b, o.group_step(b))
+    with Arena(e) as ar:
+        gb, d = _dev_group_batch(ar, b, N, K, True)
+        ev0, ev1 = e.event_create(), e.event_create()
+        e.group_step_events(ev0, ev1)
+        tot = ar.full(3, np.int64, 0x55)
+        e.group_step_totals_dev(gb, tot.ptr, e.stream)
+        e.stream_synchronize(e.stream)
+        assert e.event_elapsed_ms(ev0, ev1) >= 0.0
+        e.event_destroy(ev1)  # the pair is unregistered here
+        e.event_destroy(ev0)
+        for _ in range(2):
+            e.group_step_totals_dev(gb, tot.ptr, e.stream)
+            e.stream_synchronize(e.stream)
+            assert ar.get(tot).tolist() == want
 
 
 def test_group_step_totals_many_groups(mk_engine):
