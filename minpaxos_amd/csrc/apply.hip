@@ -656,10 +656,12 @@ hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const
 
 // ---- state.ConflictBatch over consecutive instances ------------------------------------------
 // ConflictBatch(b1, b2) (state.go:62-71) = some pair (c1 in b1, c2 in b2) with the same key and a
-// PUT among the two. A workgroup takes 256 consecutive pairs, i.e. one contiguous command range;
-// when it fits kStage commands it is staged in LDS with coalesced loads (every command is read
-// from HBM once, not once per pair it belongs to). A lane then takes one pair when both
-// instances have at most kSmall commands (MAX_BATCH-sized instances are rare) and tests all
+// PUT among the two. A workgroup takes 256 consecutive pairs, i.e. one contiguous command range.
+// Its 258 offsets are read once (one coalesced load, into LDS); when the range fits kStage
+// commands its keys are staged in LDS by 16-byte loads and its op bytes by 16-byte loads (every
+// load of the tile issued before the first LDS write; the loads start at the 16-byte boundary at
+// or below the range, the bytes before it are never read back). A lane then takes one pair when
+// both instances have at most kSmall commands (MAX_BATCH-sized instances are rare) and tests all
 // |b1| x |b2| products in registers. The wave then takes its larger pairs one at a time, lanes
 // striding over the products with an early exit on the first hit.
 // (4: the products of two 4-command instances in registers take 16 key registers, not 32, and
@@ -669,7 +671,10 @@ hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const
 #endif
 constexpr int kSmall = MPX_CONF_SMALL;
 constexpr int kConfBlock = 256;
-constexpr int kStage = 2560;
+constexpr int kStage = 2046;                // staged commands (16 KB of keys with the slack)
+constexpr int kStageKV = (kStage + 2) / 2;  // 16-byte key vectors: the range + one key of slack
+constexpr int kStageOV = (kStage + 30) / 16;  // 16-byte op vectors: the range + 15 bytes of slack
+constexpr int kKeyRounds = (kStageKV + kConfBlock - 1) / kConfBlock;
 
 template <typename KeyAt, typename PutAt>
 __device__ __forceinline__ bool small_pair(uint64_t a0, uint64_t na, uint64_t a1, uint64_t nb,
@@ -694,55 +699,118 @@ __device__ __forceinline__ bool small_pair(uint64_t a0, uint64_t na, uint64_t a1
     return hit;
 }
 
+// small_pair over the LDS-staged range: the low key halves compared first, the high halves read
+// only for the (rare) pairs whose low halves meet
+__device__ __forceinline__ bool small_pair_lds(uint32_t a0, uint64_t na, uint32_t a1, uint64_t nb,
+                                               const uint32_t* slo, const uint32_t* shi,
+                                               const uint8_t* so) {
+    uint32_t ka[kSmall], kb[kSmall];
+    uint32_t pa = 0, pb = 0;  // PUT bits
+#pragma unroll
+    for (int i = 0; i < kSmall; ++i) {
+        const bool ia = (uint64_t)i < na, ib = (uint64_t)i < nb;
+        ka[i] = ia ? slo[a0 + i] : 0u;
+        kb[i] = ib ? slo[a1 + i] : 0u;
+        pa |= (ia && so[a0 + i] == MPX_OP_PUT ? 1u : 0u) << i;
+        pb |= (ib && so[a1 + i] == MPX_OP_PUT ? 1u : 0u) << i;
+    }
+    uint32_t cand = 0;  // bit 4i + j: low halves equal and a PUT among the two
+#pragma unroll
+    for (int i = 0; i < kSmall; ++i)
+#pragma unroll
+        for (int j = 0; j < kSmall; ++j)
+            cand |= ((uint64_t)i < na && (uint64_t)j < nb && ka[i] == kb[j] &&
+                     (((pa >> i) | (pb >> j)) & 1u))
+                        ? 1u << (kSmall * i + j)
+                        : 0u;
+    while (cand) {
+        const int b = __builtin_ctz(cand);
+        cand &= cand - 1;
+        if (shi[a0 + b / kSmall] == shi[a1 + b % kSmall]) return true;
+    }
+    return false;
+}
+
 __global__ __launch_bounds__(kConfBlock) void k_conflict_batch(const uint8_t* __restrict__ op,
                                                                const int64_t* __restrict__ key,
                                                                const uint64_t* __restrict__ off,
                                                                uint64_t n_pairs,
                                                                uint8_t* __restrict__ out) {
-    __shared__ int64_t sk[kStage];
-    __shared__ uint8_t so[kStage];
-    __shared__ uint64_t range[2];
+    __shared__ uint64_t soff[kConfBlock + 2];
+    // the keys as two 32-bit planes (a lane's instance lies ~4 keys past its neighbour's: 8-byte
+    // reads would hit every 8th bank pair, 32-bit ones every 4th), the high halves read only on a
+    // low-half match
+    __shared__ uint2 slo2[kStageKV], shi2[kStageKV];
+    __shared__ int4 so4[kStageOV];
     const uint64_t p0 = (uint64_t)blockIdx.x * kConfBlock;
-    const uint64_t pair = p0 + threadIdx.x;
-    const uint64_t pe = n_pairs - p0 < (uint64_t)kConfBlock ? n_pairs : p0 + kConfBlock;
-    const int l = lane_id();
-    const bool live = pair < n_pairs;
-    uint64_t a0 = 0, a1 = 0, b1 = 0;
-    if (live) {
-        a0 = off[pair];
-        a1 = off[pair + 1];
-        b1 = off[pair + 2];
+    const int t = threadIdx.x;
+    const uint32_t np = n_pairs - p0 < (uint64_t)kConfBlock ? (uint32_t)(n_pairs - p0)
+                                                            : (uint32_t)kConfBlock;
+    // off[p0 .. p0 + np + 1]: np + 2 entries
+    {
+        const bool x = t < 2 && kConfBlock + t < (int)np + 2;
+        const uint64_t o = off[p0 + min((uint32_t)t, np + 1)];
+        const uint64_t ox = x ? off[p0 + kConfBlock + t] : 0;
+        if ((uint32_t)t < np + 2) soff[t] = o;
+        if (x) soff[kConfBlock + t] = ox;
     }
-    if (pair == p0) range[0] = a0;
-    if (pair + 1 == pe) range[1] = b1;
     __syncthreads();
-    const uint64_t c_lo = range[0], span = range[1] - range[0];
+    const uint64_t c_lo = soff[0], c_hi = soff[np + 1];
+    // vector bases at or below the range, 16-byte aligned (pointer arithmetic, so the loads
+    // stay global ones): ksh keys / osh op bytes of slack before c_lo
+    const uint32_t ksh = (uint32_t)(((uintptr_t)(key + c_lo) >> 3) & 1);
+    const uint32_t osh = (uint32_t)((uintptr_t)(op + c_lo) & 15);
+    const int4* kv = (const int4*)(key + c_lo - ksh);
+    const int4* ov = (const int4*)(op + c_lo - osh);
+    const uint64_t span = c_hi - c_lo;
     const bool staged = span <= (uint64_t)kStage;  // uniform over the workgroup
+    static_assert(kKeyRounds == 4, "four key vectors per thread");
     if (staged) {
-        for (uint32_t i = threadIdx.x; i < (uint32_t)span; i += kConfBlock) {
-            sk[i] = key[c_lo + i];
-            so[i] = op[c_lo + i];
+        const uint32_t nkv = (uint32_t)((span + ksh + 1) >> 1);
+        const uint32_t nov = (uint32_t)((span + osh + 15) >> 4);
+        if (nkv) {  // (clamped, unconditional loads: the tile's vectors all in flight at once)
+            const uint32_t i0 = (uint32_t)t, i1 = i0 + kConfBlock, i2 = i1 + kConfBlock,
+                           i3 = i2 + kConfBlock;
+            const int4 k0 = kv[min(i0, nkv - 1)], k1 = kv[min(i1, nkv - 1)],
+                       k2 = kv[min(i2, nkv - 1)], k3 = kv[min(i3, nkv - 1)];
+            const int4 o0 = ov[min(i0, nov - 1)];
+            auto put = [&](uint32_t i, int4 x) {
+                if (i < nkv) {
+                    slo2[i] = make_uint2((uint32_t)x.x, (uint32_t)x.z);
+                    shi2[i] = make_uint2((uint32_t)x.y, (uint32_t)x.w);
+                }
+            };
+            put(i0, k0);
+            put(i1, k1);
+            put(i2, k2);
+            put(i3, k3);
+            if (i0 < nov) so4[i0] = o0;
         }
         __syncthreads();
     }
+    const bool live = (uint32_t)t < np;
+    const uint64_t a0 = soff[t], a1 = soff[t + 1], b1 = soff[t + 2];
     const uint64_t na = a1 - a0, nb = b1 - a1;
     const bool small = live && na <= (uint64_t)kSmall && nb <= (uint64_t)kSmall;
     if (small) {
         bool hit;
-        if (staged)
-            hit = small_pair(a0 - c_lo, na, a1 - c_lo, nb, [&](uint64_t i) { return sk[i]; },
-                             [&](uint64_t i) { return so[i] == MPX_OP_PUT; });
-        else
+        if (staged) {
+            const uint32_t* slo = (const uint32_t*)slo2 + ksh;
+            const uint32_t* shi = (const uint32_t*)shi2 + ksh;
+            const uint8_t* so = (const uint8_t*)so4 + osh;
+            hit = small_pair_lds(a0 - c_lo, na, a1 - c_lo, nb, slo, shi, so);
+        } else {
             hit = small_pair(a0, na, a1, nb, [&](uint64_t i) { return key[i]; },
                              [&](uint64_t i) { return op[i] == MPX_OP_PUT; });
-        out[pair] = hit ? 1 : 0;
+        }
+        out[p0 + t] = hit ? 1 : 0;
     }
     // the wave's larger pairs, one at a time
+    const int l = lane_id();
     unsigned long long big = __ballot(live && !small);
     while (big) {
         const int src = __ffsll((long long)big) - 1;
         big &= big - 1;
-        const uint64_t p = (uint64_t)__shfl((long long)pair, src);
         const uint64_t x0 = (uint64_t)__shfl((long long)a0, src);
         const uint64_t x1 = (uint64_t)__shfl((long long)a1, src);
         const uint64_t y1 = (uint64_t)__shfl((long long)b1, src);
@@ -760,7 +828,7 @@ __global__ __launch_bounds__(kConfBlock) void k_conflict_batch(const uint8_t* __
                 break;
             }
         }
-        if (l == src) out[p] = hit ? 1 : 0;
+        if (l == src) out[p0 + t] = hit ? 1 : 0;
     }
 }
 
