@@ -671,7 +671,10 @@ hipError_t launch_apply(KvTable& t, const uint8_t* op, const int64_t* key, const
 #endif
 constexpr int kSmall = MPX_CONF_SMALL;
 constexpr int kConfBlock = 256;
-constexpr int kStage = 2046;                // staged commands (16 KB of keys with the slack)
+#ifndef MPX_CONF_STAGE
+#define MPX_CONF_STAGE 1534
+#endif
+constexpr int kStage = MPX_CONF_STAGE;  // staged commands: 12 KB of keys with the slack, 8 workgroups per CU
 constexpr int kStageKV = (kStage + 2) / 2;  // 16-byte key vectors: the range + one key of slack
 constexpr int kStageOV = (kStage + 30) / 16;  // 16-byte op vectors: the range + 15 bytes of slack
 constexpr int kKeyRounds = (kStageKV + kConfBlock - 1) / kConfBlock;
@@ -764,7 +767,7 @@ __global__ __launch_bounds__(kConfBlock) void k_conflict_batch(const uint8_t* __
     const int4* ov = (const int4*)(op + c_lo - osh);
     const uint64_t span = c_hi - c_lo;
     const bool staged = span <= (uint64_t)kStage;  // uniform over the workgroup
-    static_assert(kKeyRounds == 4, "four key vectors per thread");
+    static_assert(kKeyRounds == 3 || kKeyRounds == 4, "three or four key vectors per thread");
     if (staged) {
         const uint32_t nkv = (uint32_t)((span + ksh + 1) >> 1);
         const uint32_t nov = (uint32_t)((span + osh + 15) >> 4);
@@ -772,7 +775,8 @@ __global__ __launch_bounds__(kConfBlock) void k_conflict_batch(const uint8_t* __
             const uint32_t i0 = (uint32_t)t, i1 = i0 + kConfBlock, i2 = i1 + kConfBlock,
                            i3 = i2 + kConfBlock;
             const int4 k0 = kv[min(i0, nkv - 1)], k1 = kv[min(i1, nkv - 1)],
-                       k2 = kv[min(i2, nkv - 1)], k3 = kv[min(i3, nkv - 1)];
+                       k2 = kv[min(i2, nkv - 1)],
+                       k3 = kKeyRounds > 3 ? kv[min(i3, nkv - 1)] : make_int4(0, 0, 0, 0);
             const int4 o0 = ov[min(i0, nov - 1)];
             auto put = [&](uint32_t i, int4 x) {
                 if (i < nkv) {
@@ -783,7 +787,7 @@ __global__ __launch_bounds__(kConfBlock) void k_conflict_batch(const uint8_t* __
             put(i0, k0);
             put(i1, k1);
             put(i2, k2);
-            put(i3, k3);
+            if (kKeyRounds > 3) put(i3, k3);
             if (i0 < nov) so4[i0] = o0;
         }
         __syncthreads();

@@ -816,10 +816,12 @@ struct ListLds {
     uint32_t flags;
     // the run window: tiles [wt0, wt0 + kLWin) of the bin's run table, their runs' partition
     // starts (wr[kLWin]: the start of the run after the window, the bin's end past the last
-    // tile) and image offsets; per batch parity the image position of every record (P)
+    // tile) and image offsets. A batch's runs as marks: per batch parity a bit per record that
+    // starts a run or a 64-record segment (MB), the run's image offset at each mark (D)
     uint32_t wr[kLWin + 1];
     uint32_t wd[kLWin];
-    uint32_t P[2][kLB];
+    uint32_t MB[2][kLB / 32];
+    uint32_t D[kLB];
 #if MPX_RL_STAMP
     unsigned long long rph[8];
 #endif
@@ -859,22 +861,17 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
             if (u < (uint32_t)kLWin) S.wd[u] = x.y;
         }
     };
-    auto expand = [&](uint32_t base, uint32_t* Pb) {  // every thread (barriers inside)
+    // the marks of batch [base, base + kLB) into MB[mp] / D (every thread; barriers inside when
+    // the batch runs past the window)
+    auto expand = [&](uint32_t base, uint32_t mp) {
         const uint32_t end = base + kLB < r1 ? base + kLB : r1;
         for (;;) {
             for (uint32_t u = tid; u < (uint32_t)kLWin; u += kLT) {
                 const uint32_t ra = S.wr[u], re = S.wr[u + 1], d = S.wd[u];
                 const uint32_t a = ra > base ? ra : base, e = re < end ? re : end;
-                const bool lng = e > a + 32;
-                if (!lng)
-                    for (uint32_t q = a; q < e; ++q) Pb[q - base] = q + d;
-                unsigned long long m = __ballot(lng);
-                while (m) {
-                    const int src = __ffsll((long long)m) - 1;
-                    m &= m - 1;
-                    const uint32_t A = (uint32_t)__shfl((int)a, src), E = (uint32_t)__shfl((int)e, src);
-                    const uint32_t D = (uint32_t)__shfl((int)d, src);
-                    for (uint32_t q = A + (uint32_t)l; q < E; q += kWave) Pb[q - base] = q + D;
+                for (uint32_t x = a - base; a < e && x < e - base; x = (x | 63u) + 1u) {
+                    atomicOr(&S.MB[mp][x >> 5], 1u << (x & 31));
+                    S.D[x] = d;
                 }
             }
             if (S.wr[kLWin] >= end) break;
@@ -882,6 +879,17 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
             load_win(wt0 + kLWin);
             __syncthreads();
         }
+    };
+    // after the marks' barrier: the image position of the thread's record i of batch `base` (nb
+    // records; past them the last one's) - the last mark at or before it in its 64-record segment
+    auto locate = [&](uint32_t base, uint32_t mp, uint32_t nb, uint32_t i) {
+        const uint32_t x = i < nb ? i : nb - 1;
+        const uint32_t sg = x >> 6, bit = x & 63u;
+        const unsigned long long w =
+            ((unsigned long long)S.MB[mp][2 * sg + 1] << 32) | S.MB[mp][2 * sg];
+        const unsigned long long mk = bit == 63u ? ~0ull : (2ull << bit) - 1ull;
+        const uint32_t m = (sg << 6) + 63u - (uint32_t)__clzll((long long)(w & mk));
+        return base + x + S.D[m];
     };
     for (uint32_t sub = 0; sub < nsub; ++sub) {
         const uint64_t gbase = ((((uint64_t)bin << g.lgsub) | sub) * bpb) * kSB;
@@ -950,16 +958,19 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
             }
             __syncthreads();  // (the pre-insert loop's window use is over)
             load_win(0);
+            for (uint32_t i = tid; i < (uint32_t)(2 * kLB / 32); i += kLT) (&S.MB[0][0])[i] = 0u;
             __syncthreads();
-            expand(r0, S.P[1]);
+            expand(r0, 1u);  // (the first batch's tag is 1)
             __syncthreads();
             int4 kv[kLPer];
+            uint32_t nxp[kLPer];  // the loaded batch's image positions
             {
                 const uint32_t nb1 = r1 - r0 < (uint32_t)kLB ? r1 - r0 : (uint32_t)kLB;
 #pragma unroll
                 for (int hh = 0; hh < kLPer; ++hh) {
                     const uint32_t i = hh * kLT + tid;
-                    kv[hh] = img[S.P[1][i < nb1 ? i : nb1 - 1]];
+                    nxp[hh] = locate(r0, 1u, nb1, i);
+                    kv[hh] = img[nxp[hh]];
                 }
             }
             uint32_t tag = 0;
@@ -1110,16 +1121,20 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                 // resolves
                 const bool more = base + kLB < r1;  // (uniform)
                 RL_STAMP(6);
-                if (more) expand(base + kLB, S.P[par ^ 1u]);
+                if (more) expand(base + kLB, par ^ 1u);
                 RL_STAMP(0);
                 __syncthreads();
                 RL_STAMP(1);
+                uint32_t cur[kLPer];  // this batch's image positions (its results' places)
+#pragma unroll
+                for (int hh = 0; hh < kLPer; ++hh) cur[hh] = nxp[hh];
                 if (more) {
                     const uint32_t nb1 = r1 - (base + kLB) < (uint32_t)kLB ? r1 - (base + kLB) : (uint32_t)kLB;
 #pragma unroll
                     for (int hh = 0; hh < kLPer; ++hh) {  // (clamped, not guarded: no branch)
                         const uint32_t i = hh * kLT + tid;
-                        kv[hh] = img[S.P[par ^ 1u][i < nb1 ? i : nb1 - 1]];
+                        nxp[hh] = locate(base + kLB, par ^ 1u, nb1, i);
+                        kv[hh] = img[nxp[hh]];
                     }
                 }
                 // ---- heavy slots: bitmaps, then their prefix maxima (uniform branch) ----
@@ -1270,7 +1285,7 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
                     // a fixed count, so the wait for the next batch, loaded before these stores,
                     // does not wait for them)
 #if MPX_RES_IMG
-                    const uint32_t dst = (cl[hh] & 1u) ? S.P[par][i] : spare;
+                    const uint32_t dst = (cl[hh] & 1u) ? cur[hh] : spare;
 #else
                     const uint32_t dst = (cl[hh] & 1u) ? base + i : spare;
 #endif
@@ -1288,6 +1303,9 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
 #endif
                     }
                 }
+                // this batch's marks are read (after the last barrier): cleared for the batch after
+                // next (marked after the next barrier)
+                if (tid < kLB / 32) S.MB[par][tid] = 0u;
                 RL_STAMP(3);
                 __syncthreads();
                 RL_STAMP(4);
