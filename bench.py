@@ -209,7 +209,7 @@ def host_cores():
     return max(1, min(n, 16))
 
 
-TRAFFIC_DB = os.path.join(ROOT, "profiles", "traffic_r05.json")
+TRAFFIC_DB = os.path.join(ROOT, "profiles", "traffic_r06.json")
 ISSUE_BOUND = ("decode", "stream", "fanout")
 
 
@@ -455,14 +455,17 @@ def step_bench(a, rk):
             eng.stream_wait_event(comp, ev_comm[buf])
         # the timed steps' HIP events bracket the group kernel alone: the engine records them
         # right before and after its launch (mpx_group_step_events), the work-list kernel and
-        # the totals are outside
-        eng.group_step_events(*(evs or (ev_k[i] if timed else (None, None))))
+        # the totals are outside. Steps without events make no hook call at all (the hook is
+        # off between evented steps), so the enqueued timed loop carries no extra ctypes calls
+        use_ev = evs or (ev_k[i] if timed else None)
+        if use_ev:
+            eng.group_step_events(*use_ev)
         # the group step, then its totals (decided, executed instances, executed commands)
         if not a.separate_totals:
             eng.group_step_totals_dev(steps[buf], d["tot"][buf].ptr, comp)
         else:
             eng.group_step_dev(steps[buf], comp)
-        if timed or evs:
+        if use_ev:
             eng.group_step_events()
         if a.separate_totals:
             eng.step_totals_dev(steps[buf], d["tot"][buf].ptr, comp)

@@ -97,6 +97,7 @@ struct mpx_engine {
     DevBuf worklist;
     uint32_t* d_wcount = nullptr;
     hipEvent_t ev_fast0 = nullptr, ev_fast1 = nullptr;  // mpx_group_step_events
+    bool slots_dirty = false;  // a one-launch fold timed out: zero the packed slots first
     // RCCL
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -143,6 +144,9 @@ hipStream_t pick(mpx_engine* e, void* s) { return s ? (hipStream_t)s : e->stream
 
 int check_errword(mpx_engine* e, uint32_t w) {
     if (!w) return MPX_OK;
+    // a one-launch step's fold gave up on its slots: zero them before the next step (stream
+    // order), so no straggler's late add carries into a later step's totals
+    if (w & mpx::kErrSlots) e->slots_dirty = true;
     if (w & mpx::kErrNil)
         return fail(e, MPX_E_NIL_INSTANCE, "record names a nil or out-of-window instance");
     if (w & mpx::kErrBadId) return fail(e, MPX_E_BAD_ID, "reply id outside [0, N)");
@@ -766,6 +770,10 @@ int group_step_dev(mpx_engine* e, const mpx_group_batch* b, int64_t* d_totals, v
         return fail(e, MPX_E_INVAL, "n_groups exceeds mpx_config.max_groups");
     if (one_launch(e) && !mpx::step_one_launch_fits(e->cfg.n_replicas, b->ipg, e->cfg.kv_per_group))
         return fail(e, MPX_E_INVAL, "MPX_FLAG_STEP_ONE_LAUNCH: the batch shape fits no fast variant");
+    if (one_launch(e) && e->slots_dirty) {
+        HIPCHK(e, hipMemsetAsync(e->worklist.p, 0, e->worklist.cap, pick(e, stream)));
+        e->slots_dirty = false;
+    }
     HIPCHK(e, mpx::launch_group_step(e->cfg.mode, e->cfg.n_replicas, e->cfg.kv_per_group, b,
                                      (uint32_t*)e->worklist.p, e->d_wcount, d_totals, e->d_err,
                                      pick(e, stream), e->ev_fast0, e->ev_fast1, pslots(e)));
@@ -887,6 +895,10 @@ int mpx_group_step(mpx_engine* e, const mpx_group_batch* hb) {
     }
     if (one_launch(e) && !mpx::step_one_launch_fits(N, (uint32_t)ipg, (uint32_t)K))
         return fail(e, MPX_E_INVAL, "MPX_FLAG_STEP_ONE_LAUNCH: the batch shape fits no fast variant");
+    if (one_launch(e) && e->slots_dirty) {
+        HIPCHK(e, hipMemsetAsync(e->worklist.p, 0, e->worklist.cap, e->stream));
+        e->slots_dirty = false;
+    }
     HIPCHK(e, mpx::launch_group_step(e->cfg.mode, N, (uint32_t)K, &db, (uint32_t*)e->worklist.p,
                                      e->d_wcount, nullptr, e->d_err, e->stream, nullptr, nullptr,
                                      pslots(e)));

@@ -15,6 +15,9 @@ constexpr uint32_t kErrBadId = 2u;   // reply id outside [0, N)
 constexpr uint32_t kErrOrder = 4u;   // records not in ascending instance order
 constexpr uint32_t kErrKvFull = 8u;  // KV capacity exceeded
 constexpr uint32_t kErrInval = 16u;  // other malformed input (offsets, sizes)
+// (with kErrInval) a one-launch step's fold timed out: its packed totals slots were left as they
+// were and must be zeroed by the host before the next one-launch step
+constexpr uint32_t kErrSlots = 32u;
 
 // reduction scratch: kRedWords u64 per engine
 constexpr int kRedWords = 64;

@@ -436,15 +436,19 @@ __device__ void fold_packed(unsigned long long* pslots, uint32_t n_groups, int64
             if (sl >= nslots) continue;
             const uint32_t want = (n_groups - 1u - sl) / nslots + 1u;
             uint32_t spins = 0;
+            bool late = false;
             while ((w[k] & 127ull) < want) {  // a group still running (the grid's tail)
                 __builtin_amdgcn_s_sleep(2);
                 w[k] = __hip_atomic_load(pslots + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (++spins == (1u << 22)) {  // never on a well-formed launch: fail, do not hang
-                    raise_err(err, kErrInval);
+                    // the slot is left as it is (a straggler's add may still land in it): the
+                    // host zeroes every slot before the next one-launch step (kErrSlots)
+                    raise_err(err, kErrInval | kErrSlots);
+                    late = true;
                     break;
                 }
             }
-            __hip_atomic_store(pslots + sl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!late) __hip_atomic_store(pslots + sl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             d += (w[k] >> 7) & 0xFFFFull;
             xi += (w[k] >> 23) & 0xFFFFull;
             xc += w[k] >> 39;

@@ -934,13 +934,16 @@ def test_group_step_totals_many_groups(mk_engine):
 
 
 @pytest.mark.parametrize("mode", [R.MODE_MIN, R.MODE_CLASSIC])
-@pytest.mark.parametrize("G", [1, 17, 300, 4099])
+@pytest.mark.parametrize("G", [1, 17, 64, 65, 300, 4099, 64 * 70 + 1])
 def test_group_step_one_launch(mk_engine, mode, G):
     """MPX_FLAG_STEP_ONE_LAUNCH: the group step is the fast kernel alone, its last workgroup
-    folding the packed totals (16 groups a slot; G not a multiple of 16 leaves a short last
-    slot). Outputs and totals equal the oracle's over repeated steps (the slots reset
-    themselves), also replayed from a captured graph; a shape no fast variant takes is rejected
-    at the call; a group past the fast kernel's capacity fails the step"""
+    folding the packed totals: ceil(G / 64) slots, group g adding into slot g % ceil(G / 64),
+    so a slot holds at most 64 groups and, when 64 does not divide G, the slots hold unequal
+    counts (G = 65: 33 and 32; G = 64 * 70 + 1: 71 slots, the first 8 with 64 groups, the rest
+    with 63 - slot s expects (G - 1 - s) / nslots + 1). Outputs and totals equal the oracle's over repeated
+    steps (the slots reset themselves), also replayed from a captured graph; a shape no fast
+    variant takes is rejected at the call; a group past the fast kernel's capacity fails the
+    step"""
     from minpaxos_amd.devbuf import Arena
     N, K = 5, 256
     b = synth.group_batch(G, 256, N, 4, 256, seed=300 + G)

@@ -104,12 +104,16 @@ def main():
         got = {}
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
             got[c] = per_kernel(pmc_pass(args, c, os.path.join(d, c), a.steps), pats)
-        per = {}
+        per, dropped = {}, {}
         total = 0.0
         for name in sorted(set(got["FETCH_SIZE"]) & set(got["WRITE_SIZE"])):
             f, w = got["FETCH_SIZE"][name], got["WRITE_SIZE"][name]
             if 2 * len(f) < launches:  # a one-off kernel of the process (table fill, the
-                continue               # parity check's export), not part of the measured call
+                # parity check's export), not part of the measured call: listed, not counted
+                dropped[name[:120]] = {"dispatches": len(f), "launches": launches,
+                                       "fetch_kib_median": statistics.median(f),
+                                       "write_kib_median": statistics.median(w)}
+                continue
             k = max(1, round(len(f) / launches))  # dispatches of this kernel per launch
             b = (statistics.median(f) * 2 + statistics.median(w)) * 1024 * k
             per[name[:120]] = {"fetch_kib_median": statistics.median(f),
@@ -121,6 +125,7 @@ def main():
         ent.update({"key": key, "kernels": pats, "bytes_per_launch": total,
                "alg_bytes_per_launch": rf["alg_bytes_per_launch"],
                "ratio_to_alg": total / rf["alg_bytes_per_launch"], "per_kernel": per,
+               "dropped_one_off": dropped,
                "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py {args} "
                          f"(tools/pmc_collect.py)"})
         db["entries"] = [e for e in db["entries"] if e["key"] != key] + [ent]
