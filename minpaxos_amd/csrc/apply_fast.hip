@@ -757,6 +757,9 @@ __device__ __forceinline__ int64_t kv_lo_hi(int lo, int hi) {
 // MPX_RES_IMG=1: the resolve stores each result at its record's IMAGE position (the tile's own
 // slots, the runs of the records' gather), so the emit reads its tile's results in one
 // contiguous run instead of gathering them run by run from partition order
+#ifndef MPX_RL_XCD
+#define MPX_RL_XCD 1
+#endif
 #ifndef MPX_RES_IMG
 #define MPX_RES_IMG 1
 #endif
@@ -837,7 +840,10 @@ __global__ __launch_bounds__(kLT) void k_ap_resolve_list(ApGeo g, KvTable t,
     __shared__ ListLds S;
     const int tid = threadIdx.x, l = lane_id(), w = tid / kWave;
     const uint32_t bpb = 1u << g.lgbpb;
-    const uint32_t bin = blockIdx.x;
+    // XCD-contiguous bins (workgroup b runs on XCD b % 8): the bins one XCD resolves side by side
+    // are neighbours, so their runs of a tile image - adjacent in it - meet in that XCD's L2: the
+    // gathers' shared lines and the results' partial lines are merged there, not in HBM
+    const uint32_t bin = MPX_RL_XCD ? xcd_tile(g.nbin) : blockIdx.x;
     const uint32_t nslot = bpb * kSB;
     const uint32_t nsub = 1u << g.lgsub;
     const uint32_t ep = t.epoch[0];
