@@ -30,14 +30,30 @@ namespace mpx {
 #ifndef MPX_STAMPS
 #define MPX_STAMPS 0
 #endif
+// MPX_STAMPS=2 (tools/stamp_span.py) keeps instead every fast workgroup's start and end on the
+// chip-wide 100 MHz clock (s_memrealtime), stored by thread 0 with a vector store (no shared
+// accumulator: 65,536 workgroups' atomics on one word serialise), so the rounds of resident
+// workgroups - and the last, partial one - can be told apart
 #if MPX_STAMPS
 __device__ unsigned long long mpx_stamp_acc[16];
+constexpr uint32_t kSpanMax = 1u << 17;
+__device__ unsigned long long mpx_wg_span[kSpanMax][2];
 #define STAMP_DECL                                                     \
-    unsigned long long _st_prev = 0;                                   \
-    if (threadIdx.x == 0) _st_prev = __builtin_amdgcn_s_memtime();
+    unsigned long long _st_prev = 0, _st_rt0 = 0;                      \
+    if (threadIdx.x == 0) {                                            \
+        _st_prev = __builtin_amdgcn_s_memtime();                       \
+        _st_rt0 = __builtin_amdgcn_s_memrealtime();                    \
+    }
+#define STAMP_SPAN()                                                   \
+    do {                                                               \
+        if (MPX_STAMPS >= 2 && threadIdx.x == 0 && blockIdx.x < kSpanMax) { \
+            mpx_wg_span[blockIdx.x][0] = _st_rt0;                      \
+            mpx_wg_span[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                              \
+    } while (0)
 #define STAMP(k)                                                       \
     do {                                                               \
-        if (threadIdx.x == 0) {                                        \
+        if (MPX_STAMPS == 1 && threadIdx.x == 0) { /* (2: spans only) */ \
             unsigned long long _n = __builtin_amdgcn_s_memtime();      \
             atomicAdd(&mpx_stamp_acc[k], _n - _st_prev);               \
             _st_prev = _n;                                             \
@@ -46,6 +62,7 @@ __device__ unsigned long long mpx_stamp_acc[16];
 #else
 #define STAMP_DECL
 #define STAMP(k)
+#define STAMP_SPAN()
 #endif
 // Diagnostic A/B builds only (make variant DEFS=-DMPX_ABLATE=bits): skip a phase of k_group_fast
 // to price it (results are wrong). 1 tally, 2 key lookup, 4 resolve scan, 8 reply ranges,
@@ -975,6 +992,7 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
     if (ebits) raise_err(err, ebits);
     if (pslots && totals && g == gridDim.x - 1) fold_packed(pslots, gridDim.x, totals, err);
     STAMP(6);
+    STAMP_SPAN();
 }
 
 // ======================================= general path =========================================
@@ -1411,5 +1429,10 @@ extern "C" int mpx_debug_stamps(unsigned long long* out16, int reset) {
         if (hipMemcpyToSymbol(HIP_SYMBOL(mpx::mpx_stamp_acc), z, sizeof(z)) != hipSuccess) return -3;
     }
     return 0;
+}
+// every fast workgroup's (start, end) s_memrealtime of the last step, first n of them
+extern "C" int mpx_debug_spans(unsigned long long* out, unsigned n) {
+    if (n > mpx::kSpanMax) n = mpx::kSpanMax;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpx::mpx_wg_span), (size_t)n * 16) == hipSuccess ? 0 : -3;
 }
 #endif
