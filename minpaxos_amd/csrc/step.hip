@@ -281,10 +281,13 @@ __device__ __forceinline__ void table_writeback(const Dict& D, uint32_t norig, u
 // TB table entries at the start of the step, 2^HB hash slots (table + new keys). The launcher
 // picks the smallest variant a batch's shape (N, ipg, kv_per_group) fits; a group that still
 // overflows one at run time goes to the general kernel.
-template <int T_, int R_, int C_, int TB_, int HB_>
+template <int T_, int R_, int C_, int TB_, int HB_, int HN_ = (1 << HB_)>
 struct FastCfg {
     static constexpr int kFT = T_, kFRecs = R_, kFIpg = T_, kFCmds = C_, kFTab = TB_;
-    static constexpr int kFHB = HB_, kFH = 1 << HB_;
+    // kFH key slots (HN_, a power of two by default), slot ids of kFHB bits
+    static constexpr int kFHB = HB_, kFH = HN_;
+    static constexpr bool kFHPow2 = (HN_ & (HN_ - 1)) == 0;
+    static_assert(HN_ <= (1 << HB_) && HN_ >= TB_ && HN_ % 8 == 0, "slot count");
     static constexpr int kFPer = kFCmds / kFT;    // commands per thread
     static constexpr int kFRecPer = kFRecs / kFT; // replies per thread
     static constexpr int kFTabPer = (kFTab + kFT - 1) / kFT;
@@ -300,9 +303,12 @@ struct FastCfg {
     static_assert(kFCmds % kFT == 0 && kFRecs % kFT == 0, "whole items per thread");
     static_assert(kFCmds / 32 <= kWave, "the new-key bitmap is scanned by one wave");
     static_assert(kWaveCmds < 2047, "kTabLp holds 1 + a wave-relative command index");
-    static_assert(kFH % kFT == 0 && (kFH * 2) % (kWave * 16) == 0, "init strides");
+    static_assert((kFH * 2) % 16 == 0, "the wave tables are cleared by 16-byte stores");
 };
-using FastBase = FastCfg<256, 1024, 1024, 256, 9>;   // config 5: N <= 5, keys per group <= 256
+#ifndef MPX_FASTBASE_SLOTS  // A/B builds: FastBase's key slots (512, or 384: 7 workgroups per CU)
+#define MPX_FASTBASE_SLOTS 512
+#endif
+using FastBase = FastCfg<256, 1024, 1024, 256, 9, MPX_FASTBASE_SLOTS>;  // config 5: N <= 5, keys <= 256
 using FastRecs = FastCfg<256, 2048, 1024, 256, 9>;   // N <= 9
 using FastKeys = FastCfg<256, 1024, 1024, 1024, 10>; // group tables of up to 1024 keys
 using FastWide = FastCfg<512, 2048, 2048, 512, 10>;  // 512 instances per group
@@ -380,11 +386,21 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 }
 
 // home slot of a key in the fast path's table: Fibonacci hashing of the folded key (the top
-// HB bits of a 32-bit multiplicative hash)
+// HB bits of a 32-bit multiplicative hash; for a slot count that is not a power of two, the
+// hash scaled to [0, kFH) by a multiply-high)
 template <int HB>
 __device__ __forceinline__ uint32_t fhash(int64_t k) {
     const uint32_t x = (uint32_t)(uint64_t)k ^ (uint32_t)((uint64_t)k >> 32);
     return (x * 0x9E3779B1u) >> (32 - HB);
+}
+template <class Cfg>
+__device__ __forceinline__ uint32_t fhome(int64_t k) {
+    if constexpr (Cfg::kFHPow2) {
+        return fhash<Cfg::kFHB>(k);
+    } else {
+        const uint32_t x = (uint32_t)(uint64_t)k ^ (uint32_t)((uint64_t)k >> 32);
+        return (uint32_t)(((uint64_t)(x * 0x9E3779B1u) * (uint32_t)Cfg::kFH) >> 32);
+    }
 }
 
 // slot of key in the group's table, claiming a free slot if the key is absent (*fresh = 1);
@@ -394,14 +410,14 @@ template <class Cfg, class Lds>
 __device__ __forceinline__ int fast_slot(Lds& S, unsigned long long key, uint32_t h,
                                          int& fresh) {
     constexpr int kFH = Cfg::kFH;
-    uint32_t i = h & (kFH - 1);
+    uint32_t i = h;  // (fhome: < kFH)
     for (int probe = 0; probe < kFH; ++probe) {
         const unsigned long long old = atomicCAS(&S.hkey[i], kFreeKey, key);
         if (old == kFreeKey || old == key) {
             fresh = old == kFreeKey;
             return (int)i;
         }
-        i = (i + 1) & (kFH - 1);
+        i = Cfg::kFHPow2 ? (i + 1) & (kFH - 1) : (i + 1 == (uint32_t)kFH ? 0u : i + 1);
     }
     return -1;
 }
@@ -553,7 +569,8 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
     }
     // LDS initialisation (regions outside the reply image)
 #pragma unroll
-    for (int k = 0; k < kFH / kFT; ++k) S.hkey[t + k * kFT] = kFreeKey;
+    for (int k = 0; k < (kFH + kFT - 1) / kFT; ++k)
+        if (kFH % kFT == 0 || t + k * kFT < kFH) S.hkey[t + k * kFT] = kFreeKey;
     for (int i = t; i < kFH / 2; i += kFT)
         reinterpret_cast<uint32_t*>(S.tabidx)[i] = 0xFFFFFFFFu;  // kNone16 pairs
     if (t < kFCmds / 32) S.newbits[t] = 0u;
@@ -619,7 +636,7 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
             int fresh = 0;
             const int sl = (unsigned long long)tk[k] == kFreeKey
                                ? -1
-                               : fast_slot<Cfg>(S, (unsigned long long)tk[k], fhash<Cfg::kFHB>(tk[k]),
+                               : fast_slot<Cfg>(S, (unsigned long long)tk[k], fhome<Cfg>(tk[k]),
                                            fresh);
             ebits |= sl < 0 ? kOverflow : 0u;
             tslot[k] = sl < 0 ? 0 : sl;
@@ -763,8 +780,9 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
     const int wv = __builtin_amdgcn_readfirstlane(t / kWave);
     uint16_t* T = S.u.b.tab + wv * kFH;  // this wave's table (the reply image is dead)
 #pragma unroll
-    for (int k = 0; k < kFH * 2 / (kWave * 16); ++k)  // 16-byte stores clear the wave's table
-        reinterpret_cast<uint4*>(T)[l + k * kWave] = make_uint4(0u, 0u, 0u, 0u);
+    for (int k = 0; k < (kFH * 2 / 16 + kWave - 1) / kWave; ++k)  // 16-byte stores clear the wave's table
+        if ((kFH * 2 / 16) % kWave == 0 || l + k * kWave < kFH * 2 / 16)
+            reinterpret_cast<uint4*>(T)[l + k * kWave] = make_uint4(0u, 0u, 0u, 0u);
     // volatile LDS pointers: every access below is a real ds_* instruction, in program order
 #if !MPX_STEP_BALLOT
     typedef __attribute__((address_space(3))) volatile uint8_t lds_u8;
@@ -785,11 +803,11 @@ __global__ __launch_bounds__(Cfg::kFT) void k_group_fast(mpx_group_batch b, int3
         const unsigned long long key = (unsigned long long)ck[k];
         int kd = -1;
 #if MPX_ABLATE & 2
-        if (act) kd = (int)fhash<Cfg::kFHB>(ck[k]);
+        if (act) kd = (int)fhome<Cfg>(ck[k]);
 #else
         if (act && key != kFreeKey) {
             int fresh = 0;
-            kd = fast_slot<Cfg>(S, key, fhash<Cfg::kFHB>(ck[k]), fresh);
+            kd = fast_slot<Cfg>(S, key, fhome<Cfg>(ck[k]), fresh);
         }
 #endif
         ebits |= (act && kd < 0) ? kOverflow : 0u;  // table full, or the key INT64_MIN
