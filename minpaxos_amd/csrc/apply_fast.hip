@@ -17,28 +17,30 @@
 //                 they skip the partition and are resolved in log order by a per-key max-scan
 //                 (below), so a skewed key space cannot pile onto one bin. Index 0 is always the
 //                 key INT64_MIN (the table's sentinel, kept in a side slot).
-//   k_ap_count    per 4096-command log tile: commands per bin of the cold keys, and per hot key
-//                 the last position of any command and of a PUT in the tile
-//   scans         k_ap_scan_part / _top / _bins / _rows over the tile rows: bin offsets per tile
-//                 (sums), hot positions before each tile (maxima)
 //   k_ap_scatter  persistent (one workgroup per CU, XCD-contiguous tiles, the next tile
-//                 prefetched): a stable per-bin ranking (per-wave peer masks + wave prefix), the
-//                 tile's cold commands as a bin-sorted image in LDS, copied out as one contiguous
-//                 run per bin of 16-byte records (the key's hash with the command's class in its
-//                 two top bits - bin bits the partition implies - and the value); per command its
-//                 index in the tile image (ipos, log order)
-//   k_ap_resolve_list  one workgroup per bin: its table slice in LDS (key hashes, values,
-//                 state), the bin's records streamed in log order 2048 at a time (the next batch
+//                 prefetched), per 4096-command log tile: a stable per-bin ranking of the cold
+//                 commands (per-wave peer masks + wave prefix), the tile's bin-sorted IMAGE of
+//                 16-byte records (the key's hash with the command's class in its two top bits -
+//                 bin bits the partition implies - and the value) built in LDS and stored whole at
+//                 the tile's own place; the tile's row: commands per bin, the bins' image starts,
+//                 per hot key the last position of any command and of a PUT; per command its index
+//                 in the tile image (ipos, log order)
+//   scans         k_ap_scan_part / _top / _bins / _rows over the tile rows: the runs' partition
+//                 offsets per tile (sums), hot positions before each tile (maxima)
+//   k_ap_runs     the rows transposed into the bin-major run table: per (bin, tile) the run's
+//                 partition offset and its image offset
+//   k_ap_resolve_list  one workgroup per bin (XCD-contiguous bins): its table slice in LDS (key
+//                 hashes, values, state), the bin's records in log order 2048 at a time, gathered
+//                 from the tile images through a window of the run table (the next batch
 //                 prefetched); every record of a batch at once finds its slot and joins its slot's
 //                 list of the batch, then walks the list (or, for a slot with many records, reads
-//                 two bitmaps) for its predecessor and last earlier PUT; results stored in
-//                 partition order; touched slots written back once
+//                 two bitmaps) for its predecessor and last earlier PUT; results stored at the
+//                 records' image positions; touched slots written back once
 //   k_ap_hot_commit  the hot keys' final value and state
-//   k_ap_emit     per tile, log order: the tile's cold results gathered run by run into an LDS
-//                 image (each image position's run found by a binary search of the tile's run
-//                 starts, from the scanned rows), read back by ipos; a hot command's from the
-//                 per-wave peer scan, the earlier waves' tables and the tile's incoming
-//                 positions; ret / conf stored coalesced
+//   k_ap_emit     per tile, log order: the tile's cold results - its own image slots, one
+//                 contiguous run - into LDS, read back by ipos; a hot command's from the per-wave
+//                 peer scan, the earlier waves' tables and the tile's incoming positions; ret /
+//                 conf stored coalesced
 // Table traffic is one read and one write of each bin's slice per call instead of one random probe
 // per command. New keys: any command on a key the slice does not hold claims a slot for it (a GET
 // before the first PUT of a new key is still that PUT's predecessor); slots whose key never
