@@ -766,7 +766,6 @@ __device__ __forceinline__ int64_t kv_lo_hi(int lo, int hi) {
 #ifndef MPX_RES_IMG
 #define MPX_RES_IMG 1
 #endif
-static_assert(!(MPX_RES_IMG && MPX_RES16), "one result layout");
 // diagnostic build: wave 0's clock per phase of k_ap_resolve_list, printed by bin 0
 #ifndef MPX_RL_STAMP
 #define MPX_RL_STAMP 0
@@ -1497,8 +1496,14 @@ __global__ __launch_bounds__(kTT) void k_ap_emit(ApGeo g, const uint8_t* __restr
         for (int u = 0; u < kTPer; ++u) {
             const uint32_t i = tid + u * kTT;
             const bool any = i - (uint32_t)l < nc;  // (wave-uniform)
+#if MPX_RES16
+            const int4 rr = any ? reinterpret_cast<const int4*>(r_ret)[r0 + i] : make_int4(0, 0, 0, 0);
+            xr[u] = kv_lo_hi(rr.x, rr.y);
+            c[u] = (uint8_t)rr.z;
+#else
             xr[u] = any ? r_ret[r0 + i] : 0;
             c[u] = any ? r_conf[r0 + i] : 0;
+#endif
         }
 #pragma unroll
         for (int u = 0; u < kTPer; ++u) {
