@@ -1,0 +1,47 @@
+"""Extended randomised sweep of the partitioned apply pipeline (apply_fast.hip), run on demand
+(MPX_FUZZ_EXT=<seeds>, e.g. 120; skipped otherwise so the default GPU suite keeps its time):
+larger calls than test_gpu_fuzz.py's (up to 2^21 commands, so a bin's batches cross the run
+window of the resolve several times), table sizes from 4 bins to super-bins, chunked calls, and
+key mixes that leave most tiles' runs of a bin empty (the skewed cases) or long (tiny key spaces).
+Every call's results and the final table against the oracle.
+
+References: Command.Execute / executeCommands (state.go:77-103, bareminpaxos.go:1066-1098),
+state.Conflict (state.go:53-60)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle_lib import Oracle
+from minpaxos_amd import records as R
+from test_gpu_fuzz import _commands
+
+pytestmark = pytest.mark.gpu
+
+_N = int(os.environ.get("MPX_FUZZ_EXT", "0") or 0)
+
+
+@pytest.mark.skipif(_N == 0, reason="set MPX_FUZZ_EXT=<seeds> to run the extended sweep")
+@pytest.mark.parametrize("seed", range(max(_N, 1)))
+def test_fuzz_apply_partitioned_ext(mk_engine, seed):
+    rng = np.random.default_rng(91000 + seed)
+    cap = 1 << int(rng.integers(10, 23))
+    chunk = int(rng.choice([0, 0, 0, 200000, 1 << 20]))
+    e = mk_engine(5, R.MODE_MIN, kv_capacity=cap, apply_path=R.APPLY_PARTITIONED,
+                  apply_chunk=chunk)
+    o = Oracle(5, R.MODE_MIN)
+    for call in range(3):
+        m = int(rng.integers(20000, 1 << 21))
+        space = int(rng.integers(1, cap // 2 + 1))
+        if rng.random() < 0.15:
+            space = int(rng.integers(1, 64))  # long runs per tile and bin
+        kind = ["uniform", "zipf", "hot", "special"][int(rng.integers(0, 4))]
+        op, key, val = _commands(rng, m, space, kind)
+        gr, gc = e.apply(op, key, val)
+        wr, wc = o.apply(op, key, val)
+        tag = (seed, call, cap, chunk, m, space, kind)
+        assert np.array_equal(gr, wr), (tag, np.nonzero(gr != wr)[0][:5])
+        assert np.array_equal(gc, wc), (tag, np.nonzero(gc != wc)[0][:5])
+    gk, gv = e.kv_export()
+    wk, wv = o.kv_export()
+    assert np.array_equal(gk, wk) and np.array_equal(gv, wv), seed
