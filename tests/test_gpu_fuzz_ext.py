@@ -45,3 +45,37 @@ def test_fuzz_apply_partitioned_ext(mk_engine, seed):
     gk, gv = e.kv_export()
     wk, wv = o.kv_export()
     assert np.array_equal(gk, wk) and np.array_equal(gv, wv), seed
+
+
+@pytest.mark.skipif(_N == 0, reason="set MPX_FUZZ_EXT=<seeds> to run the extended sweep")
+@pytest.mark.parametrize("seed", range(max(_N // 4, 1)))
+def test_fuzz_conflict_batch_ext(mk_engine, seed):
+    """ConflictBatch (state.go:62-71) over ragged instances - empty ones, instances past the
+    register path's 4 commands, workgroup ranges past the LDS staging - with the key and op
+    arrays at every alignment the device form allows (the kernel stages from the 16-byte
+    boundary below each workgroup's range)"""
+    from minpaxos_amd.devbuf import Arena
+    import gen_cases
+    rng = np.random.default_rng(93000 + seed)
+    e, o = mk_engine(5, R.MODE_MIN), Oracle(5, R.MODE_MIN)
+    n_inst = int(rng.integers(2, 40000))
+    hi = int(rng.choice([3, 5, 9, 17]))
+    sizes = rng.integers(0, hi, n_inst)
+    if rng.random() < 0.3:
+        sizes[rng.integers(0, n_inst, 8)] = rng.integers(20, 3000, 8)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    m = int(off[-1])
+    op, key, _ = gen_cases.commands_mixed(rng, max(m, 1), int(rng.integers(1, 5000)),
+                                          neg_keys=bool(rng.random() < 0.5))
+    op, key = op[:m], key[:m]
+    want = o.conflict_batch(op, key, off)
+    ks, os_ = int(rng.integers(0, 2)), int(rng.integers(0, 16))
+    with Arena(e) as ar:
+        d_key = ar.put(np.concatenate([np.zeros(ks, np.int64), key]))
+        d_op = ar.put(np.concatenate([np.zeros(os_, np.uint8), op]))
+        d_off = ar.put(off)
+        d_out = ar.full(n_inst, np.uint8, 0xEE)
+        e.conflict_batch_dev(d_op.at(os_), d_key.at(ks), d_off.ptr, n_inst, d_out.ptr)
+        e.stream_synchronize(None)
+        got = ar.get(d_out, n_inst - 1)
+    assert np.array_equal(got, want), (seed, np.nonzero(got != want)[0][:5])
