@@ -29,6 +29,7 @@
 #include "common.hpp"
 #include "kernels.hpp"
 
+
 namespace mpx {
 
 namespace {
@@ -38,16 +39,19 @@ constexpr int kE = MPX_DECODE_WINDOW;   // entry offsets per chunk map
 constexpr int kTL = 128;                // chunks (lanes) per tile
 constexpr int kTB = kC * kTL;           // tile bytes
 constexpr int kGT = 256;                // tiles per group
+#ifndef MPX_SD_VARLDS
+#define MPX_SD_VARLDS 1
+#endif
 constexpr int kDRow = kC + 4;           // LDS row of a chunk's DP (bank-conflict padding)
 constexpr uint8_t kTerm = 0xFF;         // terminal (tree levels >= 1, tile / group maps)
 constexpr uint8_t kDeadE = 0xFF;        // no entry (past the stop)
-static_assert(kE == 64 && kE + kC <= 255, "u8 DP encoding: exit offsets, then terminals");
+static_assert(kE == 64 && kE + kC <= 255, "u8 DP encoding: landings < kC + kE, 0xFF terminal");
 
 enum { kOk = 0, kPartial = 1, kMalformed = 2, kBeyond = 3 };
 
 
 // fixed frame length by code (code byte included), 0 = variable-length message
-__device__ __forceinline__ uint32_t flen(uint32_t code, int proto) {
+__host__ __device__ __forceinline__ uint32_t flen(uint32_t code, int proto) {
     switch (code) {
     case MPX_PEER_BEACON:
     case MPX_PEER_BEACON_REPLY: return 9;
@@ -213,32 +217,22 @@ __device__ __forceinline__ uint32_t lut_len(uint64_t lut, uint32_t code) {
     return (((uint32_t)(lut >> ((i & 7u) * 8u)) & 0xFFu) & in) | (1u & ~in);
 }
 
-// Phase 1 (variable-length messages only): the bounded parse of every variable-message code of
-// the lane's chunk (bytes through L2); D[p] = its landing in the DP's byte encoding (dp_enc).
-__device__ __noinline__ void var_lengths(const Bytes by, uint64_t len, uint64_t c0,
-                                         uint64_t lim, int proto, uint64_t m_lo, uint64_t m_hi,
-                                         uint8_t* D) {
-    for (int h = 0; h < 2; ++h) {
-        uint64_t m = h ? m_hi : m_lo;
-        while (m) {
-            const int p = __ffsll((long long)m) - 1 + 64 * h;
-            m &= m - 1;
-            const VarRes r = parse_var(by, len, lim, c0 + (uint64_t)p, proto);
-            const uint32_t q = (uint32_t)p + r.f.len;  // len <= kC + kE - 1 - p (the limit)
-            D[p] = (uint8_t)(r.st == kOk && q < (uint32_t)(kC + kE) ? q : 0xFFu);
-        }
-    }
-}
 
 // The DP's byte per position p (dp_enc): the landing q = p + length of the frame at p, which
 // is < kC for a landing inside the chunk (its value is D[q]), in [kC, kC + kE) for an exit (bit 7
-// set, bit 6 clear: exit q - kC), and 0xFF for a terminal at p (value kE + p).
+// set, bit 6 clear: exit q - kC), and 0xFF for a terminal at p. The chunk map stores an exit as
+// its offset (< kE) and a terminal as 0x7F (>= kE): the walk, the one reader of a terminal's
+// position, re-scans its stop chunk (chunk_terminal).
 //
 // Phase 2a: the landings of the fixed-length frames, four positions per dword of chunk bytes.
 // v_perm_b32 looks the four codes up in an 8-byte table of length - 1 (0x7F for a variable
 // message) indexed by code - MPX_PEER_BEACON; every other code selects 0x00 or 0xFF, cleared to
 // 0 (a 1-byte frame); the positions are added bytewise (no carries: <= 0x7F + 128). Returns the
-// dword of landings; *var gets the variable-message positions as 4 bits.
+// dword of landings; *var gets bit 7 of every variable-message byte (var_bits).
+__device__ __forceinline__ uint32_t var_bits(uint32_t y2) {  // y2 bytes == 0x7F -> 0x80
+    const uint32_t z = y2 ^ 0x7F7F7F7Fu;
+    return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z | 0x7F7F7F7Fu);
+}
 __device__ __forceinline__ uint32_t dp_landings(uint32_t w, uint32_t lut_lo, uint32_t lut_hi,
                                                 uint32_t pos4, uint32_t* var) {
     const uint32_t h = w & 0x80808080u;
@@ -246,16 +240,157 @@ __device__ __forceinline__ uint32_t dp_landings(uint32_t w, uint32_t lut_lo, uin
     const uint32_t y = __builtin_amdgcn_perm(lut_hi, lut_lo, sel);
     const uint32_t hb = y & 0x80808080u;
     const uint32_t y2 = y & ~(hb | (hb - (hb >> 7)));  // 0xFF bytes (out of the table) -> 0
-    const uint32_t z = y2 ^ 0x7F7F7F7Fu;                // zero bytes = variable messages
-    const uint32_t t = ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z | 0x7F7F7F7Fu);
-    *var = (((t >> 7) * 0x204081u) >> 21) & 0xFu;
+    *var = var_bits(y2);
     return y2 + pos4;
 }
 static_assert(MPX_PEER_BEACON == 6, "dp_landings indexes the table by code - 6");
 
-// the byte mask of the 4 variable-message bits of a dword
-__device__ __forceinline__ uint32_t var_bytes(uint32_t nib) {
-    return ((nib * 0x204081u) & 0x01010101u) * 0xFFu;
+// 0xFF in every byte whose bit 7 is set (bytes of 0x80 / 0x00 from var_bits)
+__device__ __forceinline__ uint32_t byte_mask(uint32_t b7) { return b7 | (b7 - (b7 >> 7)); }
+
+// binary.ReadVarint's unsigned part at *pos (relative), every read below e; false = a failure
+// (past e, or malformed: errOverflow / more than 10 bytes)
+template <class ByteAt>
+__host__ __device__ __forceinline__ bool uvarint_at(const ByteAt& R, uint32_t* pos, uint32_t e, uint64_t* x) {
+    uint64_t v = 0;
+    uint32_t sh = 0;
+#pragma unroll 1
+    for (int i = 0; i < 10; ++i) {
+        if (*pos >= e) return false;
+        const uint32_t b = R(*pos);
+        ++*pos;
+        if (b < 0x80u) {
+            if (i == 9 && b > 1u) return false;
+            *x = v | ((uint64_t)b << sh);
+            return true;
+        }
+        v |= (uint64_t)(b & 0x7fu) << sh;
+        sh += 7;
+    }
+    return false;
+}
+// The landing (relative to the chunk) of the variable-length message at p, or 0xFF: exactly
+// "parse_var(limit = c0 + kC + kE - 1) is kOk and the frame ends before kC + kE" (every other
+// outcome - partial, malformed, past the limit - is a terminal), restated for that one question:
+// e = min(len - c0, kC + kE - 1) bounds every read and the frame's end, a zigzag varint is
+// negative iff odd, and a catch-up log of m instances needs at least 9m bytes (so m beyond what
+// is left ends at a terminal however its instances parse). No VarInfo, no second header parse,
+// 32-bit positions: the DP parses every byte 9 / 10 / 12 of the stream as a frame start.
+template <class ByteAt>
+__host__ __device__ __forceinline__ uint32_t var_land(const ByteAt& R, uint32_t p, uint32_t e, int proto) {
+    const uint32_t code = R(p);
+    uint32_t pos = p + 1 + var_hdr(code, proto);
+    if (pos > e) return 0xFFu;
+    uint64_t x;
+    if (!uvarint_at(R, &pos, e, &x) || (x & 1u)) return 0xFFu;  // n < 0: make() panics
+    if ((x >> 1) > (uint64_t)((e - pos) / 17)) return 0xFFu;
+    pos += 17 * (uint32_t)(x >> 1);
+    if (proto == MPX_MODE_MIN && code != MPX_PEER_COMMIT) {  // CatchUpLog
+        if (!uvarint_at(R, &pos, e, &x) || (x & 1u)) return 0xFFu;
+        if ((x >> 1) > (uint64_t)((e - pos) / 9)) return 0xFFu;
+#pragma unroll 1
+        for (uint32_t m = (uint32_t)(x >> 1); m; --m) {  // Instance: Ballot, Status, V(k), k Commands
+            if (pos + 8 > e) return 0xFFu;
+            pos += 8;
+            if (!uvarint_at(R, &pos, e, &x) || (x & 1u)) return 0xFFu;
+            if ((x >> 1) > (uint64_t)((e - pos) / 17)) return 0xFFu;
+            pos += 17 * (uint32_t)(x >> 1);
+        }
+    }
+    return pos;
+}
+
+// Phase 2a' (a chunk holding a variable-message code byte - any byte 9, 10 or 12, at the
+// positions of other frames' payload too: ~12 per 64 chunks of the bench's MIN stream, runs of
+// ~9 per chunk where an instance number has such a byte): the bounded parse of each, D[p] = the
+// frame's landing, or 0xFF: a terminal (unparseable, landing kE or more bytes into the next
+// chunk, or legacy mode, which stops at every variable-length message).
+// The wave's positions are one task list: each lane's positions were its own serial loop, so a
+// wave took as many rounds as its busiest lane, each as long as its deepest parse (catch-up
+// logs over zero-rich payload: ~20 dependent reads). Tasks (lane << 7 | position, u16) go to
+// T[kVarTasks] (the workgroup's G, free until the DP is done); lane j parses tasks j, j + 64,
+// ... The parse reads the rows' raw bytes (MPX_SD_VARLDS, written before the landings; a chunk's
+// next-chunk bytes from the next row when that is the same wave's, else through L2), so a row's
+// raw bytes must outlive every parse of the wave: the results wait in registers (a byte per
+// round) and are stored after the last round. More than kVarTasks positions (a var-dense wave)
+// go a window at a time, bytes through L2, results stored at once. The loops stay rolled: an
+// unrolled form was ~30 KB of code. Round 6 (profiles/r06/stream/): MIN 0.63-0.65 -> 0.47-0.51
+// ms per k_sd_tile_maps call, CLASSIC 0.44-0.46 -> 0.34-0.36 with the leaner DP init and
+// var_land; the rows-vs-L2 choice measured within noise (SD_STAMP still shows 10-80K cycles of
+// a wave's ~12 parses: dependent reads in a wave that shares its SIMD with three others).
+constexpr uint32_t kVarTasks = 256;
+static_assert(kVarTasks <= 4 * 64, "a byte of q per round");
+struct TileBytes {  // a chunk's bytes [0, kC + kE): its row and the next row (null: L2)
+    const uint8_t* row;
+    const uint8_t* next;
+    const uint8_t* g;  // the chunk's first byte in global memory
+    __host__ __device__ __forceinline__ uint32_t operator()(uint32_t i) const {
+        if (i < (uint32_t)kC) return row ? row[i] : g[i];
+        return next ? next[i - kC] : g[i];
+    }
+};
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ uint32_t var_wave(const SParams P, uint64_t t0, uint64_t m_lo, uint64_t m_hi,
+                                          uint8_t (*D)[kDRow], uint16_t* T) {
+    const uint32_t ln = threadIdx.x & 63u, w0 = threadIdx.x & ~63u;
+    const uint32_t cnt = (uint32_t)(__popcll(m_lo) + __popcll(m_hi));
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(incl, d, 64);
+        if (ln >= (uint32_t)d) incl += t;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    const bool lds = MPX_SD_VARLDS && total <= kVarTasks;
+    for (uint32_t base = 0; base < total; base += kVarTasks) {
+        const uint32_t n = min(total - base, kVarTasks);
+        uint32_t o = incl - cnt;  // this lane's first task index
+        if (o < base + n && o + cnt > base) {
+            for (int h = 0; h < 2; ++h) {
+                uint64_t m = h ? m_hi : m_lo;
+                while (m) {
+                    const uint32_t p = (uint32_t)(__ffsll((long long)m) - 1 + 64 * h);
+                    m &= m - 1;
+                    if (o >= base && o < base + n) T[o - base] = (uint16_t)((ln << 7) | p);
+                    ++o;
+                }
+            }
+        }
+        wave_sync();
+        uint32_t q = 0;  // the rounds' results, a byte each (at most 4 rounds), stored after the last
+#pragma unroll 1
+        for (uint32_t j = ln; j < ((n + 63u) & ~63u); j += 64) {
+            uint32_t v = 0xFFu;
+            if (j < n && !P.legacy) {
+                const uint32_t tk = T[j], src = w0 + (tk >> 7), p = tk & 127u;
+                const uint64_t cs = t0 + (uint64_t)src * kC;
+                const uint32_t e = (uint32_t)min(P.len - cs, (uint64_t)(kC + kE - 1));
+                const TileBytes R{lds ? D[src] : nullptr, lds && (src & 63u) != 63u ? D[src + 1] : nullptr,
+                                  P.buf + cs};
+                v = var_land(R, p, e, P.proto);
+            }
+            if (lds) {
+                q |= v << (8 * (j >> 6));
+            } else if (j < n) {
+                const uint32_t tk = T[j];
+                D[w0 + (tk >> 7)][tk & 127u] = (uint8_t)v;
+            }
+        }
+        if (lds) {
+            wave_sync();
+#pragma unroll 1
+            for (uint32_t j = ln; j < n; j += 64) {
+                const uint32_t tk = T[j];
+                D[w0 + (tk >> 7)][tk & 127u] = (uint8_t)(q >> (8 * (j >> 6)));
+            }
+        }
+        wave_sync();
+    }
+    return total;
 }
 
 // the table of dp_landings for a protocol (kLutMin / kLutClassic: lengths by code - 6)
@@ -270,8 +405,11 @@ __host__ __device__ constexpr uint64_t dp_table(uint64_t lut) {
 
 // Phase 2b: the backward DP over the chunk's positions, in the lane's LDS row, with every
 // position a pointer: a position whose value is final (an exit or a terminal, bit 7 of its
-// landing byte) gets that value written to its own row byte first and points at itself, the
-// finals made four at a time (bytewise masks from bits 7 and 6). A position is then a byte
+// landing byte) gets that value written to its own row byte first and points at itself. The
+// row is the landings with bit 7 flipped (an exit 128 + e becomes e, a terminal 0xFF becomes
+// 0x7F, the rest is overwritten by the DP) and the self-pointers one v_perm_b32 mask (the sign
+// bits of the four bytes) and one bitwise select: 4 VALU ops per dword instead of the ~17 of
+// round 4's form, which kept each terminal's position (kE + p). A position is then a byte
 // extract, the LDS read of its landing's value (already final: landings lie ahead) and the LDS
 // write of its own: ~3 VALU ops. Round 3's 64-register window compiled to ~45 VALU ops per
 // position and round 4's LDS form with a per-position length lookup and selects to ~25 (the
@@ -283,13 +421,11 @@ __device__ __forceinline__ void chunk_dp_self(uint32_t (&pw)[kC / 4], uint8_t* D
 #pragma unroll
     for (int i = 0; i < kC / 4; ++i) {
         const uint32_t x = pw[i];
-        const uint32_t f = x & 0x80808080u;
-        const uint32_t fmask = f | (f - (f >> 7));                  // finals
-        const uint32_t t = (x & (f >> 1)) & 0x40404040u;            // terminals
-        const uint32_t tmask = (t << 1) | ((t << 1) - (t >> 6));
+        // 0xFF per final byte: v_perm_b32 selectors 8..11 replicate bit 15 / 31 / 47 / 63 of
+        // {x, x << 8}, i.e. bit 7 of bytes 0, 2 (of x << 8) and 1, 3 (of x)
+        const uint32_t fmask = __builtin_amdgcn_perm(x, x << 8, 0x0B090A08u);
         const uint32_t self = (uint32_t)(4 * i) * 0x01010101u + 0x03020100u;
-        const uint32_t term = self + 0x40404040u;  // kE + p
-        row[i] = (x & 0x3F3F3F3Fu & ~tmask) | (term & tmask);
+        row[i] = x ^ 0x80808080u;
         pw[i] = (x & ~fmask) | (self & fmask);
     }
 #pragma unroll
@@ -322,11 +458,28 @@ __device__ __forceinline__ void chunk_groups(const uint8_t* X, int xstride, uint
     }
 }
 
-__global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
-    // var lengths, then the DP; rows padded to 33 dwords so the 64 lanes of a wave, each on its
-    // own row, hit 64 different banks (a 128-byte stride put every lane on two banks)
+// diagnostic build (-DMPX_SD_STAMP=1): one wave's clock per phase of k_sd_tile_maps, printed
+// for a few sample workgroups
+#ifndef MPX_SD_STAMP
+#define MPX_SD_STAMP 0
+#endif
+#if MPX_SD_STAMP
+#define SD_STAMP(k) sd_t[k] = clock64()
+#else
+#define SD_STAMP(k) do {} while (0)
+#endif
+
+__global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(4))) void k_sd_tile_maps(SParams P, Work W) {
+#if MPX_SD_STAMP
+    unsigned long long sd_t[8];
+    sd_t[0] = clock64();
+#endif
+    // the chunk's bytes (+ halo), var lengths, then the DP; rows padded to an odd dword count so
+    // the 64 lanes of a wave, each on its own row, hit 64 different banks (a 128-byte stride put
+    // every lane on two banks)
     __shared__ __attribute__((aligned(16))) uint8_t D[kTL][kDRow];
-    __shared__ uint8_t G[kTL / 8][kE];
+    __shared__ __attribute__((aligned(16))) uint8_t G[kTL / 8][kE];
+    static_assert(kTL / 8 * kE >= 2 * kVarTasks * 2, "the var task lists fit G");
     const int l = threadIdx.x;
     const uint64_t t0 = (uint64_t)blockIdx.x * kTB;
     const uint64_t c0 = t0 + (uint64_t)l * kC;
@@ -352,28 +505,54 @@ __global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
             wd[i] = x;
         }
     }
+#if MPX_SD_VARLDS
+    {   // the raw chunk into its row (the variable-message parse's bytes; wave-local readers)
+        uint32_t* row = reinterpret_cast<uint32_t*>(D[l]);
+#pragma unroll
+        for (int i = 0; i < kC / 4; ++i) row[i] = wd[i];
+    }
+#endif
     const uint64_t tab = P.proto == MPX_MODE_MIN ? dp_table(kLutMin) : dp_table(kLutClassic);
     const uint32_t tab_lo = (uint32_t)tab, tab_hi = (uint32_t)(tab >> 32);
-    uint64_t m_lo = 0, m_hi = 0;  // positions of variable-message codes
+    uint32_t any_var = 0;  // bit 7 of the chunk's variable-message bytes, OR-ed
 #pragma unroll
     for (int i = 0; i < kC / 4; ++i) {
-        uint32_t nib;
+        uint32_t vb;
         const uint32_t pos4 = (uint32_t)(4 * i + 1) * 0x01010101u + 0x03020100u;
-        wd[i] = dp_landings(wd[i], tab_lo, tab_hi, pos4, &nib);
-        if (P.legacy) wd[i] |= var_bytes(nib);  // stop at variable-length messages: terminal
-        if (i < 16) m_lo |= (uint64_t)nib << (4 * i); else m_hi |= (uint64_t)nib << (4 * (i - 16));
+        wd[i] = dp_landings(wd[i], tab_lo, tab_hi, pos4, &vb);
+        any_var |= vb;
     }
-    if (!P.legacy && (m_lo | m_hi)) {
-        const Bytes vby{P.buf, nullptr, 0, 0};
-        var_lengths(vby, P.len, c0, c0 + kC + kE - 1, P.proto, m_lo, m_hi, D[l]);
+    SD_STAMP(1);
+    {
+        const bool wv = __ballot(any_var != 0) != 0;  // (wave-uniform)
+        uint16_t* T = reinterpret_cast<uint16_t*>(&G[0][0]) + (l >> 6) * kVarTasks;
+        uint64_t m_lo = 0, m_hi = 0;
+        if (any_var) {  // positions from the landings (a variable message's is its position + 128)
+#pragma unroll
+            for (int i = 0; i < kC / 4; ++i) {
+                const uint32_t pos4 = (uint32_t)(4 * i + 1) * 0x01010101u + 0x03020100u;
+                const uint32_t t = var_bits(wd[i] - pos4) >> 7;  // 0x01 per variable-message byte
+                const uint64_t nib = (uint64_t)((t | (t >> 7) | (t >> 14) | (t >> 21)) & 0xFu);
+                if (i < 16) m_lo |= nib << (4 * i); else m_hi |= nib << (4 * (i - 16));
+            }
+        }
+        const uint32_t vt = wv ? var_wave(P, t0, m_lo, m_hi, D, T) : 0u;
+#if MPX_SD_STAMP
+        sd_t[7] = vt;
+#else
+        (void)vt;
+#endif
+    }
+    if (any_var) {
         const uint32_t* row = reinterpret_cast<const uint32_t*>(D[l]);
 #pragma unroll
         for (int i = 0; i < kC / 4; ++i) {
-            const uint32_t nib = (uint32_t)((i < 16 ? m_lo >> (4 * i) : m_hi >> (4 * (i - 16))) & 0xFu);
-            const uint32_t vm = var_bytes(nib);
+            const uint32_t pos4 = (uint32_t)(4 * i + 1) * 0x01010101u + 0x03020100u;
+            const uint32_t vm = byte_mask(var_bits(wd[i] - pos4));
             wd[i] = (wd[i] & ~vm) | (row[i] & vm);
         }
     }
+    SD_STAMP(2);
     if (c0 + kC + 17 + kE > P.len) {  // the end of the buffer: terminals (rare, per position)
 #pragma unroll
         for (int p = 0; p < kC; ++p) {
@@ -382,7 +561,9 @@ __global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
             if (a >= P.len || (x < 0xC0u && a + (x - (uint32_t)p) > P.len)) wd[p >> 2] |= 0xFFu << sh;
         }
     }
+    SD_STAMP(3);
     chunk_dp_self(wd, D[l]);
+    SD_STAMP(4);
     {  // this chunk's map (64 bytes) for the emit pass and the walk
         const uint32_t* src = reinterpret_cast<const uint32_t*>(D[l]);
         uint4* dst = reinterpret_cast<uint4*>(W.cmap + ((uint64_t)blockIdx.x * kTL + l) * kE);
@@ -391,6 +572,7 @@ __global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
             dst[i] = make_uint4(src[4 * i], src[4 * i + 1], src[4 * i + 2], src[4 * i + 3]);
     }
     __syncthreads();
+    SD_STAMP(5);
     chunk_groups(&D[0][0], kDRow, G);
     __syncthreads();
     {  // the tile map: the first and second 8 group maps composed by two halves of the
@@ -408,6 +590,13 @@ __global__ __launch_bounds__(kTL) void k_sd_tile_maps(SParams P, Work W) {
             W.tmap[(uint64_t)blockIdx.x * kE + l] =
                 (uint8_t)(y >= (uint32_t)kE ? (uint32_t)kTerm : G[1][y]);
         }
+#if MPX_SD_STAMP
+        SD_STAMP(6);
+        if ((blockIdx.x & 2047) == 1025 && (l & 63) == 0)
+            printf("SD_STAMP blk %u wave %d: land %llu var %llu (tasks %llu) eob %llu dp %llu store+bar %llu groups+tmap %llu\n",
+                   blockIdx.x, l >> 6, sd_t[1] - sd_t[0], sd_t[2] - sd_t[1], sd_t[7], sd_t[3] - sd_t[2],
+                   sd_t[4] - sd_t[3], sd_t[5] - sd_t[4], sd_t[6] - sd_t[5]);
+#endif
     }
 }
 
@@ -457,7 +646,7 @@ __global__ __launch_bounds__(kParts * kE) void k_sd_group_maps(Work W, uint32_t 
 // and chunk, then thread 0 classifies the frame at the terminal byte and writes the result.
 // The run's first map at which the chain from entry e0 reaches a terminal: part maps, the parts
 // chained by thread 0, then thread 0 walks the terminal part. S[k][e] >= kE is a terminal (kTerm
-// in tile / group maps, kE + byte in chunk maps). Thread 0 gets (map index, entry into it,
+// in tile / group maps, 0x7F in chunk maps). Thread 0 gets (map index, entry into it,
 // the terminal value); every chain reaches one (at the latest the end of the buffer).
 __device__ __forceinline__ void first_terminal(const uint8_t (*S)[kE], uint32_t n, uint32_t e0,
                                                uint8_t (*Q)[kE], uint32_t* k_out,
@@ -483,6 +672,30 @@ __device__ __forceinline__ void first_terminal(const uint8_t (*S)[kE], uint32_t 
         *v_out = v;
     }
 }
+// The position in the chunk at c0 where the chain entering at e reaches its terminal, by the
+// rules k_sd_tile_maps' DP applies (the chunk maps store a terminal without its position): the
+// end of the buffer, a frame past it, a legacy-mode or unparseable variable-length message, or
+// one landing kE or more bytes into the next chunk. Thread 0 of the walk, once per call.
+__device__ uint32_t chunk_terminal(const SParams& P, uint64_t c0, uint32_t e) {
+    const Bytes by{P.buf, nullptr, 0, 0};
+    uint32_t p = e;
+    while (p < (uint32_t)kC) {  // p increases: every frame is at least a byte
+        const uint64_t a = c0 + p;
+        if (a >= P.len) return p;
+        const uint32_t code = P.buf[a];
+        uint32_t fl = flen(code, P.proto);
+        if (!fl) {
+            if (P.legacy) return p;
+            const VarRes r = parse_var(by, P.len, c0 + kC + kE - 1, a, P.proto);
+            if (r.st != kOk || p + r.f.len >= (uint32_t)(kC + kE)) return p;
+            fl = r.f.len;
+        }
+        if (a + fl > P.len) return p;
+        p += fl;
+    }
+    return p;  // (an exit: not reached for a chain the maps end at a terminal)
+}
+
 __global__ __launch_bounds__(kParts * kE) void k_sd_walk(SParams P, Work W, uint32_t n_tiles,
                                                          uint32_t n_groups, mpx_stream_result* res) {
     __shared__ __attribute__((aligned(16))) uint8_t S[kGT][kE];
@@ -555,8 +768,9 @@ __global__ __launch_bounds__(kParts * kE) void k_sd_walk(SParams P, Work W, uint
     first_terminal(S, kTL, te, Q, &fk[0], &fk[1], &fk[2]);
     __syncthreads();
     if (t == 0) {
-        const uint32_t cs = fk[0], v = fk[2];
-        const uint64_t s = (uint64_t)ts * kTB + (uint64_t)cs * kC + (v - kE);  // terminal byte
+        const uint32_t cs = fk[0];
+        const uint64_t cb = (uint64_t)ts * kTB + (uint64_t)cs * kC;
+        const uint64_t s = cb + chunk_terminal(P, cb, fk[1]);  // terminal byte
         int32_t why, code = -1;
         uint64_t next = s;
         VarInfo f{0, 0, 0, 0, 0};

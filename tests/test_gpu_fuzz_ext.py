@@ -1,4 +1,4 @@
-"""Extended randomised sweep of the partitioned apply pipeline (apply_fast.hip), run on demand
+"""Extended randomised sweeps, run on demand: the partitioned apply pipeline (apply_fast.hip),
 (MPX_FUZZ_EXT=<seeds>, e.g. 120; skipped otherwise so the default GPU suite keeps its time):
 larger calls than test_gpu_fuzz.py's (up to 2^21 commands, so a bin's batches cross the run
 window of the resolve several times), table sizes from 4 bins to super-bins, chunked calls, and
@@ -79,3 +79,52 @@ def test_fuzz_conflict_batch_ext(mk_engine, seed):
         e.stream_synchronize(None)
         got = ar.get(d_out, n_inst - 1)
     assert np.array_equal(got, want), (seed, np.nonzero(got != want)[0][:5])
+
+
+def _var_dense(rng, n):
+    """bytes from a small alphabet of variable-message codes, zeros and small even numbers: most
+    positions parse as frame starts, catch-up logs run deep over the zeros, and a wave's chunks
+    hold far more than the framing DP's task window (256 positions)"""
+    alpha = np.array([9, 10, 12, 0, 0, 0, 2, 4, 6, 13, 0x80, 1], np.uint8)
+    return alpha[rng.integers(0, len(alpha), n)].tobytes()
+
+
+@pytest.mark.skipif(_N == 0, reason="set MPX_FUZZ_EXT=<seeds> to run the extended sweep")
+@pytest.mark.parametrize("seed", range(max(_N // 4, 1)))
+def test_fuzz_stream_decode_ext(mk_engine, seed):
+    """The full peer-stream decode (replicaListener + every Unmarshal, genericsmr.go:402-446,
+    minpaxosprotomarsh.go:352-387 / :470-507 / :648-672) on streams built to stress the framing
+    DP's variable-message pass: var-dense byte soups, leader streams whose instance numbers
+    carry 9 / 10 / 12 bytes (ballot 0: zero-rich payload), random frame mixes with most frames
+    variable, pieces of each concatenated, cut at random places, both wire formats"""
+    from minpaxos_amd import wire as W
+    from minpaxos_amd import synth
+    rng = np.random.default_rng(95000 + seed)
+    for proto in (R.MODE_MIN, R.MODE_CLASSIC):
+        e, o = mk_engine(5, proto), Oracle(5, proto)
+        parts = []
+        for _ in range(int(rng.integers(1, 5))):
+            k = int(rng.integers(0, 4))
+            if k == 0:
+                parts.append(_var_dense(rng, int(rng.integers(1, 1 << 20))))
+            elif k == 1:
+                n = int(rng.integers(1, 1 << 16))
+                base = int(rng.choice([0x0A00, 0x090000, 0x0C0C00, int(rng.integers(0, 1 << 24))]))
+                recs, _ = synth.accept_replies(n, 5, 0.7, seed=int(rng.integers(0, 1 << 30)),
+                                               inst_base=base, ballot=int(rng.choice([0, 16, 10])))
+                parts.append(bytes(W.leader_stream(proto, recs, prepare_every=int(rng.integers(1, 300)),
+                                                   n_cmds=int(rng.integers(0, 3)))))
+            elif k == 2:
+                parts.append(W.random_stream(proto, rng, int(rng.integers(1, 20000)),
+                                             p_var=float(rng.uniform(0.5, 0.95)), max_cmds=3,
+                                             p_big=0.0, max_log=6, p_unknown=0.02))
+            else:
+                parts.append(rng.integers(0, 256, int(rng.integers(1, 1 << 18)), dtype=np.uint8).tobytes())
+        b = b"".join(parts)
+        for cut in (len(b), int(rng.integers(0, len(b) + 1))):
+            got, want = e.decode_stream(b[:cut]), o.decode_stream(b[:cut])
+            for g, w, name in zip(got[:4], want[:4], ("ar", "prep", "var", "other")):
+                assert len(g) == len(w) and g.tobytes() == w.tobytes(), (seed, proto, cut, name)
+            for f in ("consumed", "next", "n_accept_replies", "n_prepare_replies", "n_var", "n_other",
+                      "stop_reason", "stop_code"):
+                assert int(got[4][f]) == int(want[4][f]), (seed, proto, cut, f)
