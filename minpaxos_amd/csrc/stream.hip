@@ -20,12 +20,17 @@
 // associatively: a workgroup reduces its 128 chunk maps to a 16 KB tile map, a group of 256
 // tile maps to a group map, one block walks the group maps from the entry, classifies the
 // terminal it reaches exactly, and the down-sweeps give every tile, then every chunk, its true
-// entry. The emit pass walks each chunk's frames on the true chain, counts them per record
-// kind, takes its output indices from a block scan plus a decoupled look-back across tiles,
-// and writes the records. A LONG terminal is decoded too and ends the call (MPX_DECODE_LONG):
-// the next call starts at its end (the host form loops).
-// HBM traffic per stream byte: 1 read (maps) + 1 read (emit) + 0.5 write + 0.5 read (the 64-byte
-// chunk maps), records written once.
+// entry. The count pass walks each chunk's frames on the true chain and counts them per record
+// kind, a scan gives every tile its output offsets, and the emit pass walks again and writes
+// the records. A LONG terminal is decoded too and ends the call (MPX_DECODE_LONG): the next
+// call starts at its end (the host form loops).
+// Chains from different entries merge within a few frames, so a tile whose 64 chains all leave
+// its first 8 chunks at one entry X (or die there) - nearly every tile of a real stream - has
+// chunk entries past those 8 chunks that do not depend on its entry: the framing pass stores
+// them with group 0's 8 chunk maps as the tile's TileEnt (640 bytes) instead of its 128 chunk
+// maps (8 KB), and the count pass and the walk read that (MPX_SD_TENT).
+// HBM traffic per stream byte: 1 read (maps) + 1 read (count) + 1 read (emit) + 0.04 (TileEnt
+// write and read), records written once.
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -43,6 +48,13 @@ constexpr int kGT = 256;                // tiles per group
 #define MPX_SD_VARLDS 1
 #endif
 constexpr int kDRow = kC + 4;           // LDS row of a chunk's DP (bank-conflict padding)
+constexpr int kTEnt = 8 * kE + kTL;     // a tile's TileEnt bytes
+#ifndef MPX_SD_TENT
+#define MPX_SD_TENT 1
+#endif
+#ifndef MPX_SD_TENT_NOCONV  // test build: every tile takes the unconverged path
+#define MPX_SD_TENT_NOCONV 0
+#endif
 constexpr uint8_t kTerm = 0xFF;         // terminal (tree levels >= 1, tile / group maps)
 constexpr uint8_t kDeadE = 0xFF;        // no entry (past the stop)
 static_assert(kE == 64 && kE + kC <= 255, "u8 DP encoding: landings < kC + kE, 0xFF terminal");
@@ -184,7 +196,9 @@ struct SParams {
 
 // ---- workspace ----------------------------------------------------------------------------
 struct Work {
-    uint8_t* cmap;             // [tiles * kTL][kE] chunk maps
+    uint8_t* cmap;             // [tiles * kTL][kE] chunk maps (MPX_SD_TENT: converged tiles skip them)
+    uint8_t* tconv;            // [tiles][kTEnt] TileEnt: group 0's chunk maps, then [0] converged,
+                               // [1] X, [8..127] the chunk entries from X (MPX_SD_TENT)
     uint8_t* tmap;             // [tiles][kE]
     uint8_t* tent;             // [tiles] true entry (kDeadE past the stop)
     uint8_t* gmap;             // [groups][kE]
@@ -469,6 +483,15 @@ __device__ __forceinline__ void chunk_groups(const uint8_t* X, int xstride, uint
 #define SD_STAMP(k) do {} while (0)
 #endif
 
+// a lane's chunk map (64 bytes of its row) into the chunk-map array
+__device__ __forceinline__ void store_chunk_map(const Work& W, uint32_t tile, const uint8_t* row) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(row);
+    uint4* dst = reinterpret_cast<uint4*>(W.cmap + ((uint64_t)tile * kTL + threadIdx.x) * kE);
+#pragma unroll
+    for (int i = 0; i < kE / 16; ++i)
+        dst[i] = make_uint4(src[4 * i], src[4 * i + 1], src[4 * i + 2], src[4 * i + 3]);
+}
+
 __global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(4))) void k_sd_tile_maps(SParams P, Work W) {
 #if MPX_SD_STAMP
     unsigned long long sd_t[8];
@@ -564,17 +587,62 @@ __global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(4))) void k
     SD_STAMP(3);
     chunk_dp_self(wd, D[l]);
     SD_STAMP(4);
-    {  // this chunk's map (64 bytes) for the emit pass and the walk
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(D[l]);
-        uint4* dst = reinterpret_cast<uint4*>(W.cmap + ((uint64_t)blockIdx.x * kTL + l) * kE);
-#pragma unroll
-        for (int i = 0; i < kE / 16; ++i)
-            dst[i] = make_uint4(src[4 * i], src[4 * i + 1], src[4 * i + 2], src[4 * i + 3]);
-    }
+#if !MPX_SD_TENT
+    store_chunk_map(W, blockIdx.x, D[l]);
+#endif
     __syncthreads();
     SD_STAMP(5);
     chunk_groups(&D[0][0], kDRow, G);
     __syncthreads();
+#if MPX_SD_TENT
+    {   // the tile's entry table (TileEnt): whether every chain from the 64 tile entries that
+        // leaves group 0 (chunks 0..7) leaves it at one entry X, and the chunk entries from X on
+        __shared__ __attribute__((aligned(16))) uint8_t TE[kTL];
+        __shared__ uint8_t GEs[kTL / 8];
+        if (l < kE) {  // wave 0: the live exits' min and max
+            const uint32_t v = G[0][l], live = v < (uint32_t)kE;
+            uint32_t mn = live ? v : 0xFFu, mx = live ? v : 0u;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                mn = min(mn, (uint32_t)__shfl_xor(mn, d));
+                mx = max(mx, (uint32_t)__shfl_xor(mx, d));
+            }
+            if (l == 0) {
+                const bool conv = (mn == 0xFFu || mn == mx) && !MPX_SD_TENT_NOCONV;
+                TE[0] = conv ? 1 : 0;
+                TE[1] = (uint8_t)(conv ? mn : 0xFFu);  // X (kDeadE: no chain leaves group 0)
+                uint32_t x = conv ? mn : (uint32_t)kDeadE;
+                for (int g = 1; g < kTL / 8; ++g) {  // the group entries from X
+                    GEs[g] = (uint8_t)x;
+                    x = x == kDeadE ? kDeadE : G[g][x];
+                }
+            }
+        }
+        __syncthreads();
+        const bool conv = TE[0] != 0;
+        if (conv && l >= 1 && l < kTL / 8) {  // chunk entries inside groups 1..15
+            uint32_t x = GEs[l];
+            for (int c = 0; c < 8; ++c) {
+                TE[8 * l + c] = (uint8_t)x;
+                const uint32_t y = x == kDeadE ? kDeadE : D[8 * l + c][x];
+                x = y < (uint32_t)kE ? y : kDeadE;
+            }
+        }
+        __syncthreads();
+        uint8_t* te = W.tconv + (uint64_t)blockIdx.x * kTEnt;
+        if (conv) {  // group 0's 8 chunk maps and the entry row: 640 bytes instead of 8 KB
+            if (l < 8 * kE / 16) {
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(D[l >> 2]) + 4 * (l & 3);
+                reinterpret_cast<uint4*>(te)[l] = make_uint4(src[0], src[1], src[2], src[3]);
+            } else if (l < kTEnt / 16) {
+                reinterpret_cast<uint4*>(te)[l] = reinterpret_cast<const uint4*>(TE)[l - 8 * kE / 16];
+            }
+        } else {
+            if (l == 0) te[8 * kE] = 0;
+            store_chunk_map(W, blockIdx.x, D[l]);
+        }
+    }
+#endif
     {  // the tile map: the first and second 8 group maps composed by two halves of the
        // workgroup side by side, then entry l through both
         static_assert(kTL == 2 * kE && kTL / 8 == 16, "two halves of 8 group maps");
@@ -760,12 +828,45 @@ __global__ __launch_bounds__(kParts * kE) void k_sd_walk(SParams P, Work W, uint
     const uint32_t ts = first + fk[0];
     const uint32_t te = fk[1];
     __syncthreads();
-    // the terminal chunk within the tile (its 128 chunk maps, 8 KB, over S)
-    for (uint32_t i = t; i < (uint32_t)kTL * kE / 16; i += blockDim.x)
+    // the terminal chunk within the tile: a converged tile's TileEnt (group 0's chunk maps, then
+    // the chunk entries from X), else its 128 chunk maps (8 KB) over S
+#if MPX_SD_TENT
+    for (uint32_t i = t; i < (uint32_t)kTEnt / 16; i += blockDim.x)
         reinterpret_cast<uint4*>(&S[0][0])[i] =
-            reinterpret_cast<const uint4*>(W.cmap + (uint64_t)ts * kTL * kE)[i];
+            reinterpret_cast<const uint4*>(W.tconv + (uint64_t)ts * kTEnt)[i];
     __syncthreads();
-    first_terminal(S, kTL, te, Q, &fk[0], &fk[1], &fk[2]);
+    const bool conv = S[8][0] != 0;
+    __syncthreads();
+    if (conv) {
+        const uint8_t* E = &S[8][0];
+        if (t == 0) fk[2] = kTL - 1;
+        __syncthreads();
+        // past group 0 the chain ends in the first chunk whose successor is dead
+        if (t >= 8 && t < kTL - 1 && E[t] != kDeadE && E[t + 1] == kDeadE) atomicMin(&fk[2], t);
+        __syncthreads();
+        if (t == 0) {
+            uint32_t x = te, c = 0;
+            for (; c < 8; ++c) {  // the chain dies in group 0, or leaves it at X = E[8]
+                const uint32_t y = S[c][x];
+                if (y >= (uint32_t)kE) break;
+                x = y;
+            }
+            if (c == 8) {
+                c = fk[2];
+                x = E[c];
+            }
+            fk[0] = c;
+            fk[1] = x;
+        }
+    } else
+#endif
+    {
+        for (uint32_t i = t; i < (uint32_t)kTL * kE / 16; i += blockDim.x)
+            reinterpret_cast<uint4*>(&S[0][0])[i] =
+                reinterpret_cast<const uint4*>(W.cmap + (uint64_t)ts * kTL * kE)[i];
+        __syncthreads();
+        first_terminal(S, kTL, te, Q, &fk[0], &fk[1], &fk[2]);
+    }
     __syncthreads();
     if (t == 0) {
         const uint32_t cs = fk[0];
@@ -1011,6 +1112,38 @@ __global__ __launch_bounds__(kTL) void k_sd_count(SParams P, Work W) {
     }
     const uint64_t t0 = (uint64_t)tile * kTB;
 #if MPX_SD_COUNT_UNION
+#if MPX_SD_TENT
+    // the TileEnt's loads first (needed first), then the tile's, all in flight together; a
+    // converged tile (the common case) needs no chunk maps past group 0
+    uint4 tev = make_uint4(0, 0, 0, 0);
+    if (l < kTEnt / 16) tev = reinterpret_cast<const uint4*>(W.tconv + (uint64_t)tile * kTEnt)[l];
+    uint4 tv[kStageVec];
+    load_tile_regs(P, t0, tv);
+    if (l < kTEnt / 16) reinterpret_cast<uint4*>(&X[0][0])[l] = tev;
+    __syncthreads();
+    if (X[8][0] != 0) {  // converged (block-uniform)
+        if (l == 0) {  // group 0 from the tile's entry; the rest is the entry row or dead
+            uint32_t x = ent;
+            for (int c = 0; c < 8; ++c) {
+                En[c] = (uint8_t)x;
+                const uint32_t y = x == kDeadE ? kDeadE : X[c][x];
+                x = y < (uint32_t)kE ? y : kDeadE;
+            }
+            GE[0] = x != kDeadE;
+        }
+        __syncthreads();
+        if (l >= 8) En[l] = GE[0] ? X[8][l] : kDeadE;
+        __syncthreads();
+    } else {  // (rare: chains still apart after group 0) the 8 KB of chunk maps
+        const uint4* csrc = reinterpret_cast<const uint4*>(W.cmap + (uint64_t)tile * kTL * kE);
+        __syncthreads();  // (every thread has read the flag)
+#pragma unroll 1
+        for (int k = 0; k < kTL * kE / 16 / kTL; ++k)
+            reinterpret_cast<uint4*>(&X[0][0])[l + k * kTL] = csrc[l + k * kTL];
+        __syncthreads();
+        chunk_entries(ent, X, G, GE, En);  // (ends with a barrier: X is dead)
+    }
+#else
     // the chunk maps' loads first (needed first), then the tile's, all in flight together
     constexpr int kCm = kTL * kE / 16 / kTL;
     uint4 cm[kCm];
@@ -1023,6 +1156,7 @@ __global__ __launch_bounds__(kTL) void k_sd_count(SParams P, Work W) {
     for (int k = 0; k < kCm; ++k) reinterpret_cast<uint4*>(&X[0][0])[l + k * kTL] = cm[k];
     __syncthreads();
     chunk_entries(ent, X, G, GE, En);  // (ends with a barrier: X is dead)
+#endif
 #pragma unroll
     for (int k = 0; k < kStageVec; ++k) {
         const int i = l + k * kTL;
@@ -1361,7 +1495,7 @@ __global__ void k_sd_empty(mpx_stream_result* res, uint64_t at) {
 // ---- host side ----------------------------------------------------------------------------
 namespace {
 struct Layout {
-    uint64_t cmap, tmap, tent, gmap, gent, tcnt, tpre, btot, boff, ticket, cinfo, stop, total;
+    uint64_t cmap, tconv, tmap, tent, gmap, gent, tcnt, tpre, btot, boff, ticket, cinfo, stop, total;
 };
 Layout layout_of(uint64_t len) {
     const uint64_t tiles = n_tiles_of(len + 16), groups = (tiles + kGT - 1) / kGT;
@@ -1369,6 +1503,7 @@ Layout layout_of(uint64_t len) {
     Layout L{};
     uint64_t o = 0;
     L.cmap = o; o += al(tiles * kTL * kE);
+    L.tconv = o; o += al(tiles * kTEnt);
     L.tmap = o; o += al(tiles * kE);
     L.tent = o; o += al(tiles);
     L.gmap = o; o += al(groups * kE);
@@ -1404,7 +1539,7 @@ hipError_t launch_decode_stream(int proto, int legacy, const uint8_t* buf, uint6
     const uint32_t groups = (tiles + kGT - 1) / kGT;
     const Layout L = layout_of(len);
     char* w = (char*)work;
-    Work W{(uint8_t*)(w + L.cmap), (uint8_t*)(w + L.tmap), (uint8_t*)(w + L.tent),
+    Work W{(uint8_t*)(w + L.cmap), (uint8_t*)(w + L.tconv), (uint8_t*)(w + L.tmap), (uint8_t*)(w + L.tent),
            (uint8_t*)(w + L.gmap), (uint8_t*)(w + L.gent), (uint32_t*)(w + L.tcnt),
            (uint32_t*)(w + L.tpre), (uint32_t*)(w + L.btot), (uint32_t*)(w + L.boff),
            (uint32_t*)(w + L.ticket), (uint2*)(w + L.cinfo), (uint64_t*)(w + L.stop)};
