@@ -239,14 +239,14 @@ __device__ __forceinline__ uint32_t lut_len(uint64_t lut, uint32_t code) {
 // position, re-scans its stop chunk (chunk_terminal).
 //
 // Phase 2a: the landings of the fixed-length frames, four positions per dword of chunk bytes.
-// v_perm_b32 looks the four codes up in an 8-byte table of length - 1 (0x7F for a variable
+// v_perm_b32 looks the four codes up in an 8-byte table of length - 1 (kVarMark for a variable
 // message) indexed by code - MPX_PEER_BEACON; every other code selects 0x00 or 0xFF, cleared to
-// 0 (a 1-byte frame); the positions are added bytewise (no carries: <= 0x7F + 128). Returns the
-// dword of landings; *var gets bit 7 of every variable-message byte (var_bits).
-__device__ __forceinline__ uint32_t var_bits(uint32_t y2) {  // y2 bytes == 0x7F -> 0x80
-    const uint32_t z = y2 ^ 0x7F7F7F7Fu;
-    return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z | 0x7F7F7F7Fu);
-}
+// 0 (a 1-byte frame); the positions are added bytewise (no carries: <= 0x40 + 128). Returns the
+// dword of landings; *var gets bit 6 of every variable-message byte (var_bits: the one table
+// value with bit 6 set - fixed lengths are at most 17 - so one AND, where round 6's first form,
+// 0x7F, needed a zero-byte test).
+constexpr uint32_t kVarMark = 0x40;
+__device__ __forceinline__ uint32_t var_bits(uint32_t y2) { return y2 & 0x40404040u; }
 __device__ __forceinline__ uint32_t dp_landings(uint32_t w, uint32_t lut_lo, uint32_t lut_hi,
                                                 uint32_t pos4, uint32_t* var) {
     const uint32_t h = w & 0x80808080u;
@@ -259,7 +259,7 @@ __device__ __forceinline__ uint32_t dp_landings(uint32_t w, uint32_t lut_lo, uin
 }
 static_assert(MPX_PEER_BEACON == 6, "dp_landings indexes the table by code - 6");
 
-// 0xFF in every byte whose bit 7 is set (bytes of 0x80 / 0x00 from var_bits)
+// 0xFF in every byte whose bit 7 is set (bytes of 0x80 / 0x00)
 __device__ __forceinline__ uint32_t byte_mask(uint32_t b7) { return b7 | (b7 - (b7 >> 7)); }
 
 // binary.ReadVarint's unsigned part at *pos (relative), every read below e; false = a failure
@@ -412,7 +412,7 @@ __host__ __device__ constexpr uint64_t dp_table(uint64_t lut) {
     uint64_t e = 0;
     for (int i = 0; i < 8; ++i) {
         const uint64_t fl = (lut >> (8 * i)) & 0xFFu;
-        e |= (fl ? fl - 1 : 0x7Fu) << (8 * i);
+        e |= (fl ? fl - 1 : (uint64_t)kVarMark) << (8 * i);
     }
     return e;
 }
@@ -550,11 +550,11 @@ __global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(4))) void k
         const bool wv = __ballot(any_var != 0) != 0;  // (wave-uniform)
         uint16_t* T = reinterpret_cast<uint16_t*>(&G[0][0]) + (l >> 6) * kVarTasks;
         uint64_t m_lo = 0, m_hi = 0;
-        if (any_var) {  // positions from the landings (a variable message's is its position + 128)
+        if (any_var) {  // positions from the landings (a variable message's is its position + 1 + kVarMark)
 #pragma unroll
             for (int i = 0; i < kC / 4; ++i) {
                 const uint32_t pos4 = (uint32_t)(4 * i + 1) * 0x01010101u + 0x03020100u;
-                const uint32_t t = var_bits(wd[i] - pos4) >> 7;  // 0x01 per variable-message byte
+                const uint32_t t = var_bits(wd[i] - pos4) >> 6;  // 0x01 per variable-message byte
                 const uint64_t nib = (uint64_t)((t | (t >> 7) | (t >> 14) | (t >> 21)) & 0xFu);
                 if (i < 16) m_lo |= nib << (4 * i); else m_hi |= nib << (4 * (i - 16));
             }
@@ -571,7 +571,7 @@ __global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
         for (int i = 0; i < kC / 4; ++i) {
             const uint32_t pos4 = (uint32_t)(4 * i + 1) * 0x01010101u + 0x03020100u;
-            const uint32_t vm = byte_mask(var_bits(wd[i] - pos4));
+            const uint32_t vm = byte_mask(var_bits(wd[i] - pos4) << 1);
             wd[i] = (wd[i] & ~vm) | (row[i] & vm);
         }
     }
@@ -597,8 +597,11 @@ __global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(4))) void k
 #if MPX_SD_TENT
     {   // the tile's entry table (TileEnt): whether every chain from the 64 tile entries that
         // leaves group 0 (chunks 0..7) leaves it at one entry X, and the chunk entries from X on
-        __shared__ __attribute__((aligned(16))) uint8_t TE[kTL];
-        __shared__ uint8_t GEs[kTL / 8];
+        // TE (the entry row, 128 bytes) and GEs (the 16 group entries) live in the rows' 4 pad
+        // bytes (rows 0..31 and 32..35): 144 more bytes of LDS would cost a workgroup per CU
+        static_assert(kDRow - kC == 4 && kTL / 4 + kTL / 8 / 4 <= kTL, "pad bytes for TE / GEs");
+        auto TE = [&](uint32_t k) -> uint8_t& { return D[k >> 2][kC + (k & 3)]; };
+        auto GEs = [&](uint32_t g) -> uint8_t& { return D[kTL / 4 + (g >> 2)][kC + (g & 3)]; };
         if (l < kE) {  // wave 0: the live exits' min and max
             const uint32_t v = G[0][l], live = v < (uint32_t)kE;
             uint32_t mn = live ? v : 0xFFu, mx = live ? v : 0u;
@@ -609,21 +612,21 @@ __global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(4))) void k
             }
             if (l == 0) {
                 const bool conv = (mn == 0xFFu || mn == mx) && !MPX_SD_TENT_NOCONV;
-                TE[0] = conv ? 1 : 0;
-                TE[1] = (uint8_t)(conv ? mn : 0xFFu);  // X (kDeadE: no chain leaves group 0)
+                TE(0) = conv ? 1 : 0;
+                TE(1) = (uint8_t)(conv ? mn : 0xFFu);  // X (kDeadE: no chain leaves group 0)
                 uint32_t x = conv ? mn : (uint32_t)kDeadE;
                 for (int g = 1; g < kTL / 8; ++g) {  // the group entries from X
-                    GEs[g] = (uint8_t)x;
+                    GEs(g) = (uint8_t)x;
                     x = x == kDeadE ? kDeadE : G[g][x];
                 }
             }
         }
         __syncthreads();
-        const bool conv = TE[0] != 0;
+        const bool conv = TE(0) != 0;
         if (conv && l >= 1 && l < kTL / 8) {  // chunk entries inside groups 1..15
-            uint32_t x = GEs[l];
+            uint32_t x = GEs(l);
             for (int c = 0; c < 8; ++c) {
-                TE[8 * l + c] = (uint8_t)x;
+                TE(8 * l + c) = (uint8_t)x;
                 const uint32_t y = x == kDeadE ? kDeadE : D[8 * l + c][x];
                 x = y < (uint32_t)kE ? y : kDeadE;
             }
@@ -634,8 +637,10 @@ __global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(4))) void k
             if (l < 8 * kE / 16) {
                 const uint32_t* src = reinterpret_cast<const uint32_t*>(D[l >> 2]) + 4 * (l & 3);
                 reinterpret_cast<uint4*>(te)[l] = make_uint4(src[0], src[1], src[2], src[3]);
-            } else if (l < kTEnt / 16) {
-                reinterpret_cast<uint4*>(te)[l] = reinterpret_cast<const uint4*>(TE)[l - 8 * kE / 16];
+            } else if (l < kTEnt / 16) {  // 16 entry bytes: four rows' pad dwords
+                const int r = 4 * (l - 8 * kE / 16);
+                auto pad = [&](int k) { return *reinterpret_cast<const uint32_t*>(&D[r + k][kC]); };
+                reinterpret_cast<uint4*>(te)[l] = make_uint4(pad(0), pad(1), pad(2), pad(3));
             }
         } else {
             if (l == 0) te[8 * kE] = 0;
