@@ -78,12 +78,23 @@ __host__ __device__ __forceinline__ uint32_t flen(uint32_t code, int proto) {
 }
 
 // bytes of the stream: an LDS-staged window [lo, hi) (relative positions), global otherwise
+// The staged tile image of the count and emit passes: 4 pad bytes after every 128-byte chunk
+// (MPX_SD_PAD), so the lanes - one per chunk, at similar offsets - read 64 different banks
+// instead of two (the emit pass's SQ pass: 72 % of its LDS cycles were bank conflicts).
+#ifndef MPX_SD_PAD
+#define MPX_SD_PAD 1
+#endif
+__host__ __device__ __forceinline__ uint32_t pofs(uint32_t o) {  // image offset of stream offset o
+    return MPX_SD_PAD ? o + ((o >> 7) << 2) : o;
+}
 struct Bytes {
     const uint8_t* g;
     const uint8_t* s;
     uint64_t lo, hi;
+    bool padded;  // s is a padded tile image (pofs)
     __host__ __device__ __forceinline__ uint32_t operator()(uint64_t i) const {
-        return (i >= lo && i < hi) ? (uint32_t)s[i - lo] : (uint32_t)g[i];
+        if (i >= lo && i < hi) return s[padded ? pofs((uint32_t)(i - lo)) : (uint32_t)(i - lo)];
+        return g[i];
     }
 };
 
@@ -963,12 +974,29 @@ struct Outs {
 __device__ __forceinline__ int32_t le32(const Bytes& by, uint64_t i) {
     return (int32_t)(by(i) | (by(i + 1) << 8) | (by(i + 2) << 16) | (by(i + 3) << 24));
 }
-// 4 bytes at LDS byte offset o from two aligned dword reads (o + 8 inside the buffer)
+// 4 bytes at stream offset o of a (padded) tile image from two aligned dword reads (each dword
+// at its own image position: a field may straddle a chunk's pad)
 __device__ __forceinline__ int32_t lds_le32(const uint8_t* B, uint32_t o) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(B) + (o >> 2);
-    const uint32_t sh = o & 3u;
-    const uint64_t x = ((uint64_t)w[1] << 32) | w[0];
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(B);
+    const uint32_t d = o >> 2, sh = o & 3u;
+    const uint32_t d0 = MPX_SD_PAD ? d + (d >> 5) : d, d1 = MPX_SD_PAD ? d + 1 + ((d + 1) >> 5) : d + 1;
+    const uint64_t x = ((uint64_t)w[d1] << 32) | w[d0];
     return (int32_t)(uint32_t)(x >> (8 * sh));
+}
+// the image's bytes: kTB + kE stream bytes, a pad per chunk (kTL + 1 chunks started), and the
+// second dword lds_le32 may read past the last byte
+constexpr int kImg = kTB + kE + (MPX_SD_PAD ? 4 * (kTL + 1) : 0) + 16;
+// 16 stream bytes (piece i of the tile) into the image: a piece never crosses a chunk
+__device__ __forceinline__ void img_put(uint8_t* B, int i, const uint4 v) {
+    if (MPX_SD_PAD) {
+        uint32_t* w = reinterpret_cast<uint32_t*>(B) + 4 * i + (i >> 3);
+        w[0] = v.x;
+        w[1] = v.y;
+        w[2] = v.z;
+        w[3] = v.w;
+    } else {
+        reinterpret_cast<uint4*>(B)[i] = v;
+    }
 }
 
 // the tile's chunk entries: the tile's true entry through its chunk maps (X, in LDS)
@@ -1054,7 +1082,7 @@ __device__ __forceinline__ void stage_tile(const SParams& P, uint64_t t0, uint8_
                 if (a + b < P.len) q[b >> 2] |= (uint32_t)P.buf[a + b] << (8 * (b & 3));
             v = make_uint4(q[0], q[1], q[2], q[3]);
         }
-        *reinterpret_cast<uint4*>(&B[i * 16]) = v;
+        img_put(B, i, v);
     }
 }
 
@@ -1097,14 +1125,17 @@ __global__ __launch_bounds__(kTL) void k_sd_count(SParams P, Work W) {
 #if MPX_SD_COUNT_UNION
     // the chunk maps are dead once the chunk entries are known: the tile's bytes (loaded into
     // registers meanwhile) take their LDS, so a workgroup needs 16.5 KB instead of 24.5 KB
-    __shared__ __attribute__((aligned(16))) uint8_t U[kTB + kE];
+    // (and the group maps of an unconverged tile's chunk entries take the bytes after X)
+    __shared__ __attribute__((aligned(16))) uint8_t U[kImg];
     uint8_t* const B = U;
     uint8_t(*const X)[kE] = reinterpret_cast<uint8_t(*)[kE]>(U);
+    uint8_t(*const G)[kE] = reinterpret_cast<uint8_t(*)[kE]>(U + kTL * kE);
+    static_assert(kTL * kE + kTL / 8 * kE <= kImg, "X and G fit the image");
 #else
-    __shared__ __attribute__((aligned(16))) uint8_t B[kTB + kE];
+    __shared__ __attribute__((aligned(16))) uint8_t B[kImg];
     __shared__ __attribute__((aligned(16))) uint8_t X[kTL][kE];
-#endif
     __shared__ uint8_t G[kTL / 8][kE];
+#endif
     __shared__ uint8_t GE[kTL / 8];
     __shared__ uint8_t En[kTL];
     __shared__ uint32_t wsum[kTL / kWave][4];
@@ -1165,7 +1196,7 @@ __global__ __launch_bounds__(kTL) void k_sd_count(SParams P, Work W) {
 #pragma unroll
     for (int k = 0; k < kStageVec; ++k) {
         const int i = l + k * kTL;
-        if (i < (kTB + kE) / 16) reinterpret_cast<uint4*>(B)[i] = tv[k];
+        if (i < (kTB + kE) / 16) img_put(B, i, tv[k]);
     }
     __syncthreads();
 #else
@@ -1175,10 +1206,10 @@ __global__ __launch_bounds__(kTL) void k_sd_count(SParams P, Work W) {
     chunk_entries(ent, X, G, GE, En);
 #endif
     const uint64_t c0 = t0 + (uint64_t)l * kC;
-    const Bytes by{P.buf, B, t0, t0 + kTB + kE < P.len ? t0 + kTB + kE : P.len};
+    const Bytes by{P.buf, B, t0, t0 + kTB + kE < P.len ? t0 + kTB + kE : P.len, MPX_SD_PAD != 0};
     uint32_t cnt[4] = {0, 0, 0, 0};
     chunk_counts(En[l], c0, W.stop[0], (int)W.stop[2] == MPX_DECODE_LONG, P, by,
-                 [&](uint64_t a) { return (uint32_t)B[a - t0]; }, cnt);
+                 [&](uint64_t a) { return (uint32_t)B[pofs((uint32_t)(a - t0))]; }, cnt);
     W.cinfo[(uint64_t)tile * kTL + l] =
         make_uint2(En[l], cnt[0] | (cnt[1] << 8) | (cnt[2] << 16) | (cnt[3] << 24));
 #pragma unroll
@@ -1275,9 +1306,9 @@ constexpr int kRegAR = 10;
 constexpr uint32_t kRegCap = 1024;
 __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint32_t n_tiles,
                                                  mpx_stream_result* res) {
-    __shared__ __attribute__((aligned(16))) uint8_t B[kTB + kE + 16];  // + lds_le32's 2nd dword
+    __shared__ __attribute__((aligned(16))) uint8_t B[kImg];
     __shared__ uint32_t wsum[kTL / kWave][4];
-    static_assert((kTB + kE + 16) / 16 >= kRegCap, "a pass of staged records fits the tile image");
+    static_assert(kImg / 16 >= kRegCap, "a pass of staged records fits the tile image");
     const int l = threadIdx.x;
     const uint32_t tile = blockIdx.x;
     const uint8_t ent = W.tent[tile];
@@ -1294,7 +1325,7 @@ __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint
 #pragma unroll
         for (int k = 0; k < kStageVec; ++k) {
             const int i = l + k * kTL;
-            if (i < (kTB + kE) / 16) reinterpret_cast<uint4*>(B)[i] = tv[k];
+            if (i < (kTB + kE) / 16) img_put(B, i, tv[k]);
         }
     } else {
         stage_tile(P, t0, B);
@@ -1305,7 +1336,7 @@ __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint
     const uint64_t stop = W.stop[0];
     const int why = (int)W.stop[2];
     const bool long_stop = why == MPX_DECODE_LONG;
-    const Bytes by{P.buf, B, t0, t0 + kTB + kE < P.len ? t0 + kTB + kE : P.len};
+    const Bytes by{P.buf, B, t0, t0 + kTB + kE < P.len ? t0 + kTB + kE : P.len, MPX_SD_PAD != 0};
     const uint64_t c0 = t0 + (uint64_t)l * kC;
     const uint32_t cnt[4] = {ci.y & 0xFFu, (ci.y >> 8) & 0xFFu, (ci.y >> 16) & 0xFFu, ci.y >> 24};
     const uint64_t lut = P.proto == MPX_MODE_MIN ? kLutMin : kLutClassic;
@@ -1354,7 +1385,7 @@ __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint
     // stored here; live = false after the chunk's last frame
     auto frame = [&](uint64_t& a, bool& live, bool& is_ar, uint4& rec) {
         is_ar = false;
-        const uint32_t code = B[a - t0];
+        const uint32_t code = B[pofs((uint32_t)(a - t0))];
         uint32_t fl = lut_len(lut, code);
         const bool at_stop = a == stop;
         if (at_stop && !long_stop) {
@@ -1415,7 +1446,7 @@ __global__ __launch_bounds__(kTL) void k_sd_emit(SParams P, Work W, Outs O, uint
             const uint32_t o = (uint32_t)(a - t0);
             rec = make_uint4((uint32_t)lds_le32(B, o + 1), (uint32_t)lds_le32(B, o + 6),
                              P.proto == MPX_MODE_MIN ? (uint32_t)lds_le32(B, o + 10) : 0xFFFFFFFFu,
-                             (uint32_t)B[o + 5]);
+                             (uint32_t)B[pofs(o + 5)]);
             is_ar = true;
         } else {
             if (idx[3] < O.oth_cap) {
