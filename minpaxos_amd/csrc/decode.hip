@@ -400,11 +400,30 @@ constexpr int kXPad = 20;  // bytes per exit map in LDS (17 used)
 #endif
 constexpr int kDecRegAR = 10;          // a 128-byte chunk starts at most 10 AcceptReply frames
 constexpr uint32_t kDecRegCap = 1024;  // staged records per LDS pass (the tile image's space)
-// 4 bytes at LDS byte offset o from two aligned dword reads (o + 8 inside the buffer)
+// The staged tile image: 4 pad bytes after every 128-byte chunk (MPX_DEC_PAD), so the lanes -
+// one per chunk, at similar offsets - read 64 LDS banks instead of two (as the stream emit)
+#ifndef MPX_DEC_PAD
+#define MPX_DEC_PAD 1
+#endif
+__device__ __forceinline__ uint32_t dpofs(uint32_t o) { return MPX_DEC_PAD ? o + ((o >> 7) << 2) : o; }
+constexpr int kDecImg = kTileBytes + 32 + (MPX_DEC_PAD ? 4 * (kTileLanes + 1) : 0) + 16;
+__device__ __forceinline__ void dimg_put(uint8_t* B, int i, const uint4 v) {
+    if (MPX_DEC_PAD) {
+        uint32_t* w = reinterpret_cast<uint32_t*>(B) + 4 * i + (i >> 3);
+        w[0] = v.x;
+        w[1] = v.y;
+        w[2] = v.z;
+        w[3] = v.w;
+    } else {
+        reinterpret_cast<uint4*>(B)[i] = v;
+    }
+}
+// 4 bytes at tile offset o from two aligned dword reads, each at its image position
 __device__ __forceinline__ int32_t lds_le32(const uint8_t* B, uint32_t o) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(B) + (o >> 2);
-    const uint32_t sh = o & 3u;
-    const uint64_t x = ((uint64_t)w[1] << 32) | w[0];
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(B);
+    const uint32_t d = o >> 2, sh = o & 3u;
+    const uint32_t d0 = MPX_DEC_PAD ? d + (d >> 5) : d, d1 = MPX_DEC_PAD ? d + 1 + ((d + 1) >> 5) : d + 1;
+    const uint64_t x = ((uint64_t)w[d1] << 32) | w[d0];
     return (int32_t)(uint32_t)(x >> (8 * sh));
 }
 __global__ __launch_bounds__(kTileLanes) void k_dec_emit(
@@ -420,11 +439,11 @@ __global__ __launch_bounds__(kTileLanes) void k_dec_emit(
     // registers meanwhile) take its LDS, 16.7 KB per workgroup instead of 21.8 KB
     constexpr int kVec = ((kTileBytes + 32) / 16 + kTileLanes - 1) / kTileLanes;
     static_assert((2 * kTileLanes - 1) * kXPad <= kTileBytes + 32, "the tree fits the tile image");
-    __shared__ __attribute__((aligned(16))) uint8_t B[kTileBytes + 32];
+    __shared__ __attribute__((aligned(16))) uint8_t B[kDecImg];
     uint8_t(*const X)[kXPad] = reinterpret_cast<uint8_t(*)[kXPad]>(B);
 #else
     __shared__ uint8_t X[2 * kTileLanes - 1][kXPad];
-    __shared__ __attribute__((aligned(16))) uint8_t B[kTileBytes + 32];
+    __shared__ __attribute__((aligned(16))) uint8_t B[kDecImg];
 #endif
     __shared__ uint32_t wsum[kTileLanes / kWave];
     const GEntry r = tres[blockIdx.x];
@@ -464,7 +483,7 @@ __global__ __launch_bounds__(kTileLanes) void k_dec_emit(
     }
 #else
     for (int i = l; i < (kTileBytes + 32) / 16; i += kTileLanes)
-        *reinterpret_cast<uint4*>(&B[i * 16]) = tile_vec(i);
+        dimg_put(B, i, tile_vec(i));
 #endif
     {
         const ulonglong2 m = xmap[(uint64_t)blockIdx.x * kTileLanes + l];
@@ -501,7 +520,7 @@ __global__ __launch_bounds__(kTileLanes) void k_dec_emit(
 #pragma unroll
     for (int k = 0; k < kVec; ++k) {
         const int i = l + k * kTileLanes;
-        if (i < (kTileBytes + 32) / 16) *reinterpret_cast<uint4*>(&B[i * 16]) = tv[k];
+        if (i < (kTileBytes + 32) / 16) dimg_put(B, i, tv[k]);
     }
     __syncthreads();
 #endif
@@ -511,7 +530,7 @@ __global__ __launch_bounds__(kTileLanes) void k_dec_emit(
     uint32_t n_ar = 0, n_oth = 0;
     if (e != kXStop) {
         for (uint32_t p = base + e; p < base + kChunk;) {
-            const uint32_t code = B[p];
+            const uint32_t code = B[dpofs(p)];
             const uint32_t fl = frame_len(code);
             if ((uint64_t)p >= tl || fl == 0 || (uint64_t)p + fl > tl) break;
             if (code == MPX_PEER_ACCEPT_REPLY) ++n_ar;
@@ -535,7 +554,7 @@ __global__ __launch_bounds__(kTileLanes) void k_dec_emit(
     // here; live = false after the chunk's last frame
     auto frame = [&](uint32_t& p, bool& live, bool& is_ar, uint4& rec) {
         is_ar = false;
-        const uint32_t code = B[p];
+        const uint32_t code = B[dpofs(p)];
         const uint32_t fl = frame_len(code);
         if ((uint64_t)p >= tl || fl == 0 || (uint64_t)p + fl > tl) {
             live = false;
@@ -543,7 +562,7 @@ __global__ __launch_bounds__(kTileLanes) void k_dec_emit(
         }
         if (code == MPX_PEER_ACCEPT_REPLY) {  // Instance, OK, Ballot, Id (little endian)
             rec = make_uint4((uint32_t)lds_le32(B, p + 1), (uint32_t)lds_le32(B, p + 6),
-                             (uint32_t)lds_le32(B, p + 10), (uint32_t)B[p + 5]);
+                             (uint32_t)lds_le32(B, p + 10), (uint32_t)B[dpofs(p + 5)]);
             is_ar = true;
         } else {
             if (oth_i < oth_cap) {
