@@ -4,12 +4,12 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-SKIP_BENCH=1 bash tools/gpu_check.sh > gpurun_out/check_r06b.txt 2>&1
-rc=$?; grep -E "rc=|passed|failed" gpurun_out/check_r06b.txt | tail -5; [ $rc = 0 ] || exit $rc
-grep -q "smoke rc=0" gpurun_out/check_r06b.txt || exit 1
+SKIP_BENCH=1 bash tools/gpu_check.sh > gpurun_out/check_r06c.txt 2>&1
+rc=$?; grep -E "rc=|passed|failed" gpurun_out/check_r06c.txt | tail -5; [ $rc = 0 ] || exit $rc
+grep -q "smoke rc=0" gpurun_out/check_r06c.txt || exit 1
 grep -qE "[0-9]+ failed" gpurun_out/pytest_gpu.log && exit 1
-OUT=gpurun_out/head_r06b; mkdir -p $OUT
+OUT=gpurun_out/head_r06c; mkdir -p $OUT
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 > $OUT/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; grep '^{' $OUT/bench.log | cut -c1-300; [ $rc = 0 ] || exit $rc
-TAG=r06s2 WORKLOADS="stream_min stream_classic" bash tools/gpu_prof_configs.sh || exit $?
-TAG=r06 TRAFFIC_SETS="--workload stream --steps 3 --warmup 1;--workload stream --mode classic --prepare-every 1 --instances 4194304 --steps 3 --warmup 1" bash tools/gpu_counters.sh
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/trace.log 2>&1
+rc=$?; echo "trace rc=$rc"; exit $rc
