@@ -264,7 +264,9 @@ __device__ __forceinline__ uint32_t dp_landings(uint32_t w, uint32_t lut_lo, uin
     const uint32_t sel = (((w | 0x80808080u) - 0x06060606u) ^ 0x80808080u) | h;  // code - 6
     const uint32_t y = __builtin_amdgcn_perm(lut_hi, lut_lo, sel);
     const uint32_t hb = y & 0x80808080u;
-    const uint32_t y2 = y & ~(hb | (hb - (hb >> 7)));  // 0xFF bytes (out of the table) -> 0
+    // 0xFF bytes (out of the table) -> 0: y ^ hb ^ (hb - (hb >> 7)) (the two masks are disjoint;
+    // one v_bitop3_b32 - the AND-NOT-OR form compiled to four ops)
+    const uint32_t y2 = __builtin_amdgcn_bitop3_b32(y, hb, hb - (hb >> 7), 0x96);
     *var = var_bits(y2);
     return y2 + pos4;
 }
