@@ -297,3 +297,19 @@ def test_stream_decode_long_frames_and_malformed(mk_engine, proto):
     b2 = b + W.prepare_reply(proto, 1, 1, 16, [])[:1 + (17 if proto == MIN else 9)] + \
         bytes([0xFF] * 9 + [0x03]) + b
     _eq_decode(e.decode_stream(b2), o.decode_stream(b2))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proto", [MIN, CLASSIC], ids=["min", "classic"])
+def test_stream_decode_tile_edges(mk_engine, proto):
+    """buffers ending exactly at, one byte before and one byte after 16 KB tile boundaries (the
+    framing pass's extra tile, a stop in a TileEnt tile's group 0 or past it), tiny buffers,
+    and leader streams whose instance numbers put a variable-message code byte in every frame
+    (var-dense framing-DP waves)"""
+    e, o = mk_engine(5, proto), Oracle(5, proto)
+    recs, _ = synth.accept_replies(1 << 15, 5, 0.7, seed=7, inst_base=0x0A0A00)
+    buf = bytes(W.leader_stream(proto, recs, prepare_every=97, n_cmds=1))
+    for cut in [1, 2, 13, 127, 128, 129, 1023] + [k * 16384 + d for k in (1, 2, 7) for d in (-1, 0, 1)] + \
+               [8 * 128 + d for d in (-1, 0, 1)] + [len(buf)]:
+        b = buf[:cut]
+        _eq_decode(e.decode_stream(b), o.decode_stream(b))
