@@ -29,6 +29,10 @@
 #include "common.hpp"
 #include "kernels.hpp"
 
+#ifndef MPX_DEC_DBL_TREE  // timing probe build: the tile tree computed twice
+#define MPX_DEC_DBL_TREE 0
+#endif
+
 namespace mpx {
 
 namespace {
@@ -232,6 +236,10 @@ __global__ __launch_bounds__(kTileLanes) void k_dec_tile_maps(const uint8_t* __r
         return;
     }
     return;
+#endif
+#if MPX_DEC_DBL_TREE  // timing probe: the tile tree twice (same result)
+    tile_reduce(T, w);
+    __syncthreads();
 #endif
     tile_reduce(T, w);
     if (threadIdx.x < kEntries) {
