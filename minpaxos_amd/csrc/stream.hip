@@ -510,9 +510,9 @@ __global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(4))) void k
     unsigned long long sd_t[8];
     sd_t[0] = clock64();
 #endif
-    // the chunk's bytes (+ halo), var lengths, then the DP; rows padded to an odd dword count so
-    // the 64 lanes of a wave, each on its own row, hit 64 different banks (a 128-byte stride put
-    // every lane on two banks)
+    // the chunk's bytes (raw, for the variable-message parses), the landings, the parses, then
+    // the DP, all in the lane's row; rows padded to an odd dword count so the 64 lanes of a
+    // wave, each on its own row, hit 64 different banks (a 128-byte stride put every lane on two)
     __shared__ __attribute__((aligned(16))) uint8_t D[kTL][kDRow];
     __shared__ __attribute__((aligned(16))) uint8_t G[kTL / 8][kE];
     static_assert(kTL / 8 * kE >= 2 * kVarTasks * 2, "the var task lists fit G");
@@ -550,7 +550,7 @@ __global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(4))) void k
 #endif
     const uint64_t tab = P.proto == MPX_MODE_MIN ? dp_table(kLutMin) : dp_table(kLutClassic);
     const uint32_t tab_lo = (uint32_t)tab, tab_hi = (uint32_t)(tab >> 32);
-    uint32_t any_var = 0;  // bit 7 of the chunk's variable-message bytes, OR-ed
+    uint32_t any_var = 0;  // bit 6 of the chunk's variable-message bytes, OR-ed
 #pragma unroll
     for (int i = 0; i < kC / 4; ++i) {
         uint32_t vb;
