@@ -48,7 +48,13 @@ constexpr int kGT = 256;                // tiles per group
 #define MPX_SD_VARLDS 1
 #endif
 constexpr int kDRow = kC + 4;           // LDS row of a chunk's DP (bank-conflict padding)
-constexpr int kTEnt = 8 * kE + kTL;     // a tile's TileEnt bytes
+constexpr int kTEnt = 8 * kE + kTL + 16;  // a tile's TileEnt bytes (+ chunks 8..127's counts)
+#ifndef MPX_SD_WPE  // k_sd_tile_maps' waves per SIMD bound (its VGPR budget)
+#define MPX_SD_WPE 5
+#endif
+#ifndef MPX_SD_TCNT  // converged tiles: chunks 8..127 counted by the framing pass (needs TENT)
+#define MPX_SD_TCNT 1
+#endif
 #ifndef MPX_SD_TENT
 #define MPX_SD_TENT 1
 #endif
@@ -505,7 +511,7 @@ __device__ __forceinline__ void store_chunk_map(const Work& W, uint32_t tile, co
         dst[i] = make_uint4(src[4 * i], src[4 * i + 1], src[4 * i + 2], src[4 * i + 3]);
 }
 
-__global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(4))) void k_sd_tile_maps(SParams P, Work W) {
+__global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(MPX_SD_WPE))) void k_sd_tile_maps(SParams P, Work W) {
 #if MPX_SD_STAMP
     unsigned long long sd_t[8];
     sd_t[0] = clock64();
@@ -559,10 +565,10 @@ __global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(4))) void k
         any_var |= vb;
     }
     SD_STAMP(1);
+    uint64_t m_lo = 0, m_hi = 0;  // the chunk's variable-message positions (kept for the counts)
     {
         const bool wv = __ballot(any_var != 0) != 0;  // (wave-uniform)
         uint16_t* T = reinterpret_cast<uint16_t*>(&G[0][0]) + (l >> 6) * kVarTasks;
-        uint64_t m_lo = 0, m_hi = 0;
         if (any_var) {  // positions from the landings (a variable message's is its position + 1 + kVarMark)
 #pragma unroll
             for (int i = 0; i < kC / 4; ++i) {
@@ -650,7 +656,7 @@ __global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(4))) void k
             if (l < 8 * kE / 16) {
                 const uint32_t* src = reinterpret_cast<const uint32_t*>(D[l >> 2]) + 4 * (l & 3);
                 reinterpret_cast<uint4*>(te)[l] = make_uint4(src[0], src[1], src[2], src[3]);
-            } else if (l < kTEnt / 16) {  // 16 entry bytes: four rows' pad dwords
+            } else if (l < (8 * kE + kTL) / 16) {  // 16 entry bytes: four rows' pad dwords
                 const int r = 4 * (l - 8 * kE / 16);
                 auto pad = [&](int k) { return *reinterpret_cast<const uint32_t*>(&D[r + k][kC]); };
                 reinterpret_cast<uint4*>(te)[l] = make_uint4(pad(0), pad(1), pad(2), pad(3));
@@ -676,6 +682,63 @@ __global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(4))) void k
             W.tmap[(uint64_t)blockIdx.x * kE + l] =
                 (uint8_t)(y >= (uint32_t)kE ? (uint32_t)kTerm : G[1][y]);
         }
+#if MPX_SD_TENT && MPX_SD_TCNT
+        // A converged tile's chunks 8..127 lie on one chain whatever the tile's entry: count
+        // their frames here (the count pass then reads 8 chunks of bytes instead of 128). Each
+        // lane walks its chunk from its entry through the DP's pointers (landing, or itself for a
+        // frame leaving the chunk), written over its row once every value read is done; a
+        // frame's kind by its length (an AcceptReply's is unique among the fixed frames) or the
+        // variable-message mask; a variable message's code through L2 (PrepareReply or not).
+        // Only the stop tile can meet a terminal on this chain, and the count pass redoes it.
+        auto TE = [&](uint32_t k) -> uint8_t& { return D[k >> 2][kC + (k & 3)]; };
+        if (TE(0) != 0) {  // converged (block-uniform)
+            uint32_t ex = kDeadE;  // where the lane's chain leaves its chunk
+            if (l == kTL - 1) {
+                const uint32_t e = TE(kTL - 1);
+                const uint32_t v = e < (uint32_t)kE ? D[kTL - 1][e] : kDeadE;
+                ex = v < (uint32_t)kE ? v : kDeadE;
+            } else if (l >= 8) {
+                ex = TE(l + 1);
+            }
+            const uint32_t ent = l >= 8 ? TE(l) : kDeadE;
+            __syncthreads();  // every value row read (TileEnt, chunk maps, the walk's entries)
+            uint32_t* row = reinterpret_cast<uint32_t*>(D[l]);
+#pragma unroll
+            for (int i = 0; i < kC / 4; ++i) row[i] = wd[i];  // the pointers
+            const uint32_t ar_len = flen(MPX_PEER_ACCEPT_REPLY, P.proto);
+            uint32_t cnt[4] = {0, 0, 0, 0};  // AcceptReplies, PrepareReplies, variable, other
+            for (uint32_t x = ent; x < (uint32_t)kC;) {
+                const uint32_t q = D[l][x];
+                const uint32_t len = q != x ? q - x : kC + ex - x;
+                const bool var = ((x < 64 ? m_lo >> x : m_hi >> (x - 64)) & 1ull) != 0;
+                if (var) {
+                    cnt[2]++;
+                    cnt[1] += P.buf[c0 + x] == MPX_PEER_PREPARE_REPLY ? 1u : 0u;
+                } else {
+                    cnt[len == ar_len ? 0 : 3]++;
+                }
+                if (q == x) break;
+                x = q;
+            }
+            if (l >= 8)
+                W.cinfo[(uint64_t)blockIdx.x * kTL + l] =
+                    make_uint2(ent, cnt[0] | (cnt[1] << 8) | (cnt[2] << 16) | (cnt[3] << 24));
+            uint32_t* ws = reinterpret_cast<uint32_t*>(&G[0][0]);  // (free: the tile map is out)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint32_t x = cnt[k];
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+                if (lane_id() == 0) ws[4 * (l / kWave) + k] = x;
+            }
+            __syncthreads();
+            if (l < 4) {
+                uint32_t x = 0;
+                for (int w = 0; w < kTL / kWave; ++w) x += ws[4 * w + l];
+                reinterpret_cast<uint32_t*>(W.tconv + (uint64_t)blockIdx.x * kTEnt + 8 * kE + kTL)[l] = x;
+            }
+        }
+#endif
 #if MPX_SD_STAMP
         SD_STAMP(6);
         if ((blockIdx.x & 2047) == 1025 && (l & 63) == 0)
@@ -1144,10 +1207,17 @@ __global__ __launch_bounds__(kTL) void k_sd_count(SParams P, Work W) {
     const int l = threadIdx.x;
     const uint32_t tile = blockIdx.x;
     const uint8_t ent = W.tent[tile];
+#if MPX_SD_TENT && MPX_SD_TCNT
+    const bool conv_tile = W.tconv[(uint64_t)tile * kTEnt + 8 * kE] != 0;
+    const bool stop_tile = W.stop[0] / kTB == tile;
+#endif
     if (ent == kDeadE) {
         if (l < 4) W.tcnt[4 * (uint64_t)tile + l] = 0;
         return;
     }
+#if MPX_SD_TENT && MPX_SD_TCNT
+    if (conv_tile && !stop_tile) return;  // k_sd_count_conv's
+#endif
     const uint64_t t0 = (uint64_t)tile * kTB;
 #if MPX_SD_COUNT_UNION
 #if MPX_SD_TENT
@@ -1226,6 +1296,64 @@ __global__ __launch_bounds__(kTL) void k_sd_count(SParams P, Work W) {
         uint32_t x = 0;
         for (int w = 0; w < kTL / kWave; ++w) x += wsum[w][l];
         W.tcnt[4 * (uint64_t)tile + l] = x;
+    }
+}
+
+// pass C1': a converged tile (not the stop tile): chunks 8..127 were counted by the framing
+// pass (their cinfo and the four totals at the end of the TileEnt), so one wave resolves the
+// entries of chunks 0..7 from group 0's maps and walks those 8 chunks: 1.2 KB of the tile's bytes
+// read instead of 16 KB (the count pass re-read every stream byte: 0.94 GB of the MIN bench's
+// 2.07 x traffic)
+constexpr int kCcVec = (9 * kC) / 16;  // chunks 0..8 (chunk 7's frames may end in chunk 8)
+__global__ __launch_bounds__(kWave) void k_sd_count_conv(SParams P, Work W) {
+    __shared__ __attribute__((aligned(16))) uint8_t TEs[kTEnt];
+    __shared__ __attribute__((aligned(16))) uint8_t B[9 * kC + 16];
+    __shared__ uint8_t En[8];
+    const int l = threadIdx.x;
+    const uint32_t tile = blockIdx.x;
+    const uint8_t ent = W.tent[tile];
+    const uint8_t* te = W.tconv + (uint64_t)tile * kTEnt;
+    const bool conv_tile = te[8 * kE] != 0;
+    const bool stop_tile = W.stop[0] / kTB == tile;
+    if (ent == kDeadE || !conv_tile || stop_tile) return;  // k_sd_count's
+    const uint64_t t0 = (uint64_t)tile * kTB;
+    // (not the stop tile: the stream goes on past this tile, so all of its bytes exist)
+    const uint4* tsrc = reinterpret_cast<const uint4*>(te);
+    const uint4* bsrc = reinterpret_cast<const uint4*>(P.buf + t0);
+    const uint4 tv = l < kTEnt / 16 ? tsrc[l] : make_uint4(0, 0, 0, 0);
+    const uint4 b0 = bsrc[l];
+    const uint4 b1 = l + kWave < kCcVec ? bsrc[l + kWave] : make_uint4(0, 0, 0, 0);
+    if (l < kTEnt / 16) reinterpret_cast<uint4*>(TEs)[l] = tv;
+    reinterpret_cast<uint4*>(B)[l] = b0;
+    if (l + kWave < kCcVec) reinterpret_cast<uint4*>(B)[l + kWave] = b1;
+    __syncthreads();
+    if (l == 0) {  // group 0 from the tile's entry (it leaves group 0 at X: not the stop tile)
+        uint32_t x = ent;
+        for (int c = 0; c < 8; ++c) {
+            En[c] = (uint8_t)x;
+            const uint32_t y = x == kDeadE ? kDeadE : TEs[c * kE + x];
+            x = y < (uint32_t)kE ? y : kDeadE;
+        }
+    }
+    __syncthreads();
+    uint32_t cnt[4] = {0, 0, 0, 0};
+    if (l < 8) {
+        const Bytes by{P.buf, B, t0, t0 + 9 * kC};
+        chunk_counts(En[l], t0 + (uint64_t)l * kC, W.stop[0], false, P, by,
+                     [&](uint64_t a) { return (uint32_t)B[a - t0]; }, cnt);
+        W.cinfo[(uint64_t)tile * kTL + l] =
+            make_uint2(En[l], cnt[0] | (cnt[1] << 8) | (cnt[2] << 16) | (cnt[3] << 24));
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t x = cnt[k];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+        cnt[k] = x;
+    }
+    if (l < 4) {
+        const uint32_t rest = reinterpret_cast<const uint32_t*>(TEs + 8 * kE + kTL)[l];
+        W.tcnt[4 * (uint64_t)tile + l] = (l == 0 ? cnt[0] : l == 1 ? cnt[1] : l == 2 ? cnt[2] : cnt[3]) + rest;
     }
 }
 
@@ -1590,6 +1718,9 @@ hipError_t launch_decode_stream(int proto, int legacy, const uint8_t* buf, uint6
     k_sd_walk<<<1, kParts * kE, 0, stream>>>(P, W, tiles, groups, res);
     k_sd_tile_entries<<<groups, kParts * kE, 0, stream>>>(W, tiles);
     k_sd_count<<<tiles, kTL, 0, stream>>>(P, W);
+#if MPX_SD_TENT && MPX_SD_TCNT
+    k_sd_count_conv<<<tiles, kWave, 0, stream>>>(P, W);
+#endif
     k_sd_scan<<<(tiles + kScanT - 1) / kScanT, kScanT, 0, stream>>>(W, tiles);
     k_sd_emit<<<tiles, kTL, 0, stream>>>(P, W, O, tiles, res);
     return hipGetLastError();
