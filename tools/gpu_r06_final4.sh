@@ -3,5 +3,5 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-TAG=r06s3 WORKLOADS="stream_min stream_classic decode" bash tools/gpu_prof_configs.sh || exit $?
-TAG=r06 TRAFFIC_SETS="--workload stream --steps 3 --warmup 1;--workload stream --mode classic --prepare-every 1 --instances 4194304 --steps 3 --warmup 1;--workload decode --steps 3 --warmup 1" bash tools/gpu_counters.sh
+TAG=r06s4 WORKLOADS="stream_min stream_classic" bash tools/gpu_prof_configs.sh || exit $?
+TAG=r06 TRAFFIC_SETS="--workload stream --steps 3 --warmup 1;--workload stream --mode classic --prepare-every 1 --instances 4194304 --steps 3 --warmup 1" INSTR_SETS="--workload stream --steps 3 --warmup 1" bash tools/gpu_counters.sh
