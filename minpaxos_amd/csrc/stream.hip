@@ -58,6 +58,9 @@ constexpr int kTEnt = 8 * kE + kTL + 16;  // a tile's TileEnt bytes (+ chunks 8.
 #ifndef MPX_SD_TENT
 #define MPX_SD_TENT 1
 #endif
+#ifndef MPX_SD_PRMARK  // PrepareReplies marked 0x60 in the landing table: a position mask, no loads
+#define MPX_SD_PRMARK 0
+#endif
 #ifndef MPX_SD_TENT_NOCONV  // test build: every tile takes the unconverged path
 #define MPX_SD_TENT_NOCONV 0
 #endif
@@ -431,7 +434,8 @@ __host__ __device__ constexpr uint64_t dp_table(uint64_t lut) {
     uint64_t e = 0;
     for (int i = 0; i < 8; ++i) {
         const uint64_t fl = (lut >> (8 * i)) & 0xFFu;
-        e |= (fl ? fl - 1 : (uint64_t)kVarMark) << (8 * i);
+        const uint64_t vm = MPX_SD_PRMARK && i == MPX_PEER_PREPARE_REPLY - MPX_PEER_BEACON ? kVarMark | 0x20u : kVarMark;
+        e |= (fl ? fl - 1 : vm) << (8 * i);
     }
     return e;
 }
@@ -566,6 +570,9 @@ __global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(MPX_SD_WPE)
     }
     SD_STAMP(1);
     uint64_t m_lo = 0, m_hi = 0;  // the chunk's variable-message positions (kept for the counts)
+#if MPX_SD_PRMARK
+    uint64_t r_lo = 0, r_hi = 0;  // its PrepareReplies' (bit 5 of the table value)
+#endif
     {
         const bool wv = __ballot(any_var != 0) != 0;  // (wave-uniform)
         uint16_t* T = reinterpret_cast<uint16_t*>(&G[0][0]) + (l >> 6) * kVarTasks;
@@ -573,9 +580,19 @@ __global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(MPX_SD_WPE)
 #pragma unroll
             for (int i = 0; i < kC / 4; ++i) {
                 const uint32_t pos4 = (uint32_t)(4 * i + 1) * 0x01010101u + 0x03020100u;
+#if MPX_SD_PRMARK
+                // bit 0 of a byte: variable message, bit 4: PrepareReply; gathered to two nibbles
+                const uint32_t d = wd[i] - pos4;
+                const uint32_t z = ((d >> 6) & 0x01010101u) | ((d >> 1) & 0x10101010u);
+                const uint32_t c = (z | (z >> 7) | (z >> 14) | (z >> 21));
+                const uint64_t nib = c & 0xFu, rnib = (c >> 4) & 0xFu;
+                if (i < 16) { m_lo |= nib << (4 * i); r_lo |= rnib << (4 * i); }
+                else { m_hi |= nib << (4 * (i - 16)); r_hi |= rnib << (4 * (i - 16)); }
+#else
                 const uint32_t t = var_bits(wd[i] - pos4) >> 6;  // 0x01 per variable-message byte
                 const uint64_t nib = (uint64_t)((t | (t >> 7) | (t >> 14) | (t >> 21)) & 0xFu);
                 if (i < 16) m_lo |= nib << (4 * i); else m_hi |= nib << (4 * (i - 16));
+#endif
             }
         }
         const uint32_t vt = wv ? var_wave(P, t0, m_lo, m_hi, D, T) : 0u;
@@ -713,7 +730,11 @@ __global__ __launch_bounds__(kTL) __attribute__((amdgpu_waves_per_eu(MPX_SD_WPE)
                 const bool var = ((x < 64 ? m_lo >> x : m_hi >> (x - 64)) & 1ull) != 0;
                 if (var) {
                     cnt[2]++;
+#if MPX_SD_PRMARK
+                    cnt[1] += (uint32_t)((x < 64 ? r_lo >> x : r_hi >> (x - 64)) & 1ull);
+#else
                     cnt[1] += P.buf[c0 + x] == MPX_PEER_PREPARE_REPLY ? 1u : 0u;
+#endif
                 } else {
                     cnt[len == ar_len ? 0 : 3]++;
                 }
