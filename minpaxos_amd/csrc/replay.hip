@@ -22,6 +22,14 @@
 //   k_rb_max          a workgroup per bin: the bin's slice of last_rec into LDS, one LDS
 //                     atomicMax per pair, the slice written back
 // 8 B x 4 of pair traffic per record + the slots read and written once, all coalesced.
+// MPX_REPLAY_SORTCHUNK=1 (round 6) drops the count, scan and scatter passes:
+//   k_rb_sort         a workgroup per chunk: the chunk's pairs sorted by bin in LDS and written
+//                     back packed (chunk-local record index << 15 | slot in bin, 4 bytes) into
+//                     the chunk's own range, with each bin's start in the chunk (run starts,
+//                     chunks x (bins + 1)) - no global histogram or scan needed
+//   k_rb_max_runs     a workgroup per bin: its run in every chunk (8 lanes per run), one LDS
+//                     atomicMax per pair as before
+// 8 B written + 8 B read + 4 B written + 4 B read of pairs per record.
 // Without the scratch (or past kRbMaxCap slots), one atomicMax per record:
 // The slot maximum without a device-scope atomic per record (MPX_REPLAY_ATOMIC=0, A/B):
 //   pass 1 (k_replay_durable) raises a slot with a plain load + store when its record index is
@@ -73,6 +81,10 @@ constexpr int kRbT = 1024;
 constexpr int kRbPer = 16;
 constexpr uint64_t kRbChunk = kRbPer * kRbT;    // pairs per count / scatter workgroup (128 KB)
 constexpr uint64_t kRbNone = ~0ull;             // an instNo outside [0, inst_cap): no slot
+#ifndef MPX_REPLAY_SORTCHUNK
+#define MPX_REPLAY_SORTCHUNK 1
+#endif
+static_assert(kRbChunk <= (1u << (32 - kRbLg)), "packed pair: chunk-local index above the slot bits");
 
 // pairs: null = the atomic form
 __global__ __launch_bounds__(kReplayBlock) void k_replay_durable(
@@ -318,6 +330,140 @@ __global__ __launch_bounds__(kRbT) void k_rb_max(const uint64_t* __restrict__ bi
     for (uint32_t j = threadIdx.x; j < ns; j += kRbT) last_rec[s0 + j] = sl[j];
 }
 
+// the chunk's pairs sorted by bin in LDS, stored packed over the chunk's own range of `packed`,
+// and the bins' starts in the chunk (rs[chunk][b], b <= bins: rs[chunk][bins] = the chunk's total)
+__global__ __launch_bounds__(kRbT) void k_rb_sort(const uint64_t* __restrict__ pairs, uint64_t n,
+                                                 uint32_t bins, uint32_t* __restrict__ packed,
+                                                 uint32_t* __restrict__ rs) {
+    __shared__ uint32_t sp[kRbChunk];
+    __shared__ uint32_t cnt[kRbMaxBins];  // counts, then the bins' starts in sp
+    __shared__ uint32_t wtot[kRbT / kWave];
+    const int t = threadIdx.x, l = lane_id(), w = t / kWave;
+    for (uint32_t b = t; b < bins; b += kRbT) cnt[b] = 0;
+    __syncthreads();
+    const uint64_t c0 = (uint64_t)blockIdx.x * kRbChunk;
+    uint64_t p[kRbPer];
+    uint32_t rk[kRbPer];
+#pragma unroll
+    for (int k = 0; k < kRbPer; ++k) {
+        const uint64_t i = c0 + (uint64_t)(t + k * kRbT);
+        p[k] = i < n ? ld_stream(pairs + i) : kRbNone;
+    }
+#pragma unroll
+    for (int k = 0; k < kRbPer; ++k)
+        rk[k] = p[k] != kRbNone ? atomicAdd(&cnt[(uint32_t)p[k] >> kRbLg], 1u) : 0u;
+    __syncthreads();
+    // exclusive scan of the counts, one bin per thread (bins <= kRbT)
+    const uint32_t c = (uint32_t)t < bins ? cnt[t] : 0u;
+    uint32_t x = c;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (l >= d) x += y;
+    }
+    if (l == kWave - 1) wtot[w] = x;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (int v = 0; v < kRbT / kWave; ++v) {
+        before += v < w ? wtot[v] : 0u;
+        total += wtot[v];
+    }
+    uint32_t* r = rs + (uint64_t)blockIdx.x * (bins + 1);
+    if ((uint32_t)t < bins) {
+        cnt[t] = before + x - c;
+        r[t] = before + x - c;
+    }
+    if (t == 0) r[bins] = total;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kRbPer; ++k)
+        if (p[k] != kRbNone)
+            sp[cnt[(uint32_t)p[k] >> kRbLg] + rk[k]] =
+                ((uint32_t)(t + k * kRbT) << kRbLg) | ((uint32_t)p[k] & (kRbSlots - 1));
+    __syncthreads();
+    for (uint32_t i = t; i < total; i += kRbT) st_stream(packed + c0 + i, sp[i]);
+}
+
+// a workgroup per bin: the slice into LDS, then the bin's run in every chunk, 8 lanes per run
+// and four runs per 8 lanes in flight (~32 pairs per run for 2^24 records over 2^24 slots), the
+// slice written back
+__global__ __launch_bounds__(kRbT) void k_rb_max_runs(const uint32_t* __restrict__ packed,
+                                                     const uint32_t* __restrict__ rs,
+                                                     uint32_t chunks, uint32_t bins,
+                                                     int32_t inst_cap, int32_t rec_base,
+                                                     int32_t* __restrict__ last_rec) {
+    __shared__ int32_t sl[kRbSlots];
+    const uint32_t b = blockIdx.x;
+    const uint64_t s0 = (uint64_t)b * kRbSlots;
+    const uint32_t ns = (uint64_t)inst_cap - s0 < kRbSlots ? (uint32_t)((uint64_t)inst_cap - s0)
+                                                            : kRbSlots;
+    constexpr int kB = 8;
+    static_assert(kRbSlots % (kB * kRbT) == 0, "whole batches of slots");
+    for (uint32_t j0 = 0; j0 < ns; j0 += kB * kRbT) {
+        int32_t v[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            const uint32_t j = j0 + threadIdx.x + k * kRbT;
+            v[k] = j < ns ? last_rec[s0 + j] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            const uint32_t j = j0 + threadIdx.x + k * kRbT;
+            if (j < ns) sl[j] = v[k];
+        }
+    }
+    __syncthreads();
+    // the bin's run starts / ends for up to kRbT chunks at a time, into LDS with one load each
+    // (a run's bounds loaded just before its pairs had put two round trips on every run)
+    __shared__ uint32_t rlo[kRbT], rhi[kRbT];
+    constexpr uint32_t kSub = 8, kGroups = kRbT / kSub;
+    constexpr int kU = 4, kR = 6;  // runs per group and pairs per lane in flight
+    const uint32_t g = threadIdx.x / kSub, sub = threadIdx.x % kSub;
+    for (uint32_t cb = 0; cb < chunks; cb += kRbT) {
+        const uint32_t nc = chunks - cb < (uint32_t)kRbT ? chunks - cb : (uint32_t)kRbT;
+        __syncthreads();  // the previous batch's readers are done
+        if (threadIdx.x < nc) {
+            const uint32_t* r = rs + (uint64_t)(cb + threadIdx.x) * (bins + 1) + b;
+            rlo[threadIdx.x] = r[0];
+            rhi[threadIdx.x] = r[1];
+        }
+        __syncthreads();
+        for (uint32_t c0 = g; c0 < nc; c0 += kU * kGroups) {
+            uint32_t q[kU][kR];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const uint32_t c = c0 + u * kGroups;
+                const uint32_t lo = c < nc ? rlo[c] : 0u, hi = c < nc ? rhi[c] : 0u;
+                const uint32_t* src = packed + (uint64_t)(cb + c) * kRbChunk;
+#pragma unroll
+                for (int k = 0; k < kR; ++k) {
+                    const uint32_t j = lo + sub + k * kSub;
+                    q[u][k] = j < hi ? src[j] : ~0u;  // cached: the run's next pieces share its lines
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const uint32_t c = c0 + u * kGroups;
+                const int32_t cbase = (int32_t)((uint32_t)rec_base + (cb + c) * (uint32_t)kRbChunk);
+#pragma unroll
+                for (int k = 0; k < kR; ++k)
+                    if (q[u][k] != ~0u)
+                        atomicMax(&sl[q[u][k] & (kRbSlots - 1)],
+                                  (int32_t)((uint32_t)cbase + (q[u][k] >> kRbLg)));
+                if (c < nc) {  // a run longer than kSub * kR pairs: its tail
+                    const uint32_t* src = packed + (uint64_t)(cb + c) * kRbChunk;
+                    for (uint32_t j = rlo[c] + sub + kR * kSub; j < rhi[c]; j += kSub) {
+                        const uint32_t x = src[j];
+                        atomicMax(&sl[x & (kRbSlots - 1)], (int32_t)((uint32_t)cbase + (x >> kRbLg)));
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < ns; j += kRbT) last_rec[s0 + j] = sl[j];
+}
+
 // the scan of hist: bins x chunks counts, then one zero item whose prefix is the total
 struct RbHistIn {
     const uint32_t* h;
@@ -330,7 +476,7 @@ struct RbHistOut {
 };
 
 struct RbLayout {
-    uint64_t pairs, binned, hist, offs, scan, total;
+    uint64_t pairs, binned, hist, offs, scan, packed, rs, total;
 };
 RbLayout rb_layout(uint64_t n, int32_t inst_cap) {
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
@@ -344,6 +490,8 @@ RbLayout rb_layout(uint64_t n, int32_t inst_cap) {
     L.hist = o; o += al(h * 4);
     L.offs = o; o += al(h * 4);
     L.scan = o; o += al(scan_scratch_bytes<uint32_t>(h));
+    L.packed = o; o += al(n * 4);
+    L.rs = o; o += al(chunks * (bins + 1) * 4);
     L.total = o;
     return L;
 }
@@ -375,6 +523,14 @@ hipError_t launch_replay_durable(const uint8_t* log, uint64_t n, int32_t inst_ca
         const uint32_t chunks = (uint32_t)((n + kRbChunk - 1) / kRbChunk);
         const uint32_t bins = (uint32_t)(((uint64_t)inst_cap + kRbSlots - 1) / kRbSlots);
         const uint64_t h = (uint64_t)bins * chunks;
+#if MPX_REPLAY_SORTCHUNK
+        uint32_t* packed = (uint32_t*)(w + L.packed);
+        uint32_t* rs = (uint32_t*)(w + L.rs);
+        k_rb_sort<<<chunks, kRbT, 0, stream>>>(pairs, n, bins, packed, rs);
+        k_rb_max_runs<<<bins, kRbT, 0, stream>>>(packed, rs, chunks, bins, inst_cap, rec_base,
+                                                 last_rec);
+        return hipGetLastError();
+#endif
         uint32_t* hist = (uint32_t*)(w + L.hist);
         uint32_t* offs = (uint32_t*)(w + L.offs);
         k_rb_count<<<chunks, kRbT, 0, stream>>>(pairs, n, bins, chunks, hist);

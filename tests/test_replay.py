@@ -193,14 +193,16 @@ def test_replay_chunked(mk_engine):
 
 @pytest.mark.gpu
 def test_replay_dev_binned_and_atomic(mk_engine):
-    """mpx_replay_durable_dev with the reserved scratch (the binned slot maximum: pairs, bin
-    counts, scan, an LDS-sorted scatter, one LDS slice per 32768 slots) and without it (one
+    """mpx_replay_durable_dev with the reserved scratch (the binned slot maximum: pairs, each
+    chunk's pairs sorted by bin in LDS with its run starts, one LDS slice per 32768 slots) and without it (one
     device atomicMax per record): the same slots as the oracle - a ragged last bin, every record
     in one bin, heavy repeats, a space past the binned limit (2^25 slots: the atomic form),
     rec_base offsets"""
     e, o = mk_engine(5, R.MODE_MIN), Oracle()
     cases = [(100003, 50000, 0), (70001, 3 * 32768 + 5, 17), (1 << 18, 1000, 5),
-             (4099, 8192, 0), (1000, (1 << 25) + 1, 3)]
+             (4099, 8192, 0), (1000, (1 << 25) + 1, 3),
+             # 64 chunks x 129 bins (a ragged last bin): the chunk-sorted runs
+             ((1 << 20) + 77, (1 << 22) + 3, 11)]
     with Arena(e) as hip:
         for n, cap, base in cases:
             log = durable_log(n, cap, n ^ cap, dup=True)
