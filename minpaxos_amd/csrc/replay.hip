@@ -12,7 +12,7 @@
 // The slot maximum, binned (the default when the engine holds the call's scratch,
 // replay_work_bytes; instance spaces up to kRbMaxCap slots): 2^24 random device-scope atomics
 // are request-bound on this chip (0.45 ms of the 0.69 ms call, round 3), so the slots are
-// maximised in LDS instead:
+// maximised in LDS instead (round 5's form, MPX_REPLAY_SORTCHUNK=0):
 //   k_replay_durable  writes pair[i] = (rec_base + i) << 32 | instNo, coalesced (8 B / record)
 //   k_rb_count        a workgroup per chunk of kRbChunk pairs: LDS histogram of the bins
 //                     (kRbSlots = 32768 instance slots each) into hist[bin][chunk], bin-major
@@ -22,7 +22,7 @@
 //   k_rb_max          a workgroup per bin: the bin's slice of last_rec into LDS, one LDS
 //                     atomicMax per pair, the slice written back
 // 8 B x 4 of pair traffic per record + the slots read and written once, all coalesced.
-// MPX_REPLAY_SORTCHUNK=1 (round 6) drops the count, scan and scatter passes:
+// MPX_REPLAY_SORTCHUNK=1 (round 6, the default) drops the count, scan and scatter passes:
 //   k_rb_sort         a workgroup per chunk: the chunk's pairs sorted by bin in LDS and written
 //                     back packed (chunk-local record index << 15 | slot in bin, 4 bytes) into
 //                     the chunk's own range, with each bin's start in the chunk (run starts,
