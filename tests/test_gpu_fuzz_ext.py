@@ -128,3 +128,61 @@ def test_fuzz_stream_decode_ext(mk_engine, seed):
             for f in ("consumed", "next", "n_accept_replies", "n_prepare_replies", "n_var", "n_other",
                       "stop_reason", "stop_code"):
                 assert int(got[4][f]) == int(want[4][f]), (seed, proto, cut, f)
+
+
+_DUR = np.dtype([("ballot", "<i4"), ("status", "<i4"), ("inst", "<i4"), ("op", "u1"),
+                 ("key", "<i8"), ("val", "<i8")])  # 29 packed bytes (getDataFromStableStore)
+
+
+@pytest.mark.skipif(_N == 0, reason="set MPX_FUZZ_EXT=<seeds> to run the extended sweep")
+@pytest.mark.parametrize("seed", range(max(_N // 4, 1)))
+def test_fuzz_replay_binned_ext(mk_engine, seed):
+    """durable-log replay (bareminpaxos.go:122-161) through the binned slot maximum (the
+    reserved scratch: chunk-sorted runs, one LDS slice per 32768 slots) against the oracle:
+    random record counts (ragged last chunk), instance spaces from one slot to 2^24 (ragged
+    last bin), permutations, uniform repeats, repeats packed into one bin, rec_base offsets
+    with slots carried from earlier chunks"""
+    from minpaxos_amd.devbuf import Arena
+    assert _DUR.itemsize == R.DURABLE_REC_BYTES
+    rng = np.random.default_rng(95000 + seed)
+    e, o = mk_engine(5, R.MODE_MIN), Oracle()
+    n = int(rng.integers(1, 1 << 21))
+    cap = int(rng.choice([int(rng.integers(1, 1 << 12)), int(rng.integers(1, 1 << 24)),
+                          32768 * int(rng.integers(1, 64)) + int(rng.integers(-2, 3))]))
+    cap = max(cap, 1)
+    kind = ["perm", "uniform", "one_bin", "hot"][int(rng.integers(0, 4))]
+    if kind == "perm" and n <= cap:
+        inst = rng.permutation(cap)[:n]
+    elif kind == "one_bin":
+        b0 = int(rng.integers(0, (cap + 32767) // 32768)) * 32768
+        inst = rng.integers(b0, min(cap, b0 + 32768), n)
+    elif kind == "hot":
+        inst = rng.integers(0, min(cap, 16), n)
+    else:
+        inst = rng.integers(0, cap, n)
+    recs = np.zeros(n, _DUR)
+    recs["ballot"] = rng.integers(-50, 50, n)
+    recs["status"] = rng.integers(0, 5, n)
+    recs["inst"] = inst
+    recs["op"] = rng.integers(0, 3, n)
+    recs["key"] = rng.integers(-(1 << 40), 1 << 40, n)
+    recs["val"] = rng.integers(-(1 << 40), 1 << 40, n)
+    log = recs.view(np.uint8).copy()
+    base = int(rng.integers(0, 1000)) if rng.random() < 0.5 else 0
+    last0 = rng.integers(-1, base, cap).astype(np.int32) if base else np.full(cap, -1, np.int32)
+    want = o.replay_durable(log, cap, 7, -1, rec_base=base, last_rec=last0)
+    with Arena(e) as hip:
+        e.replay_durable_reserve(len(log), cap)
+        d_log = hip.put(log)
+        d = [hip.put(np.zeros_like(w)) for w in want[:4]]
+        d_last = hip.put(last0)
+        d_sc = hip.put(np.array([7, -1], np.int32))
+        e.replay_durable_dev(d_log.ptr, len(log), cap, *[x.ptr for x in d], d_last.ptr,
+                             d_sc.ptr, rec_base=base)
+        e.synchronize()
+        tag = (seed, n, cap, kind, base)
+        for x, w in zip(d, want[:4]):
+            assert np.array_equal(hip.get(x), w), tag
+        got = hip.get(d_last)
+        assert np.array_equal(got, want[4]), (tag, np.nonzero(got != want[4])[0][:5])
+        assert hip.get(d_sc).tolist() == [want[5], want[6]], tag
