@@ -23,13 +23,14 @@
 //                     atomicMax per pair, the slice written back
 // 8 B x 4 of pair traffic per record + the slots read and written once, all coalesced.
 // MPX_REPLAY_SORTCHUNK=1 (round 6, the default) drops the count, scan and scatter passes:
-//   k_rb_sort         a workgroup per chunk: the chunk's pairs sorted by bin in LDS and written
+//   k_replay_durable  writes the record's instNo (4 B; the record index is its position)
+//   k_rb_sort         a workgroup per chunk: the chunk's instNos sorted by bin in LDS and written
 //                     back packed (chunk-local record index << 15 | slot in bin, 4 bytes) into
 //                     the chunk's own range, with each bin's start in the chunk (run starts,
 //                     chunks x (bins + 1)) - no global histogram or scan needed
 //   k_rb_max_runs     a workgroup per bin: its run in every chunk (8 lanes per run), one LDS
 //                     atomicMax per pair as before
-// 8 B written + 8 B read + 4 B written + 4 B read of pairs per record.
+// 4 B written + 4 B read + 4 B written + 4 B read per record.
 // Without the scratch (or past kRbMaxCap slots), one atomicMax per record:
 // The slot maximum without a device-scope atomic per record (MPX_REPLAY_ATOMIC=0, A/B):
 //   pass 1 (k_replay_durable) raises a slot with a plain load + store when its record index is
@@ -161,7 +162,9 @@ __global__ __launch_bounds__(kReplayBlock) void k_replay_durable(
             if (st == MPX_COMMITTED && inst > committed) committed = inst;
             // instanceSpace[instNo] panics outside the array (Go index check)
             const bool bad = inst < 0 || inst >= inst_cap;
-            if (pairs)
+            if (pairs && MPX_REPLAY_SORTCHUNK)  // the instNo alone: the record index is its place
+                st_stream(reinterpret_cast<uint32_t*>(pairs) + i, bad ? ~0u : (uint32_t)inst);
+            else if (pairs)
                 st_stream(pairs + i, bad ? kRbNone
                                          : ((uint64_t)(uint32_t)(rec_base + (int32_t)i) << 32) |
                                                (uint32_t)inst);
@@ -330,9 +333,16 @@ __global__ __launch_bounds__(kRbT) void k_rb_max(const uint64_t* __restrict__ bi
     for (uint32_t j = threadIdx.x; j < ns; j += kRbT) last_rec[s0 + j] = sl[j];
 }
 
-// the chunk's pairs sorted by bin in LDS, stored packed over the chunk's own range of `packed`,
+// the chunk's instNos sorted by bin in LDS, stored packed over the chunk's own range of `packed`,
 // and the bins' starts in the chunk (rs[chunk][b], b <= bins: rs[chunk][bins] = the chunk's total)
-__global__ __launch_bounds__(kRbT) void k_rb_sort(const uint64_t* __restrict__ pairs, uint64_t n,
+#ifndef MPX_RB_SORT_WPE  // k_rb_sort's waves per SIMD bound (8: two workgroups per CU)
+#define MPX_RB_SORT_WPE 0
+#endif
+__global__ __launch_bounds__(kRbT)
+#if MPX_RB_SORT_WPE
+__attribute__((amdgpu_waves_per_eu(MPX_RB_SORT_WPE)))
+#endif
+void k_rb_sort(const uint32_t* __restrict__ insts, uint64_t n,
                                                  uint32_t bins, uint32_t* __restrict__ packed,
                                                  uint32_t* __restrict__ rs) {
     __shared__ uint32_t sp[kRbChunk];
@@ -342,16 +352,16 @@ __global__ __launch_bounds__(kRbT) void k_rb_sort(const uint64_t* __restrict__ p
     for (uint32_t b = t; b < bins; b += kRbT) cnt[b] = 0;
     __syncthreads();
     const uint64_t c0 = (uint64_t)blockIdx.x * kRbChunk;
-    uint64_t p[kRbPer];
+    uint32_t p[kRbPer];  // instNo, ~0 = none
     uint32_t rk[kRbPer];
 #pragma unroll
     for (int k = 0; k < kRbPer; ++k) {
         const uint64_t i = c0 + (uint64_t)(t + k * kRbT);
-        p[k] = i < n ? ld_stream(pairs + i) : kRbNone;
+        p[k] = i < n ? ld_stream(insts + i) : ~0u;
     }
 #pragma unroll
     for (int k = 0; k < kRbPer; ++k)
-        rk[k] = p[k] != kRbNone ? atomicAdd(&cnt[(uint32_t)p[k] >> kRbLg], 1u) : 0u;
+        rk[k] = p[k] != ~0u ? atomicAdd(&cnt[p[k] >> kRbLg], 1u) : 0u;
     __syncthreads();
     // exclusive scan of the counts, one bin per thread (bins <= kRbT)
     const uint32_t c = (uint32_t)t < bins ? cnt[t] : 0u;
@@ -377,9 +387,9 @@ __global__ __launch_bounds__(kRbT) void k_rb_sort(const uint64_t* __restrict__ p
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kRbPer; ++k)
-        if (p[k] != kRbNone)
-            sp[cnt[(uint32_t)p[k] >> kRbLg] + rk[k]] =
-                ((uint32_t)(t + k * kRbT) << kRbLg) | ((uint32_t)p[k] & (kRbSlots - 1));
+        if (p[k] != ~0u)
+            sp[cnt[p[k] >> kRbLg] + rk[k]] =
+                ((uint32_t)(t + k * kRbT) << kRbLg) | (p[k] & (kRbSlots - 1));
     __syncthreads();
     for (uint32_t i = t; i < total; i += kRbT) st_stream(packed + c0 + i, sp[i]);
 }
@@ -526,7 +536,7 @@ hipError_t launch_replay_durable(const uint8_t* log, uint64_t n, int32_t inst_ca
 #if MPX_REPLAY_SORTCHUNK
         uint32_t* packed = (uint32_t*)(w + L.packed);
         uint32_t* rs = (uint32_t*)(w + L.rs);
-        k_rb_sort<<<chunks, kRbT, 0, stream>>>(pairs, n, bins, packed, rs);
+        k_rb_sort<<<chunks, kRbT, 0, stream>>>((const uint32_t*)pairs, n, bins, packed, rs);
         k_rb_max_runs<<<bins, kRbT, 0, stream>>>(packed, rs, chunks, bins, inst_cap, rec_base,
                                                  last_rec);
         return hipGetLastError();
