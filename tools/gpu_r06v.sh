@@ -4,4 +4,4 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 EXT=400 bash tools/gpu_r06u.sh || exit $?
-TAG=r06_replay2 OLD=minpaxos_amd/ab/libmpx_rphead.so bash tools/gpu_r06s.sh
+TAG=${T2:-r06_replay2} OLD=${OLD:-minpaxos_amd/ab/libmpx_rphead.so} bash tools/gpu_r06s.sh
